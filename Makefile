@@ -1,0 +1,55 @@
+# Build for AMD Instinct MI355X (gfx950). One build, backend chosen at run
+# time (--backend rccl|cpu); no PROXY_ENABLE_* configurations.
+#
+# Reference equivalent: Makefile.common / Makefile.flags.mk / Makefile.<SYSTEM>
+# (SURVEY.md C16-C18), which compiled one binary set per backend config.
+#
+#   make              # library + CLI binaries (+ *_loop aliases)
+#   make lib          # dlnetbench_amd/_lib/libdlnb.so only
+#   make clean
+#   make ARCH=gfx950 HIPCC=/opt/rocm/bin/hipcc -j8
+
+ROCM    ?= /opt/rocm
+HIPCC   ?= $(ROCM)/bin/hipcc
+ARCH    ?= gfx950
+BUILD   ?= build
+OPT     ?= -O3
+CXXFLAGS = $(OPT) -std=c++17 -fPIC -Wall -Wno-unused-result -Icsrc/include --offload-arch=$(ARCH)
+LDLIBS   = -L$(ROCM)/lib -lrccl -lamdhip64 -lpthread -lrt -Wl,-rpath,$(ROCM)/lib
+
+LIB_SRCS := $(wildcard csrc/src/*.cpp) $(wildcard csrc/kernels/*.hip)
+LIB_OBJS := $(patsubst csrc/%,$(BUILD)/obj/%.o,$(LIB_SRCS))
+APPS     := dp fsdp hybrid_2d hybrid_3d hybrid_3d_moe dlnb
+LOOPS    := dp_loop fsdp_loop hybrid_2d_loop hybrid_3d_loop hybrid_3d_moe_loop
+LIB      := $(BUILD)/libdlnb.so
+PYLIB    := dlnetbench_amd/_lib/libdlnb.so
+
+.PHONY: all lib apps clean
+all: lib apps
+
+lib: $(PYLIB)
+
+$(BUILD)/obj/%.o: csrc/%
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+
+$(LIB): $(LIB_OBJS)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ $(LDLIBS) -Wl,-soname,libdlnb.so
+
+$(PYLIB): $(LIB)
+	@mkdir -p $(dir $@)
+	cp $< $@
+
+apps: $(addprefix $(BUILD)/bin/,$(APPS)) $(addprefix $(BUILD)/bin/,$(LOOPS))
+
+$(BUILD)/bin/%: csrc/apps/%.cpp $(LIB)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(CXXFLAGS) $< -o $@ -L$(BUILD) -ldlnb $(LDLIBS) -Wl,-rpath,'$$ORIGIN/..'
+
+# The reference builds separate *_loop binaries with -DPROXY_LOOP; here the
+# same binary switches to loop mode when invoked under a *_loop name.
+$(BUILD)/bin/%_loop: $(BUILD)/bin/%
+	ln -sf $(notdir $<) $@
+
+clean:
+	rm -rf $(BUILD) $(PYLIB)

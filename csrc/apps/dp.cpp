@@ -1,0 +1,4 @@
+// CLI entry point 'dp' (reference: see dlnb/options.hpp for the contract).
+#include "dlnb/strategy.hpp"
+
+int main(int argc, char** argv) { return dlnb::main_for(dlnb::StrategyKind::DP, argc, argv); }

@@ -1,0 +1,4 @@
+// CLI entry point 'hybrid_3d_moe' (reference: see dlnb/options.hpp for the contract).
+#include "dlnb/strategy.hpp"
+
+int main(int argc, char** argv) { return dlnb::main_for(dlnb::StrategyKind::Hybrid3DMoE, argc, argv); }

@@ -1,0 +1,87 @@
+// Communication layer: one stream-ordered collective/P2P interface with a
+// run-time selected backend.
+//
+// Reference: cpp/proxy_classes.hpp:30-342 defines ProxyCommunicator with
+// request/stream "index" slots and three compile-time backends (MPI,
+// NCCL/RCCL, oneCCL) chosen by PROXY_ENABLE_* macros. Differences here:
+//   * every operation takes the Stream it is ordered on; completion is
+//     tracked with Events, so there are no request slots and no Wait(i) /
+//     WaitAll(n) (the reference's CCL "Barrier" that was not a barrier,
+//     proxy_classes.hpp:189-191, disappears: host barriers live in
+//     HostGroup);
+//   * the backend is chosen at run time (--backend rccl|cpu);
+//   * all-to-all maps to ncclAllToAll instead of a hand-rolled
+//     ncclGroupStart + per-peer send/recv loop (proxy_classes.hpp:160-182);
+//   * element type is explicit (the MPI backend's hard-coded MPI_FLOAT,
+//     proxy_classes.hpp:67,100, is gone).
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "dlnb/bootstrap.hpp"
+#include "dlnb/common.hpp"
+#include "dlnb/device.hpp"
+
+namespace dlnb {
+
+enum class CollKind : int { AllReduce, AllGather, ReduceScatter, AllToAll, SendRecv };
+
+class Communicator {
+ public:
+  virtual ~Communicator() = default;
+  int rank() const { return rank_; }
+  int size() const { return size_; }
+  const std::vector<int>& members() const { return members_; }  // world ranks
+  const std::string& name() const { return name_; }
+  virtual std::string backend_name() const = 0;
+
+  // count = elements per rank; send/recv may alias (in place).
+  virtual void all_reduce(const void* send, void* recv, size_t count, DType t, Stream& s) = 0;
+  // recv holds size()*send_count elements, rank-major.
+  virtual void all_gather(const void* send, void* recv, size_t send_count, DType t, Stream& s) = 0;
+  // send holds size()*recv_count elements; recv gets this rank's reduced block.
+  virtual void reduce_scatter(const void* send, void* recv, size_t recv_count, DType t, Stream& s) = 0;
+  // send/recv hold size()*count elements; block j goes to / comes from rank j.
+  virtual void all_to_all(const void* send, void* recv, size_t count, DType t, Stream& s) = 0;
+  // Point-to-point by group rank. Between group_start()/group_end() the
+  // operations progress together (no ordering deadlocks between a send and
+  // a recv issued in the same group).
+  virtual void send(const void* buf, size_t count, DType t, int peer, Stream& s) = 0;
+  virtual void recv(void* buf, size_t count, DType t, int peer, Stream& s) = 0;
+  virtual void group_start() {}
+  virtual void group_end() {}
+  // Returns a non-empty description if the backend detected an
+  // asynchronous failure (peer death, network error).
+  virtual std::string async_error() { return ""; }
+  virtual void abort() {}
+
+ protected:
+  int rank_ = 0;
+  int size_ = 1;
+  std::vector<int> members_;
+  std::string name_;
+};
+
+// Creates communicators over subsets of the world.
+class CommFactory {
+ public:
+  virtual ~CommFactory() = default;
+  virtual std::string backend_name() const = 0;
+  // `members` are world ranks (this rank must be one of them); `name` must
+  // be unique per group and identical on all members. capacity_bytes is the
+  // largest single message (CPU backend staging size); need_p2p requests
+  // point-to-point mailboxes.
+  virtual std::unique_ptr<Communicator> create(const std::string& name, const std::vector<int>& members,
+                                               size_t capacity_bytes, bool need_p2p) = 0;
+};
+
+std::unique_ptr<CommFactory> make_rccl_factory(HostGroup& world, Device& dev);
+std::unique_ptr<CommFactory> make_shm_factory(HostGroup& world, Device& dev);
+
+// Bytes moved per rank for bus-bandwidth accounting (nccl-tests convention):
+// busbw = algbw * factor(kind, n).
+double busbw_factor(CollKind k, int n);
+
+}  // namespace dlnb

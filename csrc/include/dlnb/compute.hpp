@@ -1,0 +1,54 @@
+// Synthetic compute that stands in for the model's forward/backward math.
+//
+// The reference simulates compute with host usleep(µs) read from the stats
+// tables (cpp/data_parallel/dp.cpp:93,98; fsdp.cpp:103,120,145;
+// hybrid_2d.cpp:111-156), which leaves the GPU idle while collectives run.
+// Modes here (all stream ordered):
+//   sleep - the stream is busy for exactly the duration, the GPU is idle
+//           (one-wave s_memrealtime wait on GPU; nanosleep task on CPU);
+//           reference parity.
+//   spin  - every CU runs dependent VALU work until the deadline.
+//   gemm  - hand-written MFMA GEMMs shaped from the model (M = token chunk,
+//           N = FFN dim, K = hidden dim) calibrated at start-up so the
+//           uncontended duration equals the table's time; the tail below
+//           the smallest GEMM is filled by a deadline spin. Under
+//           contention with RCCL kernels it takes longer, like real
+//           training compute does.
+//   flops - executes the table's FLOP count on the MI355X GEMM at whatever
+//           speed the hardware gives (MI355X-native compute time).
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "dlnb/device.hpp"
+#include "dlnb/json.hpp"
+
+namespace dlnb {
+
+enum class ComputeMode { Sleep, Spin, Gemm, Flops };
+
+ComputeMode parse_compute_mode(const std::string& s, DeviceKind dev);
+const char* compute_mode_name(ComputeMode m);
+
+struct ComputeShape {
+  int hidden = 4096;  // model hidden size (K of the stand-in GEMM)
+  int ffn = 16384;    // FFN width (N)
+  DType dtype = DType::BF16;
+};
+
+class ComputeEngine {
+ public:
+  virtual ~ComputeEngine() = default;
+  // Enqueue `us` microseconds of compute; `flops` is the real FLOP count of
+  // that piece of work (used by the flops mode).
+  virtual void run(Stream& s, double us, double flops) = 0;
+  virtual Json describe() const = 0;
+  virtual ComputeMode mode() const = 0;
+};
+
+std::unique_ptr<ComputeEngine> make_compute_engine(Device& dev, ComputeMode mode, const ComputeShape& shape,
+                                                   double time_scale);
+
+}  // namespace dlnb

@@ -1,0 +1,151 @@
+// Device layer: buffers, streams and events behind one interface for the GPU
+// (HIP on MI355X) and the CPU (worker-thread "streams").
+//
+// Reference: cpp/proxy_classes.hpp:345-444 (Device enum, Tensor<T,Device>
+// with calloc / cudaMalloc / hipMalloc / sycl::malloc_device) and the stream
+// macros of cpp/data_types.hpp:91-130. The reference drives all ordering from
+// the host thread (blocking collectives, usleep compute). Here every strategy
+// is *stream ordered*: compute and collectives are enqueued on streams and
+// ordered with events, so the host never sits on the critical path. The CPU
+// device reproduces the same semantics with one worker thread per stream, so
+// the same strategy code runs without a GPU (the reference's mpi_cpu build).
+#pragma once
+
+#include <condition_variable>
+#include <cstddef>
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+
+#include "dlnb/common.hpp"
+
+namespace dlnb {
+
+class Event {
+ public:
+  virtual ~Event() = default;
+};
+
+class Stream {
+ public:
+  virtual ~Stream() = default;
+  virtual void record(Event& e) = 0;
+  virtual void wait(Event& e) = 0;  // later work on this stream waits for e
+  virtual void synchronize() = 0;   // host waits for all enqueued work
+  virtual bool query() = 0;         // true when all enqueued work is done
+  virtual void* native() = 0;       // hipStream_t on GPU, nullptr on CPU
+};
+
+class Device;
+
+// Owning buffer (device memory on GPU, page-aligned host memory on CPU).
+class Buffer {
+ public:
+  Buffer() = default;
+  Buffer(Device* dev, size_t bytes);
+  ~Buffer();
+  Buffer(const Buffer&) = delete;
+  Buffer& operator=(const Buffer&) = delete;
+  Buffer(Buffer&& o) noexcept { *this = std::move(o); }
+  Buffer& operator=(Buffer&& o) noexcept;
+  void* data() const { return ptr_; }
+  size_t bytes() const { return bytes_; }
+  template <typename T>
+  T* as() const {
+    return static_cast<T*>(ptr_);
+  }
+  char* at(size_t byte_offset) const { return static_cast<char*>(ptr_) + byte_offset; }
+
+ private:
+  Device* dev_ = nullptr;
+  void* ptr_ = nullptr;
+  size_t bytes_ = 0;
+};
+
+class Device {
+ public:
+  virtual ~Device() = default;
+  virtual DeviceKind kind() const = 0;
+  virtual std::string name() const = 0;
+  virtual int index() const = 0;
+  virtual std::unique_ptr<Stream> create_stream(bool high_priority) = 0;
+  virtual std::unique_ptr<Event> create_event() = 0;
+  // Milliseconds from a to b; both must have completed.
+  virtual double elapsed_ms(Event& a, Event& b) = 0;
+  virtual void* raw_alloc(size_t bytes) = 0;
+  virtual void raw_free(void* p, size_t bytes) = 0;
+  // Fill with deterministic pseudo-random values of type t in [-1, 1)
+  // (random data keeps the MFMA units at realistic clocks, unlike zeros).
+  virtual void fill_random(void* p, size_t count, DType t, uint64_t seed, Stream& s) = 0;
+  virtual void memset_async(void* p, int v, size_t bytes, Stream& s) = 0;
+  virtual void copy_async(void* dst, const void* src, size_t bytes, Stream& s) = 0;
+  // Enqueue a host callback (CPU: task on the worker; GPU: hipLaunchHostFunc).
+  virtual void host_task(Stream& s, std::function<void()> fn) = 0;
+  virtual void synchronize() = 0;
+  virtual size_t total_memory() const = 0;
+  virtual size_t free_memory() const = 0;
+
+  Buffer alloc(size_t bytes) { return Buffer(this, bytes); }
+};
+
+// ---- CPU implementation (also used by the GPU-less tests) ----
+
+// Generation-counted event with HIP semantics: a wait() captures the most
+// recent record() at enqueue time and blocks until that record completes.
+class CpuEvent : public Event {
+ public:
+  uint64_t mark_recorded();           // host, at enqueue time
+  void complete(uint64_t gen);        // worker, when reached
+  uint64_t recorded() ;
+  void wait_for(uint64_t gen);        // worker or host
+  double time_s();
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  uint64_t recorded_ = 0;
+  uint64_t completed_ = 0;
+  double t_ = 0;
+};
+
+class CpuStream : public Stream {
+ public:
+  CpuStream();
+  ~CpuStream() override;
+  void record(Event& e) override;
+  void wait(Event& e) override;
+  void synchronize() override;
+  bool query() override;
+  void* native() override { return nullptr; }
+  void enqueue(std::function<void()> fn);
+
+ private:
+  void run();
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  size_t inflight_ = 0;
+  bool stop_ = false;
+  std::string error_;
+  std::thread th_;
+};
+
+std::unique_ptr<Device> make_cpu_device();
+
+// GPU device (HIP). local_index picks the visible device.
+std::unique_ptr<Device> make_gpu_device(int local_index);
+int gpu_device_count();  // 0 when no GPU / no HIP runtime
+// Text matrix of link type (XGMI / PCIE) and hop count between all visible
+// GPUs plus each GPU's PCI bus id (empty without GPUs).
+std::string describe_gpu_links();
+
+// Seconds on a monotonic host clock.
+double now_s();
+// Precise host sleep (nanosleep + short spin for the tail).
+void precise_sleep_us(double us);
+
+}  // namespace dlnb

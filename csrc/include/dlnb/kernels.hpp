@@ -1,0 +1,49 @@
+// Host launchers for the hand-written CDNA4 (gfx950) kernels.
+//
+// The reference has no GPU kernels at all: compute is host usleep()
+// (SURVEY.md §2.1 "GPU kernel inventory: none"). These kernels are new
+// capability: they put real, stream-ordered work on the MI355X so the
+// collectives contend for CUs / HBM / power the way they do in training.
+//   * fill_random       - vectorised hash fill (uniform [-1,1)), any dtype
+//   * idle_wait         - one wave sleeps on s_memrealtime until a deadline
+//                          (the device-side equivalent of the reference's
+//                          usleep: the GPU is idle, the stream is busy)
+//   * busy_spin         - every CU runs dependent FMAs until a deadline
+//   * gemm_tn           - C[M,N] (bf16) = A[M,K] · B[N,K]^T, MFMA 16x16x32
+//                          bf16 or OCP-fp8 e4m3 operands, 256x256 tiles,
+//                          global_load_lds staging into an XOR-swizzled LDS
+//                          image, XCD-aware tile order.
+// All launchers take the stream as void* (hipStream_t) so plain C++
+// translation units can call them.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+#include "dlnb/common.hpp"
+
+namespace dlnb {
+namespace kernels {
+
+void fill_random(void* p, size_t count, DType t, uint64_t seed, void* stream);
+
+// Deadline kernels; ticks of the 100 MHz s_memrealtime clock (see
+// wallclock_hz()).
+void idle_wait(uint64_t ticks, void* stream);
+void busy_spin(uint64_t ticks, int blocks, void* stream);
+double wallclock_hz(int device);
+int num_cus(int device);
+
+// GEMM: requires M % 256 == 0, N % 256 == 0, K*elem_size % 128 == 0, leading
+// dimensions in elements, 16-byte aligned rows. in_t is BF16 or FP8_E4M3;
+// C is always bf16.
+bool gemm_shape_ok(int M, int N, int K, DType in_t);
+void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
+             void* stream);
+
+// Elementwise "optimizer" stand-in (SGD-momentum on bf16 shards, fp32 math):
+// p = p - lr * (m = beta*m + g). Used by the optional --optimizer step.
+void sgd_momentum_bf16(void* param, void* mom, const void* grad, size_t n, float lr, float beta, void* stream);
+
+}  // namespace kernels
+}  // namespace dlnb

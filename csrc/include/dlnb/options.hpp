@@ -1,0 +1,69 @@
+// Command-line contract.
+//
+// Positional arguments and the short flags match the reference's easyargs
+// definitions (e.g. cpp/data_parallel/dp.cpp:108-122):
+//   dp            <model> <num_buckets> <base_path>
+//   fsdp          <model> <num_units> <sharding_factor> <base_path>
+//   hybrid_2d     <model> <num_stages> <num_microbatches> <base_path>
+//   hybrid_3d     <model> <num_stages> <num_microbatches> <num_tensor_shards> <base_path>
+//   hybrid_3d_moe <model> <num_stages> <num_microbatches> <num_expert_shards> <base_path>
+//   flags: -w warmups (3)  -r runs (5; hybrid_3d 3)  -d devices ("")
+//          -m min_exectime seconds (0)  -h
+// Long options are dlnb extensions (run-time backend, compute model,
+// schedule, output file, loop mode instead of separate *_loop builds).
+#pragma once
+
+#include <string>
+#include <vector>
+
+namespace dlnb {
+
+enum class StrategyKind { DP, FSDP, Hybrid2D, Hybrid3D, Hybrid3DMoE };
+
+StrategyKind parse_strategy(const std::string& s);
+const char* strategy_name(StrategyKind k);
+
+struct Options {
+  StrategyKind strategy = StrategyKind::DP;
+  std::string model;
+  std::string base_path = ".";
+  int num_buckets = 10;
+  int num_units = 1;
+  int sharding_factor = 1;
+  int num_stages = 1;
+  int num_microbatches = 1;
+  int num_tensor_shards = 1;
+  int num_expert_shards = 1;
+
+  int warmup = 3;
+  int runs = 5;
+  std::string devices;
+  double min_exectime = 0;
+  bool help = false;
+
+  // dlnb extensions
+  std::string backend = "auto";   // auto | rccl | cpu
+  std::string compute = "auto";   // auto | sleep | spin | gemm | flops
+  std::string wire_dtype = "bf16";
+  std::string compute_dtype = "auto";  // auto (from stats Dtype) | bf16 | fp8
+  std::string schedule = "overlap";    // overlap | reference
+  std::string tp_granularity = "microbatch";  // microbatch | layer
+  int dp_buckets = 1;  // hybrids: DP all-reduce buckets overlapped with the last backward
+  bool in_place = false;
+  bool optimizer = false;  // add an elementwise optimizer step over the local shard
+  bool loop = false;       // the reference's *_loop builds
+  long long max_loop_iters = 0;
+  double time_scale = 1.0;  // scales every compute duration (tests)
+  std::string json_path;
+  std::string store_addr;
+  std::string stats_file;  // explicit stats path (overrides base_path lookup)
+  bool topology = true;
+  bool quiet = false;
+};
+
+// Parses argv for the given strategy (argv[0] is the program name). Throws
+// dlnb::Error with a usage message on bad input.
+Options parse_options(StrategyKind kind, int argc, const char* const* argv);
+std::string usage(StrategyKind kind, const std::string& prog);
+
+}  // namespace dlnb

@@ -1,0 +1,106 @@
+// Strategy drivers: DP, FSDP/HSDP, DP+PP, DP+PP+TP, DP+PP+EP.
+//
+// Each driver reproduces the communication of one parallelism strategy with
+// the reference's group layout and message-size formulas (SURVEY.md
+// §2.2/§2.4) and overlaps it with synthetic compute. Unlike the reference,
+// the iteration is enqueued on streams (compute + one stream per
+// communicator) and ordered by events, so communication overlaps compute on
+// the device without the host thread in the loop; `--schedule reference`
+// re-inserts the reference's blocking points for A/B comparisons.
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "dlnb/bootstrap.hpp"
+#include "dlnb/comm.hpp"
+#include "dlnb/compute.hpp"
+#include "dlnb/device.hpp"
+#include "dlnb/json.hpp"
+#include "dlnb/options.hpp"
+#include "dlnb/timers.hpp"
+#include "dlnb/workload.hpp"
+
+namespace dlnb {
+
+struct Context {
+  Options opt;
+  std::unique_ptr<Bootstrap> boot;
+  std::unique_ptr<Device> dev;
+  std::unique_ptr<CommFactory> comms;
+  std::unique_ptr<ComputeEngine> compute;
+  ModelStats stats;
+  bool have_arch = false;
+  ModelArch arch;
+  DType wire = DType::BF16;
+  int rank() const { return boot->info.rank; }
+  int world() const { return boot->info.world_size; }
+  HostGroup& hg() { return *boot->world; }
+};
+
+// Rank layout shared by the hybrid drivers: inner (TP or EP) fastest, then
+// pipeline stage, then data-parallel replica (hybrid_3d.cpp:283-300,
+// hybrid_3d_moe.cpp:313-331; hybrid_2d is inner = 1, hybrid_2d.cpp:272-282).
+struct GridCoords {
+  int inner_id, stage_id, dp_id;
+};
+GridCoords grid_coords(int rank, int inner, int stages);
+std::vector<int> inner_group(int rank, int inner, int stages);  // same (dp, stage)
+std::vector<int> pp_group(int rank, int inner, int stages);     // same (dp, inner)
+std::vector<int> dp_group(int rank, int inner, int stages, int world);  // same (stage, inner)
+
+class Strategy {
+ public:
+  virtual ~Strategy() = default;
+  virtual void setup(Context& ctx) = 0;
+  // Enqueue one iteration (host returns once everything is enqueued; with
+  // --schedule reference it may block at the reference's blocking points).
+  virtual void enqueue_iteration() = 0;
+  // Host-wait for the iteration to finish (with failure detection).
+  virtual void synchronize() = 0;
+  virtual std::string section_id() const = 0;
+  virtual std::string section_title() const = 0;
+  // Per-rank key of the host iteration times ("runtimes"; fsdp uses "runtime").
+  virtual const char* runtime_key() const { return "runtimes"; }
+  virtual Json global_json() const = 0;
+  virtual Json rank_json() const = 0;
+  // Bus-bandwidth summary per collective kind for this rank (bytes, seconds).
+  virtual Json comm_summary() const = 0;
+  TimerSet* timers() { return timers_.get(); }
+
+ protected:
+  std::unique_ptr<TimerSet> timers_;
+};
+
+std::unique_ptr<Strategy> make_dp();
+std::unique_ptr<Strategy> make_fsdp();
+std::unique_ptr<Strategy> make_pipeline(StrategyKind kind);  // hybrid_2d / 3d / 3d_moe
+
+// Runs a whole benchmark (bootstrap -> setup -> warmup -> timed runs ->
+// report). Returns the report document (rank 0 has the gathered ranks).
+Json run_benchmark(const Options& opt);
+
+// Entry point shared by the CLI binaries; returns the process exit code.
+int main_for(StrategyKind kind, int argc, char** argv);
+
+// Synchronise a set of streams with a deadline; polls communicator async
+// errors so a dead peer aborts the job instead of hanging it.
+void sync_streams(const std::vector<Stream*>& streams, const std::vector<Communicator*>& comms, Device& dev);
+
+// Helper shared by the drivers: a stats summary for bus-bandwidth reporting.
+struct CommStat {
+  std::string name;
+  CollKind kind;
+  int nranks;
+  double bytes_per_op;  // algorithm bytes (nccl-tests convention)
+  std::string timer;    // timer key holding the op durations
+};
+Json comm_stats_json(const std::vector<CommStat>& stats, const TimerSet& t);
+
+void print_topology(Context& ctx);
+
+// Elementwise SGD-momentum over a bf16 shard (the optional --optimizer step).
+void optimizer_step(Context& ctx, Stream& s, void* param, void* mom, const void* grad, size_t n);
+
+}  // namespace dlnb

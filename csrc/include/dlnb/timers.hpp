@@ -1,0 +1,53 @@
+// Per-phase timers: device event pairs resolved after each iteration, plus
+// host wall-clock values.
+//
+// Reference: ccutils CCUTILS_MPI_TIMER_DEF/START/STOP host timers whose
+// std::vector<float> __timer_vals_<name> are dumped into the JSON sections
+// (cpp/data_parallel/dp.cpp:69-70,102-104,260-263; fsdp.cpp:61-66). Here a
+// "device" timer is a pair of events on a stream, so it measures the time the
+// stream spent in an operation (a collective's duration on its comm stream,
+// or the compute stream's stall waiting for a collective = exposed comm).
+#pragma once
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "dlnb/device.hpp"
+#include "dlnb/json.hpp"
+
+namespace dlnb {
+
+class TimerSet {
+ public:
+  explicit TimerSet(Device& dev) : dev_(dev) {}
+  int begin(Stream& s);
+  void end(int token, Stream& s, const std::string& name);
+  // Time the stall of stream s waiting for event e (exposed latency).
+  void stall(Stream& s, Event& e, const std::string& name);
+  void add(const std::string& name, double seconds);
+  void ensure(const std::string& name);
+  // Call after the streams involved have been synchronised.
+  void resolve();
+  void clear();
+  void set_enabled(bool on) { enabled_ = on; }
+  bool enabled() const { return enabled_; }
+  const std::vector<double>& get(const std::string& name) const;
+  double sum(const std::string& name) const;
+  Json values_json(const std::string& name) const;
+
+ private:
+  Device& dev_;
+  std::vector<std::unique_ptr<Event>> pool_;
+  size_t next_ = 0;
+  struct Pending {
+    int a, b;
+    std::string name;
+  };
+  std::vector<Pending> pending_;
+  std::map<std::string, std::vector<double>> vals_;
+  bool enabled_ = true;
+};
+
+}  // namespace dlnb

@@ -1,0 +1,376 @@
+// CDNA4 / gfx950 kernels for the dlnb runtime. See dlnb/kernels.hpp for the
+// inventory and docs/KERNELS.md for design notes and measured numbers.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#include "dlnb/kernels.hpp"
+
+#define DLNB_HIP_CHECK(expr)                                                       \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) DLNB_THROW(#expr << " failed: " << hipGetErrorString(e_)); \
+  } while (0)
+
+namespace dlnb {
+namespace kernels {
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+
+inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
+
+// ------------------------------------------------------------------ fill
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ float u01(uint64_t h, int part) {
+  // 21-bit slices of one 64-bit hash -> uniform [-1, 1)
+  uint32_t v = static_cast<uint32_t>((h >> (21 * part)) & 0x1fffff);
+  return static_cast<float>(v) * (2.0f / 2097152.0f) - 1.0f;
+}
+
+__device__ __forceinline__ uint8_t f32_to_e4m3(float f) {
+  // Saturating OCP e4m3fn conversion via the hardware packed convert.
+  int r = __builtin_amdgcn_cvt_pk_fp8_f32(f, f, 0, false);
+  return static_cast<uint8_t>(r & 0xff);
+}
+
+__device__ __forceinline__ uint8_t f32_to_e5m2(float f) {
+  int r = __builtin_amdgcn_cvt_pk_bf8_f32(f, f, 0, false);
+  return static_cast<uint8_t>(r & 0xff);
+}
+
+// Each thread produces 8 elements per step (16 B for 2-byte types).
+template <typename Tstore, int KIND>
+__global__ void fill_kernel(Tstore* __restrict__ p, size_t n8, size_t n, uint64_t seed) {
+  size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n8; i += stride) {
+    uint64_t h0 = splitmix64(seed ^ (i * 2 + 0));
+    uint64_t h1 = splitmix64(seed ^ (i * 2 + 1));
+    float f[8];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) f[j] = u01(h0, j);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) f[3 + j] = u01(h1, j);
+    f[6] = u01(h0 ^ h1, 0);
+    f[7] = u01(h0 ^ h1, 1);
+    size_t base = i * 8;
+    if (KIND == 0) {  // bf16
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = static_cast<__bf16>(f[j]);
+      if (base + 8 <= n) {
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<__bf16*>(p) + base) = v;
+      } else {
+        for (int j = 0; j < 8 && base + j < n; ++j) reinterpret_cast<__bf16*>(p)[base + j] = v[j];
+      }
+    } else if (KIND == 1) {  // fp16
+      for (int j = 0; j < 8 && base + j < n; ++j) reinterpret_cast<_Float16*>(p)[base + j] = static_cast<_Float16>(f[j]);
+    } else if (KIND == 2) {  // fp32
+      for (int j = 0; j < 8 && base + j < n; ++j) reinterpret_cast<float*>(p)[base + j] = f[j];
+    } else {  // fp8 (3 = e4m3, 4 = e5m2)
+      uint8_t b[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b[j] = KIND == 3 ? f32_to_e4m3(f[j]) : f32_to_e5m2(f[j]);
+      uint8_t* q = reinterpret_cast<uint8_t*>(p);
+      if (base + 8 <= n) {
+        uint64_t packed = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) packed |= static_cast<uint64_t>(b[j]) << (8 * j);
+        *reinterpret_cast<uint64_t*>(q + base) = packed;
+      } else {
+        for (int j = 0; j < 8 && base + j < n; ++j) q[base + j] = b[j];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------- deadlines
+
+__global__ void idle_wait_kernel(uint64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+__global__ void __launch_bounds__(256) busy_spin_kernel(uint64_t ticks, float* sink) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  float x = static_cast<float>(threadIdx.x) * 1e-3f, y = 0.999f;
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 64; ++i) x = __builtin_fmaf(x, y, 1e-3f);
+    if (__builtin_amdgcn_s_memrealtime() - t0 >= ticks) break;
+  }
+  if (x == -1.0f) sink[threadIdx.x] = x;  // never true; keeps the FMAs live
+}
+
+// ------------------------------------------------------------------ GEMM
+//
+// Tile 256 (M) x 256 (N) x 128 bytes of K per stage (64 bf16 / 128 fp8).
+// 512 threads = 8 waves as 2 (M) x 4 (N); each wave owns 128 x 64 of C as
+// 8 x 4 MFMA 16x16 accumulators (128 f32 registers).
+// LDS = 2 stages x {A, B} x 256 rows x 128 B = 128 KiB, one __shared__ array.
+//
+// Staging: global_load_lds_dwordx4 writes 1 KiB per wave-instruction
+// lane-linearly (LDS = base + 16*lane), so the bank-conflict swizzle is put on
+// the per-lane SOURCE address (cdna_hip_programming.md §5.4 rule 21): LDS slot
+// q of row r holds 16-byte chunk c = q ^ ((r >> 1) & 7). A fragment read of
+// chunk c of row r therefore looks at slot c ^ ((r >> 1) & 7); the 16 lanes of
+// each ds_read_b128 lane group then hit 16 distinct 16-B slots of the 256-B
+// bank row (conflict-free; checked by hand against the gfx950 lane groups).
+//
+// Operands are swapped in the MFMA (a <- B rows, b <- A rows) so each lane
+// ends up with 4 consecutive N columns of one M row: one 8-byte store per
+// accumulator instead of four 2-byte ones.
+
+constexpr int kTile = 256;
+constexpr int kRowBytes = 128;
+constexpr int kTileBytes = kTile * kRowBytes;  // 32 KiB
+constexpr int kStageBytes = 2 * kTileBytes;    // A + B
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * kRowBytes + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+__device__ __forceinline__ void stage_tile(const char* __restrict__ g, size_t ld_bytes, char* lds_tile, int w,
+                                           int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int slot = (i * 8 + w) * 64 + lane;
+    const int r = slot >> 3;
+    const int c = (slot & 7) ^ ((r >> 1) & 7);
+    const char* src = g + static_cast<size_t>(r) * ld_bytes + (c << 4);
+    __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(lds_tile + (i * 8 + w) * 1024), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ int xcd_remap(int b, int T) {
+  // Bijective: blocks that share an XCD (b % 8 equal) get a contiguous range
+  // of logical tile ids (cdna_hip_programming.md §5 "XCD swizzle").
+  const int q = T / 8, r = T % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+template <bool FP8>
+__global__ void __launch_bounds__(512, 2)
+    gemm_tn_256_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
+                       int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kStageBytes];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 2, wn = w & 3;
+  const int nt_m = M / kTile, nt_n = N / kTile, T = nt_m * nt_n;
+  const int b = xcd_remap(blockIdx.x, T);
+  // Grouped tile order: GROUP row-tiles share their B panels in L2.
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * nt_n;
+  const int first_m = (b / per_group) * GROUP;
+  const int gsz = min(nt_m - first_m, GROUP);
+  const int tm = first_m + (b % per_group) % gsz;
+  const int tn = (b % per_group) / gsz;
+
+  constexpr int esz = FP8 ? 1 : 2;
+  const size_t lda_b = static_cast<size_t>(lda) * esz, ldb_b = static_cast<size_t>(ldb) * esz;
+  const char* Ab = A + static_cast<size_t>(tm) * kTile * lda_b;
+  const char* Bb = B + static_cast<size_t>(tn) * kTile * ldb_b;
+  const int nk = (K * esz) / kRowBytes;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage_tile(Ab, lda_b, smem, w, lane);
+  stage_tile(Bb, ldb_b, smem + kTileBytes, w, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int r16 = lane & 15, h = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* cur = smem + (kt & 1) * kStageBytes;
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * kStageBytes;
+      stage_tile(Ab + static_cast<size_t>(kt + 1) * kRowBytes, lda_b, nxt, w, lane);
+      stage_tile(Bb + static_cast<size_t>(kt + 1) * kRowBytes, ldb_b, nxt + kTileBytes, w, lane);
+    }
+    const char* At = cur;
+    const char* Bt = cur + kTileBytes;
+    if constexpr (!FP8) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[8], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(At + swz(wm * 128 + i * 16 + r16, ks * 4 + h));
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          bfr[j] = *reinterpret_cast<const bf16x8*>(Bt + swz(wn * 64 + j * 16 + r16, ks * 4 + h));
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        long af[8], bfr[4];
+        const int chunk = ks * 2 + (h >> 1), half = (h & 1) * 8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          af[i] = *reinterpret_cast<const long*>(At + swz(wm * 128 + i * 16 + r16, chunk) + half);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          bfr[j] = *reinterpret_cast<const long*>(Bt + swz(wn * 64 + j * 16 + r16, chunk) + half);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // Epilogue: lane holds C[m = .. + (lane & 15)][n = .. + 4*(lane >> 4) + 0..3].
+  const int m_base = tm * kTile + wm * 128 + r16;
+  const int n_base = tn * kTile + wn * 64 + 4 * h;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bf16x4 o;
+      o[0] = static_cast<__bf16>(acc[i][j][0]);
+      o[1] = static_cast<__bf16>(acc[i][j][1]);
+      o[2] = static_cast<__bf16>(acc[i][j][2]);
+      o[3] = static_cast<__bf16>(acc[i][j][3]);
+      *reinterpret_cast<bf16x4*>(C + static_cast<size_t>(m_base + i * 16) * ldc + n_base + j * 16) = o;
+    }
+  }
+}
+
+// ------------------------------------------------------------- optimizer
+
+__global__ void sgd_momentum_kernel(__bf16* __restrict__ p, __bf16* __restrict__ m, const __bf16* __restrict__ g,
+                                    size_t n, float lr, float beta) {
+  size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x * 8;
+  for (size_t i = (blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x) * 8; i < n; i += stride) {
+    if (i + 8 <= n) {
+      bf16x8 pv = *reinterpret_cast<bf16x8*>(p + i);
+      bf16x8 mv = *reinterpret_cast<bf16x8*>(m + i);
+      bf16x8 gv = *reinterpret_cast<const bf16x8*>(g + i);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float mm = beta * static_cast<float>(mv[j]) + static_cast<float>(gv[j]);
+        mv[j] = static_cast<__bf16>(mm);
+        pv[j] = static_cast<__bf16>(static_cast<float>(pv[j]) - lr * mm);
+      }
+      *reinterpret_cast<bf16x8*>(p + i) = pv;
+      *reinterpret_cast<bf16x8*>(m + i) = mv;
+    } else {
+      for (size_t k = i; k < n; ++k) {
+        float mm = beta * static_cast<float>(m[k]) + static_cast<float>(g[k]);
+        m[k] = static_cast<__bf16>(mm);
+        p[k] = static_cast<__bf16>(static_cast<float>(p[k]) - lr * mm);
+      }
+    }
+  }
+}
+
+int grid_for(size_t work_items, int block) {
+  size_t g = (work_items + block - 1) / block;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return static_cast<int>(g);
+}
+
+}  // namespace
+
+void fill_random(void* p, size_t count, DType t, uint64_t seed, void* stream) {
+  if (count == 0) return;
+  size_t n8 = (count + 7) / 8;
+  int grid = grid_for(n8, 256);
+  seed = seed * 0xD1B54A32D192ED03ull + 0x632BE59BD9B4E019ull;
+  switch (t) {
+    case DType::BF16: hipLaunchKernelGGL((fill_kernel<uint16_t, 0>), grid, 256, 0, S(stream), static_cast<uint16_t*>(p), n8, count, seed); break;
+    case DType::FP16: hipLaunchKernelGGL((fill_kernel<uint16_t, 1>), grid, 256, 0, S(stream), static_cast<uint16_t*>(p), n8, count, seed); break;
+    case DType::FP32: hipLaunchKernelGGL((fill_kernel<float, 2>), grid, 256, 0, S(stream), static_cast<float*>(p), n8, count, seed); break;
+    case DType::FP8_E4M3: hipLaunchKernelGGL((fill_kernel<uint8_t, 3>), grid, 256, 0, S(stream), static_cast<uint8_t*>(p), n8, count, seed); break;
+    case DType::FP8_E5M2: hipLaunchKernelGGL((fill_kernel<uint8_t, 4>), grid, 256, 0, S(stream), static_cast<uint8_t*>(p), n8, count, seed); break;
+  }
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
+void idle_wait(uint64_t ticks, void* stream) {
+  hipLaunchKernelGGL(idle_wait_kernel, 1, 64, 0, S(stream), ticks);
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
+void busy_spin(uint64_t ticks, int blocks, void* stream) {
+  hipLaunchKernelGGL(busy_spin_kernel, blocks, 256, 0, S(stream), ticks, static_cast<float*>(nullptr));
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
+double wallclock_hz(int device) {
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) khz = 100000;
+  return static_cast<double>(khz) * 1e3;
+}
+
+int num_cus(int device) {
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n <= 0) n = 256;
+  return n;
+}
+
+bool gemm_shape_ok(int M, int N, int K, DType in_t) {
+  if (in_t != DType::BF16 && in_t != DType::FP8_E4M3) return false;
+  size_t esz = dtype_size(in_t);
+  return M > 0 && N > 0 && K > 0 && M % kTile == 0 && N % kTile == 0 && (static_cast<size_t>(K) * esz) % kRowBytes == 0;
+}
+
+void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
+             void* stream) {
+  DLNB_REQUIRE(gemm_shape_ok(M, N, K, in_t), "gemm_tn: unsupported shape M=" << M << " N=" << N << " K=" << K << " dtype="
+                                                                              << dtype_name(in_t));
+  size_t esz = dtype_size(in_t);
+  DLNB_REQUIRE(lda >= K && ldb >= K && ldc >= N, "gemm_tn: leading dimensions too small");
+  DLNB_REQUIRE((static_cast<size_t>(lda) * esz) % 16 == 0 && (static_cast<size_t>(ldb) * esz) % 16 == 0 && ldc % 4 == 0,
+               "gemm_tn: rows must be 16-byte aligned");
+  DLNB_REQUIRE(reinterpret_cast<uintptr_t>(A) % 16 == 0 && reinterpret_cast<uintptr_t>(B) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(C) % 8 == 0,
+               "gemm_tn: misaligned base pointers");
+  const int tiles = (M / kTile) * (N / kTile);
+  if (in_t == DType::BF16) {
+    hipLaunchKernelGGL(gemm_tn_256_kernel<false>, tiles, 512, 0, S(stream), static_cast<const char*>(A),
+                       static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc);
+  } else {
+    hipLaunchKernelGGL(gemm_tn_256_kernel<true>, tiles, 512, 0, S(stream), static_cast<const char*>(A),
+                       static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc);
+  }
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
+void sgd_momentum_bf16(void* param, void* mom, const void* grad, size_t n, float lr, float beta, void* stream) {
+  if (n == 0) return;
+  int grid = grid_for((n + 7) / 8, 256);
+  hipLaunchKernelGGL(sgd_momentum_kernel, grid, 256, 0, S(stream), static_cast<__bf16*>(param),
+                     static_cast<__bf16*>(mom), static_cast<const __bf16*>(grad), n, lr, beta);
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace kernels
+}  // namespace dlnb

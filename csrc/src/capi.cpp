@@ -1,0 +1,107 @@
+// C ABI for the Python package (loaded with ctypes from
+// dlnetbench_amd/_lib/libdlnb.so). Every function returns 0 on success and a
+// non-zero code on failure; dlnb_last_error() describes the failure.
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "dlnb/compute.hpp"
+#include "dlnb/kernels.hpp"
+#include "dlnb/strategy.hpp"
+#include "dlnb/workload.hpp"
+
+namespace {
+thread_local std::string g_err;
+
+char* dup(const std::string& s) {
+  char* p = static_cast<char*>(std::malloc(s.size() + 1));
+  std::memcpy(p, s.c_str(), s.size() + 1);
+  return p;
+}
+
+template <typename F>
+int guard(F f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return 1;
+  }
+}
+}  // namespace
+
+extern "C" {
+
+const char* dlnb_version() { return "dlnetbench_amd 0.1.0 (gfx950)"; }
+
+const char* dlnb_last_error() { return g_err.c_str(); }
+
+void dlnb_free(char* p) { std::free(p); }
+
+int dlnb_gpu_count() { return dlnb::gpu_device_count(); }
+
+// Runs a benchmark; *out receives the report JSON (malloc'd, free with
+// dlnb_free). argv does not include a program name.
+int dlnb_run(const char* strategy, int argc, const char** argv, char** out) {
+  return guard([&] {
+    dlnb::StrategyKind k = dlnb::parse_strategy(strategy);
+    std::vector<const char*> av;
+    av.push_back(strategy);
+    for (int i = 0; i < argc; ++i) av.push_back(argv[i]);
+    dlnb::Options o = dlnb::parse_options(k, static_cast<int>(av.size()), av.data());
+    dlnb::Json doc = dlnb::run_benchmark(o);
+    if (out) *out = dup(doc.dump());
+  });
+}
+
+int dlnb_parse_stats(const char* path, char** out) {
+  return guard([&] {
+    dlnb::ModelStats s = dlnb::parse_model_stats(path);
+    if (out) *out = dup(s.to_json().dump());
+  });
+}
+
+int dlnb_fill_random(void* p, size_t n, int dtype, unsigned long long seed, void* stream) {
+  return guard([&] { dlnb::kernels::fill_random(p, n, static_cast<dlnb::DType>(dtype), seed, stream); });
+}
+
+int dlnb_gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, int dtype,
+                 void* stream) {
+  return guard([&] {
+    dlnb::kernels::gemm_tn(A, B, C, M, N, K, lda, ldb, ldc, static_cast<dlnb::DType>(dtype), stream);
+  });
+}
+
+int dlnb_gemm_shape_ok(int M, int N, int K, int dtype) {
+  return dlnb::kernels::gemm_shape_ok(M, N, K, static_cast<dlnb::DType>(dtype)) ? 1 : 0;
+}
+
+int dlnb_idle_wait_us(double us, int device, void* stream) {
+  return guard([&] {
+    double hz = dlnb::kernels::wallclock_hz(device);
+    dlnb::kernels::idle_wait(static_cast<unsigned long long>(us * 1e-6 * hz), stream);
+  });
+}
+
+int dlnb_busy_spin_us(double us, int device, void* stream) {
+  return guard([&] {
+    double hz = dlnb::kernels::wallclock_hz(device);
+    dlnb::kernels::busy_spin(static_cast<unsigned long long>(us * 1e-6 * hz), dlnb::kernels::num_cus(device), stream);
+  });
+}
+
+int dlnb_sgd_momentum_bf16(void* p, void* m, const void* g, size_t n, float lr, float beta, void* stream) {
+  return guard([&] { dlnb::kernels::sgd_momentum_bf16(p, m, g, n, lr, beta, stream); });
+}
+
+double dlnb_wallclock_hz(int device) { return dlnb::kernels::wallclock_hz(device); }
+
+// Host conversions exposed for tests (OCP fp8 / bf16 rounding parity).
+float dlnb_bf16_to_float(unsigned short v) { return dlnb::bf16_to_float(v); }
+unsigned short dlnb_float_to_bf16(float f) { return dlnb::float_to_bf16(f); }
+float dlnb_fp8e4m3_to_float(unsigned char v) { return dlnb::fp8e4m3_to_float(v); }
+unsigned char dlnb_float_to_fp8e4m3(float f) { return dlnb::float_to_fp8e4m3(f); }
+
+}  // extern "C"

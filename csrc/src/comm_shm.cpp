@@ -1,0 +1,395 @@
+// CPU shared-memory backend: multi-process collectives and point-to-point on
+// host buffers, executed on the CPU device's worker-thread streams.
+//
+// Reference equivalent: the mpi_cpu build (MPICommunicator over calloc'd host
+// buffers, cpp/proxy_classes.hpp:53-133, README.md:96), which lets every
+// strategy run on a laptop with `mpirun -n N`. MPI is not available on the
+// target image, so ranks on one host exchange data through a POSIX shm
+// segment per communicator: W staging slots + a result region for
+// collectives, and one single-slot mailbox per (src, dst) pair for P2P.
+// Synchronisation is a sense-reversing barrier on futexes in the segment.
+#include <fcntl.h>
+#include <linux/futex.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <sys/syscall.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <sstream>
+
+#include "dlnb/comm.hpp"
+
+namespace dlnb {
+
+namespace {
+
+constexpr size_t kHeader = 4096;
+constexpr size_t kAlign = 4096;
+
+size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+struct SegHeader {
+  std::atomic<uint32_t> count;
+  std::atomic<uint32_t> gen;
+  std::atomic<uint32_t> attached;
+  uint32_t world;
+  uint64_t capacity;
+};
+
+struct Mailbox {
+  std::atomic<uint32_t> sent;  // futex word
+  std::atomic<uint32_t> taken;  // futex word
+  uint64_t bytes;
+  char pad[48];
+};
+static_assert(sizeof(Mailbox) == 64, "mailbox header must be one cache line");
+
+long futex(std::atomic<uint32_t>* addr, int op, uint32_t val) {
+  timespec ts{0, 2000000};  // 2 ms: re-check deadlines periodically
+  return syscall(SYS_futex, reinterpret_cast<uint32_t*>(addr), op, val, op == FUTEX_WAIT ? &ts : nullptr, nullptr, 0);
+}
+
+// Wait until pred() holds; spins briefly, then sleeps on the futex word.
+template <typename Pred>
+void wait_on(std::atomic<uint32_t>* word, Pred pred, double timeout_s, const char* what) {
+  for (int i = 0; i < 2000; ++i) {
+    if (pred()) return;
+    if (i > 200) sched_yield();
+  }
+  double t0 = now_s();
+  while (!pred()) {
+    uint32_t v = word->load(std::memory_order_acquire);
+    if (pred()) return;
+    futex(word, FUTEX_WAIT, v);
+    if (now_s() - t0 > timeout_s) DLNB_THROW("shm backend: timeout in " << what << " after " << timeout_s << " s");
+  }
+}
+
+void wake(std::atomic<uint32_t>* word) { futex(word, FUTEX_WAKE, INT32_MAX); }
+
+inline float bf16f(uint16_t v) {
+  uint32_t u = static_cast<uint32_t>(v) << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+inline uint16_t fbf16(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<uint16_t>(u >> 16);
+}
+
+// Sum n elements starting at element off of every source into dst, blockwise
+// through an fp32 accumulator (vectorisable inner loops).
+void reduce_sum(DType t, void* dst, const std::vector<const char*>& srcs, size_t off, size_t n) {
+  const size_t es = dtype_size(t);
+  if (srcs.size() == 1) {
+    std::memcpy(dst, srcs[0] + off * es, n * es);
+    return;
+  }
+  constexpr size_t BLK = 4096;
+  float acc[BLK];
+  for (size_t b = 0; b < n; b += BLK) {
+    const size_t m = std::min(BLK, n - b);
+    for (size_t i = 0; i < m; ++i) acc[i] = 0.f;
+    for (const char* s : srcs) {
+      const size_t e0 = off + b;
+      switch (t) {
+        case DType::BF16: {
+          const uint16_t* p = reinterpret_cast<const uint16_t*>(s) + e0;
+          for (size_t i = 0; i < m; ++i) acc[i] += bf16f(p[i]);
+          break;
+        }
+        case DType::FP32: {
+          const float* p = reinterpret_cast<const float*>(s) + e0;
+          for (size_t i = 0; i < m; ++i) acc[i] += p[i];
+          break;
+        }
+        case DType::FP16: {
+          const uint16_t* p = reinterpret_cast<const uint16_t*>(s) + e0;
+          for (size_t i = 0; i < m; ++i) acc[i] += fp16_to_float(p[i]);
+          break;
+        }
+        case DType::FP8_E4M3: {
+          const uint8_t* p = reinterpret_cast<const uint8_t*>(s) + e0;
+          for (size_t i = 0; i < m; ++i) acc[i] += fp8e4m3_to_float(p[i]);
+          break;
+        }
+        case DType::FP8_E5M2: {
+          const uint8_t* p = reinterpret_cast<const uint8_t*>(s) + e0;
+          for (size_t i = 0; i < m; ++i) acc[i] += fp8e5m2_to_float(p[i]);
+          break;
+        }
+      }
+    }
+    char* d = static_cast<char*>(dst) + b * es;
+    switch (t) {
+      case DType::BF16:
+        for (size_t i = 0; i < m; ++i) reinterpret_cast<uint16_t*>(d)[i] = fbf16(acc[i]);
+        break;
+      case DType::FP32: std::memcpy(d, acc, m * 4); break;
+      case DType::FP16:
+        for (size_t i = 0; i < m; ++i) reinterpret_cast<uint16_t*>(d)[i] = float_to_fp16(acc[i]);
+        break;
+      case DType::FP8_E4M3:
+        for (size_t i = 0; i < m; ++i) reinterpret_cast<uint8_t*>(d)[i] = float_to_fp8e4m3(acc[i]);
+        break;
+      case DType::FP8_E5M2:
+        for (size_t i = 0; i < m; ++i) reinterpret_cast<uint8_t*>(d)[i] = float_to_fp8e5m2(acc[i]);
+        break;
+    }
+  }
+}
+
+class ShmComm : public Communicator {
+ public:
+  ShmComm(const std::string& name, const std::vector<int>& members, int my_world_rank, HostGroup& world,
+          const std::string& job, size_t capacity, bool p2p)
+      : cap_(round_up(capacity ? capacity : 64, kAlign)), p2p_(p2p) {
+    name_ = name;
+    members_ = members;
+    size_ = static_cast<int>(members.size());
+    rank_ = -1;
+    for (int i = 0; i < size_; ++i)
+      if (members[i] == my_world_rank) rank_ = i;
+    DLNB_REQUIRE(rank_ >= 0, "rank " << my_world_rank << " is not a member of group " << name);
+    timeout_ = static_cast<double>(env_int("DLNB_TIMEOUT", 900));
+
+    std::ostringstream key;
+    key << "shm/" << name << "/";
+    for (int m : members) key << m << ",";
+    std::string shm_name = "/dlnb_" + job + "_" + std::to_string(std::hash<std::string>()(key.str()) & 0xffffffffffull);
+    const size_t W = static_cast<size_t>(size_);
+    slots_off_ = kHeader;
+    result_off_ = slots_off_ + W * cap_;
+    mbox_off_ = result_off_ + cap_;
+    size_t mbox_bytes = p2p ? W * W * (64 + cap_) : 0;
+    total_ = mbox_off_ + round_up(mbox_bytes, kAlign);
+
+    int fd;
+    if (rank_ == 0) {
+      shm_unlink(shm_name.c_str());
+      fd = shm_open(shm_name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+      if (fd < 0) DLNB_THROW("shm_open(" << shm_name << ") failed: " << std::strerror(errno));
+      if (ftruncate(fd, static_cast<off_t>(total_)) != 0) DLNB_THROW("ftruncate shm failed (" << total_ << " B)");
+      base_ = static_cast<char*>(mmap(nullptr, total_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0));
+      ::close(fd);
+      if (base_ == MAP_FAILED) DLNB_THROW("mmap shm failed");
+      hdr()->count.store(0);
+      hdr()->gen.store(0);
+      hdr()->attached.store(1);
+      hdr()->world = static_cast<uint32_t>(W);
+      hdr()->capacity = cap_;
+      world.store().set(key.str() + "/ready", shm_name);
+    } else {
+      world.store().get(key.str() + "/ready");
+      fd = shm_open(shm_name.c_str(), O_RDWR, 0600);
+      if (fd < 0) DLNB_THROW("shm_open(" << shm_name << ") failed: " << std::strerror(errno));
+      base_ = static_cast<char*>(mmap(nullptr, total_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0));
+      ::close(fd);
+      if (base_ == MAP_FAILED) DLNB_THROW("mmap shm failed");
+      hdr()->attached.fetch_add(1);
+    }
+    barrier();
+    if (rank_ == 0) shm_unlink(shm_name.c_str());  // mapping persists; no leak on crash
+  }
+
+  ~ShmComm() override {
+    if (base_ && base_ != MAP_FAILED) munmap(base_, total_);
+  }
+
+  std::string backend_name() const override { return "CPU-SHM"; }
+
+  void all_reduce(const void* send, void* recv, size_t count, DType t, Stream& s) override {
+    enqueue(s, [=] {
+      const size_t es = dtype_size(t), bytes = count * es;
+      check(bytes);
+      std::memcpy(slot(rank_), send, bytes);
+      barrier();
+      size_t lo, n;
+      chunk(count, rank_, lo, n);
+      reduce_sum(t, base_ + result_off_ + lo * es, all_slots(), lo, n);
+      barrier();
+      std::memcpy(recv, base_ + result_off_, bytes);
+      barrier();
+    });
+  }
+
+  void all_gather(const void* send, void* recv, size_t send_count, DType t, Stream& s) override {
+    enqueue(s, [=] {
+      const size_t bytes = send_count * dtype_size(t);
+      check(bytes);
+      std::memcpy(slot(rank_), send, bytes);
+      barrier();
+      for (int r = 0; r < size_; ++r) std::memcpy(static_cast<char*>(recv) + r * bytes, slot(r), bytes);
+      barrier();
+    });
+  }
+
+  void reduce_scatter(const void* send, void* recv, size_t recv_count, DType t, Stream& s) override {
+    enqueue(s, [=] {
+      const size_t es = dtype_size(t), bytes = recv_count * es * size_;
+      check(bytes);
+      std::memcpy(slot(rank_), send, bytes);
+      barrier();
+      reduce_sum(t, recv, all_slots(), recv_count * rank_, recv_count);
+      barrier();
+    });
+  }
+
+  void all_to_all(const void* send, void* recv, size_t count, DType t, Stream& s) override {
+    enqueue(s, [=] {
+      const size_t blk = count * dtype_size(t);
+      check(blk * size_);
+      std::memcpy(slot(rank_), send, blk * size_);
+      barrier();
+      for (int r = 0; r < size_; ++r) std::memcpy(static_cast<char*>(recv) + r * blk, slot(r) + rank_ * blk, blk);
+      barrier();
+    });
+  }
+
+  void send(const void* buf, size_t count, DType t, int peer, Stream& s) override {
+    const size_t bytes = count * dtype_size(t);
+    auto op = [=] { do_send(buf, bytes, peer); };
+    if (in_group_) {
+      group_sends_.push_back(op);
+      group_stream_ = &s;
+    } else {
+      enqueue(s, op);
+    }
+  }
+
+  void recv(void* buf, size_t count, DType t, int peer, Stream& s) override {
+    const size_t bytes = count * dtype_size(t);
+    auto op = [=] { do_recv(buf, bytes, peer); };
+    if (in_group_) {
+      group_recvs_.push_back(op);
+      group_stream_ = &s;
+    } else {
+      enqueue(s, op);
+    }
+  }
+
+  // Group: all sends (buffered into mailboxes) go first, then the receives,
+  // so a group never deadlocks on its own send/recv pairs.
+  void group_start() override { in_group_ = true; }
+  void group_end() override {
+    in_group_ = false;
+    if (!group_stream_) return;
+    auto sends = std::move(group_sends_);
+    auto recvs = std::move(group_recvs_);
+    group_sends_.clear();
+    group_recvs_.clear();
+    Stream* s = group_stream_;
+    group_stream_ = nullptr;
+    enqueue(*s, [sends, recvs] {
+      for (auto& f : sends) f();
+      for (auto& f : recvs) f();
+    });
+  }
+
+ private:
+  SegHeader* hdr() { return reinterpret_cast<SegHeader*>(base_); }
+  char* slot(int r) { return base_ + slots_off_ + static_cast<size_t>(r) * cap_; }
+  Mailbox* mbox(int src, int dst) {
+    return reinterpret_cast<Mailbox*>(base_ + mbox_off_ + (static_cast<size_t>(src) * size_ + dst) * (64 + cap_));
+  }
+  std::vector<const char*> all_slots() {
+    std::vector<const char*> v;
+    for (int r = 0; r < size_; ++r) v.push_back(slot(r));
+    return v;
+  }
+  void check(size_t bytes) {
+    if (bytes > cap_) DLNB_THROW("shm backend: message of " << bytes << " B exceeds group capacity " << cap_ << " B (" << name_ << ")");
+  }
+  void chunk(size_t count, int r, size_t& lo, size_t& n) {
+    size_t base = count / size_, rem = count % size_;
+    lo = r * base + std::min<size_t>(r, rem);
+    n = base + (static_cast<size_t>(r) < rem ? 1 : 0);
+  }
+  void enqueue(Stream& s, std::function<void()> fn) {
+    auto* cs = dynamic_cast<CpuStream*>(&s);
+    DLNB_REQUIRE(cs, "the CPU shm backend needs CPU streams (use --backend rccl on a GPU)");
+    cs->enqueue(std::move(fn));
+  }
+
+  void barrier() {
+    SegHeader* h = hdr();
+    uint32_t g = h->gen.load(std::memory_order_acquire);
+    if (h->count.fetch_add(1, std::memory_order_acq_rel) + 1 == static_cast<uint32_t>(size_)) {
+      h->count.store(0, std::memory_order_relaxed);
+      h->gen.fetch_add(1, std::memory_order_acq_rel);
+      wake(&h->gen);
+    } else {
+      wait_on(&h->gen, [&] { return h->gen.load(std::memory_order_acquire) != g; }, timeout_, "barrier");
+    }
+  }
+
+  void do_send(const void* buf, size_t bytes, int peer) {
+    DLNB_REQUIRE(p2p_, "group " << name_ << " was created without point-to-point support");
+    check(bytes);
+    Mailbox* m = mbox(rank_, peer);
+    // Wait until the previous message was taken.
+    wait_on(&m->taken, [&] { return m->taken.load(std::memory_order_acquire) == m->sent.load(std::memory_order_acquire); },
+            timeout_, "send");
+    std::memcpy(reinterpret_cast<char*>(m) + 64, buf, bytes);
+    m->bytes = bytes;
+    m->sent.fetch_add(1, std::memory_order_release);
+    wake(&m->sent);
+  }
+
+  void do_recv(void* buf, size_t bytes, int peer) {
+    DLNB_REQUIRE(p2p_, "group " << name_ << " was created without point-to-point support");
+    Mailbox* m = mbox(peer, rank_);
+    wait_on(&m->sent, [&] { return m->sent.load(std::memory_order_acquire) != m->taken.load(std::memory_order_acquire); },
+            timeout_, "recv");
+    DLNB_REQUIRE(m->bytes == bytes, "shm recv size mismatch: expected " << bytes << " got " << m->bytes);
+    std::memcpy(buf, reinterpret_cast<char*>(m) + 64, bytes);
+    m->taken.fetch_add(1, std::memory_order_release);
+    wake(&m->taken);
+  }
+
+  size_t cap_;
+  bool p2p_;
+  char* base_ = nullptr;
+  size_t total_ = 0, slots_off_ = 0, result_off_ = 0, mbox_off_ = 0;
+  double timeout_ = 900;
+  bool in_group_ = false;
+  std::vector<std::function<void()>> group_sends_, group_recvs_;
+  Stream* group_stream_ = nullptr;
+};
+
+class ShmFactory : public CommFactory {
+ public:
+  ShmFactory(HostGroup& world, Device& dev) : world_(world) {
+    DLNB_REQUIRE(dev.kind() == DeviceKind::CPU, "the cpu backend needs the CPU device (buffers in host memory)");
+    // Job id shared by all ranks so segment names never collide across jobs.
+    char buf[32];
+    std::snprintf(buf, sizeof(buf), "%d_%lx", static_cast<int>(getpid()), static_cast<unsigned long>(now_s() * 1e6));
+    job_ = world.broadcast(buf, 0);
+  }
+  std::string backend_name() const override { return "CPU-SHM"; }
+  std::unique_ptr<Communicator> create(const std::string& name, const std::vector<int>& members, size_t cap,
+                                       bool p2p) override {
+    return std::unique_ptr<Communicator>(new ShmComm(name, members, world_.rank(), world_, job_, cap, p2p));
+  }
+
+ private:
+  HostGroup& world_;
+  std::string job_;
+};
+
+}  // namespace
+
+std::unique_ptr<CommFactory> make_shm_factory(HostGroup& world, Device& dev) {
+  return std::unique_ptr<CommFactory>(new ShmFactory(world, dev));
+}
+
+}  // namespace dlnb

@@ -1,0 +1,199 @@
+#include "dlnb/compute.hpp"
+
+#include <algorithm>
+#include <cmath>
+
+#include "dlnb/kernels.hpp"
+
+namespace dlnb {
+
+ComputeMode parse_compute_mode(const std::string& s, DeviceKind dev) {
+  if (s == "auto") return dev == DeviceKind::GPU ? ComputeMode::Gemm : ComputeMode::Sleep;
+  if (s == "sleep") return ComputeMode::Sleep;
+  if (s == "spin") return ComputeMode::Spin;
+  if (s == "gemm") return ComputeMode::Gemm;
+  if (s == "flops") return ComputeMode::Flops;
+  DLNB_THROW("unknown compute mode '" << s << "' (auto, sleep, spin, gemm, flops)");
+}
+
+const char* compute_mode_name(ComputeMode m) {
+  switch (m) {
+    case ComputeMode::Sleep: return "sleep";
+    case ComputeMode::Spin: return "spin";
+    case ComputeMode::Gemm: return "gemm";
+    case ComputeMode::Flops: return "flops";
+  }
+  return "?";
+}
+
+namespace {
+
+// ------------------------------------------------------------------ CPU
+
+class CpuCompute : public ComputeEngine {
+ public:
+  CpuCompute(Device& dev, ComputeMode mode, double scale) : dev_(dev), mode_(mode), scale_(scale) {}
+  void run(Stream& s, double us, double) override {
+    double d = us * scale_;
+    if (d <= 0) return;
+    if (mode_ == ComputeMode::Spin) {
+      dev_.host_task(s, [d] {
+        double end = now_s() + d * 1e-6;
+        volatile double x = 1.0;
+        while (now_s() < end) x = x * 1.0000001 + 1e-9;
+      });
+    } else {
+      // sleep; gemm/flops have no CPU implementation and fall back to sleep.
+      dev_.host_task(s, [d] { precise_sleep_us(d); });
+    }
+  }
+  Json describe() const override {
+    Json j = Json::object();
+    j["mode"] = compute_mode_name(mode_);
+    j["effective_mode"] = mode_ == ComputeMode::Spin ? "spin" : "sleep";
+    j["time_scale"] = scale_;
+    return j;
+  }
+  ComputeMode mode() const override { return mode_; }
+
+ private:
+  Device& dev_;
+  ComputeMode mode_;
+  double scale_;
+};
+
+// ------------------------------------------------------------------ GPU
+
+struct GemmLevel {
+  int M;
+  double us;     // measured duration of one launch (back-to-back)
+  double flops;  // 2*M*N*K
+};
+
+class GpuCompute : public ComputeEngine {
+ public:
+  GpuCompute(Device& dev, ComputeMode mode, const ComputeShape& shape, double scale)
+      : dev_(dev), mode_(mode), scale_(scale) {
+    hz_ = kernels::wallclock_hz(dev.index());
+    cus_ = kernels::num_cus(dev.index());
+    dtype_ = shape.dtype == DType::FP8_E4M3 ? DType::FP8_E4M3 : DType::BF16;
+    const int kmul = dtype_ == DType::FP8_E4M3 ? 128 : 64;
+    K_ = std::max(512, (shape.hidden + kmul - 1) / kmul * kmul);
+    N_ = std::min(32768, std::max(1024, (shape.ffn + 255) / 256 * 256));
+    if (mode_ == ComputeMode::Gemm || mode_ == ComputeMode::Flops) calibrate();
+  }
+
+  void run(Stream& s, double us, double flops) override {
+    double d = us * scale_;
+    if (mode_ == ComputeMode::Sleep) {
+      if (d > 0) kernels::idle_wait(ticks(d), s.native());
+      return;
+    }
+    if (mode_ == ComputeMode::Spin) {
+      if (d > 0) kernels::busy_spin(ticks(d), cus_, s.native());
+      return;
+    }
+    if (mode_ == ComputeMode::Flops) {
+      double f = flops * scale_;
+      for (const auto& lv : levels_) {
+        long n = static_cast<long>(std::floor(f / lv.flops));
+        for (long i = 0; i < n; ++i) launch(lv.M, s);
+        f -= static_cast<double>(n) * lv.flops;
+      }
+      return;
+    }
+    // gemm: greedy fill of the duration with calibrated launches, then spin.
+    double rem = d;
+    for (const auto& lv : levels_) {
+      long n = static_cast<long>(std::floor(rem / lv.us));
+      for (long i = 0; i < n; ++i) launch(lv.M, s);
+      rem -= static_cast<double>(n) * lv.us;
+    }
+    if (rem > 1.0) kernels::busy_spin(ticks(rem), cus_, s.native());
+  }
+
+  Json describe() const override {
+    Json j = Json::object();
+    j["mode"] = compute_mode_name(mode_);
+    j["time_scale"] = scale_;
+    j["wallclock_hz"] = hz_;
+    j["num_cus"] = cus_;
+    if (!levels_.empty()) {
+      j["gemm_dtype"] = dtype_name(dtype_);
+      j["gemm_N"] = N_;
+      j["gemm_K"] = K_;
+      Json lv = Json::array();
+      for (const auto& l : levels_) {
+        Json e = Json::object();
+        e["M"] = l.M;
+        e["us_per_launch"] = l.us;
+        e["tflops"] = l.flops / (l.us * 1e-6) / 1e12;
+        lv.push_back(e);
+      }
+      j["gemm_levels"] = lv;
+    }
+    return j;
+  }
+  ComputeMode mode() const override { return mode_; }
+
+ private:
+  uint64_t ticks(double us) const { return static_cast<uint64_t>(us * 1e-6 * hz_ + 0.5); }
+
+  void launch(int M, Stream& s) {
+    kernels::gemm_tn(A_.data(), B_.data(), C_.data(), M, N_, K_, K_, K_, N_, dtype_, s.native());
+  }
+
+  void calibrate() {
+    const int Mmax = 8192;
+    const size_t esz = dtype_size(dtype_);
+    A_ = dev_.alloc(static_cast<size_t>(Mmax) * K_ * esz);
+    B_ = dev_.alloc(static_cast<size_t>(N_) * K_ * esz);
+    C_ = dev_.alloc(static_cast<size_t>(Mmax) * N_ * 2);
+    auto s = dev_.create_stream(false);
+    dev_.fill_random(A_.data(), static_cast<size_t>(Mmax) * K_, dtype_, 1, *s);
+    dev_.fill_random(B_.data(), static_cast<size_t>(N_) * K_, dtype_, 2, *s);
+    auto e0 = dev_.create_event();
+    auto e1 = dev_.create_event();
+    // Warm the clocks up (DVFS) before measuring.
+    for (int i = 0; i < 20; ++i) launch(Mmax, *s);
+    s->synchronize();
+    for (int M : {8192, 1024, 256}) {
+      // Size the batch to ~40 ms of work.
+      s->record(*e0);
+      for (int i = 0; i < 3; ++i) launch(M, *s);
+      s->record(*e1);
+      s->synchronize();
+      double probe = dev_.elapsed_ms(*e0, *e1) / 3.0;
+      int reps = std::max(5, std::min(2000, static_cast<int>(40.0 / std::max(probe, 1e-3))));
+      double best = 1e30;
+      for (int trial = 0; trial < 2; ++trial) {
+        s->record(*e0);
+        for (int i = 0; i < reps; ++i) launch(M, *s);
+        s->record(*e1);
+        s->synchronize();
+        best = std::min(best, dev_.elapsed_ms(*e0, *e1) * 1e3 / reps);
+      }
+      levels_.push_back(GemmLevel{M, best, 2.0 * M * static_cast<double>(N_) * K_});
+    }
+  }
+
+  Device& dev_;
+  ComputeMode mode_;
+  double scale_;
+  double hz_ = 1e8;
+  int cus_ = 256;
+  DType dtype_ = DType::BF16;
+  int K_ = 4096, N_ = 16384;
+  Buffer A_, B_, C_;
+  std::vector<GemmLevel> levels_;
+};
+
+}  // namespace
+
+std::unique_ptr<ComputeEngine> make_compute_engine(Device& dev, ComputeMode mode, const ComputeShape& shape,
+                                                   double time_scale) {
+  if (dev.kind() == DeviceKind::CPU) return std::unique_ptr<ComputeEngine>(new CpuCompute(dev, mode, time_scale));
+  return std::unique_ptr<ComputeEngine>(new GpuCompute(dev, mode, shape, time_scale));
+}
+
+}  // namespace dlnb

@@ -1,0 +1,231 @@
+#include <sys/mman.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+
+#include "dlnb/device.hpp"
+
+namespace dlnb {
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void precise_sleep_us(double us) {
+  if (us <= 0) return;
+  double t_end = now_s() + us * 1e-6;
+  // Sleep for all but the last ~100 µs, then spin: usleep() alone overshoots
+  // by 50-100 µs on a loaded host, which the reference silently absorbs
+  // into its compute time (cpp/data_parallel/dp.cpp:93,98).
+  double coarse = us * 1e-6 - 1e-4;
+  if (coarse > 0) {
+    timespec ts;
+    ts.tv_sec = static_cast<time_t>(coarse);
+    ts.tv_nsec = static_cast<long>((coarse - static_cast<double>(ts.tv_sec)) * 1e9);
+    while (nanosleep(&ts, &ts) != 0) {
+    }
+  }
+  while (now_s() < t_end) {
+  }
+}
+
+// ------------------------------------------------------------------ Buffer
+
+Buffer::Buffer(Device* dev, size_t bytes) : dev_(dev), bytes_(bytes) {
+  ptr_ = bytes ? dev->raw_alloc(bytes) : nullptr;
+}
+
+Buffer::~Buffer() {
+  if (ptr_ && dev_) dev_->raw_free(ptr_, bytes_);
+}
+
+Buffer& Buffer::operator=(Buffer&& o) noexcept {
+  if (this != &o) {
+    if (ptr_ && dev_) dev_->raw_free(ptr_, bytes_);
+    dev_ = o.dev_;
+    ptr_ = o.ptr_;
+    bytes_ = o.bytes_;
+    o.ptr_ = nullptr;
+    o.bytes_ = 0;
+  }
+  return *this;
+}
+
+// ---------------------------------------------------------------- CpuEvent
+
+uint64_t CpuEvent::mark_recorded() {
+  std::lock_guard<std::mutex> g(mu_);
+  return ++recorded_;
+}
+
+uint64_t CpuEvent::recorded() {
+  std::lock_guard<std::mutex> g(mu_);
+  return recorded_;
+}
+
+void CpuEvent::complete(uint64_t gen) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (gen > completed_) {
+      completed_ = gen;
+      t_ = now_s();
+    }
+  }
+  cv_.notify_all();
+}
+
+void CpuEvent::wait_for(uint64_t gen) {
+  std::unique_lock<std::mutex> g(mu_);
+  cv_.wait(g, [&] { return completed_ >= gen; });
+}
+
+double CpuEvent::time_s() {
+  wait_for(recorded());
+  std::lock_guard<std::mutex> g(mu_);
+  return t_;
+}
+
+// --------------------------------------------------------------- CpuStream
+
+CpuStream::CpuStream() : th_([this] { run(); }) {}
+
+CpuStream::~CpuStream() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  th_.join();
+}
+
+void CpuStream::enqueue(std::function<void()> fn) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    q_.push_back(std::move(fn));
+    ++inflight_;
+  }
+  cv_.notify_all();
+}
+
+void CpuStream::run() {
+  for (;;) {
+    std::function<void()> fn;
+    {
+      std::unique_lock<std::mutex> g(mu_);
+      cv_.wait(g, [&] { return stop_ || !q_.empty(); });
+      if (q_.empty()) return;
+      fn = std::move(q_.front());
+      q_.pop_front();
+    }
+    try {
+      fn();
+    } catch (const std::exception& e) {
+      // A failed task would leave peers and other streams waiting forever:
+      // fail the whole rank loudly (the launcher tears the job down).
+      std::fprintf(stderr, "[dlnb] fatal error on CPU stream: %s\n", e.what());
+      std::fflush(stderr);
+      std::_Exit(17);
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      --inflight_;
+    }
+    cv_.notify_all();
+  }
+}
+
+void CpuStream::record(Event& e) {
+  auto* ce = dynamic_cast<CpuEvent*>(&e);
+  DLNB_REQUIRE(ce, "CPU stream needs a CPU event");
+  uint64_t gen = ce->mark_recorded();
+  enqueue([ce, gen] { ce->complete(gen); });
+}
+
+void CpuStream::wait(Event& e) {
+  auto* ce = dynamic_cast<CpuEvent*>(&e);
+  DLNB_REQUIRE(ce, "CPU stream needs a CPU event");
+  uint64_t gen = ce->recorded();
+  if (gen == 0) return;  // never recorded: nothing to wait for (HIP semantics)
+  enqueue([ce, gen] { ce->wait_for(gen); });
+}
+
+bool CpuStream::query() {
+  std::lock_guard<std::mutex> g(mu_);
+  return inflight_ == 0;
+}
+
+void CpuStream::synchronize() {
+  std::unique_lock<std::mutex> g(mu_);
+  cv_.wait(g, [&] { return inflight_ == 0; });
+  if (!error_.empty()) {
+    std::string e = error_;
+    error_.clear();
+    DLNB_THROW("CPU stream task failed: " << e);
+  }
+}
+
+// --------------------------------------------------------------- CpuDevice
+
+namespace {
+
+class CpuDevice : public Device {
+ public:
+  DeviceKind kind() const override { return DeviceKind::CPU; }
+  std::string name() const override { return "CPU"; }
+  int index() const override { return 0; }
+  std::unique_ptr<Stream> create_stream(bool) override { return std::unique_ptr<Stream>(new CpuStream()); }
+  std::unique_ptr<Event> create_event() override { return std::unique_ptr<Event>(new CpuEvent()); }
+  double elapsed_ms(Event& a, Event& b) override {
+    auto* ea = dynamic_cast<CpuEvent*>(&a);
+    auto* eb = dynamic_cast<CpuEvent*>(&b);
+    DLNB_REQUIRE(ea && eb, "CPU events expected");
+    return (eb->time_s() - ea->time_s()) * 1e3;
+  }
+  void* raw_alloc(size_t bytes) override {
+    // calloc semantics like the reference's CPU Tensor (proxy_classes.hpp:395-400).
+    void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) DLNB_THROW("host allocation of " << bytes << " bytes failed");
+    return p;
+  }
+  void raw_free(void* p, size_t bytes) override { munmap(p, bytes); }
+  void fill_random(void* p, size_t count, DType t, uint64_t seed, Stream& s) override {
+    auto* cs = dynamic_cast<CpuStream*>(&s);
+    cs->enqueue([p, count, t, seed] {
+      uint64_t x = seed * 0x9E3779B97F4A7C15ull + 1;
+      for (size_t i = 0; i < count; ++i) {
+        x ^= x << 13;
+        x ^= x >> 7;
+        x ^= x << 17;
+        float f = static_cast<float>((x >> 40) & 0xffffff) / 8388608.0f - 1.0f;
+        switch (t) {
+          case DType::BF16: static_cast<uint16_t*>(p)[i] = float_to_bf16(f); break;
+          case DType::FP16: static_cast<uint16_t*>(p)[i] = float_to_fp16(f); break;
+          case DType::FP32: static_cast<float*>(p)[i] = f; break;
+          case DType::FP8_E4M3: static_cast<uint8_t*>(p)[i] = static_cast<uint8_t>(((x >> 20) & 0x77) | ((x >> 8) & 0x80)); break;
+          case DType::FP8_E5M2: static_cast<uint8_t*>(p)[i] = float_to_fp8e5m2(f); break;
+        }
+      }
+    });
+  }
+  void memset_async(void* p, int v, size_t bytes, Stream& s) override {
+    dynamic_cast<CpuStream&>(s).enqueue([p, v, bytes] { std::memset(p, v, bytes); });
+  }
+  void copy_async(void* dst, const void* src, size_t bytes, Stream& s) override {
+    dynamic_cast<CpuStream&>(s).enqueue([dst, src, bytes] { std::memcpy(dst, src, bytes); });
+  }
+  void host_task(Stream& s, std::function<void()> fn) override { dynamic_cast<CpuStream&>(s).enqueue(std::move(fn)); }
+  void synchronize() override {}
+  size_t total_memory() const override { return static_cast<size_t>(sysconf(_SC_PHYS_PAGES)) * sysconf(_SC_PAGE_SIZE); }
+  size_t free_memory() const override { return static_cast<size_t>(sysconf(_SC_AVPHYS_PAGES)) * sysconf(_SC_PAGE_SIZE); }
+};
+
+}  // namespace
+
+std::unique_ptr<Device> make_cpu_device() { return std::unique_ptr<Device>(new CpuDevice()); }
+
+}  // namespace dlnb

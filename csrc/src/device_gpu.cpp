@@ -1,0 +1,169 @@
+// HIP implementation of the device layer (MI355X / gfx950).
+#include <hip/hip_runtime.h>
+#include <hsa/hsa_ext_amd.h>
+
+#include <cstdio>
+
+#include "dlnb/device.hpp"
+#include "dlnb/kernels.hpp"
+
+#define DLNB_HIP_CHECK(expr)                                                       \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) DLNB_THROW(#expr << " failed: " << hipGetErrorString(e_)); \
+  } while (0)
+
+namespace dlnb {
+
+namespace {
+
+class GpuEvent : public Event {
+ public:
+  GpuEvent() { DLNB_HIP_CHECK(hipEventCreate(&ev)); }
+  ~GpuEvent() override { (void)hipEventDestroy(ev); }
+  hipEvent_t ev{};
+};
+
+class GpuStream : public Stream {
+ public:
+  GpuStream(int device, bool high_priority) {
+    DLNB_HIP_CHECK(hipSetDevice(device));
+    int lo = 0, hi = 0;
+    DLNB_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    // hi is the numerically smallest (= greatest) priority.
+    DLNB_HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high_priority ? hi : lo));
+  }
+  ~GpuStream() override { (void)hipStreamDestroy(s); }
+  void record(Event& e) override { DLNB_HIP_CHECK(hipEventRecord(static_cast<GpuEvent&>(e).ev, s)); }
+  void wait(Event& e) override { DLNB_HIP_CHECK(hipStreamWaitEvent(s, static_cast<GpuEvent&>(e).ev, 0)); }
+  void synchronize() override { DLNB_HIP_CHECK(hipStreamSynchronize(s)); }
+  bool query() override {
+    hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return true;
+    if (e == hipErrorNotReady) return false;
+    DLNB_THROW("hipStreamQuery failed: " << hipGetErrorString(e));
+  }
+  void* native() override { return s; }
+  hipStream_t s{};
+};
+
+void host_trampoline(void* p) {
+  auto* fn = static_cast<std::function<void()>*>(p);
+  (*fn)();
+  delete fn;
+}
+
+class GpuDevice : public Device {
+ public:
+  explicit GpuDevice(int idx) : idx_(idx) {
+    DLNB_HIP_CHECK(hipSetDevice(idx_));
+    hipDeviceProp_t prop;
+    DLNB_HIP_CHECK(hipGetDeviceProperties(&prop, idx_));
+    name_ = prop.name;
+    arch_ = prop.gcnArchName;
+    total_ = prop.totalGlobalMem;
+  }
+  DeviceKind kind() const override { return DeviceKind::GPU; }
+  std::string name() const override { return name_ + " (" + arch_ + ")"; }
+  int index() const override { return idx_; }
+  std::unique_ptr<Stream> create_stream(bool high_priority) override {
+    return std::unique_ptr<Stream>(new GpuStream(idx_, high_priority));
+  }
+  std::unique_ptr<Event> create_event() override { return std::unique_ptr<Event>(new GpuEvent()); }
+  double elapsed_ms(Event& a, Event& b) override {
+    float ms = 0;
+    DLNB_HIP_CHECK(hipEventSynchronize(static_cast<GpuEvent&>(b).ev));
+    DLNB_HIP_CHECK(hipEventElapsedTime(&ms, static_cast<GpuEvent&>(a).ev, static_cast<GpuEvent&>(b).ev));
+    return ms;
+  }
+  void* raw_alloc(size_t bytes) override {
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess)
+      DLNB_THROW("hipMalloc(" << bytes << " B) failed on device " << idx_ << ": " << hipGetErrorString(e));
+    // Zero like the reference's Tensor (proxy_classes.hpp:403-409).
+    DLNB_HIP_CHECK(hipMemset(p, 0, bytes));
+    return p;
+  }
+  void raw_free(void* p, size_t) override { (void)hipFree(p); }
+  void fill_random(void* p, size_t count, DType t, uint64_t seed, Stream& s) override {
+    kernels::fill_random(p, count, t, seed, s.native());
+  }
+  void memset_async(void* p, int v, size_t bytes, Stream& s) override {
+    DLNB_HIP_CHECK(hipMemsetAsync(p, v, bytes, static_cast<hipStream_t>(s.native())));
+  }
+  void copy_async(void* dst, const void* src, size_t bytes, Stream& s) override {
+    DLNB_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, static_cast<hipStream_t>(s.native())));
+  }
+  void host_task(Stream& s, std::function<void()> fn) override {
+    auto* heap = new std::function<void()>(std::move(fn));
+    DLNB_HIP_CHECK(hipLaunchHostFunc(static_cast<hipStream_t>(s.native()), host_trampoline, heap));
+  }
+  void synchronize() override { DLNB_HIP_CHECK(hipDeviceSynchronize()); }
+  size_t total_memory() const override { return total_; }
+  size_t free_memory() const override {
+    size_t f = 0, t = 0;
+    if (hipMemGetInfo(&f, &t) != hipSuccess) return 0;
+    return f;
+  }
+
+ private:
+  int idx_;
+  std::string name_, arch_;
+  size_t total_ = 0;
+};
+
+}  // namespace
+
+std::unique_ptr<Device> make_gpu_device(int local_index) { return std::unique_ptr<Device>(new GpuDevice(local_index)); }
+
+int gpu_device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+std::string describe_gpu_links() {
+  int n = gpu_device_count();
+  if (n <= 0) return "";
+  std::string out;
+  char buf[256];
+  for (int i = 0; i < n; ++i) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), i) != hipSuccess) std::snprintf(bus, sizeof(bus), "?");
+    hipDeviceProp_t prop;
+    std::string nm = hipGetDeviceProperties(&prop, i) == hipSuccess ? prop.name : "?";
+    std::snprintf(buf, sizeof(buf), "  GPU%d  %s  %s  CUs=%d\n", i, bus, nm.c_str(),
+                  hipGetDeviceProperties(&prop, i) == hipSuccess ? prop.multiProcessorCount : 0);
+    out += buf;
+  }
+  if (n > 1) {
+    out += "  link/hops ";
+    for (int j = 0; j < n; ++j) {
+      std::snprintf(buf, sizeof(buf), " %8s", ("GPU" + std::to_string(j)).c_str());
+      out += buf;
+    }
+    out += "\n";
+    for (int i = 0; i < n; ++i) {
+      std::snprintf(buf, sizeof(buf), "  GPU%-6d", i);
+      out += buf;
+      for (int j = 0; j < n; ++j) {
+        if (i == j) {
+          std::snprintf(buf, sizeof(buf), " %8s", "-");
+        } else {
+          uint32_t lt = 0, hops = 0;
+          const char* name = "?";
+          if (hipExtGetLinkTypeAndHopCount(i, j, &lt, &hops) == hipSuccess) {
+            name = lt == HSA_AMD_LINK_INFO_TYPE_XGMI ? "XGMI" : lt == HSA_AMD_LINK_INFO_TYPE_PCIE ? "PCIE" : "OTHER";
+          }
+          std::snprintf(buf, sizeof(buf), " %5s/%-2u", name, hops);
+        }
+        out += buf;
+      }
+      out += "\n";
+    }
+  }
+  return out;
+}
+
+}  // namespace dlnb

@@ -1,0 +1,379 @@
+// Benchmark runner shared by all strategies: bootstrap, device/backend
+// selection, warm-up, run-count estimation, timed runs, loop mode, report.
+//
+// Reference flow: main() of each driver (e.g. cpp/data_parallel/dp.cpp:127-303):
+// parse args -> read stats -> MPI_Init -> topology print -> set device ->
+// CCL init -> buffers -> barrier -> warm-up (MPI_Wtime) -> optional
+// estimate_runs -> PROXY_LOOP or timed runs -> ccutils JSON section.
+// Deviations: estimate_runs averages warm-ups over warm-ups (the reference
+// divides a world-sum by the warm-up count, cpp/utils.hpp:127-128) and takes
+// the max over ranks; loop mode is a run-time flag (or a *_loop argv[0]).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <fstream>
+#include <iostream>
+#include <map>
+#include <sstream>
+#include <thread>
+
+#include "dlnb/kernels.hpp"
+#include "dlnb/strategy.hpp"
+
+namespace dlnb {
+
+void sync_streams(const std::vector<Stream*>& streams, const std::vector<Communicator*>& comms, Device& dev) {
+  (void)dev;
+  const double timeout = static_cast<double>(env_int("DLNB_TIMEOUT", 900));
+  const double t0 = now_s();
+  int polls = 0;
+  for (Stream* s : streams) {
+    while (!s->query()) {
+      if (++polls % 64 == 0) {
+        for (Communicator* c : comms) {
+          if (!c) continue;
+          std::string err = c->async_error();
+          if (!err.empty()) {
+            for (Communicator* a : comms)
+              if (a) a->abort();
+            DLNB_THROW("communication failure: " << err);
+          }
+        }
+        if (now_s() - t0 > timeout) {
+          for (Communicator* a : comms)
+            if (a) a->abort();
+          DLNB_THROW("iteration did not complete within DLNB_TIMEOUT=" << timeout
+                                                                       << " s (hung collective or dead peer)");
+        }
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  }
+}
+
+Json comm_stats_json(const std::vector<CommStat>& stats, const TimerSet& t) {
+  Json out = Json::object();
+  for (const auto& s : stats) {
+    const auto& v = t.get(s.timer);
+    Json e = Json::object();
+    e["kind"] = s.name;
+    e["nranks"] = s.nranks;
+    e["bytes_per_op"] = s.bytes_per_op;
+    e["ops"] = static_cast<long long>(v.size());
+    double tot = 0;
+    for (double x : v) tot += x;
+    e["total_s"] = tot;
+    if (!v.empty() && tot > 0) {
+      double algbw = s.bytes_per_op * v.size() / tot / 1e9;
+      e["algbw_GBps"] = algbw;
+      e["busbw_GBps"] = algbw * busbw_factor(s.kind, s.nranks);
+    }
+    out[s.name] = e;
+  }
+  return out;
+}
+
+void optimizer_step(Context& ctx, Stream& s, void* param, void* mom, const void* grad, size_t n) {
+  if (ctx.dev->kind() == DeviceKind::GPU) {
+    kernels::sgd_momentum_bf16(param, mom, grad, n, 1e-4f, 0.9f, s.native());
+    return;
+  }
+  ctx.dev->host_task(s, [param, mom, grad, n] {
+    auto* p = static_cast<uint16_t*>(param);
+    auto* m = static_cast<uint16_t*>(mom);
+    auto* g = static_cast<const uint16_t*>(grad);
+    for (size_t i = 0; i < n; ++i) {
+      float mv = 0.9f * bf16_to_float(m[i]) + bf16_to_float(g[i]);
+      m[i] = float_to_bf16(mv);
+      p[i] = float_to_bf16(bf16_to_float(p[i]) - 1e-4f * mv);
+    }
+  });
+}
+
+// ------------------------------------------------------------- topology
+
+void print_topology(Context& ctx) {
+  // Reference: cpp/netcommunicators.hpp:142-290 builds a switch/node tree
+  // from SLURM_TOPOLOGY_ADDR (fake address when SLURM is absent, :154-157).
+  // Here each rank also reports its GPU, and rank 0 prints the node's
+  // xGMI link matrix.
+  std::string addr = env_or("SLURM_TOPOLOGY_ADDR", "");
+  if (addr.empty()) addr = "root." + ctx.boot->info.hostname;
+  std::ostringstream me;
+  me << addr << "|" << ctx.boot->info.hostname << "|" << ctx.dev->name() << "|" << ctx.dev->index();
+  auto all = ctx.hg().allgather(me.str());
+  if (ctx.rank() != 0) return;
+  // path -> ranks
+  std::map<std::string, std::vector<int>> leaves;
+  std::map<std::string, std::string> dev_of;
+  for (size_t r = 0; r < all.size(); ++r) {
+    auto f = split(all[r], '|');
+    leaves[f[0]].push_back(static_cast<int>(r));
+    dev_of[f[0]] = f.size() > 2 ? f[2] : "?";
+  }
+  std::ostringstream os;
+  os << "=== topology: " << all.size() << " ranks on " << leaves.size() << " node(s) ===\n";
+  std::vector<std::string> prev;
+  for (const auto& kv : leaves) {
+    auto parts = split(kv.first, '.');
+    size_t common = 0;
+    while (common < prev.size() && common < parts.size() - 1 && prev[common] == parts[common]) ++common;
+    for (size_t d = common; d < parts.size(); ++d) {
+      os << std::string(2 * d, ' ') << (d ? "└─ " : "") << parts[d];
+      if (d + 1 == parts.size()) {
+        os << "  ranks [";
+        for (size_t i = 0; i < kv.second.size(); ++i) os << (i ? "," : "") << kv.second[i];
+        os << "]  " << dev_of[kv.first];
+      }
+      os << "\n";
+    }
+    prev = parts;
+  }
+  if (ctx.dev->kind() == DeviceKind::GPU) os << describe_gpu_links();
+  std::cout << os.str() << std::flush;
+}
+
+namespace {
+
+std::vector<int> parse_device_list(const std::string& s) {
+  std::vector<int> v;
+  if (s.empty()) return v;
+  for (auto& p : split(s, ',')) {
+    std::string t = trim(p);
+    if (!t.empty()) v.push_back(std::stoi(t));
+  }
+  return v;
+}
+
+double percentile(std::vector<double> v, double q) {
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  double pos = q * (v.size() - 1);
+  size_t lo = static_cast<size_t>(std::floor(pos)), hi = static_cast<size_t>(std::ceil(pos));
+  return v[lo] + (v[hi] - v[lo]) * (pos - lo);
+}
+
+std::unique_ptr<Strategy> make_strategy(StrategyKind k) {
+  switch (k) {
+    case StrategyKind::DP: return make_dp();
+    case StrategyKind::FSDP: return make_fsdp();
+    default: return make_pipeline(k);
+  }
+}
+
+bool file_exists(const std::string& p) {
+  std::ifstream f(p);
+  return static_cast<bool>(f);
+}
+
+}  // namespace
+
+Json run_benchmark(const Options& opt) {
+  Context ctx;
+  ctx.opt = opt;
+  ctx.boot = bootstrap_from_env(opt.store_addr);
+  const RankInfo& ri = ctx.boot->info;
+
+  // ---- backend / device (cpp/utils.hpp:62-117 set_local_device)
+  std::string backend = opt.backend;
+  const int ngpu = gpu_device_count();
+  if (backend == "auto") backend = ngpu > 0 ? "rccl" : "cpu";
+  if (backend == "rccl") {
+    DLNB_REQUIRE(ngpu > 0, "--backend rccl requested but no GPU is visible");
+    std::vector<int> list = parse_device_list(opt.devices);
+    if (list.empty())
+      for (int i = 0; i < ngpu; ++i) list.push_back(i);
+    DLNB_REQUIRE(ri.local_rank < static_cast<int>(list.size()),
+                 "local rank " << ri.local_rank << " has no device (device list has " << list.size() << ")");
+    int dev_index = list[static_cast<size_t>(ri.local_rank)];
+    DLNB_REQUIRE(dev_index >= 0 && dev_index < ngpu, "device id " << dev_index << " out of range");
+    ctx.dev = make_gpu_device(dev_index);
+    ctx.comms = make_rccl_factory(ctx.hg(), *ctx.dev);
+  } else if (backend == "cpu") {
+    ctx.dev = make_cpu_device();
+    ctx.comms = make_shm_factory(ctx.hg(), *ctx.dev);
+  } else {
+    DLNB_THROW("unknown backend '" << backend << "' (auto, rccl, cpu)");
+  }
+
+  // ---- workload
+  std::string stats_path = opt.stats_file.empty() ? stats_path_for(opt.base_path, opt.model) : opt.stats_file;
+  ctx.stats = parse_model_stats(stats_path);
+  if (!opt.base_path.empty()) {
+    std::string ap;
+    try {
+      ap = arch_path_for(opt.base_path, opt.model);
+    } catch (const Error&) {
+    }
+    if (!ap.empty() && file_exists(ap)) {
+      ctx.arch = parse_model_arch(ap);
+      ctx.have_arch = true;
+    }
+  }
+  ctx.wire = parse_dtype(opt.wire_dtype);
+  ComputeShape shape;
+  shape.hidden = static_cast<int>(ctx.stats.embedded_dim);
+  uint64_t ffn = ctx.stats.ffn_dim ? ctx.stats.ffn_dim : (ctx.have_arch && ctx.arch.ff_dim ? ctx.arch.ff_dim : 4 * ctx.stats.embedded_dim);
+  shape.ffn = static_cast<int>(ffn);
+  std::string cdt = opt.compute_dtype;
+  if (cdt == "auto") cdt = ctx.stats.dtype.find("8") != std::string::npos ? "fp8" : "bf16";
+  shape.dtype = parse_dtype(cdt);
+  ComputeMode mode = parse_compute_mode(opt.compute, ctx.dev->kind());
+  ctx.compute = make_compute_engine(*ctx.dev, mode, shape, opt.time_scale);
+
+  if (opt.topology) print_topology(ctx);
+
+  auto strat = make_strategy(opt.strategy);
+  strat->setup(ctx);
+  TimerSet& T = *strat->timers();
+  const char* rkey = strat->runtime_key();
+  T.ensure(rkey);
+  ctx.hg().barrier();
+
+  // ---- warm-up
+  std::vector<double> warm;
+  for (int i = 0; i < opt.warmup; ++i) {
+    double t0 = now_s();
+    strat->enqueue_iteration();
+    strat->synchronize();
+    warm.push_back(now_s() - t0);
+  }
+  T.clear();
+
+  int runs = opt.runs;
+  if (opt.min_exectime > 0) {
+    // Skip the first two warm-ups when there are more (cpp/utils.hpp:121-135).
+    double s = 0;
+    int n = 0;
+    for (size_t i = warm.size() > 2 ? 2 : 0; i < warm.size(); ++i, ++n) s += warm[i];
+    double avg = n ? s / n : 1.0;
+    avg = ctx.hg().allreduce_max(avg);
+    runs = std::max(1, static_cast<int>(std::ceil(opt.min_exectime / std::max(avg, 1e-9))));
+    if (ri.rank == 0 && !opt.quiet)
+      std::cout << "Estimated runs based on warm-up times to meet minimum execution time: " << runs << std::endl;
+  }
+
+  Json doc = Json::object();
+  if (opt.loop) {
+    // Interference generator (the reference's *_loop builds): no timers,
+    // runs forever unless --max-loop-iters bounds it.
+    T.set_enabled(false);
+    for (long long it = 0; opt.max_loop_iters == 0 || it < opt.max_loop_iters; ++it) {
+      strat->enqueue_iteration();
+      strat->synchronize();
+    }
+    ctx.hg().barrier();
+    doc["section"] = strat->section_id();
+    doc["loop_iterations"] = opt.max_loop_iters;
+    return doc;
+  }
+
+  ctx.hg().barrier();
+  ctx.dev->synchronize();
+  const double T0 = now_s();
+  for (int r = 0; r < runs; ++r) {
+    double t0 = now_s();
+    strat->enqueue_iteration();
+    strat->synchronize();
+    T.add(rkey, now_s() - t0);
+  }
+  ctx.dev->synchronize();
+  ctx.hg().barrier();
+  const double timed_region = ctx.hg().allreduce_max(now_s() - T0);
+
+  // ---- report
+  Json rank = strat->rank_json();
+  rank["hostname"] = ri.hostname;
+  rank["rank"] = ri.rank;
+  rank["local_rank"] = ri.local_rank;
+  rank["device_name"] = ctx.dev->name();
+  rank["device_index"] = ctx.dev->index();
+  rank["comm"] = strat->comm_summary();
+  auto all = ctx.hg().allgather(rank.dump());
+
+  Json g = strat->global_json();
+  Json ext = Json::object();
+  ext["strategy"] = strategy_name(opt.strategy);
+  ext["schedule"] = opt.schedule;
+  ext["wire_dtype"] = dtype_name(ctx.wire);
+  ext["compute"] = ctx.compute->describe();
+  ext["stats_file"] = stats_path;
+  ext["stats_dtype"] = ctx.stats.dtype;
+  ext["stats_device"] = ctx.stats.device;
+  ext["warmup"] = opt.warmup;
+  ext["runs"] = runs;
+  ext["warmup_times"] = Json(warm);
+  ext["timed_region_s"] = timed_region;
+  // Iteration time = max over ranks per run (the slowest rank bounds a step).
+  std::vector<Json> ranks;
+  for (const auto& s : all) ranks.push_back(Json::parse(s));
+  std::vector<double> per_run(static_cast<size_t>(runs), 0.0);
+  for (const auto& rj : ranks) {
+    const Json& v = rj.at(rkey);
+    for (size_t i = 0; i < v.size() && i < per_run.size(); ++i) per_run[i] = std::max(per_run[i], v.at(i).as_double());
+  }
+  Json it = Json::object();
+  it["per_run_max_s"] = Json(per_run);
+  it["median_ms"] = percentile(per_run, 0.5) * 1e3;
+  double mean = 0;
+  for (double x : per_run) mean += x;
+  it["mean_ms"] = per_run.empty() ? 0.0 : mean / per_run.size() * 1e3;
+  it["p95_ms"] = percentile(per_run, 0.95) * 1e3;
+  it["min_ms"] = per_run.empty() ? 0.0 : *std::min_element(per_run.begin(), per_run.end()) * 1e3;
+  it["timed_ms_per_iter"] = runs > 0 ? timed_region / runs * 1e3 : 0.0;
+  double floor_us = ctx.stats.avg_forward_time_us + ctx.stats.avg_backward_time_us;
+  it["compute_floor_ms"] = floor_us / 1e3 * opt.time_scale;
+  ext["iteration"] = it;
+  g["dlnb"] = ext;
+
+  doc["section"] = strat->section_id();
+  doc["title"] = strat->section_title();
+  doc["global"] = g;
+  Json rarr = Json::array();
+  for (auto& r : ranks) rarr.push_back(r);
+  doc["ranks"] = rarr;
+
+  if (ri.rank == 0) {
+    std::string text = doc.dump();
+    std::cout << "<<<DLNB_REPORT_BEGIN " << strat->section_id() << ">>>\n"
+              << text << "\n<<<DLNB_REPORT_END " << strat->section_id() << ">>>" << std::endl;
+    if (!opt.quiet) {
+      std::printf("[dlnb] %s %s W=%d backend=%s compute=%s: iter median %.3f ms (floor %.3f ms), timed %.3f ms/iter\n",
+                  strategy_name(opt.strategy), opt.model.c_str(), ri.world_size, backend.c_str(),
+                  compute_mode_name(ctx.compute->mode()), it.at("median_ms").as_double(),
+                  it.at("compute_floor_ms").as_double(), it.at("timed_ms_per_iter").as_double());
+      std::fflush(stdout);
+    }
+    if (!opt.json_path.empty()) {
+      std::ofstream f(opt.json_path);
+      f << doc.dump(1) << "\n";
+    }
+  }
+  ctx.hg().barrier();  // keep the store (rank 0) alive until everyone is done
+  return doc;
+}
+
+int main_for(StrategyKind kind, int argc, char** argv) {
+  Options opt;
+  try {
+    opt = parse_options(kind, argc, argv);
+  } catch (const std::exception& e) {
+    std::cerr << e.what() << std::endl;
+    return 1;
+  }
+  std::string prog = argc > 0 ? argv[0] : "";
+  if (opt.help) {
+    std::cout << usage(kind, prog);
+    return 0;
+  }
+  if (ends_with(prog, "_loop")) opt.loop = true;
+  try {
+    run_benchmark(opt);
+  } catch (const std::exception& e) {
+    std::cerr << "[dlnb] rank " << env_or("RANK", env_or("DLNB_RANK", "0")) << " error: " << e.what() << std::endl;
+    return 2;
+  }
+  return 0;
+}
+
+}  // namespace dlnb

@@ -1,0 +1,244 @@
+// Fully sharded data parallelism (FSDP) and hybrid sharding (HSDP).
+//
+// Reference: cpp/data_parallel/fsdp.cpp. The model is split into U units;
+// each unit's parameters are sharded over F ranks (unit group = contiguous
+// blocks of F ranks, rank / F; replica group = rank % F, fsdp.cpp:258-265).
+// Per iteration (run_fsdp, fsdp.cpp:73-163):
+//   forward : all-gather unit 0; for each unit, prefetch-all-gather the next
+//             unit while computing this one;
+//   backward: prefetch-all-gather unit u-1 while computing unit u, then
+//             reduce-scatter unit u's gradient, then (W/F > 1) all-reduce the
+//             shard across replicas.
+// Shard size = ceil((P/U)/F) per unit (fsdp.cpp:244-255).
+//
+// MI355X design:
+//   * all-gathers, reduce-scatters and replica all-reduces each get their own
+//     communicator + stream, so a reduce-scatter of unit u runs concurrently
+//     with the all-gather prefetch of unit u-2 and the backward of unit u-1
+//     (the reference blocks the host on every reduce-scatter);
+//   * gathered parameters and full gradients are double-buffered (the
+//     reference gathers into a single buffer that the in-flight prefetch and
+//     the reduce-scatter share, a race - SURVEY.md §3.2); buffer reuse is
+//     ordered by events;
+//   * buffers are exactly sized in the wire dtype: llama3_8b at F=8 needs
+//     2x shards (2 GB) + 4 unit buffers (2 GB) on a 288 GB MI355X.
+#include "dlnb/strategy.hpp"
+
+namespace dlnb {
+
+namespace {
+
+class Fsdp : public Strategy {
+ public:
+  void setup(Context& ctx) override {
+    ctx_ = &ctx;
+    const auto& o = ctx.opt;
+    const auto& st = ctx.stats;
+    U_ = o.num_units;
+    F_ = o.sharding_factor;
+    const int W = ctx.world();
+    DLNB_REQUIRE(W % F_ == 0, "world size " << W << " must be divisible by sharding_factor " << F_);
+    R_ = W / F_;
+    P_ = st.model_size;
+    DLNB_REQUIRE(P_ >= static_cast<uint64_t>(U_), "num_units exceeds the parameter count");
+    uint64_t base = P_ / U_, rem = P_ % U_;
+    for (int u = 0; u < U_; ++u) {
+      uint64_t pu = base + (static_cast<uint64_t>(u) < rem ? 1 : 0);
+      shard_.push_back(pu / F_ + (pu % F_ ? 1 : 0));
+    }
+    max_shard_ = shard_[0];
+    fwd_us_ = st.avg_forward_time_us / U_;
+    bwd_us_ = st.avg_backward_time_us / U_;
+    fwd_flops_ = st.forward_flops / U_;
+    bwd_flops_ = st.backward_flops / U_;
+    reference_ = o.schedule == "reference";
+
+    Device& dev = *ctx.dev;
+    es_ = dtype_size(ctx.wire);
+    const int rank = ctx.rank();
+    std::vector<int> unit_members, rep_members;
+    for (int r = 0; r < W; ++r) {
+      if (r / F_ == rank / F_) unit_members.push_back(r);
+      if (r % F_ == rank % F_) rep_members.push_back(r);
+    }
+    const size_t unit_bytes = max_shard_ * F_ * es_;
+    ag_comm_ = ctx.comms->create("fsdp/unit_ag/" + std::to_string(rank / F_), unit_members, unit_bytes, false);
+    rs_comm_ = ctx.comms->create("fsdp/unit_rs/" + std::to_string(rank / F_), unit_members, unit_bytes, false);
+    if (R_ > 1)
+      ar_comm_ = ctx.comms->create("fsdp/replica/" + std::to_string(rank % F_), rep_members, max_shard_ * es_, false);
+
+    compute_ = dev.create_stream(false);
+    ag_stream_ = dev.create_stream(true);
+    rs_stream_ = dev.create_stream(true);
+    if (R_ > 1) ar_stream_ = dev.create_stream(true);
+
+    for (int u = 0; u < U_; ++u) {
+      params_.push_back(dev.alloc(shard_[u] * es_));
+      grads_.push_back(dev.alloc(shard_[u] * es_));
+      dev.fill_random(params_.back().data(), shard_[u], ctx.wire, 2000 + u, *compute_);
+    }
+    for (int b = 0; b < 2; ++b) {
+      gathered_[b] = dev.alloc(unit_bytes);
+      full_grad_[b] = dev.alloc(unit_bytes);
+      dev.fill_random(full_grad_[b].data(), max_shard_ * F_, ctx.wire, 3000 + b, *compute_);
+    }
+    auto mk = [&](std::vector<std::unique_ptr<Event>>& v) {
+      for (int u = 0; u < U_; ++u) v.push_back(dev.create_event());
+    };
+    mk(ag_f_);
+    mk(fwd_done_);
+    mk(ag_b_);
+    mk(bwd_done_);
+    mk(rs_done_);
+    mk(ar_done_);
+    if (o.optimizer) {
+      DLNB_REQUIRE(ctx.wire == DType::BF16, "--optimizer needs --wire-dtype bf16");
+      for (int u = 0; u < U_; ++u) mom_.push_back(dev.alloc(shard_[u] * es_));
+    }
+    compute_->synchronize();
+    timers_.reset(new TimerSet(dev));
+    for (const char* k : {"allgather", "allgather_wait_fwd", "allgather_wait_bwd", "reduce_scatter", "barrier",
+                          "allgather_time", "allreduce_time"})
+      timers_->ensure(k);
+    stats_.push_back({"allgather", CollKind::AllGather, F_, static_cast<double>(unit_bytes), "allgather_time"});
+    stats_.push_back({"reduce_scatter", CollKind::ReduceScatter, F_, static_cast<double>(unit_bytes), "reduce_scatter"});
+    if (R_ > 1)
+      stats_.push_back({"allreduce", CollKind::AllReduce, R_, static_cast<double>(max_shard_ * es_), "allreduce_time"});
+  }
+
+  void enqueue_iteration() override {
+    Context& ctx = *ctx_;
+    ComputeEngine& ce = *ctx.compute;
+    const DType t = ctx.wire;
+
+    auto gather = [&](int u, Event& done, bool first) {
+      int tk = timers_->begin(*ag_stream_);
+      ag_comm_->all_gather(params_[u].data(), gathered_[u & 1].data(), shard_[u], t, *ag_stream_);
+      timers_->end(tk, *ag_stream_, first ? "allgather" : "allgather_time");
+      ag_stream_->record(done);
+    };
+
+    // ---- forward
+    gather(0, *ag_f_[0], true);
+    if (reference_) ag_stream_->synchronize();  // blocking Allgather (fsdp.cpp:86-91)
+    for (int u = 0; u < U_; ++u) {
+      if (u + 1 < U_) {
+        // gathered[(u+1)&1] was last read by forward(u-1).
+        if (u >= 1) ag_stream_->wait(*fwd_done_[u - 1]);
+        gather(u + 1, *ag_f_[u + 1], false);
+      }
+      if (u == 0)
+        compute_->wait(*ag_f_[0]);
+      else
+        timers_->stall(*compute_, *ag_f_[u], "allgather_wait_fwd");
+      ce.run(*compute_, fwd_us_, fwd_flops_);
+      compute_->record(*fwd_done_[u]);
+    }
+
+    // ---- backward (unit U-1's parameters are still gathered)
+    for (int u = U_ - 1; u >= 0; --u) {
+      if (u - 1 >= 0) {
+        // gathered[(u-1)&1] was last read by backward(u+1), or by forward(U-2).
+        ag_stream_->wait(u + 1 <= U_ - 1 ? *bwd_done_[u + 1] : *fwd_done_[u - 1]);
+        gather(u - 1, *ag_b_[u - 1], false);
+      }
+      if (u < U_ - 1) timers_->stall(*compute_, *ag_b_[u], "allgather_wait_bwd");
+      // full_grad[u&1] was last read by the reduce-scatter of unit u+2.
+      if (u + 2 <= U_ - 1) compute_->wait(*rs_done_[u + 2]);
+      ce.run(*compute_, bwd_us_, bwd_flops_);
+      compute_->record(*bwd_done_[u]);
+
+      rs_stream_->wait(*bwd_done_[u]);
+      int tk = timers_->begin(*rs_stream_);
+      rs_comm_->reduce_scatter(full_grad_[u & 1].data(), grads_[u].data(), shard_[u], t, *rs_stream_);
+      timers_->end(tk, *rs_stream_, "reduce_scatter");
+      rs_stream_->record(*rs_done_[u]);
+      if (reference_) compute_->wait(*rs_done_[u]);  // blocking Reduce_Scatter_block (fsdp.cpp:124)
+      if (R_ > 1) {
+        ar_stream_->wait(*rs_done_[u]);
+        int ta = timers_->begin(*ar_stream_);
+        ar_comm_->all_reduce(grads_[u].data(), grads_[u].data(), shard_[u], t, *ar_stream_);
+        timers_->end(ta, *ar_stream_, "allreduce_time");
+        ar_stream_->record(*ar_done_[u]);
+      }
+    }
+    // ---- tail: exposed reduce-scatter / replica all-reduce
+    Stream& last = R_ > 1 ? *ar_stream_ : *rs_stream_;
+    Event& tail = R_ > 1 ? *ar_done_[0] : *rs_done_[0];
+    (void)last;
+    timers_->stall(*compute_, tail, "barrier");
+    if (ctx.opt.optimizer) {
+      if (R_ > 1)
+        for (int u = 1; u < U_; ++u) compute_->wait(*ar_done_[u]);
+      for (int u = 0; u < U_; ++u)
+        optimizer_step(ctx, *compute_, params_[u].data(), mom_[u].data(), grads_[u].data(), shard_[u]);
+    }
+  }
+
+  void synchronize() override {
+    std::vector<Stream*> ss = {compute_.get(), ag_stream_.get(), rs_stream_.get()};
+    std::vector<Communicator*> cs = {ag_comm_.get(), rs_comm_.get()};
+    if (R_ > 1) {
+      ss.push_back(ar_stream_.get());
+      cs.push_back(ar_comm_.get());
+    }
+    sync_streams(ss, cs, *ctx_->dev);
+    timers_->resolve();
+  }
+
+  std::string section_id() const override { return "fsdp"; }
+  std::string section_title() const override { return "FSDP metrics"; }
+  const char* runtime_key() const override { return "runtime"; }
+
+  Json global_json() const override {
+    const Context& ctx = *ctx_;
+    Json g = Json::object();
+    g["model_size_bytes"] = P_ * es_;
+    g["model_name"] = ctx.opt.model;
+    g["world_size"] = ctx.world();
+    g["num_units"] = U_;
+    g["sharding_factor"] = F_;
+    g["num_replicas"] = R_;
+    g["local_batch_size"] = ctx.stats.batch_size;
+    g["device"] = ctx.dev->kind() == DeviceKind::CPU ? "CPU" : "GPU";
+    g["backend"] = ag_comm_->backend_name();
+    g["fwd_time_per_unit_us"] = fwd_us_;
+    g["bwd_time_per_unit_us"] = bwd_us_;
+    g["allgather_msg_size_bytes"] = max_shard_ * F_ * es_;
+    g["reducescatter_msg_size_bytes"] = max_shard_ * es_;
+    if (R_ > 1) g["allreduce_msg_size_bytes"] = max_shard_ * es_;
+    return g;
+  }
+
+  Json rank_json() const override {
+    Json r = Json::object();
+    for (const char* k : {"runtime", "allgather", "allgather_wait_fwd", "allgather_wait_bwd", "reduce_scatter",
+                          "barrier", "allgather_time", "allreduce_time"})
+      r[k] = timers_->values_json(k);
+    r["rank"] = ctx_->rank();
+    return r;
+  }
+
+  Json comm_summary() const override { return comm_stats_json(stats_, *timers_); }
+
+ private:
+  Context* ctx_ = nullptr;
+  int U_ = 1, F_ = 1, R_ = 1;
+  uint64_t P_ = 0, max_shard_ = 0;
+  size_t es_ = 2;
+  bool reference_ = false;
+  std::vector<uint64_t> shard_;
+  double fwd_us_ = 0, bwd_us_ = 0, fwd_flops_ = 0, bwd_flops_ = 0;
+  std::unique_ptr<Communicator> ag_comm_, rs_comm_, ar_comm_;
+  std::unique_ptr<Stream> compute_, ag_stream_, rs_stream_, ar_stream_;
+  std::vector<Buffer> params_, grads_, mom_;
+  Buffer gathered_[2], full_grad_[2];
+  std::vector<std::unique_ptr<Event>> ag_f_, fwd_done_, ag_b_, bwd_done_, rs_done_, ar_done_;
+  std::vector<CommStat> stats_;
+};
+
+}  // namespace
+
+std::unique_ptr<Strategy> make_fsdp() { return std::unique_ptr<Strategy>(new Fsdp()); }
+
+}  // namespace dlnb

@@ -1,0 +1,471 @@
+// Pipeline-parallel hybrids: DP x PP (hybrid_2d), DP x PP x TP (hybrid_3d),
+// DP x PP x EP (hybrid_3d_moe).
+//
+// Reference: cpp/hybrid_parallel/hybrid_2d.cpp:90-169, hybrid_3d.cpp:94-192,
+// hybrid_3d_moe.cpp:104-211. GPipe schedule: every microbatch forward
+// (receive activations from stage-1, compute, send to stage+1), then every
+// microbatch backward (mirrored), then a data-parallel all-reduce of the
+// stage's gradients. hybrid_3d adds 2 tensor-parallel all-reduces after each
+// microbatch forward and backward (hybrid_3d.cpp:144-148,179-183);
+// hybrid_3d_moe adds 2 x layers_per_stage expert all-to-alls per microbatch
+// and direction (hybrid_3d_moe.cpp:161-165,196-200), an all-reduce of the
+// non-expert gradients over the EP group and the DP all-reduce of
+// non-expert + expert-shard gradients (:202-208).
+// Sizes (elements): pipe = s*d*B/mb; TP AR = pipe/T; DP AR = P/S (2d),
+// P/(S*T) (3d), NE/S + (P-NE)/S/EP (moe); A2A per peer = (B/mb)*s*2*d/EP
+// (top-k = 2); compute per microbatch = fwd/S/mb (/T for 3d).
+//
+// MI355X design:
+//   * each pair of adjacent stages gets its own 2-rank communicator and
+//     stream ("link"), so a stage receives microbatch i+1 from its
+//     predecessor while it computes microbatch i and while it sends
+//     microbatch i-1 to its successor; activation buffers are double
+//     buffered and reuse is ordered by events;
+//   * TP all-reduces / EP all-to-alls are on the compute stream (they are on
+//     the critical path of the layer they belong to); with --tp-granularity
+//     layer (and always for MoE) they are interleaved between the layers'
+//     compute slices instead of all issued after the microbatch;
+//   * the DP all-reduce can be split into --dp-buckets buckets that overlap
+//     the last microbatch's backward;
+//   * S = 1 is valid (no P2P), unlike the reference.
+#include "dlnb/strategy.hpp"
+
+namespace dlnb {
+
+GridCoords grid_coords(int rank, int inner, int stages) {
+  return GridCoords{rank % inner, (rank / inner) % stages, rank / (inner * stages)};
+}
+
+std::vector<int> inner_group(int rank, int inner, int stages) {
+  GridCoords c = grid_coords(rank, inner, stages);
+  std::vector<int> v;
+  for (int i = 0; i < inner; ++i) v.push_back(c.dp_id * inner * stages + c.stage_id * inner + i);
+  return v;
+}
+
+std::vector<int> pp_group(int rank, int inner, int stages) {
+  GridCoords c = grid_coords(rank, inner, stages);
+  std::vector<int> v;
+  for (int s = 0; s < stages; ++s) v.push_back(c.dp_id * inner * stages + s * inner + c.inner_id);
+  return v;
+}
+
+std::vector<int> dp_group(int rank, int inner, int stages, int world) {
+  GridCoords c = grid_coords(rank, inner, stages);
+  std::vector<int> v;
+  for (int d = 0; d < world / (inner * stages); ++d) v.push_back(d * inner * stages + c.stage_id * inner + c.inner_id);
+  return v;
+}
+
+namespace {
+
+class Pipeline : public Strategy {
+ public:
+  explicit Pipeline(StrategyKind k) : kind_(k) {}
+
+  void setup(Context& ctx) override {
+    ctx_ = &ctx;
+    const auto& o = ctx.opt;
+    const auto& st = ctx.stats;
+    const int W = ctx.world();
+    S_ = o.num_stages;
+    mb_ = o.num_microbatches;
+    inner_ = kind_ == StrategyKind::Hybrid3D ? o.num_tensor_shards
+             : kind_ == StrategyKind::Hybrid3DMoE ? o.num_expert_shards
+                                                  : 1;
+    reference_ = o.schedule == "reference";
+    DLNB_REQUIRE(ctx.have_arch, "hybrid strategies need models/<model>.json (layer count)");
+    L_ = static_cast<int>(ctx.arch.num_layers);
+    DLNB_REQUIRE(L_ > 0, "model has no layers: " << ctx.arch.path);
+    DLNB_REQUIRE(L_ % S_ == 0, "num_layers " << L_ << " must be divisible by num_stages " << S_);
+    DLNB_REQUIRE(st.batch_size % mb_ == 0, "batch size " << st.batch_size << " must be divisible by num_microbatches " << mb_);
+    DLNB_REQUIRE(W % (S_ * inner_) == 0, "world size " << W << " must be divisible by stages*" << (kind_ == StrategyKind::Hybrid3DMoE ? "expert" : "tensor") << " shards = " << S_ * inner_);
+    if (kind_ == StrategyKind::Hybrid3DMoE)
+      DLNB_REQUIRE(st.experts % inner_ == 0, "experts " << st.experts << " must be divisible by num_expert_shards " << inner_);
+    dp_size_ = W / (S_ * inner_);
+    layers_per_stage_ = L_ / S_;
+
+    GridCoords c = grid_coords(ctx.rank(), inner_, S_);
+    stage_ = c.stage_id;
+    inner_id_ = c.inner_id;
+    dp_id_ = c.dp_id;
+
+    spmb_ = st.batch_size / mb_;
+    pipe_ = st.seq_len * st.embedded_dim * spmb_;
+    double tshard = kind_ == StrategyKind::Hybrid3D ? inner_ : 1;
+    fwd_mb_us_ = st.avg_forward_time_us / S_ / (mb_ * tshard);
+    bwd_mb_us_ = st.avg_backward_time_us / S_ / (mb_ * tshard);
+    fwd_mb_flops_ = st.forward_flops / S_ / (mb_ * tshard);
+    bwd_mb_flops_ = st.backward_flops / S_ / (mb_ * tshard);
+    const uint64_t P = st.model_size;
+    if (kind_ == StrategyKind::Hybrid2D) {
+      dp_ar_ = P / S_;
+    } else if (kind_ == StrategyKind::Hybrid3D) {
+      dp_ar_ = P / (S_ * inner_);
+      tp_ar_ = pipe_ / inner_;
+    } else {
+      const uint64_t NE = st.non_expert_size;
+      ne_ = NE / S_;
+      uint64_t expert = ((P - NE) / S_) / inner_;
+      dp_ar_ = ne_ + expert;
+      const int top_k = 2;  // hybrid_3d_moe.cpp:357
+      a2a_ = (spmb_ * st.seq_len * top_k * st.embedded_dim) / inner_;
+    }
+
+    Device& dev = *ctx.dev;
+    es_ = dtype_size(ctx.wire);
+    const int rank = ctx.rank();
+    compute_ = dev.create_stream(false);
+    std::vector<int> pp = pp_group(rank, inner_, S_);
+    // Link communicators between adjacent stages of this pipeline. Created
+    // in stage order by every member so creation never deadlocks.
+    for (int s = 0; s + 1 < S_; ++s) {
+      if (stage_ == s || stage_ == s + 1) {
+        std::string nm = "pp/link/" + std::to_string(dp_id_) + "/" + std::to_string(inner_id_) + "/" + std::to_string(s);
+        auto comm = ctx.comms->create(nm, {pp[s], pp[s + 1]}, pipe_ * es_, true);
+        if (stage_ == s) {
+          next_ = std::move(comm);
+          next_peer_ = 1;
+        } else {
+          prev_ = std::move(comm);
+          prev_peer_ = 0;
+        }
+      }
+    }
+    if (prev_) prev_stream_ = dev.create_stream(true);
+    if (next_) next_stream_ = dev.create_stream(true);
+    if (inner_ > 1) {
+      std::string nm = std::string(kind_ == StrategyKind::Hybrid3D ? "tp/" : "ep/") + std::to_string(dp_id_) + "/" +
+                       std::to_string(stage_);
+      size_t cap = kind_ == StrategyKind::Hybrid3D ? tp_ar_ * es_ : std::max<uint64_t>(a2a_ * inner_, ne_) * es_;
+      inner_comm_ = ctx.comms->create(nm, inner_group(rank, inner_, S_), cap, false);
+    } else if (kind_ == StrategyKind::Hybrid3DMoE) {
+      inner_comm_ = ctx.comms->create("ep/" + std::to_string(dp_id_) + "/" + std::to_string(stage_),
+                                      inner_group(rank, inner_, S_), std::max<uint64_t>(a2a_, ne_) * es_, false);
+    }
+    if (kind_ == StrategyKind::Hybrid3D && inner_ == 1) {
+      inner_comm_ = ctx.comms->create("tp/" + std::to_string(dp_id_) + "/" + std::to_string(stage_),
+                                      inner_group(rank, inner_, S_), tp_ar_ * es_, false);
+    }
+    {
+      std::string nm = "dp/" + std::to_string(stage_) + "/" + std::to_string(inner_id_);
+      const int nbk = o.dp_buckets;
+      dp_comm_ = ctx.comms->create(nm, dp_group(rank, inner_, S_, W), (dp_ar_ / nbk + 1) * es_, false);
+      dp_stream_ = dev.create_stream(true);
+    }
+
+    // Buffers.
+    for (int b = 0; b < 2; ++b) {
+      if (prev_) {
+        act_in_[b] = dev.alloc(pipe_ * es_);
+        grad_out_[b] = dev.alloc(pipe_ * es_);
+        dev.fill_random(grad_out_[b].data(), pipe_, ctx.wire, 4000 + b, *compute_);
+      }
+      if (next_) {
+        act_out_[b] = dev.alloc(pipe_ * es_);
+        grad_in_[b] = dev.alloc(pipe_ * es_);
+        dev.fill_random(act_out_[b].data(), pipe_, ctx.wire, 4100 + b, *compute_);
+      }
+    }
+    grad_ = dev.alloc(dp_ar_ * es_);
+    dev.fill_random(grad_.data(), dp_ar_, ctx.wire, 4200, *compute_);
+    if (!o.in_place) sum_grad_ = dev.alloc(dp_ar_ * es_);
+    if (kind_ == StrategyKind::Hybrid3D) {
+      tp_buf_ = dev.alloc(tp_ar_ * es_);
+      tp_res_ = dev.alloc(tp_ar_ * es_);
+      dev.fill_random(tp_buf_.data(), tp_ar_, ctx.wire, 4300, *compute_);
+    }
+    if (kind_ == StrategyKind::Hybrid3DMoE) {
+      ep_send_ = dev.alloc(a2a_ * inner_ * es_);
+      ep_recv_ = dev.alloc(a2a_ * inner_ * es_);
+      dev.fill_random(ep_send_.data(), a2a_ * inner_, ctx.wire, 4400, *compute_);
+    }
+    if (o.optimizer) {
+      DLNB_REQUIRE(ctx.wire == DType::BF16, "--optimizer needs --wire-dtype bf16");
+      params_ = dev.alloc(dp_ar_ * es_);
+      mom_ = dev.alloc(dp_ar_ * es_);
+    }
+    auto mk = [&](std::vector<std::unique_ptr<Event>>& v) {
+      for (int i = 0; i < mb_; ++i) v.push_back(dev.create_event());
+    };
+    mk(recv_f_);
+    mk(fwd_done_);
+    mk(send_f_);
+    mk(recv_b_);
+    mk(bwd_done_);
+    mk(send_b_);
+    for (int k = 0; k < o.dp_buckets; ++k) {
+      bucket_ready_.push_back(dev.create_event());
+    }
+    dp_done_ = dev.create_event();
+    compute_->synchronize();
+
+    timers_.reset(new TimerSet(dev));
+    for (const char* k : {"pp_comm_time", "dp_comm_time", "pp_send_time", "pp_recv_time", "dp_exposed_time"})
+      timers_->ensure(k);
+    if (kind_ == StrategyKind::Hybrid3D) timers_->ensure("tp_comm_time");
+    if (kind_ == StrategyKind::Hybrid3DMoE) {
+      timers_->ensure("ep_comm_time");
+      timers_->ensure("dp_ep_comm_time");
+    }
+    if (prev_ || next_) stats_.push_back({"sendrecv", CollKind::SendRecv, 2, static_cast<double>(pipe_ * es_), "pp_send_time"});
+    stats_.push_back({"dp_allreduce", CollKind::AllReduce, dp_size_, static_cast<double>(dp_ar_ / o.dp_buckets * es_), "dp_comm_time"});
+    if (kind_ == StrategyKind::Hybrid3D)
+      stats_.push_back({"tp_allreduce", CollKind::AllReduce, inner_, static_cast<double>(tp_ar_ * es_), "tp_comm_time"});
+    if (kind_ == StrategyKind::Hybrid3DMoE)
+      stats_.push_back({"ep_alltoall", CollKind::AllToAll, inner_, static_cast<double>(a2a_ * inner_ * es_), "ep_comm_time"});
+  }
+
+  // Compute of one microbatch with the inner-group collectives interleaved.
+  void micro_compute(double us, double flops) {
+    Context& ctx = *ctx_;
+    ComputeEngine& ce = *ctx.compute;
+    if (kind_ == StrategyKind::Hybrid3D) {
+      const bool layer = ctx.opt.tp_granularity == "layer";
+      const int n_ar = layer ? 4 * layers_per_stage_ / 2 : 2;  // layer: 2 per layer
+      if (layer) {
+        const int slices = n_ar;
+        for (int i = 0; i < slices; ++i) {
+          ce.run(*compute_, us / slices, flops / slices);
+          tp_allreduce();
+        }
+      } else {
+        ce.run(*compute_, us, flops);
+        tp_allreduce();
+        tp_allreduce();
+      }
+    } else if (kind_ == StrategyKind::Hybrid3DMoE) {
+      const int n = 2 * layers_per_stage_;
+      if (reference_) {
+        ce.run(*compute_, us, flops);
+        for (int i = 0; i < n; ++i) ep_alltoall();
+      } else {
+        for (int i = 0; i < n; ++i) {
+          ce.run(*compute_, us / n, flops / n);
+          ep_alltoall();
+        }
+      }
+    } else {
+      ce.run(*compute_, us, flops);
+    }
+  }
+
+  void tp_allreduce() {
+    int t = timers_->begin(*compute_);
+    inner_comm_->all_reduce(tp_buf_.data(), tp_res_.data(), tp_ar_, ctx_->wire, *compute_);
+    timers_->end(t, *compute_, "tp_comm_time");
+  }
+
+  void ep_alltoall() {
+    int t = timers_->begin(*compute_);
+    inner_comm_->all_to_all(ep_send_.data(), ep_recv_.data(), a2a_, ctx_->wire, *compute_);
+    timers_->end(t, *compute_, "ep_comm_time");
+  }
+
+  void enqueue_iteration() override {
+    Context& ctx = *ctx_;
+    const DType t = ctx.wire;
+    const int nbk = ctx.opt.dp_buckets;
+
+    // ---------------- forward
+    for (int i = 0; i < mb_; ++i) {
+      const int b = i & 1;
+      if (prev_) {
+        if (i >= 2) prev_stream_->wait(*fwd_done_[i - 2]);  // act_in[b] consumed
+        int tk = timers_->begin(*prev_stream_);
+        prev_->recv(act_in_[b].data(), pipe_, t, prev_peer_, *prev_stream_);
+        timers_->end(tk, *prev_stream_, "pp_recv_time");
+        prev_stream_->record(*recv_f_[i]);
+        timers_->stall(*compute_, *recv_f_[i], "pp_comm_time");
+      } else {
+        timers_->add("pp_comm_time", 0.0);
+      }
+      if (next_ && i >= 2) compute_->wait(*send_f_[i - 2]);  // act_out[b] sent
+      micro_compute(fwd_mb_us_, fwd_mb_flops_);
+      compute_->record(*fwd_done_[i]);
+      if (next_) {
+        next_stream_->wait(*fwd_done_[i]);
+        int tk = timers_->begin(*next_stream_);
+        next_->send(act_out_[b].data(), pipe_, t, next_peer_, *next_stream_);
+        timers_->end(tk, *next_stream_, "pp_send_time");
+        next_stream_->record(*send_f_[i]);
+        if (reference_) compute_->wait(*send_f_[i]);  // blocking send
+      }
+    }
+    // ---------------- backward
+    for (int i = 0; i < mb_; ++i) {
+      const int b = i & 1;
+      if (next_) {
+        if (i >= 2) next_stream_->wait(*bwd_done_[i - 2]);  // grad_in[b] consumed
+        int tk = timers_->begin(*next_stream_);
+        next_->recv(grad_in_[b].data(), pipe_, t, next_peer_, *next_stream_);
+        timers_->end(tk, *next_stream_, "pp_recv_time");
+        next_stream_->record(*recv_b_[i]);
+        timers_->stall(*compute_, *recv_b_[i], "pp_comm_time");
+      } else {
+        timers_->add("pp_comm_time", 0.0);
+      }
+      if (prev_ && i >= 2) compute_->wait(*send_b_[i - 2]);
+      const bool last = i == mb_ - 1;
+      if (last && nbk > 1 && !reference_) {
+        // Overlap the DP all-reduce with the last microbatch's backward.
+        for (int k = 0; k < nbk; ++k) {
+          ctx.compute->run(*compute_, bwd_mb_us_ / nbk, bwd_mb_flops_ / nbk);
+          compute_->record(*bucket_ready_[k]);
+          dp_stream_->wait(*bucket_ready_[k]);
+          dp_allreduce_bucket(k, nbk);
+        }
+        compute_->record(*bwd_done_[i]);
+      } else {
+        micro_compute(bwd_mb_us_, bwd_mb_flops_);
+        compute_->record(*bwd_done_[i]);
+      }
+      if (prev_) {
+        prev_stream_->wait(*bwd_done_[i]);
+        int tk = timers_->begin(*prev_stream_);
+        prev_->send(grad_out_[b].data(), pipe_, t, prev_peer_, *prev_stream_);
+        timers_->end(tk, *prev_stream_, "pp_send_time");
+        prev_stream_->record(*send_b_[i]);
+        if (reference_) compute_->wait(*send_b_[i]);
+      }
+    }
+    // ---------------- gradient synchronisation
+    if (kind_ == StrategyKind::Hybrid3DMoE) {
+      // Non-expert gradients are replicated across the EP group.
+      int tk = timers_->begin(*compute_);
+      void* out = ctx.opt.in_place ? grad_.data() : sum_grad_.data();
+      inner_comm_->all_reduce(grad_.data(), out, ne_, t, *compute_);
+      timers_->end(tk, *compute_, "dp_ep_comm_time");
+    }
+    if (nbk == 1 || reference_) {
+      compute_->record(*bucket_ready_[0]);
+      dp_stream_->wait(*bucket_ready_[0]);
+      dp_allreduce_bucket(0, 1);
+    }
+    dp_stream_->record(*dp_done_);
+    timers_->stall(*compute_, *dp_done_, "dp_exposed_time");
+    if (ctx.opt.optimizer) {
+      void* g = ctx.opt.in_place ? grad_.data() : sum_grad_.data();
+      optimizer_step(ctx, *compute_, params_.data(), mom_.data(), g, dp_ar_);
+    }
+  }
+
+  void dp_allreduce_bucket(int k, int nbk) {
+    const uint64_t base = dp_ar_ / nbk, rem = dp_ar_ % nbk;
+    const uint64_t off = k * base + std::min<uint64_t>(k, rem);
+    const uint64_t n = base + (static_cast<uint64_t>(k) < rem ? 1 : 0);
+    void* in = grad_.at(off * es_);
+    void* out = ctx_->opt.in_place ? in : sum_grad_.at(off * es_);
+    int tk = timers_->begin(*dp_stream_);
+    dp_comm_->all_reduce(in, out, n, ctx_->wire, *dp_stream_);
+    timers_->end(tk, *dp_stream_, "dp_comm_time");
+  }
+
+  void synchronize() override {
+    std::vector<Stream*> ss = {compute_.get(), dp_stream_.get()};
+    std::vector<Communicator*> cs = {dp_comm_.get()};
+    if (prev_) {
+      ss.push_back(prev_stream_.get());
+      cs.push_back(prev_.get());
+    }
+    if (next_) {
+      ss.push_back(next_stream_.get());
+      cs.push_back(next_.get());
+    }
+    if (inner_comm_) cs.push_back(inner_comm_.get());
+    sync_streams(ss, cs, *ctx_->dev);
+    timers_->resolve();
+  }
+
+  std::string section_id() const override {
+    return kind_ == StrategyKind::Hybrid2D ? "dp_pp" : kind_ == StrategyKind::Hybrid3D ? "dp_pp_tp" : "dp_pp_ep";
+  }
+  std::string section_title() const override {
+    return kind_ == StrategyKind::Hybrid2D   ? "Data + Pipeline Parallelism"
+           : kind_ == StrategyKind::Hybrid3D ? "Data + Pipeline + Tensor Parallelism"
+                                             : "Data + Pipeline + Expert Parallelism";
+  }
+
+  Json global_json() const override {
+    const Context& ctx = *ctx_;
+    Json g = Json::object();
+    g["model_name"] = ctx.opt.model;
+    g["num_stages"] = S_;
+    g["num_microbatches"] = mb_;
+    if (kind_ == StrategyKind::Hybrid3D) g["num_tensor_shards"] = inner_;
+    if (kind_ == StrategyKind::Hybrid3DMoE) {
+      g["num_expert_shards"] = inner_;
+      g["num_experts"] = ctx.stats.experts;
+      g["sequence_length"] = ctx.stats.seq_len;
+      g["embedded_dim"] = ctx.stats.embedded_dim;
+    }
+    g["samples_per_microbatch"] = spmb_;
+    g["local_batch_size"] = ctx.stats.batch_size;
+    // hybrid_2d.cpp:453 reports world*B/S; hybrid_3d.cpp:530 dp_size*B.
+    g["global_batch_size"] = kind_ == StrategyKind::Hybrid2D
+                                 ? static_cast<uint64_t>(ctx.world()) * ctx.stats.batch_size / S_
+                                 : static_cast<uint64_t>(dp_size_) * ctx.stats.batch_size;
+    g["world_size"] = ctx.world();
+    g["dp_size"] = dp_size_;
+    g["num_layers"] = L_;
+    g["fwd_rt_per_microbatch"] = fwd_mb_us_;
+    g["bwd_rt_per_microbatch"] = bwd_mb_us_;
+    g["total_model_size_params"] = ctx.stats.model_size;
+    g["pipe_msg_size_bytes"] = pipe_ * es_;
+    if (kind_ == StrategyKind::Hybrid3D) g["tp_allreduce_size_bytes"] = tp_ar_ * es_;
+    if (kind_ == StrategyKind::Hybrid3DMoE) {
+      g["ep_alltoall_size_bytes"] = a2a_ * es_;
+      g["ep_allreduce_size_bytes"] = ne_ * es_;
+    }
+    g["dp_allreduce_size_bytes"] = dp_ar_ * es_;
+    g["device"] = ctx.dev->kind() == DeviceKind::CPU ? "CPU" : "GPU";
+    g["backend"] = dp_comm_->backend_name();
+    return g;
+  }
+
+  Json rank_json() const override {
+    Json r = Json::object();
+    r["runtimes"] = timers_->values_json("runtimes");
+    r["pp_comm_time"] = timers_->values_json("pp_comm_time");
+    r["dp_comm_time"] = timers_->values_json("dp_comm_time");
+    if (kind_ == StrategyKind::Hybrid3D) r["tp_comm_time"] = timers_->values_json("tp_comm_time");
+    if (kind_ == StrategyKind::Hybrid3DMoE) {
+      r["ep_comm_time"] = timers_->values_json("ep_comm_time");
+      r["dp_ep_comm_time"] = timers_->values_json("dp_ep_comm_time");
+    }
+    r["pp_send_time"] = timers_->values_json("pp_send_time");
+    r["pp_recv_time"] = timers_->values_json("pp_recv_time");
+    r["dp_exposed_time"] = timers_->values_json("dp_exposed_time");
+    r["stage_id"] = stage_;
+    if (kind_ == StrategyKind::Hybrid3D) r["tp_id"] = inner_id_;
+    if (kind_ == StrategyKind::Hybrid3DMoE) r["ep_id"] = inner_id_;
+    if (kind_ != StrategyKind::Hybrid2D) r["dp_id"] = dp_id_;
+    return r;
+  }
+
+  Json comm_summary() const override { return comm_stats_json(stats_, *timers_); }
+
+ private:
+  StrategyKind kind_;
+  Context* ctx_ = nullptr;
+  int S_ = 1, mb_ = 1, inner_ = 1, L_ = 0, layers_per_stage_ = 0, dp_size_ = 1;
+  int stage_ = 0, inner_id_ = 0, dp_id_ = 0;
+  bool reference_ = false;
+  uint64_t spmb_ = 0, pipe_ = 0, dp_ar_ = 0, tp_ar_ = 0, ne_ = 0, a2a_ = 0;
+  size_t es_ = 2;
+  double fwd_mb_us_ = 0, bwd_mb_us_ = 0, fwd_mb_flops_ = 0, bwd_mb_flops_ = 0;
+  std::unique_ptr<Communicator> prev_, next_, inner_comm_, dp_comm_;
+  int prev_peer_ = 0, next_peer_ = 1;
+  std::unique_ptr<Stream> compute_, prev_stream_, next_stream_, dp_stream_;
+  Buffer act_in_[2], act_out_[2], grad_in_[2], grad_out_[2];
+  Buffer grad_, sum_grad_, tp_buf_, tp_res_, ep_send_, ep_recv_, params_, mom_;
+  std::vector<std::unique_ptr<Event>> recv_f_, fwd_done_, send_f_, recv_b_, bwd_done_, send_b_, bucket_ready_;
+  std::unique_ptr<Event> dp_done_;
+  std::vector<CommStat> stats_;
+};
+
+}  // namespace
+
+std::unique_ptr<Strategy> make_pipeline(StrategyKind kind) { return std::unique_ptr<Strategy>(new Pipeline(kind)); }
+
+}  // namespace dlnb
