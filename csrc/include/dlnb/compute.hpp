@@ -8,12 +8,16 @@
 //           (one-wave s_memrealtime wait on GPU; nanosleep task on CPU);
 //           reference parity.
 //   spin  - every CU runs dependent VALU work until the deadline.
-//   gemm  - hand-written MFMA GEMMs shaped from the model (M = token chunk,
-//           N = FFN dim, K = hidden dim) calibrated at start-up so the
-//           uncontended duration equals the table's time; the tail below
-//           the smallest GEMM is filled by a deadline spin. Under
-//           contention with RCCL kernels it takes longer, like real
-//           training compute does.
+//   gemm  - (default on GPU) hand-written MFMA GEMM shaped from the model
+//           (M = 8192-token chunk, N = FFN dim, K = hidden dim) run as a
+//           persistent kernel on every CU that stops at a device-clock
+//           deadline: exactly the table's duration, with the matrix cores
+//           and HBM as busy as in training (the reference's usleep leaves
+//           the GPU idle, so its collectives never contend with compute).
+//   gemm-work - the same GEMM launched a fixed number of times, calibrated
+//           at start-up (after a DVFS settle) so the uncontended duration
+//           matches the table; contention / clock drops stretch it, like
+//           real training compute.
 //   flops - executes the table's FLOP count on the MI355X GEMM at whatever
 //           speed the hardware gives (MI355X-native compute time).
 #pragma once
@@ -27,7 +31,7 @@
 
 namespace dlnb {
 
-enum class ComputeMode { Sleep, Spin, Gemm, Flops };
+enum class ComputeMode { Sleep, Spin, Gemm, GemmWork, Flops };
 
 ComputeMode parse_compute_mode(const std::string& s, DeviceKind dev);
 const char* compute_mode_name(ComputeMode m);

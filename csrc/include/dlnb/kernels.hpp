@@ -41,6 +41,14 @@ bool gemm_shape_ok(int M, int N, int K, DType in_t);
 void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
              void* stream);
 
+// Persistent deadline variant (the default stand-in compute): a grid of
+// `grid` blocks (<= one per CU: 128 KiB LDS each) walks the M x N tile space
+// of C = A.B^T round-robin until *stamp_slot + ticks, where *stamp_slot is
+// written by a one-wave stamp kernel enqueued just before on the same stream.
+// Leading dimensions are K, K and N.
+void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
+                      uint64_t* stamp_slot, int grid, void* stream);
+
 // Elementwise "optimizer" stand-in (SGD-momentum on bf16 shards, fp32 math):
 // p = p - lr * (m = beta*m + g). Used by the optional --optimizer step.
 void sgd_momentum_bf16(void* param, void* mom, const void* grad, size_t n, float lr, float beta, void* stream);

@@ -59,6 +59,7 @@ struct Options {
   std::string stats_file;  // explicit stats path (overrides base_path lookup)
   bool topology = true;
   bool quiet = false;
+  bool silent = false;  // print nothing (library use, e.g. bench.py)
 };
 
 // Parses argv for the given strategy (argv[0] is the program name). Throws

@@ -159,15 +159,26 @@ __device__ __forceinline__ int xcd_remap(int b, int T) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-template <bool FP8>
+// DEADLINE = false: one launch computes every tile once (grid = tiles).
+// DEADLINE = true : persistent stand-in compute. grid <= resident blocks;
+//   each block walks the tile space round-robin (wrapping) and the whole
+//   grid stops at *t0 + ticks of the 100 MHz s_memrealtime clock, where *t0
+//   was stamped by stamp_kernel right before this launch on the same stream.
+//   The stop decision is made block-uniform with __syncthreads_or once per
+//   K-tile, so every wave leaves the K-loop at the same barrier.
+template <bool FP8, bool DEADLINE>
 __global__ void __launch_bounds__(512, 2)
     gemm_tn_256_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
-                       int K, int lda, int ldb, int ldc) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * kStageBytes];
+                       int K, int lda, int ldb, int ldc, const uint64_t* __restrict__ t0, uint64_t ticks) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kStageBytes + 16];
+  volatile int* stop_flag = reinterpret_cast<volatile int*>(smem + 2 * kStageBytes);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 2, wn = w & 3;
   const int nt_m = M / kTile, nt_n = N / kTile, T = nt_m * nt_n;
-  const int b = xcd_remap(blockIdx.x, T);
+  uint64_t deadline = 0;
+  if constexpr (DEADLINE) deadline = *t0 + ticks;
+  for (int round = 0;; ++round) {
+  const int b = xcd_remap(DEADLINE ? (blockIdx.x + round * gridDim.x) % T : blockIdx.x, T);
   // Grouped tile order: GROUP row-tiles share their B panels in L2.
   constexpr int GROUP = 8;
   const int per_group = GROUP * nt_n;
@@ -192,9 +203,10 @@ __global__ void __launch_bounds__(512, 2)
   stage_tile(Bb, ldb_b, smem + kTileBytes, w, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  int expired = 0;
 
   const int r16 = lane & 15, h = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
+  for (int kt = 0; kt < nk && !expired; ++kt) {
     const char* cur = smem + (kt & 1) * kStageBytes;
     if (kt + 1 < nk) {
       char* nxt = smem + ((kt + 1) & 1) * kStageBytes;
@@ -242,8 +254,17 @@ __global__ void __launch_bounds__(512, 2)
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if constexpr (DEADLINE) {
+      // Double-buffered flag: written before barrier kt, read after it; the
+      // other slot is rewritten only after every wave passed barrier kt+1.
+      if (tid == 0) stop_flag[kt & 1] = __builtin_amdgcn_s_memrealtime() >= deadline;
+      __syncthreads();
+      expired = __builtin_amdgcn_readfirstlane(stop_flag[kt & 1]);
+    } else {
+      __syncthreads();
+    }
   }
+  if (expired) return;  // partial tile: the stand-in result is not needed
 
   // Epilogue: lane holds C[m = .. + (lane & 15)][n = .. + 4*(lane >> 4) + 0..3].
   const int m_base = tm * kTile + wm * 128 + r16;
@@ -260,6 +281,12 @@ __global__ void __launch_bounds__(512, 2)
       *reinterpret_cast<bf16x4*>(C + static_cast<size_t>(m_base + i * 16) * ldc + n_base + j * 16) = o;
     }
   }
+  if constexpr (!DEADLINE) return;
+  }  // round
+}
+
+__global__ void stamp_kernel(uint64_t* slot) {
+  if (threadIdx.x == 0) *slot = __builtin_amdgcn_s_memrealtime();
 }
 
 // ------------------------------------------------------------- optimizer
@@ -355,11 +382,30 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
                "gemm_tn: misaligned base pointers");
   const int tiles = (M / kTile) * (N / kTile);
   if (in_t == DType::BF16) {
-    hipLaunchKernelGGL(gemm_tn_256_kernel<false>, tiles, 512, 0, S(stream), static_cast<const char*>(A),
-                       static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc);
+    hipLaunchKernelGGL((gemm_tn_256_kernel<false, false>), tiles, 512, 0, S(stream), static_cast<const char*>(A),
+                       static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc,
+                       static_cast<const uint64_t*>(nullptr), 0ull);
   } else {
-    hipLaunchKernelGGL(gemm_tn_256_kernel<true>, tiles, 512, 0, S(stream), static_cast<const char*>(A),
-                       static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc);
+    hipLaunchKernelGGL((gemm_tn_256_kernel<true, false>), tiles, 512, 0, S(stream), static_cast<const char*>(A),
+                       static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc,
+                       static_cast<const uint64_t*>(nullptr), 0ull);
+  }
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
+void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
+                      uint64_t* stamp_slot, int grid, void* stream) {
+  DLNB_REQUIRE(gemm_shape_ok(M, N, K, in_t), "gemm_tn_deadline: unsupported shape");
+  DLNB_REQUIRE(stamp_slot != nullptr && grid > 0, "gemm_tn_deadline: need a stamp slot and a grid");
+  hipLaunchKernelGGL(stamp_kernel, 1, 64, 0, S(stream), stamp_slot);
+  if (in_t == DType::BF16) {
+    hipLaunchKernelGGL((gemm_tn_256_kernel<false, true>), grid, 512, 0, S(stream), static_cast<const char*>(A),
+                       static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, K, K, N,
+                       static_cast<const uint64_t*>(stamp_slot), ticks);
+  } else {
+    hipLaunchKernelGGL((gemm_tn_256_kernel<true, true>), grid, 512, 0, S(stream), static_cast<const char*>(A),
+                       static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, K, K, N,
+                       static_cast<const uint64_t*>(stamp_slot), ticks);
   }
   DLNB_HIP_CHECK(hipGetLastError());
 }

@@ -74,6 +74,17 @@ int dlnb_gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int
   });
 }
 
+int dlnb_gemm_deadline_us(const void* A, const void* B, void* C, int M, int N, int K, int dtype, double us,
+                          int device, void* stamp_slot, int grid, void* stream) {
+  return guard([&] {
+    double hz = dlnb::kernels::wallclock_hz(device);
+    if (grid <= 0) grid = dlnb::kernels::num_cus(device);
+    dlnb::kernels::gemm_tn_deadline(A, B, C, M, N, K, static_cast<dlnb::DType>(dtype),
+                                    static_cast<unsigned long long>(us * 1e-6 * hz), static_cast<uint64_t*>(stamp_slot),
+                                    grid, stream);
+  });
+}
+
 int dlnb_gemm_shape_ok(int M, int N, int K, int dtype) {
   return dlnb::kernels::gemm_shape_ok(M, N, K, static_cast<dlnb::DType>(dtype)) ? 1 : 0;
 }

@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <map>
 
 #include "dlnb/kernels.hpp"
 
@@ -12,6 +13,7 @@ ComputeMode parse_compute_mode(const std::string& s, DeviceKind dev) {
   if (s == "sleep") return ComputeMode::Sleep;
   if (s == "spin") return ComputeMode::Spin;
   if (s == "gemm") return ComputeMode::Gemm;
+  if (s == "gemm-work" || s == "gemm_work") return ComputeMode::GemmWork;
   if (s == "flops") return ComputeMode::Flops;
   DLNB_THROW("unknown compute mode '" << s << "' (auto, sleep, spin, gemm, flops)");
 }
@@ -21,6 +23,7 @@ const char* compute_mode_name(ComputeMode m) {
     case ComputeMode::Sleep: return "sleep";
     case ComputeMode::Spin: return "spin";
     case ComputeMode::Gemm: return "gemm";
+    case ComputeMode::GemmWork: return "gemm-work";
     case ComputeMode::Flops: return "flops";
   }
   return "?";
@@ -80,7 +83,11 @@ class GpuCompute : public ComputeEngine {
     const int kmul = dtype_ == DType::FP8_E4M3 ? 128 : 64;
     K_ = std::max(512, (shape.hidden + kmul - 1) / kmul * kmul);
     N_ = std::min(32768, std::max(1024, (shape.ffn + 255) / 256 * 256));
-    if (mode_ == ComputeMode::Gemm || mode_ == ComputeMode::Flops) calibrate();
+    if (mode_ != ComputeMode::Sleep && mode_ != ComputeMode::Spin) calibrate();
+    if (mode_ == ComputeMode::Gemm) {
+      slots_ = dev_.alloc(kSlots * 64);
+      grid_ = cus_;
+    }
   }
 
   void run(Stream& s, double us, double flops) override {
@@ -93,6 +100,19 @@ class GpuCompute : public ComputeEngine {
       if (d > 0) kernels::busy_spin(ticks(d), cus_, s.native());
       return;
     }
+    if (mode_ == ComputeMode::Gemm) {
+      // Fixed duration, real MFMA work: persistent deadline GEMM (the stand-in
+      // keeps the matrix cores and HBM busy for exactly the table's time, so
+      // DVFS or contention changes how much work is done, not how long).
+      if (d <= 0) return;
+      if (d < 20.0) {
+        kernels::busy_spin(ticks(d), cus_, s.native());
+        return;
+      }
+      kernels::gemm_tn_deadline(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, ticks(d), slot_for(s), grid_,
+                                s.native());
+      return;
+    }
     if (mode_ == ComputeMode::Flops) {
       double f = flops * scale_;
       for (const auto& lv : levels_) {
@@ -102,7 +122,7 @@ class GpuCompute : public ComputeEngine {
       }
       return;
     }
-    // gemm: greedy fill of the duration with calibrated launches, then spin.
+    // gemm-work: greedy fill of the duration with calibrated launches, then spin.
     double rem = d;
     for (const auto& lv : levels_) {
       long n = static_cast<long>(std::floor(rem / lv.us));
@@ -118,6 +138,7 @@ class GpuCompute : public ComputeEngine {
     j["time_scale"] = scale_;
     j["wallclock_hz"] = hz_;
     j["num_cus"] = cus_;
+    if (mode_ == ComputeMode::Gemm) j["deadline_grid"] = grid_;
     if (!levels_.empty()) {
       j["gemm_dtype"] = dtype_name(dtype_);
       j["gemm_N"] = N_;
@@ -143,8 +164,21 @@ class GpuCompute : public ComputeEngine {
     kernels::gemm_tn(A_.data(), B_.data(), C_.data(), M, N_, K_, K_, K_, N_, dtype_, s.native());
   }
 
+  uint64_t* slot_for(Stream& s) {
+    auto it = slot_of_.find(&s);
+    size_t idx;
+    if (it == slot_of_.end()) {
+      idx = slot_of_.size();
+      DLNB_REQUIRE(idx < kSlots, "too many compute streams");
+      slot_of_[&s] = idx;
+    } else {
+      idx = it->second;
+    }
+    return slots_.as<uint64_t>() + idx * 8;  // one 64-B line per stream
+  }
+
   void calibrate() {
-    const int Mmax = 8192;
+    const int Mmax = kMmax;
     const size_t esz = dtype_size(dtype_);
     A_ = dev_.alloc(static_cast<size_t>(Mmax) * K_ * esz);
     B_ = dev_.alloc(static_cast<size_t>(N_) * K_ * esz);
@@ -154,8 +188,9 @@ class GpuCompute : public ComputeEngine {
     dev_.fill_random(B_.data(), static_cast<size_t>(N_) * K_, dtype_, 2, *s);
     auto e0 = dev_.create_event();
     auto e1 = dev_.create_event();
-    // Warm the clocks up (DVFS) before measuring.
-    for (int i = 0; i < 20; ++i) launch(Mmax, *s);
+    // Run ~0.3 s first so the measurement sees the sustained (DVFS-settled)
+    // clock rather than the cold-start boost.
+    for (int i = 0; i < 400; ++i) launch(Mmax, *s);
     s->synchronize();
     for (int M : {8192, 1024, 256}) {
       // Size the batch to ~40 ms of work.
@@ -177,9 +212,14 @@ class GpuCompute : public ComputeEngine {
     }
   }
 
+  static constexpr int kMmax = 8192;
+  static constexpr size_t kSlots = 64;
   Device& dev_;
   ComputeMode mode_;
   double scale_;
+  Buffer slots_;
+  std::map<Stream*, size_t> slot_of_;
+  int grid_ = 256;
   double hz_ = 1e8;
   int cus_ = 256;
   DType dtype_ = DType::BF16;

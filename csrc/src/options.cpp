@@ -68,7 +68,7 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  -m, --min_exectime S   run at least S seconds (overrides --runs)\n"
      << "  -h, --help             this help\n"
      << "  --backend B            auto | rccl | cpu\n"
-     << "  --compute C            auto | sleep | spin | gemm | flops\n"
+     << "  --compute C            auto | sleep | spin | gemm | gemm-work | flops\n"
      << "  --wire-dtype T         bf16 | fp16 | fp32 | fp8 (collective element type)\n"
      << "  --compute-dtype T      auto | bf16 | fp8 (GEMM operand type for gemm/flops)\n"
      << "  --schedule S           overlap (stream-ordered) | reference (blocking like DLNetBench)\n"
@@ -82,7 +82,8 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  --stats-file PATH      stats file to use instead of <base>/model_stats/<model>.txt\n"
      << "  --store HOST:PORT      rendezvous store address\n"
      << "  --no-topology          do not print the topology graph\n"
-     << "  --quiet                only print the report section\n";
+     << "  --quiet                only print the report section\n"
+     << "  --silent               print nothing (the report is returned to the caller)\n";
   return os.str();
 }
 
@@ -145,6 +146,9 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
     } else if (is("--store")) {
       o.store_addr = val("store");
     } else if (a == "--no-topology") {
+      o.topology = false;
+    } else if (a == "--silent") {
+      o.silent = o.quiet = true;
       o.topology = false;
     } else if (a == "--quiet") {
       o.quiet = true;

@@ -17,6 +17,8 @@
 #include <sstream>
 #include <thread>
 
+extern char** environ;
+
 #include "dlnb/kernels.hpp"
 #include "dlnb/strategy.hpp"
 
@@ -304,6 +306,19 @@ Json run_benchmark(const Options& opt) {
   ext["runs"] = runs;
   ext["warmup_times"] = Json(warm);
   ext["timed_region_s"] = timed_region;
+  {
+    // Collective-library knobs of this run (the reference recorded them as
+    // SbatchMan job variables, plots/parser.py:151-154).
+    Json env = Json::object();
+    for (char** e = environ; e && *e; ++e) {
+      std::string kv = *e;
+      if (starts_with(kv, "NCCL_") || starts_with(kv, "RCCL_") || starts_with(kv, "HSA_") || starts_with(kv, "DLNB_")) {
+        size_t eq = kv.find('=');
+        if (eq != std::string::npos) env[kv.substr(0, eq)] = kv.substr(eq + 1);
+      }
+    }
+    ext["env"] = env;
+  }
   // Iteration time = max over ranks per run (the slowest rank bounds a step).
   std::vector<Json> ranks;
   for (const auto& s : all) ranks.push_back(Json::parse(s));
@@ -333,7 +348,7 @@ Json run_benchmark(const Options& opt) {
   for (auto& r : ranks) rarr.push_back(r);
   doc["ranks"] = rarr;
 
-  if (ri.rank == 0) {
+  if (ri.rank == 0 && !opt.silent) {
     std::string text = doc.dump();
     std::cout << "<<<DLNB_REPORT_BEGIN " << strat->section_id() << ">>>\n"
               << text << "\n<<<DLNB_REPORT_END " << strat->section_id() << ">>>" << std::endl;
@@ -344,10 +359,10 @@ Json run_benchmark(const Options& opt) {
                   it.at("compute_floor_ms").as_double(), it.at("timed_ms_per_iter").as_double());
       std::fflush(stdout);
     }
-    if (!opt.json_path.empty()) {
-      std::ofstream f(opt.json_path);
-      f << doc.dump(1) << "\n";
-    }
+  }
+  if (ri.rank == 0 && !opt.json_path.empty()) {
+    std::ofstream f(opt.json_path);
+    f << doc.dump(1) << "\n";
   }
   ctx.hg().barrier();  // keep the store (rank 0) alive until everyone is done
   return doc;

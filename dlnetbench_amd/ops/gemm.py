@@ -1,0 +1,90 @@
+"""Torch-facing wrappers for the hand-written CDNA4 kernels.
+
+These call straight into libdlnb.so on torch's current HIP stream; there is
+no fallback: on a GPU box a missing library is an error, never a silent
+PyTorch path.
+"""
+from __future__ import annotations
+
+from .. import _native
+
+
+def _stream(t):
+    import torch
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def gemm_tn(a, b, out=None):
+    """C[M,N] (bf16) = A[M,K] @ B[N,K]^T with the 256x256 MFMA kernel.
+
+    a, b: bf16 or float8_e4m3fn (OCP) CUDA tensors, row-major, K contiguous.
+    M and N must be multiples of 256; K*elem_size a multiple of 128 bytes.
+    """
+    import torch
+    if a.dtype != b.dtype:
+        raise TypeError("a and b must have the same dtype")
+    if a.dtype == torch.bfloat16:
+        dt = _native.DTYPES["bf16"]
+    elif a.dtype == getattr(torch, "float8_e4m3fn", None):
+        dt = _native.DTYPES["fp8_e4m3"]
+    else:
+        raise TypeError(f"unsupported dtype {a.dtype}")
+    M, K = a.shape
+    N, K2 = b.shape
+    if K != K2:
+        raise ValueError("K mismatch")
+    if not a.is_contiguous() or not b.is_contiguous():
+        raise ValueError("a and b must be contiguous")
+    L = _native.lib()
+    if not L.dlnb_gemm_shape_ok(M, N, K, dt):
+        raise ValueError(f"unsupported shape M={M} N={N} K={K} (M,N % 256, K bytes % 128)")
+    if out is None:
+        out = torch.empty((M, N), device=a.device, dtype=torch.bfloat16)
+    _native.check(L.dlnb_gemm_tn(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, K, K, N, dt, _stream(a)))
+    return out
+
+
+def gemm_deadline_us(a, b, c, us: float, stamp=None, grid: int = 0):
+    """Persistent MFMA GEMM over C = A.B^T tiles that stops after `us` microseconds
+    (device clock). `stamp` is a CUDA int64 tensor with >= 1 element (scratch)."""
+    import torch
+    dt = _native.DTYPES["bf16"] if a.dtype == torch.bfloat16 else _native.DTYPES["fp8_e4m3"]
+    M, K = a.shape
+    N = b.shape[0]
+    if stamp is None:
+        stamp = torch.zeros(8, dtype=torch.int64, device=a.device)
+    _native.check(_native.lib().dlnb_gemm_deadline_us(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, dt, us,
+                                                      a.device.index or 0, stamp.data_ptr(), grid, _stream(a)))
+    return c
+
+
+def fill_random_(t, seed: int = 0):
+    """In-place uniform [-1, 1) fill with the native hash kernel."""
+    import torch
+    m = {torch.bfloat16: "bf16", torch.float16: "fp16", torch.float32: "fp32"}
+    f8 = getattr(torch, "float8_e4m3fn", None)
+    if f8 is not None:
+        m[f8] = "fp8_e4m3"
+    f85 = getattr(torch, "float8_e5m2", None)
+    if f85 is not None:
+        m[f85] = "fp8_e5m2"
+    dt = _native.DTYPES[m[t.dtype]]
+    _native.check(_native.lib().dlnb_fill_random(t.data_ptr(), t.numel(), dt, seed, _stream(t)))
+    return t
+
+
+def sgd_momentum_(param, mom, grad, lr: float = 1e-4, beta: float = 0.9):
+    """param -= lr * (mom = beta*mom + grad), bf16 tensors, fp32 math."""
+    _native.check(_native.lib().dlnb_sgd_momentum_bf16(param.data_ptr(), mom.data_ptr(), grad.data_ptr(),
+                                                       param.numel(), lr, beta, _stream(param)))
+    return param
+
+
+def idle_wait_us(us: float, device: int = 0):
+    import torch
+    _native.check(_native.lib().dlnb_idle_wait_us(us, device, torch.cuda.current_stream(device).cuda_stream))
+
+
+def busy_spin_us(us: float, device: int = 0):
+    import torch
+    _native.check(_native.lib().dlnb_busy_spin_us(us, device, torch.cuda.current_stream(device).cuda_stream))

@@ -1,0 +1,194 @@
+"""Parallel layouts and message sizes, mirrored in Python.
+
+These are the exact formulas the native drivers use (csrc/src/strategy_*.cpp),
+which in turn follow the reference:
+
+* DP   (cpp/data_parallel/dp.cpp:159-164): bucket i = P // nb (+1 for i < P % nb).
+* FSDP (cpp/data_parallel/fsdp.cpp:244-265): unit u = P // U (+1 for u < P % U);
+  shard = ceil(unit / F); unit group = rank // F; replica group = rank % F.
+* Hybrids (hybrid_2d.cpp:236-282, hybrid_3d.cpp:283-325, hybrid_3d_moe.cpp:313-363):
+  inner (TP/EP) fastest, then stage, then DP replica; pipe = s*d*B/mb;
+  TP AR = pipe/T; DP AR = P/S, P/(S*T), NE/S + (P-NE)/S/EP; A2A per peer =
+  (B/mb)*s*2*d/EP.
+
+Used by the tests (golden values), by ``python -m dlnetbench_amd.parallel.plan``
+(prints a run's messages, bytes and memory before launching it) and by the
+results tooling (bus-bandwidth accounting).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+from dataclasses import asdict, dataclass, field
+from typing import Dict, List, Optional
+
+from ..utils.stats import ModelStats, load_stats
+
+WIRE_BYTES = {"bf16": 2, "fp16": 2, "fp32": 4, "fp8": 1, "fp8_e4m3": 1, "fp8_e5m2": 1}
+
+
+# --------------------------------------------------------------- layouts
+def grid_coords(rank: int, inner: int, stages: int):
+    """(inner_id, stage_id, dp_id) with inner fastest."""
+    return rank % inner, (rank // inner) % stages, rank // (inner * stages)
+
+
+def inner_group(rank: int, inner: int, stages: int) -> List[int]:
+    i, s, d = grid_coords(rank, inner, stages)
+    return [d * inner * stages + s * inner + k for k in range(inner)]
+
+
+def pp_group(rank: int, inner: int, stages: int) -> List[int]:
+    i, s, d = grid_coords(rank, inner, stages)
+    return [d * inner * stages + k * inner + i for k in range(stages)]
+
+
+def dp_group(rank: int, inner: int, stages: int, world: int) -> List[int]:
+    i, s, d = grid_coords(rank, inner, stages)
+    return [k * inner * stages + s * inner + i for k in range(world // (inner * stages))]
+
+
+def fsdp_groups(rank: int, F: int, world: int):
+    unit = [r for r in range(world) if r // F == rank // F]
+    replica = [r for r in range(world) if r % F == rank % F]
+    return unit, replica
+
+
+# ----------------------------------------------------------------- plans
+@dataclass
+class Message:
+    name: str
+    op: str            # allreduce | allgather | reduce_scatter | alltoall | sendrecv
+    group_size: int
+    elements: int      # per-op element count in the reference's convention
+    calls_per_iter: int
+    wire_bytes: int = 0  # bytes moved by one op (algbw numerator)
+
+
+@dataclass
+class Plan:
+    strategy: str
+    world: int
+    params: Dict[str, int]
+    compute_per_unit_us: Dict[str, float]
+    messages: List[Message] = field(default_factory=list)
+    memory_bytes: int = 0
+
+    def to_json(self) -> dict:
+        d = asdict(self)
+        return d
+
+
+def _split(total: int, parts: int) -> List[int]:
+    base, rem = divmod(total, parts)
+    return [base + (1 if i < rem else 0) for i in range(parts)]
+
+
+def plan_dp(st: ModelStats, world: int, nb: int, wire: str = "bf16") -> Plan:
+    es = WIRE_BYTES[wire]
+    sizes = _split(st.model_size, nb)
+    p = Plan("dp", world, {"num_buckets": nb},
+             {"fwd": st.fwd_us, "bwd_per_bucket": st.bwd_us / nb})
+    p.messages.append(Message("bucket_allreduce", "allreduce", world, sizes[0], nb, sizes[0] * es))
+    p.memory_bytes = 2 * st.model_size * es
+    return p
+
+
+def fsdp_shards(st: ModelStats, U: int, F: int) -> List[int]:
+    return [u // F + (1 if u % F else 0) for u in _split(st.model_size, U)]
+
+
+def plan_fsdp(st: ModelStats, world: int, U: int, F: int, wire: str = "bf16") -> Plan:
+    if world % F:
+        raise ValueError("world size must be divisible by the sharding factor")
+    es = WIRE_BYTES[wire]
+    sh = fsdp_shards(st, U, F)
+    R = world // F
+    p = Plan("fsdp", world, {"num_units": U, "sharding_factor": F, "num_replicas": R},
+             {"fwd_per_unit": st.fwd_us / U, "bwd_per_unit": st.bwd_us / U})
+    p.messages.append(Message("allgather", "allgather", F, sh[0], 2 * U - 1, sh[0] * F * es))
+    p.messages.append(Message("reduce_scatter", "reduce_scatter", F, sh[0], U, sh[0] * F * es))
+    if R > 1:
+        p.messages.append(Message("replica_allreduce", "allreduce", R, sh[0], U, sh[0] * es))
+    p.memory_bytes = (2 * sum(sh) + 4 * sh[0] * F) * es
+    return p
+
+
+def plan_hybrid(st: ModelStats, world: int, kind: str, S: int, mb: int, inner: int = 1, layers: int = 0,
+                wire: str = "bf16", tp_granularity: str = "microbatch") -> Plan:
+    es = WIRE_BYTES[wire]
+    if layers and layers % S:
+        raise ValueError("num_layers must be divisible by num_stages")
+    if st.batch % mb:
+        raise ValueError("batch must be divisible by num_microbatches")
+    if world % (S * inner):
+        raise ValueError("world must be divisible by stages*inner")
+    spmb = st.batch // mb
+    pipe = st.seq_len * st.hidden * spmb
+    tsh = inner if kind == "hybrid_3d" else 1
+    P = st.model_size
+    params = {"num_stages": S, "num_microbatches": mb, "dp_size": world // (S * inner)}
+    p = Plan(kind, world, params, {"fwd_per_microbatch": st.fwd_us / S / (mb * tsh),
+                                   "bwd_per_microbatch": st.bwd_us / S / (mb * tsh)})
+    if S > 1:
+        p.messages.append(Message("pipe_sendrecv", "sendrecv", 2, pipe, 2 * mb, pipe * es))
+    if kind == "hybrid_2d":
+        dp_ar = P // S
+    elif kind == "hybrid_3d":
+        params["num_tensor_shards"] = inner
+        dp_ar = P // (S * inner)
+        tp = pipe // inner
+        n = 4 * mb if tp_granularity == "microbatch" else 2 * (layers // S) * 2 * mb
+        p.messages.append(Message("tp_allreduce", "allreduce", inner, tp, n, tp * es))
+    else:
+        params["num_expert_shards"] = inner
+        ne = st.non_expert_size // S
+        dp_ar = ne + ((P - st.non_expert_size) // S) // inner
+        a2a = (spmb * st.seq_len * 2 * st.hidden) // inner
+        p.messages.append(Message("ep_alltoall", "alltoall", inner, a2a, 2 * (layers // S) * mb * 2, a2a * inner * es))
+        p.messages.append(Message("ep_nonexpert_allreduce", "allreduce", inner, ne, 1, ne * es))
+    p.messages.append(Message("dp_allreduce", "allreduce", world // (S * inner), dp_ar, 1, dp_ar * es))
+    p.memory_bytes = (8 * pipe + 2 * dp_ar) * es
+    return p
+
+
+def busbw_factor(op: str, n: int) -> float:
+    """nccl-tests bus-bandwidth factor (BASELINE.md 'Metric definitions')."""
+    if n <= 1:
+        return 1.0
+    if op == "allreduce":
+        return 2.0 * (n - 1) / n
+    if op in ("allgather", "reduce_scatter", "alltoall"):
+        return (n - 1) / n
+    return 1.0
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description="Print the messages and memory of a benchmark run")
+    ap.add_argument("strategy", choices=["dp", "fsdp", "hybrid_2d", "hybrid_3d", "hybrid_3d_moe"])
+    ap.add_argument("model")
+    ap.add_argument("params", nargs="+", type=int)
+    ap.add_argument("--world", type=int, required=True)
+    ap.add_argument("--base", default=".")
+    ap.add_argument("--wire", default="bf16")
+    a = ap.parse_args(argv)
+    st = load_stats(os.path.join(a.base, "model_stats", a.model + ".txt"))
+    if a.strategy == "dp":
+        pl = plan_dp(st, a.world, *a.params, wire=a.wire)
+    elif a.strategy == "fsdp":
+        pl = plan_fsdp(st, a.world, *a.params, wire=a.wire)
+    else:
+        base = a.model.rsplit("_", 2)[0]
+        with open(os.path.join(a.base, "models", base + ".json")) as f:
+            arch = json.load(f)
+        L = arch.get("num_encoder_blocks", 0) + arch.get("num_decoder_blocks", 0)
+        inner = a.params[2] if len(a.params) > 2 else 1
+        pl = plan_hybrid(st, a.world, a.strategy, a.params[0], a.params[1], inner, L, wire=a.wire)
+    print(json.dumps(pl.to_json(), indent=1))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,194 @@
+"""Every strategy as a multi-process job on the CPU backend (shared memory),
+driven through the real CLI binaries and the launcher.
+
+This is the reference's "mpi_cpu" plumbing configuration (README.md:96,
+BASELINE.json config 1) made testable: W = 1, 2, 4, 8 ranks, golden report
+keys, timer counts, and timing sanity (an iteration can not
+be shorter than its compute).
+"""
+import os
+
+import pytest
+
+from dlnetbench_amd.utils import launch, report
+
+BIN = None
+
+
+@pytest.fixture(scope="module", autouse=True)
+def binaries(root):
+    global BIN
+    BIN = os.path.join(root, "build", "bin")
+    if not os.path.exists(os.path.join(BIN, "dp")):
+        pytest.skip("native binaries not built (run make)")
+
+
+def run(n, prog, *args, timeout=120):
+    code, outs = launch.launch(n, [os.path.join(BIN, prog), *map(str, args), "--quiet"], timeout=timeout,
+                               capture=True)
+    text = "".join(o or "" for o in outs)
+    assert code == 0, text[-3000:]
+    docs = report.parse_output(outs[0])
+    assert len(docs) == 1, outs[0][-2000:]
+    return next(iter(docs.values()))
+
+
+DP_GLOBAL = {"model_name", "num_buckets", "local_batch_size", "world_size", "fwd_rt_whole_model",
+             "bwd_rt_per_bucket", "total_model_size_params", "msg_size_avg_bytes", "msg_size_std_bytes",
+             "device", "backend"}
+DP_RANK = {"runtimes", "barrier_time", "hostname"}
+FSDP_GLOBAL = {"model_size_bytes", "model_name", "world_size", "num_units", "sharding_factor", "num_replicas",
+               "local_batch_size", "device", "backend", "fwd_time_per_unit_us", "bwd_time_per_unit_us",
+               "allgather_msg_size_bytes", "reducescatter_msg_size_bytes"}
+FSDP_RANK = {"runtime", "allgather", "allgather_wait_fwd", "allgather_wait_bwd", "reduce_scatter", "barrier",
+             "hostname", "rank"}
+PP_GLOBAL = {"model_name", "num_stages", "num_microbatches", "samples_per_microbatch", "local_batch_size",
+             "global_batch_size", "world_size", "dp_size", "fwd_rt_per_microbatch", "bwd_rt_per_microbatch",
+             "total_model_size_params", "pipe_msg_size_bytes", "dp_allreduce_size_bytes", "device", "backend"}
+PP_RANK = {"runtimes", "pp_comm_time", "dp_comm_time", "hostname", "stage_id"}
+
+
+@pytest.mark.parametrize("w", [1, 2, 4])
+def test_dp(w, data_dir):
+    d = run(w, "dp", "tiny_dense_8_bfloat16", 5, data_dir, "-w", 1, "-r", 3)
+    g = d["global"]
+    assert DP_GLOBAL <= set(g) and g["world_size"] == w and g["backend"] == "CPU-SHM"
+    assert g["num_buckets"] == 5 and g["total_model_size_params"] == 1000003
+    # 1000003 / 5 -> buckets of 200001 (x3) and 200000 (x2): bf16 bytes
+    assert g["msg_size_avg_bytes"] == pytest.approx(200000.6 * 2)
+    assert len(d["ranks"]) == w
+    for r in d["ranks"]:
+        assert DP_RANK <= set(r)
+        assert len(r["runtimes"]) == 3 and len(r["barrier_time"]) == 3 and len(r["allreduce_time"]) == 15
+        for rt in r["runtimes"]:
+            assert rt >= 0.006 * 0.98  # fwd + bwd = 6 ms of compute
+    assert d["global"]["dlnb"]["iteration"]["median_ms"] >= 6.0 * 0.98
+
+
+@pytest.mark.parametrize("w,F", [(2, 2), (4, 2), (4, 4)])
+def test_fsdp(w, F, data_dir):
+    U = 4
+    d = run(w, "fsdp", "tiny_dense_8_bfloat16", U, F, data_dir, "-w", 1, "-r", 2)
+    g = d["global"]
+    assert FSDP_GLOBAL <= set(g)
+    assert g["num_replicas"] == w // F and g["sharding_factor"] == F
+    shard = -(-(1000003 // U + 1) // F)  # unit 0 gets the remainder element
+    assert g["reducescatter_msg_size_bytes"] == shard * 2
+    assert g["allgather_msg_size_bytes"] == shard * F * 2
+    if w // F > 1:
+        assert "allreduce_msg_size_bytes" in g
+    for r in d["ranks"]:
+        assert FSDP_RANK <= set(r)
+        runs = 2
+        assert len(r["runtime"]) == runs
+        assert len(r["allgather"]) == runs
+        assert len(r["allgather_wait_fwd"]) == runs * (U - 1)
+        assert len(r["allgather_wait_bwd"]) == runs * (U - 1)
+        assert len(r["reduce_scatter"]) == runs * U
+        assert len(r["allreduce_time"]) == (runs * U if w // F > 1 else 0)
+        assert min(r["runtime"]) >= 0.006 * 0.98
+
+
+def test_fsdp_reference_schedule(data_dir):
+    d = run(2, "fsdp", "tiny_dense_8_bfloat16", 4, 2, data_dir, "-w", 1, "-r", 2, "--schedule", "reference")
+    assert d["global"]["dlnb"]["schedule"] == "reference"
+
+
+@pytest.mark.parametrize("w,S,mb", [(1, 1, 2), (2, 2, 4), (4, 4, 8), (4, 2, 2)])
+def test_hybrid_2d(w, S, mb, data_dir):
+    d = run(w, "hybrid_2d", "tiny_dense_8_bfloat16", S, mb, data_dir, "-w", 1, "-r", 2)
+    g = d["global"]
+    assert PP_GLOBAL <= set(g)
+    assert g["dp_size"] == w // S and g["samples_per_microbatch"] == 8 // mb
+    assert g["pipe_msg_size_bytes"] == 64 * 128 * (8 // mb) * 2
+    assert g["dp_allreduce_size_bytes"] == (1000003 // S) * 2
+    stages = sorted(r["stage_id"] for r in d["ranks"])
+    assert stages == sorted([r % S for r in range(w)])
+    for r in d["ranks"]:
+        assert PP_RANK <= set(r)
+        assert len(r["pp_comm_time"]) == 2 * mb * 2  # fwd + bwd entries per microbatch, 2 runs
+        assert len(r["dp_comm_time"]) == 2
+    # GPipe: (mb + S - 1) microbatch slots of (fwd + bwd) per stage
+    per_mb = 6.0 / S / mb
+    assert g["dlnb"]["iteration"]["median_ms"] >= 0.95 * (mb + S - 1) * per_mb
+
+
+@pytest.mark.parametrize("w,S,T,gran", [(2, 1, 2, "microbatch"), (4, 2, 2, "microbatch"), (4, 2, 2, "layer"),
+                                        (8, 2, 2, "microbatch")])
+def test_hybrid_3d(w, S, T, gran, data_dir):
+    mb = 2
+    d = run(w, "hybrid_3d", "tiny_dense_8_bfloat16", S, mb, T, data_dir, "-w", 1, "-r", 2,
+            "--tp-granularity", gran)
+    g = d["global"]
+    assert PP_GLOBAL | {"num_tensor_shards", "tp_allreduce_size_bytes"} <= set(g)
+    assert g["tp_allreduce_size_bytes"] == 64 * 128 * (8 // mb) // T * 2
+    assert g["dp_allreduce_size_bytes"] == (1000003 // (S * T)) * 2
+    n_ar = 4 * mb if gran == "microbatch" else 2 * (4 // S) * 2 * mb
+    for r in d["ranks"]:
+        assert {"tp_comm_time", "tp_id", "dp_id"} <= set(r)
+        assert len(r["tp_comm_time"]) == 2 * n_ar
+        assert r["tp_id"] == r["rank"] % T
+
+
+@pytest.mark.parametrize("w,S,EP", [(2, 1, 2), (4, 2, 2), (8, 2, 4)])
+def test_hybrid_3d_moe(w, S, EP, data_dir):
+    mb = 2
+    d = run(w, "hybrid_3d_moe", "tiny_moe_8_bfloat16", S, mb, EP, data_dir, "-w", 1, "-r", 2)
+    g = d["global"]
+    assert PP_GLOBAL | {"num_expert_shards", "num_experts", "sequence_length", "embedded_dim",
+                        "ep_alltoall_size_bytes"} <= set(g)
+    assert g["num_experts"] == 4
+    assert g["ep_alltoall_size_bytes"] == (8 // mb) * 64 * 2 * 128 // EP * 2
+    ne = 400000 // S
+    assert g["dp_allreduce_size_bytes"] == (ne + (2000000 - 400000) // S // EP) * 2
+    for r in d["ranks"]:
+        assert {"ep_comm_time", "dp_ep_comm_time", "ep_id", "dp_id"} <= set(r)
+        assert len(r["ep_comm_time"]) == 2 * (2 * (4 // S) * mb * 2)
+        assert len(r["dp_ep_comm_time"]) == 2
+
+
+def test_hybrid_3d_moe_rejects_bad_expert_split(data_dir):
+    code, outs = launch.launch(3, [os.path.join(BIN, "hybrid_3d_moe"), "tiny_moe_8_bfloat16", "1", "2", "3",
+                                   data_dir, "--quiet"], timeout=60, capture=True)
+    assert code != 0
+    assert "divisible" in "".join(o or "" for o in outs)
+
+
+def test_dp_options_inplace_optimizer_minexec(data_dir):
+    d = run(2, "dp", "tiny_dense_8_bfloat16", 4, data_dir, "-w", 3, "-m", 0.05, "--in-place", "--optimizer")
+    g = d["global"]
+    assert g["in_place"] is True
+    runs = g["dlnb"]["runs"]
+    import math
+    warm = g["dlnb"]["warmup_times"]
+    assert runs >= math.ceil(0.05 / max(warm) - 1e-9)
+    assert len(d["ranks"][0]["runtimes"]) == runs
+
+
+def test_pipeline_dp_buckets(data_dir):
+    d = run(4, "hybrid_2d", "tiny_dense_8_bfloat16", 2, 4, data_dir, "-w", 1, "-r", 2, "--dp-buckets", 4)
+    for r in d["ranks"]:
+        assert len(r["dp_comm_time"]) == 2 * 4
+
+
+def test_loop_mode_terminates_with_max_iters(data_dir):
+    code, outs = launch.launch(2, [os.path.join(BIN, "dp_loop"), "tiny_dense_8_bfloat16", "2", data_dir,
+                                   "--quiet", "--max-loop-iters", "5"], timeout=60, capture=True)
+    assert code == 0
+    assert "DLNB_REPORT_BEGIN" not in outs[0]
+
+
+def test_json_output_file(tmp_path, data_dir):
+    out = tmp_path / "r.json"
+    run(2, "dp", "tiny_dense_8_bfloat16", 2, data_dir, "-w", 0, "-r", 1, "--json", out)
+    import json
+    d = json.loads(out.read_text())
+    assert d["section"] == "dp" and len(d["ranks"]) == 2
+
+
+def test_gpt2_l_dp_cpu_baseline_config1(root):
+    """BASELINE.json config 1: gpt2_l DP on the CPU backend, W = 2 (full-size buffers)."""
+    d = run(2, "dp", "gpt2_l_16_bfloat16", 10, root, "-w", 1, "-r", 2, timeout=300)
+    it = d["global"]["dlnb"]["iteration"]
+    assert it["median_ms"] >= it["compute_floor_ms"] * 0.98
+    assert d["global"]["msg_size_avg_bytes"] == 77403008 * 2

@@ -1,0 +1,106 @@
+"""Numerics of the hand-written gfx950 kernels against fp32 PyTorch references."""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+from dlnetbench_amd.ops import gemm  # noqa: E402
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 512, 128), (512, 256, 1024), (768, 1280, 640),
+                                   (2048, 1024, 4096)])
+def test_gemm_bf16_matches_torch(M, N, K):
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", generator=g).to(torch.bfloat16)
+    c = gemm.gemm_tn(a, b)
+    torch.cuda.synchronize()
+    ref = a.float() @ b.float().t()
+    tol = 2e-2 * ref.abs().max().item() + 1e-2
+    assert (c.float() - ref).abs().max().item() < tol
+
+
+def test_gemm_bf16_identity_asymmetric():
+    # A = I picks rows of B: catches any row/column swap in the C write.
+    M = N = 256
+    K = 256
+    a = torch.eye(M, K, device="cuda", dtype=torch.bfloat16)
+    b = (torch.arange(N * K, device="cuda", dtype=torch.float32).reshape(N, K) % 97 / 8.0).to(torch.bfloat16)
+    c = gemm.gemm_tn(a, b)
+    torch.cuda.synchronize()
+    assert torch.equal(c.float(), b.float().t())
+
+
+@pytest.mark.skipif(not hasattr(torch, "float8_e4m3fn"), reason="torch without float8")
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 512), (1024, 512, 2048)])
+def test_gemm_fp8_matches_torch(M, N, K):
+    g = torch.Generator(device="cuda").manual_seed(7 + M)
+    a = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(torch.float8_e4m3fn)
+    b = (torch.randn(N, K, device="cuda", generator=g) * 0.5).to(torch.float8_e4m3fn)
+    c = gemm.gemm_tn(a, b)
+    torch.cuda.synchronize()
+    ref = a.float() @ b.float().t()
+    tol = 2e-2 * ref.abs().max().item() + 1e-2
+    assert (c.float() - ref).abs().max().item() < tol
+
+
+def test_fill_random_uniform():
+    t = torch.empty(1 << 20, device="cuda", dtype=torch.bfloat16)
+    gemm.fill_random_(t, seed=3)
+    torch.cuda.synchronize()
+    f = t.float()
+    assert f.min().item() >= -1.0 and f.max().item() <= 1.0
+    assert abs(f.mean().item()) < 0.01
+    assert abs(f.std().item() - (1 / 3) ** 0.5) < 0.02
+
+
+def test_sgd_momentum_matches_torch():
+    n = 100003
+    p = torch.randn(n, device="cuda").to(torch.bfloat16)
+    m = torch.randn(n, device="cuda").to(torch.bfloat16)
+    g = torch.randn(n, device="cuda").to(torch.bfloat16)
+    m_ref = 0.9 * m.float() + g.float()
+    p_ref = p.float() - 1e-2 * m_ref
+    gemm.sgd_momentum_(p, m, g, lr=1e-2, beta=0.9)
+    torch.cuda.synchronize()
+    assert (m.float() - m_ref).abs().max().item() < 2e-2
+    assert (p.float() - p_ref).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("fn", ["idle", "spin"])
+def test_deadline_kernels_hit_duration(fn):
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for us in (200.0, 5000.0):
+        e0.record(s)
+        (gemm.idle_wait_us if fn == "idle" else gemm.busy_spin_us)(us)
+        e1.record(s)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        assert us / 1e3 * 0.97 <= ms <= us / 1e3 * 1.10 + 0.05, (us, ms)
+
+
+@pytest.mark.parametrize("us", [100.0, 2000.0, 30000.0])
+def test_deadline_gemm_duration(us):
+    a = torch.empty(8192, 4096, device="cuda", dtype=torch.bfloat16)
+    b = torch.empty(14336, 4096, device="cuda", dtype=torch.bfloat16)
+    gemm.fill_random_(a, 1)
+    gemm.fill_random_(b, 2)
+    c = torch.empty(8192, 14336, device="cuda", dtype=torch.bfloat16)
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    gemm.gemm_deadline_us(a, b, c, us)  # warm
+    e0.record(s)
+    gemm.gemm_deadline_us(a, b, c, us)
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1)
+    assert us / 1e3 <= ms * 1.01 and ms <= us / 1e3 * 1.05 + 0.03, (us, ms)

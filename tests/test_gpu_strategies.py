@@ -1,0 +1,51 @@
+"""Every strategy end to end on one MI355X (RCCL, 1-rank groups, GEMM compute)."""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+from dlnetbench_amd import engine  # noqa: E402
+
+CASES = [
+    ("dp", "tiny_dense_8_bfloat16", (4,)),
+    ("fsdp", "tiny_dense_8_bfloat16", (4, 1)),
+    ("hybrid_2d", "tiny_dense_8_bfloat16", (1, 4)),
+    ("hybrid_3d", "tiny_dense_8_bfloat16", (1, 2, 1)),
+    ("hybrid_3d_moe", "tiny_moe_8_bfloat16", (1, 2, 1)),
+]
+
+
+@pytest.mark.parametrize("strategy,model,params", CASES)
+@pytest.mark.parametrize("compute", ["gemm", "sleep"])
+def test_strategy_runs_on_gpu(strategy, model, params, compute, data_dir):
+    doc = engine.run(strategy, model, *params, base_path=data_dir, warmup=1, runs=2, compute=compute,
+                     backend="rccl", quiet=True)
+    g = doc["global"]
+    assert g["backend"] == "RCCL" and g["device"] == "GPU"
+    it = g["dlnb"]["iteration"]
+    floor = it["compute_floor_ms"]
+    if strategy.startswith("hybrid"):
+        floor = floor  # S = 1: the single stage does all the compute
+    # compute is stream-ordered device work of exactly the table's duration
+    assert it["median_ms"] >= 0.9 * floor
+    assert it["median_ms"] < 3.0 * floor + 5.0
+    if compute == "gemm":
+        lv = g["dlnb"]["compute"]["gemm_levels"]
+        assert lv and lv[0]["tflops"] > 50
+
+
+def test_fsdp_llama3_8b_single_gpu_iteration(root):
+    """The bench config at N=1 with time scaled down 20x (memory + collectives full size)."""
+    doc = engine.run("fsdp", "llama3_8b_16_bfloat16", 32, 1, base_path=root, warmup=1, runs=1,
+                     compute="gemm", backend="rccl", time_scale=0.05, quiet=True)
+    it = doc["global"]["dlnb"]["iteration"]
+    assert it["median_ms"] >= 0.9 * it["compute_floor_ms"]
+    assert doc["global"]["allgather_msg_size_bytes"] == 250945664 * 2

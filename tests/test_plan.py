@@ -1,0 +1,98 @@
+"""Layouts and message sizes: golden values from SURVEY.md §2.4 / BASELINE.md."""
+import os
+
+import pytest
+
+from dlnetbench_amd.parallel import plan as P
+from dlnetbench_amd.utils.stats import load_stats
+
+
+@pytest.fixture(scope="module")
+def stats(root):
+    return lambda n: load_stats(os.path.join(root, "model_stats", n + ".txt"))
+
+
+def test_grid_3d_reference_layout():
+    # hybrid_3d.cpp:283-300: tp_id = rank % T, stage = (rank/T) % S, dp = rank/(T*S)
+    T, S, W = 4, 2, 16
+    for r in range(W):
+        i, s, d = P.grid_coords(r, T, S)
+        assert (i, s, d) == (r % T, (r // T) % S, r // (T * S))
+        assert r in P.inner_group(r, T, S) and r in P.pp_group(r, T, S) and r in P.dp_group(r, T, S, W)
+        # pp rank == stage id (hybrid_3d.cpp:308)
+        assert P.pp_group(r, T, S).index(r) == s
+    assert P.inner_group(5, 4, 2) == [4, 5, 6, 7]
+    assert P.pp_group(5, 4, 2) == [1, 5]
+    assert P.dp_group(5, 4, 2, 16) == [5, 13]
+
+
+def test_grid_2d_reference_layout():
+    # hybrid_2d.cpp:272-282: pp groups are contiguous blocks of S ranks
+    assert P.pp_group(5, 1, 4) == [4, 5, 6, 7]
+    assert P.dp_group(5, 1, 4, 8) == [1, 5]
+    assert P.grid_coords(6, 1, 4)[1] == 2
+
+
+def test_fsdp_groups():
+    unit, rep = P.fsdp_groups(5, 4, 8)
+    assert unit == [4, 5, 6, 7] and rep == [1, 5]
+
+
+def test_c2_llama3_8b_fsdp(stats):
+    st = stats("llama3_8b_16_bfloat16")
+    sh = P.fsdp_shards(st, 32, 8)
+    assert sh[0] == 31368208
+    pl = P.plan_fsdp(st, 8, 32, 8)
+    ag = [m for m in pl.messages if m.name == "allgather"][0]
+    assert ag.wire_bytes == 250945664 * 2
+    # per-rank wire bytes: 2 AG passes + 1 RS ~ 42.16 GB
+    per_rank = (2 * 32 * 7 + 32 * 7) * sh[0] * 2
+    assert per_rank / 1e9 == pytest.approx(42.16, abs=0.01)
+
+
+def test_c3_llama3_70b_hybrid_3d(stats):
+    st = stats("llama3_70b_16_bfloat16")
+    pl = P.plan_hybrid(st, 8, "hybrid_3d", 2, 4, 4, layers=80)
+    m = {x.name: x for x in pl.messages}
+    assert m["pipe_sendrecv"].elements == 268435456
+    assert m["tp_allreduce"].elements == 67108864 and m["tp_allreduce"].calls_per_iter == 16
+    assert m["dp_allreduce"].elements == 8819213312
+    assert pl.params["dp_size"] == 1
+    assert pl.compute_per_unit_us["fwd_per_microbatch"] == pytest.approx(254109.35, abs=0.01)
+
+
+def test_c4_mixtral_hybrid_moe(stats):
+    st = stats("mixtral_8x7b_16_bfloat16")
+    pl = P.plan_hybrid(st, 8, "hybrid_3d_moe", 2, 16, 4, layers=32)
+    m = {x.name: x for x in pl.messages}
+    assert m["ep_alltoall"].elements == 67108864
+    assert m["ep_alltoall"].calls_per_iter == 1024
+    assert m["dp_allreduce"].elements == 6475349088
+
+
+def test_c5_vit_h_dp(stats):
+    st = stats("vit_h_32_float8")
+    pl = P.plan_dp(st, 8, 1)
+    assert pl.messages[0].elements == 632404480
+
+
+def test_dp_bucket_remainder(stats):
+    st = stats("gpt2_l_16_bfloat16")
+    sizes = P._split(st.model_size, 7)
+    assert sum(sizes) == st.model_size and max(sizes) - min(sizes) <= 1
+    assert sizes[0] >= sizes[-1]
+
+
+def test_busbw_factors():
+    assert P.busbw_factor("allreduce", 8) == pytest.approx(1.75)
+    assert P.busbw_factor("allgather", 8) == pytest.approx(0.875)
+    assert P.busbw_factor("sendrecv", 2) == 1.0
+    assert P.busbw_factor("allreduce", 1) == 1.0
+
+
+def test_invalid_layouts(stats):
+    st = stats("llama3_8b_16_bfloat16")
+    with pytest.raises(ValueError):
+        P.plan_fsdp(st, 6, 4, 4)
+    with pytest.raises(ValueError):
+        P.plan_hybrid(st, 8, "hybrid_3d", 3, 4, 2, layers=32)
