@@ -1,0 +1,72 @@
+// Auxiliary subsystems: energy metering, roctx tracing, fault injection.
+//
+// Reference: energy was only a build hook
+// (WITH_ENERGY_PROFILER / WITH_NVML -> -DPROXY_ENERGY_PROFILING, no source
+// consumes it; POWER_SAMPLING_RATE_MS unused, dp.cpp:67) although the plot
+// parser expects a per-rank "energy_consumed" list (plots/parser.py:172);
+// tracing was host MPI timers only; there was no failure handling beyond
+// exit() in check macros and no fault injection. Here:
+//   * EnergyMeter reads the GPU's accumulated energy counter through
+//     libamd_smi (dlopen'd: no link dependency) at iteration boundaries, so
+//     every run reports Joules per rank;
+//   * Tracer emits roctx ranges (libroctx64, dlopen'd) around iterations
+//     and phases when --trace is given, visible with rocprofv3 --marker-trace;
+//   * FaultInjector (DLNB_INJECT_FAULT="rank=R,iter=I,mode=exit|hang|throw")
+//     kills, hangs or fails one rank at one iteration to exercise the
+//     timeout / async-error detection and the launcher's teardown.
+#pragma once
+
+#include <memory>
+#include <string>
+
+namespace dlnb {
+
+class EnergyMeter {
+ public:
+  // device_index: HIP device; returns an inert meter on CPU or when amd-smi
+  // is unavailable (available() == false).
+  static std::unique_ptr<EnergyMeter> open_gpu(int device_index);
+  static std::unique_ptr<EnergyMeter> none();
+  virtual ~EnergyMeter() = default;
+  virtual bool available() const { return false; }
+  virtual double joules() { return 0.0; }  // monotonically increasing counter
+  virtual std::string source() const { return "none"; }
+};
+
+class Tracer {
+ public:
+  static Tracer& get();
+  void enable(bool on);
+  bool enabled() const { return on_; }
+  void push(const char* name);
+  void pop();
+  void mark(const char* name);
+
+ private:
+  bool on_ = false;
+  void* lib_ = nullptr;
+  int (*push_)(const char*) = nullptr;
+  int (*pop_)() = nullptr;
+  void (*mark_)(const char*) = nullptr;
+};
+
+struct TraceRange {
+  explicit TraceRange(const char* n) { Tracer::get().push(n); }
+  ~TraceRange() { Tracer::get().pop(); }
+};
+
+class FaultInjector {
+ public:
+  // Parses DLNB_INJECT_FAULT for this rank.
+  explicit FaultInjector(int rank);
+  // Called at the start of every iteration (warm-up and timed, counted from 0).
+  void at_iteration(long long iter);
+  bool armed() const { return armed_; }
+
+ private:
+  bool armed_ = false;
+  long long iter_ = 0;
+  std::string mode_;
+};
+
+}  // namespace dlnb

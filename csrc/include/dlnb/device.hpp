@@ -73,7 +73,11 @@ class Device {
   virtual std::string name() const = 0;
   virtual int index() const = 0;
   virtual std::unique_ptr<Stream> create_stream(bool high_priority) = 0;
-  virtual std::unique_ptr<Event> create_event() = 0;
+  // timing = false: a dependency-only event (no timestamp, device-scope
+  // release: no L2 writeback / system fence on AMD, which otherwise costs
+  // tens of µs per record after a large GEMM). timing = true: timestamped,
+  // still without the system-scope fence.
+  virtual std::unique_ptr<Event> create_event(bool timing = false) = 0;
   // Milliseconds from a to b; both must have completed.
   virtual double elapsed_ms(Event& a, Event& b) = 0;
   virtual void* raw_alloc(size_t bytes) = 0;

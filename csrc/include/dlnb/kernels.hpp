@@ -43,11 +43,13 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
 
 // Persistent deadline variant (the default stand-in compute): a grid of
 // `grid` blocks (<= one per CU: 128 KiB LDS each) walks the M x N tile space
-// of C = A.B^T round-robin until *stamp_slot + ticks, where *stamp_slot is
-// written by a one-wave stamp kernel enqueued just before on the same stream.
-// Leading dimensions are K, K and N.
+// of C = A.B^T round-robin and stops `ticks` (100 MHz s_memrealtime) after
+// the first block started. The start time is agreed through *slot: the first
+// block of launch `epoch` (1..65535, different from the slot's previous
+// launch) CASes {epoch:16 | t0:48} into it, the others read it. One launch,
+// no separate stamp kernel. Leading dimensions are K, K and N.
 void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
-                      uint64_t* stamp_slot, int grid, void* stream);
+                      uint64_t* slot, uint32_t epoch, int grid, void* stream);
 
 // Elementwise "optimizer" stand-in (SGD-momentum on bf16 shards, fp32 math):
 // p = p - lr * (m = beta*m + g). Used by the optional --optimizer step.

@@ -60,6 +60,7 @@ struct Options {
   bool topology = true;
   bool quiet = false;
   bool silent = false;  // print nothing (library use, e.g. bench.py)
+  bool trace = false;   // roctx ranges around iterations and phases
 };
 
 // Parses argv for the given strategy (argv[0] is the program name). Throws

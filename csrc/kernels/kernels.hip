@@ -162,21 +162,38 @@ __device__ __forceinline__ int xcd_remap(int b, int T) {
 // DEADLINE = false: one launch computes every tile once (grid = tiles).
 // DEADLINE = true : persistent stand-in compute. grid <= resident blocks;
 //   each block walks the tile space round-robin (wrapping) and the whole
-//   grid stops at *t0 + ticks of the 100 MHz s_memrealtime clock, where *t0
-//   was stamped by stamp_kernel right before this launch on the same stream.
-//   The stop decision is made block-uniform with __syncthreads_or once per
-//   K-tile, so every wave leaves the K-loop at the same barrier.
+//   grid stops `ticks` of the 100 MHz s_memrealtime clock after the first
+//   block started (agreed through an epoch-tagged CAS on *slot). Thread 0
+//   decides once per K-tile and publishes the decision through a
+//   double-buffered LDS flag read after the K-tile's barrier, so every wave
+//   leaves the K-loop at the same barrier.
 template <bool FP8, bool DEADLINE>
 __global__ void __launch_bounds__(512, 2)
     gemm_tn_256_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
-                       int K, int lda, int ldb, int ldc, const uint64_t* __restrict__ t0, uint64_t ticks) {
+                       int K, int lda, int ldb, int ldc, uint64_t* __restrict__ slot, uint32_t epoch,
+                       uint64_t ticks) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kStageBytes + 16];
   volatile int* stop_flag = reinterpret_cast<volatile int*>(smem + 2 * kStageBytes);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 2, wn = w & 3;
   const int nt_m = M / kTile, nt_n = N / kTile, T = nt_m * nt_n;
-  uint64_t deadline = 0;
-  if constexpr (DEADLINE) deadline = *t0 + ticks;
+  constexpr uint64_t kMask48 = (1ull << 48) - 1;
+  uint64_t t0 = 0;
+  if constexpr (DEADLINE) {
+    if (tid == 0) {
+      const uint64_t now = __builtin_amdgcn_s_memrealtime() & kMask48;
+      const uint64_t mine = (static_cast<uint64_t>(epoch) << 48) | now;
+      uint64_t cur = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while ((cur >> 48) != epoch) {
+        if (__hip_atomic_compare_exchange_strong(slot, &cur, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          cur = mine;
+          break;
+        }
+      }
+      t0 = cur & kMask48;
+    }
+  }
   for (int round = 0;; ++round) {
   const int b = xcd_remap(DEADLINE ? (blockIdx.x + round * gridDim.x) % T : blockIdx.x, T);
   // Grouped tile order: GROUP row-tiles share their B panels in L2.
@@ -257,7 +274,7 @@ __global__ void __launch_bounds__(512, 2)
     if constexpr (DEADLINE) {
       // Double-buffered flag: written before barrier kt, read after it; the
       // other slot is rewritten only after every wave passed barrier kt+1.
-      if (tid == 0) stop_flag[kt & 1] = __builtin_amdgcn_s_memrealtime() >= deadline;
+      if (tid == 0) stop_flag[kt & 1] = ((__builtin_amdgcn_s_memrealtime() - t0) & kMask48) >= ticks;
       __syncthreads();
       expired = __builtin_amdgcn_readfirstlane(stop_flag[kt & 1]);
     } else {
@@ -285,9 +302,6 @@ __global__ void __launch_bounds__(512, 2)
   }  // round
 }
 
-__global__ void stamp_kernel(uint64_t* slot) {
-  if (threadIdx.x == 0) *slot = __builtin_amdgcn_s_memrealtime();
-}
 
 // ------------------------------------------------------------- optimizer
 
@@ -384,28 +398,27 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
   if (in_t == DType::BF16) {
     hipLaunchKernelGGL((gemm_tn_256_kernel<false, false>), tiles, 512, 0, S(stream), static_cast<const char*>(A),
                        static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc,
-                       static_cast<const uint64_t*>(nullptr), 0ull);
+                       static_cast<uint64_t*>(nullptr), 0u, 0ull);
   } else {
     hipLaunchKernelGGL((gemm_tn_256_kernel<true, false>), tiles, 512, 0, S(stream), static_cast<const char*>(A),
                        static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc,
-                       static_cast<const uint64_t*>(nullptr), 0ull);
+                       static_cast<uint64_t*>(nullptr), 0u, 0ull);
   }
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
 void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
-                      uint64_t* stamp_slot, int grid, void* stream) {
+                      uint64_t* slot, uint32_t epoch, int grid, void* stream) {
   DLNB_REQUIRE(gemm_shape_ok(M, N, K, in_t), "gemm_tn_deadline: unsupported shape");
-  DLNB_REQUIRE(stamp_slot != nullptr && grid > 0, "gemm_tn_deadline: need a stamp slot and a grid");
-  hipLaunchKernelGGL(stamp_kernel, 1, 64, 0, S(stream), stamp_slot);
+  DLNB_REQUIRE(slot != nullptr && grid > 0 && epoch > 0 && epoch < 65536, "gemm_tn_deadline: bad slot/grid/epoch");
   if (in_t == DType::BF16) {
     hipLaunchKernelGGL((gemm_tn_256_kernel<false, true>), grid, 512, 0, S(stream), static_cast<const char*>(A),
                        static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, K, K, N,
-                       static_cast<const uint64_t*>(stamp_slot), ticks);
+                       slot, epoch, ticks);
   } else {
     hipLaunchKernelGGL((gemm_tn_256_kernel<true, true>), grid, 512, 0, S(stream), static_cast<const char*>(A),
                        static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, K, K, N,
-                       static_cast<const uint64_t*>(stamp_slot), ticks);
+                       slot, epoch, ticks);
   }
   DLNB_HIP_CHECK(hipGetLastError());
 }

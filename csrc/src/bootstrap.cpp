@@ -208,6 +208,12 @@ TcpStore::TcpStore(const std::string& host, int port, bool is_server, double tim
         freeaddrinfo(res);
         int one = 1;
         setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+        // A blocking get() gives up after the store timeout: a rank that died
+        // or hangs before a host barrier fails the job instead of hanging it.
+        timeval tv;
+        tv.tv_sec = static_cast<long>(timeout_s_);
+        tv.tv_usec = 0;
+        setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
         fd_ = fd;
         break;
       }
@@ -231,7 +237,9 @@ std::string TcpStore::request(uint8_t op, const std::string& key, const std::str
   write_blob(fd_, key);
   write_blob(fd_, value);
   std::string out;
-  if (!read_blob(fd_, out)) DLNB_THROW("store: connection lost (op " << int(op) << " key " << key << ")");
+  if (!read_blob(fd_, out))
+    DLNB_THROW("store: no reply within " << timeout_s_ << " s or connection lost (op " << int(op) << " key " << key
+                                         << "): a peer rank died or hangs");
   return out;
 }
 

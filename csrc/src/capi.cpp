@@ -76,12 +76,14 @@ int dlnb_gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int
 
 int dlnb_gemm_deadline_us(const void* A, const void* B, void* C, int M, int N, int K, int dtype, double us,
                           int device, void* stamp_slot, int grid, void* stream) {
+  static uint32_t epoch = 0;
   return guard([&] {
+    epoch = epoch % 65535 + 1;
     double hz = dlnb::kernels::wallclock_hz(device);
     if (grid <= 0) grid = dlnb::kernels::num_cus(device);
     dlnb::kernels::gemm_tn_deadline(A, B, C, M, N, K, static_cast<dlnb::DType>(dtype),
                                     static_cast<unsigned long long>(us * 1e-6 * hz), static_cast<uint64_t*>(stamp_slot),
-                                    grid, stream);
+                                    epoch, grid, stream);
   });
 }
 

@@ -109,8 +109,10 @@ class GpuCompute : public ComputeEngine {
         kernels::busy_spin(ticks(d), cus_, s.native());
         return;
       }
-      kernels::gemm_tn_deadline(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, ticks(d), slot_for(s), grid_,
-                                s.native());
+      uint32_t& ep = epoch_[slot_for(s)];
+      ep = ep % 65535 + 1;  // 1..65535, never 0 (a fresh slot reads as epoch 0)
+      kernels::gemm_tn_deadline(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, ticks(d), slot_for(s), ep,
+                                grid_, s.native());
       return;
     }
     if (mode_ == ComputeMode::Flops) {
@@ -186,8 +188,8 @@ class GpuCompute : public ComputeEngine {
     auto s = dev_.create_stream(false);
     dev_.fill_random(A_.data(), static_cast<size_t>(Mmax) * K_, dtype_, 1, *s);
     dev_.fill_random(B_.data(), static_cast<size_t>(N_) * K_, dtype_, 2, *s);
-    auto e0 = dev_.create_event();
-    auto e1 = dev_.create_event();
+    auto e0 = dev_.create_event(true);
+    auto e1 = dev_.create_event(true);
     // Run ~0.3 s first so the measurement sees the sustained (DVFS-settled)
     // clock rather than the cold-start boost.
     for (int i = 0; i < 400; ++i) launch(Mmax, *s);
@@ -219,6 +221,7 @@ class GpuCompute : public ComputeEngine {
   double scale_;
   Buffer slots_;
   std::map<Stream*, size_t> slot_of_;
+  std::map<uint64_t*, uint32_t> epoch_;
   int grid_ = 256;
   double hz_ = 1e8;
   int cus_ = 256;

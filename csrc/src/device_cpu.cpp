@@ -179,7 +179,7 @@ class CpuDevice : public Device {
   std::string name() const override { return "CPU"; }
   int index() const override { return 0; }
   std::unique_ptr<Stream> create_stream(bool) override { return std::unique_ptr<Stream>(new CpuStream()); }
-  std::unique_ptr<Event> create_event() override { return std::unique_ptr<Event>(new CpuEvent()); }
+  std::unique_ptr<Event> create_event(bool) override { return std::unique_ptr<Event>(new CpuEvent()); }
   double elapsed_ms(Event& a, Event& b) override {
     auto* ea = dynamic_cast<CpuEvent*>(&a);
     auto* eb = dynamic_cast<CpuEvent*>(&b);

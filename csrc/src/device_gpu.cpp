@@ -19,7 +19,16 @@ namespace {
 
 class GpuEvent : public Event {
  public:
-  GpuEvent() { DLNB_HIP_CHECK(hipEventCreate(&ev)); }
+  explicit GpuEvent(bool timing) {
+    // Prefer no system-scope fence (newer HIP); older runtimes (e.g. the
+    // ROCm 7.0 HIP bundled with torch) reject the flag: fall back.
+    const unsigned base = timing ? 0u : static_cast<unsigned>(hipEventDisableTiming);
+    if (hipEventCreateWithFlags(&ev, base | hipEventDisableSystemFence) == hipSuccess) return;
+    (void)hipGetLastError();
+    if (hipEventCreateWithFlags(&ev, base | hipEventReleaseToDevice) == hipSuccess) return;
+    (void)hipGetLastError();
+    DLNB_HIP_CHECK(hipEventCreateWithFlags(&ev, base));
+  }
   ~GpuEvent() override { (void)hipEventDestroy(ev); }
   hipEvent_t ev{};
 };
@@ -69,7 +78,7 @@ class GpuDevice : public Device {
   std::unique_ptr<Stream> create_stream(bool high_priority) override {
     return std::unique_ptr<Stream>(new GpuStream(idx_, high_priority));
   }
-  std::unique_ptr<Event> create_event() override { return std::unique_ptr<Event>(new GpuEvent()); }
+  std::unique_ptr<Event> create_event(bool timing) override { return std::unique_ptr<Event>(new GpuEvent(timing)); }
   double elapsed_ms(Event& a, Event& b) override {
     float ms = 0;
     DLNB_HIP_CHECK(hipEventSynchronize(static_cast<GpuEvent&>(b).ev));

@@ -83,7 +83,10 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  --store HOST:PORT      rendezvous store address\n"
      << "  --no-topology          do not print the topology graph\n"
      << "  --quiet                only print the report section\n"
-     << "  --silent               print nothing (the report is returned to the caller)\n";
+     << "  --silent               print nothing (the report is returned to the caller)\n"
+     << "  --trace                emit roctx ranges (rocprofv3 --marker-trace)\n"
+     << "env: DLNB_TIMEOUT (s, hang detection), DLNB_INJECT_FAULT=rank=R,iter=I,mode=exit|hang|throw,\n"
+     << "     DLNB_STORE_ADDR=host:port, DLNB_NO_ENERGY=1\n";
   return os.str();
 }
 
@@ -147,6 +150,8 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
       o.store_addr = val("store");
     } else if (a == "--no-topology") {
       o.topology = false;
+    } else if (a == "--trace") {
+      o.trace = true;
     } else if (a == "--silent") {
       o.silent = o.quiet = true;
       o.topology = false;

@@ -19,6 +19,7 @@
 
 extern char** environ;
 
+#include "dlnb/aux.hpp"
 #include "dlnb/kernels.hpp"
 #include "dlnb/strategy.hpp"
 
@@ -225,8 +226,17 @@ Json run_benchmark(const Options& opt) {
 
   if (opt.topology) print_topology(ctx);
 
+  Tracer::get().enable(opt.trace);
+  std::unique_ptr<EnergyMeter> meter =
+      ctx.dev->kind() == DeviceKind::GPU ? EnergyMeter::open_gpu(ctx.dev->index()) : EnergyMeter::none();
+  FaultInjector fault(ri.rank);
+  long long iter_no = 0;
+
   auto strat = make_strategy(opt.strategy);
-  strat->setup(ctx);
+  {
+    TraceRange tr("dlnb:setup");
+    strat->setup(ctx);
+  }
   TimerSet& T = *strat->timers();
   const char* rkey = strat->runtime_key();
   T.ensure(rkey);
@@ -235,6 +245,8 @@ Json run_benchmark(const Options& opt) {
   // ---- warm-up
   std::vector<double> warm;
   for (int i = 0; i < opt.warmup; ++i) {
+    fault.at_iteration(iter_no++);
+    TraceRange tr("dlnb:warmup_iteration");
     double t0 = now_s();
     strat->enqueue_iteration();
     strat->synchronize();
@@ -261,6 +273,8 @@ Json run_benchmark(const Options& opt) {
     // runs forever unless --max-loop-iters bounds it.
     T.set_enabled(false);
     for (long long it = 0; opt.max_loop_iters == 0 || it < opt.max_loop_iters; ++it) {
+      fault.at_iteration(iter_no++);
+      TraceRange tr("dlnb:loop_iteration");
       strat->enqueue_iteration();
       strat->synchronize();
     }
@@ -274,10 +288,14 @@ Json run_benchmark(const Options& opt) {
   ctx.dev->synchronize();
   const double T0 = now_s();
   for (int r = 0; r < runs; ++r) {
+    fault.at_iteration(iter_no++);
+    TraceRange tr("dlnb:iteration");
+    const double j0 = meter->joules();
     double t0 = now_s();
     strat->enqueue_iteration();
     strat->synchronize();
     T.add(rkey, now_s() - t0);
+    if (meter->available()) T.add("energy_consumed", meter->joules() - j0);
   }
   ctx.dev->synchronize();
   ctx.hg().barrier();
@@ -285,6 +303,7 @@ Json run_benchmark(const Options& opt) {
 
   // ---- report
   Json rank = strat->rank_json();
+  rank["energy_consumed"] = T.values_json("energy_consumed");
   rank["hostname"] = ri.hostname;
   rank["rank"] = ri.rank;
   rank["local_rank"] = ri.local_rank;
@@ -306,6 +325,7 @@ Json run_benchmark(const Options& opt) {
   ext["runs"] = runs;
   ext["warmup_times"] = Json(warm);
   ext["timed_region_s"] = timed_region;
+  ext["energy_source"] = meter->source();
   {
     // Collective-library knobs of this run (the reference recorded them as
     // SbatchMan job variables, plots/parser.py:151-154).

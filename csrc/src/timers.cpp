@@ -4,7 +4,7 @@ namespace dlnb {
 
 int TimerSet::begin(Stream& s) {
   if (!enabled_) return -1;
-  if (next_ == pool_.size()) pool_.push_back(dev_.create_event());
+  if (next_ == pool_.size()) pool_.push_back(dev_.create_event(true));
   int idx = static_cast<int>(next_++);
   s.record(*pool_[static_cast<size_t>(idx)]);
   return idx;
@@ -12,7 +12,7 @@ int TimerSet::begin(Stream& s) {
 
 void TimerSet::end(int token, Stream& s, const std::string& name) {
   if (!enabled_ || token < 0) return;
-  if (next_ == pool_.size()) pool_.push_back(dev_.create_event());
+  if (next_ == pool_.size()) pool_.push_back(dev_.create_event(true));
   int idx = static_cast<int>(next_++);
   s.record(*pool_[static_cast<size_t>(idx)]);
   pending_.push_back(Pending{token, idx, name});

@@ -27,6 +27,16 @@ for step in "$@"; do
     prof)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       run prof_fsdp 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_fsdp -o fsdp -- python3 bench.py --steps 1 --warmup 1 ;;
+    gemmbench)
+      run gemmbench_bf16 300 python -m dlnetbench_amd.tools.gemm_bench --dtype bf16
+      run gemmbench_fp8 300 python -m dlnetbench_amd.tools.gemm_bench --dtype fp8 --shapes 4096x4096x4096,8192x8192x8192,8192x14336x4096 ;;
+    pmcfsdp)
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      run pmc_fsdp 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_fsdp -o fsdp -- python3 bench.py --steps 1 --warmup 0 ;;
+    pmc)
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      run pmc_gemm 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_gemm -o gemm -- python3 -m dlnetbench_amd.tools.gemm_bench --shapes 8192x14336x4096 --rounds 2 --iters 5 ;;
+    dp8) run bench_dp 300 python -m dlnetbench_amd.tools.sweep --quick ;;
     *) echo "unknown step $step" >> gpurun_out/steps.log ;;
   esac
 done

@@ -1,0 +1,127 @@
+"""Tooling: sweep checkpoint/resume, report parsing to DataFrames, plots,
+fault injection / failure detection, CLI contract of the binaries."""
+import json
+import os
+import subprocess
+
+import pytest
+
+from dlnetbench_amd.tools import plots, sweep
+from dlnetbench_amd.utils import launch, report
+
+
+@pytest.fixture(scope="module")
+def bindir(root):
+    d = os.path.join(root, "build", "bin")
+    if not os.path.exists(os.path.join(d, "dp")):
+        pytest.skip("binaries not built")
+    return d
+
+
+def test_sweep_runs_and_resumes(tmp_path, bindir):
+    out = tmp_path / "r.jsonl"
+    assert sweep.main(["--quick", "--out", str(out), "--bin", bindir]) == 0
+    lines = out.read_text().splitlines()
+    assert len(lines) == 4
+    recs = [json.loads(l) for l in lines]
+    assert all(r["exit_code"] == 0 and r["summary"]["median_ms"] > 0 for r in recs)
+    # resume: nothing left to do
+    assert sweep.main(["--quick", "--out", str(out), "--bin", bindir]) == 0
+    assert len(out.read_text().splitlines()) == 4
+    # partial file -> only the missing points run again
+    out.write_text("\n".join(lines[:2]) + "\n")
+    assert sweep.main(["--quick", "--out", str(out), "--bin", bindir]) == 0
+    keys = [json.loads(l)["key"] for l in out.read_text().splitlines()]
+    assert len(keys) == 4 and len(set(keys)) == 4
+
+
+def test_sweep_expansion_env_matrix():
+    spec = {"points": [{"strategy": "fsdp", "model": "m", "params": [4, "W"], "world": [2, 4],
+                        "env": {"NCCL_PROTO": ["Simple", "LL128"], "NCCL_ALGO": "Ring"}}]}
+    pts = list(sweep.expand(spec))
+    assert len(pts) == 4
+    assert {tuple(p["params"]) for p in pts} == {(4, 2), (4, 4)}
+    assert len({sweep.point_key(p) for p in pts}) == 4
+
+
+def test_report_dataframes(tmp_path, bindir, data_dir):
+    code, outs = launch.launch(2, [os.path.join(bindir, "fsdp"), "tiny_dense_8_bfloat16", "4", "2", data_dir,
+                                   "--quiet", "-w", "1", "-r", "2"], timeout=60, capture=True)
+    assert code == 0
+    doc = report.parse_output(outs[0])["fsdp"]
+    assert report.validate(doc, expected_world=2, nodes=1) == []
+    assert report.validate(doc, expected_world=4) != []
+    rt, comm = report.fsdp_dataframes(doc)
+    assert len(rt) == 2 * 2 and len(comm) == 2 * 2 * 4
+    assert set(["runtime", "allgather", "barrier", "rank"]) <= set(rt.columns)
+    assert set(["allgather_wait_fwd", "allgather_wait_bwd", "reduce_scatter", "unit_idx"]) <= set(comm.columns)
+    code, outs = launch.launch(2, [os.path.join(bindir, "dp"), "tiny_dense_8_bfloat16", "3", data_dir, "--quiet",
+                                   "-w", "0", "-r", "3"], timeout=60, capture=True, env=dict(os.environ, NCCL_PROTO="Simple"))
+    doc = report.parse_output(outs[0])["dp"]
+    df = report.dp_dataframe(doc)
+    assert len(df) == 6 and (df["protocol"] == "Simple").all()
+    assert {"runtime", "barrier_time", "energy_consumed", "msg_size_avg_bytes"} <= set(df.columns)
+    s = report.summary(doc)
+    assert s["busbw_GBps"]["allreduce"] > 0
+
+
+def test_plots(tmp_path, bindir):
+    out = tmp_path / "r.jsonl"
+    sweep.main(["--quick", "--out", str(out), "--bin", bindir])
+    for kind in ("scaling", "barrier", "pareto"):
+        png = tmp_path / f"{kind}.png"
+        assert plots.main([kind, str(out), "-o", str(png)]) == 0
+        assert png.exists() and png.stat().st_size > 1000
+
+
+def test_plot_utils():
+    assert plots.format_bytes(1536) == "1.5 KiB"
+    assert plots.format_bytes(512) == "512 B"
+    assert plots.parse_bytes("1.5 KiB") == 1536
+    assert plots.parse_bytes("2GB") == 2_000_000_000
+    pts = [(1, 5), (2, 3), (3, 4), (4, 1), (2.5, 2.9)]
+    assert plots.pareto_front(pts) == [0, 1, 4, 3]
+
+
+@pytest.mark.parametrize("mode,code", [("exit", 42), ("throw", 2), ("hang", 17)])
+def test_fault_injection_is_detected(mode, code, bindir, data_dir):
+    env = dict(os.environ, DLNB_INJECT_FAULT=f"rank=1,iter=1,mode={mode}", DLNB_TIMEOUT="5")
+    rc, outs = launch.launch(2, [os.path.join(bindir, "dp"), "tiny_dense_8_bfloat16", "2", data_dir, "--quiet",
+                                 "-w", "2", "-r", "2"], timeout=90, capture=True, env=env)
+    text = "".join(o or "" for o in outs)
+    assert rc == code, text[-2000:]
+    assert "DLNB_INJECT_FAULT" in text
+
+
+def test_cli_contract(bindir, data_dir):
+    r = subprocess.run([os.path.join(bindir, "dp"), "-h"], capture_output=True, text=True)
+    assert r.returncode == 0 and "<model> <num_buckets> <base_path>" in r.stdout
+    r = subprocess.run([os.path.join(bindir, "hybrid_3d"), "-h"], capture_output=True, text=True)
+    assert "<num_tensor_shards>" in r.stdout and "default 3" in r.stdout
+    r = subprocess.run([os.path.join(bindir, "fsdp"), "m", "4"], capture_output=True, text=True)
+    assert r.returncode == 1 and "expected 4 positional" in r.stderr
+    r = subprocess.run([os.path.join(bindir, "dp"), "m", "x", "."], capture_output=True, text=True)
+    assert r.returncode == 1 and "invalid integer" in r.stderr
+    r = subprocess.run([os.path.join(bindir, "dp"), "nope_1_bfloat16", "2", data_dir, "--quiet"],
+                       capture_output=True, text=True)
+    assert r.returncode == 2 and "does not exist" in r.stderr
+    r = subprocess.run([os.path.join(bindir, "dlnb"), "fsdp", "-h"], capture_output=True, text=True)
+    assert r.returncode == 0 and "<sharding_factor>" in r.stdout
+
+
+def test_topology_print(bindir, data_dir):
+    code, outs = launch.launch(2, [os.path.join(bindir, "dp"), "tiny_dense_8_bfloat16", "2", data_dir, "-w", "0",
+                                   "-r", "1"], timeout=60, capture=True)
+    assert code == 0
+    assert "=== topology: 2 ranks on 1 node(s) ===" in outs[0]
+    env = dict(os.environ, SLURM_TOPOLOGY_ADDR="root.sw1.nodeA")
+    code, outs = launch.launch(2, [os.path.join(bindir, "dp"), "tiny_dense_8_bfloat16", "2", data_dir, "-w", "0",
+                                   "-r", "1"], timeout=60, capture=True, env=env)
+    assert "sw1" in outs[0] and "ranks [0,1]" in outs[0]
+
+
+def test_plan_cli(capsys, root):
+    from dlnetbench_amd.parallel import plan
+    assert plan.main(["hybrid_3d", "llama3_70b_16_bfloat16", "2", "4", "4", "--world", "8", "--base", root]) == 0
+    d = json.loads(capsys.readouterr().out)
+    assert d["params"]["num_tensor_shards"] == 4
