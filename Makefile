@@ -24,7 +24,7 @@ LOOPS    := dp_loop fsdp_loop hybrid_2d_loop hybrid_3d_loop hybrid_3d_moe_loop
 LIB      := $(BUILD)/libdlnb.so
 PYLIB    := dlnetbench_amd/_lib/libdlnb.so
 
-.PHONY: all lib apps clean
+.PHONY: all lib apps clean asan
 all: lib apps
 
 lib: $(PYLIB)
@@ -51,5 +51,11 @@ $(BUILD)/bin/%: csrc/apps/%.cpp $(LIB)
 $(BUILD)/bin/%_loop: $(BUILD)/bin/%
 	ln -sf $(notdir $<) $@
 
+# Host AddressSanitizer build of the library + binaries into build-asan/
+# (device code is not instrumented: GPU ASan is not available on the pool).
+asan:
+	$(MAKE) BUILD=build-asan OPT="-O1 -g -fno-omit-frame-pointer -Xarch_host -fsanitize=address" \
+	  LDLIBS="$(LDLIBS) -fsanitize=address" PYLIB=build-asan/unused.so apps
+
 clean:
-	rm -rf $(BUILD) $(PYLIB)
+	rm -rf $(BUILD) build-asan $(PYLIB)

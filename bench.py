@@ -16,7 +16,7 @@ Prints one JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
-import datetime
+import time
 import json
 import os
 import sys
@@ -32,28 +32,40 @@ BASELINE_MS = 2814.74976
 
 
 def _store_addr(world: int, rank: int) -> str:
-    """Rendezvous for the native runtime's TCP store under torchrun: rank 0
-    binds an ephemeral port and publishes it through torchrun's own store."""
+    """Address of the native runtime's TCP rendezvous store under torchrun.
+
+    Single node (the bench's case): rank 0 binds an ephemeral port and
+    publishes it in a file named after torchrun's MASTER_PORT/run id; the
+    other local ranks poll that file. Multi-node: MASTER_PORT + 1."""
     if world == 1:
         return ""
     host = os.environ.get("MASTER_ADDR", "127.0.0.1")
     port = int(os.environ.get("MASTER_PORT", "29500"))
-    try:
-        import torch.distributed as dist
-        store = dist.TCPStore(host, port, world, is_master=False, timeout=datetime.timedelta(seconds=120))
-        key = "dlnb_bench_store_port"
-        if rank == 0:
-            import socket
-            with socket.socket() as s:
-                s.bind(("", 0))
-                p = s.getsockname()[1]
-            store.set(key, str(p))
-        else:
-            p = int(store.get(key).decode())
-        return f"{host}:{p}"
-    except Exception as e:  # not under torchrun's agent store
-        print(f"[bench] torchrun store unavailable ({e}); using MASTER_PORT+1", file=sys.stderr)
+    if int(os.environ.get("LOCAL_WORLD_SIZE", world)) != world:
         return f"{host}:{port + 1}"
+    run_id = os.environ.get("TORCHELASTIC_RUN_ID", "none")
+    path = f"/tmp/dlnb_bench_store_{port}_{run_id}"
+    if rank == 0:
+        import socket
+        with socket.socket() as s:
+            s.bind(("", 0))
+            p = s.getsockname()[1]
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(str(p))
+        os.replace(tmp, path)
+        return f"127.0.0.1:{p}"
+    deadline = time.time() + 300
+    while time.time() < deadline:
+        try:
+            with open(path) as f:
+                txt = f.read().strip()
+            if txt:
+                return f"127.0.0.1:{int(txt)}"
+        except (OSError, ValueError):
+            pass
+        time.sleep(0.05)
+    raise RuntimeError(f"rank {rank}: no store address in {path}")
 
 
 def main() -> int:
@@ -74,9 +86,13 @@ def main() -> int:
     if world != a.gpus:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # Everything below is native (HIP + RCCL from /opt/rocm); torch is not needed.
+    os.environ.setdefault("DLNB_NO_TORCH", "1")
     addr = _store_addr(world, rank)
 
     from dlnetbench_amd import engine
+    from dlnetbench_amd.utils.stats import load_stats
+    st = load_stats(os.path.join(ROOT, "model_stats", a.model + ".txt"))
     doc = engine.run("fsdp", a.model, a.units, world, base_path=ROOT, warmup=a.warmup, runs=a.steps,
                      compute=a.compute, schedule=a.schedule, backend=a.backend, wire_dtype="bf16",
                      store=addr or None, silent=True, json=a.json)
@@ -108,7 +124,7 @@ def main() -> int:
         "config": {
             "model": a.model,
             "global_batch": int(g["local_batch_size"]) * world,
-            "seq_len": 8192,
+            "seq_len": st.seq_len,
             "parallelism": f"fsdp{world}",
             "num_units": g["num_units"],
             "sharding_factor": g["sharding_factor"],

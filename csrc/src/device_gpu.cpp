@@ -20,14 +20,10 @@ namespace {
 class GpuEvent : public Event {
  public:
   explicit GpuEvent(bool timing) {
-    // Prefer no system-scope fence (newer HIP); older runtimes (e.g. the
-    // ROCm 7.0 HIP bundled with torch) reject the flag: fall back.
-    const unsigned base = timing ? 0u : static_cast<unsigned>(hipEventDisableTiming);
-    if (hipEventCreateWithFlags(&ev, base | hipEventDisableSystemFence) == hipSuccess) return;
-    (void)hipGetLastError();
-    if (hipEventCreateWithFlags(&ev, base | hipEventReleaseToDevice) == hipSuccess) return;
-    (void)hipGetLastError();
-    DLNB_HIP_CHECK(hipEventCreateWithFlags(&ev, base));
+    // Dependency-only events skip the timestamp. (hipEventDisableSystemFence
+    // is rejected by hipEventCreateWithFlags on ROCm 7.0 and 7.2 alike, so
+    // the default release scope is kept.)
+    DLNB_HIP_CHECK(hipEventCreateWithFlags(&ev, timing ? hipEventDefault : hipEventDisableTiming));
   }
   ~GpuEvent() override { (void)hipEventDestroy(ev); }
   hipEvent_t ev{};

@@ -5,7 +5,9 @@ travels with the repository. torch (when installed) is imported *first*: its
 wheel bundles libamdhip64.so / librccl.so with the same sonames as
 /opt/rocm, and loading torch first makes the dynamic loader resolve our
 library's HIP/RCCL dependencies to the already-loaded copies, so one process
-never ends up with two HIP runtimes.
+never ends up with two HIP runtimes. DLNB_NO_TORCH=1 skips that import (the
+process then runs entirely on /opt/rocm's HIP and RCCL, like the CLI binaries;
+do not import torch afterwards in such a process).
 """
 from __future__ import annotations
 
@@ -29,10 +31,11 @@ def lib() -> ctypes.CDLL:
     global _LIB
     if _LIB is not None:
         return _LIB
-    try:  # see module docstring
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    if os.environ.get("DLNB_NO_TORCH", "0") != "1":
+        try:  # see module docstring
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     if not os.path.exists(LIB_PATH):
         raise NativeError(f"{LIB_PATH} is missing: build it with `make` (or __graft_entry__.build())")
     L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)

@@ -20,3 +20,12 @@ def root():
 @pytest.fixture(scope="session")
 def data_dir():
     return os.path.join(ROOT, "tests", "data")
+
+
+def pytest_sessionstart(session):
+    """Build the native library and binaries if this checkout has not been built."""
+    import subprocess
+    need = [os.path.join(ROOT, "dlnetbench_amd", "_lib", "libdlnb.so"), os.path.join(ROOT, "build", "bin", "dp")]
+    if not all(os.path.exists(p) for p in need):
+        subprocess.run(["make", "-C", ROOT, f"-j{min(16, os.cpu_count() or 4)}"], check=True,
+                       stdout=subprocess.DEVNULL)

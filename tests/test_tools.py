@@ -125,3 +125,18 @@ def test_plan_cli(capsys, root):
     assert plan.main(["hybrid_3d", "llama3_70b_16_bfloat16", "2", "4", "4", "--world", "8", "--base", root]) == 0
     d = json.loads(capsys.readouterr().out)
     assert d["params"]["num_tensor_shards"] == 4
+
+
+@pytest.mark.parametrize("prog,args", [("fsdp", ["tiny_dense_8_bfloat16", "4", "2"]),
+                                       ("hybrid_3d_moe", ["tiny_moe_8_bfloat16", "2", "2", "1"]),
+                                       ("hybrid_3d", ["tiny_dense_8_bfloat16", "2", "2", "1"])])
+def test_asan_build_is_clean(prog, args, root, data_dir):
+    """Host AddressSanitizer build (make asan): no memory errors in the runtime."""
+    b = os.path.join(root, "build-asan", "bin", prog)
+    if not os.path.exists(b):
+        pytest.skip("make asan not built")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1")
+    code, outs = launch.launch(2, [b, *args, data_dir, "--quiet", "-w", "1", "-r", "2"], timeout=120,
+                               capture=True, env=env)
+    text = "".join(o or "" for o in outs)
+    assert code == 0 and "AddressSanitizer" not in text, text[-3000:]
