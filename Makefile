@@ -31,7 +31,10 @@ lib: $(PYLIB)
 
 $(BUILD)/obj/%.o: csrc/%
 	@mkdir -p $(dir $@)
-	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+	$(HIPCC) $(CXXFLAGS) -MMD -MP -c $< -o $@
+
+# header dependencies (every object is rebuilt when a header it includes changes)
+-include $(LIB_OBJS:.o=.d)
 
 $(LIB): $(LIB_OBJS)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ $(LDLIBS) -Wl,-soname,libdlnb.so
@@ -42,7 +45,7 @@ $(PYLIB): $(LIB)
 
 apps: $(addprefix $(BUILD)/bin/,$(APPS)) $(addprefix $(BUILD)/bin/,$(LOOPS))
 
-$(BUILD)/bin/%: csrc/apps/%.cpp $(LIB)
+$(BUILD)/bin/%: csrc/apps/%.cpp $(LIB) $(wildcard csrc/include/dlnb/*.hpp)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(CXXFLAGS) $< -o $@ -L$(BUILD) -ldlnb $(LDLIBS) -Wl,-rpath,'$$ORIGIN/..'
 
