@@ -43,8 +43,10 @@ def _store_addr(world: int, rank: int) -> str:
     port = int(os.environ.get("MASTER_PORT", "29500"))
     if int(os.environ.get("LOCAL_WORLD_SIZE", world)) != world:
         return f"{host}:{port + 1}"
-    run_id = os.environ.get("TORCHELASTIC_RUN_ID", "none")
-    path = f"/tmp/dlnb_bench_store_{port}_{run_id}"
+    # All local workers of one torchrun job share the launcher (the elastic
+    # agent) as parent process: its pid makes the file unique per job, so a
+    # stale file from an earlier job on the same port is never read.
+    path = f"/tmp/dlnb_bench_store_{port}_{os.getppid()}"
     if rank == 0:
         import socket
         with socket.socket() as s:
@@ -54,6 +56,8 @@ def _store_addr(world: int, rank: int) -> str:
         with open(tmp, "w") as f:
             f.write(str(p))
         os.replace(tmp, path)
+        import atexit
+        atexit.register(lambda: os.path.exists(path) and os.remove(path))
         return f"127.0.0.1:{p}"
     deadline = time.time() + 300
     while time.time() < deadline:

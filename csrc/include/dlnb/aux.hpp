@@ -6,9 +6,10 @@
 // parser expects a per-rank "energy_consumed" list (plots/parser.py:172);
 // tracing was host MPI timers only; there was no failure handling beyond
 // exit() in check macros and no fault injection. Here:
-//   * EnergyMeter reads the GPU's accumulated energy counter through
-//     libamd_smi (dlopen'd: no link dependency) at iteration boundaries, so
-//     every run reports Joules per rank;
+//   * EnergyMeter reads the GPU's energy at iteration boundaries so every
+//     run reports Joules per rank: hwmon sysfs (energy counter, or power
+//     sampled every 5 ms and integrated) by default, amd-smi's accumulated
+//     energy counter with DLNB_ENERGY=amdsmi;
 //   * Tracer emits roctx ranges (libroctx64, dlopen'd) around iterations
 //     and phases when --trace is given, visible with rocprofv3 --marker-trace;
 //   * FaultInjector (DLNB_INJECT_FAULT="rank=R,iter=I,mode=exit|hang|throw")

@@ -40,6 +40,7 @@ struct ComputeShape {
   int hidden = 4096;  // model hidden size (K of the stand-in GEMM)
   int ffn = 16384;    // FFN width (N)
   DType dtype = DType::BF16;
+  int comm_cus = 32;  // CUs the persistent compute leaves to collectives
 };
 
 class ComputeEngine {

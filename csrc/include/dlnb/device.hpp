@@ -90,6 +90,13 @@ class Device {
   // Enqueue a host callback (CPU: task on the worker; GPU: hipLaunchHostFunc).
   virtual void host_task(Stream& s, std::function<void()> fn) = 0;
   virtual void synchronize() = 0;
+  // Timestamps taken when a stream reaches a point (device clock on GPU: a
+  // one-wave kernel stores s_memrealtime into host-mapped memory; host clock
+  // on CPU). Unlike timing events they are exact across cross-stream waits.
+  virtual uint64_t* alloc_stamps(size_t n) = 0;  // zeroed, host-readable
+  virtual void free_stamps(uint64_t* p, size_t n) = 0;
+  virtual void stamp(Stream& s, uint64_t* slot) = 0;
+  virtual double stamp_hz() const = 0;
   virtual size_t total_memory() const = 0;
   virtual size_t free_memory() const = 0;
 

@@ -32,6 +32,9 @@ void fill_random(void* p, size_t count, DType t, uint64_t seed, void* stream);
 void idle_wait(uint64_t ticks, void* stream);
 void busy_spin(uint64_t ticks, int blocks, void* stream);
 double wallclock_hz(int device);
+// One wave stores s_memrealtime into *slot (host-mapped memory) when the
+// stream reaches this point.
+void stamp(uint64_t* slot, void* stream);
 int num_cus(int device);
 
 // GEMM: requires M % 256 == 0, N % 256 == 0, K*elem_size % 128 == 0, leading
@@ -43,13 +46,16 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
 
 // Persistent deadline variant (the default stand-in compute): a grid of
 // `grid` blocks (<= one per CU: 128 KiB LDS each) walks the M x N tile space
-// of C = A.B^T round-robin and stops `ticks` (100 MHz s_memrealtime) after
-// the first block started. The start time is agreed through *slot: the first
-// block of launch `epoch` (1..65535, different from the slot's previous
-// launch) CASes {epoch:16 | t0:48} into it, the others read it. One launch,
-// no separate stamp kernel. Leading dimensions are K, K and N.
+// of C = A.B^T round-robin and stops min(ticks, slice_end) (100 MHz
+// s_memrealtime) after t0. t0 is agreed through *slot: the first block of the
+// first launch of `epoch` (1..65535, different from the slot's previous task)
+// CASes {epoch:16 | t0:48} into it; every other block and every later launch
+// with the same epoch reads it. A long task is issued as several launches
+// (slices) with increasing slice_end so that collectives on other streams get
+// CUs at slice boundaries, as they do between a training step's kernels.
+// Leading dimensions are K, K and N.
 void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
-                      uint64_t* slot, uint32_t epoch, int grid, void* stream);
+                      uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end = 0);
 
 // Elementwise "optimizer" stand-in (SGD-momentum on bf16 shards, fp32 math):
 // p = p - lr * (m = beta*m + g). Used by the optional --optimizer step.

@@ -61,6 +61,7 @@ struct Options {
   bool quiet = false;
   bool silent = false;  // print nothing (library use, e.g. bench.py)
   bool trace = false;   // roctx ranges around iterations and phases
+  int comm_cus = 32;    // CUs left free by the persistent compute for collectives
 };
 
 // Parses argv for the given strategy (argv[0] is the program name). Throws

@@ -4,9 +4,13 @@
 // Reference: ccutils CCUTILS_MPI_TIMER_DEF/START/STOP host timers whose
 // std::vector<float> __timer_vals_<name> are dumped into the JSON sections
 // (cpp/data_parallel/dp.cpp:69-70,102-104,260-263; fsdp.cpp:61-66). Here a
-// "device" timer is a pair of events on a stream, so it measures the time the
-// stream spent in an operation (a collective's duration on its comm stream,
-// or the compute stream's stall waiting for a collective = exposed comm).
+// "device" timer is a pair of timestamps taken when a stream reaches two
+// points (Device::stamp: a one-wave s_memrealtime kernel on the GPU), so it
+// measures the time the stream spent in an operation (a collective's
+// duration on its comm stream, or the compute stream's stall waiting for a
+// collective = exposed comm). HIP timing events are not used for this: on
+// ROCm 7.2 an event recorded right after a cross-stream wait can carry the
+// timestamp of the wait's start.
 #pragma once
 
 #include <map>
@@ -21,7 +25,10 @@ namespace dlnb {
 
 class TimerSet {
  public:
-  explicit TimerSet(Device& dev) : dev_(dev) {}
+  explicit TimerSet(Device& dev);
+  ~TimerSet();
+  TimerSet(const TimerSet&) = delete;
+  TimerSet& operator=(const TimerSet&) = delete;
   int begin(Stream& s);
   void end(int token, Stream& s, const std::string& name);
   // Time the stall of stream s waiting for event e (exposed latency).
@@ -39,7 +46,8 @@ class TimerSet {
 
  private:
   Device& dev_;
-  std::vector<std::unique_ptr<Event>> pool_;
+  uint64_t* stamps_ = nullptr;  // host-readable timestamp slots
+  size_t cap_ = 0;
   size_t next_ = 0;
   struct Pending {
     int a, b;

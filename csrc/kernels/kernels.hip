@@ -103,6 +103,13 @@ __global__ void idle_wait_kernel(uint64_t ticks) {
   while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
 
+__global__ void stamp_kernel(uint64_t* slot) {
+  if (threadIdx.x == 0) {
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    __hip_atomic_store(slot, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 __global__ void __launch_bounds__(256) busy_spin_kernel(uint64_t ticks, float* sink) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   float x = static_cast<float>(threadIdx.x) * 1e-3f, y = 0.999f;
@@ -162,8 +169,11 @@ __device__ __forceinline__ int xcd_remap(int b, int T) {
 // DEADLINE = false: one launch computes every tile once (grid = tiles).
 // DEADLINE = true : persistent stand-in compute. grid <= resident blocks;
 //   each block walks the tile space round-robin (wrapping) and the whole
-//   grid stops `ticks` of the 100 MHz s_memrealtime clock after the first
-//   block started (agreed through an epoch-tagged CAS on *slot). Thread 0
+//   grid stops `min(ticks, slice_end)` of the 100 MHz s_memrealtime clock
+//   after t0, the time the first block of the first launch of this epoch
+//   started (agreed through an epoch-tagged CAS on *slot; later launches of
+//   the same epoch reuse t0, so a task cut into slices keeps one absolute
+//   deadline however late a slice starts). Thread 0
 //   decides once per K-tile and publishes the decision through a
 //   double-buffered LDS flag read after the K-tile's barrier, so every wave
 //   leaves the K-loop at the same barrier.
@@ -171,7 +181,7 @@ template <bool FP8, bool DEADLINE>
 __global__ void __launch_bounds__(512, 2)
     gemm_tn_256_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
                        int K, int lda, int ldb, int ldc, uint64_t* __restrict__ slot, uint32_t epoch,
-                       uint64_t ticks) {
+                       uint64_t ticks, uint64_t slice_end) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kStageBytes + 16];
   volatile int* stop_flag = reinterpret_cast<volatile int*>(smem + 2 * kStageBytes);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -274,7 +284,10 @@ __global__ void __launch_bounds__(512, 2)
     if constexpr (DEADLINE) {
       // Double-buffered flag: written before barrier kt, read after it; the
       // other slot is rewritten only after every wave passed barrier kt+1.
-      if (tid == 0) stop_flag[kt & 1] = ((__builtin_amdgcn_s_memrealtime() - t0) & kMask48) >= ticks;
+      if (tid == 0) {
+        const uint64_t el = (__builtin_amdgcn_s_memrealtime() - t0) & kMask48;
+        stop_flag[kt & 1] = el >= ticks || el >= slice_end;
+      }
       __syncthreads();
       expired = __builtin_amdgcn_readfirstlane(stop_flag[kt & 1]);
     } else {
@@ -360,6 +373,11 @@ void idle_wait(uint64_t ticks, void* stream) {
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
+void stamp(uint64_t* slot, void* stream) {
+  hipLaunchKernelGGL(stamp_kernel, 1, 64, 0, S(stream), slot);
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
 void busy_spin(uint64_t ticks, int blocks, void* stream) {
   hipLaunchKernelGGL(busy_spin_kernel, blocks, 256, 0, S(stream), ticks, static_cast<float*>(nullptr));
   DLNB_HIP_CHECK(hipGetLastError());
@@ -398,27 +416,28 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
   if (in_t == DType::BF16) {
     hipLaunchKernelGGL((gemm_tn_256_kernel<false, false>), tiles, 512, 0, S(stream), static_cast<const char*>(A),
                        static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc,
-                       static_cast<uint64_t*>(nullptr), 0u, 0ull);
+                       static_cast<uint64_t*>(nullptr), 0u, 0ull, 0ull);
   } else {
     hipLaunchKernelGGL((gemm_tn_256_kernel<true, false>), tiles, 512, 0, S(stream), static_cast<const char*>(A),
                        static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc,
-                       static_cast<uint64_t*>(nullptr), 0u, 0ull);
+                       static_cast<uint64_t*>(nullptr), 0u, 0ull, 0ull);
   }
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
 void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
-                      uint64_t* slot, uint32_t epoch, int grid, void* stream) {
+                      uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end) {
+  if (slice_end == 0) slice_end = ticks;
   DLNB_REQUIRE(gemm_shape_ok(M, N, K, in_t), "gemm_tn_deadline: unsupported shape");
   DLNB_REQUIRE(slot != nullptr && grid > 0 && epoch > 0 && epoch < 65536, "gemm_tn_deadline: bad slot/grid/epoch");
   if (in_t == DType::BF16) {
     hipLaunchKernelGGL((gemm_tn_256_kernel<false, true>), grid, 512, 0, S(stream), static_cast<const char*>(A),
                        static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, K, K, N,
-                       slot, epoch, ticks);
+                       slot, epoch, ticks, slice_end);
   } else {
     hipLaunchKernelGGL((gemm_tn_256_kernel<true, true>), grid, 512, 0, S(stream), static_cast<const char*>(A),
                        static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, K, K, N,
-                       slot, epoch, ticks);
+                       slot, epoch, ticks, slice_end);
   }
   DLNB_HIP_CHECK(hipGetLastError());
 }

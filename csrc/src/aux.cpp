@@ -1,9 +1,12 @@
 #include "dlnb/aux.hpp"
 
+#include <dirent.h>
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <unistd.h>
 
+#include <atomic>
+#include <cctype>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -42,8 +45,10 @@ class AmdSmiMeter : public EnergyMeter {
     auto init = reinterpret_cast<smi_init_t>(dlsym(lib_, "amdsmi_init"));
     auto from_bdf = reinterpret_cast<smi_from_bdf_t>(dlsym(lib_, "amdsmi_get_processor_handle_from_bdf"));
     energy_ = reinterpret_cast<smi_energy_t>(dlsym(lib_, "amdsmi_get_energy_count"));
+    shut_ = reinterpret_cast<int (*)()>(dlsym(lib_, "amdsmi_shut_down"));
     if (!init || !from_bdf || !energy_) return false;
     if (init(kInitAmdGpus) != 0) return false;
+    inited_ = true;
     char bus[64] = {0};
     if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) return false;
     unsigned dom = 0, b = 0, d = 0, fn = 0;
@@ -61,6 +66,9 @@ class AmdSmiMeter : public EnergyMeter {
     bus_ = bus;
     return true;
   }
+  ~AmdSmiMeter() override {
+    if (inited_ && shut_) shut_();
+  }
   bool available() const override { return true; }
   double joules() override {
     uint64_t acc = 0, ts = 0;
@@ -74,7 +82,94 @@ class AmdSmiMeter : public EnergyMeter {
   void* lib_ = nullptr;
   smi_handle h_ = nullptr;
   smi_energy_t energy_ = nullptr;
+  int (*shut_)() = nullptr;
+  bool inited_ = false;
   std::string bus_;
+};
+
+// hwmon sysfs: energy1_input (µJ counter) when the driver exposes it, else
+// power1_average / power1_input (µW) integrated by a 5 ms sampling thread
+// (the reference's POWER_SAMPLING_RATE_MS, dp.cpp:67). No library is loaded,
+// so nothing interferes with the HIP runtime's teardown (amd-smi does: a
+// process that initialised it aborts with a heap error at exit on ROCm 7.2).
+class HwmonMeter : public EnergyMeter {
+ public:
+  bool init(int dev) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) return false;
+    std::string b = bus;
+    for (auto& c : b) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+    std::string base = "/sys/bus/pci/devices/" + b + "/hwmon";
+    DIR* d = opendir(base.c_str());
+    if (!d) return false;
+    std::string hw;
+    while (dirent* e = readdir(d)) {
+      if (std::string(e->d_name).rfind("hwmon", 0) == 0) hw = base + "/" + e->d_name;
+    }
+    closedir(d);
+    if (hw.empty()) return false;
+    for (const char* f : {"energy1_input"}) {
+      double v;
+      if (read_num(hw + "/" + f, v)) {
+        energy_path_ = hw + "/" + f;
+        src_ = "hwmon " + energy_path_;
+        return true;
+      }
+    }
+    for (const char* f : {"power1_average", "power1_input"}) {
+      double v;
+      if (read_num(hw + "/" + f, v)) {
+        power_path_ = hw + "/" + f;
+        src_ = "hwmon " + power_path_ + " sampled every 5 ms";
+        stop_ = false;
+        th_ = std::thread([this] { sample(); });
+        return true;
+      }
+    }
+    return false;
+  }
+  ~HwmonMeter() override {
+    stop_ = true;
+    if (th_.joinable()) th_.join();
+  }
+  bool available() const override { return true; }
+  double joules() override {
+    if (!energy_path_.empty()) {
+      double v = 0;
+      return read_num(energy_path_, v) ? v * 1e-6 : 0.0;
+    }
+    return acc_j_.load();
+  }
+  std::string source() const override { return src_; }
+
+ private:
+  static bool read_num(const std::string& p, double& v) {
+    FILE* f = std::fopen(p.c_str(), "r");
+    if (!f) return false;
+    bool ok = std::fscanf(f, "%lf", &v) == 1;
+    std::fclose(f);
+    return ok;
+  }
+  void sample() {
+    auto last = std::chrono::steady_clock::now();
+    double last_w = 0;
+    double v;
+    if (read_num(power_path_, v)) last_w = v * 1e-6;
+    while (!stop_) {
+      std::this_thread::sleep_for(std::chrono::milliseconds(5));
+      auto now = std::chrono::steady_clock::now();
+      double w = last_w;
+      if (read_num(power_path_, v)) w = v * 1e-6;
+      double dt = std::chrono::duration<double>(now - last).count();
+      acc_j_.store(acc_j_.load() + 0.5 * (w + last_w) * dt);
+      last = now;
+      last_w = w;
+    }
+  }
+  std::string energy_path_, power_path_, src_;
+  std::atomic<bool> stop_{true};
+  std::atomic<double> acc_j_{0.0};
+  std::thread th_;
 };
 
 }  // namespace
@@ -82,9 +177,15 @@ class AmdSmiMeter : public EnergyMeter {
 std::unique_ptr<EnergyMeter> EnergyMeter::none() { return std::unique_ptr<EnergyMeter>(new EnergyMeter()); }
 
 std::unique_ptr<EnergyMeter> EnergyMeter::open_gpu(int device_index) {
-  if (env_int("DLNB_NO_ENERGY", 0)) return none();
-  std::unique_ptr<AmdSmiMeter> m(new AmdSmiMeter());
-  if (m->init(device_index)) return std::unique_ptr<EnergyMeter>(m.release());
+  std::string how = env_or("DLNB_ENERGY", "hwmon");  // hwmon | amdsmi | none
+  if (env_int("DLNB_NO_ENERGY", 0) || how == "none") return none();
+  if (how == "amdsmi") {
+    std::unique_ptr<AmdSmiMeter> m(new AmdSmiMeter());
+    if (m->init(device_index)) return std::unique_ptr<EnergyMeter>(m.release());
+    return none();
+  }
+  std::unique_ptr<HwmonMeter> h(new HwmonMeter());
+  if (h->init(device_index)) return std::unique_ptr<EnergyMeter>(h.release());
   return none();
 }
 

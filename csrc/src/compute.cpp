@@ -86,7 +86,13 @@ class GpuCompute : public ComputeEngine {
     if (mode_ != ComputeMode::Sleep && mode_ != ComputeMode::Spin) calibrate();
     if (mode_ == ComputeMode::Gemm) {
       slots_ = dev_.alloc(kSlots * 64);
-      grid_ = cus_;
+      // Leave `comm_cus` CUs to collectives: one 128-KiB-LDS block fits per
+      // CU, so a grid of CUs - comm_cus blocks never touches those CUs and
+      // RCCL / copy kernels on the high-priority comm streams always find
+      // room (with the whole chip taken, a comm kernel only starts at a
+      // compute boundary, and overlap collapses).
+      grid_ = std::max(1, cus_ - std::max(0, shape.comm_cus));
+      slice_us_ = static_cast<double>(env_int("DLNB_GEMM_SLICE_US", 500));
     }
   }
 
@@ -111,8 +117,13 @@ class GpuCompute : public ComputeEngine {
       }
       uint32_t& ep = epoch_[slot_for(s)];
       ep = ep % 65535 + 1;  // 1..65535, never 0 (a fresh slot reads as epoch 0)
-      kernels::gemm_tn_deadline(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, ticks(d), slot_for(s), ep,
-                                grid_, s.native());
+      const uint64_t total = ticks(d);
+      const uint64_t slice = std::max<uint64_t>(ticks(slice_us_), 1);
+      for (uint64_t end = slice;; end += slice) {
+        kernels::gemm_tn_deadline(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, total, slot_for(s), ep,
+                                  grid_, s.native(), std::min(end, total));
+        if (end >= total) break;
+      }
       return;
     }
     if (mode_ == ComputeMode::Flops) {
@@ -140,7 +151,11 @@ class GpuCompute : public ComputeEngine {
     j["time_scale"] = scale_;
     j["wallclock_hz"] = hz_;
     j["num_cus"] = cus_;
-    if (mode_ == ComputeMode::Gemm) j["deadline_grid"] = grid_;
+    if (mode_ == ComputeMode::Gemm) {
+      j["deadline_grid"] = grid_;
+      j["comm_reserved_cus"] = cus_ - grid_;
+      j["deadline_slice_us"] = slice_us_;
+    }
     if (!levels_.empty()) {
       j["gemm_dtype"] = dtype_name(dtype_);
       j["gemm_N"] = N_;
@@ -223,6 +238,7 @@ class GpuCompute : public ComputeEngine {
   std::map<Stream*, size_t> slot_of_;
   std::map<uint64_t*, uint32_t> epoch_;
   int grid_ = 256;
+  double slice_us_ = 500;
   double hz_ = 1e8;
   int cus_ = 256;
   DType dtype_ = DType::BF16;

@@ -220,6 +220,12 @@ class CpuDevice : public Device {
   }
   void host_task(Stream& s, std::function<void()> fn) override { dynamic_cast<CpuStream&>(s).enqueue(std::move(fn)); }
   void synchronize() override {}
+  uint64_t* alloc_stamps(size_t n) override { return static_cast<uint64_t*>(std::calloc(n, sizeof(uint64_t))); }
+  void free_stamps(uint64_t* p, size_t) override { std::free(p); }
+  void stamp(Stream& s, uint64_t* slot) override {
+    dynamic_cast<CpuStream&>(s).enqueue([slot] { *slot = static_cast<uint64_t>(now_s() * 1e9); });
+  }
+  double stamp_hz() const override { return 1e9; }
   size_t total_memory() const override { return static_cast<size_t>(sysconf(_SC_PHYS_PAGES)) * sysconf(_SC_PAGE_SIZE); }
   size_t free_memory() const override { return static_cast<size_t>(sysconf(_SC_AVPHYS_PAGES)) * sysconf(_SC_PAGE_SIZE); }
 };

@@ -3,6 +3,7 @@
 #include <hsa/hsa_ext_amd.h>
 
 #include <cstdio>
+#include <cstring>
 
 #include "dlnb/device.hpp"
 #include "dlnb/kernels.hpp"
@@ -20,10 +21,20 @@ namespace {
 class GpuEvent : public Event {
  public:
   explicit GpuEvent(bool timing) {
-    // Dependency-only events skip the timestamp. (hipEventDisableSystemFence
-    // is rejected by hipEventCreateWithFlags on ROCm 7.0 and 7.2 alike, so
-    // the default release scope is kept.)
-    DLNB_HIP_CHECK(hipEventCreateWithFlags(&ev, timing ? hipEventDefault : hipEventDisableTiming));
+    // Dependency-only events: no timestamp and, on HIP >= 7.2, no
+    // system-scope fence (an L2 writeback after every GEMM otherwise; the
+    // ordering we need is device-local). Timing events keep the defaults.
+    unsigned flags = timing ? hipEventDefault : hipEventDisableTiming;
+    if (!timing && runtime_version() >= 70200000) flags |= hipEventDisableSystemFence;
+    DLNB_HIP_CHECK(hipEventCreateWithFlags(&ev, flags));
+  }
+  static int runtime_version() {
+    static const int v = [] {
+      int x = 0;
+      if (hipRuntimeGetVersion(&x) != hipSuccess) x = 0;
+      return x;
+    }();
+    return v;
   }
   ~GpuEvent() override { (void)hipEventDestroy(ev); }
   hipEvent_t ev{};
@@ -67,6 +78,7 @@ class GpuDevice : public Device {
     name_ = prop.name;
     arch_ = prop.gcnArchName;
     total_ = prop.totalGlobalMem;
+    hz_ = kernels::wallclock_hz(idx_);
   }
   DeviceKind kind() const override { return DeviceKind::GPU; }
   std::string name() const override { return name_ + " (" + arch_ + ")"; }
@@ -105,6 +117,15 @@ class GpuDevice : public Device {
     DLNB_HIP_CHECK(hipLaunchHostFunc(static_cast<hipStream_t>(s.native()), host_trampoline, heap));
   }
   void synchronize() override { DLNB_HIP_CHECK(hipDeviceSynchronize()); }
+  uint64_t* alloc_stamps(size_t n) override {
+    void* p = nullptr;
+    DLNB_HIP_CHECK(hipHostMalloc(&p, n * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(p, 0, n * sizeof(uint64_t));
+    return static_cast<uint64_t*>(p);
+  }
+  void free_stamps(uint64_t* p, size_t) override { (void)hipHostFree(p); }
+  void stamp(Stream& s, uint64_t* slot) override { kernels::stamp(slot, s.native()); }
+  double stamp_hz() const override { return hz_; }
   size_t total_memory() const override { return total_; }
   size_t free_memory() const override {
     size_t f = 0, t = 0;
@@ -116,6 +137,7 @@ class GpuDevice : public Device {
   int idx_;
   std::string name_, arch_;
   size_t total_ = 0;
+  double hz_ = 1e8;
 };
 
 }  // namespace

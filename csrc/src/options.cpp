@@ -85,6 +85,7 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  --quiet                only print the report section\n"
      << "  --silent               print nothing (the report is returned to the caller)\n"
      << "  --trace                emit roctx ranges (rocprofv3 --marker-trace)\n"
+     << "  --comm-cus N           CUs the gemm compute leaves free for collectives (default 32)\n"
      << "env: DLNB_TIMEOUT (s, hang detection), DLNB_INJECT_FAULT=rank=R,iter=I,mode=exit|hang|throw,\n"
      << "     DLNB_STORE_ADDR=host:port, DLNB_NO_ENERGY=1\n";
   return os.str();
@@ -150,6 +151,8 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
       o.store_addr = val("store");
     } else if (a == "--no-topology") {
       o.topology = false;
+    } else if (is("--comm-cus")) {
+      o.comm_cus = to_int(val("comm-cus"), "comm-cus");
     } else if (a == "--trace") {
       o.trace = true;
     } else if (a == "--silent") {

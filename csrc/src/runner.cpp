@@ -221,6 +221,7 @@ Json run_benchmark(const Options& opt) {
   std::string cdt = opt.compute_dtype;
   if (cdt == "auto") cdt = ctx.stats.dtype.find("8") != std::string::npos ? "fp8" : "bf16";
   shape.dtype = parse_dtype(cdt);
+  shape.comm_cus = opt.comm_cus;
   ComputeMode mode = parse_compute_mode(opt.compute, ctx.dev->kind());
   ctx.compute = make_compute_engine(*ctx.dev, mode, shape, opt.time_scale);
 

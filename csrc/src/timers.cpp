@@ -2,19 +2,28 @@
 
 namespace dlnb {
 
+TimerSet::TimerSet(Device& dev) : dev_(dev) {
+  cap_ = 1 << 16;
+  stamps_ = dev_.alloc_stamps(cap_);
+}
+
+TimerSet::~TimerSet() {
+  if (stamps_) dev_.free_stamps(stamps_, cap_);
+}
+
 int TimerSet::begin(Stream& s) {
   if (!enabled_) return -1;
-  if (next_ == pool_.size()) pool_.push_back(dev_.create_event(true));
+  DLNB_REQUIRE(next_ < cap_, "too many timer stamps in one iteration");
   int idx = static_cast<int>(next_++);
-  s.record(*pool_[static_cast<size_t>(idx)]);
+  dev_.stamp(s, stamps_ + idx);
   return idx;
 }
 
 void TimerSet::end(int token, Stream& s, const std::string& name) {
   if (!enabled_ || token < 0) return;
-  if (next_ == pool_.size()) pool_.push_back(dev_.create_event(true));
+  DLNB_REQUIRE(next_ < cap_, "too many timer stamps in one iteration");
   int idx = static_cast<int>(next_++);
-  s.record(*pool_[static_cast<size_t>(idx)]);
+  dev_.stamp(s, stamps_ + idx);
   pending_.push_back(Pending{token, idx, name});
 }
 
@@ -31,9 +40,12 @@ void TimerSet::add(const std::string& name, double seconds) {
 void TimerSet::ensure(const std::string& name) { vals_[name]; }
 
 void TimerSet::resolve() {
+  // Called after the streams were synchronised: every stamp has landed.
+  const double hz = dev_.stamp_hz();
   for (const auto& p : pending_) {
-    double ms = dev_.elapsed_ms(*pool_[static_cast<size_t>(p.a)], *pool_[static_cast<size_t>(p.b)]);
-    vals_[p.name].push_back(ms * 1e-3);
+    const uint64_t a = __atomic_load_n(stamps_ + p.a, __ATOMIC_ACQUIRE);
+    const uint64_t b = __atomic_load_n(stamps_ + p.b, __ATOMIC_ACQUIRE);
+    vals_[p.name].push_back(b >= a ? static_cast<double>(b - a) / hz : 0.0);
   }
   pending_.clear();
   next_ = 0;

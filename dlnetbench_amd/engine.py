@@ -25,7 +25,7 @@ _FLAG = {
     "backend": "--backend", "compute": "--compute", "wire_dtype": "--wire-dtype",
     "compute_dtype": "--compute-dtype", "schedule": "--schedule", "tp_granularity": "--tp-granularity",
     "dp_buckets": "--dp-buckets", "max_loop_iters": "--max-loop-iters", "time_scale": "--time-scale",
-    "json": "--json", "store": "--store", "stats_file": "--stats-file",
+    "json": "--json", "store": "--store", "stats_file": "--stats-file", "comm_cus": "--comm-cus",
 }
 _BOOL = {"in_place": "--in-place", "optimizer": "--optimizer", "loop": "--loop", "quiet": "--quiet",
          "silent": "--silent"}
