@@ -41,8 +41,11 @@ int num_cus(int device);
 // dimensions in elements, 16-byte aligned rows. in_t is BF16 or FP8_E4M3;
 // C is always bf16.
 bool gemm_shape_ok(int M, int N, int K, DType in_t);
+// waves: 8 (2 per SIMD, 128x64 per wave) or 4 (1 per SIMD, 128x128 per wave);
+// 0 = the default (DLNB_GEMM_WAVES, else 8).
 void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
-             void* stream);
+             void* stream, int waves = 0);
+int gemm_default_waves();
 
 // Persistent deadline variant (the default stand-in compute): a grid of
 // `grid` blocks (<= one per CU: 128 KiB LDS each) walks the M x N tile space

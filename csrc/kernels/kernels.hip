@@ -147,15 +147,18 @@ constexpr int kStageBytes = 2 * kTileBytes;    // A + B
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * kRowBytes + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
+// One 256 x 128-byte tile = 2048 16-B slots = 32 wave-instructions of
+// global_load_lds_dwordx4, spread over the block's NW waves.
+template <int NW>
 __device__ __forceinline__ void stage_tile(const char* __restrict__ g, size_t ld_bytes, char* lds_tile, int w,
                                            int lane) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int slot = (i * 8 + w) * 64 + lane;
+  for (int i = 0; i < 32 / NW; ++i) {
+    const int slot = (i * NW + w) * 64 + lane;
     const int r = slot >> 3;
     const int c = (slot & 7) ^ ((r >> 1) & 7);
     const char* src = g + static_cast<size_t>(r) * ld_bytes + (c << 4);
-    __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(lds_tile + (i * 8 + w) * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)(lds_tile + (i * NW + w) * 1024), 16, 0, 0);
   }
 }
 
@@ -177,15 +180,21 @@ __device__ __forceinline__ int xcd_remap(int b, int T) {
 //   decides once per K-tile and publishes the decision through a
 //   double-buffered LDS flag read after the K-tile's barrier, so every wave
 //   leaves the K-loop at the same barrier.
-template <bool FP8, bool DEADLINE>
-__global__ void __launch_bounds__(512, 2)
+// WN = waves along N (WM = 2 along M): WN = 4 -> 8 waves (2 per SIMD) of
+// 128 x 64; WN = 2 -> 4 waves (1 per SIMD) of 128 x 128, twice the MFMAs per
+// LDS fragment read and the 256 accumulators in AGPRs.
+template <bool FP8, bool DEADLINE, int WN>
+__global__ void __launch_bounds__(128 * WN, WN == 4 ? 2 : 1)
     gemm_tn_256_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
                        int K, int lda, int ldb, int ldc, uint64_t* __restrict__ slot, uint32_t epoch,
                        uint64_t ticks, uint64_t slice_end) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kStageBytes + 16];
   volatile int* stop_flag = reinterpret_cast<volatile int*>(smem + 2 * kStageBytes);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 2, wn = w & 3;
+  constexpr int NW = 2 * WN;          // waves per block
+  constexpr int FN = kTile / WN / 16;  // 16-wide fragments along N per wave
+  constexpr int WTN = kTile / WN;      // wave tile width (N)
+  const int wm = w / WN, wn = w % WN;
   const int nt_m = M / kTile, nt_n = N / kTile, T = nt_m * nt_n;
   constexpr uint64_t kMask48 = (1ull << 48) - 1;
   uint64_t t0 = 0;
@@ -220,14 +229,14 @@ __global__ void __launch_bounds__(512, 2)
   const char* Bb = B + static_cast<size_t>(tn) * kTile * ldb_b;
   const int nk = (K * esz) / kRowBytes;
 
-  f32x4 acc[8][4];
+  f32x4 acc[8][FN];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage_tile(Ab, lda_b, smem, w, lane);
-  stage_tile(Bb, ldb_b, smem + kTileBytes, w, lane);
+  stage_tile<NW>(Ab, lda_b, smem, w, lane);
+  stage_tile<NW>(Bb, ldb_b, smem + kTileBytes, w, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int expired = 0;
@@ -237,45 +246,45 @@ __global__ void __launch_bounds__(512, 2)
     const char* cur = smem + (kt & 1) * kStageBytes;
     if (kt + 1 < nk) {
       char* nxt = smem + ((kt + 1) & 1) * kStageBytes;
-      stage_tile(Ab + static_cast<size_t>(kt + 1) * kRowBytes, lda_b, nxt, w, lane);
-      stage_tile(Bb + static_cast<size_t>(kt + 1) * kRowBytes, ldb_b, nxt + kTileBytes, w, lane);
+      stage_tile<NW>(Ab + static_cast<size_t>(kt + 1) * kRowBytes, lda_b, nxt, w, lane);
+      stage_tile<NW>(Bb + static_cast<size_t>(kt + 1) * kRowBytes, ldb_b, nxt + kTileBytes, w, lane);
     }
     const char* At = cur;
     const char* Bt = cur + kTileBytes;
     if constexpr (!FP8) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 af[8], bfr[4];
+        bf16x8 af[8], bfr[FN];
 #pragma unroll
         for (int i = 0; i < 8; ++i)
           af[i] = *reinterpret_cast<const bf16x8*>(At + swz(wm * 128 + i * 16 + r16, ks * 4 + h));
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          bfr[j] = *reinterpret_cast<const bf16x8*>(Bt + swz(wn * 64 + j * 16 + r16, ks * 4 + h));
+        for (int j = 0; j < FN; ++j)
+          bfr[j] = *reinterpret_cast<const bf16x8*>(Bt + swz(wn * WTN + j * 16 + r16, ks * 4 + h));
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
       }
     } else {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        long af[8], bfr[4];
+        long af[8], bfr[FN];
         const int chunk = ks * 2 + (h >> 1), half = (h & 1) * 8;
 #pragma unroll
         for (int i = 0; i < 8; ++i)
           af[i] = *reinterpret_cast<const long*>(At + swz(wm * 128 + i * 16 + r16, chunk) + half);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          bfr[j] = *reinterpret_cast<const long*>(Bt + swz(wn * 64 + j * 16 + r16, chunk) + half);
+        for (int j = 0; j < FN; ++j)
+          bfr[j] = *reinterpret_cast<const long*>(Bt + swz(wn * WTN + j * 16 + r16, chunk) + half);
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(bfr[j], af[i], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
       }
@@ -298,11 +307,11 @@ __global__ void __launch_bounds__(512, 2)
 
   // Epilogue: lane holds C[m = .. + (lane & 15)][n = .. + 4*(lane >> 4) + 0..3].
   const int m_base = tm * kTile + wm * 128 + r16;
-  const int n_base = tn * kTile + wn * 64 + 4 * h;
+  const int n_base = tn * kTile + wn * WTN + 4 * h;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < FN; ++j) {
       bf16x4 o;
       o[0] = static_cast<__bf16>(acc[i][j][0]);
       o[1] = static_cast<__bf16>(acc[i][j][1]);
@@ -401,8 +410,44 @@ bool gemm_shape_ok(int M, int N, int K, DType in_t) {
   return M > 0 && N > 0 && K > 0 && M % kTile == 0 && N % kTile == 0 && (static_cast<size_t>(K) * esz) % kRowBytes == 0;
 }
 
+namespace {
+
+template <bool FP8, bool DEADLINE, int WN>
+void launch_gemm(int grid, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                 uint64_t* slot, uint32_t epoch, uint64_t ticks, uint64_t slice_end, hipStream_t st) {
+  hipLaunchKernelGGL((gemm_tn_256_kernel<FP8, DEADLINE, WN>), grid, 128 * WN, 0, st, static_cast<const char*>(A),
+                     static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc, slot, epoch, ticks,
+                     slice_end);
+}
+
+template <bool DEADLINE>
+void dispatch_gemm(int waves, DType in_t, int grid, const void* A, const void* B, void* C, int M, int N, int K,
+                   int lda, int ldb, int ldc, uint64_t* slot, uint32_t epoch, uint64_t ticks, uint64_t slice_end,
+                   hipStream_t st) {
+  const bool fp8 = in_t == DType::FP8_E4M3;
+  if (waves == 4) {
+    if (fp8)
+      launch_gemm<true, DEADLINE, 2>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
+    else
+      launch_gemm<false, DEADLINE, 2>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
+  } else {
+    if (fp8)
+      launch_gemm<true, DEADLINE, 4>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
+    else
+      launch_gemm<false, DEADLINE, 4>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
+  }
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace
+
+int gemm_default_waves() {
+  static const int w = env_int("DLNB_GEMM_WAVES", 8) == 4 ? 4 : 8;
+  return w;
+}
+
 void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
-             void* stream) {
+             void* stream, int waves) {
   DLNB_REQUIRE(gemm_shape_ok(M, N, K, in_t), "gemm_tn: unsupported shape M=" << M << " N=" << N << " K=" << K << " dtype="
                                                                               << dtype_name(in_t));
   size_t esz = dtype_size(in_t);
@@ -413,16 +458,8 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
                    reinterpret_cast<uintptr_t>(C) % 8 == 0,
                "gemm_tn: misaligned base pointers");
   const int tiles = (M / kTile) * (N / kTile);
-  if (in_t == DType::BF16) {
-    hipLaunchKernelGGL((gemm_tn_256_kernel<false, false>), tiles, 512, 0, S(stream), static_cast<const char*>(A),
-                       static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc,
-                       static_cast<uint64_t*>(nullptr), 0u, 0ull, 0ull);
-  } else {
-    hipLaunchKernelGGL((gemm_tn_256_kernel<true, false>), tiles, 512, 0, S(stream), static_cast<const char*>(A),
-                       static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc,
-                       static_cast<uint64_t*>(nullptr), 0u, 0ull, 0ull);
-  }
-  DLNB_HIP_CHECK(hipGetLastError());
+  dispatch_gemm<false>(waves ? waves : gemm_default_waves(), in_t, tiles, A, B, C, M, N, K, lda, ldb, ldc, nullptr, 0u,
+                       0ull, 0ull, S(stream));
 }
 
 void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
@@ -430,16 +467,8 @@ void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K
   if (slice_end == 0) slice_end = ticks;
   DLNB_REQUIRE(gemm_shape_ok(M, N, K, in_t), "gemm_tn_deadline: unsupported shape");
   DLNB_REQUIRE(slot != nullptr && grid > 0 && epoch > 0 && epoch < 65536, "gemm_tn_deadline: bad slot/grid/epoch");
-  if (in_t == DType::BF16) {
-    hipLaunchKernelGGL((gemm_tn_256_kernel<false, true>), grid, 512, 0, S(stream), static_cast<const char*>(A),
-                       static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, K, K, N,
-                       slot, epoch, ticks, slice_end);
-  } else {
-    hipLaunchKernelGGL((gemm_tn_256_kernel<true, true>), grid, 512, 0, S(stream), static_cast<const char*>(A),
-                       static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, K, K, N,
-                       slot, epoch, ticks, slice_end);
-  }
-  DLNB_HIP_CHECK(hipGetLastError());
+  // 8 waves: the 4-wave variant spills once the deadline logic is added.
+  dispatch_gemm<true>(8, in_t, grid, A, B, C, M, N, K, K, K, N, slot, epoch, ticks, slice_end, S(stream));
 }
 
 void sgd_momentum_bf16(void* param, void* mom, const void* grad, size_t n, float lr, float beta, void* stream) {

@@ -74,6 +74,12 @@ int dlnb_gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int
   });
 }
 
+int dlnb_gemm_tn_waves(const void* A, const void* B, void* C, int M, int N, int K, int dtype, int waves, void* stream) {
+  return guard([&] {
+    dlnb::kernels::gemm_tn(A, B, C, M, N, K, K, K, N, static_cast<dlnb::DType>(dtype), stream, waves);
+  });
+}
+
 int dlnb_gemm_deadline_us(const void* A, const void* B, void* C, int M, int N, int K, int dtype, double us,
                           int device, void* stamp_slot, int grid, void* stream) {
   static uint32_t epoch = 0;

@@ -14,7 +14,7 @@ def _stream(t):
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
-def gemm_tn(a, b, out=None):
+def gemm_tn(a, b, out=None, waves: int = 0):
     """C[M,N] (bf16) = A[M,K] @ B[N,K]^T with the 256x256 MFMA kernel.
 
     a, b: bf16 or float8_e4m3fn (OCP) CUDA tensors, row-major, K contiguous.
@@ -40,7 +40,10 @@ def gemm_tn(a, b, out=None):
         raise ValueError(f"unsupported shape M={M} N={N} K={K} (M,N % 256, K bytes % 128)")
     if out is None:
         out = torch.empty((M, N), device=a.device, dtype=torch.bfloat16)
-    _native.check(L.dlnb_gemm_tn(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, K, K, N, dt, _stream(a)))
+    if waves:
+        _native.check(L.dlnb_gemm_tn_waves(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, dt, waves, _stream(a)))
+    else:
+        _native.check(L.dlnb_gemm_tn(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, K, K, N, dt, _stream(a)))
     return out
 
 

@@ -34,7 +34,10 @@ def main(argv=None) -> int:
         flop = 2.0 * M * N * K
 
         def ours():
-            gemm.gemm_tn(A, B, C)
+            gemm.gemm_tn(A, B, C, waves=8)
+
+        def ours4():
+            gemm.gemm_tn(A, B, C, waves=4)
 
         if dt == torch.bfloat16:
             def ref():
@@ -45,13 +48,13 @@ def main(argv=None) -> int:
             def ref():
                 torch._scaled_mm(A, B.t(), scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
 
-        res = {"ours": [], "torch": []}
-        for fn in (ours, ref):  # warm
+        res = {"ours": [], "ours4": [], "torch": []}
+        for fn in (ours, ours4, ref):  # warm
             for _ in range(3):
                 fn()
         torch.cuda.synchronize()
         for _ in range(a.rounds):
-            for name, fn in (("ours", ours), ("torch", ref)):
+            for name, fn in (("ours", ours), ("ours4", ours4), ("torch", ref)):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.iters):

@@ -15,13 +15,14 @@ def need_gpu():
 from dlnetbench_amd.ops import gemm  # noqa: E402
 
 
+@pytest.mark.parametrize("waves", [8, 4])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 512, 128), (512, 256, 1024), (768, 1280, 640),
                                    (2048, 1024, 4096)])
-def test_gemm_bf16_matches_torch(M, N, K):
+def test_gemm_bf16_matches_torch(M, N, K, waves):
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
     b = torch.randn(N, K, device="cuda", generator=g).to(torch.bfloat16)
-    c = gemm.gemm_tn(a, b)
+    c = gemm.gemm_tn(a, b, waves=waves)
     torch.cuda.synchronize()
     ref = a.float() @ b.float().t()
     tol = 2e-2 * ref.abs().max().item() + 1e-2
@@ -40,12 +41,13 @@ def test_gemm_bf16_identity_asymmetric():
 
 
 @pytest.mark.skipif(not hasattr(torch, "float8_e4m3fn"), reason="torch without float8")
+@pytest.mark.parametrize("waves", [8, 4])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 512), (1024, 512, 2048)])
-def test_gemm_fp8_matches_torch(M, N, K):
+def test_gemm_fp8_matches_torch(M, N, K, waves):
     g = torch.Generator(device="cuda").manual_seed(7 + M)
     a = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(torch.float8_e4m3fn)
     b = (torch.randn(N, K, device="cuda", generator=g) * 0.5).to(torch.float8_e4m3fn)
-    c = gemm.gemm_tn(a, b)
+    c = gemm.gemm_tn(a, b, waves=waves)
     torch.cuda.synchronize()
     ref = a.float() @ b.float().t()
     tol = 2e-2 * ref.abs().max().item() + 1e-2
