@@ -32,6 +32,9 @@ class Store {
   virtual std::string get(const std::string& key) = 0;
   // Atomically adds delta to an integer key (missing = 0); returns the new value.
   virtual long long add(const std::string& key, long long delta) = 0;
+  // The job completed cleanly: a server-side store keeps serving until the
+  // other ranks disconnect (bounded), so none loses the final barrier reply.
+  virtual void finish() {}
 };
 
 // In-process store for world_size == 1.
@@ -57,6 +60,7 @@ class TcpStore : public Store {
   void set(const std::string& key, const std::string& value) override;
   std::string get(const std::string& key) override;
   long long add(const std::string& key, long long delta) override;
+  void finish() override;
   int port() const { return port_; }
 
  private:

@@ -62,6 +62,10 @@ struct Options {
   bool silent = false;  // print nothing (library use, e.g. bench.py)
   bool trace = false;   // roctx ranges around iterations and phases
   int comm_cus = 32;    // CUs left free by the persistent compute for collectives
+  // fsdp: "single" = every collective of a rank on one in-order comm lane
+  // (deadlock-free across communicators), "split" = one lane per collective
+  // kind so all-gather / reduce-scatter / replica all-reduce run concurrently.
+  std::string comm_lanes = "single";
 };
 
 // Parses argv for the given strategy (argv[0] is the program name). Throws

@@ -96,6 +96,8 @@ struct TcpStore::Server {
   std::thread acceptor;
   std::vector<std::thread> workers;
   std::vector<int> client_fds;
+  int active = 0;    // connected clients
+  int linger_s = 0;  // set by finish()
   std::mutex mu;
   std::condition_variable cv;
   std::map<std::string, std::string> kv;
@@ -119,7 +121,7 @@ struct TcpStore::Server {
           {
             std::unique_lock<std::mutex> g(mu);
             cv.wait(g, [&] { return stop.load() || kv.count(key) > 0; });
-            if (stop.load()) break;
+            if (!kv.count(key)) break;  // stopping and the key never came
             out = kv[key];
           }
           write_blob(fd, out);
@@ -141,6 +143,11 @@ struct TcpStore::Server {
       }
     }
     ::close(fd);
+    {
+      std::lock_guard<std::mutex> g(mu);
+      --active;
+    }
+    cv.notify_all();
   }
 
   void accept_loop() {
@@ -154,11 +161,19 @@ struct TcpStore::Server {
       setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
       std::lock_guard<std::mutex> g(mu);
       client_fds.push_back(fd);
+      ++active;
       workers.emplace_back([this, fd] { serve(fd); });
     }
   }
 
   ~Server() {
+    // Graceful first: the other ranks close their connections when they exit;
+    // tearing the server down while one of them still waits for the reply of
+    // the final barrier would fail that rank. Give them a bounded grace.
+    {
+      std::unique_lock<std::mutex> g(mu);
+      cv.wait_for(g, std::chrono::seconds(linger_s), [&] { return active == 0; });
+    }
     stop.store(true);
     cv.notify_all();
     if (acceptor.joinable()) acceptor.join();
@@ -241,6 +256,10 @@ std::string TcpStore::request(uint8_t op, const std::string& key, const std::str
     DLNB_THROW("store: no reply within " << timeout_s_ << " s or connection lost (op " << int(op) << " key " << key
                                          << "): a peer rank died or hangs");
   return out;
+}
+
+void TcpStore::finish() {
+  if (server_) server_->linger_s = static_cast<int>(env_int("DLNB_STORE_LINGER", 30));
 }
 
 void TcpStore::set(const std::string& key, const std::string& value) { request(OP_SET, key, value); }

@@ -86,6 +86,7 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  --silent               print nothing (the report is returned to the caller)\n"
      << "  --trace                emit roctx ranges (rocprofv3 --marker-trace)\n"
      << "  --comm-cus N           CUs the gemm compute leaves free for collectives (default 32)\n"
+     << "  --comm-lanes single|split  fsdp: all collectives on one ordered lane (default) or one per kind\n"
      << "env: DLNB_TIMEOUT (s, hang detection), DLNB_INJECT_FAULT=rank=R,iter=I,mode=exit|hang|throw,\n"
      << "     DLNB_STORE_ADDR=host:port, DLNB_NO_ENERGY=1\n";
   return os.str();
@@ -153,6 +154,8 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
       o.topology = false;
     } else if (is("--comm-cus")) {
       o.comm_cus = to_int(val("comm-cus"), "comm-cus");
+    } else if (is("--comm-lanes")) {
+      o.comm_lanes = val("comm-lanes");
     } else if (a == "--trace") {
       o.trace = true;
     } else if (a == "--silent") {
@@ -202,6 +205,7 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
   DLNB_REQUIRE(o.schedule == "overlap" || o.schedule == "reference", "--schedule must be overlap or reference");
   DLNB_REQUIRE(o.tp_granularity == "microbatch" || o.tp_granularity == "layer",
                "--tp-granularity must be microbatch or layer");
+  DLNB_REQUIRE(o.comm_lanes == "single" || o.comm_lanes == "split", "--comm-lanes must be single or split");
   DLNB_REQUIRE(o.dp_buckets >= 1, "--dp-buckets must be >= 1");
   DLNB_REQUIRE(o.time_scale > 0, "--time-scale must be > 0");
   return o;

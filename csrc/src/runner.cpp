@@ -280,6 +280,7 @@ Json run_benchmark(const Options& opt) {
       strat->synchronize();
     }
     ctx.hg().barrier();
+    ctx.hg().store().finish();
     doc["section"] = strat->section_id();
     doc["loop_iterations"] = opt.max_loop_iters;
     return doc;
@@ -386,6 +387,7 @@ Json run_benchmark(const Options& opt) {
     f << doc.dump(1) << "\n";
   }
   ctx.hg().barrier();  // keep the store (rank 0) alive until everyone is done
+  ctx.hg().store().finish();
   return doc;
 }
 

@@ -12,10 +12,19 @@
 // Shard size = ceil((P/U)/F) per unit (fsdp.cpp:244-255).
 //
 // MI355X design:
-//   * all-gathers, reduce-scatters and replica all-reduces each get their own
-//     communicator + stream, so a reduce-scatter of unit u runs concurrently
-//     with the all-gather prefetch of unit u-2 and the backward of unit u-1
-//     (the reference blocks the host on every reduce-scatter);
+//   * collectives are stream-ordered behind events, never host-blocking, so
+//     the reduce-scatter of unit u and the all-gather prefetch of unit u-2
+//     run under the backward of unit u-1 (the reference blocks the host on
+//     every reduce-scatter). By default (--comm-lanes single) all of a rank's
+//     collectives go through ONE high-priority stream and ONE unit
+//     communicator in the same program order on every rank: at most one RCCL
+//     kernel per rank is in flight, so kernels of different communicators can
+//     never hold CUs while waiting on each other across GPUs (the multi-
+//     communicator deadlock RCCL/NCCL warn about). At 8 GPUs a 0.5 GB
+//     all-gather is ~1.5 ms against ~29 ms of compute per unit, so
+//     serialising the lanes costs nothing. --comm-lanes split gives
+//     all-gather, reduce-scatter and replica all-reduce their own
+//     communicator + stream (concurrent, for experiments);
 //   * gathered parameters and full gradients are double-buffered (the
 //     reference gathers into a single buffer that the in-flight prefetch and
 //     the reduce-scatter share, a race - SURVEY.md §3.2); buffer reuse is
@@ -62,15 +71,27 @@ class Fsdp : public Strategy {
       if (r % F_ == rank % F_) rep_members.push_back(r);
     }
     const size_t unit_bytes = max_shard_ * F_ * es_;
-    ag_comm_ = ctx.comms->create("fsdp/unit_ag/" + std::to_string(rank / F_), unit_members, unit_bytes, false);
-    rs_comm_ = ctx.comms->create("fsdp/unit_rs/" + std::to_string(rank / F_), unit_members, unit_bytes, false);
+    const bool split = o.comm_lanes == "split";
+    auto own_comm = [&](std::unique_ptr<Communicator> c) {
+      comms_.push_back(std::move(c));
+      return comms_.back().get();
+    };
+    auto own_stream = [&](std::unique_ptr<Stream> s) {
+      lanes_.push_back(std::move(s));
+      return lanes_.back().get();
+    };
+    ag_comm_ = own_comm(ctx.comms->create("fsdp/unit/" + std::to_string(rank / F_), unit_members, unit_bytes, false));
+    rs_comm_ = split ? own_comm(ctx.comms->create("fsdp/unit_rs/" + std::to_string(rank / F_), unit_members,
+                                                  unit_bytes, false))
+                     : ag_comm_;
     if (R_ > 1)
-      ar_comm_ = ctx.comms->create("fsdp/replica/" + std::to_string(rank % F_), rep_members, max_shard_ * es_, false);
+      ar_comm_ = own_comm(
+          ctx.comms->create("fsdp/replica/" + std::to_string(rank % F_), rep_members, max_shard_ * es_, false));
 
     compute_ = dev.create_stream(false);
-    ag_stream_ = dev.create_stream(true);
-    rs_stream_ = dev.create_stream(true);
-    if (R_ > 1) ar_stream_ = dev.create_stream(true);
+    ag_stream_ = own_stream(dev.create_stream(true));
+    rs_stream_ = split ? own_stream(dev.create_stream(true)) : ag_stream_;
+    if (R_ > 1) ar_stream_ = split ? own_stream(dev.create_stream(true)) : ag_stream_;
 
     for (int u = 0; u < U_; ++u) {
       params_.push_back(dev.alloc(shard_[u] * es_));
@@ -163,9 +184,7 @@ class Fsdp : public Strategy {
       }
     }
     // ---- tail: exposed reduce-scatter / replica all-reduce
-    Stream& last = R_ > 1 ? *ar_stream_ : *rs_stream_;
     Event& tail = R_ > 1 ? *ar_done_[0] : *rs_done_[0];
-    (void)last;
     timers_->stall(*compute_, tail, "barrier");
     if (ctx.opt.optimizer) {
       if (R_ > 1)
@@ -176,12 +195,10 @@ class Fsdp : public Strategy {
   }
 
   void synchronize() override {
-    std::vector<Stream*> ss = {compute_.get(), ag_stream_.get(), rs_stream_.get()};
-    std::vector<Communicator*> cs = {ag_comm_.get(), rs_comm_.get()};
-    if (R_ > 1) {
-      ss.push_back(ar_stream_.get());
-      cs.push_back(ar_comm_.get());
-    }
+    std::vector<Stream*> ss = {compute_.get()};
+    std::vector<Communicator*> cs;
+    for (auto& s : lanes_) ss.push_back(s.get());
+    for (auto& c : comms_) cs.push_back(c.get());
     sync_streams(ss, cs, *ctx_->dev);
     timers_->resolve();
   }
@@ -202,6 +219,7 @@ class Fsdp : public Strategy {
     g["local_batch_size"] = ctx.stats.batch_size;
     g["device"] = ctx.dev->kind() == DeviceKind::CPU ? "CPU" : "GPU";
     g["backend"] = ag_comm_->backend_name();
+    g["comm_lanes"] = ctx.opt.comm_lanes;
     g["fwd_time_per_unit_us"] = fwd_us_;
     g["bwd_time_per_unit_us"] = bwd_us_;
     g["allgather_msg_size_bytes"] = max_shard_ * F_ * es_;
@@ -229,8 +247,11 @@ class Fsdp : public Strategy {
   bool reference_ = false;
   std::vector<uint64_t> shard_;
   double fwd_us_ = 0, bwd_us_ = 0, fwd_flops_ = 0, bwd_flops_ = 0;
-  std::unique_ptr<Communicator> ag_comm_, rs_comm_, ar_comm_;
-  std::unique_ptr<Stream> compute_, ag_stream_, rs_stream_, ar_stream_;
+  std::vector<std::unique_ptr<Communicator>> comms_;
+  std::vector<std::unique_ptr<Stream>> lanes_;
+  Communicator *ag_comm_ = nullptr, *rs_comm_ = nullptr, *ar_comm_ = nullptr;
+  std::unique_ptr<Stream> compute_;
+  Stream *ag_stream_ = nullptr, *rs_stream_ = nullptr, *ar_stream_ = nullptr;
   std::vector<Buffer> params_, grads_, mom_;
   Buffer gathered_[2], full_grad_[2];
   std::vector<std::unique_ptr<Event>> ag_f_, fwd_done_, ag_b_, bwd_done_, rs_done_, ar_done_;

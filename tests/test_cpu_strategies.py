@@ -89,6 +89,14 @@ def test_fsdp(w, F, data_dir):
         assert min(r["runtime"]) >= 0.006 * 0.98
 
 
+@pytest.mark.parametrize("lanes", ["single", "split"])
+def test_fsdp_comm_lanes(lanes, data_dir):
+    d = run(4, "fsdp", "tiny_dense_8_bfloat16", 4, 2, data_dir, "-w", 1, "-r", 2, "--comm-lanes", lanes)
+    assert d["global"]["comm_lanes"] == lanes
+    for r in d["ranks"]:
+        assert len(r["reduce_scatter"]) == 2 * 4 and len(r["allreduce_time"]) == 2 * 4
+
+
 def test_fsdp_reference_schedule(data_dir):
     d = run(2, "fsdp", "tiny_dense_8_bfloat16", 4, 2, data_dir, "-w", 1, "-r", 2, "--schedule", "reference")
     assert d["global"]["dlnb"]["schedule"] == "reference"
