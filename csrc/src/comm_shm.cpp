@@ -20,6 +20,8 @@
 #include <atomic>
 #include <cstring>
 #include <sstream>
+#include <thread>
+#include <vector>
 
 #include "dlnb/comm.hpp"
 
@@ -148,6 +150,53 @@ void reduce_sum(DType t, void* dst, const std::vector<const char*>& srcs, size_t
   }
 }
 
+// Large copies / reductions are split over a few threads: one core cannot
+// saturate the socket's memory bandwidth. Threads per rank default to the
+// host's cores divided by the ranks on it (DLNB_SHM_THREADS overrides).
+int shm_threads() {
+  static const int n = [] {
+    long long env = env_int("DLNB_SHM_THREADS", 0);
+    if (env > 0) return static_cast<int>(env);
+    long long local = env_int("DLNB_LOCAL_WORLD_SIZE", env_int("LOCAL_WORLD_SIZE", 1));
+    unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    return static_cast<int>(std::max<long long>(1, std::min<long long>(8, hw / std::max<long long>(1, local))));
+  }();
+  return n;
+}
+
+// Runs fn(lo, n) over [0, total) in up to shm_threads() pieces of at least
+// min_piece elements; the calling thread takes the first piece.
+template <typename F>
+void par_range(size_t total, size_t min_piece, F fn) {
+  size_t T = std::min<size_t>(static_cast<size_t>(shm_threads()), std::max<size_t>(1, total / min_piece));
+  if (T <= 1) {
+    fn(size_t(0), total);
+    return;
+  }
+  size_t per = (total + T - 1) / T;
+  std::vector<std::thread> th;
+  for (size_t i = 1; i < T; ++i) {
+    size_t lo = i * per;
+    if (lo >= total) break;
+    th.emplace_back([=] { fn(lo, std::min(per, total - lo)); });
+  }
+  fn(size_t(0), std::min(per, total));
+  for (auto& t : th) t.join();
+}
+
+void par_copy(void* dst, const void* src, size_t bytes) {
+  par_range(bytes, size_t(4) << 20, [=](size_t lo, size_t n) {
+    std::memcpy(static_cast<char*>(dst) + lo, static_cast<const char*>(src) + lo, n);
+  });
+}
+
+void par_reduce_sum(DType t, void* dst, const std::vector<const char*>& srcs, size_t off, size_t n) {
+  const size_t es = dtype_size(t);
+  par_range(n, size_t(1) << 20, [&, dst, off](size_t lo, size_t m) {
+    reduce_sum(t, static_cast<char*>(dst) + lo * es, srcs, off + lo, m);
+  });
+}
+
 class ShmComm : public Communicator {
  public:
   ShmComm(const std::string& name, const std::vector<int>& members, int my_world_rank, HostGroup& world,
@@ -211,13 +260,13 @@ class ShmComm : public Communicator {
     enqueue(s, [=] {
       const size_t es = dtype_size(t), bytes = count * es;
       check(bytes);
-      std::memcpy(slot(rank_), send, bytes);
+      par_copy(slot(rank_), send, bytes);
       barrier();
       size_t lo, n;
       chunk(count, rank_, lo, n);
-      reduce_sum(t, base_ + result_off_ + lo * es, all_slots(), lo, n);
+      par_reduce_sum(t, base_ + result_off_ + lo * es, all_slots(), lo, n);
       barrier();
-      std::memcpy(recv, base_ + result_off_, bytes);
+      par_copy(recv, base_ + result_off_, bytes);
       barrier();
     });
   }
@@ -226,9 +275,9 @@ class ShmComm : public Communicator {
     enqueue(s, [=] {
       const size_t bytes = send_count * dtype_size(t);
       check(bytes);
-      std::memcpy(slot(rank_), send, bytes);
+      par_copy(slot(rank_), send, bytes);
       barrier();
-      for (int r = 0; r < size_; ++r) std::memcpy(static_cast<char*>(recv) + r * bytes, slot(r), bytes);
+      for (int r = 0; r < size_; ++r) par_copy(static_cast<char*>(recv) + r * bytes, slot(r), bytes);
       barrier();
     });
   }
@@ -237,9 +286,9 @@ class ShmComm : public Communicator {
     enqueue(s, [=] {
       const size_t es = dtype_size(t), bytes = recv_count * es * size_;
       check(bytes);
-      std::memcpy(slot(rank_), send, bytes);
+      par_copy(slot(rank_), send, bytes);
       barrier();
-      reduce_sum(t, recv, all_slots(), recv_count * rank_, recv_count);
+      par_reduce_sum(t, recv, all_slots(), recv_count * rank_, recv_count);
       barrier();
     });
   }
@@ -248,9 +297,9 @@ class ShmComm : public Communicator {
     enqueue(s, [=] {
       const size_t blk = count * dtype_size(t);
       check(blk * size_);
-      std::memcpy(slot(rank_), send, blk * size_);
+      par_copy(slot(rank_), send, blk * size_);
       barrier();
-      for (int r = 0; r < size_; ++r) std::memcpy(static_cast<char*>(recv) + r * blk, slot(r) + rank_ * blk, blk);
+      for (int r = 0; r < size_; ++r) par_copy(static_cast<char*>(recv) + r * blk, slot(r) + rank_ * blk, blk);
       barrier();
     });
   }
