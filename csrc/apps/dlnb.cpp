@@ -1,4 +1,5 @@
 // Unified entry point: dlnb <dp|fsdp|hybrid_2d|hybrid_3d|hybrid_3d_moe> <args...>
+//                      dlnb commtest [options]   (collective check / bandwidth)
 #include <iostream>
 #include <string>
 
@@ -6,8 +7,17 @@
 
 int main(int argc, char** argv) {
   if (argc < 2 || std::string(argv[1]) == "-h" || std::string(argv[1]) == "--help") {
-    std::cout << "Usage: dlnb <dp|fsdp|hybrid_2d|hybrid_3d|hybrid_3d_moe> <args...>  (dlnb <strategy> -h for details)\n";
+    std::cout << "Usage: dlnb <dp|fsdp|hybrid_2d|hybrid_3d|hybrid_3d_moe> <args...>  (dlnb <strategy> -h for details)\n"
+                 "       dlnb commtest [--backend B] [--bench] ...   (dlnb commtest -h)\n";
     return argc < 2 ? 1 : 0;
+  }
+  if (std::string(argv[1]) == "commtest") {
+    try {
+      return dlnb::commtest_main(argc - 1, argv + 1);
+    } catch (const std::exception& e) {
+      std::cerr << "[dlnb] commtest error: " << e.what() << std::endl;
+      return 2;
+    }
   }
   dlnb::StrategyKind k;
   try {

@@ -77,6 +77,14 @@ std::unique_ptr<Strategy> make_dp();
 std::unique_ptr<Strategy> make_fsdp();
 std::unique_ptr<Strategy> make_pipeline(StrategyKind kind);  // hybrid_2d / 3d / 3d_moe
 
+// Creates ctx.dev + ctx.comms for a backend (auto | rccl | xgmi | cpu);
+// GPU ranks take device list[local_rank] ("-d 0,1,..", default all GPUs).
+// Returns the resolved backend name. ctx.boot must be set.
+std::string select_backend(Context& ctx, const std::string& requested, const std::string& devices);
+
+// Collective correctness / bandwidth tool: dlnb commtest [options].
+int commtest_main(int argc, char** argv);
+
 // Runs a whole benchmark (bootstrap -> setup -> warmup -> timed runs ->
 // report). Returns the report document (rank 0 has the gathered ranks).
 Json run_benchmark(const Options& opt);

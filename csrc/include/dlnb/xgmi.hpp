@@ -1,0 +1,82 @@
+// Device side of the "xgmi" backend: collectives and point-to-point copies
+// done by our own kernels through IPC-mapped peer windows (SURVEY.md §7.2
+// step 7). Every rank owns one window (uncached device memory, so stores
+// that peers make over xGMI are never shadowed by a stale L2 line) plus a
+// small flag array; each rank maps all peers' windows with
+// hipIpcOpenMemHandle. A collective is one kernel per piece: every block
+// owns the same slice of the message on every rank, pushes its slice to all
+// peers with 16-B stores (the 7 xGMI links run concurrently, staggered by
+// rank so no link is hot-spotted), fences at system scope, raises one flag
+// per peer and waits for the peers' flags for the same block, then finishes
+// locally (copy-out or fp32-accumulated reduction). No grid-wide barrier,
+// no host involvement; windows alternate between two parity regions, so a
+// piece never waits for a peer to finish reading the previous one (stream
+// order on the peer guarantees piece k-2 is fully consumed when any of its
+// blocks reached piece k-1's flags).
+//
+// Reference equivalent: none (the reference only calls NCCL/RCCL/MPI,
+// cpp/proxy_classes.hpp:135-253); this is new MI355X-native capability.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+#include "dlnb/common.hpp"
+
+namespace dlnb {
+namespace xgmi {
+
+constexpr int kMaxRanks = 8;     // one node: 8 MI355X, fully connected by xGMI
+constexpr int kMaxBlocks = 256;  // per-block flags
+constexpr int kThreads = 512;
+
+// Flag words (uint32) in each rank's flag array.
+constexpr size_t kFlagColl = 0;                                    // [phase 2][src 8][block 256]
+constexpr size_t kFlagP2PSeq = 2 * kMaxRanks * kMaxBlocks;         // [src 8][block 256]
+constexpr size_t kFlagP2PConsumed = kFlagP2PSeq + kMaxRanks * kMaxBlocks;  // [dst 8]
+constexpr size_t kFlagP2PCount = kFlagP2PConsumed + 64;            // [src 8] local block counters
+constexpr size_t kFlagWords = kFlagP2PCount + 64;
+constexpr size_t kFlagBytes = 64 * 1024;
+
+struct Peers {
+  char* win[kMaxRanks];        // each rank's window, mapped in this process
+  uint32_t* flags[kMaxRanks];  // each rank's flag array, mapped in this process
+  uint32_t* abort_word;        // host-mapped: non-zero = give up waiting
+  uint32_t* error_word;        // host-mapped: set by a kernel that timed out
+  uint64_t timeout_ticks;      // s_memrealtime ticks (100 MHz) before a wait gives up
+  int rank;
+  int nranks;
+};
+
+enum class Op : int { AllGather, ReduceScatter, AllReduceOneShot, AllReduceTwoShot, AllToAll };
+
+struct CollPiece {
+  const char* send;
+  char* recv;
+  size_t bytes;        // bytes per rank block of this piece
+  size_t send_stride;  // bytes between rank blocks in send (RS, A2A)
+  size_t recv_stride;  // bytes between rank blocks in recv (AG, A2A)
+  size_t region;       // parity region offset in the windows
+  size_t slot;         // bytes between source slots inside the region
+  size_t ag_off;       // two-shot: offset of the all-gather slots inside the region
+  uint32_t epoch;
+  DType dtype;
+};
+
+// Number of blocks a piece of `bytes` per rank uses (identical on all ranks).
+int blocks_for(size_t bytes, int max_blocks);
+
+void launch_coll(Op op, const Peers& p, const CollPiece& c, int blocks, void* stream);
+
+// Point-to-point: message n (1-based) of the (me -> dst) channel goes to
+// parity region n & 1 of dst's window at offset `off`; the sender waits until
+// dst consumed message n-2.
+void launch_send(const Peers& p, const char* buf, size_t bytes, int dst, size_t off, uint32_t n, int blocks,
+                 void* stream);
+// `target` = cumulative number of receive blocks on the (src -> me) channel
+// after this message (the last block to finish signals "consumed").
+void launch_recv(const Peers& p, char* buf, size_t bytes, int src, size_t off, uint32_t n, uint32_t target,
+                 int blocks, void* stream);
+
+}  // namespace xgmi
+}  // namespace dlnb

@@ -1,0 +1,470 @@
+// Kernels of the "xgmi" backend (see dlnb/xgmi.hpp for the protocol).
+//
+// Data path: 16-B vector loads/stores, 512 threads per block, every block
+// owns one contiguous slice of the per-rank message (the same slice on all
+// ranks). Pushes go to the peers' uncached windows over xGMI; peers' targets
+// are visited in rank-staggered order so the 7 links of an MI355X carry
+// traffic at the same time. Reductions accumulate in fp32 and round once.
+#include <hip/hip_runtime.h>
+
+#include "dlnb/xgmi.hpp"
+
+#define DLNB_HIP_CHECK(expr)                                                       \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) DLNB_THROW(#expr << " failed: " << hipGetErrorString(e_)); \
+  } while (0)
+
+namespace dlnb {
+namespace xgmi {
+
+namespace {
+
+constexpr int T = kThreads;
+
+__device__ __forceinline__ void sys_store(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t sys_load(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Spin until *f >= v (wrap-safe). Every wait has an exit: the host's abort
+// word or the timeout (which also raises the error word), so a dead peer
+// never leaves a grid that cannot drain.
+__device__ void wait_geq(uint32_t* f, uint32_t v, const Peers& P) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (unsigned k = 1; static_cast<int>(sys_load(f) - v) < 0; ++k) {
+    __builtin_amdgcn_s_sleep(1);
+    if ((k & 255u) == 0) {
+      if (__hip_atomic_load(P.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > P.timeout_ticks) {
+        __hip_atomic_store(P.error_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t* coll_flag(const Peers& P, int owner, int phase, int src) {
+  return P.flags[owner] + kFlagColl + (static_cast<size_t>(phase) * kMaxRanks + src) * kMaxBlocks + blockIdx.x;
+}
+
+// This block's window stores are visible system-wide -> raise one flag per
+// peer -> wait for every peer's flag of the same block and phase.
+__device__ void exchange(const Peers& P, int phase, uint32_t epoch) {
+  __threadfence_system();
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < P.nranks && t != P.rank) sys_store(coll_flag(P, t, phase, P.rank), epoch);
+  if (t < P.nranks && t != P.rank) wait_geq(coll_flag(P, P.rank, phase, t), epoch, P);
+  __syncthreads();
+}
+
+__device__ __forceinline__ void blk_range(size_t n, size_t& lo, size_t& hi) {
+  const size_t per = (n + gridDim.x - 1) / gridDim.x;
+  lo = min(n, static_cast<size_t>(blockIdx.x) * per);
+  hi = min(n, lo + per);
+}
+
+__device__ __forceinline__ const uint4* V(const char* p) { return reinterpret_cast<const uint4*>(p); }
+__device__ __forceinline__ uint4* V(char* p) { return reinterpret_cast<uint4*>(p); }
+
+// dst[i] = src[i] for 16-B vectors i in [lo, hi), 4 loads in flight per thread.
+__device__ __forceinline__ void copy_vec(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t lo,
+                                         size_t hi) {
+  size_t i = lo + threadIdx.x;
+  for (; i + 3 * T < hi; i += 4 * T) {
+    uint4 a = src[i], b = src[i + T], c = src[i + 2 * T], d = src[i + 3 * T];
+    dst[i] = a;
+    dst[i + T] = b;
+    dst[i + 2 * T] = c;
+    dst[i + 3 * T] = d;
+  }
+  for (; i < hi; i += T) dst[i] = src[i];
+}
+
+// Byte tail [from, to) of a message, done by the last block.
+__device__ __forceinline__ void copy_tail(char* dst, const char* src, size_t from, size_t to) {
+  if (blockIdx.x != gridDim.x - 1) return;
+  for (size_t i = from + threadIdx.x; i < to; i += T) dst[i] = src[i];
+}
+
+// ---------------------------------------------------------------- dtypes
+
+template <DType D>
+struct Elt;
+template <>
+struct Elt<DType::BF16> {
+  static constexpr int N = 8;
+  __device__ static float ld(const char* p, size_t i) {
+    uint32_t u = static_cast<uint32_t>(reinterpret_cast<const uint16_t*>(p)[i]) << 16;
+    return __uint_as_float(u);
+  }
+  __device__ static void st(char* p, size_t i, float f) {
+    __bf16 b = static_cast<__bf16>(f);
+    reinterpret_cast<__bf16*>(p)[i] = b;
+  }
+  __device__ static void unpack(uint4 v, float* f) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f[2 * k] = __uint_as_float(w[k] << 16);
+      f[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
+  }
+  __device__ static uint4 pack(const float* f) {
+    typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+    bf16x8 b;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) b[k] = static_cast<__bf16>(f[k]);
+    return __builtin_bit_cast(uint4, b);
+  }
+};
+template <>
+struct Elt<DType::FP16> {
+  static constexpr int N = 8;
+  __device__ static float ld(const char* p, size_t i) { return static_cast<float>(reinterpret_cast<const _Float16*>(p)[i]); }
+  __device__ static void st(char* p, size_t i, float f) { reinterpret_cast<_Float16*>(p)[i] = static_cast<_Float16>(f); }
+  __device__ static void unpack(uint4 v, float* f) {
+    typedef __attribute__((ext_vector_type(8))) _Float16 h8;
+    h8 h = __builtin_bit_cast(h8, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = static_cast<float>(h[k]);
+  }
+  __device__ static uint4 pack(const float* f) {
+    typedef __attribute__((ext_vector_type(8))) _Float16 h8;
+    h8 h;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = static_cast<_Float16>(f[k]);
+    return __builtin_bit_cast(uint4, h);
+  }
+};
+template <>
+struct Elt<DType::FP32> {
+  static constexpr int N = 4;
+  __device__ static float ld(const char* p, size_t i) { return reinterpret_cast<const float*>(p)[i]; }
+  __device__ static void st(char* p, size_t i, float f) { reinterpret_cast<float*>(p)[i] = f; }
+  __device__ static void unpack(uint4 v, float* f) {
+    f[0] = __uint_as_float(v.x);
+    f[1] = __uint_as_float(v.y);
+    f[2] = __uint_as_float(v.z);
+    f[3] = __uint_as_float(v.w);
+  }
+  __device__ static uint4 pack(const float* f) {
+    return make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3]));
+  }
+};
+// OCP fp8 (gfx950 converts natively; FP8_E5M2 = "bf8" in the ISA).
+template <bool E5M2>
+struct Fp8 {
+  static constexpr int N = 16;
+  __device__ static float cvt(uint32_t w, int sel) {
+    if constexpr (E5M2) {
+      switch (sel) {
+        case 0: return __builtin_amdgcn_cvt_f32_bf8(w, 0);
+        case 1: return __builtin_amdgcn_cvt_f32_bf8(w, 1);
+        case 2: return __builtin_amdgcn_cvt_f32_bf8(w, 2);
+        default: return __builtin_amdgcn_cvt_f32_bf8(w, 3);
+      }
+    } else {
+      switch (sel) {
+        case 0: return __builtin_amdgcn_cvt_f32_fp8(w, 0);
+        case 1: return __builtin_amdgcn_cvt_f32_fp8(w, 1);
+        case 2: return __builtin_amdgcn_cvt_f32_fp8(w, 2);
+        default: return __builtin_amdgcn_cvt_f32_fp8(w, 3);
+      }
+    }
+  }
+  __device__ static uint32_t pk(float a, float b, float c, float d) {
+    int r;
+    if constexpr (E5M2) {
+      r = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+      r = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, r, true);
+    } else {
+      r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+      r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
+    }
+    return static_cast<uint32_t>(r);
+  }
+  __device__ static float ld(const char* p, size_t i) { return cvt(reinterpret_cast<const uint8_t*>(p)[i], 0); }
+  __device__ static void st(char* p, size_t i, float f) {
+    reinterpret_cast<uint8_t*>(p)[i] = static_cast<uint8_t>(pk(f, f, f, f) & 0xffu);
+  }
+  __device__ static void unpack(uint4 v, float* f) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f[4 * k + 0] = cvt(w[k], 0);
+      f[4 * k + 1] = cvt(w[k], 1);
+      f[4 * k + 2] = cvt(w[k], 2);
+      f[4 * k + 3] = cvt(w[k], 3);
+    }
+  }
+  __device__ static uint4 pack(const float* f) {
+    return make_uint4(pk(f[0], f[1], f[2], f[3]), pk(f[4], f[5], f[6], f[7]), pk(f[8], f[9], f[10], f[11]),
+                      pk(f[12], f[13], f[14], f[15]));
+  }
+};
+template <>
+struct Elt<DType::FP8_E4M3> : Fp8<false> {};
+template <>
+struct Elt<DType::FP8_E5M2> : Fp8<true> {};
+
+// out[i] = sum over srcs of vector i, for i in [lo, hi).
+template <DType D>
+__device__ __forceinline__ void reduce_vec(uint4* out, const uint4* const* srcs, int ns, size_t lo, size_t hi) {
+  using E = Elt<D>;
+  for (size_t i = lo + threadIdx.x; i < hi; i += T) {
+    float acc[E::N], f[E::N];
+    E::unpack(srcs[0][i], acc);
+    for (int s = 1; s < ns; ++s) {
+      E::unpack(srcs[s][i], f);
+#pragma unroll
+      for (int k = 0; k < E::N; ++k) acc[k] += f[k];
+    }
+    out[i] = E::pack(acc);
+  }
+}
+
+// Element tail [e0, e1) (elements), last block only.
+template <DType D>
+__device__ __forceinline__ void reduce_tail(char* out, const char* const* srcs, int ns, size_t e0, size_t e1) {
+  using E = Elt<D>;
+  if (blockIdx.x != gridDim.x - 1) return;
+  for (size_t i = e0 + threadIdx.x; i < e1; i += T) {
+    float a = 0.f;
+    for (int s = 0; s < ns; ++s) a += E::ld(srcs[s], i);
+    E::st(out, i, a);
+  }
+}
+
+// --------------------------------------------------------------- kernels
+
+__device__ __forceinline__ int peer_at(const Peers& P, int j) { return (P.rank + j) % P.nranks; }
+
+__global__ void __launch_bounds__(T) ag_kernel(Peers P, CollPiece c) {
+  const size_t nv = c.bytes / 16;
+  size_t lo, hi;
+  blk_range(nv, lo, hi);
+  char* own = c.recv + static_cast<size_t>(P.rank) * c.recv_stride;
+  const bool in_place = own == c.send;
+  // push my block into slot[rank] of every peer's window (+ my own recv)
+  for (size_t i = lo + threadIdx.x; i < hi; i += T) {
+    uint4 v = V(c.send)[i];
+    for (int j = 1; j < P.nranks; ++j) V(P.win[peer_at(P, j)] + c.region + c.slot * P.rank)[i] = v;
+    if (!in_place) V(own)[i] = v;
+  }
+  for (int j = 1; j < P.nranks; ++j) copy_tail(P.win[peer_at(P, j)] + c.region + c.slot * P.rank, c.send, nv * 16, c.bytes);
+  if (!in_place) copy_tail(own, c.send, nv * 16, c.bytes);
+  exchange(P, 0, c.epoch);
+  for (int j = 1; j < P.nranks; ++j) {
+    const int src = peer_at(P, P.nranks - j);
+    const char* w = P.win[P.rank] + c.region + c.slot * src;
+    char* d = c.recv + static_cast<size_t>(src) * c.recv_stride;
+    copy_vec(V(d), V(w), lo, hi);
+    copy_tail(d, w, nv * 16, c.bytes);
+  }
+}
+
+__global__ void __launch_bounds__(T) a2a_kernel(Peers P, CollPiece c) {
+  const size_t nv = c.bytes / 16;
+  size_t lo, hi;
+  blk_range(nv, lo, hi);
+  for (int j = 1; j < P.nranks; ++j) {
+    const int p = peer_at(P, j);
+    char* w = P.win[p] + c.region + c.slot * P.rank;
+    const char* s = c.send + static_cast<size_t>(p) * c.send_stride;
+    copy_vec(V(w), V(s), lo, hi);
+    copy_tail(w, s, nv * 16, c.bytes);
+  }
+  {
+    char* d = c.recv + static_cast<size_t>(P.rank) * c.recv_stride;
+    const char* s = c.send + static_cast<size_t>(P.rank) * c.send_stride;
+    copy_vec(V(d), V(s), lo, hi);
+    copy_tail(d, s, nv * 16, c.bytes);
+  }
+  exchange(P, 0, c.epoch);
+  for (int j = 1; j < P.nranks; ++j) {
+    const int src = peer_at(P, P.nranks - j);
+    const char* w = P.win[P.rank] + c.region + c.slot * src;
+    char* d = c.recv + static_cast<size_t>(src) * c.recv_stride;
+    copy_vec(V(d), V(w), lo, hi);
+    copy_tail(d, w, nv * 16, c.bytes);
+  }
+}
+
+template <DType D>
+__global__ void __launch_bounds__(T) rs_kernel(Peers P, CollPiece c) {
+  const size_t es = sizeof(uint4) / Elt<D>::N;
+  const size_t nv = c.bytes / 16;
+  size_t lo, hi;
+  blk_range(nv, lo, hi);
+  for (int j = 1; j < P.nranks; ++j) {
+    const int p = peer_at(P, j);
+    char* w = P.win[p] + c.region + c.slot * P.rank;
+    const char* s = c.send + static_cast<size_t>(p) * c.send_stride;
+    copy_vec(V(w), V(s), lo, hi);
+    copy_tail(w, s, nv * 16, c.bytes);
+  }
+  exchange(P, 0, c.epoch);
+  const uint4* srcs[kMaxRanks];
+  const char* srcb[kMaxRanks];
+  srcb[0] = c.send + static_cast<size_t>(P.rank) * c.send_stride;
+  for (int j = 1; j < P.nranks; ++j) srcb[j] = P.win[P.rank] + c.region + c.slot * peer_at(P, j);
+  for (int j = 0; j < P.nranks; ++j) srcs[j] = V(srcb[j]);
+  reduce_vec<D>(V(c.recv), srcs, P.nranks, lo, hi);
+  reduce_tail<D>(c.recv, srcb, P.nranks, nv * 16 / es, c.bytes / es);
+}
+
+template <DType D>
+__global__ void __launch_bounds__(T) ar1_kernel(Peers P, CollPiece c) {
+  const size_t es = sizeof(uint4) / Elt<D>::N;
+  const size_t nv = c.bytes / 16;
+  size_t lo, hi;
+  blk_range(nv, lo, hi);
+  for (size_t i = lo + threadIdx.x; i < hi; i += T) {
+    uint4 v = V(c.send)[i];
+    for (int j = 1; j < P.nranks; ++j) V(P.win[peer_at(P, j)] + c.region + c.slot * P.rank)[i] = v;
+  }
+  for (int j = 1; j < P.nranks; ++j) copy_tail(P.win[peer_at(P, j)] + c.region + c.slot * P.rank, c.send, nv * 16, c.bytes);
+  exchange(P, 0, c.epoch);
+  // every rank sums in the same (rank) order -> bitwise identical results
+  const uint4* srcs[kMaxRanks];
+  const char* srcb[kMaxRanks];
+  for (int r = 0; r < P.nranks; ++r) srcb[r] = r == P.rank ? c.send : P.win[P.rank] + c.region + c.slot * r;
+  for (int r = 0; r < P.nranks; ++r) srcs[r] = V(srcb[r]);
+  reduce_vec<D>(V(c.recv), srcs, P.nranks, lo, hi);
+  reduce_tail<D>(c.recv, srcb, P.nranks, nv * 16 / es, c.bytes / es);
+}
+
+// Two-shot (reduce-scatter + all-gather inside one kernel). c.bytes is a
+// multiple of 16; chunk p = vectors [p*cv, min((p+1)*cv, nv)).
+template <DType D>
+__global__ void __launch_bounds__(T) ar2_kernel(Peers P, CollPiece c) {
+  const size_t nv = c.bytes / 16;
+  const size_t cv = (nv + P.nranks - 1) / P.nranks;
+  size_t lo, hi;  // this block's slice of a chunk
+  blk_range(cv, lo, hi);
+  auto chunk_hi = [&](int p, size_t h) { return min(h, nv > p * cv ? nv - p * cv : size_t(0)); };
+  // 1. chunk p -> peer p's RS slot[rank]
+  for (int j = 1; j < P.nranks; ++j) {
+    const int p = peer_at(P, j);
+    copy_vec(V(P.win[p] + c.region + c.slot * P.rank), V(c.send) + p * cv, lo, chunk_hi(p, hi));
+  }
+  exchange(P, 0, c.epoch);
+  // 2. reduce my chunk (rank order), write it to recv and to every peer's AG slot[rank]
+  const uint4* srcs[kMaxRanks];
+  for (int r = 0; r < P.nranks; ++r)
+    srcs[r] = r == P.rank ? V(c.send) + P.rank * cv : V(P.win[P.rank] + c.region + c.slot * r);
+  uint4* outs[kMaxRanks];
+  for (int j = 1; j < P.nranks; ++j) outs[j - 1] = V(P.win[peer_at(P, j)] + c.region + c.ag_off + c.slot * P.rank);
+  // srcs are chunk-relative; recv chunk rank
+  {
+    using E = Elt<D>;
+    const size_t h = chunk_hi(P.rank, hi);
+    uint4* out = V(c.recv) + P.rank * cv;
+    for (size_t i = lo + threadIdx.x; i < h; i += T) {
+      float acc[E::N], f[E::N];
+      E::unpack(srcs[0][i], acc);
+      for (int s = 1; s < P.nranks; ++s) {
+        E::unpack(srcs[s][i], f);
+#pragma unroll
+        for (int k = 0; k < E::N; ++k) acc[k] += f[k];
+      }
+      uint4 r = E::pack(acc);
+      out[i] = r;
+      for (int o = 0; o + 1 < P.nranks; ++o) outs[o][i] = r;
+    }
+  }
+  exchange(P, 1, c.epoch);
+  // 3. copy the peers' reduced chunks out of my AG slots
+  for (int j = 1; j < P.nranks; ++j) {
+    const int src = peer_at(P, P.nranks - j);
+    copy_vec(V(c.recv) + src * cv, V(P.win[P.rank] + c.region + c.ag_off + c.slot * src), lo, chunk_hi(src, hi));
+  }
+}
+
+__global__ void __launch_bounds__(T) send_kernel(Peers P, const char* buf, size_t bytes, int dst, size_t off,
+                                                 uint32_t n) {
+  if (threadIdx.x == 0 && n > 2) wait_geq(P.flags[P.rank] + kFlagP2PConsumed + dst, n - 2, P);
+  __syncthreads();
+  const size_t nv = bytes / 16;
+  size_t lo, hi;
+  blk_range(nv, lo, hi);
+  char* w = P.win[dst] + off;
+  copy_vec(V(w), V(buf), lo, hi);
+  copy_tail(w, buf, nv * 16, bytes);
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) sys_store(P.flags[dst] + kFlagP2PSeq + static_cast<size_t>(P.rank) * kMaxBlocks + blockIdx.x, n);
+}
+
+__global__ void __launch_bounds__(T) recv_kernel(Peers P, char* buf, size_t bytes, int src, size_t off, uint32_t n,
+                                                 uint32_t target) {
+  if (threadIdx.x == 0) wait_geq(P.flags[P.rank] + kFlagP2PSeq + static_cast<size_t>(src) * kMaxBlocks + blockIdx.x, n, P);
+  __syncthreads();
+  const size_t nv = bytes / 16;
+  size_t lo, hi;
+  blk_range(nv, lo, hi);
+  const char* w = P.win[P.rank] + off;
+  copy_vec(V(buf), V(w), lo, hi);
+  copy_tail(buf, w, nv * 16, bytes);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t old = atomicAdd(P.flags[P.rank] + kFlagP2PCount + src, 1u);
+    if (old + 1 == target) sys_store(P.flags[src] + kFlagP2PConsumed + P.rank, n);
+  }
+}
+
+#define DLNB_XGMI_TYPED(KERNEL)                                                                       \
+  switch (c.dtype) {                                                                                 \
+    case DType::BF16: KERNEL<DType::BF16><<<blocks, T, 0, s>>>(p, c); break;                         \
+    case DType::FP16: KERNEL<DType::FP16><<<blocks, T, 0, s>>>(p, c); break;                         \
+    case DType::FP32: KERNEL<DType::FP32><<<blocks, T, 0, s>>>(p, c); break;                         \
+    case DType::FP8_E4M3: KERNEL<DType::FP8_E4M3><<<blocks, T, 0, s>>>(p, c); break;                 \
+    case DType::FP8_E5M2: KERNEL<DType::FP8_E5M2><<<blocks, T, 0, s>>>(p, c); break;                 \
+  }
+
+}  // namespace
+
+int blocks_for(size_t bytes, int max_blocks) {
+  // ~64 KB per block (512 threads x 16 B x 8) keeps enough stores in flight
+  // per CU; small messages use few blocks (fewer flags to exchange).
+  size_t b = (bytes + 65535) / 65536;
+  if (b < 1) b = 1;
+  if (b > static_cast<size_t>(max_blocks)) b = static_cast<size_t>(max_blocks);
+  if (b > static_cast<size_t>(kMaxBlocks)) b = kMaxBlocks;
+  return static_cast<int>(b);
+}
+
+void launch_coll(Op op, const Peers& p, const CollPiece& c, int blocks, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  DLNB_REQUIRE(blocks >= 1 && blocks <= kMaxBlocks, "xgmi: bad block count " << blocks);
+  DLNB_REQUIRE(p.nranks >= 1 && p.nranks <= kMaxRanks, "xgmi: bad group size " << p.nranks);
+  switch (op) {
+    case Op::AllGather: ag_kernel<<<blocks, T, 0, s>>>(p, c); break;
+    case Op::AllToAll: a2a_kernel<<<blocks, T, 0, s>>>(p, c); break;
+    case Op::ReduceScatter: DLNB_XGMI_TYPED(rs_kernel) break;
+    case Op::AllReduceOneShot: DLNB_XGMI_TYPED(ar1_kernel) break;
+    case Op::AllReduceTwoShot:
+      DLNB_REQUIRE(c.bytes % 16 == 0, "xgmi: two-shot piece must be a multiple of 16 B");
+      DLNB_XGMI_TYPED(ar2_kernel) break;
+  }
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
+void launch_send(const Peers& p, const char* buf, size_t bytes, int dst, size_t off, uint32_t n, int blocks,
+                 void* stream) {
+  send_kernel<<<blocks, T, 0, static_cast<hipStream_t>(stream)>>>(p, buf, bytes, dst, off, n);
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
+void launch_recv(const Peers& p, char* buf, size_t bytes, int src, size_t off, uint32_t n, uint32_t target,
+                 int blocks, void* stream) {
+  recv_kernel<<<blocks, T, 0, static_cast<hipStream_t>(stream)>>>(p, buf, bytes, src, off, n, target);
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace xgmi
+}  // namespace dlnb

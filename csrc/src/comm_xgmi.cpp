@@ -1,0 +1,345 @@
+// "xgmi" backend: our own collective / P2P kernels over IPC-mapped peer
+// windows (protocol and kernels: dlnb/xgmi.hpp, csrc/kernels/xgmi.hip).
+//
+// Setup per communicator: each member allocates its window + flag array in
+// uncached device memory, publishes hipIpcMemHandles through the job's TCP
+// store and opens every peer's handles; the members must share one node
+// (xGMI). Each operation is cut into pieces that fit one parity region of
+// the windows and each piece is one kernel on the caller's stream, tagged
+// with a per-communicator epoch (identical on all members because every
+// member issues the same sequence of operations on a communicator - the
+// same rule RCCL has). Ops on one communicator must be stream-ordered.
+//
+// Selection: --backend xgmi (GPU only). Several ranks may share one GPU
+// (-d 0,0): IPC works within a device, which is how the kernels are tested
+// on a 1-GPU machine; RCCL refuses that configuration.
+//
+// Tunables (env): DLNB_XGMI_REGION_MB (per-parity collective region, default
+// 256), DLNB_XGMI_P2P_MB (per-source, per-parity P2P slot, default 128),
+// DLNB_XGMI_BLOCKS (max blocks per kernel, default 64),
+// DLNB_XGMI_ONESHOT_KB (all-reduce one-shot threshold, default 256),
+// DLNB_XGMI_TIMEOUT_S (device-side wait timeout, default 600).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <sstream>
+
+#include "dlnb/comm.hpp"
+#include "dlnb/xgmi.hpp"
+
+#define DLNB_HIP_CHECK(expr)                                                       \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) DLNB_THROW(#expr << " failed: " << hipGetErrorString(e_)); \
+  } while (0)
+
+namespace dlnb {
+
+namespace {
+
+using xgmi::CollPiece;
+using xgmi::Op;
+
+size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+std::string hex(const void* p, size_t n) {
+  static const char* d = "0123456789abcdef";
+  std::string s;
+  const unsigned char* b = static_cast<const unsigned char*>(p);
+  for (size_t i = 0; i < n; ++i) {
+    s += d[b[i] >> 4];
+    s += d[b[i] & 15];
+  }
+  return s;
+}
+
+void unhex(const std::string& s, void* p, size_t n) {
+  DLNB_REQUIRE(s.size() == 2 * n, "xgmi: bad handle encoding");
+  auto v = [](char c) { return c <= '9' ? c - '0' : c - 'a' + 10; };
+  unsigned char* b = static_cast<unsigned char*>(p);
+  for (size_t i = 0; i < n; ++i) b[i] = static_cast<unsigned char>(v(s[2 * i]) << 4 | v(s[2 * i + 1]));
+}
+
+hipStream_t hs(Stream& s) { return static_cast<hipStream_t>(s.native()); }
+
+class XgmiComm : public Communicator {
+ public:
+  XgmiComm(const std::string& name, const std::vector<int>& members, int my_world_rank, HostGroup& world,
+           size_t capacity, bool p2p) {
+    name_ = name;
+    members_ = members;
+    size_ = static_cast<int>(members.size());
+    rank_ = -1;
+    for (int i = 0; i < size_; ++i)
+      if (members[i] == my_world_rank) rank_ = i;
+    DLNB_REQUIRE(rank_ >= 0, "rank " << my_world_rank << " is not a member of group " << name);
+    DLNB_REQUIRE(size_ <= xgmi::kMaxRanks, "xgmi backend: group " << name << " has " << size_ << " ranks (max "
+                                                                 << xgmi::kMaxRanks << ", one node)");
+    max_blocks_ = static_cast<int>(std::max<long long>(1, std::min<long long>(xgmi::kMaxBlocks, env_int("DLNB_XGMI_BLOCKS", 64))));
+    oneshot_ = static_cast<size_t>(env_int("DLNB_XGMI_ONESHOT_KB", 256)) << 10;
+    const size_t cap = std::max<size_t>(capacity, 4096);
+    // Collective region per parity: AG/RS/A2A need W slots of a piece, the
+    // two-shot all-reduce 2W slots of a chunk (~2 x piece).
+    region_ = p2p ? (size_t(1) << 20)
+                  : std::min(round_up(2 * cap + 2 * size_ * 256, 1 << 20),
+                             static_cast<size_t>(env_int("DLNB_XGMI_REGION_MB", 256)) << 20);
+    p2p_slot_ = p2p ? std::min(round_up(cap, 256), static_cast<size_t>(env_int("DLNB_XGMI_P2P_MB", 128)) << 20) : 0;
+    p2p_off_ = 2 * region_;
+    win_bytes_ = p2p_off_ + static_cast<size_t>(size_) * 2 * p2p_slot_;
+
+    DLNB_HIP_CHECK(hipGetDevice(&dev_));
+    // Uncached by default (peers' xGMI stores are never shadowed by a stale
+    // L2 line); DLNB_XGMI_MEM=fine|coarse for experiments.
+    const std::string mem = env_or("DLNB_XGMI_MEM", "uncached");
+    const unsigned flags = mem == "coarse" ? hipDeviceMallocDefault
+                           : mem == "fine" ? hipDeviceMallocFinegrained
+                                           : hipDeviceMallocUncached;
+    DLNB_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&win_), win_bytes_, flags));
+    DLNB_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), xgmi::kFlagBytes, flags));
+    DLNB_HIP_CHECK(hipMemset(flags_, 0, xgmi::kFlagBytes));
+    DLNB_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_words_), 64, hipHostMallocMapped));
+    std::memset(host_words_, 0, 64);
+    uint32_t* dev_words = nullptr;
+    DLNB_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&dev_words), host_words_, 0));
+    DLNB_HIP_CHECK(hipDeviceSynchronize());
+
+    // Exchange IPC handles (and host names: the group must share a node).
+    hipIpcMemHandle_t hw, hf;
+    DLNB_HIP_CHECK(hipIpcGetMemHandle(&hw, win_));
+    DLNB_HIP_CHECK(hipIpcGetMemHandle(&hf, flags_));
+    std::ostringstream key;
+    key << "xgmi/" << name << "/";
+    for (int m : members) key << m << ",";
+    const std::string me = get_hostname() + " " + hex(&hw, sizeof(hw)) + " " + hex(&hf, sizeof(hf));
+    world.store().set(key.str() + std::to_string(rank_), me);
+    std::memset(&peers_, 0, sizeof(peers_));
+    for (int r = 0; r < size_; ++r) {
+      if (r == rank_) {
+        peers_.win[r] = win_;
+        peers_.flags[r] = flags_;
+        continue;
+      }
+      std::istringstream in(world.store().get(key.str() + std::to_string(r)));
+      std::string host, sw, sf;
+      in >> host >> sw >> sf;
+      DLNB_REQUIRE(host == get_hostname(), "xgmi backend: group " << name << " spans hosts (" << host << " and "
+                                                                  << get_hostname() << "); use --backend rccl");
+      hipIpcMemHandle_t pw, pf;
+      unhex(sw, &pw, sizeof(pw));
+      unhex(sf, &pf, sizeof(pf));
+      void* a = nullptr;
+      void* b = nullptr;
+      DLNB_HIP_CHECK(hipIpcOpenMemHandle(&a, pw, hipIpcMemLazyEnablePeerAccess));
+      DLNB_HIP_CHECK(hipIpcOpenMemHandle(&b, pf, hipIpcMemLazyEnablePeerAccess));
+      peers_.win[r] = static_cast<char*>(a);
+      peers_.flags[r] = static_cast<uint32_t*>(b);
+      opened_.push_back(a);
+      opened_.push_back(b);
+    }
+    peers_.abort_word = dev_words;
+    peers_.error_word = dev_words + 16;
+    peers_.timeout_ticks = static_cast<uint64_t>(env_int("DLNB_XGMI_TIMEOUT_S", 600)) * 100000000ull;
+    peers_.rank = rank_;
+    peers_.nranks = size_;
+    // Nobody may free its window before every member has mapped it.
+    const std::string done = key.str() + "opened";
+    if (world.store().add(done, 1) == size_) world.store().set(done + "/go", "1");
+    world.store().get(done + "/go");
+    sent_.assign(static_cast<size_t>(size_), 0);
+    recvd_.assign(static_cast<size_t>(size_), 0);
+    recv_blocks_.assign(static_cast<size_t>(size_), 0);
+  }
+
+  ~XgmiComm() override {
+    (void)hipDeviceSynchronize();
+    for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
+    if (win_) (void)hipFree(win_);
+    if (flags_) (void)hipFree(flags_);
+    if (host_words_) (void)hipHostFree(host_words_);
+  }
+
+  std::string backend_name() const override { return "XGMI"; }
+
+  void all_gather(const void* send, void* recv, size_t send_count, DType t, Stream& s) override {
+    const size_t es = dtype_size(t), bytes = send_count * es;
+    const size_t piece = piece_bytes(region_ / size_, es);
+    for (size_t off = 0; off < bytes; off += piece) {
+      CollPiece c = base(t);
+      c.bytes = std::min(piece, bytes - off);
+      c.send = static_cast<const char*>(send) + off;
+      c.recv = static_cast<char*>(recv) + off;
+      c.recv_stride = bytes;
+      c.slot = round_up(c.bytes, 256);
+      launch(Op::AllGather, c, s);
+    }
+  }
+
+  void reduce_scatter(const void* send, void* recv, size_t recv_count, DType t, Stream& s) override {
+    const size_t es = dtype_size(t), bytes = recv_count * es;
+    const size_t piece = piece_bytes(region_ / size_, es);
+    for (size_t off = 0; off < bytes; off += piece) {
+      CollPiece c = base(t);
+      c.bytes = std::min(piece, bytes - off);
+      c.send = static_cast<const char*>(send) + off;
+      c.recv = static_cast<char*>(recv) + off;
+      c.send_stride = bytes;
+      c.slot = round_up(c.bytes, 256);
+      launch(Op::ReduceScatter, c, s);
+    }
+  }
+
+  void all_to_all(const void* send, void* recv, size_t count, DType t, Stream& s) override {
+    DLNB_REQUIRE(send != recv, "xgmi all_to_all is out-of-place only");
+    const size_t es = dtype_size(t), bytes = count * es;
+    const size_t piece = piece_bytes(region_ / size_, es);
+    for (size_t off = 0; off < bytes; off += piece) {
+      CollPiece c = base(t);
+      c.bytes = std::min(piece, bytes - off);
+      c.send = static_cast<const char*>(send) + off;
+      c.recv = static_cast<char*>(recv) + off;
+      c.send_stride = c.recv_stride = bytes;
+      c.slot = round_up(c.bytes, 256);
+      launch(Op::AllToAll, c, s);
+    }
+  }
+
+  void all_reduce(const void* send, void* recv, size_t count, DType t, Stream& s) override {
+    const size_t es = dtype_size(t), bytes = count * es;
+    const char* sp = static_cast<const char*>(send);
+    char* rp = static_cast<char*>(recv);
+    if (size_ == 1) {
+      if (send != recv) DLNB_HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, hs(s)));
+      return;
+    }
+    // One-shot for latency-bound sizes: every rank pushes the whole buffer.
+    const size_t one_max = std::min(oneshot_, piece_bytes(region_ / size_, es));
+    if (bytes <= one_max) {
+      CollPiece c = base(t);
+      c.bytes = bytes;
+      c.send = sp;
+      c.recv = rp;
+      c.slot = round_up(bytes, 256);
+      launch(Op::AllReduceOneShot, c, s);
+      return;
+    }
+    // Two-shot on 16-B multiples; a ragged tail (< 16 B) goes one-shot.
+    const size_t body = bytes / 16 * 16;
+    // chunk = ceil(piece / W) rounded to 256 B per slot: 2 W slots < region
+    const size_t piece = std::max<size_t>(16 * size_, (region_ / 2 - size_ * 512) / 16 * 16);
+    for (size_t off = 0; off < body; off += piece) {
+      CollPiece c = base(t);
+      c.bytes = std::min(piece, body - off);
+      c.send = sp + off;
+      c.recv = rp + off;
+      const size_t chunk = (c.bytes / 16 + size_ - 1) / size_ * 16;
+      c.slot = round_up(chunk, 256);
+      c.ag_off = c.slot * size_;
+      launch(Op::AllReduceTwoShot, c, s);
+    }
+    if (body < bytes) {
+      CollPiece c = base(t);
+      c.bytes = bytes - body;
+      c.send = sp + body;
+      c.recv = rp + body;
+      c.slot = 256;
+      launch(Op::AllReduceOneShot, c, s);
+    }
+  }
+
+  void send(const void* buf, size_t count, DType t, int peer, Stream& s) override {
+    DLNB_REQUIRE(p2p_slot_ > 0, "xgmi: communicator " << name_ << " was created without point-to-point support");
+    DLNB_REQUIRE(peer >= 0 && peer < size_ && peer != rank_, "xgmi: bad peer " << peer);
+    const size_t bytes = count * dtype_size(t);
+    for (size_t off = 0; off < bytes || (bytes == 0 && off == 0); off += p2p_slot_) {
+      const size_t n = std::min(p2p_slot_, bytes - off);
+      const uint32_t seq = ++sent_[static_cast<size_t>(peer)];
+      const size_t woff = p2p_off_ + (static_cast<size_t>(rank_) * 2 + (seq & 1)) * p2p_slot_;
+      xgmi::launch_send(peers_, static_cast<const char*>(buf) + off, n, peer, woff, seq,
+                        xgmi::blocks_for(n, max_blocks_), hs(s));
+      if (bytes == 0) break;
+    }
+  }
+
+  void recv(void* buf, size_t count, DType t, int peer, Stream& s) override {
+    DLNB_REQUIRE(p2p_slot_ > 0, "xgmi: communicator " << name_ << " was created without point-to-point support");
+    DLNB_REQUIRE(peer >= 0 && peer < size_ && peer != rank_, "xgmi: bad peer " << peer);
+    const size_t bytes = count * dtype_size(t);
+    for (size_t off = 0; off < bytes || (bytes == 0 && off == 0); off += p2p_slot_) {
+      const size_t n = std::min(p2p_slot_, bytes - off);
+      const uint32_t seq = ++recvd_[static_cast<size_t>(peer)];
+      const int nb = xgmi::blocks_for(n, max_blocks_);
+      recv_blocks_[static_cast<size_t>(peer)] += static_cast<uint32_t>(nb);
+      const size_t woff = p2p_off_ + (static_cast<size_t>(peer) * 2 + (seq & 1)) * p2p_slot_;
+      xgmi::launch_recv(peers_, static_cast<char*>(buf) + off, n, peer, woff, seq,
+                        recv_blocks_[static_cast<size_t>(peer)], nb, hs(s));
+      if (bytes == 0) break;
+    }
+  }
+
+  // Sends never wait for the matching receive (only for the receiver to have
+  // drained the message two before), so a group needs no special handling.
+  void group_start() override {}
+  void group_end() override {}
+
+  std::string async_error() override {
+    if (__atomic_load_n(host_words_ + 16, __ATOMIC_ACQUIRE))
+      return "xgmi: a device-side wait timed out in " + name_ + " (a peer died or hangs)";
+    return "";
+  }
+  void abort() override { __atomic_store_n(host_words_, 1u, __ATOMIC_RELEASE); }
+
+ private:
+  // Largest piece (bytes per rank block) fitting `slot_cap`, element aligned.
+  static size_t piece_bytes(size_t slot_cap, size_t es) {
+    size_t p = (slot_cap / 256) * 256;
+    p = p / es * es;
+    return std::max(p, es);
+  }
+  CollPiece base(DType t) {
+    CollPiece c;
+    std::memset(&c, 0, sizeof(c));
+    c.dtype = t;
+    c.epoch = ++epoch_;
+    c.region = (epoch_ & 1) * region_;
+    return c;
+  }
+  void launch(Op op, const CollPiece& c, Stream& s) {
+    xgmi::launch_coll(op, peers_, c, xgmi::blocks_for(c.bytes, max_blocks_), hs(s));
+  }
+
+  int dev_ = 0;
+  int max_blocks_ = 64;
+  size_t oneshot_ = 0, region_ = 0, p2p_slot_ = 0, p2p_off_ = 0, win_bytes_ = 0;
+  char* win_ = nullptr;
+  uint32_t* flags_ = nullptr;
+  uint32_t* host_words_ = nullptr;  // [0] abort, [16] error
+  std::vector<void*> opened_;
+  xgmi::Peers peers_;
+  uint32_t epoch_ = 0;
+  std::vector<uint32_t> sent_, recvd_, recv_blocks_;
+};
+
+class XgmiFactory : public CommFactory {
+ public:
+  XgmiFactory(HostGroup& world, Device& dev) : world_(world) {
+    DLNB_REQUIRE(dev.kind() == DeviceKind::GPU, "the xgmi backend needs a GPU device");
+  }
+  std::string backend_name() const override { return "XGMI"; }
+  std::unique_ptr<Communicator> create(const std::string& name, const std::vector<int>& members,
+                                       size_t capacity_bytes, bool need_p2p) override {
+    return std::unique_ptr<Communicator>(
+        new XgmiComm(name, members, world_.rank(), world_, capacity_bytes, need_p2p));
+  }
+
+ private:
+  HostGroup& world_;
+};
+
+}  // namespace
+
+std::unique_ptr<CommFactory> make_xgmi_factory(HostGroup& world, Device& dev) {
+  return std::unique_ptr<CommFactory>(new XgmiFactory(world, dev));
+}
+
+}  // namespace dlnb

@@ -1,0 +1,271 @@
+// dlnb commtest: correctness and bandwidth of every collective of a backend.
+//
+//   dlnb commtest [--backend auto|rccl|xgmi|cpu] [-d 0,1,..] [--dtype bf16]
+//                 [--sizes 1,7,4096,...] [--bench] [--iters N] [--warmup N]
+//
+// Check mode (default): every rank fills its buffers with exact small
+// integers v(rank, i), runs all-reduce (out-of-place and in-place),
+// all-gather, reduce-scatter, all-to-all and a ring send/recv for each size,
+// copies the results back and compares with the closed-form expectation
+// (exact in every wire dtype at <= 8 ranks). Bench mode prints algbw/busbw
+// per collective and size (nccl-tests conventions, SURVEY.md §5 "Metrics"),
+// so RCCL and the xgmi kernels can be compared on one node.
+//
+// Reference equivalent: none (DLNetBench relies on nccl-tests externally).
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <iostream>
+#include <sstream>
+
+#include "dlnb/strategy.hpp"
+
+namespace dlnb {
+
+namespace {
+
+double now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// v(rank, i) in 1..8 * 1..4 (fp8: 1): sums over <= 8 ranks are exact integers.
+float val(int rank, size_t i, DType t) {
+  if (t == DType::FP8_E4M3 || t == DType::FP8_E5M2) return 1.0f;
+  return static_cast<float>((rank % 8 + 1) * static_cast<int>(i % 4 + 1));
+}
+
+void encode(DType t, float f, void* p, size_t i) {
+  switch (t) {
+    case DType::BF16: static_cast<uint16_t*>(p)[i] = float_to_bf16(f); break;
+    case DType::FP16: static_cast<uint16_t*>(p)[i] = float_to_fp16(f); break;
+    case DType::FP32: static_cast<float*>(p)[i] = f; break;
+    case DType::FP8_E4M3: static_cast<uint8_t*>(p)[i] = float_to_fp8e4m3(f); break;
+    case DType::FP8_E5M2: static_cast<uint8_t*>(p)[i] = float_to_fp8e5m2(f); break;
+  }
+}
+
+float decode(DType t, const void* p, size_t i) {
+  switch (t) {
+    case DType::BF16: return bf16_to_float(static_cast<const uint16_t*>(p)[i]);
+    case DType::FP16: return fp16_to_float(static_cast<const uint16_t*>(p)[i]);
+    case DType::FP32: return static_cast<const float*>(p)[i];
+    case DType::FP8_E4M3: return fp8e4m3_to_float(static_cast<const uint8_t*>(p)[i]);
+    case DType::FP8_E5M2: return fp8e5m2_to_float(static_cast<const uint8_t*>(p)[i]);
+  }
+  return 0.f;
+}
+
+struct Tester {
+  Context& ctx;
+  Communicator& comm;
+  Stream& s;
+  DType t;
+  size_t es;
+  int W, me;
+  long long failures = 0;
+
+  void upload(Buffer& b, const std::vector<char>& h) {
+    ctx.dev->copy_async(b.data(), h.data(), h.size(), s);
+    s.synchronize();
+  }
+  std::vector<char> download(const Buffer& b, size_t bytes) {
+    std::vector<char> h(bytes);
+    ctx.dev->copy_async(h.data(), b.data(), bytes, s);
+    s.synchronize();
+    return h;
+  }
+  // host vector of n elements: element i = v(rank, off + i)
+  std::vector<char> pattern(int rank, size_t off, size_t n) {
+    std::vector<char> h(n * es);
+    for (size_t i = 0; i < n; ++i) encode(t, val(rank, off + i, t), h.data(), i);
+    return h;
+  }
+  void expect(const char* what, size_t n, const std::vector<char>& got, size_t i, float want) {
+    float g = decode(t, got.data(), i);
+    if (g != want) {
+      if (failures < 10)
+        std::fprintf(stderr, "[commtest] rank %d %s n=%zu: element %zu = %g, expected %g\n", me, what, n, i, g, want);
+      ++failures;
+    }
+  }
+  float sum_over_ranks(size_t i) {
+    float a = 0.f;
+    for (int r = 0; r < W; ++r) a += val(r, i, t);
+    return a;
+  }
+
+  void check(size_t n) {
+    const long long before = failures;
+    Buffer a = ctx.dev->alloc(std::max<size_t>(1, n * W * es)), b = ctx.dev->alloc(std::max<size_t>(1, n * W * es));
+    // all-reduce out of place
+    upload(a, pattern(me, 0, n));
+    comm.all_reduce(a.data(), b.data(), n, t, s);
+    auto got = download(b, n * es);
+    for (size_t i = 0; i < n; ++i) expect("all_reduce", n, got, i, sum_over_ranks(i));
+    // all-reduce in place
+    comm.all_reduce(a.data(), a.data(), n, t, s);
+    got = download(a, n * es);
+    for (size_t i = 0; i < n; ++i) expect("all_reduce(in-place)", n, got, i, sum_over_ranks(i));
+    // all-gather
+    upload(a, pattern(me, 0, n));
+    comm.all_gather(a.data(), b.data(), n, t, s);
+    got = download(b, n * W * es);
+    for (int r = 0; r < W; ++r)
+      for (size_t i = 0; i < n; ++i) expect("all_gather", n, got, r * n + i, val(r, i, t));
+    // reduce-scatter: send has W blocks of n, element j = v(me, j)
+    upload(a, pattern(me, 0, n * W));
+    comm.reduce_scatter(a.data(), b.data(), n, t, s);
+    got = download(b, n * es);
+    for (size_t i = 0; i < n; ++i) expect("reduce_scatter", n, got, i, sum_over_ranks(me * n + i));
+    // all-to-all: block p of rank r's send = v(r, p*n + i) -> recv block p on me = v(p, me*n + i)
+    upload(a, pattern(me, 0, n * W));
+    comm.all_to_all(a.data(), b.data(), n, t, s);
+    got = download(b, n * W * es);
+    for (int p = 0; p < W; ++p)
+      for (size_t i = 0; i < n; ++i) expect("all_to_all", n, got, p * n + i, val(p, me * n + i, t));
+    s.synchronize();
+    if (failures != before) std::fprintf(stderr, "[commtest] rank %d: n=%zu FAILED\n", me, n);
+  }
+
+  void check_p2p(Communicator& link, size_t n) {
+    if (W < 2) return;
+    Buffer a = ctx.dev->alloc(std::max<size_t>(1, n * es)), b = ctx.dev->alloc(std::max<size_t>(1, n * es));
+    const int next = (me + 1) % W, prev = (me + W - 1) % W;
+    for (int rep = 0; rep < 3; ++rep) {  // several messages: exercises the double-buffered slots
+      upload(a, pattern(me, static_cast<size_t>(rep), n));
+      link.group_start();
+      link.send(a.data(), n, t, next, s);
+      link.recv(b.data(), n, t, prev, s);
+      link.group_end();
+      auto got = download(b, n * es);
+      for (size_t i = 0; i < n; ++i) expect("send/recv", n, got, i, val(prev, rep + i, t));
+    }
+  }
+};
+
+}  // namespace
+
+int commtest_main(int argc, char** argv) {
+  std::string backend = "auto", devices, dtype = "bf16", sizes_s, json_path;
+  bool bench = false;
+  int iters = 20, warmup = 5;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto val = [&](const char* what) -> std::string {
+      if (i + 1 >= argc) DLNB_THROW("missing value for " << what);
+      return argv[++i];
+    };
+    if (a == "--backend") backend = val("--backend");
+    else if (a == "-d" || a == "--devices") devices = val("-d");
+    else if (a == "--dtype") dtype = val("--dtype");
+    else if (a == "--sizes") sizes_s = val("--sizes");
+    else if (a == "--bench") bench = true;
+    else if (a == "--iters") iters = std::stoi(val("--iters"));
+    else if (a == "--warmup") warmup = std::stoi(val("--warmup"));
+    else if (a == "--json") json_path = val("--json");
+    else if (a == "-h" || a == "--help") {
+      std::cout << "Usage: dlnb commtest [--backend auto|rccl|xgmi|cpu] [-d 0,1,..] [--dtype bf16|fp16|fp32|fp8_e4m3|"
+                   "fp8_e5m2]\n                     [--sizes n1,n2,..] [--bench] [--iters N] [--warmup N]\n"
+                   "  sizes are elements per rank; check mode verifies every collective exactly\n";
+      return 0;
+    } else DLNB_THROW("unknown option " << a);
+  }
+  Context ctx;
+  ctx.boot = bootstrap_from_env("");
+  backend = select_backend(ctx, backend, devices);
+  const DType t = parse_dtype(dtype);
+  const int W = ctx.world(), me = ctx.rank();
+  std::vector<size_t> sizes;
+  if (sizes_s.empty()) {
+    if (bench)
+      for (size_t n = 1024; n <= (size_t(256) << 20); n *= 4) sizes.push_back(n);
+    else
+      sizes = {1, 7, 8, 100, 4097, 65536, 300007, (size_t(1) << 21) + 5};
+  } else {
+    for (auto& x : split(sizes_s, ',')) sizes.push_back(static_cast<size_t>(std::stoull(x)));
+  }
+  size_t maxn = 1;
+  for (size_t n : sizes) maxn = std::max(maxn, n);
+  std::vector<int> all;
+  for (int r = 0; r < W; ++r) all.push_back(r);
+  const size_t es = dtype_size(t);
+  auto comm = ctx.comms->create("commtest/world", all, maxn * W * es, false);
+  auto link = ctx.comms->create("commtest/link", all, maxn * es, true);
+  auto stream = ctx.dev->create_stream(true);
+  Tester T{ctx, *comm, *stream, t, es, W, me};
+  long long total_fail = 0;
+  if (!bench) {
+    for (size_t n : sizes) {
+      T.check(n);
+      T.check_p2p(*link, n);
+    }
+    total_fail = static_cast<long long>(ctx.hg().allreduce_sum(static_cast<double>(T.failures)));
+    if (me == 0) {
+      Json j = Json::object();
+      j["commtest"] = "check";
+      j["backend"] = comm->backend_name();
+      j["world_size"] = W;
+      j["dtype"] = dtype_name(t);
+      Json sz = Json::array();
+      for (size_t n : sizes) sz.push_back(static_cast<double>(n));
+      j["sizes"] = sz;
+      j["failures"] = static_cast<double>(total_fail);
+      j["ok"] = total_fail == 0;
+      std::cout << j.dump() << std::endl;
+    }
+  } else {
+    Buffer a = ctx.dev->alloc(maxn * W * es), b = ctx.dev->alloc(maxn * W * es);
+    ctx.dev->fill_random(a.data(), maxn * W, t, 7 + me, *stream);
+    stream->synchronize();
+    struct K {
+      const char* name;
+      CollKind kind;
+    };
+    const K kinds[] = {{"all_reduce", CollKind::AllReduce},
+                       {"all_gather", CollKind::AllGather},
+                       {"reduce_scatter", CollKind::ReduceScatter},
+                       {"all_to_all", CollKind::AllToAll}};
+    for (size_t n : sizes) {
+      for (const K& k : kinds) {
+        auto op = [&] {
+          switch (k.kind) {
+            case CollKind::AllReduce: comm->all_reduce(a.data(), b.data(), n, t, *stream); break;
+            case CollKind::AllGather: comm->all_gather(a.data(), b.data(), n, t, *stream); break;
+            case CollKind::ReduceScatter: comm->reduce_scatter(a.data(), b.data(), n, t, *stream); break;
+            default: comm->all_to_all(a.data(), b.data(), n, t, *stream); break;
+          }
+        };
+        for (int w = 0; w < warmup; ++w) op();
+        stream->synchronize();
+        ctx.hg().barrier();
+        const double t0 = now();
+        for (int it = 0; it < iters; ++it) op();
+        stream->synchronize();
+        const double dt = ctx.hg().allreduce_max(now() - t0) / iters;
+        // algorithm bytes per rank (nccl-tests): AR/RS/A2A n*W... AG output
+        double bytes = static_cast<double>(n) * es;
+        if (k.kind != CollKind::AllReduce) bytes *= W;
+        if (me == 0) {
+          Json j = Json::object();
+          j["commtest"] = "bench";
+          j["backend"] = comm->backend_name();
+          j["op"] = k.name;
+          j["world_size"] = W;
+          j["dtype"] = dtype_name(t);
+          j["count"] = static_cast<double>(n);
+          j["bytes"] = bytes;
+          j["time_us"] = dt * 1e6;
+          j["algbw_GBps"] = bytes / dt / 1e9;
+          j["busbw_GBps"] = bytes / dt / 1e9 * busbw_factor(k.kind, W);
+          std::cout << j.dump() << std::endl;
+        }
+      }
+    }
+  }
+  stream->synchronize();
+  ctx.hg().barrier();
+  ctx.hg().store().finish();
+  return total_fail == 0 ? 0 : 3;
+}
+
+}  // namespace dlnb

@@ -67,7 +67,7 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  -d, --devices LIST     comma-separated device ids indexed by local rank\n"
      << "  -m, --min_exectime S   run at least S seconds (overrides --runs)\n"
      << "  -h, --help             this help\n"
-     << "  --backend B            auto | rccl | cpu\n"
+     << "  --backend B            auto | rccl | xgmi | cpu\n"
      << "  --compute C            auto | sleep | spin | gemm | gemm-work | flops\n"
      << "  --wire-dtype T         bf16 | fp16 | fp32 | fp8 (collective element type)\n"
      << "  --compute-dtype T      auto | bf16 | fp8 (GEMM operand type for gemm/flops)\n"

@@ -171,19 +171,14 @@ bool file_exists(const std::string& p) {
 
 }  // namespace
 
-Json run_benchmark(const Options& opt) {
-  Context ctx;
-  ctx.opt = opt;
-  ctx.boot = bootstrap_from_env(opt.store_addr);
+std::string select_backend(Context& ctx, const std::string& requested, const std::string& devices) {
   const RankInfo& ri = ctx.boot->info;
-
-  // ---- backend / device (cpp/utils.hpp:62-117 set_local_device)
-  std::string backend = opt.backend;
+  std::string backend = requested;
   const int ngpu = gpu_device_count();
   if (backend == "auto") backend = ngpu > 0 ? "rccl" : "cpu";
-  if (backend == "rccl") {
-    DLNB_REQUIRE(ngpu > 0, "--backend rccl requested but no GPU is visible");
-    std::vector<int> list = parse_device_list(opt.devices);
+  if (backend == "rccl" || backend == "xgmi") {
+    DLNB_REQUIRE(ngpu > 0, "--backend " << backend << " requested but no GPU is visible");
+    std::vector<int> list = parse_device_list(devices);
     if (list.empty())
       for (int i = 0; i < ngpu; ++i) list.push_back(i);
     DLNB_REQUIRE(ri.local_rank < static_cast<int>(list.size()),
@@ -191,13 +186,24 @@ Json run_benchmark(const Options& opt) {
     int dev_index = list[static_cast<size_t>(ri.local_rank)];
     DLNB_REQUIRE(dev_index >= 0 && dev_index < ngpu, "device id " << dev_index << " out of range");
     ctx.dev = make_gpu_device(dev_index);
-    ctx.comms = make_rccl_factory(ctx.hg(), *ctx.dev);
+    ctx.comms = backend == "rccl" ? make_rccl_factory(ctx.hg(), *ctx.dev) : make_xgmi_factory(ctx.hg(), *ctx.dev);
   } else if (backend == "cpu") {
     ctx.dev = make_cpu_device();
     ctx.comms = make_shm_factory(ctx.hg(), *ctx.dev);
   } else {
-    DLNB_THROW("unknown backend '" << backend << "' (auto, rccl, cpu)");
+    DLNB_THROW("unknown backend '" << backend << "' (auto, rccl, xgmi, cpu)");
   }
+  return backend;
+}
+
+Json run_benchmark(const Options& opt) {
+  Context ctx;
+  ctx.opt = opt;
+  ctx.boot = bootstrap_from_env(opt.store_addr);
+  const RankInfo& ri = ctx.boot->info;
+
+  // ---- backend / device (cpp/utils.hpp:62-117 set_local_device)
+  const std::string backend = select_backend(ctx, opt.backend, opt.devices);
 
   // ---- workload
   std::string stats_path = opt.stats_file.empty() ? stats_path_for(opt.base_path, opt.model) : opt.stats_file;

@@ -1,0 +1,123 @@
+"""Exact collective checks (dlnb commtest) for every backend.
+
+CPU: the shared-memory backend at W = 1..4 in every wire dtype.
+GPU: RCCL at W=1, and the xgmi backend's own kernels with 2 and 4 ranks
+sharing one MI355X (-d 0,0,..: IPC within a device exercises the same
+windows, flags and kernels as across xGMI), with small windows so every
+operation is cut into many pieces. Strategies also run end to end on xgmi.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DLNB = os.path.join(ROOT, "build", "bin", "dlnb")
+
+
+def launch(n, args, env_extra=None, timeout=240):
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.update(env_extra or {})
+    cmd = [sys.executable, "-m", "dlnetbench_amd.utils.launch", "-n", str(n), "--timeout", str(timeout)] + args
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout + 30, env=env, cwd=ROOT)
+
+
+def commtest(n, *extra, env_extra=None):
+    p = launch(n, [DLNB, "commtest", *extra], env_extra)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and lines, p.stdout[-2000:] + p.stderr[-3000:]
+    return [json.loads(ln) for ln in lines]
+
+
+@pytest.mark.parametrize("w", [1, 2, 3, 4])
+@pytest.mark.parametrize("dtype", ["bf16", "fp32", "fp16", "fp8_e4m3", "fp8_e5m2"])
+def test_cpu_backend_exact(w, dtype):
+    out = commtest(w, "--backend", "cpu", "--dtype", dtype, "--sizes", "1,7,100,4097,70001")
+    assert out[0]["ok"] and out[0]["world_size"] == w and out[0]["backend"] == "CPU-SHM"
+
+
+def test_cpu_backend_bench_lines():
+    out = commtest(2, "--backend", "cpu", "--bench", "--sizes", "4096,65536", "--iters", "2", "--warmup", "1")
+    ops = {(o["op"], o["count"]) for o in out}
+    assert len(ops) == 8
+    for o in out:
+        assert o["busbw_GBps"] > 0 and o["time_us"] > 0
+
+
+def test_commtest_usage():
+    p = subprocess.run([DLNB, "commtest", "--help"], capture_output=True, text=True)
+    assert p.returncode == 0 and "commtest" in p.stdout
+    p = subprocess.run([DLNB, "commtest", "--bogus"], capture_output=True, text=True)
+    assert p.returncode == 2
+
+
+# ----------------------------------------------------------------- GPU
+
+
+def _need_gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+SMALL_WINDOWS = {"DLNB_XGMI_REGION_MB": "1", "DLNB_XGMI_P2P_MB": "1", "DLNB_XGMI_TIMEOUT_S": "60"}
+
+
+@pytest.mark.gpu
+def test_rccl_single_rank_exact():
+    _need_gpu()
+    out = commtest(1, "--backend", "rccl")
+    assert out[0]["ok"] and out[0]["backend"] == "RCCL"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,dtype", [(1, "bf16"), (2, "bf16"), (2, "fp32"), (2, "fp8_e4m3"), (4, "bf16"),
+                                     (4, "fp16"), (3, "bf16")])
+def test_xgmi_kernels_exact(w, dtype):
+    _need_gpu()
+    devs = ",".join(["0"] * w)
+    sizes = "1,7,100,4097,65536,300007,1048583"
+    out = commtest(w, "--backend", "xgmi", "-d", devs, "--dtype", dtype, "--sizes", sizes, env_extra=SMALL_WINDOWS)
+    assert out[0]["ok"] and out[0]["backend"] == "XGMI", out
+
+
+@pytest.mark.gpu
+def test_xgmi_default_windows_large_message():
+    _need_gpu()
+    out = commtest(2, "--backend", "xgmi", "-d", "0,0", "--sizes", "33554441", env_extra={"DLNB_XGMI_TIMEOUT_S": "60"})
+    assert out[0]["ok"]
+
+
+@pytest.mark.gpu
+def test_xgmi_bench_runs():
+    _need_gpu()
+    out = commtest(2, "--backend", "xgmi", "-d", "0,0", "--bench", "--sizes", "65536,4194304", "--iters", "5",
+                   "--warmup", "2", env_extra={"DLNB_XGMI_TIMEOUT_S": "60"})
+    assert len(out) == 8 and all(o["busbw_GBps"] > 0 for o in out)
+
+
+XGMI_STRATS = [
+    ("dp", "tiny_dense_8_bfloat16", ["2"], 2),
+    ("fsdp", "tiny_dense_8_bfloat16", ["4", "2"], 2),
+    ("fsdp", "tiny_dense_8_bfloat16", ["4", "2"], 4),
+    ("hybrid_2d", "tiny_dense_8_bfloat16", ["2", "4"], 2),
+    ("hybrid_3d", "tiny_dense_8_bfloat16", ["2", "2", "2"], 4),
+    ("hybrid_3d_moe", "tiny_moe_8_bfloat16", ["1", "2", "2"], 2),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy,model,params,w", XGMI_STRATS)
+def test_strategies_on_xgmi(strategy, model, params, w, tmp_path):
+    _need_gpu()
+    out = tmp_path / "r.json"
+    data = os.path.join(ROOT, "tests", "data")
+    args = [os.path.join(ROOT, "build", "bin", strategy), model, *params, data, "-w", "1", "-r", "2",
+            "--backend", "xgmi", "-d", ",".join(["0"] * w), "--compute", "sleep", "--quiet", "--json", str(out)]
+    p = launch(w, args, {"DLNB_XGMI_TIMEOUT_S": "60"})
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    d = json.loads(out.read_text())
+    assert d["global"]["backend"] == "XGMI" and len(d["ranks"]) == w
