@@ -22,11 +22,25 @@ namespace {
 
 constexpr int T = kThreads;
 
+// Flags are raised with a system-scope atomic RMW, not a store: L2 is per
+// XCD and not coherent across XCDs, and a plain (even release) store made
+// through a peer's IPC mapping can sit in the writer's L2 after the release
+// fence has written back the data before it - the waiter, polling its
+// uncached flag word, then spins until that line happens to be evicted
+// (seen as intermittent multi-second stalls with two ranks on one GPU).
+// Atomics execute at the memory side. Epochs only grow, so max == store.
 __device__ __forceinline__ void sys_store(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_fetch_max(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// Polled with an idempotent atomic RMW for the same reason: a plain
+// system-scope load can keep hitting a stale line in the poller's own XCD L2.
+// (A compare-and-swap that never matches: LLVM folds an idempotent add/or
+// into a plain load.)
 __device__ __forceinline__ uint32_t sys_load(uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  uint32_t v = 0xffffffffu;
+  __hip_atomic_compare_exchange_strong(p, &v, 0xffffffffu, __ATOMIC_ACQUIRE, __ATOMIC_ACQUIRE,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+  return v;
 }
 
 // Spin until *f >= v (wrap-safe). Every wait has an exit: the host's abort

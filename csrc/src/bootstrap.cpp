@@ -11,7 +11,9 @@
 #include <chrono>
 #include <cerrno>
 #include <cstring>
+#include <fstream>
 #include <sstream>
+#include <thread>
 
 #include "dlnb/common.hpp"
 
@@ -357,9 +359,36 @@ std::unique_ptr<Bootstrap> bootstrap_from_env(const std::string& store_addr_in) 
     b->store = std::make_shared<LocalStore>();
   } else {
     std::string addr = store_addr_in.empty() ? env_or("DLNB_STORE_ADDR", "") : store_addr_in;
+    const std::string file = env_or("DLNB_STORE_FILE", "");
     std::string host;
     int port;
-    if (!addr.empty()) {
+    if (addr.empty() && !file.empty()) {
+      // File rendezvous: rank 0 serves on an ephemeral port and publishes
+      // host:port (write + rename, so readers never see a partial file); no
+      // port is chosen ahead of time, so none can be taken in between.
+      if (ri.rank == 0) {
+        auto st = std::make_shared<TcpStore>("127.0.0.1", 0, true, timeout);
+        const std::string tmp = file + ".tmp";
+        {
+          std::ofstream f(tmp);
+          f << env_or("DLNB_STORE_HOST", "127.0.0.1") << ":" << st->port() << "\n";
+        }
+        DLNB_REQUIRE(std::rename(tmp.c_str(), file.c_str()) == 0, "cannot publish the store address to " << file);
+        b->store = st;
+      } else {
+        auto t0 = std::chrono::steady_clock::now();
+        std::string line;
+        for (;;) {
+          std::ifstream f(file);
+          if (f && std::getline(f, line) && !line.empty()) break;
+          DLNB_REQUIRE(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < timeout,
+                       "rank 0 never published the store address in " << file);
+          std::this_thread::sleep_for(std::chrono::milliseconds(20));
+        }
+        size_t c = line.rfind(':');
+        b->store = std::make_shared<TcpStore>(line.substr(0, c), std::stoi(line.substr(c + 1)), false, timeout);
+      }
+    } else if (!addr.empty()) {
       size_t c = addr.rfind(':');
       DLNB_REQUIRE(c != std::string::npos, "store address must be host:port, got " << addr);
       host = addr.substr(0, c);
@@ -368,7 +397,7 @@ std::unique_ptr<Bootstrap> bootstrap_from_env(const std::string& store_addr_in) 
       host = env_or("MASTER_ADDR", "127.0.0.1");
       port = static_cast<int>(env_int("DLNB_STORE_PORT", env_int("MASTER_PORT", 29599) + 1));
     }
-    b->store = std::make_shared<TcpStore>(host, port, ri.rank == 0, timeout);
+    if (!b->store) b->store = std::make_shared<TcpStore>(host, port, ri.rank == 0, timeout);
   }
   b->world.reset(new HostGroup(b->store, ri.rank, ri.world_size, "world"));
 

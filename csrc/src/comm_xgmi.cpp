@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <sstream>
 
@@ -247,40 +248,28 @@ class XgmiComm : public Communicator {
     }
   }
 
+  // Messages larger than a P2P slot travel as several chunks. Inside a group
+  // the chunks of all operations are issued round-robin (send chunk r, recv
+  // chunk r, ...): a send's chunk r waits for the peer to drain chunk r-2,
+  // so two ranks exchanging large messages must interleave their receives
+  // with their sends or both would stall behind their own sends.
   void send(const void* buf, size_t count, DType t, int peer, Stream& s) override {
-    DLNB_REQUIRE(p2p_slot_ > 0, "xgmi: communicator " << name_ << " was created without point-to-point support");
-    DLNB_REQUIRE(peer >= 0 && peer < size_ && peer != rank_, "xgmi: bad peer " << peer);
-    const size_t bytes = count * dtype_size(t);
-    for (size_t off = 0; off < bytes || (bytes == 0 && off == 0); off += p2p_slot_) {
-      const size_t n = std::min(p2p_slot_, bytes - off);
-      const uint32_t seq = ++sent_[static_cast<size_t>(peer)];
-      const size_t woff = p2p_off_ + (static_cast<size_t>(rank_) * 2 + (seq & 1)) * p2p_slot_;
-      xgmi::launch_send(peers_, static_cast<const char*>(buf) + off, n, peer, woff, seq,
-                        xgmi::blocks_for(n, max_blocks_), hs(s));
-      if (bytes == 0) break;
-    }
+    p2p_op(true, const_cast<void*>(buf), count * dtype_size(t), peer, s);
   }
-
   void recv(void* buf, size_t count, DType t, int peer, Stream& s) override {
-    DLNB_REQUIRE(p2p_slot_ > 0, "xgmi: communicator " << name_ << " was created without point-to-point support");
-    DLNB_REQUIRE(peer >= 0 && peer < size_ && peer != rank_, "xgmi: bad peer " << peer);
-    const size_t bytes = count * dtype_size(t);
-    for (size_t off = 0; off < bytes || (bytes == 0 && off == 0); off += p2p_slot_) {
-      const size_t n = std::min(p2p_slot_, bytes - off);
-      const uint32_t seq = ++recvd_[static_cast<size_t>(peer)];
-      const int nb = xgmi::blocks_for(n, max_blocks_);
-      recv_blocks_[static_cast<size_t>(peer)] += static_cast<uint32_t>(nb);
-      const size_t woff = p2p_off_ + (static_cast<size_t>(peer) * 2 + (seq & 1)) * p2p_slot_;
-      xgmi::launch_recv(peers_, static_cast<char*>(buf) + off, n, peer, woff, seq,
-                        recv_blocks_[static_cast<size_t>(peer)], nb, hs(s));
-      if (bytes == 0) break;
-    }
+    p2p_op(false, buf, count * dtype_size(t), peer, s);
   }
-
-  // Sends never wait for the matching receive (only for the receiver to have
-  // drained the message two before), so a group needs no special handling.
-  void group_start() override {}
-  void group_end() override {}
+  void group_start() override { in_group_ = true; }
+  void group_end() override {
+    in_group_ = false;
+    std::vector<P2POp> ops;
+    ops.swap(pending_);
+    size_t rounds = 0;
+    for (auto& o : ops) rounds = std::max(rounds, chunks(o.bytes));
+    for (size_t r = 0; r < rounds; ++r)
+      for (auto& o : ops)
+        if (r < chunks(o.bytes)) p2p_chunk(o, r);
+  }
 
   std::string async_error() override {
     if (__atomic_load_n(host_words_ + 16, __ATOMIC_ACQUIRE))
@@ -290,6 +279,43 @@ class XgmiComm : public Communicator {
   void abort() override { __atomic_store_n(host_words_, 1u, __ATOMIC_RELEASE); }
 
  private:
+  struct P2POp {
+    bool is_send;
+    char* buf;
+    size_t bytes;
+    int peer;
+    Stream* s;
+  };
+  size_t chunks(size_t bytes) const { return bytes == 0 ? 1 : (bytes + p2p_slot_ - 1) / p2p_slot_; }
+  void p2p_op(bool is_send, void* buf, size_t bytes, int peer, Stream& s) {
+    DLNB_REQUIRE(p2p_slot_ > 0, "xgmi: communicator " << name_ << " was created without point-to-point support");
+    DLNB_REQUIRE(peer >= 0 && peer < size_ && peer != rank_, "xgmi: bad peer " << peer);
+    P2POp o{is_send, static_cast<char*>(buf), bytes, peer, &s};
+    if (in_group_) {
+      pending_.push_back(o);
+      return;
+    }
+    for (size_t r = 0; r < chunks(bytes); ++r) p2p_chunk(o, r);
+  }
+  void p2p_chunk(const P2POp& o, size_t r) {
+    const size_t off = r * p2p_slot_;
+    const size_t n = o.bytes == 0 ? 0 : std::min(p2p_slot_, o.bytes - off);
+    const size_t p = static_cast<size_t>(o.peer);
+    const int nb = xgmi::blocks_for(n, max_blocks_);
+    if (o.is_send) {
+      const uint32_t seq = ++sent_[p];
+      const size_t woff = p2p_off_ + (static_cast<size_t>(rank_) * 2 + (seq & 1)) * p2p_slot_;
+      xgmi::launch_send(peers_, o.buf + off, n, o.peer, woff, seq, nb, hs(*o.s));
+      debug("send", seq, n, *o.s);
+    } else {
+      const uint32_t seq = ++recvd_[p];
+      recv_blocks_[p] += static_cast<uint32_t>(nb);
+      const size_t woff = p2p_off_ + (p * 2 + (seq & 1)) * p2p_slot_;
+      xgmi::launch_recv(peers_, o.buf + off, n, o.peer, woff, seq, recv_blocks_[p], nb, hs(*o.s));
+      debug("recv", seq, n, *o.s);
+    }
+  }
+
   // Largest piece (bytes per rank block) fitting `slot_cap`, element aligned.
   static size_t piece_bytes(size_t slot_cap, size_t es) {
     size_t p = (slot_cap / 256) * 256;
@@ -306,6 +332,25 @@ class XgmiComm : public Communicator {
   }
   void launch(Op op, const CollPiece& c, Stream& s) {
     xgmi::launch_coll(op, peers_, c, xgmi::blocks_for(c.bytes, max_blocks_), hs(s));
+    debug("coll", c.epoch, c.bytes, s);
+  }
+  // DLNB_XGMI_DEBUG=1: synchronise after every kernel and dump the flags.
+  void debug(const char* what, uint32_t tag, size_t bytes, Stream& s) {
+    static const bool on = env_int("DLNB_XGMI_DEBUG", 0) != 0;
+    if (!on) return;
+    DLNB_HIP_CHECK(hipStreamSynchronize(hs(s)));
+    std::vector<uint32_t> f(xgmi::kFlagWords);
+    DLNB_HIP_CHECK(hipMemcpy(f.data(), flags_, f.size() * 4, hipMemcpyDeviceToHost));
+    std::fprintf(stderr, "[xgmi-debug] %s r%d %s tag=%u bytes=%zu err=%u coll0=[", name_.c_str(), rank_, what, tag,
+                 bytes, host_words_[16]);
+    for (int r = 0; r < size_; ++r) std::fprintf(stderr, "%u ", f[xgmi::kFlagColl + r * xgmi::kMaxBlocks]);
+    std::fprintf(stderr, "] seq0=[");
+    for (int r = 0; r < size_; ++r) std::fprintf(stderr, "%u ", f[xgmi::kFlagP2PSeq + r * xgmi::kMaxBlocks]);
+    std::fprintf(stderr, "] consumed=[");
+    for (int r = 0; r < size_; ++r) std::fprintf(stderr, "%u ", f[xgmi::kFlagP2PConsumed + r]);
+    std::fprintf(stderr, "] count=[");
+    for (int r = 0; r < size_; ++r) std::fprintf(stderr, "%u ", f[xgmi::kFlagP2PCount + r]);
+    std::fprintf(stderr, "]\n");
   }
 
   int dev_ = 0;
@@ -318,6 +363,8 @@ class XgmiComm : public Communicator {
   xgmi::Peers peers_;
   uint32_t epoch_ = 0;
   std::vector<uint32_t> sent_, recvd_, recv_blocks_;
+  bool in_group_ = false;
+  std::vector<P2POp> pending_;
 };
 
 class XgmiFactory : public CommFactory {

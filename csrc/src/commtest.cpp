@@ -195,9 +195,23 @@ int commtest_main(int argc, char** argv) {
   Tester T{ctx, *comm, *stream, t, es, W, me};
   long long total_fail = 0;
   if (!bench) {
+    const bool verbose = env_int("DLNB_COMMTEST_VERBOSE", 0) != 0;
     for (size_t n : sizes) {
+      const double t0 = now();
+      if (verbose) std::fprintf(stderr, "[commtest] rank %d: collectives n=%zu\n", me, n);
       T.check(n);
+      const double t1 = now();
+      if (verbose) std::fprintf(stderr, "[commtest] rank %d: send/recv n=%zu (collectives took %.3f s)\n", me, n, t1 - t0);
       T.check_p2p(*link, n);
+      if (verbose) std::fprintf(stderr, "[commtest] rank %d: n=%zu send/recv took %.3f s\n", me, n, now() - t1);
+    }
+    // a device-side wait that timed out is a failure even if the data came
+    for (Communicator* c : {comm.get(), link.get()}) {
+      std::string err = c->async_error();
+      if (!err.empty()) {
+        std::fprintf(stderr, "[commtest] rank %d: %s\n", me, err.c_str());
+        ++T.failures;
+      }
     }
     total_fail = static_cast<long long>(ctx.hg().allreduce_sum(static_cast<double>(T.failures)));
     if (me == 0) {

@@ -98,8 +98,12 @@ class GpuDevice : public Device {
     hipError_t e = hipMalloc(&p, bytes);
     if (e != hipSuccess)
       DLNB_THROW("hipMalloc(" << bytes << " B) failed on device " << idx_ << ": " << hipGetErrorString(e));
-    // Zero like the reference's Tensor (proxy_classes.hpp:403-409).
+    // Zero like the reference's Tensor (proxy_classes.hpp:403-409). The
+    // memset runs on the null stream, which our non-blocking streams do not
+    // order against: finish it here, or it can land after the first copy or
+    // kernel a caller enqueues on its own stream (zeroing fresh data).
     DLNB_HIP_CHECK(hipMemset(p, 0, bytes));
+    DLNB_HIP_CHECK(hipStreamSynchronize(nullptr));
     return p;
   }
   void raw_free(void* p, size_t) override { (void)hipFree(p); }

@@ -26,14 +26,16 @@ def free_port(host: str = "127.0.0.1") -> int:
         return s.getsockname()[1]
 
 
-def rank_env(rank: int, world: int, store_addr: str, base: Optional[Dict[str, str]] = None) -> Dict[str, str]:
+def rank_env(rank: int, world: int, store_file: str, base: Optional[Dict[str, str]] = None) -> Dict[str, str]:
     env = dict(os.environ if base is None else base)
+    env.pop("DLNB_STORE_ADDR", None)
     env.update({
         "DLNB_RANK": str(rank),
         "DLNB_WORLD_SIZE": str(world),
         "DLNB_LOCAL_RANK": str(rank),
         "DLNB_LOCAL_WORLD_SIZE": str(world),
-        "DLNB_STORE_ADDR": store_addr,
+        # rank 0 serves the store on an ephemeral port and publishes it here
+        "DLNB_STORE_FILE": store_file,
         # dmabuf IPC only on this pool (RCCL / tensor sharing across processes)
         "HSA_ENABLE_IPC_MODE_LEGACY": env.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
     })
@@ -47,12 +49,15 @@ def rank_env(rank: int, world: int, store_addr: str, base: Optional[Dict[str, st
 def launch(n: int, cmd: Sequence[str], timeout: Optional[float] = None, capture: bool = False,
            env: Optional[Dict[str, str]] = None, cwd: Optional[str] = None):
     """Start n ranks of cmd; returns (exit_code, [stdout per rank] or None)."""
-    addr = f"127.0.0.1:{free_port()}"
+    import shutil
+    import tempfile
+    rdv = tempfile.mkdtemp(prefix="dlnb_rdv_")
+    store_file = os.path.join(rdv, "store")
     procs: List[subprocess.Popen] = []
     outs: List[Optional[str]] = [None] * n
     for r in range(n):
         procs.append(subprocess.Popen(
-            list(cmd), env=rank_env(r, n, addr, env), cwd=cwd,
+            list(cmd), env=rank_env(r, n, store_file, env), cwd=cwd,
             stdout=subprocess.PIPE if capture else None,
             stderr=subprocess.STDOUT if capture else None,
             start_new_session=True, text=True))
@@ -92,6 +97,8 @@ def launch(n: int, cmd: Sequence[str], timeout: Optional[float] = None, capture:
     except KeyboardInterrupt:
         _kill_all(procs)
         raise
+    finally:
+        shutil.rmtree(rdv, ignore_errors=True)
     return code, (outs if capture else None)
 
 

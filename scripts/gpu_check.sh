@@ -39,8 +39,8 @@ for step in "$@"; do
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       run pmc_gemm 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_gemm -o gemm -- python3 -m dlnetbench_amd.tools.gemm_bench --shapes 8192x14336x4096 --rounds 2 --iters 5 ;;
     xgmi)
-      run xgmi_w2 150 env DLNB_XGMI_TIMEOUT_S=30 DLNB_XGMI_REGION_MB=1 DLNB_XGMI_P2P_MB=1 python -m dlnetbench_amd.utils.launch -n 2 --timeout 120 build/bin/dlnb commtest --backend xgmi -d 0,0
-      run xgmi_w4 150 env DLNB_XGMI_TIMEOUT_S=30 python -m dlnetbench_amd.utils.launch -n 4 --timeout 120 build/bin/dlnb commtest --backend xgmi -d 0,0,0,0
+      run xgmi_w2 150 env DLNB_COMMTEST_VERBOSE=1 DLNB_XGMI_TIMEOUT_S=10 DLNB_XGMI_REGION_MB=1 DLNB_XGMI_P2P_MB=1 python -m dlnetbench_amd.utils.launch -n 2 --timeout 120 build/bin/dlnb commtest --backend xgmi -d 0,0
+      run xgmi_w4 150 env DLNB_COMMTEST_VERBOSE=1 DLNB_XGMI_TIMEOUT_S=10 python -m dlnetbench_amd.utils.launch -n 4 --timeout 120 build/bin/dlnb commtest --backend xgmi -d 0,0,0,0
       run xgmi_bench 200 env DLNB_XGMI_TIMEOUT_S=30 python -m dlnetbench_amd.utils.launch -n 2 --timeout 180 build/bin/dlnb commtest --backend xgmi -d 0,0 --bench --sizes 1024,65536,1048576,16777216,67108864
       run rccl_bench 200 build/bin/dlnb commtest --backend rccl --bench --sizes 1024,65536,1048576,16777216,67108864 ;;
     dp8) run bench_dp 300 python -m dlnetbench_amd.tools.sweep --quick ;;
