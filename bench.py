@@ -29,6 +29,7 @@ METRIC = "proxy iter time (ms) + effective GB/s, Llama-3-8B DP/FSDP at 1/2/4/8 M
 # floor (fwd + bwd of llama3_8b_16_bfloat16 = 2814.7 ms) is the number an
 # ideal overlap would hit on any hardware.
 BASELINE_MS = 2814.74976
+DEFAULT_MODEL = "llama3_8b_16_bfloat16"
 
 
 def _store_addr(world: int, rank: int) -> str:
@@ -77,7 +78,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--model", default="llama3_8b_16_bfloat16")
+    ap.add_argument("--model", default=DEFAULT_MODEL)
     ap.add_argument("--units", type=int, default=32)
     ap.add_argument("--compute", default="gemm")
     ap.add_argument("--schedule", default="overlap")
@@ -97,9 +98,19 @@ def main() -> int:
     from dlnetbench_amd import engine
     from dlnetbench_amd.utils.stats import load_stats
     st = load_stats(os.path.join(ROOT, "model_stats", a.model + ".txt"))
-    doc = engine.run("fsdp", a.model, a.units, world, base_path=ROOT, warmup=a.warmup, runs=a.steps,
-                     compute=a.compute, schedule=a.schedule, backend=a.backend, wire_dtype="bf16",
-                     store=addr or None, silent=True, json=a.json)
+    # The result line must be the only stdout line: route whatever the native
+    # libraries print (e.g. RCCL's banner) to stderr while the benchmark runs.
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        doc = engine.run("fsdp", a.model, a.units, world, base_path=ROOT, warmup=a.warmup, runs=a.steps,
+                         compute=a.compute, schedule=a.schedule, backend=a.backend, wire_dtype="bf16",
+                         store=addr or None, silent=True, json=a.json)
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
     if rank != 0:
         return 0
     g = doc["global"]
@@ -122,7 +133,7 @@ def main() -> int:
         "ms_per_step": round(ms, 3),
         "higher_is_better": False,
         "scaling": "weak",
-        "vs_baseline": round(ms / BASELINE_MS, 4),
+        "vs_baseline": round(ms / BASELINE_MS, 4) if a.model == DEFAULT_MODEL else None,
         "dtype": "bf16",
         "data": "synthetic (random-init buffers; compute = MFMA GEMM stand-in bounded to the table durations)",
         "config": {
