@@ -20,6 +20,7 @@ namespace {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
@@ -269,7 +270,11 @@ __global__ void __launch_bounds__(128 * WN, WN == 4 ? 2 : 1)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
       }
-    } else {
+    } else if constexpr (DEADLINE) {
+      // Deadline (persistent stand-in) variant: the non-scaled 16x16x32 fp8
+      // MFMA; the MX path below needs ~48 more VGPRs than the deadline
+      // bookkeeping leaves (it would spill), and a deadline kernel's rate
+      // does not change how long it runs.
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         long af[8], bfr[FN];
@@ -286,6 +291,33 @@ __global__ void __launch_bounds__(128 * WN, WN == 4 ? 2 : 1)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    } else {
+      // fp8 e4m3 through the MX-scaled MFMA (16x16x128, unit E8M0 scales =
+      // 127): one instruction covers the whole 128-byte K-tile at twice the
+      // non-scaled fp8 rate. Lane l holds 32 consecutive K bytes (chunks
+      // 2h, 2h+1) of its row; A and B use the same K order, which is all
+      // the product needs (checked exactly by scripts/probes/
+      // mfma_f8f6f4_layout.hip and tests/test_gpu_kernels.py).
+      i32x8 bfr[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn * WTN + j * 16 + r16;
+        const int4 lo = *reinterpret_cast<const int4*>(Bt + swz(row, 2 * h));
+        const int4 hi = *reinterpret_cast<const int4*>(Bt + swz(row, 2 * h + 1));
+        bfr[j] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = wm * 128 + i * 16 + r16;
+        const int4 lo = *reinterpret_cast<const int4*>(At + swz(row, 2 * h));
+        const int4 hi = *reinterpret_cast<const int4*>(At + swz(row, 2 * h + 1));
+        const i32x8 af = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af, acc[i][j], 0, 0, 0, 127, 0, 127);
         __builtin_amdgcn_s_setprio(0);
       }
     }
@@ -425,11 +457,11 @@ void dispatch_gemm(int waves, DType in_t, int grid, const void* A, const void* B
                    int lda, int ldb, int ldc, uint64_t* slot, uint32_t epoch, uint64_t ticks, uint64_t slice_end,
                    hipStream_t st) {
   const bool fp8 = in_t == DType::FP8_E4M3;
-  if (waves == 4) {
+  if (!DEADLINE && waves == 4) {  // (the 4-wave deadline variant would spill: never instantiated)
     if (fp8)
-      launch_gemm<true, DEADLINE, 2>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
+      launch_gemm<true, false, 2>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
     else
-      launch_gemm<false, DEADLINE, 2>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
+      launch_gemm<false, false, 2>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
   } else {
     if (fp8)
       launch_gemm<true, DEADLINE, 4>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
