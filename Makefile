@@ -24,7 +24,7 @@ LOOPS    := dp_loop fsdp_loop hybrid_2d_loop hybrid_3d_loop hybrid_3d_moe_loop
 LIB      := $(BUILD)/libdlnb.so
 PYLIB    := dlnetbench_amd/_lib/libdlnb.so
 
-.PHONY: all lib apps clean asan
+.PHONY: all lib apps clean asan probes
 all: lib apps
 
 lib: $(PYLIB)
@@ -53,6 +53,12 @@ $(BUILD)/bin/%: csrc/apps/%.cpp $(LIB) $(wildcard csrc/include/dlnb/*.hpp)
 # same binary switches to loop mode when invoked under a *_loop name.
 $(BUILD)/bin/%_loop: $(BUILD)/bin/%
 	ln -sf $(notdir $<) $@
+
+# Small measurement programs (scripts/probes/*.cpp) linked against the library.
+probes: $(BUILD)/bin/boundary_cost
+$(BUILD)/bin/boundary_cost: scripts/probes/boundary_cost.cpp $(LIB)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(CXXFLAGS) $< -o $@ -L$(BUILD) -ldlnb $(LDLIBS) -Wl,-rpath,'$$ORIGIN/..'
 
 # Host AddressSanitizer build of the library + binaries into build-asan/
 # (device code is not instrumented: GPU ASan is not available on the pool).
