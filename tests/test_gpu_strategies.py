@@ -49,3 +49,14 @@ def test_fsdp_llama3_8b_single_gpu_iteration(root):
     it = doc["global"]["dlnb"]["iteration"]
     assert it["median_ms"] >= 0.9 * it["compute_floor_ms"]
     assert doc["global"]["allgather_msg_size_bytes"] == 250945664 * 2
+
+
+def test_measured_stats_generator(tmp_path):
+    """models.measure times a real block on the GPU and writes a parseable table."""
+    from dlnetbench_amd.models import measure
+    from dlnetbench_amd.models.registry import get_model
+    from dlnetbench_amd.utils.stats import load_stats
+    p = measure.write_measured(str(tmp_path), get_model("vit_b"), 2, "bfloat16", reps=2)
+    st = load_stats(p)
+    assert st.fwd_us > 0 and st.bwd_us > 0 and st.num_layers == 12
+    assert "measured" in st.device
