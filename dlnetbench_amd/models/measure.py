@@ -211,7 +211,10 @@ def measure_stats(m: ModelArch, batch: int, dtype: str = "bfloat16", reps: int =
     fwd = m.layers * t_f + e_f
     bwd = m.layers * max(t_fb - t_f, 0.0) + e_b
     roof = compute_stats(m, batch, dtype if dtype in ("bfloat16", "float8") else "bfloat16", "b200")
-    name = torch.cuda.get_device_name(0)
+    props = torch.cuda.get_device_properties(0)
+    arch = getattr(props, "gcnArchName", "").split(":")[0]
+    # the marketing name is often just "AMD Radeon Graphics" (no amdgpu.ids on the box)
+    name = "AMD Instinct MI355X (gfx950)" if arch == "gfx950" else f"{torch.cuda.get_device_name(0)} ({arch})"
     st = Stats(
         forward_flops=roof.forward_flops, backward_flops=roof.backward_flops, model_size=roof.model_size,
         non_expert_size=roof.non_expert_size, fwd_us=fwd * 1e6, bwd_us=bwd * 1e6, batch=batch,
