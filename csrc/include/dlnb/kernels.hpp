@@ -41,8 +41,10 @@ int num_cus(int device);
 // dimensions in elements, 16-byte aligned rows. in_t is BF16 or FP8_E4M3;
 // C is always bf16.
 bool gemm_shape_ok(int M, int N, int K, DType in_t);
-// waves: 8 (2 per SIMD, 128x64 per wave) or 4 (1 per SIMD, 128x128 per wave);
-// 0 = the default (DLNB_GEMM_WAVES, else 8).
+// waves selects the variant: 8 = 8 waves (2 per SIMD, 128x64 per wave)
+// double buffered, 1 = the same with a 3-deep A ring (160 KiB LDS),
+// 4 = 4 waves (1 per SIMD, 128x128 per wave); 0 = the default (ring if
+// DLNB_GEMM_RING=1, else DLNB_GEMM_WAVES or 8).
 void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
              void* stream, int waves = 0);
 int gemm_default_waves();

@@ -170,6 +170,102 @@ __device__ __forceinline__ int xcd_remap(int b, int T) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
+// One 128-byte K-tile of MFMA work for a wave owning rows wm*128.. (8
+// fragments) and columns wn*WTN.. (FN fragments) of the block tile.
+template <bool FP8, bool DEADLINE, int FN, int WTN>
+__device__ __forceinline__ void ktile_mfma(const char* __restrict__ At, const char* __restrict__ Bt, f32x4 (&acc)[8][FN],
+                                           int wm, int wn, int r16, int h) {
+  if constexpr (!FP8) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[8], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(At + swz(wm * 128 + i * 16 + r16, ks * 4 + h));
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bt + swz(wn * WTN + j * 16 + r16, ks * 4 + h));
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  } else if constexpr (DEADLINE) {
+    // Deadline (persistent stand-in) variant: the non-scaled 16x16x32 fp8
+    // MFMA; the MX path below needs ~48 more VGPRs than the deadline
+    // bookkeeping leaves (it would spill), and a deadline kernel's rate
+    // does not change how long it runs.
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      long af[8], bfr[FN];
+      const int chunk = ks * 2 + (h >> 1), half = (h & 1) * 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        af[i] = *reinterpret_cast<const long*>(At + swz(wm * 128 + i * 16 + r16, chunk) + half);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = *reinterpret_cast<const long*>(Bt + swz(wn * WTN + j * 16 + r16, chunk) + half);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  } else {
+    // fp8 e4m3 through the MX-scaled MFMA (16x16x128, unit E8M0 scales =
+    // 127): one instruction covers the whole 128-byte K-tile at twice the
+    // non-scaled fp8 rate. Lane l holds 32 consecutive K bytes (chunks
+    // 2h, 2h+1) of its row; A and B use the same K order, which is all
+    // the product needs (checked exactly by scripts/probes/
+    // mfma_f8f6f4_layout.hip and tests/test_gpu_kernels.py).
+    i32x8 bfr[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int row = wn * WTN + j * 16 + r16;
+      const int4 lo = *reinterpret_cast<const int4*>(Bt + swz(row, 2 * h));
+      const int4 hi = *reinterpret_cast<const int4*>(Bt + swz(row, 2 * h + 1));
+      bfr[j] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = wm * 128 + i * 16 + r16;
+      const int4 lo = *reinterpret_cast<const int4*>(At + swz(row, 2 * h));
+      const int4 hi = *reinterpret_cast<const int4*>(At + swz(row, 2 * h + 1));
+      const i32x8 af = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af, acc[i][j], 0, 0, 0, 127, 0, 127);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+}
+
+// Epilogue: lane holds C[m = .. + (lane & 15)][n = .. + 4*(lane >> 4) + 0..3].
+template <int FN, int WTN>
+__device__ __forceinline__ void store_tile(__bf16* __restrict__ C, int ldc, int tm, int tn, int wm, int wn, int r16,
+                                           int h, const f32x4 (&acc)[8][FN]) {
+  const int m_base = tm * kTile + wm * 128 + r16;
+  const int n_base = tn * kTile + wn * WTN + 4 * h;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      bf16x4 o;
+      o[0] = static_cast<__bf16>(acc[i][j][0]);
+      o[1] = static_cast<__bf16>(acc[i][j][1]);
+      o[2] = static_cast<__bf16>(acc[i][j][2]);
+      o[3] = static_cast<__bf16>(acc[i][j][3]);
+      *reinterpret_cast<bf16x4*>(C + static_cast<size_t>(m_base + i * 16) * ldc + n_base + j * 16) = o;
+    }
+  }
+}
+
 // DEADLINE = false: one launch computes every tile once (grid = tiles).
 // DEADLINE = true : persistent stand-in compute. grid <= resident blocks;
 //   each block walks the tile space round-robin (wrapping) and the whole
@@ -252,75 +348,7 @@ __global__ void __launch_bounds__(128 * WN, WN == 4 ? 2 : 1)
     }
     const char* At = cur;
     const char* Bt = cur + kTileBytes;
-    if constexpr (!FP8) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 af[8], bfr[FN];
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          af[i] = *reinterpret_cast<const bf16x8*>(At + swz(wm * 128 + i * 16 + r16, ks * 4 + h));
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          bfr[j] = *reinterpret_cast<const bf16x8*>(Bt + swz(wn * WTN + j * 16 + r16, ks * 4 + h));
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      }
-    } else if constexpr (DEADLINE) {
-      // Deadline (persistent stand-in) variant: the non-scaled 16x16x32 fp8
-      // MFMA; the MX path below needs ~48 more VGPRs than the deadline
-      // bookkeeping leaves (it would spill), and a deadline kernel's rate
-      // does not change how long it runs.
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        long af[8], bfr[FN];
-        const int chunk = ks * 2 + (h >> 1), half = (h & 1) * 8;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          af[i] = *reinterpret_cast<const long*>(At + swz(wm * 128 + i * 16 + r16, chunk) + half);
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          bfr[j] = *reinterpret_cast<const long*>(Bt + swz(wn * WTN + j * 16 + r16, chunk) + half);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(bfr[j], af[i], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      }
-    } else {
-      // fp8 e4m3 through the MX-scaled MFMA (16x16x128, unit E8M0 scales =
-      // 127): one instruction covers the whole 128-byte K-tile at twice the
-      // non-scaled fp8 rate. Lane l holds 32 consecutive K bytes (chunks
-      // 2h, 2h+1) of its row; A and B use the same K order, which is all
-      // the product needs (checked exactly by scripts/probes/
-      // mfma_f8f6f4_layout.hip and tests/test_gpu_kernels.py).
-      i32x8 bfr[FN];
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int row = wn * WTN + j * 16 + r16;
-        const int4 lo = *reinterpret_cast<const int4*>(Bt + swz(row, 2 * h));
-        const int4 hi = *reinterpret_cast<const int4*>(Bt + swz(row, 2 * h + 1));
-        bfr[j] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int row = wm * 128 + i * 16 + r16;
-        const int4 lo = *reinterpret_cast<const int4*>(At + swz(row, 2 * h));
-        const int4 hi = *reinterpret_cast<const int4*>(At + swz(row, 2 * h + 1));
-        const i32x8 af = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bfr[j], af, acc[i][j], 0, 0, 0, 127, 0, 127);
-        __builtin_amdgcn_s_setprio(0);
-      }
-    }
+    ktile_mfma<FP8, DEADLINE, FN, WTN>(At, Bt, acc, wm, wn, r16, h);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (DEADLINE) {
       // Double-buffered flag: written before barrier kt, read after it; the
@@ -337,25 +365,76 @@ __global__ void __launch_bounds__(128 * WN, WN == 4 ? 2 : 1)
   }
   if (expired) return;  // partial tile: the stand-in result is not needed
 
-  // Epilogue: lane holds C[m = .. + (lane & 15)][n = .. + 4*(lane >> 4) + 0..3].
-  const int m_base = tm * kTile + wm * 128 + r16;
-  const int n_base = tn * kTile + wn * WTN + 4 * h;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      bf16x4 o;
-      o[0] = static_cast<__bf16>(acc[i][j][0]);
-      o[1] = static_cast<__bf16>(acc[i][j][1]);
-      o[2] = static_cast<__bf16>(acc[i][j][2]);
-      o[3] = static_cast<__bf16>(acc[i][j][3]);
-      *reinterpret_cast<bf16x4*>(C + static_cast<size_t>(m_base + i * 16) * ldc + n_base + j * 16) = o;
-    }
-  }
+  store_tile<FN, WTN>(C, ldc, tm, tn, wm, wn, r16, h, acc);
   if constexpr (!DEADLINE) return;
   }  // round
 }
 
+
+// Non-deadline GEMM with a deeper A pipeline: A in a ring of 3 K-tiles, B
+// double-buffered (5 x 32 KiB = the whole 160 KiB LDS). Each K-tile issues
+// B(k+1) then A(k+2) (4 + 4 glds per thread) and, after the MFMAs, waits
+// with a COUNTED vmcnt(4) - only A(k+2) may stay in flight - then a raw
+// s_barrier (a __syncthreads() would drain every glds with vmcnt(0),
+// cdna_hip_programming.md §5 "Pipelining across barriers"). A panels get two
+// K-tiles of latency hiding, B panels (shared by the 8 M-tiles of a tile
+// group, so mostly L2 hits) one. Slots written in iteration k held A(k-1) /
+// B(k-1), whose reads every wave finished before the barrier ending k-1.
+template <bool FP8>
+__global__ void __launch_bounds__(512, 1)
+    gemm_tn_ring_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
+                        int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[5 * kTileBytes];  // A0 A1 A2 | B0 B1
+  char* const Aring = smem;
+  char* const Bring = smem + 3 * kTileBytes;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr int NW = 8, WN = 4, FN = 4, WTN = 64;
+  const int wm = w / WN, wn = w % WN;
+  const int nt_m = M / kTile, nt_n = N / kTile, T = nt_m * nt_n;
+  const int b = xcd_remap(blockIdx.x, T);
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * nt_n;
+  const int first_m = (b / per_group) * GROUP;
+  const int gsz = min(nt_m - first_m, GROUP);
+  const int tm = first_m + (b % per_group) % gsz;
+  const int tn = (b % per_group) / gsz;
+  constexpr int esz = FP8 ? 1 : 2;
+  const size_t lda_b = static_cast<size_t>(lda) * esz, ldb_b = static_cast<size_t>(ldb) * esz;
+  const char* Ab = A + static_cast<size_t>(tm) * kTile * lda_b;
+  const char* Bb = B + static_cast<size_t>(tn) * kTile * ldb_b;
+  const int nk = (K * esz) / kRowBytes;
+
+  f32x4 acc[8][FN];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage_tile<NW>(Ab, lda_b, Aring, w, lane);
+  stage_tile<NW>(Bb, ldb_b, Bring, w, lane);
+  if (nk > 1) {
+    stage_tile<NW>(Ab + kRowBytes, lda_b, Aring + kTileBytes, w, lane);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  const int r16 = lane & 15, h = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk)
+      stage_tile<NW>(Bb + static_cast<size_t>(kt + 1) * kRowBytes, ldb_b, Bring + ((kt + 1) & 1) * kTileBytes, w, lane);
+    if (kt + 2 < nk)
+      stage_tile<NW>(Ab + static_cast<size_t>(kt + 2) * kRowBytes, lda_b, Aring + ((kt + 2) % 3) * kTileBytes, w, lane);
+    ktile_mfma<FP8, false, FN, WTN>(Aring + (kt % 3) * kTileBytes, Bring + (kt & 1) * kTileBytes, acc, wm, wn, r16, h);
+    if (kt + 2 < nk)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  store_tile<FN, WTN>(C, ldc, tm, tn, wm, wn, r16, h, acc);
+}
 
 // ------------------------------------------------------------- optimizer
 
@@ -452,6 +531,14 @@ void launch_gemm(int grid, const void* A, const void* B, void* C, int M, int N, 
                      slice_end);
 }
 
+bool gemm_ring_enabled() {
+  // Off by default: measured 7 % slower than the double-buffered kernel for
+  // bf16 and +1 % for fp8 (profiles/gemm_bench_r1.md) - the A latency it
+  // hides is not what limits this kernel.
+  static const bool on = env_int("DLNB_GEMM_RING", 0) != 0;
+  return on;
+}
+
 template <bool DEADLINE>
 void dispatch_gemm(int waves, DType in_t, int grid, const void* A, const void* B, void* C, int M, int N, int K,
                    int lda, int ldb, int ldc, uint64_t* slot, uint32_t epoch, uint64_t ticks, uint64_t slice_end,
@@ -462,6 +549,13 @@ void dispatch_gemm(int waves, DType in_t, int grid, const void* A, const void* B
       launch_gemm<true, false, 2>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
     else
       launch_gemm<false, false, 2>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
+  } else if (!DEADLINE && waves == 1) {
+    if (fp8)
+      hipLaunchKernelGGL(gemm_tn_ring_kernel<true>, grid, 512, 0, st, static_cast<const char*>(A),
+                         static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc);
+    else
+      hipLaunchKernelGGL(gemm_tn_ring_kernel<false>, grid, 512, 0, st, static_cast<const char*>(A),
+                         static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc);
   } else {
     if (fp8)
       launch_gemm<true, DEADLINE, 4>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
@@ -490,8 +584,9 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
                    reinterpret_cast<uintptr_t>(C) % 8 == 0,
                "gemm_tn: misaligned base pointers");
   const int tiles = (M / kTile) * (N / kTile);
-  dispatch_gemm<false>(waves ? waves : gemm_default_waves(), in_t, tiles, A, B, C, M, N, K, lda, ldb, ldc, nullptr, 0u,
-                       0ull, 0ull, S(stream));
+  DLNB_REQUIRE(waves == 0 || waves == 1 || waves == 4 || waves == 8, "gemm_tn: variant must be 0, 1, 4 or 8");
+  if (waves == 0) waves = gemm_ring_enabled() ? 1 : gemm_default_waves();
+  dispatch_gemm<false>(waves, in_t, tiles, A, B, C, M, N, K, lda, ldb, ldc, nullptr, 0u, 0ull, 0ull, S(stream));
 }
 
 void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
