@@ -81,6 +81,7 @@ def main() -> int:
     ap.add_argument("--model", default=DEFAULT_MODEL)
     ap.add_argument("--units", type=int, default=32)
     ap.add_argument("--compute", default="gemm")
+    ap.add_argument("--graph", action="store_true", help="replay one captured HIP graph per iteration")
     ap.add_argument("--schedule", default="overlap")
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--json", default=None, help="also write the full report here (rank 0)")
@@ -106,7 +107,7 @@ def main() -> int:
     try:
         doc = engine.run("fsdp", a.model, a.units, world, base_path=ROOT, warmup=a.warmup, runs=a.steps,
                          compute=a.compute, schedule=a.schedule, backend=a.backend, wire_dtype="bf16",
-                         store=addr or None, silent=True, json=a.json)
+                         store=addr or None, silent=True, json=a.json, graph=a.graph or None)
     finally:
         sys.stdout.flush()
         os.dup2(saved, 1)
@@ -146,6 +147,7 @@ def main() -> int:
             "compute": a.compute,
             "schedule": a.schedule,
             "backend": g["backend"],
+            "hip_graph": bool(a.graph),
         },
         "effective_busbw_GBps": {k: round(v, 2) for k, v in bw.items()},
         "exposed_comm_ms": round(exposed, 3),

@@ -49,6 +49,9 @@ class ComputeEngine {
   // Enqueue `us` microseconds of compute; `flops` is the real FLOP count of
   // that piece of work (used by the flops mode).
   virtual void run(Stream& s, double us, double flops) = 0;
+  // Graph mode: enqueue on s a reset of whatever per-task device state the
+  // engine keys by epoch (a replayed graph repeats the captured epochs).
+  virtual void reset_clocks(Stream& s) { (void)s; }
   virtual Json describe() const = 0;
   virtual ComputeMode mode() const = 0;
 };

@@ -20,6 +20,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <vector>
 
 #include "dlnb/common.hpp"
 
@@ -41,6 +42,14 @@ class Stream {
 };
 
 class Device;
+
+// An instantiated HIP graph of one captured iteration (GPU only).
+class GraphExec {
+ public:
+  virtual ~GraphExec() = default;
+  virtual void launch(Stream& s) = 0;
+  virtual size_t nodes() const = 0;
+};
 
 // Owning buffer (device memory on GPU, page-aligned host memory on CPU).
 class Buffer {
@@ -99,6 +108,11 @@ class Device {
   virtual double stamp_hz() const = 0;
   virtual size_t total_memory() const = 0;
   virtual size_t free_memory() const = 0;
+  // Capture everything `enqueue` puts on `origin` and `others` into one graph:
+  // the other streams are forked from origin before and joined back after,
+  // so the graph is launched on origin alone. GPU only.
+  virtual std::unique_ptr<GraphExec> capture(Stream& origin, const std::vector<Stream*>& others,
+                                             const std::function<void()>& enqueue);
 
   Buffer alloc(size_t bytes) { return Buffer(this, bytes); }
 };

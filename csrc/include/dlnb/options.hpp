@@ -66,6 +66,7 @@ struct Options {
   // (deadlock-free across communicators), "split" = one lane per collective
   // kind so all-gather / reduce-scatter / replica all-reduce run concurrently.
   std::string comm_lanes = "single";
+  bool graph = false;  // capture one iteration into a HIP graph and replay it
 };
 
 // Parses argv for the given strategy (argv[0] is the program name). Throws

@@ -59,6 +59,12 @@ class Strategy {
   virtual void enqueue_iteration() = 0;
   // Host-wait for the iteration to finish (with failure detection).
   virtual void synchronize() = 0;
+  // Every stream the iteration uses, the compute stream first (graph
+  // capture forks the others from it and joins them back).
+  virtual std::vector<Stream*> streams() = 0;
+  // False when enqueue_iteration() blocks the host (--schedule reference),
+  // which a graph capture cannot contain.
+  virtual bool capturable() const = 0;
   virtual std::string section_id() const = 0;
   virtual std::string section_title() const = 0;
   // Per-rank key of the host iteration times ("runtimes"; fsdp uses "runtime").

@@ -38,6 +38,11 @@ class TimerSet {
   // Call after the streams involved have been synchronised.
   void resolve();
   void clear();
+  // Graph mode: between begin_capture() and end_capture() host values are
+  // recorded instead of applied; afterwards the stamp pairs and the recorded
+  // host values are re-applied by every resolve() (one per graph replay).
+  void begin_capture();
+  void end_capture();
   void set_enabled(bool on) { enabled_ = on; }
   bool enabled() const { return enabled_; }
   const std::vector<double>& get(const std::string& name) const;
@@ -55,6 +60,8 @@ class TimerSet {
   };
   std::vector<Pending> pending_;
   std::map<std::string, std::vector<double>> vals_;
+  std::vector<std::pair<std::string, double>> captured_adds_;
+  bool capturing_ = false, frozen_ = false;
   bool enabled_ = true;
 };
 

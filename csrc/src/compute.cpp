@@ -96,6 +96,10 @@ class GpuCompute : public ComputeEngine {
     }
   }
 
+  void reset_clocks(Stream& s) override {
+    if (mode_ == ComputeMode::Gemm) dev_.memset_async(slots_.data(), 0, kSlots * 64, s);
+  }
+
   void run(Stream& s, double us, double flops) override {
     double d = us * scale_;
     if (mode_ == ComputeMode::Sleep) {

@@ -234,4 +234,8 @@ class CpuDevice : public Device {
 
 std::unique_ptr<Device> make_cpu_device() { return std::unique_ptr<Device>(new CpuDevice()); }
 
+std::unique_ptr<GraphExec> Device::capture(Stream&, const std::vector<Stream*>&, const std::function<void()>&) {
+  DLNB_THROW("--graph needs a GPU device (HIP graphs)");
+}
+
 }  // namespace dlnb

@@ -63,6 +63,18 @@ class GpuStream : public Stream {
   hipStream_t s{};
 };
 
+class GpuGraphExec : public GraphExec {
+ public:
+  GpuGraphExec(hipGraphExec_t e, size_t n) : exec_(e), n_(n) {}
+  ~GpuGraphExec() override { (void)hipGraphExecDestroy(exec_); }
+  void launch(Stream& s) override { DLNB_HIP_CHECK(hipGraphLaunch(exec_, static_cast<hipStream_t>(s.native()))); }
+  size_t nodes() const override { return n_; }
+
+ private:
+  hipGraphExec_t exec_;
+  size_t n_;
+};
+
 void host_trampoline(void* p) {
   auto* fn = static_cast<std::function<void()>*>(p);
   (*fn)();
@@ -135,6 +147,38 @@ class GpuDevice : public Device {
     size_t f = 0, t = 0;
     if (hipMemGetInfo(&f, &t) != hipSuccess) return 0;
     return f;
+  }
+  std::unique_ptr<GraphExec> capture(Stream& origin, const std::vector<Stream*>& others,
+                                     const std::function<void()>& enqueue) override {
+    // Fork/join events exist before the capture starts (no creation inside).
+    auto fork = create_event(false);
+    std::vector<std::unique_ptr<Event>> joins;
+    for (size_t i = 0; i < others.size(); ++i) joins.push_back(create_event(false));
+    hipStream_t o = static_cast<hipStream_t>(origin.native());
+    DLNB_HIP_CHECK(hipStreamBeginCapture(o, hipStreamCaptureModeThreadLocal));
+    try {
+      origin.record(*fork);
+      for (Stream* s : others) s->wait(*fork);
+      enqueue();
+      for (size_t i = 0; i < others.size(); ++i) {
+        others[i]->record(*joins[i]);
+        origin.wait(*joins[i]);
+      }
+    } catch (...) {
+      hipGraph_t g = nullptr;
+      (void)hipStreamEndCapture(o, &g);
+      if (g) (void)hipGraphDestroy(g);
+      throw;
+    }
+    hipGraph_t g = nullptr;
+    DLNB_HIP_CHECK(hipStreamEndCapture(o, &g));
+    size_t n = 0;
+    (void)hipGraphGetNodes(g, nullptr, &n);
+    hipGraphExec_t e = nullptr;
+    hipError_t err = hipGraphInstantiate(&e, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (err != hipSuccess) DLNB_THROW("hipGraphInstantiate failed: " << hipGetErrorString(err));
+    return std::unique_ptr<GraphExec>(new GpuGraphExec(e, n));
   }
 
  private:

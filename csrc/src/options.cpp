@@ -87,6 +87,7 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  --trace                emit roctx ranges (rocprofv3 --marker-trace)\n"
      << "  --comm-cus N           CUs the gemm compute leaves free for collectives (default 32)\n"
      << "  --comm-lanes single|split  fsdp: all collectives on one ordered lane (default) or one per kind\n"
+     << "  --graph                capture one iteration into a HIP graph, replay it every iteration (rccl)\n"
      << "env: DLNB_TIMEOUT (s, hang detection), DLNB_INJECT_FAULT=rank=R,iter=I,mode=exit|hang|throw,\n"
      << "     DLNB_STORE_ADDR=host:port, DLNB_NO_ENERGY=1\n";
   return os.str();
@@ -154,6 +155,8 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
       o.topology = false;
     } else if (is("--comm-cus")) {
       o.comm_cus = to_int(val("comm-cus"), "comm-cus");
+    } else if (a == "--graph") {
+      o.graph = true;
     } else if (is("--comm-lanes")) {
       o.comm_lanes = val("comm-lanes");
     } else if (a == "--trace") {

@@ -247,6 +247,33 @@ Json run_benchmark(const Options& opt) {
   TimerSet& T = *strat->timers();
   const char* rkey = strat->runtime_key();
   T.ensure(rkey);
+
+  // ---- HIP graph: capture one iteration, replay it every iteration
+  std::unique_ptr<GraphExec> graph;
+  if (opt.graph) {
+    DLNB_REQUIRE(ctx.dev->kind() == DeviceKind::GPU, "--graph needs a GPU");
+    DLNB_REQUIRE(backend == "rccl", "--graph needs --backend rccl (the xgmi kernels tag every piece with a fresh "
+                                    "epoch, which a replayed graph would repeat)");
+    DLNB_REQUIRE(strat->capturable(), "--graph cannot capture --schedule reference (it blocks the host)");
+    std::vector<Stream*> ss = strat->streams();
+    std::vector<Stream*> others(ss.begin() + 1, ss.end());
+    TraceRange tr("dlnb:graph_capture");
+    T.begin_capture();
+    graph = ctx.dev->capture(*ss[0], others, [&] {
+      ctx.compute->reset_clocks(*ss[0]);
+      strat->enqueue_iteration();
+    });
+    T.end_capture();
+    if (ri.rank == 0 && !opt.quiet)
+      std::cout << "[dlnb] captured one iteration into a HIP graph of " << graph->nodes() << " nodes" << std::endl;
+  }
+  Stream* origin = graph ? strat->streams()[0] : nullptr;
+  auto enqueue = [&] {
+    if (graph)
+      graph->launch(*origin);
+    else
+      strat->enqueue_iteration();
+  };
   ctx.hg().barrier();
 
   // ---- warm-up
@@ -255,7 +282,7 @@ Json run_benchmark(const Options& opt) {
     fault.at_iteration(iter_no++);
     TraceRange tr("dlnb:warmup_iteration");
     double t0 = now_s();
-    strat->enqueue_iteration();
+    enqueue();
     strat->synchronize();
     warm.push_back(now_s() - t0);
   }
@@ -282,7 +309,7 @@ Json run_benchmark(const Options& opt) {
     for (long long it = 0; opt.max_loop_iters == 0 || it < opt.max_loop_iters; ++it) {
       fault.at_iteration(iter_no++);
       TraceRange tr("dlnb:loop_iteration");
-      strat->enqueue_iteration();
+      enqueue();
       strat->synchronize();
     }
     ctx.hg().barrier();
@@ -300,7 +327,7 @@ Json run_benchmark(const Options& opt) {
     TraceRange tr("dlnb:iteration");
     const double j0 = meter->joules();
     double t0 = now_s();
-    strat->enqueue_iteration();
+    enqueue();
     strat->synchronize();
     T.add(rkey, now_s() - t0);
     if (meter->available()) T.add("energy_consumed", meter->joules() - j0);
@@ -324,6 +351,7 @@ Json run_benchmark(const Options& opt) {
   Json ext = Json::object();
   ext["strategy"] = strategy_name(opt.strategy);
   ext["schedule"] = opt.schedule;
+  ext["graph"] = graph ? static_cast<double>(graph->nodes()) : 0.0;
   ext["wire_dtype"] = dtype_name(ctx.wire);
   ext["compute"] = ctx.compute->describe();
   ext["stats_file"] = stats_path;

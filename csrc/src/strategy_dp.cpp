@@ -90,6 +90,9 @@ class DataParallel : public Strategy {
     }
   }
 
+  std::vector<Stream*> streams() override { return {compute_.get(), comm_stream_.get()}; }
+  bool capturable() const override { return true; }
+
   void synchronize() override {
     sync_streams({compute_.get(), comm_stream_.get()}, {comm_.get()}, *ctx_->dev);
     timers_->resolve();

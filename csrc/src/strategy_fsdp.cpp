@@ -194,6 +194,13 @@ class Fsdp : public Strategy {
     }
   }
 
+  std::vector<Stream*> streams() override {
+    std::vector<Stream*> ss = {compute_.get()};
+    for (auto& s : lanes_) ss.push_back(s.get());
+    return ss;
+  }
+  bool capturable() const override { return !reference_; }
+
   void synchronize() override {
     std::vector<Stream*> ss = {compute_.get()};
     std::vector<Communicator*> cs;

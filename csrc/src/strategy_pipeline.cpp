@@ -361,6 +361,14 @@ class Pipeline : public Strategy {
     timers_->end(tk, *dp_stream_, "dp_comm_time");
   }
 
+  std::vector<Stream*> streams() override {
+    std::vector<Stream*> ss = {compute_.get(), dp_stream_.get()};
+    if (prev_) ss.push_back(prev_stream_.get());
+    if (next_) ss.push_back(next_stream_.get());
+    return ss;
+  }
+  bool capturable() const override { return !reference_; }
+
   void synchronize() override {
     std::vector<Stream*> ss = {compute_.get(), dp_stream_.get()};
     std::vector<Communicator*> cs = {dp_comm_.get()};

@@ -40,7 +40,23 @@ void TimerSet::stall(Stream& s, Event& e, const std::string& name) {
 }
 
 void TimerSet::add(const std::string& name, double seconds) {
+  if (capturing_) {
+    captured_adds_.emplace_back(name, seconds);
+    return;
+  }
   if (enabled_) vals_[name].push_back(seconds);
+}
+
+void TimerSet::begin_capture() {
+  pending_.clear();
+  next_ = 0;
+  captured_adds_.clear();
+  capturing_ = true;
+}
+
+void TimerSet::end_capture() {
+  capturing_ = false;
+  frozen_ = true;
 }
 
 void TimerSet::ensure(const std::string& name) { vals_[name]; }
@@ -48,18 +64,23 @@ void TimerSet::ensure(const std::string& name) { vals_[name]; }
 void TimerSet::resolve() {
   // Called after the streams were synchronised: every stamp has landed.
   const double hz = dev_.stamp_hz();
+  if (frozen_ && enabled_)
+    for (const auto& a : captured_adds_) vals_[a.first].push_back(a.second);
   for (const auto& p : pending_) {
     const uint64_t a = __atomic_load_n(stamps_ + p.a, __ATOMIC_ACQUIRE);
     const uint64_t b = __atomic_load_n(stamps_ + p.b, __ATOMIC_ACQUIRE);
-    vals_[p.name].push_back(b >= a ? static_cast<double>(b - a) / hz : 0.0);
+    if (enabled_) vals_[p.name].push_back(b >= a ? static_cast<double>(b - a) / hz : 0.0);
   }
+  if (frozen_) return;  // the same stamps are rewritten by the next replay
   pending_.clear();
   next_ = 0;
 }
 
 void TimerSet::clear() {
-  pending_.clear();
-  next_ = 0;
+  if (!frozen_) {
+    pending_.clear();
+    next_ = 0;
+  }
   for (auto& kv : vals_) kv.second.clear();
 }
 

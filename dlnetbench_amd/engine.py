@@ -26,9 +26,10 @@ _FLAG = {
     "compute_dtype": "--compute-dtype", "schedule": "--schedule", "tp_granularity": "--tp-granularity",
     "dp_buckets": "--dp-buckets", "max_loop_iters": "--max-loop-iters", "time_scale": "--time-scale",
     "json": "--json", "store": "--store", "stats_file": "--stats-file", "comm_cus": "--comm-cus",
+    "comm_lanes": "--comm-lanes",
 }
 _BOOL = {"in_place": "--in-place", "optimizer": "--optimizer", "loop": "--loop", "quiet": "--quiet",
-         "silent": "--silent"}
+         "silent": "--silent", "graph": "--graph", "trace": "--trace"}
 
 
 def build_args(strategy: str, model: str, *params: int, base_path: str = ".", topology: bool = False,

@@ -60,3 +60,19 @@ def test_measured_stats_generator(tmp_path):
     st = load_stats(p)
     assert st.fwd_us > 0 and st.bwd_us > 0 and st.num_layers == 12
     assert "measured" in st.device
+
+
+@pytest.mark.parametrize("strategy,model,params", CASES)
+def test_strategy_hip_graph_replay(strategy, model, params, data_dir):
+    """--graph: one captured iteration replayed per run, timings like eager enqueue."""
+    doc = engine.run(strategy, model, *params, base_path=data_dir, warmup=1, runs=3, compute="gemm",
+                     backend="rccl", quiet=True, graph=True)
+    g = doc["global"]
+    assert g["dlnb"]["graph"] > 0
+    it = g["dlnb"]["iteration"]
+    assert it["median_ms"] >= 0.9 * it["compute_floor_ms"]
+    assert it["median_ms"] < 1.5 * it["compute_floor_ms"] + 5.0
+    r = doc["ranks"][0]
+    # per-run timer vectors keep their length under replay
+    key = "runtime" if strategy == "fsdp" else "runtimes"
+    assert len(r[key]) == 3

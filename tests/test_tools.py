@@ -140,3 +140,9 @@ def test_asan_build_is_clean(prog, args, root, data_dir):
                                capture=True, env=env)
     text = "".join(o or "" for o in outs)
     assert code == 0 and "AddressSanitizer" not in text, text[-3000:]
+
+
+def test_graph_needs_gpu(bindir, data_dir):
+    p = subprocess.run([os.path.join(bindir, "dp"), "tiny_dense_8_bfloat16", "2", data_dir, "--backend",
+                        "cpu", "--graph", "-w", "0", "-r", "1"], capture_output=True, text=True)
+    assert p.returncode == 2 and "graph" in p.stderr
