@@ -49,6 +49,16 @@ class ComputeEngine {
   // Enqueue `us` microseconds of compute; `flops` is the real FLOP count of
   // that piece of work (used by the flops mode).
   virtual void run(Stream& s, double us, double flops) = 0;
+  // Same, and the kernel itself writes the task's start time (device clock,
+  // Device::stamp_hz) into *start (host-mapped) - only where
+  // stamps_task_start() is true. task_ticks(us) = the task's duration in
+  // those clock ticks.
+  virtual void run_stamped(Stream& s, double us, double flops, uint64_t* start) {
+    (void)start;
+    run(s, us, flops);
+  }
+  virtual bool stamps_task_start() const { return false; }
+  virtual uint64_t task_ticks(double us) const { (void)us; return 0; }
   // Graph mode: enqueue on s a reset of whatever per-task device state the
   // engine keys by epoch (a replayed graph repeats the captured epochs).
   virtual void reset_clocks(Stream& s) { (void)s; }

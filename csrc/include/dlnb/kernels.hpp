@@ -59,8 +59,11 @@ int gemm_default_waves();
 // (slices) with increasing slice_end so that collectives on other streams get
 // CUs at slice boundaries, as they do between a training step's kernels.
 // Leading dimensions are K, K and N.
+// tstart (optional, host-mapped): the block that claims the epoch stores the
+// task's start (s_memrealtime) there - stall timing without extra kernels.
 void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
-                      uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end = 0);
+                      uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end = 0,
+                      uint64_t* tstart = nullptr);
 
 // Elementwise "optimizer" stand-in (SGD-momentum on bf16 shards, fp32 math):
 // p = p - lr * (m = beta*m + g). Used by the optional --optimizer step.

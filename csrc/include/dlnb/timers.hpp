@@ -33,6 +33,14 @@ class TimerSet {
   void end(int token, Stream& s, const std::string& name);
   // Time the stall of stream s waiting for event e (exposed latency).
   void stall(Stream& s, Event& e, const std::string& name);
+  // Stamp-free variant for a wait between two compute tasks on one stream
+  // whose kernels stamp their own start (ComputeEngine::run_stamped):
+  // slot() hands out a host-mapped stamp slot for the next task's start, and
+  // gap() records value = next_start - (prev_start + prev_ticks), i.e. how
+  // long the stream sat between the previous task's deadline and the next
+  // task's first block (the dependency wait plus the launch).
+  uint64_t* slot();
+  void gap(const uint64_t* prev_start, uint64_t prev_ticks, const uint64_t* next_start, const std::string& name);
   void add(const std::string& name, double seconds);
   void ensure(const std::string& name);
   // Call after the streams involved have been synchronised.
@@ -59,6 +67,12 @@ class TimerSet {
     std::string name;
   };
   std::vector<Pending> pending_;
+  struct Gap {
+    int prev, next;
+    uint64_t prev_ticks;
+    std::string name;
+  };
+  std::vector<Gap> gaps_;
   std::map<std::string, std::vector<double>> vals_;
   std::vector<std::pair<std::string, double>> captured_adds_;
   bool capturing_ = false, frozen_ = false;

@@ -284,7 +284,7 @@ template <bool FP8, bool DEADLINE, int WN>
 __global__ void __launch_bounds__(128 * WN, WN == 4 ? 2 : 1)
     gemm_tn_256_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
                        int K, int lda, int ldb, int ldc, uint64_t* __restrict__ slot, uint32_t epoch,
-                       uint64_t ticks, uint64_t slice_end) {
+                       uint64_t ticks, uint64_t slice_end, uint64_t* __restrict__ tstart) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kStageBytes + 16];
   volatile int* stop_flag = reinterpret_cast<volatile int*>(smem + 2 * kStageBytes);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -297,13 +297,16 @@ __global__ void __launch_bounds__(128 * WN, WN == 4 ? 2 : 1)
   uint64_t t0 = 0;
   if constexpr (DEADLINE) {
     if (tid == 0) {
-      const uint64_t now = __builtin_amdgcn_s_memrealtime() & kMask48;
+      const uint64_t raw = __builtin_amdgcn_s_memrealtime();
+      const uint64_t now = raw & kMask48;
       const uint64_t mine = (static_cast<uint64_t>(epoch) << 48) | now;
       uint64_t cur = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       while ((cur >> 48) != epoch) {
         if (__hip_atomic_compare_exchange_strong(slot, &cur, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT)) {
           cur = mine;
+          // the task's start, for stamp-free stall timing (host-mapped)
+          if (tstart) __hip_atomic_store(tstart, raw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           break;
         }
       }
@@ -525,10 +528,11 @@ namespace {
 
 template <bool FP8, bool DEADLINE, int WN>
 void launch_gemm(int grid, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
-                 uint64_t* slot, uint32_t epoch, uint64_t ticks, uint64_t slice_end, hipStream_t st) {
+                 uint64_t* slot, uint32_t epoch, uint64_t ticks, uint64_t slice_end, hipStream_t st,
+                 uint64_t* tstart = nullptr) {
   hipLaunchKernelGGL((gemm_tn_256_kernel<FP8, DEADLINE, WN>), grid, 128 * WN, 0, st, static_cast<const char*>(A),
                      static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc, slot, epoch, ticks,
-                     slice_end);
+                     slice_end, tstart);
 }
 
 bool gemm_ring_enabled() {
@@ -542,7 +546,7 @@ bool gemm_ring_enabled() {
 template <bool DEADLINE>
 void dispatch_gemm(int waves, DType in_t, int grid, const void* A, const void* B, void* C, int M, int N, int K,
                    int lda, int ldb, int ldc, uint64_t* slot, uint32_t epoch, uint64_t ticks, uint64_t slice_end,
-                   hipStream_t st) {
+                   hipStream_t st, uint64_t* tstart = nullptr) {
   const bool fp8 = in_t == DType::FP8_E4M3;
   if (!DEADLINE && waves == 4) {  // (the 4-wave deadline variant would spill: never instantiated)
     if (fp8)
@@ -558,9 +562,9 @@ void dispatch_gemm(int waves, DType in_t, int grid, const void* A, const void* B
                          static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc);
   } else {
     if (fp8)
-      launch_gemm<true, DEADLINE, 4>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
+      launch_gemm<true, DEADLINE, 4>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st, tstart);
     else
-      launch_gemm<false, DEADLINE, 4>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
+      launch_gemm<false, DEADLINE, 4>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st, tstart);
   }
   DLNB_HIP_CHECK(hipGetLastError());
 }
@@ -590,12 +594,12 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
 }
 
 void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
-                      uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end) {
+                      uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end, uint64_t* tstart) {
   if (slice_end == 0) slice_end = ticks;
   DLNB_REQUIRE(gemm_shape_ok(M, N, K, in_t), "gemm_tn_deadline: unsupported shape");
   DLNB_REQUIRE(slot != nullptr && grid > 0 && epoch > 0 && epoch < 65536, "gemm_tn_deadline: bad slot/grid/epoch");
   // 8 waves: the 4-wave variant spills once the deadline logic is added.
-  dispatch_gemm<true>(8, in_t, grid, A, B, C, M, N, K, K, K, N, slot, epoch, ticks, slice_end, S(stream));
+  dispatch_gemm<true>(8, in_t, grid, A, B, C, M, N, K, K, K, N, slot, epoch, ticks, slice_end, S(stream), tstart);
 }
 
 void sgd_momentum_bf16(void* param, void* mom, const void* grad, size_t n, float lr, float beta, void* stream) {

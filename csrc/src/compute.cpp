@@ -100,7 +100,11 @@ class GpuCompute : public ComputeEngine {
     if (mode_ == ComputeMode::Gemm) dev_.memset_async(slots_.data(), 0, kSlots * 64, s);
   }
 
-  void run(Stream& s, double us, double flops) override {
+  bool stamps_task_start() const override { return mode_ == ComputeMode::Gemm; }
+  uint64_t task_ticks(double us) const override { return ticks(us * scale_); }
+  void run(Stream& s, double us, double flops) override { run_stamped(s, us, flops, nullptr); }
+
+  void run_stamped(Stream& s, double us, double flops, uint64_t* start) override {
     double d = us * scale_;
     if (mode_ == ComputeMode::Sleep) {
       if (d > 0) kernels::idle_wait(ticks(d), s.native());
@@ -116,6 +120,7 @@ class GpuCompute : public ComputeEngine {
       // DVFS or contention changes how much work is done, not how long).
       if (d <= 0) return;
       if (d < 20.0) {
+        if (start) dev_.stamp(s, start);
         kernels::busy_spin(ticks(d), cus_, s.native());
         return;
       }
@@ -125,7 +130,7 @@ class GpuCompute : public ComputeEngine {
       const uint64_t slice = std::max<uint64_t>(ticks(slice_us_), 1);
       for (uint64_t end = slice;; end += slice) {
         kernels::gemm_tn_deadline(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, total, slot_for(s), ep,
-                                  grid_, s.native(), std::min(end, total));
+                                  grid_, s.native(), std::min(end, total), end == slice ? start : nullptr);
         if (end >= total) break;
       }
       return;

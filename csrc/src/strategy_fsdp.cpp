@@ -127,10 +127,36 @@ class Fsdp : public Strategy {
       stats_.push_back({"allreduce", CollKind::AllReduce, R_, static_cast<double>(max_shard_ * es_), "allreduce_time"});
   }
 
+  // One unit's compute on the compute stream after waiting for `dep`. When
+  // the engine's kernels stamp their own start, the exposed wait is timed as
+  // the gap between the previous task's deadline and this task's start (no
+  // stamp kernels: each costs a kernel boundary right after a full-chip
+  // GEMM); otherwise with a stamp pair around the wait.
+  void compute_after(Event* dep, const char* timer, double us, double flops) {
+    ComputeEngine& ce = *ctx_->compute;
+    if (ce.stamps_task_start()) {
+      if (dep) compute_->wait(*dep);
+      uint64_t* st = timers_->slot();
+      ce.run_stamped(*compute_, us, flops, st);
+      if (timer && prev_start_) timers_->gap(prev_start_, prev_ticks_, st, timer);
+      prev_start_ = st;
+      prev_ticks_ = ce.task_ticks(us);
+      return;
+    }
+    if (dep) {
+      if (timer)
+        timers_->stall(*compute_, *dep, timer);
+      else
+        compute_->wait(*dep);
+    }
+    ce.run(*compute_, us, flops);
+  }
+  void compute_after(Event& dep, const char* timer, double us, double flops) { compute_after(&dep, timer, us, flops); }
+
   void enqueue_iteration() override {
     Context& ctx = *ctx_;
-    ComputeEngine& ce = *ctx.compute;
     const DType t = ctx.wire;
+    prev_start_ = nullptr;
 
     auto gather = [&](int u, Event& done, bool first) {
       int tk = timers_->begin(*ag_stream_);
@@ -148,11 +174,7 @@ class Fsdp : public Strategy {
         if (u >= 1) ag_stream_->wait(*fwd_done_[u - 1]);
         gather(u + 1, *ag_f_[u + 1], false);
       }
-      if (u == 0)
-        compute_->wait(*ag_f_[0]);
-      else
-        timers_->stall(*compute_, *ag_f_[u], "allgather_wait_fwd");
-      ce.run(*compute_, fwd_us_, fwd_flops_);
+      compute_after(*ag_f_[u], u == 0 ? nullptr : "allgather_wait_fwd", fwd_us_, fwd_flops_);
       compute_->record(*fwd_done_[u]);
     }
 
@@ -163,10 +185,12 @@ class Fsdp : public Strategy {
         ag_stream_->wait(u + 1 <= U_ - 1 ? *bwd_done_[u + 1] : *fwd_done_[u - 1]);
         gather(u - 1, *ag_b_[u - 1], false);
       }
-      if (u < U_ - 1) timers_->stall(*compute_, *ag_b_[u], "allgather_wait_bwd");
       // full_grad[u&1] was last read by the reduce-scatter of unit u+2.
       if (u + 2 <= U_ - 1) compute_->wait(*rs_done_[u + 2]);
-      ce.run(*compute_, bwd_us_, bwd_flops_);
+      if (u < U_ - 1)
+        compute_after(*ag_b_[u], "allgather_wait_bwd", bwd_us_, bwd_flops_);
+      else
+        compute_after(nullptr, nullptr, bwd_us_, bwd_flops_);
       compute_->record(*bwd_done_[u]);
 
       rs_stream_->wait(*bwd_done_[u]);
@@ -263,6 +287,8 @@ class Fsdp : public Strategy {
   Buffer gathered_[2], full_grad_[2];
   std::vector<std::unique_ptr<Event>> ag_f_, fwd_done_, ag_b_, bwd_done_, rs_done_, ar_done_;
   std::vector<CommStat> stats_;
+  const uint64_t* prev_start_ = nullptr;  // start stamp of the previous compute task
+  uint64_t prev_ticks_ = 0;
 };
 
 }  // namespace

@@ -39,6 +39,17 @@ void TimerSet::stall(Stream& s, Event& e, const std::string& name) {
   end(t, s, name);
 }
 
+uint64_t* TimerSet::slot() {
+  DLNB_REQUIRE(next_ < cap_, "too many timer stamps in one iteration");
+  return stamps_ + next_++;
+}
+
+void TimerSet::gap(const uint64_t* prev_start, uint64_t prev_ticks, const uint64_t* next_start,
+                   const std::string& name) {
+  if (!enabled_) return;
+  gaps_.push_back(Gap{static_cast<int>(prev_start - stamps_), static_cast<int>(next_start - stamps_), prev_ticks, name});
+}
+
 void TimerSet::add(const std::string& name, double seconds) {
   if (capturing_) {
     captured_adds_.emplace_back(name, seconds);
@@ -49,6 +60,7 @@ void TimerSet::add(const std::string& name, double seconds) {
 
 void TimerSet::begin_capture() {
   pending_.clear();
+  gaps_.clear();
   next_ = 0;
   captured_adds_.clear();
   capturing_ = true;
@@ -71,14 +83,21 @@ void TimerSet::resolve() {
     const uint64_t b = __atomic_load_n(stamps_ + p.b, __ATOMIC_ACQUIRE);
     if (enabled_) vals_[p.name].push_back(b >= a ? static_cast<double>(b - a) / hz : 0.0);
   }
+  for (const auto& g : gaps_) {
+    const uint64_t a = __atomic_load_n(stamps_ + g.prev, __ATOMIC_ACQUIRE) + g.prev_ticks;
+    const uint64_t b = __atomic_load_n(stamps_ + g.next, __ATOMIC_ACQUIRE);
+    if (enabled_) vals_[g.name].push_back(b >= a ? static_cast<double>(b - a) / hz : 0.0);
+  }
   if (frozen_) return;  // the same stamps are rewritten by the next replay
   pending_.clear();
+  gaps_.clear();
   next_ = 0;
 }
 
 void TimerSet::clear() {
   if (!frozen_) {
     pending_.clear();
+    gaps_.clear();
     next_ = 0;
   }
   for (auto& kv : vals_) kv.second.clear();
