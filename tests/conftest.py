@@ -29,3 +29,8 @@ def pytest_sessionstart(session):
     if not all(os.path.exists(p) for p in need):
         subprocess.run(["make", "-C", ROOT, f"-j{min(16, os.cpu_count() or 4)}"], check=True,
                        stdout=subprocess.DEVNULL)
+    # An existing host-ASan build is brought up to date (incremental) so its
+    # tests never run stale binaries.
+    if os.path.isdir(os.path.join(ROOT, "build-asan", "bin")):
+        subprocess.run(["make", "-C", ROOT, f"-j{min(16, os.cpu_count() or 4)}", "asan"], check=False,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
