@@ -32,45 +32,28 @@ BASELINE_MS = 2814.74976
 DEFAULT_MODEL = "llama3_8b_16_bfloat16"
 
 
-def _store_addr(world: int, rank: int) -> str:
-    """Address of the native runtime's TCP rendezvous store under torchrun.
+def _store_env(world: int, rank: int, attempt: str = "") -> None:
+    """Point the native runtime's TCP rendezvous store at this torchrun job.
 
-    Single node (the bench's case): rank 0 binds an ephemeral port and
-    publishes it in a file named after torchrun's MASTER_PORT/run id; the
-    other local ranks poll that file. Multi-node: MASTER_PORT + 1."""
+    Single node (the bench's case): rank 0's store binds an ephemeral port
+    and publishes host:port in a file named after torchrun's MASTER_PORT and
+    the launcher's pid (all local workers of one job share the elastic agent
+    as parent, so a stale file from an earlier job is never read); the other
+    ranks poll that file (DLNB_STORE_FILE). Multi-node: MASTER_PORT + 1."""
+    os.environ.pop("DLNB_STORE_ADDR", None)
+    os.environ.pop("DLNB_STORE_FILE", None)
     if world == 1:
-        return ""
+        return
     host = os.environ.get("MASTER_ADDR", "127.0.0.1")
     port = int(os.environ.get("MASTER_PORT", "29500"))
     if int(os.environ.get("LOCAL_WORLD_SIZE", world)) != world:
-        return f"{host}:{port + 1}"
-    # All local workers of one torchrun job share the launcher (the elastic
-    # agent) as parent process: its pid makes the file unique per job, so a
-    # stale file from an earlier job on the same port is never read.
-    path = f"/tmp/dlnb_bench_store_{port}_{os.getppid()}"
+        os.environ["DLNB_STORE_ADDR"] = f"{host}:{port + 1 + (1 if attempt else 0)}"
+        return
+    path = f"/tmp/dlnb_bench_store_{port}_{os.getppid()}{attempt}"
+    os.environ["DLNB_STORE_FILE"] = path
     if rank == 0:
-        import socket
-        with socket.socket() as s:
-            s.bind(("", 0))
-            p = s.getsockname()[1]
-        tmp = path + ".tmp"
-        with open(tmp, "w") as f:
-            f.write(str(p))
-        os.replace(tmp, path)
         import atexit
         atexit.register(lambda: os.path.exists(path) and os.remove(path))
-        return f"127.0.0.1:{p}"
-    deadline = time.time() + 300
-    while time.time() < deadline:
-        try:
-            with open(path) as f:
-                txt = f.read().strip()
-            if txt:
-                return f"127.0.0.1:{int(txt)}"
-        except (OSError, ValueError):
-            pass
-        time.sleep(0.05)
-    raise RuntimeError(f"rank {rank}: no store address in {path}")
 
 
 def main() -> int:
@@ -81,7 +64,8 @@ def main() -> int:
     ap.add_argument("--model", default=DEFAULT_MODEL)
     ap.add_argument("--units", type=int, default=32)
     ap.add_argument("--compute", default="gemm")
-    ap.add_argument("--graph", action="store_true", help="replay one captured HIP graph per iteration")
+    ap.add_argument("--no-graph", dest="graph", action="store_false",
+                    help="enqueue every iteration instead of replaying one captured HIP graph")
     ap.add_argument("--schedule", default="overlap")
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--json", default=None, help="also write the full report here (rank 0)")
@@ -94,20 +78,35 @@ def main() -> int:
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     # Everything below is native (HIP + RCCL from /opt/rocm); torch is not needed.
     os.environ.setdefault("DLNB_NO_TORCH", "1")
-    addr = _store_addr(world, rank)
+    _store_env(world, rank)
 
     from dlnetbench_amd import engine
     from dlnetbench_amd.utils.stats import load_stats
     st = load_stats(os.path.join(ROOT, "model_stats", a.model + ".txt"))
     # The result line must be the only stdout line: route whatever the native
     # libraries print (e.g. RCCL's banner) to stderr while the benchmark runs.
+    graph = a.graph and a.backend in ("auto", "rccl") and a.schedule == "overlap"
+
+    def attempt(use_graph: bool):
+        return engine.run("fsdp", a.model, a.units, world, base_path=ROOT, warmup=a.warmup, runs=a.steps,
+                          compute=a.compute, schedule=a.schedule, backend=a.backend, wire_dtype="bf16",
+                          silent=True, json=a.json, graph=use_graph or None)
+
     sys.stdout.flush()
     saved = os.dup(1)
     os.dup2(2, 1)
     try:
-        doc = engine.run("fsdp", a.model, a.units, world, base_path=ROOT, warmup=a.warmup, runs=a.steps,
-                         compute=a.compute, schedule=a.schedule, backend=a.backend, wire_dtype="bf16",
-                         store=addr or None, silent=True, json=a.json, graph=a.graph or None)
+        try:
+            doc = attempt(graph)
+        except RuntimeError as e:
+            if not graph:
+                raise
+            # Graph capture is symmetric across ranks, so every rank takes this
+            # path; the retry rendezvouses on a fresh store.
+            print(f"[bench] HIP graph run failed ({e}); retrying with per-iteration enqueue", file=sys.stderr)
+            graph = False
+            _store_env(world, rank, ".retry")
+            doc = attempt(False)
     finally:
         sys.stdout.flush()
         os.dup2(saved, 1)
@@ -147,7 +146,7 @@ def main() -> int:
             "compute": a.compute,
             "schedule": a.schedule,
             "backend": g["backend"],
-            "hip_graph": bool(a.graph),
+            "hip_graph": bool(graph),
         },
         "effective_busbw_GBps": {k: round(v, 2) for k, v in bw.items()},
         "exposed_comm_ms": round(exposed, 3),
