@@ -48,6 +48,7 @@ struct Options {
   std::string compute_dtype = "auto";  // auto (from stats Dtype) | bf16 | fp8
   std::string schedule = "overlap";    // overlap | reference
   std::string tp_granularity = "microbatch";  // microbatch | layer
+  std::string pp_schedule = "gpipe";          // gpipe (reference) | 1f1b
   int dp_buckets = 1;  // hybrids: DP all-reduce buckets overlapped with the last backward
   bool in_place = false;
   bool optimizer = false;  // add an elementwise optimizer step over the local shard

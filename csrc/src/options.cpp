@@ -73,6 +73,7 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  --compute-dtype T      auto | bf16 | fp8 (GEMM operand type for gemm/flops)\n"
      << "  --schedule S           overlap (stream-ordered) | reference (blocking like DLNetBench)\n"
      << "  --tp-granularity G     microbatch | layer (hybrid_3d)\n"
+     << "  --pp-schedule gpipe|1f1b  hybrids: all forwards then all backwards (reference) or one-forward-one-backward\n"
      << "  --dp-buckets K         hybrids: DP all-reduce buckets overlapped with the last backward\n"
      << "  --in-place             in-place all-reduce (halves DP buffer memory)\n"
      << "  --optimizer            add an SGD-momentum step over the local gradient shard\n"
@@ -133,6 +134,8 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
       o.schedule = val("schedule");
     } else if (is("--tp-granularity")) {
       o.tp_granularity = val("tp-granularity");
+    } else if (is("--pp-schedule")) {
+      o.pp_schedule = val("pp-schedule");
     } else if (is("--dp-buckets")) {
       o.dp_buckets = to_int(val("dp-buckets"), "dp-buckets");
     } else if (a == "--in-place") {
@@ -206,6 +209,7 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
                    o.num_microbatches >= 1 && o.num_tensor_shards >= 1 && o.num_expert_shards >= 1,
                "parallelism degrees must be >= 1");
   DLNB_REQUIRE(o.schedule == "overlap" || o.schedule == "reference", "--schedule must be overlap or reference");
+  DLNB_REQUIRE(o.pp_schedule == "gpipe" || o.pp_schedule == "1f1b", "--pp-schedule must be gpipe or 1f1b");
   DLNB_REQUIRE(o.tp_granularity == "microbatch" || o.tp_granularity == "layer",
                "--tp-granularity must be microbatch or layer");
   DLNB_REQUIRE(o.comm_lanes == "single" || o.comm_lanes == "split", "--comm-lanes must be single or split");

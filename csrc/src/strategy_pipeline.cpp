@@ -74,6 +74,8 @@ class Pipeline : public Strategy {
              : kind_ == StrategyKind::Hybrid3DMoE ? o.num_expert_shards
                                                   : 1;
     reference_ = o.schedule == "reference";
+    one_f_one_b_ = o.pp_schedule == "1f1b";
+    DLNB_REQUIRE(!(one_f_one_b_ && reference_), "--pp-schedule 1f1b needs --schedule overlap");
     DLNB_REQUIRE(ctx.have_arch, "hybrid strategies need models/<model>.json (layer count)");
     L_ = static_cast<int>(ctx.arch.num_layers);
     DLNB_REQUIRE(L_ > 0, "model has no layers: " << ctx.arch.path);
@@ -262,7 +264,7 @@ class Pipeline : public Strategy {
     timers_->end(t, *compute_, "ep_comm_time");
   }
 
-  void enqueue_iteration() override {
+  void enqueue_gpipe() {
     Context& ctx = *ctx_;
     const DType t = ctx.wire;
     const int nbk = ctx.opt.dp_buckets;
@@ -329,7 +331,14 @@ class Pipeline : public Strategy {
         if (reference_) compute_->wait(*send_b_[i]);
       }
     }
-    // ---------------- gradient synchronisation
+    finish_iteration();
+  }
+
+  // DP (and MoE non-expert) gradient synchronisation after the backwards.
+  void finish_iteration() {
+    Context& ctx = *ctx_;
+    const DType t = ctx.wire;
+    const int nbk = ctx.opt.dp_buckets;
     if (kind_ == StrategyKind::Hybrid3DMoE) {
       // Non-expert gradients are replicated across the EP group.
       int tk = timers_->begin(*compute_);
@@ -348,6 +357,106 @@ class Pipeline : public Strategy {
       void* g = ctx.opt.in_place ? grad_.data() : sum_grad_.data();
       optimizer_step(ctx, *compute_, params_.data(), mom_.data(), g, dp_ar_);
     }
+  }
+
+
+  // ---------------------------------------------------------------- 1F1B
+  // Non-interleaved one-forward-one-backward (PipeDream-flush): stage s runs
+  // w = min(S-s-1, mb) warm-up forwards, then alternates F(w+j) / B(j), then
+  // drains the remaining backwards. Same bubble as GPipe, at most w+1
+  // microbatches in flight. A send and the opposite-direction receive on the
+  // same link are posted as ONE group (send_forward_recv_backward /
+  // send_backward_recv_forward), so the two sides of a link never block each
+  // other; every link op waits only on events already enqueued.
+  void prev_link(int send_b, int recv_f) {
+    const DType t = ctx_->wire;
+    Stream& ls = *prev_stream_;
+    if (send_b >= 0) ls.wait(*bwd_done_[send_b]);
+    if (recv_f >= 2) ls.wait(*fwd_done_[recv_f - 2]);  // act_in[recv_f & 1] consumed
+    int tk = timers_->begin(ls);
+    prev_->group_start();
+    if (send_b >= 0) prev_->send(grad_out_[send_b & 1].data(), pipe_, t, prev_peer_, ls);
+    if (recv_f >= 0) prev_->recv(act_in_[recv_f & 1].data(), pipe_, t, prev_peer_, ls);
+    prev_->group_end();
+    timers_->end(tk, ls, send_b >= 0 ? "pp_send_time" : "pp_recv_time");
+    if (send_b >= 0) ls.record(*send_b_[send_b]);
+    if (recv_f >= 0) ls.record(*recv_f_[recv_f]);
+  }
+
+  void next_link(int send_f, int recv_b) {
+    const DType t = ctx_->wire;
+    Stream& ls = *next_stream_;
+    if (send_f >= 0) ls.wait(*fwd_done_[send_f]);
+    if (recv_b >= 2) ls.wait(*bwd_done_[recv_b - 2]);  // grad_in[recv_b & 1] consumed
+    int tk = timers_->begin(ls);
+    next_->group_start();
+    if (send_f >= 0) next_->send(act_out_[send_f & 1].data(), pipe_, t, next_peer_, ls);
+    if (recv_b >= 0) next_->recv(grad_in_[recv_b & 1].data(), pipe_, t, next_peer_, ls);
+    next_->group_end();
+    timers_->end(tk, ls, send_f >= 0 ? "pp_send_time" : "pp_recv_time");
+    if (send_f >= 0) ls.record(*send_f_[send_f]);
+    if (recv_b >= 0) ls.record(*recv_b_[recv_b]);
+  }
+
+  void fwd_step(int i) {
+    if (prev_)
+      timers_->stall(*compute_, *recv_f_[i], "pp_comm_time");
+    else
+      timers_->add("pp_comm_time", 0.0);
+    if (next_ && i >= 2) compute_->wait(*send_f_[i - 2]);  // act_out[i & 1] sent
+    micro_compute(fwd_mb_us_, fwd_mb_flops_);
+    compute_->record(*fwd_done_[i]);
+  }
+
+  void bwd_step(int j) {
+    const int nbk = ctx_->opt.dp_buckets;
+    if (next_)
+      timers_->stall(*compute_, *recv_b_[j], "pp_comm_time");
+    else
+      timers_->add("pp_comm_time", 0.0);
+    if (prev_ && j >= 2) compute_->wait(*send_b_[j - 2]);  // grad_out[j & 1] sent
+    if (j == mb_ - 1 && nbk > 1) {
+      for (int k = 0; k < nbk; ++k) {  // DP buckets overlap the last backward
+        ctx_->compute->run(*compute_, bwd_mb_us_ / nbk, bwd_mb_flops_ / nbk);
+        compute_->record(*bucket_ready_[k]);
+        dp_stream_->wait(*bucket_ready_[k]);
+        dp_allreduce_bucket(k, nbk);
+      }
+    } else {
+      micro_compute(bwd_mb_us_, bwd_mb_flops_);
+    }
+    compute_->record(*bwd_done_[j]);
+  }
+
+  void enqueue_1f1b() {
+    const int w = std::min(S_ - stage_ - 1, mb_);
+    const int steady = mb_ - w;
+    for (int i = 0; i < w; ++i) {
+      if (prev_) prev_link(-1, i);
+      fwd_step(i);
+      if (next_) next_link(i, -1);
+    }
+    if (steady > 0 && prev_) prev_link(-1, w);
+    for (int j = 0; j < steady; ++j) {
+      const int i = w + j;
+      fwd_step(i);
+      if (next_) next_link(i, j);  // send F(i) + receive B(j)
+      bwd_step(j);
+      if (prev_) prev_link(j, j + 1 < steady ? i + 1 : -1);  // send B(j) (+ receive F(i+1))
+    }
+    for (int j = steady; j < mb_; ++j) {
+      if (next_) next_link(-1, j);
+      bwd_step(j);
+      if (prev_) prev_link(j, -1);
+    }
+    finish_iteration();
+  }
+
+  void enqueue_iteration() override {
+    if (one_f_one_b_)
+      enqueue_1f1b();
+    else
+      enqueue_gpipe();
   }
 
   void dp_allreduce_bucket(int k, int nbk) {
@@ -426,6 +535,7 @@ class Pipeline : public Strategy {
       g["ep_allreduce_size_bytes"] = ne_ * es_;
     }
     g["dp_allreduce_size_bytes"] = dp_ar_ * es_;
+    g["pp_schedule"] = ctx.opt.pp_schedule;
     g["device"] = ctx.dev->kind() == DeviceKind::CPU ? "CPU" : "GPU";
     g["backend"] = dp_comm_->backend_name();
     return g;
@@ -459,6 +569,7 @@ class Pipeline : public Strategy {
   int S_ = 1, mb_ = 1, inner_ = 1, L_ = 0, layers_per_stage_ = 0, dp_size_ = 1;
   int stage_ = 0, inner_id_ = 0, dp_id_ = 0;
   bool reference_ = false;
+  bool one_f_one_b_ = false;
   uint64_t spmb_ = 0, pipe_ = 0, dp_ar_ = 0, tp_ar_ = 0, ne_ = 0, a2a_ = 0;
   size_t es_ = 2;
   double fwd_mb_us_ = 0, bwd_mb_us_ = 0, fwd_mb_flops_ = 0, bwd_mb_flops_ = 0;

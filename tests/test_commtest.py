@@ -99,23 +99,28 @@ def test_xgmi_bench_runs():
     assert len(out) == 8 and all(o["busbw_GBps"] > 0 for o in out)
 
 
-XGMI_STRATS = [
-    ("dp", "tiny_dense_8_bfloat16", ["2"], 2),
-    ("fsdp", "tiny_dense_8_bfloat16", ["4", "2"], 2),
-    ("fsdp", "tiny_dense_8_bfloat16", ["4", "2"], 4),
-    ("hybrid_2d", "tiny_dense_8_bfloat16", ["2", "4"], 2),
-    ("hybrid_3d", "tiny_dense_8_bfloat16", ["2", "2", "2"], 4),
-    ("hybrid_3d_moe", "tiny_moe_8_bfloat16", ["1", "2", "2"], 2),
+XGMI_STRATS = [  # strategy, model, positional args, extra flags, ranks
+    ("dp", "tiny_dense_8_bfloat16", ["2"], [], 2),
+    ("dp", "tiny_dense_8_bfloat16", ["4"], [], 8),
+    ("fsdp", "tiny_dense_8_bfloat16", ["4", "2"], [], 2),
+    ("fsdp", "tiny_dense_8_bfloat16", ["4", "2"], [], 4),
+    ("fsdp", "tiny_dense_8_bfloat16", ["4", "8"], [], 8),
+    ("hybrid_2d", "tiny_dense_8_bfloat16", ["2", "4"], [], 2),
+    ("hybrid_2d", "tiny_dense_8_bfloat16", ["4", "8"], ["--pp-schedule", "1f1b"], 4),
+    ("hybrid_3d", "tiny_dense_8_bfloat16", ["2", "2", "2"], [], 4),
+    ("hybrid_3d", "tiny_dense_8_bfloat16", ["2", "4", "2"], ["--pp-schedule", "1f1b"], 8),
+    ("hybrid_3d_moe", "tiny_moe_8_bfloat16", ["1", "2", "2"], [], 2),
 ]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("strategy,model,params,w", XGMI_STRATS)
-def test_strategies_on_xgmi(strategy, model, params, w, tmp_path):
+@pytest.mark.parametrize("strategy,model,params,extra,w", XGMI_STRATS)
+def test_strategies_on_xgmi(strategy, model, params, extra, w, tmp_path):
+    """Up to 8 ranks (a node's worth) sharing one MI355X through the xgmi backend."""
     _need_gpu()
     out = tmp_path / "r.json"
     data = os.path.join(ROOT, "tests", "data")
-    args = [os.path.join(ROOT, "build", "bin", strategy), model, *params, data, "-w", "1", "-r", "2",
+    args = [os.path.join(ROOT, "build", "bin", strategy), model, *params, data, *extra, "-w", "1", "-r", "2",
             "--backend", "xgmi", "-d", ",".join(["0"] * w), "--compute", "sleep", "--quiet", "--json", str(out)]
     p = launch(w, args, {"DLNB_XGMI_TIMEOUT_S": "60"})
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]

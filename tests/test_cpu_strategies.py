@@ -121,6 +121,33 @@ def test_hybrid_2d(w, S, mb, data_dir):
     assert g["dlnb"]["iteration"]["median_ms"] >= 0.95 * (mb + S - 1) * per_mb
 
 
+@pytest.mark.parametrize("w,S,mb", [(2, 2, 4), (4, 4, 8), (4, 4, 2), (4, 2, 1), (2, 2, 8)])
+def test_hybrid_2d_1f1b(w, S, mb, data_dir):
+    d = run(w, "hybrid_2d", "tiny_dense_8_bfloat16", S, mb, data_dir, "-w", 1, "-r", 2, "--pp-schedule", "1f1b")
+    g = d["global"]
+    assert g["pp_schedule"] == "1f1b"
+    for r in d["ranks"]:
+        assert len(r["pp_comm_time"]) == 2 * mb * 2
+        assert len(r["dp_comm_time"]) == 2
+    # same bubble as GPipe: (mb + S - 1) slots of (fwd + bwd) per microbatch
+    per_mb = 6.0 / S / mb
+    assert g["dlnb"]["iteration"]["median_ms"] >= 0.95 * (mb + S - 1) * per_mb
+
+
+@pytest.mark.parametrize("prog,model,params,w", [("hybrid_3d", "tiny_dense_8_bfloat16", (2, 4, 2), 8),
+                                                 ("hybrid_3d_moe", "tiny_moe_8_bfloat16", (2, 4, 2), 4)])
+def test_hybrid_3d_1f1b(prog, model, params, w, data_dir):
+    d = run(w, prog, model, *params, data_dir, "-w", 1, "-r", 2, "--pp-schedule", "1f1b", "--dp-buckets", "2")
+    assert d["global"]["pp_schedule"] == "1f1b" and len(d["ranks"]) == w
+
+
+def test_1f1b_rejects_reference_schedule(data_dir):
+    import subprocess
+    p = subprocess.run([os.path.join(BIN, "hybrid_2d"), "tiny_dense_8_bfloat16", "1", "2", data_dir, "--pp-schedule",
+                        "1f1b", "--schedule", "reference"], capture_output=True, text=True)
+    assert p.returncode == 2 and "1f1b" in p.stderr
+
+
 @pytest.mark.parametrize("w,S,T,gran", [(2, 1, 2, "microbatch"), (4, 2, 2, "microbatch"), (4, 2, 2, "layer"),
                                         (8, 2, 2, "microbatch")])
 def test_hybrid_3d(w, S, T, gran, data_dir):
