@@ -172,10 +172,47 @@ __device__ __forceinline__ int xcd_remap(int b, int T) {
 
 // One 128-byte K-tile of MFMA work for a wave owning rows wm*128.. (8
 // fragments) and columns wn*WTN.. (FN fragments) of the block tile.
-template <bool FP8, bool DEADLINE, int FN, int WTN>
+template <bool FP8, bool DEADLINE, int FN, int WTN, bool SWP = false>
 __device__ __forceinline__ void ktile_mfma(const char* __restrict__ At, const char* __restrict__ Bt, f32x4 (&acc)[8][FN],
                                            int wm, int wn, int r16, int h) {
-  if constexpr (!FP8) {
+  if constexpr (SWP && !FP8 && FN == 4) {
+    // Software-pipelined: step 1's 12 fragment reads are interleaved with
+    // step 0's 32 MFMAs (2 MFMAs, 1 ds_read, ...), so they are in flight
+    // while the matrix cores work instead of after a lgkmcnt(0) drain.
+    bf16x8 af[2][8], bfr[2][FN];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      af[0][i] = *reinterpret_cast<const bf16x8*>(At + swz(wm * 128 + i * 16 + r16, h));
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+      bfr[0][j] = *reinterpret_cast<const bf16x8*>(Bt + swz(wn * WTN + j * 16 + r16, h));
+    __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      af[1][i] = *reinterpret_cast<const bf16x8*>(At + swz(wm * 128 + i * 16 + r16, 4 + h));
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+      bfr[1][j] = *reinterpret_cast<const bf16x8*>(Bt + swz(wn * WTN + j * 16 + r16, 4 + h));
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j], af[0][i], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[1][j], af[1][i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  } else if constexpr (!FP8) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 af[8], bfr[FN];
@@ -280,7 +317,7 @@ __device__ __forceinline__ void store_tile(__bf16* __restrict__ C, int ldc, int 
 // WN = waves along N (WM = 2 along M): WN = 4 -> 8 waves (2 per SIMD) of
 // 128 x 64; WN = 2 -> 4 waves (1 per SIMD) of 128 x 128, twice the MFMAs per
 // LDS fragment read and the 256 accumulators in AGPRs.
-template <bool FP8, bool DEADLINE, int WN>
+template <bool FP8, bool DEADLINE, int WN, bool SWP = false>
 __global__ void __launch_bounds__(128 * WN, WN == 4 ? 2 : 1)
     gemm_tn_256_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
                        int K, int lda, int ldb, int ldc, uint64_t* __restrict__ slot, uint32_t epoch,
@@ -351,7 +388,7 @@ __global__ void __launch_bounds__(128 * WN, WN == 4 ? 2 : 1)
     }
     const char* At = cur;
     const char* Bt = cur + kTileBytes;
-    ktile_mfma<FP8, DEADLINE, FN, WTN>(At, Bt, acc, wm, wn, r16, h);
+    ktile_mfma<FP8, DEADLINE, FN, WTN, SWP>(At, Bt, acc, wm, wn, r16, h);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (DEADLINE) {
       // Double-buffered flag: written before barrier kt, read after it; the
@@ -526,11 +563,11 @@ bool gemm_shape_ok(int M, int N, int K, DType in_t) {
 
 namespace {
 
-template <bool FP8, bool DEADLINE, int WN>
+template <bool FP8, bool DEADLINE, int WN, bool SWP = false>
 void launch_gemm(int grid, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                  uint64_t* slot, uint32_t epoch, uint64_t ticks, uint64_t slice_end, hipStream_t st,
                  uint64_t* tstart = nullptr) {
-  hipLaunchKernelGGL((gemm_tn_256_kernel<FP8, DEADLINE, WN>), grid, 128 * WN, 0, st, static_cast<const char*>(A),
+  hipLaunchKernelGGL((gemm_tn_256_kernel<FP8, DEADLINE, WN, SWP>), grid, 128 * WN, 0, st, static_cast<const char*>(A),
                      static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc, slot, epoch, ticks,
                      slice_end, tstart);
 }
@@ -553,6 +590,8 @@ void dispatch_gemm(int waves, DType in_t, int grid, const void* A, const void* B
       launch_gemm<true, false, 2>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
     else
       launch_gemm<false, false, 2>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
+  } else if (!DEADLINE && waves == 2 && !fp8) {
+    launch_gemm<false, false, 4, true>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
   } else if (!DEADLINE && waves == 1) {
     if (fp8)
       hipLaunchKernelGGL(gemm_tn_ring_kernel<true>, grid, 512, 0, st, static_cast<const char*>(A),
@@ -588,7 +627,8 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
                    reinterpret_cast<uintptr_t>(C) % 8 == 0,
                "gemm_tn: misaligned base pointers");
   const int tiles = (M / kTile) * (N / kTile);
-  DLNB_REQUIRE(waves == 0 || waves == 1 || waves == 4 || waves == 8, "gemm_tn: variant must be 0, 1, 4 or 8");
+  DLNB_REQUIRE(waves == 0 || waves == 1 || waves == 2 || waves == 4 || waves == 8,
+               "gemm_tn: variant must be 0, 1, 2, 4 or 8");
   if (waves == 0) waves = gemm_ring_enabled() ? 1 : gemm_default_waves();
   dispatch_gemm<false>(waves, in_t, tiles, A, B, C, M, N, K, lda, ldb, ldc, nullptr, 0u, 0ull, 0ull, S(stream));
 }
