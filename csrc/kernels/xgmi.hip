@@ -257,6 +257,31 @@ __device__ __forceinline__ void reduce_tail(char* out, const char* const* srcs, 
 
 __device__ __forceinline__ int peer_at(const Peers& P, int j) { return (P.rank + j) % P.nranks; }
 
+// Push vectors [lo, hi) of src to slot `slot_off` of every peer's window
+// (and to `own` unless null): 4 loads in flight per thread, each loaded
+// vector stored to all peers (rank-staggered) before the next batch.
+__device__ __forceinline__ void push_all(const Peers& P, const uint4* __restrict__ src, size_t slot_off,
+                                         uint4* __restrict__ own, size_t lo, size_t hi) {
+  size_t i = lo + threadIdx.x;
+  for (; i + 3 * T < hi; i += 4 * T) {
+    uint4 v[4] = {src[i], src[i + T], src[i + 2 * T], src[i + 3 * T]};
+    for (int j = 1; j < P.nranks; ++j) {
+      uint4* d = V(P.win[peer_at(P, j)] + slot_off);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) d[i + u * T] = v[u];
+    }
+    if (own) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) own[i + u * T] = v[u];
+    }
+  }
+  for (; i < hi; i += T) {
+    const uint4 v = src[i];
+    for (int j = 1; j < P.nranks; ++j) V(P.win[peer_at(P, j)] + slot_off)[i] = v;
+    if (own) own[i] = v;
+  }
+}
+
 __global__ void __launch_bounds__(T) ag_kernel(Peers P, CollPiece c) {
   const size_t nv = c.bytes / 16;
   size_t lo, hi;
@@ -264,11 +289,7 @@ __global__ void __launch_bounds__(T) ag_kernel(Peers P, CollPiece c) {
   char* own = c.recv + static_cast<size_t>(P.rank) * c.recv_stride;
   const bool in_place = own == c.send;
   // push my block into slot[rank] of every peer's window (+ my own recv)
-  for (size_t i = lo + threadIdx.x; i < hi; i += T) {
-    uint4 v = V(c.send)[i];
-    for (int j = 1; j < P.nranks; ++j) V(P.win[peer_at(P, j)] + c.region + c.slot * P.rank)[i] = v;
-    if (!in_place) V(own)[i] = v;
-  }
+  push_all(P, V(c.send), c.region + c.slot * P.rank, in_place ? nullptr : V(own), lo, hi);
   for (int j = 1; j < P.nranks; ++j) copy_tail(P.win[peer_at(P, j)] + c.region + c.slot * P.rank, c.send, nv * 16, c.bytes);
   if (!in_place) copy_tail(own, c.send, nv * 16, c.bytes);
   exchange(P, 0, c.epoch);
@@ -337,10 +358,7 @@ __global__ void __launch_bounds__(T) ar1_kernel(Peers P, CollPiece c) {
   const size_t nv = c.bytes / 16;
   size_t lo, hi;
   blk_range(nv, lo, hi);
-  for (size_t i = lo + threadIdx.x; i < hi; i += T) {
-    uint4 v = V(c.send)[i];
-    for (int j = 1; j < P.nranks; ++j) V(P.win[peer_at(P, j)] + c.region + c.slot * P.rank)[i] = v;
-  }
+  push_all(P, V(c.send), c.region + c.slot * P.rank, nullptr, lo, hi);
   for (int j = 1; j < P.nranks; ++j) copy_tail(P.win[peer_at(P, j)] + c.region + c.slot * P.rank, c.send, nv * 16, c.bytes);
   exchange(P, 0, c.epoch);
   // every rank sums in the same (rank) order -> bitwise identical results
