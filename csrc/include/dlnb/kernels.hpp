@@ -42,9 +42,10 @@ int num_cus(int device);
 // C is always bf16.
 bool gemm_shape_ok(int M, int N, int K, DType in_t);
 // waves selects the variant: 8 = 8 waves (2 per SIMD, 128x64 per wave)
-// double buffered, 1 = the same with a 3-deep A ring (160 KiB LDS),
-// 4 = 4 waves (1 per SIMD, 128x128 per wave); 0 = the default (ring if
-// DLNB_GEMM_RING=1, else DLNB_GEMM_WAVES or 8).
+// double buffered, 2 = the same with software-pipelined fragment reads
+// (bf16), 1 = 8 waves with a 3-deep A ring (160 KiB LDS), 4 = 4 waves (1 per
+// SIMD, 128x128 per wave); 0 = the default: 2 for bf16, 8 for fp8 (ring if
+// DLNB_GEMM_RING=1, 4 waves if DLNB_GEMM_WAVES=4).
 void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
              void* stream, int waves = 0);
 int gemm_default_waves();
