@@ -68,6 +68,8 @@ def main() -> int:
                     help="enqueue every iteration instead of replaying one captured HIP graph")
     ap.add_argument("--schedule", default="overlap")
     ap.add_argument("--backend", default="auto")
+    ap.add_argument("--devices", default=None,
+                    help="device list by local rank, e.g. 0,0 to put 2 ranks on one GPU (xgmi backend tests)")
     ap.add_argument("--json", default=None, help="also write the full report here (rank 0)")
     a = ap.parse_args()
 
@@ -90,7 +92,7 @@ def main() -> int:
     def attempt(use_graph: bool):
         return engine.run("fsdp", a.model, a.units, world, base_path=ROOT, warmup=a.warmup, runs=a.steps,
                           compute=a.compute, schedule=a.schedule, backend=a.backend, wire_dtype="bf16",
-                          silent=True, json=a.json, graph=use_graph or None)
+                          silent=True, json=a.json, graph=use_graph or None, devices=a.devices)
 
     sys.stdout.flush()
     saved = os.dup(1)
