@@ -146,3 +146,14 @@ def test_graph_needs_gpu(bindir, data_dir):
     p = subprocess.run([os.path.join(bindir, "dp"), "tiny_dense_8_bfloat16", "2", data_dir, "--backend",
                         "cpu", "--graph", "-w", "0", "-r", "1"], capture_output=True, text=True)
     assert p.returncode == 2 and "graph" in p.stderr
+
+
+def test_unified_cli(tmp_path, data_dir, root):
+    from dlnetbench_amd.__main__ import main
+    out = tmp_path / "r.json"
+    assert main(["run", "-n", "2", "dp", "tiny_dense_8_bfloat16", "2", data_dir, "--backend", "cpu", "-w", "0", "-r",
+                 "1", "--silent", "--json", str(out)]) == 0
+    assert json.loads(out.read_text())["global"]["world_size"] == 2
+    assert main(["run", "bogus"]) == 1
+    assert main(["nope"]) == 1
+    assert main(["plan", "fsdp", "llama3_8b_16_bfloat16", "32", "8", "--world", "8", "--base", root]) == 0
