@@ -49,6 +49,7 @@ struct Options {
   std::string schedule = "overlap";    // overlap | reference
   std::string tp_granularity = "microbatch";  // microbatch | layer
   std::string pp_schedule = "gpipe";          // gpipe (reference) | 1f1b
+  bool ep_overlap = false;  // moe: overlap each half-microbatch's all-to-all with the other half's compute
   int dp_buckets = 1;  // hybrids: DP all-reduce buckets overlapped with the last backward
   bool in_place = false;
   bool optimizer = false;  // add an elementwise optimizer step over the local shard

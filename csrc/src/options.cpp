@@ -74,6 +74,7 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  --schedule S           overlap (stream-ordered) | reference (blocking like DLNetBench)\n"
      << "  --tp-granularity G     microbatch | layer (hybrid_3d)\n"
      << "  --pp-schedule gpipe|1f1b  hybrids: all forwards then all backwards (reference) or one-forward-one-backward\n"
+     << "  --ep-overlap           hybrid_3d_moe: two half-microbatches, each one's all-to-all under the other's compute\n"
      << "  --dp-buckets K         hybrids: DP all-reduce buckets overlapped with the last backward\n"
      << "  --in-place             in-place all-reduce (halves DP buffer memory)\n"
      << "  --optimizer            add an SGD-momentum step over the local gradient shard\n"
@@ -134,6 +135,8 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
       o.schedule = val("schedule");
     } else if (is("--tp-granularity")) {
       o.tp_granularity = val("tp-granularity");
+    } else if (a == "--ep-overlap") {
+      o.ep_overlap = true;
     } else if (is("--pp-schedule")) {
       o.pp_schedule = val("pp-schedule");
     } else if (is("--dp-buckets")) {

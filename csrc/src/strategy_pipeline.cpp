@@ -75,6 +75,7 @@ class Pipeline : public Strategy {
                                                   : 1;
     reference_ = o.schedule == "reference";
     one_f_one_b_ = o.pp_schedule == "1f1b";
+    ep_overlap_ = o.ep_overlap && kind_ == StrategyKind::Hybrid3DMoE && !reference_;
     DLNB_REQUIRE(!(one_f_one_b_ && reference_), "--pp-schedule 1f1b needs --schedule overlap");
     DLNB_REQUIRE(ctx.have_arch, "hybrid strategies need models/<model>.json (layer count)");
     L_ = static_cast<int>(ctx.arch.num_layers);
@@ -181,6 +182,13 @@ class Pipeline : public Strategy {
       ep_send_ = dev.alloc(a2a_ * inner_ * es_);
       ep_recv_ = dev.alloc(a2a_ * inner_ * es_);
       dev.fill_random(ep_send_.data(), a2a_ * inner_, ctx.wire, 4400, *compute_);
+      if (ep_overlap_) {
+        ep_stream_ = dev.create_stream(true);
+        for (int hh = 0; hh < 2; ++hh) {
+          chunk_done_[hh] = dev.create_event();
+          a2a_done_[hh] = dev.create_event();
+        }
+      }
     }
     if (o.optimizer) {
       DLNB_REQUIRE(ctx.wire == DType::BF16, "--optimizer needs --wire-dtype bf16");
@@ -215,7 +223,8 @@ class Pipeline : public Strategy {
     if (kind_ == StrategyKind::Hybrid3D)
       stats_.push_back({"tp_allreduce", CollKind::AllReduce, inner_, static_cast<double>(tp_ar_ * es_), "tp_comm_time"});
     if (kind_ == StrategyKind::Hybrid3DMoE)
-      stats_.push_back({"ep_alltoall", CollKind::AllToAll, inner_, static_cast<double>(a2a_ * inner_ * es_), "ep_comm_time"});
+      stats_.push_back({"ep_alltoall", CollKind::AllToAll, inner_,
+                        static_cast<double>((ep_overlap_ ? a2a_ / 2 : a2a_) * inner_ * es_), "ep_comm_time"});
   }
 
   // Compute of one microbatch with the inner-group collectives interleaved.
@@ -241,6 +250,23 @@ class Pipeline : public Strategy {
       if (reference_) {
         ce.run(*compute_, us, flops);
         for (int i = 0; i < n; ++i) ep_alltoall();
+      } else if (ep_overlap_) {
+        // Two half-microbatches in flight: the all-to-all of one half runs on
+        // the EP stream under the compute of the other (the dual-batch
+        // overlap of MoE training); a half's next chunk waits for its own
+        // previous all-to-all. One EP stream = one ordered lane per rank.
+        for (int i = 0; i < n; ++i) {
+          for (int hh = 0; hh < 2; ++hh) {
+            if (i > 0) compute_->wait(*a2a_done_[hh]);
+            ce.run(*compute_, us / n / 2, flops / n / 2);
+            compute_->record(*chunk_done_[hh]);
+            ep_stream_->wait(*chunk_done_[hh]);
+            ep_alltoall_half(hh);
+            ep_stream_->record(*a2a_done_[hh]);
+          }
+        }
+        compute_->wait(*a2a_done_[0]);
+        compute_->wait(*a2a_done_[1]);
       } else {
         for (int i = 0; i < n; ++i) {
           ce.run(*compute_, us / n, flops / n);
@@ -262,6 +288,16 @@ class Pipeline : public Strategy {
     int t = timers_->begin(*compute_);
     inner_comm_->all_to_all(ep_send_.data(), ep_recv_.data(), a2a_, ctx_->wire, *compute_);
     timers_->end(t, *compute_, "ep_comm_time");
+  }
+
+  // Half-microbatch all-to-all (--ep-overlap): half hh owns its own slice of
+  // the send / receive buffers, so the two halves never share memory.
+  void ep_alltoall_half(int hh) {
+    const uint64_t c0 = a2a_ / 2, c = hh == 0 ? c0 : a2a_ - c0;
+    const size_t off = static_cast<size_t>(hh) * c0 * inner_ * es_;
+    int t = timers_->begin(*ep_stream_);
+    inner_comm_->all_to_all(ep_send_.at(off), ep_recv_.at(off), c, ctx_->wire, *ep_stream_);
+    timers_->end(t, *ep_stream_, "ep_comm_time");
   }
 
   void enqueue_gpipe() {
@@ -474,12 +510,14 @@ class Pipeline : public Strategy {
     std::vector<Stream*> ss = {compute_.get(), dp_stream_.get()};
     if (prev_) ss.push_back(prev_stream_.get());
     if (next_) ss.push_back(next_stream_.get());
+    if (ep_stream_) ss.push_back(ep_stream_.get());
     return ss;
   }
   bool capturable() const override { return !reference_; }
 
   void synchronize() override {
     std::vector<Stream*> ss = {compute_.get(), dp_stream_.get()};
+    if (ep_stream_) ss.push_back(ep_stream_.get());
     std::vector<Communicator*> cs = {dp_comm_.get()};
     if (prev_) {
       ss.push_back(prev_stream_.get());
@@ -536,6 +574,7 @@ class Pipeline : public Strategy {
     }
     g["dp_allreduce_size_bytes"] = dp_ar_ * es_;
     g["pp_schedule"] = ctx.opt.pp_schedule;
+    if (kind_ == StrategyKind::Hybrid3DMoE) g["ep_overlap"] = ep_overlap_;
     g["device"] = ctx.dev->kind() == DeviceKind::CPU ? "CPU" : "GPU";
     g["backend"] = dp_comm_->backend_name();
     return g;
@@ -570,6 +609,9 @@ class Pipeline : public Strategy {
   int stage_ = 0, inner_id_ = 0, dp_id_ = 0;
   bool reference_ = false;
   bool one_f_one_b_ = false;
+  bool ep_overlap_ = false;
+  std::unique_ptr<Stream> ep_stream_;
+  std::unique_ptr<Event> chunk_done_[2], a2a_done_[2];
   uint64_t spmb_ = 0, pipe_ = 0, dp_ar_ = 0, tp_ar_ = 0, ne_ = 0, a2a_ = 0;
   size_t es_ = 2;
   double fwd_mb_us_ = 0, bwd_mb_us_ = 0, fwd_mb_flops_ = 0, bwd_mb_flops_ = 0;

@@ -29,7 +29,7 @@ _FLAG = {
     "comm_lanes": "--comm-lanes", "pp_schedule": "--pp-schedule",
 }
 _BOOL = {"in_place": "--in-place", "optimizer": "--optimizer", "loop": "--loop", "quiet": "--quiet",
-         "silent": "--silent", "graph": "--graph", "trace": "--trace"}
+         "silent": "--silent", "graph": "--graph", "trace": "--trace", "ep_overlap": "--ep-overlap"}
 
 
 def build_args(strategy: str, model: str, *params: int, base_path: str = ".", topology: bool = False,

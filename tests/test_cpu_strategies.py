@@ -141,6 +141,17 @@ def test_hybrid_3d_1f1b(prog, model, params, w, data_dir):
     assert d["global"]["pp_schedule"] == "1f1b" and len(d["ranks"]) == w
 
 
+@pytest.mark.parametrize("sched", ["gpipe", "1f1b"])
+def test_moe_ep_overlap(sched, data_dir):
+    base = run(4, "hybrid_3d_moe", "tiny_moe_8_bfloat16", 2, 4, 2, data_dir, "-w", 1, "-r", 2, "--pp-schedule", sched)
+    d = run(4, "hybrid_3d_moe", "tiny_moe_8_bfloat16", 2, 4, 2, data_dir, "-w", 1, "-r", 2, "--pp-schedule", sched,
+            "--ep-overlap")
+    assert d["global"]["ep_overlap"] is True and base["global"]["ep_overlap"] is False
+    for r0, r1 in zip(base["ranks"], d["ranks"]):
+        assert len(r1["ep_comm_time"]) == 2 * len(r0["ep_comm_time"])  # two halves per chunk
+        assert r1["comm"]["ep_alltoall"]["bytes_per_op"] * 2 == r0["comm"]["ep_alltoall"]["bytes_per_op"]
+
+
 def test_1f1b_rejects_reference_schedule(data_dir):
     import subprocess
     p = subprocess.run([os.path.join(BIN, "hybrid_2d"), "tiny_dense_8_bfloat16", "1", "2", data_dir, "--pp-schedule",
