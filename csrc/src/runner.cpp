@@ -244,6 +244,16 @@ Json run_benchmark(const Options& opt) {
     TraceRange tr("dlnb:setup");
     strat->setup(ctx);
   }
+  if (ctx.dev->kind() == DeviceKind::GPU) {
+    // More streams than hardware queues makes HIP share an in-order queue
+    // between two streams: a collective spinning on its peers can then hold
+    // back an unrelated kernel queued behind it on the other stream.
+    const char* hwq = std::getenv("GPU_MAX_HW_QUEUES");
+    const size_t nq = hwq ? static_cast<size_t>(std::max(1, std::atoi(hwq))) : 4;
+    if (strat->streams().size() > nq && ri.rank == 0)
+      std::cerr << "[dlnb] warning: " << strat->streams().size() << " streams per rank > GPU_MAX_HW_QUEUES=" << nq
+                << "; streams will share hardware queues" << std::endl;
+  }
   TimerSet& T = *strat->timers();
   const char* rkey = strat->runtime_key();
   T.ensure(rkey);

@@ -183,7 +183,15 @@ class Pipeline : public Strategy {
       ep_recv_ = dev.alloc(a2a_ * inner_ * es_);
       dev.fill_random(ep_send_.data(), a2a_ * inner_, ctx.wire, 4400, *compute_);
       if (ep_overlap_) {
-        ep_stream_ = dev.create_stream(true);
+        // The half-microbatch all-to-alls share the DP lane instead of a
+        // fifth stream: a middle stage already has compute + dp + prev + next,
+        // and with more streams than hardware queues (GPU_MAX_HW_QUEUES = 4)
+        // HIP aliases two streams onto one in-order queue, so a collective
+        // spinning on its peers can block an unrelated stream's kernel behind
+        // it (a cross-rank deadlock). One ordered lane is safe: every member
+        // of the EP and DP groups sits at the same stage and enqueues the
+        // same sequence.
+        ep_stream_ = dp_stream_.get();
         for (int hh = 0; hh < 2; ++hh) {
           chunk_done_[hh] = dev.create_event();
           a2a_done_[hh] = dev.create_event();
@@ -510,14 +518,12 @@ class Pipeline : public Strategy {
     std::vector<Stream*> ss = {compute_.get(), dp_stream_.get()};
     if (prev_) ss.push_back(prev_stream_.get());
     if (next_) ss.push_back(next_stream_.get());
-    if (ep_stream_) ss.push_back(ep_stream_.get());
     return ss;
   }
   bool capturable() const override { return !reference_; }
 
   void synchronize() override {
     std::vector<Stream*> ss = {compute_.get(), dp_stream_.get()};
-    if (ep_stream_) ss.push_back(ep_stream_.get());
     std::vector<Communicator*> cs = {dp_comm_.get()};
     if (prev_) {
       ss.push_back(prev_stream_.get());
@@ -610,7 +616,7 @@ class Pipeline : public Strategy {
   bool reference_ = false;
   bool one_f_one_b_ = false;
   bool ep_overlap_ = false;
-  std::unique_ptr<Stream> ep_stream_;
+  Stream* ep_stream_ = nullptr;  // = dp_stream_ (see setup)
   std::unique_ptr<Event> chunk_done_[2], a2a_done_[2];
   uint64_t spmb_ = 0, pipe_ = 0, dp_ar_ = 0, tp_ar_ = 0, ne_ = 0, a2a_ = 0;
   size_t es_ = 2;

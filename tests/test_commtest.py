@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DLNB = os.path.join(ROOT, "build", "bin", "dlnb")
 
 
-def launch(n, args, env_extra=None, timeout=240):
+def launch(n, args, env_extra=None, timeout=140):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.update(env_extra or {})
