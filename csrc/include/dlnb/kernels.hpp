@@ -46,8 +46,12 @@ bool gemm_shape_ok(int M, int N, int K, DType in_t);
 // (bf16), 1 = 8 waves with a 3-deep A ring (160 KiB LDS), 4 = 4 waves (1 per
 // SIMD, 128x128 per wave); 0 = the default: 2 for bf16, 8 for fp8 (ring if
 // DLNB_GEMM_RING=1, 4 waves if DLNB_GEMM_WAVES=4).
+// 3 = the 8-phase ping-pong schedule (gemm_8phase.hip; needs >= 2 K-tiles).
 void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
              void* stream, int waves = 0);
+bool gemm_8phase_shape_ok(int M, int N, int K, DType in_t);
+void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
+                    void* stream);
 int gemm_default_waves();
 
 // Persistent deadline variant (the default stand-in compute): a grid of

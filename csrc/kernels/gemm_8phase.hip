@@ -1,0 +1,289 @@
+// 8-phase ping-pong MFMA GEMM for gfx950: C[M,N] (bf16) = A[M,K] . B[N,K]^T.
+//
+// Same operand contract as gemm_tn_256_kernel (kernels.hip) - bf16 or OCP
+// fp8 e4m3 inputs, 256 x 256 block tile, 128-byte K-tiles, XOR-swizzled
+// lane-linear LDS image filled by global_load_lds - but a different schedule
+// (cdna_hip_programming.md §5 "The 256² 8-phase template", T3+T4):
+//
+//   * A K-tile is split into four 128-row half-tiles (A0 A1 | B0 B1, 16 KiB
+//     each; two 64 KiB buffers = 128 KiB LDS) and its MFMA work into four
+//     phases, one per 128 x 128 quadrant of C, visited (0,0) (0,1) (1,1)
+//     (1,0) so every phase after the first reads ONE half-tile's fragments
+//     (the B0 fragments of phase 0 stay in registers for phase 3).
+//   * Every phase = {ds_read its fragments, issue one half-tile of
+//     global_load_lds (2 per thread), counted vmcnt, raw s_barrier, MFMAs
+//     under s_setprio(1), raw s_barrier}. The two wave rows run one barrier
+//     apart (wave row 1 takes an extra barrier up front), so on every SIMD
+//     one wave issues its loads while the other one runs its MFMAs.
+//   * Loads stay in flight across barriers: a half-tile is waited for
+//     (vmcnt(8) = 4 half-tiles still in flight) four phases after it was
+//     issued and read one phase after that wait; a buffer slot is re-staged
+//     at least two phases after its last read (the RAW / WAR rules of the
+//     staggered schedule; derivation in docs/KERNELS.md).
+//
+// Variant 3 of dlnb::kernels::gemm_tn (the library's one-shot GEMM).
+#include <hip/hip_runtime.h>
+
+#include "dlnb/kernels.hpp"
+
+namespace dlnb {
+namespace kernels {
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+
+constexpr int kT = 256;          // block tile (M and N)
+constexpr int kRB = 128;         // bytes of K per K-tile row
+constexpr int kHalf = 128 * kRB; // one half-tile: 128 rows x 128 B = 16 KiB
+constexpr int kBuf = 4 * kHalf;  // A0 A1 B0 B1
+enum : int { kA0 = 0, kA1 = 1, kB0 = 2, kB1 = 3 };
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * kRB + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+// s_waitcnt vmcnt(N) only (expcnt / lgkmcnt left at "no wait"), gfx9 encoding.
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// One half-tile: 16 wave-instructions of global_load_lds_dwordx4, 2 per wave.
+// The swizzle is applied to the per-lane source address (LDS writes are
+// lane-linear): LDS slot q of row r holds chunk q ^ ((r >> 1) & 7).
+__device__ __forceinline__ void stage_half(const char* __restrict__ g, size_t ld, char* lds, int w, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int inst = i * 8 + w;
+    const int slot = inst * 64 + lane;
+    const int r = slot >> 3;
+    const int c = (slot & 7) ^ ((r >> 1) & 7);
+    __builtin_amdgcn_global_load_lds((gbl_ptr_t)(g + static_cast<size_t>(r) * ld + (c << 4)),
+                                     (lds_ptr_t)(lds + inst * 1024), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ int xcd_remap(int b, int T) {
+  const int q = T / 8, r = T % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// Fragment registers of one wave. bf16: [k-step][frag] 16-B reads;
+// fp8: one 32-B (two-chunk) read pair per fragment covers the whole K-tile.
+template <bool FP8>
+struct Frags;
+template <>
+struct Frags<false> {
+  bf16x8 a[2][4], bx[2][2], by[2][2];
+};
+template <>
+struct Frags<true> {
+  i32x8 a[4], bx[2], by[2];
+};
+
+template <bool FP8, int NF>
+__device__ __forceinline__ void read_frags(const char* half, int row0, int r16, int h, bf16x8 (&f)[2][NF]) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int i = 0; i < NF; ++i) f[ks][i] = *reinterpret_cast<const bf16x8*>(half + swz(row0 + i * 16 + r16, ks * 4 + h));
+}
+template <bool FP8, int NF>
+__device__ __forceinline__ void read_frags(const char* half, int row0, int r16, int h, i32x8 (&f)[NF]) {
+#pragma unroll
+  for (int i = 0; i < NF; ++i) {
+    const int row = row0 + i * 16 + r16;
+    const int4 lo = *reinterpret_cast<const int4*>(half + swz(row, 2 * h));
+    const int4 hi = *reinterpret_cast<const int4*>(half + swz(row, 2 * h + 1));
+    f[i] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  }
+}
+
+// acc[i][j] += A-frags x B-frags for one 64 x 32 sub-tile of a quadrant.
+__device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[4][2], const bf16x8 (&a)[2][4], const bf16x8 (&b)[2][2]) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][j], a[ks][i], acc[i][j], 0, 0, 0);
+}
+__device__ __forceinline__ void mfma_quadrant(f32x4 (&acc)[4][2], const i32x8 (&a)[4], const i32x8 (&b)[2]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(b[j], a[i], acc[i][j], 0, 0, 0, 127, 0, 127);
+}
+
+struct Ctx {
+  const char* Ab;  // A rows of this block tile, K-tile 0
+  const char* Bb;
+  size_t lda, ldb;  // bytes
+  char* smem;
+  int w, lane, wr, wc, r16, h;
+};
+
+// Where half-tile `slot` of K-tile t comes from / goes to.
+__device__ __forceinline__ void stage(const Ctx& c, int t, int slot) {
+  const bool isA = slot == kA0 || slot == kA1;
+  const int hi = slot == kA1 || slot == kB1;
+  const char* src = (isA ? c.Ab + static_cast<size_t>(hi) * 128 * c.lda : c.Bb + static_cast<size_t>(hi) * 128 * c.ldb) +
+                    static_cast<size_t>(t) * kRB;
+  stage_half(src, isA ? c.lda : c.ldb, c.smem + (t & 1) * kBuf + slot * kHalf, c.w, c.lane);
+}
+
+// Phase Q of K-tile v. Staging schedule (G = half-tile issued in the phase):
+//   Q0: B1(v+1)  Q1: A1(v+1)  Q2: A0(v+2)  Q3: B0(v+2)
+// VM = vmcnt after the issue (8 in steady state: retires the half-tile
+// issued four phases earlier); STAGE = whether the phase's G exists.
+template <bool FP8, int Q, int VM, bool STAGE>
+__device__ __forceinline__ void phase(const Ctx& c, int v, Frags<FP8>& f, f32x4 (&acc)[2][2][4][2]) {
+  const char* cur = c.smem + (v & 1) * kBuf;
+  if constexpr (Q == 0) {
+    read_frags<FP8, 2>(cur + kB0 * kHalf, c.wc * 32, c.r16, c.h, f.bx);
+    __builtin_amdgcn_sched_barrier(0);
+    read_frags<FP8, 4>(cur + kA0 * kHalf, c.wr * 64, c.r16, c.h, f.a);
+  } else if constexpr (Q == 1) {
+    read_frags<FP8, 2>(cur + kB1 * kHalf, c.wc * 32, c.r16, c.h, f.by);
+  } else if constexpr (Q == 2) {
+    read_frags<FP8, 4>(cur + kA1 * kHalf, c.wr * 64, c.r16, c.h, f.a);
+  }
+  if constexpr (STAGE) {
+    if constexpr (Q == 0) stage(c, v + 1, kB1);
+    if constexpr (Q == 1) stage(c, v + 1, kA1);
+    if constexpr (Q == 2) stage(c, v + 2, kA0);
+    if constexpr (Q == 3) stage(c, v + 2, kB0);
+  }
+  wait_vm<VM>();
+  raw_barrier();
+  __builtin_amdgcn_s_setprio(1);
+  if constexpr (Q == 0) mfma_quadrant(acc[0][0], f.a, f.bx);
+  if constexpr (Q == 1) mfma_quadrant(acc[0][1], f.a, f.by);
+  if constexpr (Q == 2) mfma_quadrant(acc[1][1], f.a, f.by);
+  if constexpr (Q == 3) mfma_quadrant(acc[1][0], f.a, f.bx);
+  __builtin_amdgcn_s_setprio(0);
+  raw_barrier();
+}
+
+template <bool FP8, int V0, int V1, int V2, int V3, bool S01, bool S23>
+__device__ __forceinline__ void ktile(const Ctx& c, int v, Frags<FP8>& f, f32x4 (&acc)[2][2][4][2]) {
+  phase<FP8, 0, V0, S01>(c, v, f, acc);
+  phase<FP8, 1, V1, S01>(c, v, f, acc);
+  phase<FP8, 2, V2, S23>(c, v, f, acc);
+  phase<FP8, 3, V3, S23>(c, v, f, acc);
+}
+
+template <bool FP8>
+__global__ void __launch_bounds__(512, 1)
+    gemm_8phase_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
+                       int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
+  const int tid = threadIdx.x;
+  Ctx c;
+  c.lane = tid & 63;
+  c.w = tid >> 6;
+  c.wr = c.w >> 2;  // waves w and w+4 share a SIMD: one per wave row
+  c.wc = c.w & 3;
+  c.r16 = c.lane & 15;
+  c.h = c.lane >> 4;
+  c.smem = smem;
+  const int nt_m = M / kT, nt_n = N / kT, T = nt_m * nt_n;
+  const int b = xcd_remap(blockIdx.x, T);
+  constexpr int GROUP = 8;  // GROUP M-tiles share their B panels in L2
+  const int per_group = GROUP * nt_n;
+  const int first_m = (b / per_group) * GROUP;
+  const int gsz = min(nt_m - first_m, GROUP);
+  const int tm = first_m + (b % per_group) % gsz;
+  const int tn = (b % per_group) / gsz;
+  constexpr int esz = FP8 ? 1 : 2;
+  c.lda = static_cast<size_t>(lda) * esz;
+  c.ldb = static_cast<size_t>(ldb) * esz;
+  c.Ab = A + static_cast<size_t>(tm) * kT * c.lda;
+  c.Bb = B + static_cast<size_t>(tn) * kT * c.ldb;
+  const int nk = (K * esz) / kRB;  // >= 2 (host checks)
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[qm][qn][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  Frags<FP8> f;
+
+  // Prologue, in the steady-state issue order: A0(0) B0(0) B1(0) A1(0) A0(1) B0(1).
+  stage(c, 0, kA0);
+  stage(c, 0, kB0);
+  stage(c, 0, kB1);
+  stage(c, 0, kA1);
+  stage(c, 1, kA0);
+  stage(c, 1, kB0);
+  wait_vm<8>();  // A0(0), B0(0) landed
+  raw_barrier();
+  if (c.wr == 1) raw_barrier();  // wave row 1 runs one barrier behind
+
+  int v = 0;
+  for (; v < nk - 2; ++v) ktile<FP8, 8, 8, 8, 8, true, true>(c, v, f, acc);
+  ktile<FP8, 8, 8, 6, 4, true, false>(c, v, f, acc);       // v = nk-2: stages only tile nk-1
+  ktile<FP8, 2, 0, 0, 0, false, false>(c, v + 1, f, acc);  // v = nk-1: drains
+  if (c.wr == 0) raw_barrier();  // re-align the barrier counts of the two rows
+
+  // Epilogue: lane holds C[m = .. + r16][n = .. + 4h + 0..3] of each fragment.
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int m = tm * kT + qm * 128 + c.wr * 64 + i * 16 + c.r16;
+          const int n = tn * kT + qn * 128 + c.wc * 32 + j * 16 + 4 * c.h;
+          const f32x4 a = acc[qm][qn][i][j];
+          bf16x4 o;
+          o[0] = static_cast<__bf16>(a[0]);
+          o[1] = static_cast<__bf16>(a[1]);
+          o[2] = static_cast<__bf16>(a[2]);
+          o[3] = static_cast<__bf16>(a[3]);
+          *reinterpret_cast<bf16x4*>(C + static_cast<size_t>(m) * ldc + n) = o;
+        }
+}
+
+}  // namespace
+
+bool gemm_8phase_shape_ok(int M, int N, int K, DType in_t) {
+  const size_t esz = dtype_size(in_t);
+  return gemm_shape_ok(M, N, K, in_t) && (static_cast<size_t>(K) * esz) / kRB >= 2;
+}
+
+void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
+                    void* stream) {
+  DLNB_REQUIRE(gemm_8phase_shape_ok(M, N, K, in_t), "gemm 8-phase: unsupported shape M=" << M << " N=" << N << " K=" << K);
+  const int tiles = (M / kT) * (N / kT);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (in_t == DType::FP8_E4M3)
+    hipLaunchKernelGGL(gemm_8phase_kernel<true>, tiles, 512, 0, st, static_cast<const char*>(A),
+                       static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc);
+  else
+    hipLaunchKernelGGL(gemm_8phase_kernel<false>, tiles, 512, 0, st, static_cast<const char*>(A),
+                       static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) DLNB_THROW("gemm 8-phase launch failed: " << hipGetErrorString(e));
+}
+
+}  // namespace kernels
+}  // namespace dlnb

@@ -627,14 +627,19 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
                    reinterpret_cast<uintptr_t>(C) % 8 == 0,
                "gemm_tn: misaligned base pointers");
   const int tiles = (M / kTile) * (N / kTile);
-  DLNB_REQUIRE(waves == 0 || waves == 1 || waves == 2 || waves == 4 || waves == 8,
-               "gemm_tn: variant must be 0, 1, 2, 4 or 8");
+  DLNB_REQUIRE(waves == 0 || waves == 1 || waves == 2 || waves == 3 || waves == 4 || waves == 8,
+               "gemm_tn: variant must be 0, 1, 2, 3, 4 or 8");
+  if (waves == 3 && gemm_8phase_shape_ok(M, N, K, in_t)) {  // (one K-tile: falls back to the default)
+    gemm_tn_8phase(A, B, C, M, N, K, lda, ldb, ldc, in_t, stream);
+    return;
+  }
   if (waves == 0) {
     // bf16: the software-pipelined 8-wave body (+3-6 % over the plain one,
     // profiles/gemm_bench_r1.md); fp8: the plain MX body.
     const int w = gemm_default_waves();
     waves = gemm_ring_enabled() ? 1 : w == 4 ? 4 : in_t == DType::BF16 ? 2 : 8;
   }
+  if (waves == 3) waves = in_t == DType::BF16 ? 2 : 8;
   dispatch_gemm<false>(waves, in_t, tiles, A, B, C, M, N, K, lda, ldb, ldc, nullptr, 0u, 0ull, 0ull, S(stream));
 }
 

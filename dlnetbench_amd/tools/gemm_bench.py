@@ -1,12 +1,14 @@
-"""Throughput of the hand-written MFMA GEMM vs torch (hipBLASLt) on MI355X.
+"""Throughput of the hand-written MFMA GEMM variants vs torch (hipBLASLt) on MI355X.
 
     python -m dlnetbench_amd.tools.gemm_bench [--shapes 8192x14336x4096,...] [--dtype bf16|fp8]
+                                              [--variants 2,3,8]
 
-Interleaves the two implementations round by round in one process
+Interleaves the implementations round by round in one process
 (cdna_hip_programming.md §5.4 rule 24) on random [-1, 1) operands (rule 25)
-and prints TFLOP/s (median, best) as JSON lines. Variants: ours = 8 waves double
-buffered (default), ours_alt = the variant under test (bf16: software-pipelined
-fragment reads, waves=2; fp8: the 3-deep A ring, waves=1), ours4 = 4 waves.
+and prints TFLOP/s (median, best) as JSON lines, one key per variant
+(``v<n>_tflops_*``, n = the ``waves`` selector of ops.gemm.gemm_tn: 8 = double
+buffered, 2 = software-pipelined fragment reads (bf16 default), 1 = 3-deep A
+ring, 4 = 4 waves, 3 = 8-phase ping-pong) and ``torch_tflops_*``.
 """
 from __future__ import annotations
 
@@ -24,6 +26,7 @@ def main(argv=None) -> int:
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--variants", default=None, help="comma list of gemm_tn variants (default: 2,3,8 bf16; 8,3 fp8)")
     a = ap.parse_args(argv)
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float8_e4m3fn
     for shp in a.shapes.split(","):
@@ -35,15 +38,12 @@ def main(argv=None) -> int:
         C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         flop = 2.0 * M * N * K
 
-        def ours():
-            gemm.gemm_tn(A, B, C, waves=8)
+        variants = [int(v) for v in (a.variants or ("2,3,8" if a.dtype == "bf16" else "8,3")).split(",")]
 
-        def ours8():
-            gemm.gemm_tn(A, B, C, waves=2 if dt == torch.bfloat16 else 1)
+        def mk(v):
+            return lambda: gemm.gemm_tn(A, B, C, waves=v)
 
-        def ours4():
-            gemm.gemm_tn(A, B, C, waves=4)
-
+        fns = [(f"v{v}", mk(v)) for v in variants]
         if dt == torch.bfloat16:
             def ref():
                 torch.matmul(A, B.t(), out=C)
@@ -52,14 +52,14 @@ def main(argv=None) -> int:
 
             def ref():
                 torch._scaled_mm(A, B.t(), scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
-
-        res = {"ours": [], "ours_alt": [], "ours4": [], "torch": []}
-        for fn in (ours, ours8, ours4, ref):  # warm
+        fns.append(("torch", ref))
+        res = {name: [] for name, _ in fns}
+        for _, fn in fns:  # warm
             for _ in range(3):
                 fn()
         torch.cuda.synchronize()
         for _ in range(a.rounds):
-            for name, fn in (("ours", ours), ("ours_alt", ours8), ("ours4", ours4), ("torch", ref)):
+            for name, fn in fns:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.iters):

@@ -15,7 +15,7 @@ def need_gpu():
 from dlnetbench_amd.ops import gemm  # noqa: E402
 
 
-@pytest.mark.parametrize("waves", [0, 1, 2, 8, 4])
+@pytest.mark.parametrize("waves", [0, 1, 2, 3, 8, 4])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 512, 128), (512, 256, 1024), (768, 1280, 640),
                                    (2048, 1024, 4096)])
 def test_gemm_bf16_matches_torch(M, N, K, waves):
@@ -29,19 +29,20 @@ def test_gemm_bf16_matches_torch(M, N, K, waves):
     assert (c.float() - ref).abs().max().item() < tol
 
 
-def test_gemm_bf16_identity_asymmetric():
-    # A = I picks rows of B: catches any row/column swap in the C write.
+@pytest.mark.parametrize("waves", [0, 3])
+def test_gemm_bf16_identity_asymmetric(waves):
+    # A = I picks rows of B: catches any row/column/quadrant swap in the C write.
     M = N = 256
     K = 256
     a = torch.eye(M, K, device="cuda", dtype=torch.bfloat16)
     b = (torch.arange(N * K, device="cuda", dtype=torch.float32).reshape(N, K) % 97 / 8.0).to(torch.bfloat16)
-    c = gemm.gemm_tn(a, b)
+    c = gemm.gemm_tn(a, b, waves=waves)
     torch.cuda.synchronize()
     assert torch.equal(c.float(), b.float().t())
 
 
 @pytest.mark.skipif(not hasattr(torch, "float8_e4m3fn"), reason="torch without float8")
-@pytest.mark.parametrize("waves", [0, 1, 2, 8, 4])
+@pytest.mark.parametrize("waves", [0, 1, 2, 3, 8, 4])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 512), (1024, 512, 2048)])
 def test_gemm_fp8_matches_torch(M, N, K, waves):
     g = torch.Generator(device="cuda").manual_seed(7 + M)
