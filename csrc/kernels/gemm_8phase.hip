@@ -144,21 +144,45 @@ __device__ __forceinline__ void stage(const Ctx& c, int t, int slot) {
   stage_half(src, isA ? c.lda : c.ldb, c.smem + (t & 1) * kBuf + slot * kHalf, c.w, c.lane);
 }
 
+// Deadline state of the persistent variant: thread 0 (wave row 0) reads the
+// clock in phase 3 of every K-tile, writes the stop decision into an LDS flag
+// (completed before its barrier), and every wave reads it after its own first
+// barrier of that phase - the write precedes every read (the rows are one
+// barrier apart) and the next write is four phases away.
+typedef __attribute__((address_space(3))) volatile int lds_flag_t;
+struct Deadline {
+  uint64_t t0, ticks, slice_end;
+  lds_flag_t* flag;  // 2 ints at the end of the staging array (typed LDS: a
+                     // generic pointer becomes a flat store that waits vmcnt(0))
+  int tid;
+};
+
 // Phase Q of K-tile v. Staging schedule (G = half-tile issued in the phase):
 //   Q0: B1(v+1)  Q1: A1(v+1)  Q2: A0(v+2)  Q3: B0(v+2)
 // VM = vmcnt after the issue (8 in steady state: retires the half-tile
 // issued four phases earlier); STAGE = whether the phase's G exists.
-template <bool FP8, int Q, int VM, bool STAGE>
-__device__ __forceinline__ void phase(const Ctx& c, int v, Frags<FP8>& f, f32x4 (&acc)[2][2][4][2]) {
+// Returns (DL, phase 3) whether the deadline has passed.
+template <bool FP8, bool DL, int Q, int VM, bool STAGE>
+__device__ __forceinline__ bool phase(const Ctx& c, int v, Frags<FP8>& f, f32x4 (&acc)[2][2][4][2], const Deadline& d,
+                                      uint64_t& now) {
   const char* cur = c.smem + (v & 1) * kBuf;
   if constexpr (Q == 0) {
     read_frags<FP8, 2>(cur + kB0 * kHalf, c.wc * 32, c.r16, c.h, f.bx);
     __builtin_amdgcn_sched_barrier(0);
     read_frags<FP8, 4>(cur + kA0 * kHalf, c.wr * 64, c.r16, c.h, f.a);
+    // the clock is read three phases before its use, so its (scalar-memory)
+    // latency never stalls wave 0 in front of a barrier
+    if constexpr (DL) now = __builtin_amdgcn_s_memrealtime();
   } else if constexpr (Q == 1) {
     read_frags<FP8, 2>(cur + kB1 * kHalf, c.wc * 32, c.r16, c.h, f.by);
   } else if constexpr (Q == 2) {
     read_frags<FP8, 4>(cur + kA1 * kHalf, c.wr * 64, c.r16, c.h, f.a);
+  } else if constexpr (DL) {
+    if (d.tid == 0) {
+      const uint64_t el = (now - d.t0) & ((1ull << 48) - 1);
+      d.flag[v & 1] = el >= d.ticks || el >= d.slice_end;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
   }
   if constexpr (STAGE) {
     if constexpr (Q == 0) stage(c, v + 1, kB1);
@@ -168,6 +192,8 @@ __device__ __forceinline__ void phase(const Ctx& c, int v, Frags<FP8>& f, f32x4 
   }
   wait_vm<VM>();
   raw_barrier();
+  bool stop = false;
+  if constexpr (DL && Q == 3) stop = __builtin_amdgcn_readfirstlane(d.flag[v & 1]) != 0;
   __builtin_amdgcn_s_setprio(1);
   if constexpr (Q == 0) mfma_quadrant(acc[0][0], f.a, f.bx);
   if constexpr (Q == 1) mfma_quadrant(acc[0][1], f.a, f.by);
@@ -175,32 +201,24 @@ __device__ __forceinline__ void phase(const Ctx& c, int v, Frags<FP8>& f, f32x4 
   if constexpr (Q == 3) mfma_quadrant(acc[1][0], f.a, f.bx);
   __builtin_amdgcn_s_setprio(0);
   raw_barrier();
+  return stop;
 }
 
-template <bool FP8, int V0, int V1, int V2, int V3, bool S01, bool S23>
-__device__ __forceinline__ void ktile(const Ctx& c, int v, Frags<FP8>& f, f32x4 (&acc)[2][2][4][2]) {
-  phase<FP8, 0, V0, S01>(c, v, f, acc);
-  phase<FP8, 1, V1, S01>(c, v, f, acc);
-  phase<FP8, 2, V2, S23>(c, v, f, acc);
-  phase<FP8, 3, V3, S23>(c, v, f, acc);
+template <bool FP8, bool DL, int V0, int V1, int V2, int V3, bool S01, bool S23>
+__device__ __forceinline__ bool ktile(const Ctx& c, int v, Frags<FP8>& f, f32x4 (&acc)[2][2][4][2], const Deadline& d) {
+  uint64_t now = 0;
+  phase<FP8, DL, 0, V0, S01>(c, v, f, acc, d, now);
+  phase<FP8, DL, 1, V1, S01>(c, v, f, acc, d, now);
+  phase<FP8, DL, 2, V2, S23>(c, v, f, acc, d, now);
+  return phase<FP8, DL, 3, V3, S23>(c, v, f, acc, d, now);
 }
 
-template <bool FP8>
-__global__ void __launch_bounds__(512, 1)
-    gemm_8phase_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
-                       int K, int lda, int ldb, int ldc) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
-  const int tid = threadIdx.x;
-  Ctx c;
-  c.lane = tid & 63;
-  c.w = tid >> 6;
-  c.wr = c.w >> 2;  // waves w and w+4 share a SIMD: one per wave row
-  c.wc = c.w & 3;
-  c.r16 = c.lane & 15;
-  c.h = c.lane >> 4;
-  c.smem = smem;
-  const int nt_m = M / kT, nt_n = N / kT, T = nt_m * nt_n;
-  const int b = xcd_remap(blockIdx.x, T);
+// One 256 x 256 tile of C. Returns false if the deadline stopped it (no
+// store; every staged load has been waited for).
+template <bool FP8, bool DL>
+__device__ __forceinline__ bool tile(Ctx& c, const char* __restrict__ A, const char* __restrict__ B,
+                                     __bf16* __restrict__ C, int M, int N, int K, int ldc, int b, const Deadline& d) {
+  const int nt_m = M / kT, nt_n = N / kT;
   constexpr int GROUP = 8;  // GROUP M-tiles share their B panels in L2
   const int per_group = GROUP * nt_n;
   const int first_m = (b / per_group) * GROUP;
@@ -208,8 +226,6 @@ __global__ void __launch_bounds__(512, 1)
   const int tm = first_m + (b % per_group) % gsz;
   const int tn = (b % per_group) / gsz;
   constexpr int esz = FP8 ? 1 : 2;
-  c.lda = static_cast<size_t>(lda) * esz;
-  c.ldb = static_cast<size_t>(ldb) * esz;
   c.Ab = A + static_cast<size_t>(tm) * kT * c.lda;
   c.Bb = B + static_cast<size_t>(tn) * kT * c.ldb;
   const int nk = (K * esz) / kRB;  // >= 2 (host checks)
@@ -236,11 +252,18 @@ __global__ void __launch_bounds__(512, 1)
   raw_barrier();
   if (c.wr == 1) raw_barrier();  // wave row 1 runs one barrier behind
 
+  bool stop = false;
   int v = 0;
-  for (; v < nk - 2; ++v) ktile<FP8, 8, 8, 8, 8, true, true>(c, v, f, acc);
-  ktile<FP8, 8, 8, 6, 4, true, false>(c, v, f, acc);       // v = nk-2: stages only tile nk-1
-  ktile<FP8, 2, 0, 0, 0, false, false>(c, v + 1, f, acc);  // v = nk-1: drains
+  for (; v < nk - 2 && !stop; ++v) stop = ktile<FP8, DL, 8, 8, 8, 8, true, true>(c, v, f, acc, d);
+  if (!stop) stop = ktile<FP8, DL, 8, 8, 6, 4, true, false>(c, v, f, acc, d);  // v = nk-2: stages only tile nk-1
+  if (!stop) stop = ktile<FP8, DL, 2, 0, 0, 0, false, false>(c, v + 1, f, acc, d);  // v = nk-1: drains
   if (c.wr == 0) raw_barrier();  // re-align the barrier counts of the two rows
+  if constexpr (DL) {
+    if (stop) {  // partial tile: the stand-in result is not needed
+      wait_vm<0>();
+      return false;
+    }
+  }
 
   // Epilogue: lane holds C[m = .. + r16][n = .. + 4h + 0..3] of each fragment.
 #pragma unroll
@@ -261,6 +284,54 @@ __global__ void __launch_bounds__(512, 1)
           o[3] = static_cast<__bf16>(a[3]);
           *reinterpret_cast<bf16x4*>(C + static_cast<size_t>(m) * ldc + n) = o;
         }
+  return true;
+}
+
+// DL = false: one launch, grid = tiles. DL = true: persistent stand-in
+// compute with the contract of gemm_tn_256_kernel's deadline mode
+// (kernels.hip): grid <= resident blocks walks the tiles round-robin and
+// stops min(ticks, slice_end) after t0, agreed per epoch through *slot.
+template <bool FP8, bool DL>
+__global__ void __launch_bounds__(512, 1)
+    gemm_8phase_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
+                       int K, int lda, int ldb, int ldc, uint64_t* __restrict__ slot, uint32_t epoch, uint64_t ticks,
+                       uint64_t slice_end, uint64_t* __restrict__ tstart) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + 16];  // ONE array: staging + deadline flag
+  const int tid = threadIdx.x;
+  Ctx c;
+  c.lane = tid & 63;
+  c.w = tid >> 6;
+  c.wr = c.w >> 2;  // waves w and w+4 share a SIMD: one per wave row
+  c.wc = c.w & 3;
+  c.r16 = c.lane & 15;
+  c.h = c.lane >> 4;
+  c.smem = smem;
+  constexpr int esz = FP8 ? 1 : 2;
+  c.lda = static_cast<size_t>(lda) * esz;
+  c.ldb = static_cast<size_t>(ldb) * esz;
+  const int T = (M / kT) * (N / kT);
+  Deadline d{0, ticks, slice_end, (lds_flag_t*)(smem + 2 * kBuf), tid};
+  if constexpr (!DL) {
+    tile<FP8, false>(c, A, B, C, M, N, K, ldc, xcd_remap(blockIdx.x, T), d);
+  } else {
+    constexpr uint64_t kMask48 = (1ull << 48) - 1;
+    if (tid == 0) {
+      const uint64_t raw = __builtin_amdgcn_s_memrealtime();
+      const uint64_t mine = (static_cast<uint64_t>(epoch) << 48) | (raw & kMask48);
+      uint64_t cur = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while ((cur >> 48) != epoch) {
+        if (__hip_atomic_compare_exchange_strong(slot, &cur, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          cur = mine;
+          if (tstart) __hip_atomic_store(tstart, raw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+      }
+      d.t0 = cur & kMask48;  // only thread 0 reads the clock
+    }
+    for (int round = 0;; ++round)
+      if (!tile<FP8, true>(c, A, B, C, M, N, K, ldc, xcd_remap((blockIdx.x + round * gridDim.x) % T, T), d)) return;
+  }
 }
 
 }  // namespace
@@ -275,14 +346,34 @@ void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, 
   DLNB_REQUIRE(gemm_8phase_shape_ok(M, N, K, in_t), "gemm 8-phase: unsupported shape M=" << M << " N=" << N << " K=" << K);
   const int tiles = (M / kT) * (N / kT);
   hipStream_t st = static_cast<hipStream_t>(stream);
+  auto* a = static_cast<const char*>(A);
+  auto* b = static_cast<const char*>(B);
+  auto* cc = static_cast<__bf16*>(C);
   if (in_t == DType::FP8_E4M3)
-    hipLaunchKernelGGL(gemm_8phase_kernel<true>, tiles, 512, 0, st, static_cast<const char*>(A),
-                       static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc);
+    hipLaunchKernelGGL((gemm_8phase_kernel<true, false>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc, nullptr,
+                       0u, 0ull, 0ull, nullptr);
   else
-    hipLaunchKernelGGL(gemm_8phase_kernel<false>, tiles, 512, 0, st, static_cast<const char*>(A),
-                       static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc);
+    hipLaunchKernelGGL((gemm_8phase_kernel<false, false>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc, nullptr,
+                       0u, 0ull, 0ull, nullptr);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 8-phase launch failed: " << hipGetErrorString(e));
+}
+
+void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
+                             uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
+                             uint64_t* tstart) {
+  DLNB_REQUIRE(gemm_8phase_shape_ok(M, N, K, in_t), "gemm 8-phase deadline: unsupported shape");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  auto* a = static_cast<const char*>(A);
+  auto* b = static_cast<const char*>(B);
+  auto* cc = static_cast<__bf16*>(C);
+  // bf16 only: the fp8 MX body plus the deadline bookkeeping spills inside
+  // the K-loop (256 VGPRs); fp8 deadline work stays on gemm_tn_256_kernel.
+  DLNB_REQUIRE(in_t == DType::BF16, "gemm 8-phase deadline: bf16 only");
+  hipLaunchKernelGGL((gemm_8phase_kernel<false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
+                     ticks, slice_end, tstart);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) DLNB_THROW("gemm 8-phase deadline launch failed: " << hipGetErrorString(e));
 }
 
 }  // namespace kernels

@@ -610,6 +610,11 @@ void dispatch_gemm(int waves, DType in_t, int grid, const void* A, const void* B
 
 }  // namespace
 
+bool gemm_8phase_enabled() {
+  static const bool on = env_int("DLNB_GEMM_8PHASE", 1) != 0;
+  return on;
+}
+
 int gemm_default_waves() {
   static const int w = env_int("DLNB_GEMM_WAVES", 8) == 4 ? 4 : 8;
   return w;
@@ -629,7 +634,8 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
   const int tiles = (M / kTile) * (N / kTile);
   DLNB_REQUIRE(waves == 0 || waves == 1 || waves == 2 || waves == 3 || waves == 4 || waves == 8,
                "gemm_tn: variant must be 0, 1, 2, 3, 4 or 8");
-  if (waves == 3 && gemm_8phase_shape_ok(M, N, K, in_t)) {  // (one K-tile: falls back to the default)
+  if (waves == 0 && gemm_8phase_enabled()) waves = 3;
+  if (waves == 3 && gemm_8phase_shape_ok(M, N, K, in_t)) {  // (one K-tile: falls back)
     gemm_tn_8phase(A, B, C, M, N, K, lda, ldb, ldc, in_t, stream);
     return;
   }
@@ -648,6 +654,10 @@ void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K
   if (slice_end == 0) slice_end = ticks;
   DLNB_REQUIRE(gemm_shape_ok(M, N, K, in_t), "gemm_tn_deadline: unsupported shape");
   DLNB_REQUIRE(slot != nullptr && grid > 0 && epoch > 0 && epoch < 65536, "gemm_tn_deadline: bad slot/grid/epoch");
+  if (gemm_8phase_enabled() && in_t == DType::BF16 && gemm_8phase_shape_ok(M, N, K, in_t)) {
+    gemm_tn_8phase_deadline(A, B, C, M, N, K, in_t, ticks, slot, epoch, grid, stream, slice_end, tstart);
+    return;
+  }
   // 8 waves: the 4-wave variant spills once the deadline logic is added.
   dispatch_gemm<true>(8, in_t, grid, A, B, C, M, N, K, K, K, N, slot, epoch, ticks, slice_end, S(stream), tstart);
 }

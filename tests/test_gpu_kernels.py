@@ -82,13 +82,19 @@ def test_sgd_momentum_matches_torch():
 def test_deadline_kernels_hit_duration(fn):
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    run = gemm.idle_wait_us if fn == "idle" else gemm.busy_spin_us
+    run(50.0)  # first launch of the kernel (code object load) outside the timing
+    torch.cuda.synchronize()
     for us in (200.0, 5000.0):
-        e0.record(s)
-        (gemm.idle_wait_us if fn == "idle" else gemm.busy_spin_us)(us)
-        e1.record(s)
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1)
-        assert us / 1e3 * 0.97 <= ms <= us / 1e3 * 1.10 + 0.05, (us, ms)
+        times = []
+        for _ in range(3):
+            e0.record(s)
+            run(us)
+            e1.record(s)
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1))
+        ms = sorted(times)[1]
+        assert us / 1e3 * 0.97 <= ms <= us / 1e3 * 1.10 + 0.05, (us, times)
 
 
 @pytest.mark.parametrize("us", [100.0, 2000.0, 30000.0])
@@ -100,10 +106,15 @@ def test_deadline_gemm_duration(us):
     c = torch.empty(8192, 14336, device="cuda", dtype=torch.bfloat16)
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    gemm.gemm_deadline_us(a, b, c, us)  # warm
-    e0.record(s)
-    gemm.gemm_deadline_us(a, b, c, us)
-    e1.record(s)
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1)
-    assert us / 1e3 <= ms * 1.01 and ms <= us / 1e3 * 1.05 + 0.03, (us, ms)
+    stamp = torch.zeros(8, dtype=torch.int64, device="cuda")
+    for _ in range(3):  # warm: code object load, clocks out of idle
+        gemm.gemm_deadline_us(a, b, c, us, stamp)
+    times = []
+    for _ in range(5):
+        e0.record(s)
+        gemm.gemm_deadline_us(a, b, c, us, stamp)
+        e1.record(s)
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1))
+    ms = sorted(times)[2]
+    assert us / 1e3 <= ms * 1.01 and ms <= us / 1e3 * 1.05 + 0.03, (us, times)
