@@ -52,6 +52,10 @@ struct Options {
   bool ep_overlap = false;  // moe: overlap each half-microbatch's all-to-all with the other half's compute
   int dp_buckets = 1;  // hybrids: DP all-reduce buckets overlapped with the last backward
   bool in_place = false;
+  // dp: ZeRO stage. 0 = replicated (reference), 1 = optimizer state sharded
+  // (all-reduce grads, step on the 1/W shard, all-gather parameters), 2 =
+  // gradients sharded too (bucketed reduce-scatter instead of all-reduce).
+  int zero = 0;
   bool optimizer = false;  // add an elementwise optimizer step over the local shard
   bool loop = false;       // the reference's *_loop builds
   long long max_loop_iters = 0;

@@ -77,6 +77,8 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  --ep-overlap           hybrid_3d_moe: two half-microbatches, each one's all-to-all under the other's compute\n"
      << "  --dp-buckets K         hybrids: DP all-reduce buckets overlapped with the last backward\n"
      << "  --in-place             in-place all-reduce (halves DP buffer memory)\n"
+     << "  --zero 0|1|2           dp: ZeRO stage (1: sharded optimizer + parameter all-gather, 2: + gradient\n"
+     << "                         reduce-scatter instead of all-reduce)\n"
      << "  --optimizer            add an SGD-momentum step over the local gradient shard\n"
      << "  --loop [--max-loop-iters N]  run iterations forever (interference generator)\n"
      << "  --time-scale F         scale all compute durations by F\n"
@@ -143,6 +145,8 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
       o.dp_buckets = to_int(val("dp-buckets"), "dp-buckets");
     } else if (a == "--in-place") {
       o.in_place = true;
+    } else if (is("--zero")) {
+      o.zero = to_int(val("zero"), "zero");
     } else if (a == "--optimizer") {
       o.optimizer = true;
     } else if (a == "--loop") {
@@ -217,6 +221,8 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
                "--tp-granularity must be microbatch or layer");
   DLNB_REQUIRE(o.comm_lanes == "single" || o.comm_lanes == "split", "--comm-lanes must be single or split");
   DLNB_REQUIRE(o.dp_buckets >= 1, "--dp-buckets must be >= 1");
+  DLNB_REQUIRE(o.zero >= 0 && o.zero <= 2, "--zero must be 0, 1 or 2 (ZeRO-3 is the fsdp strategy)");
+  DLNB_REQUIRE(o.zero == 0 || kind == StrategyKind::DP, "--zero applies to dp");
   DLNB_REQUIRE(o.time_scale > 0, "--time-scale must be > 0");
   return o;
 }

@@ -11,6 +11,17 @@
 // the all-reduce of bucket i waits on it from a high-priority comm stream.
 // One stream per communicator (RCCL serialises a communicator anyway; the
 // reference's nb streams on one comm add nothing but ordering hazards).
+//
+// Extension (absent from the reference): --zero 1|2 shards
+// the optimizer state (ZeRO-1) and the gradients (ZeRO-2) over the W ranks.
+// Bucket i is padded to W * ceil(size_i / W) elements. ZeRO-1: bucketed
+// all-reduce as above, then the optimizer updates this rank's 1/W slice of
+// every bucket and the updated parameter slices are all-gathered; ZeRO-2:
+// the backward's all-reduces become reduce-scatters into the rank's gradient
+// shard (half the bytes per rank). After the gradients (barrier_time = the
+// exposed part, as in dp) the optimizer updates the shard bucket by bucket and
+// bucket i's parameter all-gather runs under bucket i+1's update; the next
+// forward waits for all of them ("param_allgather_exposed").
 #include <cmath>
 
 #include "dlnb/strategy.hpp"
@@ -37,22 +48,35 @@ class DataParallel : public Strategy {
 
     Device& dev = *ctx.dev;
     es_ = dtype_size(ctx.wire);
+    zero_ = o.zero;
+    W_ = ctx.world();
+    for (uint64_t sz : sizes_) shard_.push_back((sz + W_ - 1) / W_);
     std::vector<int> all;
     for (int r = 0; r < ctx.world(); ++r) all.push_back(r);
-    comm_ = ctx.comms->create("dp/world", all, sizes_[0] * es_, false);
+    comm_ = ctx.comms->create("dp/world", all, (zero_ ? shard_[0] * W_ : sizes_[0]) * es_, false);
     compute_ = dev.create_stream(false);
     comm_stream_ = dev.create_stream(true);
     // Out-of-place like the reference unless asked (or forced by memory).
     size_t need = static_cast<size_t>(P_) * es_ * 2;
     in_place_ = o.in_place || (dev.kind() == DeviceKind::GPU && need > dev.free_memory() * 0.85);
+    if (zero_ == 2) in_place_ = false;  // the reduce-scatter writes a separate shard
     for (int i = 0; i < nb_; ++i) {
-      grads_.push_back(dev.alloc(sizes_[i] * es_));
-      if (!in_place_) sums_.push_back(dev.alloc(sizes_[i] * es_));
+      const uint64_t n = zero_ ? shard_[i] * W_ : sizes_[i];  // padded for ZeRO
+      grads_.push_back(dev.alloc(n * es_));
+      if (!in_place_) sums_.push_back(dev.alloc((zero_ == 2 ? shard_[i] : n) * es_));
       ready_.push_back(dev.create_event());
-      dev.fill_random(grads_.back().data(), sizes_[i], ctx.wire, 1000 + i, *compute_);
+      dev.fill_random(grads_.back().data(), n, ctx.wire, 1000 + i, *compute_);
+      if (zero_) {
+        pshard_.push_back(dev.alloc(shard_[i] * es_));
+        mshard_.push_back(dev.alloc(shard_[i] * es_));
+        pfull_.push_back(dev.alloc(shard_[i] * W_ * es_));
+        dev.fill_random(pshard_.back().data(), shard_[i], ctx.wire, 2000 + i, *compute_);
+        opt_done_.push_back(dev.create_event());
+      }
     }
     done_ = dev.create_event();
-    if (o.optimizer) {
+    ag_done_ = dev.create_event();
+    if (o.optimizer && !zero_) {
       DLNB_REQUIRE(ctx.wire == DType::BF16, "--optimizer needs --wire-dtype bf16");
       params_ = dev.alloc(P_ * es_);
       mom_ = dev.alloc(P_ * es_);
@@ -61,10 +85,64 @@ class DataParallel : public Strategy {
     timers_.reset(new TimerSet(dev));
     timers_->ensure("barrier_time");
     timers_->ensure("allreduce_time");
-    stats_ = {{"allreduce", CollKind::AllReduce, comm_->size(), static_cast<double>(sizes_[0] * es_), "allreduce_time"}};
+    if (zero_ == 2)
+      stats_ = {{"reduce_scatter", CollKind::ReduceScatter, W_, static_cast<double>(shard_[0] * W_ * es_),
+                 "reduce_scatter_time"}};
+    else
+      stats_ = {{"allreduce", CollKind::AllReduce, W_, static_cast<double>((zero_ ? shard_[0] * W_ : sizes_[0]) * es_),
+                 "allreduce_time"}};
+    if (zero_) {
+      for (const char* k : {"reduce_scatter_time", "param_allgather_time", "param_allgather_exposed"}) timers_->ensure(k);
+      stats_.push_back({"param_allgather", CollKind::AllGather, W_, static_cast<double>(shard_[0] * W_ * es_),
+                        "param_allgather_time"});
+    }
+  }
+
+  // ZeRO-1/2 backward communication, optimizer on the shard, parameter all-gather.
+  void enqueue_zero() {
+    Context& ctx = *ctx_;
+    ComputeEngine& ce = *ctx.compute;
+    const int me = comm_->rank();
+    ce.run(*compute_, fwd_us_, fwd_flops_);
+    for (int i = 0; i < nb_; ++i) {
+      ce.run(*compute_, bwd_us_per_bucket_, bwd_flops_per_bucket_);
+      compute_->record(*ready_[i]);
+      comm_stream_->wait(*ready_[i]);
+      const uint64_t n = shard_[i] * W_;
+      if (zero_ == 2) {
+        int t = timers_->begin(*comm_stream_);
+        comm_->reduce_scatter(grads_[i].data(), sums_[i].data(), shard_[i], ctx.wire, *comm_stream_);
+        timers_->end(t, *comm_stream_, "reduce_scatter_time");
+      } else {
+        int t = timers_->begin(*comm_stream_);
+        void* out = in_place_ ? grads_[i].data() : sums_[i].data();
+        comm_->all_reduce(grads_[i].data(), out, n, ctx.wire, *comm_stream_);
+        timers_->end(t, *comm_stream_, "allreduce_time");
+      }
+    }
+    comm_stream_->record(*done_);
+    timers_->stall(*compute_, *done_, "barrier_time");  // exposed gradient communication (as dp)
+    // Optimizer step on this rank's slice of each bucket, then that bucket's
+    // parameter all-gather, which overlaps the next bucket's update.
+    for (int i = 0; i < nb_; ++i) {
+      const void* g = zero_ == 2 ? sums_[i].data()
+                                 : (in_place_ ? grads_[i].at(me * shard_[i] * es_) : sums_[i].at(me * shard_[i] * es_));
+      if (ctx.wire == DType::BF16) optimizer_step(ctx, *compute_, pshard_[i].data(), mshard_[i].data(), g, shard_[i]);
+      compute_->record(*opt_done_[i]);
+      comm_stream_->wait(*opt_done_[i]);
+      int t = timers_->begin(*comm_stream_);
+      comm_->all_gather(pshard_[i].data(), pfull_[i].data(), shard_[i], ctx.wire, *comm_stream_);
+      timers_->end(t, *comm_stream_, "param_allgather_time");
+    }
+    comm_stream_->record(*ag_done_);
+    timers_->stall(*compute_, *ag_done_, "param_allgather_exposed");
   }
 
   void enqueue_iteration() override {
+    if (zero_) {
+      enqueue_zero();
+      return;
+    }
     Context& ctx = *ctx_;
     ComputeEngine& ce = *ctx.compute;
     ce.run(*compute_, fwd_us_, fwd_flops_);
@@ -121,6 +199,11 @@ class DataParallel : public Strategy {
     g["device"] = ctx.dev->kind() == DeviceKind::CPU ? "CPU" : "GPU";
     g["backend"] = comm_->backend_name();
     g["in_place"] = in_place_;
+    g["zero_stage"] = zero_;
+    if (zero_) {
+      g["shard_size_params"] = shard_[0];
+      g["param_allgather_msg_size_bytes"] = static_cast<double>(shard_[0] * W_ * es_);
+    }
     return g;
   }
 
@@ -129,6 +212,11 @@ class DataParallel : public Strategy {
     r["runtimes"] = timers_->values_json("runtimes");
     r["barrier_time"] = timers_->values_json("barrier_time");
     r["allreduce_time"] = timers_->values_json("allreduce_time");
+    if (zero_) {
+      r["reduce_scatter_time"] = timers_->values_json("reduce_scatter_time");
+      r["param_allgather_time"] = timers_->values_json("param_allgather_time");
+      r["param_allgather_exposed"] = timers_->values_json("param_allgather_exposed");
+    }
     return r;
   }
 
@@ -142,6 +230,11 @@ class DataParallel : public Strategy {
   std::vector<uint64_t> sizes_;
   double fwd_us_ = 0, bwd_us_per_bucket_ = 0, fwd_flops_ = 0, bwd_flops_per_bucket_ = 0;
   bool in_place_ = false;
+  int zero_ = 0, W_ = 1;
+  std::vector<uint64_t> shard_;        // per bucket: ceil(size / W)
+  std::vector<Buffer> pshard_, mshard_, pfull_;  // ZeRO: parameter / momentum shards, gathered parameters
+  std::vector<std::unique_ptr<Event>> opt_done_;
+  std::unique_ptr<Event> ag_done_;
   std::unique_ptr<Communicator> comm_;
   std::unique_ptr<Stream> compute_, comm_stream_;
   std::vector<Buffer> grads_, sums_;

@@ -86,13 +86,26 @@ def _split(total: int, parts: int) -> List[int]:
     return [base + (1 if i < rem else 0) for i in range(parts)]
 
 
-def plan_dp(st: ModelStats, world: int, nb: int, wire: str = "bf16") -> Plan:
+def plan_dp(st: ModelStats, world: int, nb: int, wire: str = "bf16", zero: int = 0) -> Plan:
+    """zero = 1|2: ZeRO extension of csrc/src/strategy_dp.cpp (buckets padded to
+    world * ceil(size / world); stage 2 reduce-scatters instead of all-reducing)."""
     es = WIRE_BYTES[wire]
     sizes = _split(st.model_size, nb)
-    p = Plan("dp", world, {"num_buckets": nb},
+    p = Plan("dp", world, {"num_buckets": nb, "zero": zero},
              {"fwd": st.fwd_us, "bwd_per_bucket": st.bwd_us / nb})
-    p.messages.append(Message("bucket_allreduce", "allreduce", world, sizes[0], nb, sizes[0] * es))
-    p.memory_bytes = 2 * st.model_size * es
+    if not zero:
+        p.messages.append(Message("bucket_allreduce", "allreduce", world, sizes[0], nb, sizes[0] * es))
+        p.memory_bytes = 2 * st.model_size * es
+        return p
+    shard = -(-sizes[0] // world)
+    if zero == 2:
+        p.messages.append(Message("bucket_reduce_scatter", "reduce_scatter", world, shard, nb, shard * world * es))
+    else:
+        p.messages.append(Message("bucket_allreduce", "allreduce", world, shard * world, nb, shard * world * es))
+    p.messages.append(Message("param_allgather", "allgather", world, shard, nb, shard * world * es))
+    total = sum(-(-s // world) for s in sizes)
+    # padded grads + (zero 1: reduced copy | zero 2: reduced shard) + param/momentum shards + gathered params
+    p.memory_bytes = (2 * total * world + (total * world if zero == 1 else total) + 2 * total) * es
     return p
 
 
@@ -173,10 +186,11 @@ def main(argv=None) -> int:
     ap.add_argument("--world", type=int, required=True)
     ap.add_argument("--base", default=".")
     ap.add_argument("--wire", default="bf16")
+    ap.add_argument("--zero", type=int, default=0, help="dp: ZeRO stage 0|1|2")
     a = ap.parse_args(argv)
     st = load_stats(os.path.join(a.base, "model_stats", a.model + ".txt"))
     if a.strategy == "dp":
-        pl = plan_dp(st, a.world, *a.params, wire=a.wire)
+        pl = plan_dp(st, a.world, *a.params, wire=a.wire, zero=a.zero)
     elif a.strategy == "fsdp":
         pl = plan_fsdp(st, a.world, *a.params, wire=a.wire)
     else:

@@ -65,6 +65,34 @@ def test_dp(w, data_dir):
     assert d["global"]["dlnb"]["iteration"]["median_ms"] >= 6.0 * 0.98
 
 
+@pytest.mark.parametrize("w,zero", [(1, 1), (2, 1), (2, 2), (4, 2), (3, 2)])
+def test_dp_zero(w, zero, data_dir):
+    """ZeRO-1/2 (extension): sharded optimizer + parameter all-gather, reduce-scatter for stage 2."""
+    d = run(w, "dp", "tiny_dense_8_bfloat16", 5, data_dir, "-w", 1, "-r", 2, "--zero", zero)
+    g = d["global"]
+    assert DP_GLOBAL <= set(g) and g["zero_stage"] == zero
+    shard = -(-200001 // w)  # largest bucket 200001 elements, padded to w shards
+    assert g["shard_size_params"] == shard
+    assert g["param_allgather_msg_size_bytes"] == shard * w * 2
+    for r in d["ranks"]:
+        assert len(r["runtimes"]) == 2 and len(r["param_allgather_time"]) == 10
+        assert len(r["param_allgather_exposed"]) == 2
+        key = "reduce_scatter_time" if zero == 2 else "allreduce_time"
+        assert len(r[key]) == 10
+        other = "allreduce_time" if zero == 2 else "reduce_scatter_time"
+        assert len(r[other]) == 0
+        kinds = set(r["comm"])
+        assert "param_allgather" in kinds and ("reduce_scatter" if zero == 2 else "allreduce") in kinds
+        for rt in r["runtimes"]:
+            assert rt >= 0.006 * 0.98
+
+
+def test_dp_zero_rejected_elsewhere(data_dir):
+    code, outs = launch.launch(1, [os.path.join(BIN, "fsdp"), "tiny_dense_8_bfloat16", "4", "1", data_dir, "--zero", "1"],
+                               timeout=60, capture=True)
+    assert code != 0 and "--zero applies to dp" in "".join(o or "" for o in outs)
+
+
 @pytest.mark.parametrize("w,F", [(2, 2), (4, 2), (4, 4)])
 def test_fsdp(w, F, data_dir):
     U = 4

@@ -96,3 +96,19 @@ def test_invalid_layouts(stats):
         P.plan_fsdp(st, 6, 4, 4)
     with pytest.raises(ValueError):
         P.plan_hybrid(st, 8, "hybrid_3d", 3, 4, 2, layers=32)
+
+
+
+def test_plan_dp_zero(stats):
+    st = stats("llama3_8b_16_bfloat16")
+    base = P.plan_dp(st, 8, 10)
+    z1 = P.plan_dp(st, 8, 10, zero=1)
+    z2 = P.plan_dp(st, 8, 10, zero=2)
+    b0 = base.messages[0].elements
+    shard = -(-b0 // 8)
+    assert [m.op for m in z1.messages] == ["allreduce", "allgather"]
+    assert [m.op for m in z2.messages] == ["reduce_scatter", "allgather"]
+    assert z2.messages[0].elements == shard and z2.messages[1].wire_bytes == shard * 8 * 2
+    # ZeRO-2 moves half the gradient bytes of an all-reduce per rank (busbw factor (n-1)/n vs 2(n-1)/n)
+    assert P.busbw_factor("reduce_scatter", 8) * 2 == P.busbw_factor("allreduce", 8)
+    assert z2.memory_bytes < z1.memory_bytes
