@@ -7,6 +7,7 @@
 //   hybrid_2d     <model> <num_stages> <num_microbatches> <base_path>
 //   hybrid_3d     <model> <num_stages> <num_microbatches> <num_tensor_shards> <base_path>
 //   hybrid_3d_moe <model> <num_stages> <num_microbatches> <num_expert_shards> <base_path>
+//   hybrid_cp     <model> <num_cp_shards> <base_path>   (extension: DP x context parallel)
 //   flags: -w warmups (3)  -r runs (5; hybrid_3d 3)  -d devices ("")
 //          -m min_exectime seconds (0)  -h
 // Long options are dlnb extensions (run-time backend, compute model,
@@ -18,7 +19,7 @@
 
 namespace dlnb {
 
-enum class StrategyKind { DP, FSDP, Hybrid2D, Hybrid3D, Hybrid3DMoE };
+enum class StrategyKind { DP, FSDP, Hybrid2D, Hybrid3D, Hybrid3DMoE, HybridCP };
 
 StrategyKind parse_strategy(const std::string& s);
 const char* strategy_name(StrategyKind k);
@@ -34,6 +35,8 @@ struct Options {
   int num_microbatches = 1;
   int num_tensor_shards = 1;
   int num_expert_shards = 1;
+  int num_cp_shards = 1;
+  std::string cp_algo = "ring";  // hybrid_cp: ring (P2P KV blocks) | ulysses (all-to-all)
 
   int warmup = 3;
   int runs = 5;

@@ -73,6 +73,11 @@ class Strategy {
   virtual Json rank_json() const = 0;
   // Bus-bandwidth summary per collective kind for this rank (bytes, seconds).
   virtual Json comm_summary() const = 0;
+  // Lower bound of an iteration from compute alone (µs): fwd + bwd for
+  // dp/fsdp, the pipeline's (mb + S - 1)(f_mb + b_mb), (fwd + bwd) / C for CP.
+  virtual double compute_floor_us(const Context& ctx) const {
+    return ctx.stats.avg_forward_time_us + ctx.stats.avg_backward_time_us;
+  }
   TimerSet* timers() { return timers_.get(); }
 
  protected:
@@ -82,6 +87,7 @@ class Strategy {
 std::unique_ptr<Strategy> make_dp();
 std::unique_ptr<Strategy> make_fsdp();
 std::unique_ptr<Strategy> make_pipeline(StrategyKind kind);  // hybrid_2d / 3d / 3d_moe
+std::unique_ptr<Strategy> make_cp();                          // hybrid_cp (extension)
 
 // Creates ctx.dev + ctx.comms for a backend (auto | rccl | xgmi | cpu);
 // GPU ranks take device list[local_rank] ("-d 0,1,..", default all GPUs).

@@ -13,7 +13,8 @@ StrategyKind parse_strategy(const std::string& s) {
   if (s == "hybrid_2d" || s == "dp_pp") return StrategyKind::Hybrid2D;
   if (s == "hybrid_3d" || s == "dp_pp_tp") return StrategyKind::Hybrid3D;
   if (s == "hybrid_3d_moe" || s == "dp_pp_ep") return StrategyKind::Hybrid3DMoE;
-  DLNB_THROW("unknown strategy '" << s << "' (dp, fsdp, hybrid_2d, hybrid_3d, hybrid_3d_moe)");
+  if (s == "hybrid_cp" || s == "dp_cp") return StrategyKind::HybridCP;
+  DLNB_THROW("unknown strategy '" << s << "' (dp, fsdp, hybrid_2d, hybrid_3d, hybrid_3d_moe, hybrid_cp)");
 }
 
 const char* strategy_name(StrategyKind k) {
@@ -23,6 +24,7 @@ const char* strategy_name(StrategyKind k) {
     case StrategyKind::Hybrid2D: return "hybrid_2d";
     case StrategyKind::Hybrid3D: return "hybrid_3d";
     case StrategyKind::Hybrid3DMoE: return "hybrid_3d_moe";
+    case StrategyKind::HybridCP: return "hybrid_cp";
   }
   return "?";
 }
@@ -37,6 +39,7 @@ std::vector<std::string> positional_names(StrategyKind k) {
     case StrategyKind::Hybrid3D: return {"model", "num_stages", "num_microbatches", "num_tensor_shards", "base_path"};
     case StrategyKind::Hybrid3DMoE:
       return {"model", "num_stages", "num_microbatches", "num_expert_shards", "base_path"};
+    case StrategyKind::HybridCP: return {"model", "num_cp_shards", "base_path"};
   }
   return {};
 }
@@ -76,6 +79,8 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  --pp-schedule gpipe|1f1b  hybrids: all forwards then all backwards (reference) or one-forward-one-backward\n"
      << "  --ep-overlap           hybrid_3d_moe: two half-microbatches, each one's all-to-all under the other's compute\n"
      << "  --dp-buckets K         hybrids: DP all-reduce buckets overlapped with the last backward\n"
+     << "                         (hybrid_cp: gradient buckets by layer, overlapped with the backward)\n"
+     << "  --cp-algo ring|ulysses hybrid_cp: KV blocks around a P2P ring, or all-to-alls over heads\n"
      << "  --in-place             in-place all-reduce (halves DP buffer memory)\n"
      << "  --zero 0|1|2           dp: ZeRO stage (1: sharded optimizer + parameter all-gather, 2: + gradient\n"
      << "                         reduce-scatter instead of all-reduce)\n"
@@ -141,6 +146,8 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
       o.ep_overlap = true;
     } else if (is("--pp-schedule")) {
       o.pp_schedule = val("pp-schedule");
+    } else if (is("--cp-algo")) {
+      o.cp_algo = val("cp-algo");
     } else if (is("--dp-buckets")) {
       o.dp_buckets = to_int(val("dp-buckets"), "dp-buckets");
     } else if (a == "--in-place") {
@@ -210,10 +217,15 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
       o.num_microbatches = to_int(pos[2], "num_microbatches");
       o.num_expert_shards = to_int(pos[3], "num_expert_shards");
       break;
+    case StrategyKind::HybridCP:
+      o.num_cp_shards = to_int(pos[1], "num_cp_shards");
+      if (o.dp_buckets == 1) o.dp_buckets = 4;  // default: 4 layer buckets
+      break;
   }
   DLNB_REQUIRE(o.warmup >= 0 && o.runs >= 0, "warmups and runs must be >= 0");
   DLNB_REQUIRE(o.num_buckets >= 1 && o.num_units >= 1 && o.sharding_factor >= 1 && o.num_stages >= 1 &&
-                   o.num_microbatches >= 1 && o.num_tensor_shards >= 1 && o.num_expert_shards >= 1,
+                   o.num_microbatches >= 1 && o.num_tensor_shards >= 1 && o.num_expert_shards >= 1 &&
+                   o.num_cp_shards >= 1,
                "parallelism degrees must be >= 1");
   DLNB_REQUIRE(o.schedule == "overlap" || o.schedule == "reference", "--schedule must be overlap or reference");
   DLNB_REQUIRE(o.pp_schedule == "gpipe" || o.pp_schedule == "1f1b", "--pp-schedule must be gpipe or 1f1b");
@@ -221,6 +233,7 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
                "--tp-granularity must be microbatch or layer");
   DLNB_REQUIRE(o.comm_lanes == "single" || o.comm_lanes == "split", "--comm-lanes must be single or split");
   DLNB_REQUIRE(o.dp_buckets >= 1, "--dp-buckets must be >= 1");
+  DLNB_REQUIRE(o.cp_algo == "ring" || o.cp_algo == "ulysses", "--cp-algo must be ring or ulysses");
   DLNB_REQUIRE(o.zero >= 0 && o.zero <= 2, "--zero must be 0, 1 or 2 (ZeRO-3 is the fsdp strategy)");
   DLNB_REQUIRE(o.zero == 0 || kind == StrategyKind::DP, "--zero applies to dp");
   DLNB_REQUIRE(o.time_scale > 0, "--time-scale must be > 0");

@@ -160,6 +160,7 @@ std::unique_ptr<Strategy> make_strategy(StrategyKind k) {
   switch (k) {
     case StrategyKind::DP: return make_dp();
     case StrategyKind::FSDP: return make_fsdp();
+    case StrategyKind::HybridCP: return make_cp();
     default: return make_pipeline(k);
   }
 }
@@ -402,7 +403,7 @@ Json run_benchmark(const Options& opt) {
   it["p95_ms"] = percentile(per_run, 0.95) * 1e3;
   it["min_ms"] = per_run.empty() ? 0.0 : *std::min_element(per_run.begin(), per_run.end()) * 1e3;
   it["timed_ms_per_iter"] = runs > 0 ? timed_region / runs * 1e3 : 0.0;
-  double floor_us = ctx.stats.avg_forward_time_us + ctx.stats.avg_backward_time_us;
+  double floor_us = strat->compute_floor_us(ctx);
   it["compute_floor_ms"] = floor_us / 1e3 * opt.time_scale;
   ext["iteration"] = it;
   g["dlnb"] = ext;

@@ -538,6 +538,10 @@ class Pipeline : public Strategy {
     timers_->resolve();
   }
 
+  double compute_floor_us(const Context&) const override {
+    return (mb_ + S_ - 1) * (fwd_mb_us_ + bwd_mb_us_);  // GPipe / 1F1B bubble included
+  }
+
   std::string section_id() const override {
     return kind_ == StrategyKind::Hybrid2D ? "dp_pp" : kind_ == StrategyKind::Hybrid3D ? "dp_pp_tp" : "dp_pp_ep";
   }

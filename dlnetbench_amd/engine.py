@@ -18,6 +18,7 @@ POSITIONAL = {
     "hybrid_2d": ["num_stages", "num_microbatches"],
     "hybrid_3d": ["num_stages", "num_microbatches", "num_tensor_shards"],
     "hybrid_3d_moe": ["num_stages", "num_microbatches", "num_expert_shards"],
+    "hybrid_cp": ["num_cp_shards"],
 }
 
 _FLAG = {
@@ -26,7 +27,7 @@ _FLAG = {
     "compute_dtype": "--compute-dtype", "schedule": "--schedule", "tp_granularity": "--tp-granularity",
     "dp_buckets": "--dp-buckets", "max_loop_iters": "--max-loop-iters", "time_scale": "--time-scale",
     "json": "--json", "store": "--store", "stats_file": "--stats-file", "comm_cus": "--comm-cus",
-    "comm_lanes": "--comm-lanes", "pp_schedule": "--pp-schedule", "zero": "--zero",
+    "comm_lanes": "--comm-lanes", "pp_schedule": "--pp-schedule", "zero": "--zero", "cp_algo": "--cp-algo",
 }
 _BOOL = {"in_place": "--in-place", "optimizer": "--optimizer", "loop": "--loop", "quiet": "--quiet",
          "silent": "--silent", "graph": "--graph", "trace": "--trace", "ep_overlap": "--ep-overlap"}

@@ -111,6 +111,9 @@ XGMI_STRATS = [  # strategy, model, positional args, extra flags, ranks
     ("hybrid_3d", "tiny_dense_8_bfloat16", ["2", "4", "2"], ["--pp-schedule", "1f1b"], 8),
     ("hybrid_3d_moe", "tiny_moe_8_bfloat16", ["1", "2", "2"], [], 2),
     ("hybrid_3d_moe", "tiny_moe_8_bfloat16", ["2", "4", "2"], ["--pp-schedule", "1f1b", "--ep-overlap"], 4),
+    ("dp", "tiny_dense_8_bfloat16", ["4"], ["--zero", "2"], 4),
+    ("hybrid_cp", "tiny_dense_8_bfloat16", ["2"], [], 4),
+    ("hybrid_cp", "tiny_dense_8_bfloat16", ["4"], ["--cp-algo", "ulysses"], 4),
 ]
 
 

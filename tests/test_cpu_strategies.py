@@ -266,3 +266,47 @@ def test_gpt2_l_dp_cpu_baseline_config1(root):
     it = d["global"]["dlnb"]["iteration"]
     assert it["median_ms"] >= it["compute_floor_ms"] * 0.98
     assert d["global"]["msg_size_avg_bytes"] == 77403008 * 2
+
+
+CP_GLOBAL = {"model_name", "num_cp_shards", "cp_algo", "local_batch_size", "world_size", "dp_size", "sequence_length",
+             "local_sequence_length", "num_layers", "attention_fraction", "fwd_rt_per_layer", "bwd_rt_per_layer",
+             "total_model_size_params", "num_dp_buckets", "dp_allreduce_size_bytes", "device", "backend"}
+CP_RANK = {"runtimes", "cp_comm_time", "cp_exposed_time", "dp_comm_time", "dp_exposed_time", "cp_id", "dp_id", "hostname"}
+
+
+@pytest.mark.parametrize("w,C,algo", [(2, 2, "ring"), (4, 2, "ring"), (4, 4, "ring"), (2, 2, "ulysses"),
+                                      (4, 4, "ulysses"), (2, 1, "ring")])
+def test_hybrid_cp(w, C, algo, data_dir):
+    """Context parallelism (extension): ring attention P2P or Ulysses all-to-all + DP gradient buckets."""
+    d = run(w, "hybrid_cp", "tiny_dense_8_bfloat16", C, data_dir, "-w", 1, "-r", 2, "--cp-algo", algo)
+    g = d["global"]
+    assert d["section"] == "dp_cp" and CP_GLOBAL <= set(g)
+    assert g["num_cp_shards"] == C and g["dp_size"] == w // C and g["cp_algo"] == algo
+    s_loc = 64 // C
+    assert g["local_sequence_length"] == s_loc and g["num_layers"] == 4 and g["num_dp_buckets"] == 4
+    if algo == "ring":
+        assert g["cp_kv_block_size_bytes"] == 2 * 8 * s_loc * 128 * 2  # K+V, B=8, d_kv=d (no GQA), bf16
+    else:
+        assert g["cp_alltoall_qkv_size_bytes"] == 8 * s_loc * 3 * 128 * 2
+        assert g["cp_alltoall_out_size_bytes"] == 8 * s_loc * 128 * 2
+    floor_ms = 6.0 / C
+    assert g["dlnb"]["iteration"]["compute_floor_ms"] == pytest.approx(floor_ms)
+    assert sorted(r["cp_id"] for r in d["ranks"]) == sorted(r % C for r in range(w))
+    for r in d["ranks"]:
+        assert CP_RANK <= set(r)
+        assert len(r["runtimes"]) == 2 and len(r["dp_exposed_time"]) == 2 and len(r["dp_comm_time"]) == 2
+        assert len(r["cp_comm_time"]) == (2 if C > 1 else 0) and len(r["cp_exposed_time"]) == (2 if C > 1 else 0)
+        for rt in r["runtimes"]:
+            assert rt * 1e3 >= floor_ms * 0.98
+        if C > 1:
+            kinds = set(r["comm"])
+            assert ("cp_ring_sendrecv" in kinds) if algo == "ring" else ("cp_alltoall_qkv" in kinds)
+            # ring: 2 * L * (C - 1) sends per iteration; ulysses: 4 * L all-to-alls
+            first = "cp_ring_sendrecv" if algo == "ring" else "cp_alltoall_qkv"
+            assert r["comm"][first]["ops"] == 2 * (4 * (C - 1) if algo == "ring" else 2 * 4)
+
+
+def test_hybrid_cp_rejects_bad_split(data_dir):
+    code, outs = launch.launch(3, [os.path.join(BIN, "hybrid_cp"), "tiny_dense_8_bfloat16", "3", data_dir, "--quiet"],
+                               timeout=60, capture=True)
+    assert code != 0 and "seq_len 64 must be divisible by num_cp_shards 3" in "".join(o or "" for o in outs)

@@ -20,6 +20,7 @@ CASES = [
     ("hybrid_2d", "tiny_dense_8_bfloat16", (1, 4)),
     ("hybrid_3d", "tiny_dense_8_bfloat16", (1, 2, 1)),
     ("hybrid_3d_moe", "tiny_moe_8_bfloat16", (1, 2, 1)),
+    ("hybrid_cp", "tiny_dense_8_bfloat16", (1,)),
 ]
 
 
@@ -76,3 +77,12 @@ def test_strategy_hip_graph_replay(strategy, model, params, data_dir):
     # per-run timer vectors keep their length under replay
     key = "runtime" if strategy == "fsdp" else "runtimes"
     assert len(r[key]) == 3
+
+
+@pytest.mark.parametrize("zero", [1, 2])
+def test_dp_zero_on_gpu(zero, data_dir):
+    doc = engine.run("dp", "tiny_dense_8_bfloat16", 4, base_path=data_dir, warmup=1, runs=2, compute="gemm",
+                     backend="rccl", quiet=True, zero=zero, graph=True)
+    g = doc["global"]
+    assert g["zero_stage"] == zero and g["dlnb"]["graph"] > 0
+    assert len(doc["ranks"][0]["param_allgather_time"]) == 2 * 4
