@@ -19,8 +19,8 @@ LDLIBS   = -L$(ROCM)/lib -lrccl -lamdhip64 -lpthread -lrt -Wl,-rpath,$(ROCM)/lib
 
 LIB_SRCS := $(wildcard csrc/src/*.cpp) $(wildcard csrc/kernels/*.hip)
 LIB_OBJS := $(patsubst csrc/%,$(BUILD)/obj/%.o,$(LIB_SRCS))
-APPS     := dp fsdp hybrid_2d hybrid_3d hybrid_3d_moe hybrid_cp dlnb
-LOOPS    := dp_loop fsdp_loop hybrid_2d_loop hybrid_3d_loop hybrid_3d_moe_loop hybrid_cp_loop
+APPS     := dp fsdp hybrid_2d hybrid_3d hybrid_3d_moe hybrid_cp hybrid_4d dlnb
+LOOPS    := dp_loop fsdp_loop hybrid_2d_loop hybrid_3d_loop hybrid_3d_moe_loop hybrid_cp_loop hybrid_4d_loop
 LIB      := $(BUILD)/libdlnb.so
 PYLIB    := dlnetbench_amd/_lib/libdlnb.so
 

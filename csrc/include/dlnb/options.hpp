@@ -8,6 +8,8 @@
 //   hybrid_3d     <model> <num_stages> <num_microbatches> <num_tensor_shards> <base_path>
 //   hybrid_3d_moe <model> <num_stages> <num_microbatches> <num_expert_shards> <base_path>
 //   hybrid_cp     <model> <num_cp_shards> <base_path>   (extension: DP x context parallel)
+//   hybrid_4d     <model> <num_stages> <num_microbatches> <num_tensor_shards> <num_expert_shards> <base_path>
+//                 (extension: DP x PP x TP x EP)
 //   flags: -w warmups (3)  -r runs (5; hybrid_3d 3)  -d devices ("")
 //          -m min_exectime seconds (0)  -h
 // Long options are dlnb extensions (run-time backend, compute model,
@@ -19,7 +21,7 @@
 
 namespace dlnb {
 
-enum class StrategyKind { DP, FSDP, Hybrid2D, Hybrid3D, Hybrid3DMoE, HybridCP };
+enum class StrategyKind { DP, FSDP, Hybrid2D, Hybrid3D, Hybrid3DMoE, HybridCP, Hybrid4D };
 
 StrategyKind parse_strategy(const std::string& s);
 const char* strategy_name(StrategyKind k);

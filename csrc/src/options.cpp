@@ -14,7 +14,8 @@ StrategyKind parse_strategy(const std::string& s) {
   if (s == "hybrid_3d" || s == "dp_pp_tp") return StrategyKind::Hybrid3D;
   if (s == "hybrid_3d_moe" || s == "dp_pp_ep") return StrategyKind::Hybrid3DMoE;
   if (s == "hybrid_cp" || s == "dp_cp") return StrategyKind::HybridCP;
-  DLNB_THROW("unknown strategy '" << s << "' (dp, fsdp, hybrid_2d, hybrid_3d, hybrid_3d_moe, hybrid_cp)");
+  if (s == "hybrid_4d" || s == "dp_pp_tp_ep") return StrategyKind::Hybrid4D;
+  DLNB_THROW("unknown strategy '" << s << "' (dp, fsdp, hybrid_2d, hybrid_3d, hybrid_3d_moe, hybrid_cp, hybrid_4d)");
 }
 
 const char* strategy_name(StrategyKind k) {
@@ -25,6 +26,7 @@ const char* strategy_name(StrategyKind k) {
     case StrategyKind::Hybrid3D: return "hybrid_3d";
     case StrategyKind::Hybrid3DMoE: return "hybrid_3d_moe";
     case StrategyKind::HybridCP: return "hybrid_cp";
+    case StrategyKind::Hybrid4D: return "hybrid_4d";
   }
   return "?";
 }
@@ -40,6 +42,8 @@ std::vector<std::string> positional_names(StrategyKind k) {
     case StrategyKind::Hybrid3DMoE:
       return {"model", "num_stages", "num_microbatches", "num_expert_shards", "base_path"};
     case StrategyKind::HybridCP: return {"model", "num_cp_shards", "base_path"};
+    case StrategyKind::Hybrid4D:
+      return {"model", "num_stages", "num_microbatches", "num_tensor_shards", "num_expert_shards", "base_path"};
   }
   return {};
 }
@@ -75,7 +79,7 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  --wire-dtype T         bf16 | fp16 | fp32 | fp8 (collective element type)\n"
      << "  --compute-dtype T      auto | bf16 | fp8 (GEMM operand type for gemm/flops)\n"
      << "  --schedule S           overlap (stream-ordered) | reference (blocking like DLNetBench)\n"
-     << "  --tp-granularity G     microbatch | layer (hybrid_3d)\n"
+     << "  --tp-granularity G     microbatch | layer (hybrid_3d, hybrid_4d)\n"
      << "  --pp-schedule gpipe|1f1b  hybrids: all forwards then all backwards (reference) or one-forward-one-backward\n"
      << "  --ep-overlap           hybrid_3d_moe: two half-microbatches, each one's all-to-all under the other's compute\n"
      << "  --dp-buckets K         hybrids: DP all-reduce buckets overlapped with the last backward\n"
@@ -220,6 +224,12 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
     case StrategyKind::HybridCP:
       o.num_cp_shards = to_int(pos[1], "num_cp_shards");
       if (o.dp_buckets == 1) o.dp_buckets = 4;  // default: 4 layer buckets
+      break;
+    case StrategyKind::Hybrid4D:
+      o.num_stages = to_int(pos[1], "num_stages");
+      o.num_microbatches = to_int(pos[2], "num_microbatches");
+      o.num_tensor_shards = to_int(pos[3], "num_tensor_shards");
+      o.num_expert_shards = to_int(pos[4], "num_expert_shards");
       break;
   }
   DLNB_REQUIRE(o.warmup >= 0 && o.runs >= 0, "warmups and runs must be >= 0");

@@ -1,5 +1,6 @@
 // Pipeline-parallel hybrids: DP x PP (hybrid_2d), DP x PP x TP (hybrid_3d),
-// DP x PP x EP (hybrid_3d_moe).
+// DP x PP x EP (hybrid_3d_moe), and the 4-D DP x PP x TP x EP (hybrid_4d,
+// an extension: the reference only lists a hybrid_4d binary in .gitignore:6).
 //
 // Reference: cpp/hybrid_parallel/hybrid_2d.cpp:90-169, hybrid_3d.cpp:94-192,
 // hybrid_3d_moe.cpp:104-211. GPipe schedule: every microbatch forward
@@ -70,32 +71,39 @@ class Pipeline : public Strategy {
     const int W = ctx.world();
     S_ = o.num_stages;
     mb_ = o.num_microbatches;
-    inner_ = kind_ == StrategyKind::Hybrid3D ? o.num_tensor_shards
-             : kind_ == StrategyKind::Hybrid3DMoE ? o.num_expert_shards
-                                                  : 1;
+    has_tp_ = kind_ == StrategyKind::Hybrid3D || kind_ == StrategyKind::Hybrid4D;
+    has_ep_ = kind_ == StrategyKind::Hybrid3DMoE || kind_ == StrategyKind::Hybrid4D;
+    T_ = has_tp_ ? o.num_tensor_shards : 1;
+    E_ = has_ep_ ? o.num_expert_shards : 1;
+    inner_ = T_ * E_;  // TP fastest, then EP (hybrid_4d), then stage, then DP replica
     reference_ = o.schedule == "reference";
     one_f_one_b_ = o.pp_schedule == "1f1b";
-    ep_overlap_ = o.ep_overlap && kind_ == StrategyKind::Hybrid3DMoE && !reference_;
+    ep_overlap_ = o.ep_overlap && has_ep_ && !reference_;
+    DLNB_REQUIRE(!(ep_overlap_ && has_tp_), "--ep-overlap is not supported with tensor parallelism (hybrid_4d)");
     DLNB_REQUIRE(!(one_f_one_b_ && reference_), "--pp-schedule 1f1b needs --schedule overlap");
     DLNB_REQUIRE(ctx.have_arch, "hybrid strategies need models/<model>.json (layer count)");
     L_ = static_cast<int>(ctx.arch.num_layers);
     DLNB_REQUIRE(L_ > 0, "model has no layers: " << ctx.arch.path);
     DLNB_REQUIRE(L_ % S_ == 0, "num_layers " << L_ << " must be divisible by num_stages " << S_);
     DLNB_REQUIRE(st.batch_size % mb_ == 0, "batch size " << st.batch_size << " must be divisible by num_microbatches " << mb_);
-    DLNB_REQUIRE(W % (S_ * inner_) == 0, "world size " << W << " must be divisible by stages*" << (kind_ == StrategyKind::Hybrid3DMoE ? "expert" : "tensor") << " shards = " << S_ * inner_);
-    if (kind_ == StrategyKind::Hybrid3DMoE)
-      DLNB_REQUIRE(st.experts % inner_ == 0, "experts " << st.experts << " must be divisible by num_expert_shards " << inner_);
+    DLNB_REQUIRE(W % (S_ * inner_) == 0, "world size " << W << " must be divisible by stages*"
+                                             << (has_tp_ && has_ep_ ? "tensor*expert" : has_ep_ ? "expert" : "tensor")
+                                             << " shards = " << S_ * inner_);
+    if (has_ep_)
+      DLNB_REQUIRE(st.experts % E_ == 0, "experts " << st.experts << " must be divisible by num_expert_shards " << E_);
     dp_size_ = W / (S_ * inner_);
     layers_per_stage_ = L_ / S_;
 
     GridCoords c = grid_coords(ctx.rank(), inner_, S_);
     stage_ = c.stage_id;
     inner_id_ = c.inner_id;
+    tp_id_ = inner_id_ % T_;
+    ep_id_ = inner_id_ / T_;
     dp_id_ = c.dp_id;
 
     spmb_ = st.batch_size / mb_;
     pipe_ = st.seq_len * st.embedded_dim * spmb_;
-    double tshard = kind_ == StrategyKind::Hybrid3D ? inner_ : 1;
+    double tshard = T_;
     fwd_mb_us_ = st.avg_forward_time_us / S_ / (mb_ * tshard);
     bwd_mb_us_ = st.avg_backward_time_us / S_ / (mb_ * tshard);
     fwd_mb_flops_ = st.forward_flops / S_ / (mb_ * tshard);
@@ -104,15 +112,19 @@ class Pipeline : public Strategy {
     if (kind_ == StrategyKind::Hybrid2D) {
       dp_ar_ = P / S_;
     } else if (kind_ == StrategyKind::Hybrid3D) {
-      dp_ar_ = P / (S_ * inner_);
-      tp_ar_ = pipe_ / inner_;
+      dp_ar_ = P / (S_ * T_);
+      tp_ar_ = pipe_ / T_;
     } else {
+      // MoE (hybrid_3d_moe.cpp:340-363); hybrid_4d also shards the
+      // non-expert weights and each expert over TP, and the TP ranks of an
+      // EP rank dispatch disjoint 1/T of its tokens (sequence-parallel).
       const uint64_t NE = st.non_expert_size;
-      ne_ = NE / S_;
-      uint64_t expert = ((P - NE) / S_) / inner_;
+      ne_ = NE / S_ / T_;
+      uint64_t expert = ((P - NE) / S_) / E_ / T_;
       dp_ar_ = ne_ + expert;
       const int top_k = 2;  // hybrid_3d_moe.cpp:357
-      a2a_ = (spmb_ * st.seq_len * top_k * st.embedded_dim) / inner_;
+      a2a_ = (spmb_ * st.seq_len * top_k * st.embedded_dim) / E_ / T_;
+      if (has_tp_) tp_ar_ = pipe_ / T_;
     }
 
     Device& dev = *ctx.dev;
@@ -137,18 +149,24 @@ class Pipeline : public Strategy {
     }
     if (prev_) prev_stream_ = dev.create_stream(true);
     if (next_) next_stream_ = dev.create_stream(true);
-    if (inner_ > 1) {
-      std::string nm = std::string(kind_ == StrategyKind::Hybrid3D ? "tp/" : "ep/") + std::to_string(dp_id_) + "/" +
-                       std::to_string(stage_);
-      size_t cap = kind_ == StrategyKind::Hybrid3D ? tp_ar_ * es_ : std::max<uint64_t>(a2a_ * inner_, ne_) * es_;
-      inner_comm_ = ctx.comms->create(nm, inner_group(rank, inner_, S_), cap, false);
-    } else if (kind_ == StrategyKind::Hybrid3DMoE) {
-      inner_comm_ = ctx.comms->create("ep/" + std::to_string(dp_id_) + "/" + std::to_string(stage_),
-                                      inner_group(rank, inner_, S_), std::max<uint64_t>(a2a_, ne_) * es_, false);
-    }
-    if (kind_ == StrategyKind::Hybrid3D && inner_ == 1) {
-      inner_comm_ = ctx.comms->create("tp/" + std::to_string(dp_id_) + "/" + std::to_string(stage_),
-                                      inner_group(rank, inner_, S_), tp_ar_ * es_, false);
+    {
+      // TP group: same (dp, stage, ep); EP group: same (dp, stage, tp). With
+      // one of the two degrees = 1 these are the reference's inner groups
+      // (inner_group()); 1-rank groups are kept (the reference issues its
+      // TP all-reduces at T = 1 too).
+      const int base = dp_id_ * inner_ * S_ + stage_ * inner_;
+      const std::string where = std::to_string(dp_id_) + "/" + std::to_string(stage_);
+      if (has_tp_) {
+        std::vector<int> m;
+        for (int t = 0; t < T_; ++t) m.push_back(base + ep_id_ * T_ + t);
+        tp_comm_ = ctx.comms->create("tp/" + where + "/" + std::to_string(ep_id_), m, tp_ar_ * es_, false);
+      }
+      if (has_ep_) {
+        std::vector<int> m;
+        for (int e = 0; e < E_; ++e) m.push_back(base + e * T_ + tp_id_);
+        ep_comm_ = ctx.comms->create("ep/" + where + "/" + std::to_string(tp_id_), m,
+                                     std::max<uint64_t>(a2a_ * E_, ne_) * es_, false);
+      }
     }
     {
       std::string nm = "dp/" + std::to_string(stage_) + "/" + std::to_string(inner_id_);
@@ -173,15 +191,15 @@ class Pipeline : public Strategy {
     grad_ = dev.alloc(dp_ar_ * es_);
     dev.fill_random(grad_.data(), dp_ar_, ctx.wire, 4200, *compute_);
     if (!o.in_place) sum_grad_ = dev.alloc(dp_ar_ * es_);
-    if (kind_ == StrategyKind::Hybrid3D) {
+    if (has_tp_) {
       tp_buf_ = dev.alloc(tp_ar_ * es_);
       tp_res_ = dev.alloc(tp_ar_ * es_);
       dev.fill_random(tp_buf_.data(), tp_ar_, ctx.wire, 4300, *compute_);
     }
-    if (kind_ == StrategyKind::Hybrid3DMoE) {
-      ep_send_ = dev.alloc(a2a_ * inner_ * es_);
-      ep_recv_ = dev.alloc(a2a_ * inner_ * es_);
-      dev.fill_random(ep_send_.data(), a2a_ * inner_, ctx.wire, 4400, *compute_);
+    if (has_ep_) {
+      ep_send_ = dev.alloc(a2a_ * E_ * es_);
+      ep_recv_ = dev.alloc(a2a_ * E_ * es_);
+      dev.fill_random(ep_send_.data(), a2a_ * E_, ctx.wire, 4400, *compute_);
       if (ep_overlap_) {
         // The half-microbatch all-to-alls share the DP lane instead of a
         // fifth stream: a middle stage already has compute + dp + prev + next,
@@ -221,48 +239,37 @@ class Pipeline : public Strategy {
     timers_.reset(new TimerSet(dev));
     for (const char* k : {"pp_comm_time", "dp_comm_time", "pp_send_time", "pp_recv_time", "dp_exposed_time"})
       timers_->ensure(k);
-    if (kind_ == StrategyKind::Hybrid3D) timers_->ensure("tp_comm_time");
-    if (kind_ == StrategyKind::Hybrid3DMoE) {
+    if (has_tp_) timers_->ensure("tp_comm_time");
+    if (has_ep_) {
       timers_->ensure("ep_comm_time");
       timers_->ensure("dp_ep_comm_time");
     }
     if (prev_ || next_) stats_.push_back({"sendrecv", CollKind::SendRecv, 2, static_cast<double>(pipe_ * es_), "pp_send_time"});
     stats_.push_back({"dp_allreduce", CollKind::AllReduce, dp_size_, static_cast<double>(dp_ar_ / o.dp_buckets * es_), "dp_comm_time"});
-    if (kind_ == StrategyKind::Hybrid3D)
-      stats_.push_back({"tp_allreduce", CollKind::AllReduce, inner_, static_cast<double>(tp_ar_ * es_), "tp_comm_time"});
-    if (kind_ == StrategyKind::Hybrid3DMoE)
-      stats_.push_back({"ep_alltoall", CollKind::AllToAll, inner_,
-                        static_cast<double>((ep_overlap_ ? a2a_ / 2 : a2a_) * inner_ * es_), "ep_comm_time"});
+    if (has_tp_)
+      stats_.push_back({"tp_allreduce", CollKind::AllReduce, T_, static_cast<double>(tp_ar_ * es_), "tp_comm_time"});
+    if (has_ep_)
+      stats_.push_back({"ep_alltoall", CollKind::AllToAll, E_,
+                        static_cast<double>((ep_overlap_ ? a2a_ / 2 : a2a_) * E_ * es_), "ep_comm_time"});
   }
 
   // Compute of one microbatch with the inner-group collectives interleaved.
   void micro_compute(double us, double flops) {
     Context& ctx = *ctx_;
     ComputeEngine& ce = *ctx.compute;
-    if (kind_ == StrategyKind::Hybrid3D) {
-      const bool layer = ctx.opt.tp_granularity == "layer";
-      const int n_ar = layer ? 4 * layers_per_stage_ / 2 : 2;  // layer: 2 per layer
-      if (layer) {
-        const int slices = n_ar;
-        for (int i = 0; i < slices; ++i) {
-          ce.run(*compute_, us / slices, flops / slices);
-          tp_allreduce();
-        }
-      } else {
-        ce.run(*compute_, us, flops);
-        tp_allreduce();
-        tp_allreduce();
-      }
-    } else if (kind_ == StrategyKind::Hybrid3DMoE) {
+    const bool tp_layer = has_tp_ && ctx.opt.tp_granularity == "layer";
+    if (has_ep_) {
       const int n = 2 * layers_per_stage_;
       if (reference_) {
         ce.run(*compute_, us, flops);
         for (int i = 0; i < n; ++i) ep_alltoall();
+        if (has_tp_)
+          for (int i = 0; i < (tp_layer ? n : 2); ++i) tp_allreduce();
       } else if (ep_overlap_) {
         // Two half-microbatches in flight: the all-to-all of one half runs on
-        // the EP stream under the compute of the other (the dual-batch
+        // the EP lane under the compute of the other (the dual-batch
         // overlap of MoE training); a half's next chunk waits for its own
-        // previous all-to-all. One EP stream = one ordered lane per rank.
+        // previous all-to-all. One EP lane = one ordered lane per rank.
         for (int i = 0; i < n; ++i) {
           for (int hh = 0; hh < 2; ++hh) {
             if (i > 0) compute_->wait(*a2a_done_[hh]);
@@ -276,10 +283,29 @@ class Pipeline : public Strategy {
         compute_->wait(*a2a_done_[0]);
         compute_->wait(*a2a_done_[1]);
       } else {
+        // hybrid_4d: the TP all-reduce of a slice (attention / expert output)
+        // precedes its all-to-all (dispatch / combine).
         for (int i = 0; i < n; ++i) {
           ce.run(*compute_, us / n, flops / n);
+          if (tp_layer) tp_allreduce();
           ep_alltoall();
         }
+        if (has_tp_ && !tp_layer) {
+          tp_allreduce();
+          tp_allreduce();
+        }
+      }
+    } else if (has_tp_) {
+      if (tp_layer) {
+        const int slices = 4 * layers_per_stage_ / 2;  // 2 per layer
+        for (int i = 0; i < slices; ++i) {
+          ce.run(*compute_, us / slices, flops / slices);
+          tp_allreduce();
+        }
+      } else {
+        ce.run(*compute_, us, flops);
+        tp_allreduce();
+        tp_allreduce();
       }
     } else {
       ce.run(*compute_, us, flops);
@@ -288,13 +314,13 @@ class Pipeline : public Strategy {
 
   void tp_allreduce() {
     int t = timers_->begin(*compute_);
-    inner_comm_->all_reduce(tp_buf_.data(), tp_res_.data(), tp_ar_, ctx_->wire, *compute_);
+    tp_comm_->all_reduce(tp_buf_.data(), tp_res_.data(), tp_ar_, ctx_->wire, *compute_);
     timers_->end(t, *compute_, "tp_comm_time");
   }
 
   void ep_alltoall() {
     int t = timers_->begin(*compute_);
-    inner_comm_->all_to_all(ep_send_.data(), ep_recv_.data(), a2a_, ctx_->wire, *compute_);
+    ep_comm_->all_to_all(ep_send_.data(), ep_recv_.data(), a2a_, ctx_->wire, *compute_);
     timers_->end(t, *compute_, "ep_comm_time");
   }
 
@@ -302,9 +328,9 @@ class Pipeline : public Strategy {
   // the send / receive buffers, so the two halves never share memory.
   void ep_alltoall_half(int hh) {
     const uint64_t c0 = a2a_ / 2, c = hh == 0 ? c0 : a2a_ - c0;
-    const size_t off = static_cast<size_t>(hh) * c0 * inner_ * es_;
+    const size_t off = static_cast<size_t>(hh) * c0 * E_ * es_;
     int t = timers_->begin(*ep_stream_);
-    inner_comm_->all_to_all(ep_send_.at(off), ep_recv_.at(off), c, ctx_->wire, *ep_stream_);
+    ep_comm_->all_to_all(ep_send_.at(off), ep_recv_.at(off), c, ctx_->wire, *ep_stream_);
     timers_->end(t, *ep_stream_, "ep_comm_time");
   }
 
@@ -383,11 +409,11 @@ class Pipeline : public Strategy {
     Context& ctx = *ctx_;
     const DType t = ctx.wire;
     const int nbk = ctx.opt.dp_buckets;
-    if (kind_ == StrategyKind::Hybrid3DMoE) {
+    if (has_ep_) {
       // Non-expert gradients are replicated across the EP group.
       int tk = timers_->begin(*compute_);
       void* out = ctx.opt.in_place ? grad_.data() : sum_grad_.data();
-      inner_comm_->all_reduce(grad_.data(), out, ne_, t, *compute_);
+      ep_comm_->all_reduce(grad_.data(), out, ne_, t, *compute_);
       timers_->end(tk, *compute_, "dp_ep_comm_time");
     }
     if (nbk == 1 || reference_) {
@@ -533,7 +559,8 @@ class Pipeline : public Strategy {
       ss.push_back(next_stream_.get());
       cs.push_back(next_.get());
     }
-    if (inner_comm_) cs.push_back(inner_comm_.get());
+    if (tp_comm_) cs.push_back(tp_comm_.get());
+    if (ep_comm_) cs.push_back(ep_comm_.get());
     sync_streams(ss, cs, *ctx_->dev);
     timers_->resolve();
   }
@@ -543,12 +570,16 @@ class Pipeline : public Strategy {
   }
 
   std::string section_id() const override {
-    return kind_ == StrategyKind::Hybrid2D ? "dp_pp" : kind_ == StrategyKind::Hybrid3D ? "dp_pp_tp" : "dp_pp_ep";
+    return kind_ == StrategyKind::Hybrid2D      ? "dp_pp"
+           : kind_ == StrategyKind::Hybrid3D    ? "dp_pp_tp"
+           : kind_ == StrategyKind::Hybrid3DMoE ? "dp_pp_ep"
+                                                : "dp_pp_tp_ep";
   }
   std::string section_title() const override {
-    return kind_ == StrategyKind::Hybrid2D   ? "Data + Pipeline Parallelism"
-           : kind_ == StrategyKind::Hybrid3D ? "Data + Pipeline + Tensor Parallelism"
-                                             : "Data + Pipeline + Expert Parallelism";
+    return kind_ == StrategyKind::Hybrid2D      ? "Data + Pipeline Parallelism"
+           : kind_ == StrategyKind::Hybrid3D    ? "Data + Pipeline + Tensor Parallelism"
+           : kind_ == StrategyKind::Hybrid3DMoE ? "Data + Pipeline + Expert Parallelism"
+                                                : "Data + Pipeline + Tensor + Expert Parallelism";
   }
 
   Json global_json() const override {
@@ -557,9 +588,9 @@ class Pipeline : public Strategy {
     g["model_name"] = ctx.opt.model;
     g["num_stages"] = S_;
     g["num_microbatches"] = mb_;
-    if (kind_ == StrategyKind::Hybrid3D) g["num_tensor_shards"] = inner_;
-    if (kind_ == StrategyKind::Hybrid3DMoE) {
-      g["num_expert_shards"] = inner_;
+    if (has_tp_) g["num_tensor_shards"] = T_;
+    if (has_ep_) {
+      g["num_expert_shards"] = E_;
       g["num_experts"] = ctx.stats.experts;
       g["sequence_length"] = ctx.stats.seq_len;
       g["embedded_dim"] = ctx.stats.embedded_dim;
@@ -577,14 +608,15 @@ class Pipeline : public Strategy {
     g["bwd_rt_per_microbatch"] = bwd_mb_us_;
     g["total_model_size_params"] = ctx.stats.model_size;
     g["pipe_msg_size_bytes"] = pipe_ * es_;
-    if (kind_ == StrategyKind::Hybrid3D) g["tp_allreduce_size_bytes"] = tp_ar_ * es_;
-    if (kind_ == StrategyKind::Hybrid3DMoE) {
+    if (has_tp_) g["tp_allreduce_size_bytes"] = tp_ar_ * es_;
+    if (has_ep_) {
       g["ep_alltoall_size_bytes"] = a2a_ * es_;
       g["ep_allreduce_size_bytes"] = ne_ * es_;
     }
     g["dp_allreduce_size_bytes"] = dp_ar_ * es_;
     g["pp_schedule"] = ctx.opt.pp_schedule;
-    if (kind_ == StrategyKind::Hybrid3DMoE) g["ep_overlap"] = ep_overlap_;
+    if (has_ep_) g["ep_overlap"] = ep_overlap_;
+    if (has_tp_) g["tp_granularity"] = ctx.opt.tp_granularity;
     g["device"] = ctx.dev->kind() == DeviceKind::CPU ? "CPU" : "GPU";
     g["backend"] = dp_comm_->backend_name();
     return g;
@@ -595,8 +627,8 @@ class Pipeline : public Strategy {
     r["runtimes"] = timers_->values_json("runtimes");
     r["pp_comm_time"] = timers_->values_json("pp_comm_time");
     r["dp_comm_time"] = timers_->values_json("dp_comm_time");
-    if (kind_ == StrategyKind::Hybrid3D) r["tp_comm_time"] = timers_->values_json("tp_comm_time");
-    if (kind_ == StrategyKind::Hybrid3DMoE) {
+    if (has_tp_) r["tp_comm_time"] = timers_->values_json("tp_comm_time");
+    if (has_ep_) {
       r["ep_comm_time"] = timers_->values_json("ep_comm_time");
       r["dp_ep_comm_time"] = timers_->values_json("dp_ep_comm_time");
     }
@@ -604,8 +636,8 @@ class Pipeline : public Strategy {
     r["pp_recv_time"] = timers_->values_json("pp_recv_time");
     r["dp_exposed_time"] = timers_->values_json("dp_exposed_time");
     r["stage_id"] = stage_;
-    if (kind_ == StrategyKind::Hybrid3D) r["tp_id"] = inner_id_;
-    if (kind_ == StrategyKind::Hybrid3DMoE) r["ep_id"] = inner_id_;
+    if (has_tp_) r["tp_id"] = tp_id_;
+    if (has_ep_) r["ep_id"] = ep_id_;
     if (kind_ != StrategyKind::Hybrid2D) r["dp_id"] = dp_id_;
     return r;
   }
@@ -616,7 +648,8 @@ class Pipeline : public Strategy {
   StrategyKind kind_;
   Context* ctx_ = nullptr;
   int S_ = 1, mb_ = 1, inner_ = 1, L_ = 0, layers_per_stage_ = 0, dp_size_ = 1;
-  int stage_ = 0, inner_id_ = 0, dp_id_ = 0;
+  int stage_ = 0, inner_id_ = 0, dp_id_ = 0, tp_id_ = 0, ep_id_ = 0, T_ = 1, E_ = 1;
+  bool has_tp_ = false, has_ep_ = false;
   bool reference_ = false;
   bool one_f_one_b_ = false;
   bool ep_overlap_ = false;
@@ -625,7 +658,7 @@ class Pipeline : public Strategy {
   uint64_t spmb_ = 0, pipe_ = 0, dp_ar_ = 0, tp_ar_ = 0, ne_ = 0, a2a_ = 0;
   size_t es_ = 2;
   double fwd_mb_us_ = 0, bwd_mb_us_ = 0, fwd_mb_flops_ = 0, bwd_mb_flops_ = 0;
-  std::unique_ptr<Communicator> prev_, next_, inner_comm_, dp_comm_;
+  std::unique_ptr<Communicator> prev_, next_, tp_comm_, ep_comm_, dp_comm_;
   int prev_peer_ = 0, next_peer_ = 1;
   std::unique_ptr<Stream> compute_, prev_stream_, next_stream_, dp_stream_;
   Buffer act_in_[2], act_out_[2], grad_in_[2], grad_out_[2];

@@ -1,6 +1,6 @@
 """One command line for the whole toolkit: ``python -m dlnetbench_amd <command> ...``
 
-    run [-n N] [--timeout S] <dp|fsdp|hybrid_2d|hybrid_3d|hybrid_3d_moe|hybrid_cp> <args...>
+    run [-n N] [--timeout S] <dp|fsdp|hybrid_2d|hybrid_3d|hybrid_3d_moe|hybrid_cp|hybrid_4d> <args...>
                       launch N ranks of a strategy binary (build/bin/<strategy>)
     commtest [-n N] <args...>
                       exact check / bandwidth sweep of a comm backend (dlnb commtest)
@@ -20,7 +20,7 @@ import sys
 from typing import List, Optional
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-STRATEGIES = ("dp", "fsdp", "hybrid_2d", "hybrid_3d", "hybrid_3d_moe", "hybrid_cp")
+STRATEGIES = ("dp", "fsdp", "hybrid_2d", "hybrid_3d", "hybrid_3d_moe", "hybrid_cp", "hybrid_4d")
 
 TOOLS = {
     "launch": "dlnetbench_amd.utils.launch",

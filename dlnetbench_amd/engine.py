@@ -19,6 +19,7 @@ POSITIONAL = {
     "hybrid_3d": ["num_stages", "num_microbatches", "num_tensor_shards"],
     "hybrid_3d_moe": ["num_stages", "num_microbatches", "num_expert_shards"],
     "hybrid_cp": ["num_cp_shards"],
+    "hybrid_4d": ["num_stages", "num_microbatches", "num_tensor_shards", "num_expert_shards"],
 }
 
 _FLAG = {

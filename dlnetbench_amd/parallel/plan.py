@@ -130,7 +130,10 @@ def plan_fsdp(st: ModelStats, world: int, U: int, F: int, wire: str = "bf16") ->
 
 
 def plan_hybrid(st: ModelStats, world: int, kind: str, S: int, mb: int, inner: int = 1, layers: int = 0,
-                wire: str = "bf16", tp_granularity: str = "microbatch") -> Plan:
+                wire: str = "bf16", tp_granularity: str = "microbatch", experts: int = 1) -> Plan:
+    """hybrid_4d: inner = T (tensor shards), experts = E (expert shards); TP fastest, then EP."""
+    if kind == "hybrid_4d":
+        return _plan_4d(st, world, S, mb, inner, experts, layers, wire, tp_granularity)
     es = WIRE_BYTES[wire]
     if layers and layers % S:
         raise ValueError("num_layers must be divisible by num_stages")
@@ -167,6 +170,62 @@ def plan_hybrid(st: ModelStats, world: int, kind: str, S: int, mb: int, inner: i
     return p
 
 
+def _plan_4d(st: ModelStats, world: int, S: int, mb: int, T: int, E: int, layers: int, wire: str,
+             tp_granularity: str) -> Plan:
+    """DP x PP x TP x EP (csrc/src/strategy_pipeline.cpp, Hybrid4D)."""
+    es = WIRE_BYTES[wire]
+    if world % (S * T * E):
+        raise ValueError("world must be divisible by stages*T*E")
+    if st.batch % mb or (layers and layers % S):
+        raise ValueError("batch % mb and layers % S must be 0")
+    spmb = st.batch // mb
+    pipe = st.seq_len * st.hidden * spmb
+    lps = layers // S if layers else 1
+    p = Plan("hybrid_4d", world, {"num_stages": S, "num_microbatches": mb, "num_tensor_shards": T,
+                                  "num_expert_shards": E, "dp_size": world // (S * T * E)},
+             {"fwd_per_microbatch": st.fwd_us / S / (mb * T), "bwd_per_microbatch": st.bwd_us / S / (mb * T)})
+    if S > 1:
+        p.messages.append(Message("pipe_sendrecv", "sendrecv", 2, pipe, 2 * mb, pipe * es))
+    tp = pipe // T
+    n_tp = (2 * lps if tp_granularity == "layer" else 2) * 2 * mb
+    p.messages.append(Message("tp_allreduce", "allreduce", T, tp, n_tp, tp * es))
+    a2a = (spmb * st.seq_len * 2 * st.hidden) // E // T
+    p.messages.append(Message("ep_alltoall", "alltoall", E, a2a, 2 * lps * 2 * mb, a2a * E * es))
+    ne = st.non_expert_size // S // T
+    p.messages.append(Message("ep_nonexpert_allreduce", "allreduce", E, ne, 1, ne * es))
+    dp_ar = ne + ((st.model_size - st.non_expert_size) // S) // E // T
+    p.messages.append(Message("dp_allreduce", "allreduce", world // (S * T * E), dp_ar, 1, dp_ar * es))
+    p.memory_bytes = (8 * pipe + 2 * dp_ar + 2 * a2a * E + 2 * tp) * es
+    return p
+
+
+def plan_cp(st: ModelStats, world: int, C: int, layers: int, heads: int, kv_heads: int, algo: str = "ring",
+            buckets: int = 4, wire: str = "bf16") -> Plan:
+    """DP x CP (csrc/src/strategy_cp.cpp): ring KV blocks or Ulysses all-to-alls per layer."""
+    es = WIRE_BYTES[wire]
+    if world % C or st.seq_len % C:
+        raise ValueError("world and seq_len must be divisible by num_cp_shards")
+    s_loc = st.seq_len // C
+    dkv = st.hidden * kv_heads // heads
+    p = Plan("hybrid_cp", world, {"num_cp_shards": C, "dp_size": world // C, "num_dp_buckets": min(buckets, layers)},
+             {"fwd_per_layer": st.fwd_us / C / layers, "bwd_per_layer": st.bwd_us / C / layers})
+    if C > 1:
+        if algo == "ring":
+            kv = 2 * st.batch * s_loc * dkv
+            p.messages.append(Message("cp_ring_kv", "sendrecv", 2, kv, layers * (C - 1), kv * es))
+            p.messages.append(Message("cp_ring_kv_dkv", "sendrecv", 2, 2 * kv, layers * (C - 1), 2 * kv * es))
+        else:
+            qkv = -(-st.batch * s_loc * (st.hidden + 2 * dkv) // C)
+            out = -(-st.batch * s_loc * st.hidden // C)
+            p.messages.append(Message("cp_alltoall_qkv", "alltoall", C, qkv, 2 * layers, qkv * C * es))
+            p.messages.append(Message("cp_alltoall_out", "alltoall", C, out, 2 * layers, out * C * es))
+    nb = min(buckets, layers)
+    b0 = _split(st.model_size, nb)[0]
+    p.messages.append(Message("dp_allreduce", "allreduce", world, b0, nb, b0 * es))
+    p.memory_bytes = (st.model_size + 4 * st.batch * s_loc * max(dkv, st.hidden)) * es
+    return p
+
+
 def busbw_factor(op: str, n: int) -> float:
     """nccl-tests bus-bandwidth factor (BASELINE.md 'Metric definitions')."""
     if n <= 1:
@@ -180,13 +239,15 @@ def busbw_factor(op: str, n: int) -> float:
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description="Print the messages and memory of a benchmark run")
-    ap.add_argument("strategy", choices=["dp", "fsdp", "hybrid_2d", "hybrid_3d", "hybrid_3d_moe"])
+    ap.add_argument("strategy", choices=["dp", "fsdp", "hybrid_2d", "hybrid_3d", "hybrid_3d_moe", "hybrid_4d",
+                                         "hybrid_cp"])
     ap.add_argument("model")
     ap.add_argument("params", nargs="+", type=int)
     ap.add_argument("--world", type=int, required=True)
     ap.add_argument("--base", default=".")
     ap.add_argument("--wire", default="bf16")
     ap.add_argument("--zero", type=int, default=0, help="dp: ZeRO stage 0|1|2")
+    ap.add_argument("--cp-algo", default="ring", choices=["ring", "ulysses"])
     a = ap.parse_args(argv)
     st = load_stats(os.path.join(a.base, "model_stats", a.model + ".txt"))
     if a.strategy == "dp":
@@ -198,8 +259,15 @@ def main(argv=None) -> int:
         with open(os.path.join(a.base, "models", base + ".json")) as f:
             arch = json.load(f)
         L = arch.get("num_encoder_blocks", 0) + arch.get("num_decoder_blocks", 0)
-        inner = a.params[2] if len(a.params) > 2 else 1
-        pl = plan_hybrid(st, a.world, a.strategy, a.params[0], a.params[1], inner, L, wire=a.wire)
+        if a.strategy == "hybrid_cp":
+            heads = arch.get("num_heads", 1)
+            kv = arch.get("dlnb", {}).get("num_kv_heads", heads)
+            pl = plan_cp(st, a.world, a.params[0], L, heads, kv, a.cp_algo, wire=a.wire)
+        else:
+            inner = a.params[2] if len(a.params) > 2 else 1
+            experts = a.params[3] if len(a.params) > 3 else 1
+            pl = plan_hybrid(st, a.world, a.strategy, a.params[0], a.params[1], inner, L, wire=a.wire,
+                             experts=experts)
     print(json.dumps(pl.to_json(), indent=1))
     return 0
 

@@ -310,3 +310,33 @@ def test_hybrid_cp_rejects_bad_split(data_dir):
     code, outs = launch.launch(3, [os.path.join(BIN, "hybrid_cp"), "tiny_dense_8_bfloat16", "3", data_dir, "--quiet"],
                                timeout=60, capture=True)
     assert code != 0 and "seq_len 64 must be divisible by num_cp_shards 3" in "".join(o or "" for o in outs)
+
+
+@pytest.mark.parametrize("w,S,mb,T,E,extra", [(8, 2, 2, 2, 2, []), (4, 1, 2, 2, 2, []),
+                                              (4, 2, 4, 2, 1, ["--pp-schedule", "1f1b"]),
+                                              (4, 1, 2, 2, 2, ["--tp-granularity", "layer"]),
+                                              (8, 1, 2, 2, 2, [])])
+def test_hybrid_4d(w, S, mb, T, E, extra, data_dir):
+    """DP x PP x TP x EP (extension): TP fastest, then EP, then stage, then DP."""
+    d = run(w, "hybrid_4d", "tiny_moe_8_bfloat16", S, mb, T, E, data_dir, "-w", 1, "-r", 2, *extra)
+    g = d["global"]
+    assert d["section"] == "dp_pp_tp_ep" and PP_GLOBAL <= set(g)
+    assert g["num_tensor_shards"] == T and g["num_expert_shards"] == E and g["dp_size"] == w // (S * T * E)
+    spmb = 8 // mb
+    pipe = 64 * 128 * spmb
+    assert g["pipe_msg_size_bytes"] == pipe * 2 and g["tp_allreduce_size_bytes"] == pipe // T * 2
+    assert g["ep_alltoall_size_bytes"] == spmb * 64 * 2 * 128 // E // T * 2
+    ne = 400000 // S // T
+    assert g["ep_allreduce_size_bytes"] == ne * 2
+    assert g["dp_allreduce_size_bytes"] == (ne + (1600000 // S) // E // T) * 2
+    assert g["dlnb"]["iteration"]["compute_floor_ms"] == pytest.approx((mb + S - 1) * 6.0 / S / (mb * T))
+    coords = sorted((r["tp_id"], r["ep_id"], r["stage_id"], r["dp_id"]) for r in d["ranks"])
+    expect = sorted((r % T, (r // T) % E, (r // (T * E)) % S, r // (T * E * S)) for r in range(w))
+    assert coords == expect
+    layer = "layer" in extra
+    # TP all-reduces per microbatch and direction: 2 (reference granularity) or 2 per layer; x 2 directions x 2 runs
+    n_tp = (2 * (4 // S) if layer else 2) * mb * 2 * 2
+    for r in d["ranks"]:
+        assert len(r["runtimes"]) == 2
+        assert len(r["tp_comm_time"]) == n_tp
+        assert len(r["ep_comm_time"]) == 2 * (4 // S) * mb * 2 * 2

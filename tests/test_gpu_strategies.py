@@ -21,6 +21,7 @@ CASES = [
     ("hybrid_3d", "tiny_dense_8_bfloat16", (1, 2, 1)),
     ("hybrid_3d_moe", "tiny_moe_8_bfloat16", (1, 2, 1)),
     ("hybrid_cp", "tiny_dense_8_bfloat16", (1,)),
+    ("hybrid_4d", "tiny_moe_8_bfloat16", (1, 2, 1, 1)),
 ]
 
 

@@ -112,3 +112,23 @@ def test_plan_dp_zero(stats):
     # ZeRO-2 moves half the gradient bytes of an all-reduce per rank (busbw factor (n-1)/n vs 2(n-1)/n)
     assert P.busbw_factor("reduce_scatter", 8) * 2 == P.busbw_factor("allreduce", 8)
     assert z2.memory_bytes < z1.memory_bytes
+
+
+def test_plan_4d_and_cp(stats):
+    st = stats("mixtral_8x7b_16_bfloat16")
+    p4 = P.plan_hybrid(st, 16, "hybrid_4d", 2, 16, 2, 32, experts=4)
+    names = {m.name: m for m in p4.messages}
+    assert names["ep_alltoall"].elements == (1 * st.seq_len * 2 * st.hidden) // 4 // 2
+    assert names["tp_allreduce"].elements == st.seq_len * st.hidden // 2
+    assert names["dp_allreduce"].group_size == 1
+    # E = 1, T = 1 4-D plan degenerates to the hybrid_3d_moe message sizes at EP = 1
+    moe = {m.name: m for m in P.plan_hybrid(st, 2, "hybrid_3d_moe", 2, 16, 1, 32).messages}
+    d4 = {m.name: m for m in P.plan_hybrid(st, 2, "hybrid_4d", 2, 16, 1, 32, experts=1).messages}
+    assert d4["ep_alltoall"].elements == moe["ep_alltoall"].elements
+    assert d4["dp_allreduce"].elements == moe["dp_allreduce"].elements
+    l8 = stats("llama3_8b_16_bfloat16")
+    ring = P.plan_cp(l8, 8, 8, 32, 32, 8)
+    kv = 2 * 16 * (8192 // 8) * (4096 * 8 // 32)
+    assert ring.messages[0].elements == kv and ring.messages[0].calls_per_iter == 32 * 7
+    uly = P.plan_cp(l8, 8, 8, 32, 32, 8, algo="ulysses")
+    assert uly.messages[0].op == "alltoall" and uly.messages[0].calls_per_iter == 64
