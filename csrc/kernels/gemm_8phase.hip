@@ -145,7 +145,8 @@ __device__ __forceinline__ void stage(const Ctx& c, int t, int slot) {
 }
 
 // Deadline state of the persistent variant: thread 0 (wave row 0) reads the
-// clock in phase 3 of every K-tile, writes the stop decision into an LDS flag
+// clock in phase 2 of every K-tile, writes the stop
+// decision in phase 3 into an LDS flag
 // (completed before its barrier), and every wave reads it after its own first
 // barrier of that phase - the write precedes every read (the rows are one
 // barrier apart) and the next write is four phases away.
@@ -170,13 +171,13 @@ __device__ __forceinline__ bool phase(const Ctx& c, int v, Frags<FP8>& f, f32x4 
     read_frags<FP8, 2>(cur + kB0 * kHalf, c.wc * 32, c.r16, c.h, f.bx);
     __builtin_amdgcn_sched_barrier(0);
     read_frags<FP8, 4>(cur + kA0 * kHalf, c.wr * 64, c.r16, c.h, f.a);
-    // the clock is read three phases before its use, so its (scalar-memory)
-    // latency never stalls wave 0 in front of a barrier
-    if constexpr (DL) now = __builtin_amdgcn_s_memrealtime();
   } else if constexpr (Q == 1) {
     read_frags<FP8, 2>(cur + kB1 * kHalf, c.wc * 32, c.r16, c.h, f.by);
   } else if constexpr (Q == 2) {
     read_frags<FP8, 4>(cur + kA1 * kHalf, c.wr * 64, c.r16, c.h, f.a);
+    // the clock is read one phase before its use, so its (scalar-memory)
+    // latency does not stall wave 0 in front of a barrier
+    if constexpr (DL) now = __builtin_amdgcn_s_memrealtime();
   } else if constexpr (DL) {
     if (d.tid == 0) {
       const uint64_t el = (now - d.t0) & ((1ull << 48) - 1);
@@ -296,7 +297,7 @@ __global__ void __launch_bounds__(512, 1)
     gemm_8phase_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
                        int K, int lda, int ldb, int ldc, uint64_t* __restrict__ slot, uint32_t epoch, uint64_t ticks,
                        uint64_t slice_end, uint64_t* __restrict__ tstart) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + 16];  // ONE array: staging + deadline flag
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + 16];  // ONE array: staging + deadline flags
   const int tid = threadIdx.x;
   Ctx c;
   c.lane = tid & 63;

@@ -117,6 +117,11 @@ int dlnb_sgd_momentum_bf16(void* p, void* m, const void* g, size_t n, float lr, 
 
 double dlnb_wallclock_hz(int device) { return dlnb::kernels::wallclock_hz(device); }
 
+// One wave writes s_memrealtime into *slot when the stream reaches this point.
+int dlnb_stamp(void* slot, void* stream) {
+  return guard([&] { dlnb::kernels::stamp(static_cast<uint64_t*>(slot), stream); });
+}
+
 // Host conversions exposed for tests (OCP fp8 / bf16 rounding parity).
 float dlnb_bf16_to_float(unsigned short v) { return dlnb::bf16_to_float(v); }
 unsigned short dlnb_float_to_bf16(float f) { return dlnb::float_to_bf16(f); }

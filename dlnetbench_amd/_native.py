@@ -56,6 +56,7 @@ def lib() -> ctypes.CDLL:
     L.dlnb_idle_wait_us.argtypes = [c_dbl, c_int, c_vp]
     L.dlnb_busy_spin_us.argtypes = [c_dbl, c_int, c_vp]
     L.dlnb_sgd_momentum_bf16.argtypes = [c_vp, c_vp, c_vp, c_size, c_float, c_float, c_vp]
+    L.dlnb_stamp.argtypes = [c_vp, c_vp]
     L.dlnb_wallclock_hz.argtypes = [c_int]
     L.dlnb_wallclock_hz.restype = c_dbl
     L.dlnb_bf16_to_float.argtypes = [ctypes.c_ushort]

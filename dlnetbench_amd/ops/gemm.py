@@ -91,3 +91,10 @@ def idle_wait_us(us: float, device: int = 0):
 def busy_spin_us(us: float, device: int = 0):
     import torch
     _native.check(_native.lib().dlnb_busy_spin_us(us, device, torch.cuda.current_stream(device).cuda_stream))
+
+
+def stamp_(slot, index: int = 0):
+    """Write the device wall clock (s_memrealtime, 100 MHz) into slot[index] (int64 CUDA tensor)
+    when torch's current stream reaches this point."""
+    _native.check(_native.lib().dlnb_stamp(slot.data_ptr() + 8 * index, _stream(slot)))
+    return slot
