@@ -80,6 +80,7 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  --compute-dtype T      auto | bf16 | fp8 (GEMM operand type for gemm/flops)\n"
      << "  --schedule S           overlap (stream-ordered) | reference (blocking like DLNetBench)\n"
      << "  --tp-granularity G     microbatch | layer (hybrid_3d, hybrid_4d)\n"
+     << "  --sequence-parallel    hybrid_3d/4d: each TP all-reduce becomes all-gather + reduce-scatter (Megatron-SP)\n"
      << "  --pp-schedule gpipe|1f1b  hybrids: all forwards then all backwards (reference) or one-forward-one-backward\n"
      << "  --ep-overlap           hybrid_3d_moe: two half-microbatches, each one's all-to-all under the other's compute\n"
      << "  --dp-buckets K         hybrids: DP all-reduce buckets overlapped with the last backward\n"
@@ -146,6 +147,8 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
       o.schedule = val("schedule");
     } else if (is("--tp-granularity")) {
       o.tp_granularity = val("tp-granularity");
+    } else if (a == "--sequence-parallel") {
+      o.sequence_parallel = true;
     } else if (a == "--ep-overlap") {
       o.ep_overlap = true;
     } else if (is("--pp-schedule")) {

@@ -127,6 +127,8 @@ class Pipeline : public Strategy {
       if (has_tp_) tp_ar_ = pipe_ / T_;
     }
 
+    sp_ = has_tp_ && o.sequence_parallel;
+    tp_shard_ = has_tp_ ? (tp_ar_ + T_ - 1) / T_ : 0;
     Device& dev = *ctx.dev;
     es_ = dtype_size(ctx.wire);
     const int rank = ctx.rank();
@@ -159,7 +161,7 @@ class Pipeline : public Strategy {
       if (has_tp_) {
         std::vector<int> m;
         for (int t = 0; t < T_; ++t) m.push_back(base + ep_id_ * T_ + t);
-        tp_comm_ = ctx.comms->create("tp/" + where + "/" + std::to_string(ep_id_), m, tp_ar_ * es_, false);
+        tp_comm_ = ctx.comms->create("tp/" + where + "/" + std::to_string(ep_id_), m, tp_shard_ * T_ * es_, false);
       }
       if (has_ep_) {
         std::vector<int> m;
@@ -192,9 +194,9 @@ class Pipeline : public Strategy {
     dev.fill_random(grad_.data(), dp_ar_, ctx.wire, 4200, *compute_);
     if (!o.in_place) sum_grad_ = dev.alloc(dp_ar_ * es_);
     if (has_tp_) {
-      tp_buf_ = dev.alloc(tp_ar_ * es_);
-      tp_res_ = dev.alloc(tp_ar_ * es_);
-      dev.fill_random(tp_buf_.data(), tp_ar_, ctx.wire, 4300, *compute_);
+      tp_buf_ = dev.alloc(tp_shard_ * T_ * es_);
+      tp_res_ = dev.alloc(tp_shard_ * T_ * es_);
+      dev.fill_random(tp_buf_.data(), tp_shard_ * T_, ctx.wire, 4300, *compute_);
     }
     if (has_ep_) {
       ep_send_ = dev.alloc(a2a_ * E_ * es_);
@@ -240,14 +242,23 @@ class Pipeline : public Strategy {
     for (const char* k : {"pp_comm_time", "dp_comm_time", "pp_send_time", "pp_recv_time", "dp_exposed_time"})
       timers_->ensure(k);
     if (has_tp_) timers_->ensure("tp_comm_time");
+    if (sp_) {
+      timers_->ensure("tp_ag_time");
+      timers_->ensure("tp_rs_time");
+    }
     if (has_ep_) {
       timers_->ensure("ep_comm_time");
       timers_->ensure("dp_ep_comm_time");
     }
     if (prev_ || next_) stats_.push_back({"sendrecv", CollKind::SendRecv, 2, static_cast<double>(pipe_ * es_), "pp_send_time"});
     stats_.push_back({"dp_allreduce", CollKind::AllReduce, dp_size_, static_cast<double>(dp_ar_ / o.dp_buckets * es_), "dp_comm_time"});
-    if (has_tp_)
+    if (has_tp_ && !sp_)
       stats_.push_back({"tp_allreduce", CollKind::AllReduce, T_, static_cast<double>(tp_ar_ * es_), "tp_comm_time"});
+    if (has_tp_ && sp_) {
+      stats_.push_back({"tp_allgather", CollKind::AllGather, T_, static_cast<double>(tp_shard_ * T_ * es_), "tp_ag_time"});
+      stats_.push_back({"tp_reduce_scatter", CollKind::ReduceScatter, T_, static_cast<double>(tp_shard_ * T_ * es_),
+                        "tp_rs_time"});
+    }
     if (has_ep_)
       stats_.push_back({"ep_alltoall", CollKind::AllToAll, E_,
                         static_cast<double>((ep_overlap_ ? a2a_ / 2 : a2a_) * E_ * es_), "ep_comm_time"});
@@ -312,8 +323,22 @@ class Pipeline : public Strategy {
     }
   }
 
+  // One TP all-reduce of the activations, or with --sequence-parallel the
+  // Megatron-SP pair that replaces it: all-gather of the sequence shards into
+  // the tensor-parallel region, reduce-scatter out of it (same bytes on the
+  // wire, activations outside the TP region stay 1/T).
   void tp_allreduce() {
     int t = timers_->begin(*compute_);
+    if (sp_) {
+      int ta = timers_->begin(*compute_);
+      tp_comm_->all_gather(tp_buf_.data(), tp_res_.data(), tp_shard_, ctx_->wire, *compute_);
+      timers_->end(ta, *compute_, "tp_ag_time");
+      int tr = timers_->begin(*compute_);
+      tp_comm_->reduce_scatter(tp_res_.data(), tp_buf_.data(), tp_shard_, ctx_->wire, *compute_);
+      timers_->end(tr, *compute_, "tp_rs_time");
+      timers_->end(t, *compute_, "tp_comm_time");
+      return;
+    }
     tp_comm_->all_reduce(tp_buf_.data(), tp_res_.data(), tp_ar_, ctx_->wire, *compute_);
     timers_->end(t, *compute_, "tp_comm_time");
   }
@@ -609,6 +634,7 @@ class Pipeline : public Strategy {
     g["total_model_size_params"] = ctx.stats.model_size;
     g["pipe_msg_size_bytes"] = pipe_ * es_;
     if (has_tp_) g["tp_allreduce_size_bytes"] = tp_ar_ * es_;
+    if (has_tp_) g["sequence_parallel"] = sp_;
     if (has_ep_) {
       g["ep_alltoall_size_bytes"] = a2a_ * es_;
       g["ep_allreduce_size_bytes"] = ne_ * es_;
@@ -649,7 +675,8 @@ class Pipeline : public Strategy {
   Context* ctx_ = nullptr;
   int S_ = 1, mb_ = 1, inner_ = 1, L_ = 0, layers_per_stage_ = 0, dp_size_ = 1;
   int stage_ = 0, inner_id_ = 0, dp_id_ = 0, tp_id_ = 0, ep_id_ = 0, T_ = 1, E_ = 1;
-  bool has_tp_ = false, has_ep_ = false;
+  bool has_tp_ = false, has_ep_ = false, sp_ = false;
+  uint64_t tp_shard_ = 0;  // ceil(tp_ar_ / T): sequence-parallel shard
   bool reference_ = false;
   bool one_f_one_b_ = false;
   bool ep_overlap_ = false;

@@ -31,7 +31,8 @@ _FLAG = {
     "comm_lanes": "--comm-lanes", "pp_schedule": "--pp-schedule", "zero": "--zero", "cp_algo": "--cp-algo",
 }
 _BOOL = {"in_place": "--in-place", "optimizer": "--optimizer", "loop": "--loop", "quiet": "--quiet",
-         "silent": "--silent", "graph": "--graph", "trace": "--trace", "ep_overlap": "--ep-overlap"}
+         "silent": "--silent", "graph": "--graph", "trace": "--trace", "ep_overlap": "--ep-overlap",
+         "sequence_parallel": "--sequence-parallel"}
 
 
 def build_args(strategy: str, model: str, *params: int, base_path: str = ".", topology: bool = False,

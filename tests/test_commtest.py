@@ -115,6 +115,7 @@ XGMI_STRATS = [  # strategy, model, positional args, extra flags, ranks
     ("hybrid_cp", "tiny_dense_8_bfloat16", ["2"], [], 4),
     ("hybrid_cp", "tiny_dense_8_bfloat16", ["4"], ["--cp-algo", "ulysses"], 4),
     ("hybrid_4d", "tiny_moe_8_bfloat16", ["2", "2", "2", "2"], ["--pp-schedule", "1f1b"], 8),
+    ("hybrid_3d", "tiny_dense_8_bfloat16", ["2", "2", "2"], ["--sequence-parallel"], 4),
 ]
 
 

@@ -340,3 +340,20 @@ def test_hybrid_4d(w, S, mb, T, E, extra, data_dir):
         assert len(r["runtimes"]) == 2
         assert len(r["tp_comm_time"]) == n_tp
         assert len(r["ep_comm_time"]) == 2 * (4 // S) * mb * 2 * 2
+
+
+@pytest.mark.parametrize("prog,model,params", [("hybrid_3d", "tiny_dense_8_bfloat16", (2, 2, 2)),
+                                               ("hybrid_4d", "tiny_moe_8_bfloat16", (1, 2, 2, 2))])
+def test_sequence_parallel(prog, model, params, data_dir):
+    """--sequence-parallel (Megatron-SP): every TP all-reduce becomes all-gather + reduce-scatter of 1/T shards."""
+    base = run(4, prog, model, *params, data_dir, "-w", 1, "-r", 2)
+    d = run(4, prog, model, *params, data_dir, "-w", 1, "-r", 2, "--sequence-parallel")
+    assert d["global"]["sequence_parallel"] is True and base["global"]["sequence_parallel"] is False
+    T = params[2]
+    tp = d["global"]["tp_allreduce_size_bytes"] // 2
+    for r, rb in zip(d["ranks"], base["ranks"]):
+        c = r["comm"]
+        assert "tp_allreduce" not in c and c["tp_allgather"]["ops"] == c["tp_reduce_scatter"]["ops"]
+        assert c["tp_allgather"]["ops"] == rb["comm"]["tp_allreduce"]["ops"]
+        assert c["tp_allgather"]["bytes_per_op"] == -(-tp // T) * T * 2
+        assert len(r["tp_comm_time"]) == len(rb["tp_comm_time"])
