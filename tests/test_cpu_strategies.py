@@ -48,7 +48,7 @@ PP_GLOBAL = {"model_name", "num_stages", "num_microbatches", "samples_per_microb
 PP_RANK = {"runtimes", "pp_comm_time", "dp_comm_time", "hostname", "stage_id"}
 
 
-@pytest.mark.parametrize("w", [1, 2, 4])
+@pytest.mark.parametrize("w", [1, 2, 4, 8])
 def test_dp(w, data_dir):
     d = run(w, "dp", "tiny_dense_8_bfloat16", 5, data_dir, "-w", 1, "-r", 3)
     g = d["global"]
@@ -65,7 +65,7 @@ def test_dp(w, data_dir):
     assert d["global"]["dlnb"]["iteration"]["median_ms"] >= 6.0 * 0.98
 
 
-@pytest.mark.parametrize("w,zero", [(1, 1), (2, 1), (2, 2), (4, 2), (3, 2)])
+@pytest.mark.parametrize("w,zero", [(1, 1), (2, 1), (2, 2), (4, 2), (3, 2), (8, 1), (8, 2)])
 def test_dp_zero(w, zero, data_dir):
     """ZeRO-1/2 (extension): sharded optimizer + parameter all-gather, reduce-scatter for stage 2."""
     d = run(w, "dp", "tiny_dense_8_bfloat16", 5, data_dir, "-w", 1, "-r", 2, "--zero", zero)
@@ -93,7 +93,7 @@ def test_dp_zero_rejected_elsewhere(data_dir):
     assert code != 0 and "--zero applies to dp" in "".join(o or "" for o in outs)
 
 
-@pytest.mark.parametrize("w,F", [(2, 2), (4, 2), (4, 4)])
+@pytest.mark.parametrize("w,F", [(2, 2), (4, 2), (4, 4), (8, 8), (8, 4)])
 def test_fsdp(w, F, data_dir):
     U = 4
     d = run(w, "fsdp", "tiny_dense_8_bfloat16", U, F, data_dir, "-w", 1, "-r", 2)
@@ -130,7 +130,7 @@ def test_fsdp_reference_schedule(data_dir):
     assert d["global"]["dlnb"]["schedule"] == "reference"
 
 
-@pytest.mark.parametrize("w,S,mb", [(1, 1, 2), (2, 2, 4), (4, 4, 8), (4, 2, 2)])
+@pytest.mark.parametrize("w,S,mb", [(1, 1, 2), (2, 2, 4), (4, 4, 8), (4, 2, 2), (8, 4, 8)])
 def test_hybrid_2d(w, S, mb, data_dir):
     d = run(w, "hybrid_2d", "tiny_dense_8_bfloat16", S, mb, data_dir, "-w", 1, "-r", 2)
     g = d["global"]
@@ -275,7 +275,7 @@ CP_RANK = {"runtimes", "cp_comm_time", "cp_exposed_time", "dp_comm_time", "dp_ex
 
 
 @pytest.mark.parametrize("w,C,algo", [(2, 2, "ring"), (4, 2, "ring"), (4, 4, "ring"), (2, 2, "ulysses"),
-                                      (4, 4, "ulysses"), (2, 1, "ring")])
+                                      (4, 4, "ulysses"), (2, 1, "ring"), (8, 4, "ring"), (8, 4, "ulysses")])
 def test_hybrid_cp(w, C, algo, data_dir):
     """Context parallelism (extension): ring attention P2P or Ulysses all-to-all + DP gradient buckets."""
     d = run(w, "hybrid_cp", "tiny_dense_8_bfloat16", C, data_dir, "-w", 1, "-r", 2, "--cp-algo", algo)
