@@ -19,3 +19,8 @@ run h2d_llama3_8b hybrid_2d llama3_8b_16_bfloat16 1 4
 run h3d_llama3_8b hybrid_3d llama3_8b_16_bfloat16 1 4 1
 run h3d_1f1b_llama3_8b hybrid_3d llama3_8b_16_bfloat16 1 4 1 --pp-schedule 1f1b
 run moe_mixtral_scaled hybrid_3d_moe mixtral_8x7b_16_bfloat16 1 4 1 --time-scale 0.1
+# extensions
+run dpz2_llama3_8b dp llama3_8b_16_bfloat16 10 --zero 2
+run cp_llama3_8b hybrid_cp llama3_8b_16_bfloat16 1
+run h3d_sp_llama3_8b hybrid_3d llama3_8b_16_bfloat16 1 4 1 --sequence-parallel
+run h4d_mixtral_scaled hybrid_4d mixtral_8x7b_16_bfloat16 1 4 1 1 --time-scale 0.1
