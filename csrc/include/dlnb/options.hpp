@@ -54,7 +54,8 @@ struct Options {
   std::string schedule = "overlap";    // overlap | reference
   std::string tp_granularity = "microbatch";  // microbatch | layer
   bool sequence_parallel = false;  // TP all-reduce -> all-gather + reduce-scatter (Megatron-SP)
-  std::string pp_schedule = "gpipe";          // gpipe (reference) | 1f1b
+  std::string pp_schedule = "gpipe";          // gpipe (reference) | 1f1b | interleaved
+  int pp_virtual = 2;                         // interleaved: model chunks (virtual stages) per stage
   bool ep_overlap = false;  // moe: overlap each half-microbatch's all-to-all with the other half's compute
   int dp_buckets = 1;  // hybrids: DP all-reduce buckets overlapped with the last backward
   bool in_place = false;

@@ -81,7 +81,9 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  --schedule S           overlap (stream-ordered) | reference (blocking like DLNetBench)\n"
      << "  --tp-granularity G     microbatch | layer (hybrid_3d, hybrid_4d)\n"
      << "  --sequence-parallel    hybrid_3d/4d: each TP all-reduce becomes all-gather + reduce-scatter (Megatron-SP)\n"
-     << "  --pp-schedule gpipe|1f1b  hybrids: all forwards then all backwards (reference) or one-forward-one-backward\n"
+     << "  --pp-schedule gpipe|1f1b|interleaved  hybrids: all forwards then all backwards (reference),\n"
+     << "                         one-forward-one-backward, or interleaved 1F1B over --pp-virtual V chunks per stage\n"
+     << "  --pp-virtual V         interleaved: model chunks per stage (default 2)\n"
      << "  --ep-overlap           hybrid_3d_moe: two half-microbatches, each one's all-to-all under the other's compute\n"
      << "  --dp-buckets K         hybrids: DP all-reduce buckets overlapped with the last backward\n"
      << "                         (hybrid_cp: gradient buckets by layer, overlapped with the backward)\n"
@@ -153,6 +155,8 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
       o.ep_overlap = true;
     } else if (is("--pp-schedule")) {
       o.pp_schedule = val("pp-schedule");
+    } else if (is("--pp-virtual")) {
+      o.pp_virtual = to_int(val("pp-virtual"), "pp-virtual");
     } else if (is("--cp-algo")) {
       o.cp_algo = val("cp-algo");
     } else if (is("--dp-buckets")) {
@@ -241,7 +245,8 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
                    o.num_cp_shards >= 1,
                "parallelism degrees must be >= 1");
   DLNB_REQUIRE(o.schedule == "overlap" || o.schedule == "reference", "--schedule must be overlap or reference");
-  DLNB_REQUIRE(o.pp_schedule == "gpipe" || o.pp_schedule == "1f1b", "--pp-schedule must be gpipe or 1f1b");
+  DLNB_REQUIRE(o.pp_schedule == "gpipe" || o.pp_schedule == "1f1b" || o.pp_schedule == "interleaved",
+               "--pp-schedule must be gpipe, 1f1b or interleaved");
   DLNB_REQUIRE(o.tp_granularity == "microbatch" || o.tp_granularity == "layer",
                "--tp-granularity must be microbatch or layer");
   DLNB_REQUIRE(o.comm_lanes == "single" || o.comm_lanes == "split", "--comm-lanes must be single or split");

@@ -78,9 +78,13 @@ class Pipeline : public Strategy {
     inner_ = T_ * E_;  // TP fastest, then EP (hybrid_4d), then stage, then DP replica
     reference_ = o.schedule == "reference";
     one_f_one_b_ = o.pp_schedule == "1f1b";
+    interleaved_ = o.pp_schedule == "interleaved";
+    V_ = interleaved_ ? o.pp_virtual : 1;
     ep_overlap_ = o.ep_overlap && has_ep_ && !reference_;
     DLNB_REQUIRE(!(ep_overlap_ && has_tp_), "--ep-overlap is not supported with tensor parallelism (hybrid_4d)");
-    DLNB_REQUIRE(!(one_f_one_b_ && reference_), "--pp-schedule 1f1b needs --schedule overlap");
+    DLNB_REQUIRE(!((one_f_one_b_ || interleaved_) && reference_), "--pp-schedule " << o.pp_schedule
+                                                                                   << " needs --schedule overlap");
+    DLNB_REQUIRE(V_ >= 1, "--pp-virtual must be >= 1");
     DLNB_REQUIRE(ctx.have_arch, "hybrid strategies need models/<model>.json (layer count)");
     L_ = static_cast<int>(ctx.arch.num_layers);
     DLNB_REQUIRE(L_ > 0, "model has no layers: " << ctx.arch.path);
@@ -93,6 +97,12 @@ class Pipeline : public Strategy {
       DLNB_REQUIRE(st.experts % E_ == 0, "experts " << st.experts << " must be divisible by num_expert_shards " << E_);
     dp_size_ = W / (S_ * inner_);
     layers_per_stage_ = L_ / S_;
+    if (interleaved_) {
+      DLNB_REQUIRE(L_ % (S_ * V_) == 0, "interleaved: num_layers " << L_ << " must be divisible by stages*virtual "
+                                                                   << S_ * V_);
+      DLNB_REQUIRE(mb_ % S_ == 0, "interleaved: num_microbatches " << mb_ << " must be a multiple of num_stages " << S_);
+    }
+    layers_per_chunk_ = layers_per_stage_ / V_;
 
     GridCoords c = grid_coords(ctx.rank(), inner_, S_);
     stage_ = c.stage_id;
@@ -141,6 +151,21 @@ class Pipeline : public Strategy {
         std::string nm = "pp/link/" + std::to_string(dp_id_) + "/" + std::to_string(inner_id_) + "/" + std::to_string(s);
         auto comm = ctx.comms->create(nm, {pp[s], pp[s + 1]}, pipe_ * es_, true);
         if (stage_ == s) {
+          next_ = std::move(comm);
+          next_peer_ = 1;
+        } else {
+          prev_ = std::move(comm);
+          prev_peer_ = 0;
+        }
+      }
+    }
+    if (interleaved_ && S_ > 1) {
+      // The interleaved schedule's ring closes: chunk c of the last stage
+      // feeds chunk c+1 of stage 0 over a wrap link.
+      if (stage_ == S_ - 1 || stage_ == 0) {
+        std::string nm = "pp/wrap/" + std::to_string(dp_id_) + "/" + std::to_string(inner_id_);
+        auto comm = ctx.comms->create(nm, {pp[S_ - 1], pp[0]}, pipe_ * es_, true);
+        if (stage_ == S_ - 1) {
           next_ = std::move(comm);
           next_peer_ = 1;
         } else {
@@ -224,7 +249,7 @@ class Pipeline : public Strategy {
       mom_ = dev.alloc(dp_ar_ * es_);
     }
     auto mk = [&](std::vector<std::unique_ptr<Event>>& v) {
-      for (int i = 0; i < mb_; ++i) v.push_back(dev.create_event());
+      for (int i = 0; i < mb_ * V_; ++i) v.push_back(dev.create_event());
     };
     mk(recv_f_);
     mk(fwd_done_);
@@ -270,7 +295,7 @@ class Pipeline : public Strategy {
     ComputeEngine& ce = *ctx.compute;
     const bool tp_layer = has_tp_ && ctx.opt.tp_granularity == "layer";
     if (has_ep_) {
-      const int n = 2 * layers_per_stage_;
+      const int n = 2 * layers_per_chunk_;
       if (reference_) {
         ce.run(*compute_, us, flops);
         for (int i = 0; i < n; ++i) ep_alltoall();
@@ -308,7 +333,7 @@ class Pipeline : public Strategy {
       }
     } else if (has_tp_) {
       if (tp_layer) {
-        const int slices = 4 * layers_per_stage_ / 2;  // 2 per layer
+        const int slices = 2 * layers_per_chunk_;  // 2 per layer
         for (int i = 0; i < slices; ++i) {
           ce.run(*compute_, us / slices, flops / slices);
           tp_allreduce();
@@ -547,8 +572,94 @@ class Pipeline : public Strategy {
     finish_iteration();
   }
 
+  // ------------------------------------------------- interleaved 1F1B
+  // Megatron's interleaved (virtual-stage) schedule: each stage holds V
+  // model chunks; virtual stage c*S + s is chunk c of stage s, so a
+  // microbatch crosses the S-stage ring V times (the last stage's chunk c
+  // feeds stage 0's chunk c+1 over the wrap link). Forward k of a stage runs
+  // chunk (k/S)%V of microbatch (k/(S*V))*S + k%S; backward k the chunk
+  // V-1-(k/S)%V. Warm-up = (S-s-1)*2 + (V-1)*S forwards (all of them when
+  // mb == S), then forward/backward pairs, then the remaining backwards; the
+  // bubble shrinks from (S-1)(f+b) to (S-1)(f+b)/V. The P2P after each step
+  // is Megatron's, split per link: next link {send F, receive B}, previous
+  // link {send B, receive F}.
+  int chunk_f(int k) const { return (k / S_) % V_; }
+  int chunk_b(int k) const { return V_ - 1 - (k / S_) % V_; }
+  bool in_f(int k) const { return !(stage_ == 0 && chunk_f(k) == 0); }
+  bool out_f(int k) const { return !(stage_ == S_ - 1 && chunk_f(k) == V_ - 1); }
+  bool in_b(int k) const { return !(stage_ == S_ - 1 && chunk_b(k) == V_ - 1); }
+  bool out_b(int k) const { return !(stage_ == 0 && chunk_b(k) == 0); }
+
+  void fwd_chunk(int k) {
+    if (S_ > 1 && in_f(k))
+      timers_->stall(*compute_, *recv_f_[k], "pp_comm_time");
+    else
+      timers_->add("pp_comm_time", 0.0);
+    if (S_ > 1 && k >= 2) compute_->wait(*send_f_[k - 2]);  // act_out[k & 1] sent (no-op if never recorded)
+    micro_compute(fwd_mb_us_ / V_, fwd_mb_flops_ / V_);
+    compute_->record(*fwd_done_[k]);
+  }
+
+  void bwd_chunk(int j) {
+    const int nbk = ctx_->opt.dp_buckets;
+    const int total = mb_ * V_;
+    if (S_ > 1 && in_b(j))
+      timers_->stall(*compute_, *recv_b_[j], "pp_comm_time");
+    else
+      timers_->add("pp_comm_time", 0.0);
+    if (S_ > 1 && j >= 2) compute_->wait(*send_b_[j - 2]);  // grad_out[j & 1] sent
+    if (j == total - 1 && nbk > 1) {
+      for (int k = 0; k < nbk; ++k) {  // DP buckets overlap the last backward
+        ctx_->compute->run(*compute_, bwd_mb_us_ / V_ / nbk, bwd_mb_flops_ / V_ / nbk);
+        compute_->record(*bucket_ready_[k]);
+        dp_stream_->wait(*bucket_ready_[k]);
+        dp_allreduce_bucket(k, nbk);
+      }
+    } else {
+      micro_compute(bwd_mb_us_ / V_, bwd_mb_flops_ / V_);
+    }
+    compute_->record(*bwd_done_[j]);
+  }
+
+  // Link groups of one step (-1 = nothing in that slot).
+  void links(int send_f, int recv_b, int send_b, int recv_f) {
+    if (S_ == 1) return;
+    if (send_f >= 0 || recv_b >= 0) next_link(send_f, recv_b);
+    if (send_b >= 0 || recv_f >= 0) prev_link(send_b, recv_f);
+  }
+
+  void enqueue_interleaved() {
+    const int total = mb_ * V_;
+    const int w = mb_ == S_ ? total : std::min((S_ - stage_ - 1) * 2 + (V_ - 1) * S_, total);
+    const int rem = total - w;
+    links(-1, -1, -1, in_f(0) ? 0 : -1);
+    for (int k = 0; k < w; ++k) {
+      fwd_chunk(k);
+      const int rf = k + 1 < total && in_f(k + 1) ? k + 1 : -1;
+      const int rb = k == w - 1 && rem > 0 && in_b(0) ? 0 : -1;
+      links(out_f(k) ? k : -1, rb, -1, rf);
+    }
+    for (int j = 0; j < rem; ++j) {
+      const int k = w + j;
+      fwd_chunk(k);
+      bwd_chunk(j);
+      const int rf = k + 1 < total && in_f(k + 1) ? k + 1 : -1;
+      const int rb = j + 1 < total && in_b(j + 1) ? j + 1 : -1;
+      links(out_f(k) ? k : -1, rb, out_b(j) ? j : -1, rf);
+    }
+    if (rem == 0) links(-1, in_b(0) ? 0 : -1, -1, -1);
+    for (int j = rem; j < total; ++j) {
+      bwd_chunk(j);
+      const int rb = j + 1 < total && in_b(j + 1) ? j + 1 : -1;
+      links(-1, rb, out_b(j) ? j : -1, -1);
+    }
+    finish_iteration();
+  }
+
   void enqueue_iteration() override {
-    if (one_f_one_b_)
+    if (interleaved_)
+      enqueue_interleaved();
+    else if (one_f_one_b_)
       enqueue_1f1b();
     else
       enqueue_gpipe();
@@ -591,7 +702,8 @@ class Pipeline : public Strategy {
   }
 
   double compute_floor_us(const Context&) const override {
-    return (mb_ + S_ - 1) * (fwd_mb_us_ + bwd_mb_us_);  // GPipe / 1F1B bubble included
+    // GPipe / 1F1B: (mb + S - 1)(f + b); interleaved: the bubble / V
+    return (mb_ + static_cast<double>(S_ - 1) / V_) * (fwd_mb_us_ + bwd_mb_us_);
   }
 
   std::string section_id() const override {
@@ -641,6 +753,7 @@ class Pipeline : public Strategy {
     }
     g["dp_allreduce_size_bytes"] = dp_ar_ * es_;
     g["pp_schedule"] = ctx.opt.pp_schedule;
+    if (interleaved_) g["pp_virtual_stages"] = V_;
     if (has_ep_) g["ep_overlap"] = ep_overlap_;
     if (has_tp_) g["tp_granularity"] = ctx.opt.tp_granularity;
     g["device"] = ctx.dev->kind() == DeviceKind::CPU ? "CPU" : "GPU";
@@ -678,7 +791,8 @@ class Pipeline : public Strategy {
   bool has_tp_ = false, has_ep_ = false, sp_ = false;
   uint64_t tp_shard_ = 0;  // ceil(tp_ar_ / T): sequence-parallel shard
   bool reference_ = false;
-  bool one_f_one_b_ = false;
+  bool one_f_one_b_ = false, interleaved_ = false;
+  int V_ = 1, layers_per_chunk_ = 0;
   bool ep_overlap_ = false;
   Stream* ep_stream_ = nullptr;  // = dp_stream_ (see setup)
   std::unique_ptr<Event> chunk_done_[2], a2a_done_[2];

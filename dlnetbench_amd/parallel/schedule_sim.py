@@ -1,0 +1,209 @@
+"""Discrete-event model of the pipeline schedules' enqueue logic.
+
+Mirrors csrc/src/strategy_pipeline.cpp (enqueue_gpipe / enqueue_1f1b /
+enqueue_interleaved): per rank a compute stream and two link streams (prev,
+next) executing their operations in order; compute waits on receive events
+and on the send of the buffer it overwrites; a link operation is a group of
+at most one send and one receive that completes when every matching
+operation (per channel FIFO order) sits at the head of its own stream with
+its waits satisfied. Links cost nothing, so a finished run's makespan is the
+schedule's compute critical path and a stuck run is a deadlock.
+
+    python -m dlnetbench_amd.parallel.schedule_sim --stages 4 --microbatches 8 --virtual 2
+"""
+from __future__ import annotations
+
+import argparse
+from typing import Dict, List, Tuple
+
+
+def build(S: int, mb: int, V: int, f: float, b: float, sched: str) -> Dict[Tuple[int, str], List[dict]]:
+    streams: Dict[Tuple[int, str], List[dict]] = {}
+    total = mb * V
+
+    def op(r, st, **kw):
+        streams.setdefault((r, st), []).append(kw)
+
+    for s in range(S):
+        il = sched == "interleaved"
+
+        def chunk_f(k):
+            return (k // S) % V
+
+        def chunk_b(k):
+            return V - 1 - (k // S) % V
+
+        def in_f(k):
+            return not (s == 0 and chunk_f(k) == 0) if il else s > 0
+
+        def out_f(k):
+            return not (s == S - 1 and chunk_f(k) == V - 1) if il else s < S - 1
+
+        def in_b(k):
+            return not (s == S - 1 and chunk_b(k) == V - 1) if il else s < S - 1
+
+        def out_b(k):
+            return not (s == 0 and chunk_b(k) == 0) if il else s > 0
+
+        def fwd(k):
+            waits = [(s, "recvF", k)] if S > 1 and in_f(k) else []
+            if k >= 2 and S > 1 and out_f(k - 2):
+                waits.append((s, "sentF", k - 2))
+            op(s, "c", dur=f / V, waits=waits, rec=[(s, "fdone", k)])
+
+        def bwd(j):
+            waits = [(s, "recvB", j)] if S > 1 and in_b(j) else []
+            if j >= 2 and S > 1 and out_b(j - 2):
+                waits.append((s, "sentB", j - 2))
+            op(s, "c", dur=b / V, waits=waits, rec=[(s, "bdone", j)])
+
+        def nxt(sf, rb):  # next link: send F(sf) to s+1, receive B(rb) from s+1
+            if S == 1 or (sf < 0 and rb < 0):
+                return
+            waits, p2p, rec = [], [], []
+            if sf >= 0:
+                waits.append((s, "fdone", sf)); p2p.append(("send", "F", (s + 1) % S)); rec.append((s, "sentF", sf))
+            if rb >= 0:
+                if rb >= 2:
+                    waits.append((s, "bdone", rb - 2))
+                p2p.append(("recv", "B", (s + 1) % S)); rec.append((s, "recvB", rb))
+            op(s, "n", dur=0.0, waits=waits, rec=rec, p2p=p2p)
+
+        def prv(sb, rf):  # previous link: send B(sb) to s-1, receive F(rf) from s-1
+            if S == 1 or (sb < 0 and rf < 0):
+                return
+            waits, p2p, rec = [], [], []
+            if sb >= 0:
+                waits.append((s, "bdone", sb)); p2p.append(("send", "B", (s - 1) % S)); rec.append((s, "sentB", sb))
+            if rf >= 0:
+                if rf >= 2:
+                    waits.append((s, "fdone", rf - 2))
+                p2p.append(("recv", "F", (s - 1) % S)); rec.append((s, "recvF", rf))
+            op(s, "p", dur=0.0, waits=waits, rec=rec, p2p=p2p)
+
+        if il:
+            w = total if mb == S else min((S - s - 1) * 2 + (V - 1) * S, total)
+            rem = total - w
+            if in_f(0):
+                prv(-1, 0)
+            for k in range(w):
+                fwd(k)
+                nxt(k if out_f(k) else -1, 0 if (k == w - 1 and rem > 0 and in_b(0)) else -1)
+                prv(-1, k + 1 if k + 1 < total and in_f(k + 1) else -1)
+            for j in range(rem):
+                k = w + j
+                fwd(k)
+                bwd(j)
+                nxt(k if out_f(k) else -1, j + 1 if j + 1 < total and in_b(j + 1) else -1)
+                prv(j if out_b(j) else -1, k + 1 if k + 1 < total and in_f(k + 1) else -1)
+            if rem == 0 and in_b(0):
+                nxt(-1, 0)
+            for j in range(rem, total):
+                bwd(j)
+                nxt(-1, j + 1 if j + 1 < total and in_b(j + 1) else -1)
+                prv(j if out_b(j) else -1, -1)
+        elif sched == "1f1b":
+            w = min(S - s - 1, mb)
+            steady = mb - w
+            for i in range(w):
+                prv(-1, i) if s > 0 else None
+                fwd(i)
+                nxt(i, -1) if s < S - 1 else None
+            if steady > 0 and s > 0:
+                prv(-1, w)
+            for j in range(steady):
+                i = w + j
+                fwd(i)
+                nxt(i, j) if s < S - 1 else None
+                bwd(j)
+                prv(j, i + 1 if j + 1 < steady else -1) if s > 0 else None
+            for j in range(steady, mb):
+                nxt(-1, j) if s < S - 1 else None
+                bwd(j)
+                prv(j, -1) if s > 0 else None
+        else:  # gpipe
+            for i in range(mb):
+                prv(-1, i) if s > 0 else None
+                fwd(i)
+                nxt(i, -1) if s < S - 1 else None
+            for j in range(mb):
+                nxt(-1, j) if s < S - 1 else None
+                bwd(j)
+                prv(j, -1) if s > 0 else None
+    return streams
+
+
+def simulate(streams) -> Tuple[float, List[Tuple[int, str]]]:
+    """Returns (makespan, streams left unfinished = deadlock)."""
+    posted: Dict[tuple, int] = {}
+    for key, ops in streams.items():
+        for o in ops:
+            for kind, d, peer in o.get("p2p", []):
+                ch = (key[0], peer, d) if kind == "send" else (peer, key[0], d)
+                n = posted.get((ch, kind), 0)
+                o.setdefault("tags", []).append((ch, kind, n))
+                posted[(ch, kind)] = n + 1
+    done: Dict[tuple, float] = {}
+    heads = {k: 0 for k in streams}
+    free = {k: 0.0 for k in streams}
+    t_end, progress = 0.0, True
+    while progress:
+        progress = False
+        ready = {}
+        for key, ops in streams.items():
+            if heads[key] < len(ops):
+                o = ops[heads[key]]
+                if all(w in done for w in o["waits"]):
+                    ready[key] = max([free[key]] + [done[w] for w in o["waits"]])
+        for key in ready:
+            group, todo, ok = {key}, [key], True
+            while todo and ok:
+                k1 = todo.pop()
+                for ch, kind, n in streams[k1][heads[k1]].get("tags", []):
+                    other = "recv" if kind == "send" else "send"
+                    hit = [k2 for k2 in ready if (ch, other, n) in streams[k2][heads[k2]].get("tags", [])]
+                    if not hit:
+                        ok = False
+                        break
+                    for k2 in hit:
+                        if k2 not in group:
+                            group.add(k2)
+                            todo.append(k2)
+            if not ok:
+                continue
+            t = max(ready[k] for k in group)
+            for k in group:
+                o = streams[k][heads[k]]
+                fin = t + o["dur"]
+                for e in o["rec"]:
+                    done[e] = fin
+                free[k] = fin
+                heads[k] += 1
+                t_end = max(t_end, fin)
+            progress = True
+            break
+    return t_end, [k for k in streams if heads[k] < len(streams[k])]
+
+
+def floor(S: int, mb: int, V: int, f: float, b: float) -> float:
+    """The driver's compute floor (compute_floor_us): (mb + (S-1)/V)(f_mb + b_mb), f/b per microbatch."""
+    return (mb + (S - 1) / V) * (f + b)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--stages", type=int, default=4)
+    ap.add_argument("--microbatches", type=int, default=8)
+    ap.add_argument("--virtual", type=int, default=2)
+    ap.add_argument("--fwd", type=float, default=1.0, help="forward time of one microbatch on one stage")
+    ap.add_argument("--bwd", type=float, default=2.0)
+    a = ap.parse_args(argv)
+    for sched, V in (("gpipe", 1), ("1f1b", 1), ("interleaved", a.virtual)):
+        t, stuck = simulate(build(a.stages, a.microbatches, V, a.fwd, a.bwd, sched))
+        print(f"{sched:12s} V={V}: makespan {t:.3f}  floor {floor(a.stages, a.microbatches, V, a.fwd, a.bwd):.3f}"
+              + (f"  DEADLOCK {stuck[:4]}" if stuck else ""))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

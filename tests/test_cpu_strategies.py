@@ -357,3 +357,20 @@ def test_sequence_parallel(prog, model, params, data_dir):
         assert c["tp_allgather"]["ops"] == rb["comm"]["tp_allreduce"]["ops"]
         assert c["tp_allgather"]["bytes_per_op"] == -(-tp // T) * T * 2
         assert len(r["tp_comm_time"]) == len(rb["tp_comm_time"])
+
+
+@pytest.mark.parametrize("w,S,mb,V", [(2, 2, 2, 2), (4, 2, 4, 2), (2, 2, 4, 3), (4, 4, 4, 3), (4, 4, 8, 2),
+                                      (8, 4, 4, 2), (1, 1, 2, 4)])
+def test_interleaved_1f1b(w, S, mb, V, data_dir):
+    """--pp-schedule interleaved (extension): V model chunks per stage, wrap link, bubble / V."""
+    d = run(w, "hybrid_2d", "tiny_deep_8_bfloat16", S, mb, data_dir, "-w", 1, "-r", 2, "--pp-schedule", "interleaved",
+            "--pp-virtual", V)
+    g = d["global"]
+    assert g["pp_schedule"] == "interleaved" and g["pp_virtual_stages"] == V
+    f_mb, b_mb = 2.0 / S / mb, 4.0 / S / mb  # ms (tiny tables: fwd 2 ms, bwd 4 ms)
+    floor = (mb + (S - 1) / V) * (f_mb + b_mb)
+    assert g["dlnb"]["iteration"]["compute_floor_ms"] == pytest.approx(floor)
+    for r in d["ranks"]:
+        assert len(r["pp_comm_time"]) == 2 * 2 * mb * V  # one per chunk forward / backward, 2 runs
+        for rt in r["runtimes"]:
+            assert rt * 1e3 >= floor * 0.98
