@@ -133,8 +133,15 @@ def build(S: int, mb: int, V: int, f: float, b: float, sched: str) -> Dict[Tuple
     return streams
 
 
-def simulate(streams) -> Tuple[float, List[Tuple[int, str]]]:
-    """Returns (makespan, streams left unfinished = deadlock)."""
+def simulate(streams, semantics: str = "rendezvous") -> Tuple[float, List[Tuple[int, str]]]:
+    """Returns (makespan, streams left unfinished = deadlock).
+
+    semantics: "rendezvous" (NCCL/RCCL-like and the strictest: a group completes only when every matching
+    operation's group sits at the head of its stream) or "buffered" (the xgmi / shared-memory backends:
+    a send needs only the receiver to have consumed message seq-2 of its channel, a receive needs the
+    matching send done, and a group's operations run one after the other in issue order)."""
+    if semantics == "buffered":
+        return _simulate_buffered(streams)
     posted: Dict[tuple, int] = {}
     for key, ops in streams.items():
         for o in ops:
@@ -182,6 +189,63 @@ def simulate(streams) -> Tuple[float, List[Tuple[int, str]]]:
                 t_end = max(t_end, fin)
             progress = True
             break
+    return t_end, [k for k in streams if heads[k] < len(streams[k])]
+
+
+def _simulate_buffered(streams, slots: int = 2) -> Tuple[float, List[Tuple[int, str]]]:
+    seq = {}
+    for key, ops in streams.items():
+        lst = []
+        for o in ops:  # a group becomes its operations, in issue order (sends first, as the backends do)
+            p2p = o.get("p2p")
+            if not p2p:
+                lst.append(o)
+                continue
+            order = sorted(range(len(p2p)), key=lambda i: p2p[i][0] != "send")
+            for n, i in enumerate(order):
+                kind, d, peer = p2p[i]
+                ch = (key[0], peer, d) if kind == "send" else (peer, key[0], d)
+                m = seq.get((ch, kind), 0)
+                seq[(ch, kind)] = m + 1
+                lst.append({"dur": 0.0, "waits": o["waits"] if n == 0 else [], "rec": [o["rec"][i]],
+                            "msg": (ch, kind, m)})
+        streams_key = key
+        seq_streams = lst
+        streams = dict(streams)
+        streams[streams_key] = seq_streams
+    sent: Dict[tuple, float] = {}
+    consumed: Dict[tuple, float] = {}
+    done: Dict[tuple, float] = {}
+    heads = {k: 0 for k in streams}
+    free = {k: 0.0 for k in streams}
+    t_end, progress = 0.0, True
+    while progress:
+        progress = False
+        for key, ops in streams.items():
+            while heads[key] < len(ops):
+                o = ops[heads[key]]
+                if not all(w in done for w in o["waits"]):
+                    break
+                t = max([free[key]] + [done[w] for w in o["waits"]])
+                if "msg" in o:
+                    ch, kind, m = o["msg"]
+                    if kind == "send":
+                        if m >= slots and (ch, m - slots) not in consumed:
+                            break
+                        t = max(t, consumed.get((ch, m - slots), 0.0))
+                        sent[(ch, m)] = t
+                    else:
+                        if (ch, m) not in sent:
+                            break
+                        t = max(t, sent[(ch, m)])
+                        consumed[(ch, m)] = t
+                fin = t + o["dur"]
+                for e in o["rec"]:
+                    done[e] = fin
+                free[key] = fin
+                heads[key] += 1
+                t_end = max(t_end, fin)
+                progress = True
     return t_end, [k for k in streams if heads[k] < len(streams[k])]
 
 

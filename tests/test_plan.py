@@ -134,12 +134,14 @@ def test_plan_4d_and_cp(stats):
     assert uly.messages[0].op == "alltoall" and uly.messages[0].calls_per_iter == 64
 
 
+@pytest.mark.parametrize("semantics", ["rendezvous", "buffered"])
 @pytest.mark.parametrize("sched,V", [("gpipe", 1), ("1f1b", 1), ("interleaved", 2), ("interleaved", 3)])
 @pytest.mark.parametrize("S,mb", [(1, 2), (2, 2), (2, 4), (3, 6), (4, 4), (4, 8), (8, 8), (8, 16)])
-def test_schedule_model_no_deadlock_and_floor(sched, V, S, mb):
-    """The enqueue order of every pipeline schedule (model of strategy_pipeline.cpp) never deadlocks and
-    reaches the driver's compute floor when links cost nothing."""
+def test_schedule_model_no_deadlock_and_floor(sched, V, S, mb, semantics):
+    """The enqueue order of every pipeline schedule (model of strategy_pipeline.cpp) never deadlocks - with
+    RCCL-like rendezvous groups or the xgmi / shared-memory backends' buffered sends - and reaches the
+    driver's compute floor when links cost nothing."""
     from dlnetbench_amd.parallel import schedule_sim as sim
-    t, stuck = sim.simulate(sim.build(S, mb, V, 1.0, 2.0, sched))
+    t, stuck = sim.simulate(sim.build(S, mb, V, 1.0, 2.0, sched), semantics)
     assert not stuck
     assert t == pytest.approx(sim.floor(S, mb, V, 1.0, 2.0))
