@@ -128,7 +128,7 @@ def fsdp_dataframes(doc: dict, job_vars: Optional[dict] = None, network: str = "
 
 
 def hybrid_dataframe(doc: dict, network: str = "mi355x"):
-    """One row per rank x run for dp_pp / dp_pp_tp / dp_pp_ep sections."""
+    """One row per rank x run for dp_pp / dp_pp_tp / dp_pp_ep / dp_pp_tp_ep sections."""
     import pandas as pd
     g = doc["global"]
     rows = []
@@ -144,6 +144,23 @@ def hybrid_dataframe(doc: dict, network: str = "mi355x"):
                 if k in r and r[k]:
                     per = len(r[k]) // runs
                     row[k] = sum(r[k][i * per:(i + 1) * per])
+            rows.append(row)
+    return pd.DataFrame(rows)
+
+
+def cp_dataframe(doc: dict, network: str = "mi355x"):
+    """One row per rank x run for dp_cp sections (hybrid_cp: per-iteration CP / DP communication sums)."""
+    import pandas as pd
+    g = doc["global"]
+    rows = []
+    for r in doc["ranks"]:
+        for i, rt in enumerate(r["runtimes"]):
+            row = {"network": network, "section": doc["section"], "model_name": g["model_name"],
+                   "world_size": g["world_size"], "num_cp_shards": g["num_cp_shards"], "cp_algo": g["cp_algo"],
+                   "dp_size": g["dp_size"], "rank": r["rank"], "cp_id": r.get("cp_id"), "run": i, "runtime": rt}
+            for k in ("cp_comm_time", "cp_exposed_time", "dp_comm_time", "dp_exposed_time"):
+                v = r.get(k) or []
+                row[k] = v[i] if i < len(v) else 0.0
             rows.append(row)
     return pd.DataFrame(rows)
 
@@ -179,6 +196,8 @@ def main(argv=None) -> int:
             frames.append(dp_dataframe(d))
         elif d["section"] == "fsdp":
             frames.append(fsdp_dataframes(d)[0])
+        elif d["section"] == "dp_cp":
+            frames.append(cp_dataframe(d))
         else:
             frames.append(hybrid_dataframe(d))
         print(json.dumps(summary(d)))

@@ -63,6 +63,17 @@ def test_report_dataframes(tmp_path, bindir, data_dir):
     assert {"runtime", "barrier_time", "energy_consumed", "msg_size_avg_bytes"} <= set(df.columns)
     s = report.summary(doc)
     assert s["busbw_GBps"]["allreduce"] > 0
+    # extensions: context parallel and 4-D sections
+    code, outs = launch.launch(4, [os.path.join(bindir, "hybrid_cp"), "tiny_dense_8_bfloat16", "2", data_dir, "--quiet",
+                                   "-w", "0", "-r", "2"], timeout=60, capture=True)
+    assert code == 0
+    df = report.cp_dataframe(report.parse_output(outs[0])["dp_cp"])
+    assert len(df) == 4 * 2 and {"cp_comm_time", "cp_exposed_time", "dp_exposed_time", "cp_id"} <= set(df.columns)
+    code, outs = launch.launch(4, [os.path.join(bindir, "hybrid_4d"), "tiny_moe_8_bfloat16", "1", "2", "2", "2",
+                                   data_dir, "--quiet", "-w", "0", "-r", "2"], timeout=60, capture=True)
+    assert code == 0
+    df = report.hybrid_dataframe(report.parse_output(outs[0])["dp_pp_tp_ep"])
+    assert len(df) == 4 * 2 and {"tp_comm_time", "ep_comm_time"} <= set(df.columns)
 
 
 def test_plots(tmp_path, bindir):
