@@ -44,15 +44,16 @@ bool gemm_shape_ok(int M, int N, int K, DType in_t);
 // waves selects the variant: 8 = 8 waves (2 per SIMD, 128x64 per wave)
 // double buffered, 2 = the same with software-pipelined fragment reads
 // (bf16), 1 = 8 waves with a 3-deep A ring (160 KiB LDS), 4 = 4 waves (1 per
-// SIMD, 128x128 per wave); 0 = the default: 3 where it applies (>= 2
-// K-tiles), else 2 for bf16 / 8 for fp8 (ring if DLNB_GEMM_RING=1, 4 waves if
-// DLNB_GEMM_WAVES=4).
+// SIMD, 128x128 per wave), 6 = 8-phase with balanced fragment reads (bf16;
+// even K-tile counts, else 3); 0 = the default: 6 (bf16) / 3 (fp8) where it
+// applies (>= 2 K-tiles), else 2 for bf16 / 8 for fp8 (ring if
+// DLNB_GEMM_RING=1, 4 waves if DLNB_GEMM_WAVES=4).
 // 3 = the 8-phase ping-pong schedule (gemm_8phase.hip; needs >= 2 K-tiles).
 void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
              void* stream, int waves = 0);
 bool gemm_8phase_shape_ok(int M, int N, int K, DType in_t);
 void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
-                    void* stream);
+                    void* stream, bool balanced = false);
 void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
                              uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
                              uint64_t* tstart);

@@ -159,64 +159,89 @@ struct Deadline {
 };
 
 // Phase Q of K-tile v. Staging schedule (G = half-tile issued in the phase):
-//   Q0: B1(v+1)  Q1: A1(v+1)  Q2: A0(v+2)  Q3: B0(v+2)
+//   Q0: B1(v+1)  Q1: A1(v+1)  Q2: A0(v+2)  Q3: B0(v+2)          (BAL = false)
+//   Q0: B1(v+1)  Q1: A1(v+1)  Q2: B0(v+2)  Q3: A0(v+2)          (BAL = true)
 // VM = vmcnt after the issue (8 in steady state: retires the half-tile
 // issued four phases earlier); STAGE = whether the phase's G exists.
+// BAL ("balanced"): fragment reads per phase 8/4/8/4 instead of 12/4/8/0 -
+// phase 3 reads the NEXT K-tile's B0 fragments into the register set the
+// current tile used for B1, so the two B sets swap roles every K-tile (PAR =
+// v & 1; B0(v+1) is staged one phase earlier so it is retired by phase 2).
+// Every buffer slot is still restaged >= 2 phases after its last read.
 // Returns (DL, phase 3) whether the deadline has passed.
-template <bool FP8, bool DL, int Q, int VM, bool STAGE>
-__device__ __forceinline__ bool phase(const Ctx& c, int v, Frags<FP8>& f, f32x4 (&acc)[2][2][4][2], const Deadline& d,
-                                      uint64_t& now) {
+template <bool FP8, bool DL, bool BAL, int Q, int VM, bool STAGE, typename AF, typename BF>
+__device__ __forceinline__ bool phase(const Ctx& c, int v, AF& fa, BF& b0r, BF& b1r, f32x4 (&acc)[2][2][4][2],
+                                      const Deadline& d, uint64_t& now, bool has_next) {
+  // b0r: this K-tile's B0 fragments; b1r: its B1 fragments (BAL: the next
+  // K-tile's B0 is read into them in phase 3)
   const char* cur = c.smem + (v & 1) * kBuf;
   if constexpr (Q == 0) {
-    read_frags<FP8, 2>(cur + kB0 * kHalf, c.wc * 32, c.r16, c.h, f.bx);
-    __builtin_amdgcn_sched_barrier(0);
-    read_frags<FP8, 4>(cur + kA0 * kHalf, c.wr * 64, c.r16, c.h, f.a);
+    if constexpr (!BAL) {
+      read_frags<FP8, 2>(cur + kB0 * kHalf, c.wc * 32, c.r16, c.h, b0r);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    read_frags<FP8, 4>(cur + kA0 * kHalf, c.wr * 64, c.r16, c.h, fa);
   } else if constexpr (Q == 1) {
-    read_frags<FP8, 2>(cur + kB1 * kHalf, c.wc * 32, c.r16, c.h, f.by);
+    read_frags<FP8, 2>(cur + kB1 * kHalf, c.wc * 32, c.r16, c.h, b1r);
   } else if constexpr (Q == 2) {
-    read_frags<FP8, 4>(cur + kA1 * kHalf, c.wr * 64, c.r16, c.h, f.a);
+    read_frags<FP8, 4>(cur + kA1 * kHalf, c.wr * 64, c.r16, c.h, fa);
     // the clock is read one phase before its use, so its (scalar-memory)
     // latency does not stall wave 0 in front of a barrier
     if constexpr (DL) now = __builtin_amdgcn_s_memrealtime();
-  } else if constexpr (DL) {
+  } else {
+    if constexpr (BAL) {
+      if (has_next) read_frags<FP8, 2>(c.smem + ((v + 1) & 1) * kBuf + kB0 * kHalf, c.wc * 32, c.r16, c.h, b1r);
+    }
+    if constexpr (DL) {
     if (d.tid == 0) {
       const uint64_t el = (now - d.t0) & ((1ull << 48) - 1);
       d.flag[v & 1] = el >= d.ticks || el >= d.slice_end;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
+    }
   }
   if constexpr (STAGE) {
     if constexpr (Q == 0) stage(c, v + 1, kB1);
     if constexpr (Q == 1) stage(c, v + 1, kA1);
-    if constexpr (Q == 2) stage(c, v + 2, kA0);
-    if constexpr (Q == 3) stage(c, v + 2, kB0);
+    if constexpr (Q == 2) stage(c, v + 2, BAL ? kB0 : kA0);
+    if constexpr (Q == 3) stage(c, v + 2, BAL ? kA0 : kB0);
   }
   wait_vm<VM>();
   raw_barrier();
   bool stop = false;
   if constexpr (DL && Q == 3) stop = __builtin_amdgcn_readfirstlane(d.flag[v & 1]) != 0;
   __builtin_amdgcn_s_setprio(1);
-  if constexpr (Q == 0) mfma_quadrant(acc[0][0], f.a, f.bx);
-  if constexpr (Q == 1) mfma_quadrant(acc[0][1], f.a, f.by);
-  if constexpr (Q == 2) mfma_quadrant(acc[1][1], f.a, f.by);
-  if constexpr (Q == 3) mfma_quadrant(acc[1][0], f.a, f.bx);
+  if constexpr (Q == 0) mfma_quadrant(acc[0][0], fa, b0r);
+  if constexpr (Q == 1) mfma_quadrant(acc[0][1], fa, b1r);
+  if constexpr (Q == 2) mfma_quadrant(acc[1][1], fa, b1r);
+  if constexpr (Q == 3) mfma_quadrant(acc[1][0], fa, b0r);
   __builtin_amdgcn_s_setprio(0);
   raw_barrier();
   return stop;
 }
 
-template <bool FP8, bool DL, int V0, int V1, int V2, int V3, bool S01, bool S23>
-__device__ __forceinline__ bool ktile(const Ctx& c, int v, Frags<FP8>& f, f32x4 (&acc)[2][2][4][2], const Deadline& d) {
+template <bool FP8, bool DL, bool BAL, int PAR, int V0, int V1, int V2, int V3, bool S01, bool S23>
+__device__ __forceinline__ bool ktile(const Ctx& c, int v, Frags<FP8>& f, f32x4 (&acc)[2][2][4][2], const Deadline& d,
+                                      bool has_next = true) {
   uint64_t now = 0;
-  phase<FP8, DL, 0, V0, S01>(c, v, f, acc, d, now);
-  phase<FP8, DL, 1, V1, S01>(c, v, f, acc, d, now);
-  phase<FP8, DL, 2, V2, S23>(c, v, f, acc, d, now);
-  return phase<FP8, DL, 3, V3, S23>(c, v, f, acc, d, now);
+  auto& b0r = (BAL && PAR == 1) ? f.by : f.bx;
+  auto& b1r = (BAL && PAR == 1) ? f.bx : f.by;
+  phase<FP8, DL, BAL, 0, V0, S01>(c, v, f.a, b0r, b1r, acc, d, now, has_next);
+  phase<FP8, DL, BAL, 1, V1, S01>(c, v, f.a, b0r, b1r, acc, d, now, has_next);
+  phase<FP8, DL, BAL, 2, V2, S23>(c, v, f.a, b0r, b1r, acc, d, now, has_next);
+  return phase<FP8, DL, BAL, 3, V3, S23>(c, v, f.a, b0r, b1r, acc, d, now, has_next);
+}
+
+// The last two K-tiles (v = nk-2 stages only tile nk-1, v = nk-1 drains).
+template <bool FP8, bool DL, bool BAL, int PAR>
+__device__ __forceinline__ bool tail(const Ctx& c, int v, Frags<FP8>& f, f32x4 (&acc)[2][2][4][2], const Deadline& d) {
+  if (ktile<FP8, DL, BAL, PAR, 8, 8, 6, 4, true, false>(c, v, f, acc, d)) return true;
+  return ktile<FP8, DL, BAL, 1 - PAR, 2, 0, 0, 0, false, false>(c, v + 1, f, acc, d, false);
 }
 
 // One 256 x 256 tile of C. Returns false if the deadline stopped it (no
 // store; every staged load has been waited for).
-template <bool FP8, bool DL>
+template <bool FP8, bool DL, bool BAL>
 __device__ __forceinline__ bool tile(Ctx& c, const char* __restrict__ A, const char* __restrict__ B,
                                      __bf16* __restrict__ C, int M, int N, int K, int ldc, int b, const Deadline& d) {
   const int nt_m = M / kT, nt_n = N / kT;
@@ -242,22 +267,32 @@ __device__ __forceinline__ bool tile(Ctx& c, const char* __restrict__ A, const c
         for (int j = 0; j < 2; ++j) acc[qm][qn][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   Frags<FP8> f;
 
-  // Prologue, in the steady-state issue order: A0(0) B0(0) B1(0) A1(0) A0(1) B0(1).
-  stage(c, 0, kA0);
-  stage(c, 0, kB0);
+  // Prologue, in the steady-state issue order: A0(0) B0(0) B1(0) A1(0) A0(1) B0(1)
+  // (BAL: B0(0) A0(0) B1(0) A1(0) B0(1) A0(1)).
+  stage(c, 0, BAL ? kB0 : kA0);
+  stage(c, 0, BAL ? kA0 : kB0);
   stage(c, 0, kB1);
   stage(c, 0, kA1);
-  stage(c, 1, kA0);
-  stage(c, 1, kB0);
+  stage(c, 1, BAL ? kB0 : kA0);
+  stage(c, 1, BAL ? kA0 : kB0);
   wait_vm<8>();  // A0(0), B0(0) landed
   raw_barrier();
+  if constexpr (BAL) read_frags<FP8, 2>(c.smem + kB0 * kHalf, c.wc * 32, c.r16, c.h, f.bx);  // B0(0), PAR 0
   if (c.wr == 1) raw_barrier();  // wave row 1 runs one barrier behind
 
   bool stop = false;
   int v = 0;
-  for (; v < nk - 2 && !stop; ++v) stop = ktile<FP8, DL, 8, 8, 8, 8, true, true>(c, v, f, acc, d);
-  if (!stop) stop = ktile<FP8, DL, 8, 8, 6, 4, true, false>(c, v, f, acc, d);  // v = nk-2: stages only tile nk-1
-  if (!stop) stop = ktile<FP8, DL, 2, 0, 0, 0, false, false>(c, v + 1, f, acc, d);  // v = nk-1: drains
+  if constexpr (!BAL) {
+    for (; v < nk - 2 && !stop; ++v) stop = ktile<FP8, DL, false, 0, 8, 8, 8, 8, true, true>(c, v, f, acc, d);
+    if (!stop) stop = tail<FP8, DL, false, 0>(c, v, f, acc, d);
+  } else {
+    // register roles alternate per K-tile: unrolled by two (nk even, host-checked)
+    for (; v < nk - 2 && !stop; v += 2) {
+      stop = ktile<FP8, DL, true, 0, 8, 8, 8, 8, true, true>(c, v, f, acc, d);
+      if (!stop) stop = ktile<FP8, DL, true, 1, 8, 8, 8, 8, true, true>(c, v + 1, f, acc, d);
+    }
+    if (!stop) stop = tail<FP8, DL, true, 0>(c, v, f, acc, d);
+  }
   if (c.wr == 0) raw_barrier();  // re-align the barrier counts of the two rows
   if constexpr (DL) {
     if (stop) {  // partial tile: the stand-in result is not needed
@@ -292,7 +327,7 @@ __device__ __forceinline__ bool tile(Ctx& c, const char* __restrict__ A, const c
 // compute with the contract of gemm_tn_256_kernel's deadline mode
 // (kernels.hip): grid <= resident blocks walks the tiles round-robin and
 // stops min(ticks, slice_end) after t0, agreed per epoch through *slot.
-template <bool FP8, bool DL>
+template <bool FP8, bool DL, bool BAL = false>
 __global__ void __launch_bounds__(512, 1)
     gemm_8phase_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
                        int K, int lda, int ldb, int ldc, uint64_t* __restrict__ slot, uint32_t epoch, uint64_t ticks,
@@ -313,7 +348,7 @@ __global__ void __launch_bounds__(512, 1)
   const int T = (M / kT) * (N / kT);
   Deadline d{0, ticks, slice_end, (lds_flag_t*)(smem + 2 * kBuf), tid};
   if constexpr (!DL) {
-    tile<FP8, false>(c, A, B, C, M, N, K, ldc, xcd_remap(blockIdx.x, T), d);
+    tile<FP8, false, BAL>(c, A, B, C, M, N, K, ldc, xcd_remap(blockIdx.x, T), d);
   } else {
     constexpr uint64_t kMask48 = (1ull << 48) - 1;
     if (tid == 0) {
@@ -331,7 +366,7 @@ __global__ void __launch_bounds__(512, 1)
       d.t0 = cur & kMask48;  // only thread 0 reads the clock
     }
     for (int round = 0;; ++round)
-      if (!tile<FP8, true>(c, A, B, C, M, N, K, ldc, xcd_remap((blockIdx.x + round * gridDim.x) % T, T), d)) return;
+      if (!tile<FP8, true, BAL>(c, A, B, C, M, N, K, ldc, xcd_remap((blockIdx.x + round * gridDim.x) % T, T), d)) return;
   }
 }
 
@@ -343,19 +378,30 @@ bool gemm_8phase_shape_ok(int M, int N, int K, DType in_t) {
 }
 
 void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
-                    void* stream) {
+                    void* stream, bool balanced) {
   DLNB_REQUIRE(gemm_8phase_shape_ok(M, N, K, in_t), "gemm 8-phase: unsupported shape M=" << M << " N=" << N << " K=" << K);
   const int tiles = (M / kT) * (N / kT);
   hipStream_t st = static_cast<hipStream_t>(stream);
   auto* a = static_cast<const char*>(A);
   auto* b = static_cast<const char*>(B);
   auto* cc = static_cast<__bf16*>(C);
-  if (in_t == DType::FP8_E4M3)
-    hipLaunchKernelGGL((gemm_8phase_kernel<true, false>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc, nullptr,
-                       0u, 0ull, 0ull, nullptr);
-  else
-    hipLaunchKernelGGL((gemm_8phase_kernel<false, false>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc, nullptr,
-                       0u, 0ull, 0ull, nullptr);
+  // the balanced schedule is unrolled by two K-tiles: even K-tile counts only
+  balanced = balanced && ((static_cast<size_t>(K) * dtype_size(in_t) / kRB) % 2 == 0);
+  if (in_t == DType::FP8_E4M3) {
+    if (balanced)
+      hipLaunchKernelGGL((gemm_8phase_kernel<true, false, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc,
+                         nullptr, 0u, 0ull, 0ull, nullptr);
+    else
+      hipLaunchKernelGGL((gemm_8phase_kernel<true, false>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc, nullptr,
+                         0u, 0ull, 0ull, nullptr);
+  } else {
+    if (balanced)
+      hipLaunchKernelGGL((gemm_8phase_kernel<false, false, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc,
+                         nullptr, 0u, 0ull, 0ull, nullptr);
+    else
+      hipLaunchKernelGGL((gemm_8phase_kernel<false, false>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc, nullptr,
+                         0u, 0ull, 0ull, nullptr);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 8-phase launch failed: " << hipGetErrorString(e));
 }

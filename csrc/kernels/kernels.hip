@@ -632,11 +632,11 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
                    reinterpret_cast<uintptr_t>(C) % 8 == 0,
                "gemm_tn: misaligned base pointers");
   const int tiles = (M / kTile) * (N / kTile);
-  DLNB_REQUIRE(waves == 0 || waves == 1 || waves == 2 || waves == 3 || waves == 4 || waves == 8,
-               "gemm_tn: variant must be 0, 1, 2, 3, 4 or 8");
-  if (waves == 0 && gemm_8phase_enabled()) waves = 3;
-  if (waves == 3 && gemm_8phase_shape_ok(M, N, K, in_t)) {  // (one K-tile: falls back)
-    gemm_tn_8phase(A, B, C, M, N, K, lda, ldb, ldc, in_t, stream);
+  DLNB_REQUIRE(waves == 0 || waves == 1 || waves == 2 || waves == 3 || waves == 4 || waves == 6 || waves == 8,
+               "gemm_tn: variant must be 0, 1, 2, 3, 4, 6 or 8");
+  if (waves == 0 && gemm_8phase_enabled()) waves = in_t == DType::BF16 ? 6 : 3;  // bf16: balanced reads
+  if ((waves == 3 || waves == 6) && gemm_8phase_shape_ok(M, N, K, in_t)) {  // (one K-tile: falls back)
+    gemm_tn_8phase(A, B, C, M, N, K, lda, ldb, ldc, in_t, stream, waves == 6);
     return;
   }
   if (waves == 0) {
@@ -645,7 +645,7 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
     const int w = gemm_default_waves();
     waves = gemm_ring_enabled() ? 1 : w == 4 ? 4 : in_t == DType::BF16 ? 2 : 8;
   }
-  if (waves == 3) waves = in_t == DType::BF16 ? 2 : 8;
+  if (waves == 3 || waves == 6) waves = in_t == DType::BF16 ? 2 : 8;
   dispatch_gemm<false>(waves, in_t, tiles, A, B, C, M, N, K, lda, ldb, ldc, nullptr, 0u, 0ull, 0ull, S(stream));
 }
 

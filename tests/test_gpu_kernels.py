@@ -15,7 +15,7 @@ def need_gpu():
 from dlnetbench_amd.ops import gemm  # noqa: E402
 
 
-@pytest.mark.parametrize("waves", [0, 1, 2, 3, 8, 4])
+@pytest.mark.parametrize("waves", [0, 1, 2, 3, 6, 8, 4])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 512, 128), (512, 256, 1024), (768, 1280, 640),
                                    (2048, 1024, 4096)])
 def test_gemm_bf16_matches_torch(M, N, K, waves):
@@ -29,7 +29,7 @@ def test_gemm_bf16_matches_torch(M, N, K, waves):
     assert (c.float() - ref).abs().max().item() < tol
 
 
-@pytest.mark.parametrize("waves", [0, 3])
+@pytest.mark.parametrize("waves", [0, 3, 6])
 def test_gemm_bf16_identity_asymmetric(waves):
     # A = I picks rows of B: catches any row/column/quadrant swap in the C write.
     M = N = 256
@@ -42,7 +42,7 @@ def test_gemm_bf16_identity_asymmetric(waves):
 
 
 @pytest.mark.skipif(not hasattr(torch, "float8_e4m3fn"), reason="torch without float8")
-@pytest.mark.parametrize("waves", [0, 1, 2, 3, 8, 4])
+@pytest.mark.parametrize("waves", [0, 1, 2, 3, 6, 8, 4])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 512), (1024, 512, 2048)])
 def test_gemm_fp8_matches_torch(M, N, K, waves):
     g = torch.Generator(device="cuda").manual_seed(7 + M)
