@@ -17,7 +17,7 @@ from dlnetbench_amd.ops import gemm  # noqa: E402
 
 @pytest.mark.parametrize("waves", [0, 1, 2, 3, 6, 8, 4])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 512, 128), (512, 256, 1024), (768, 1280, 640),
-                                   (2048, 1024, 4096)])
+                                   (2048, 1024, 4096), (256, 256, 192), (512, 768, 320)])
 def test_gemm_bf16_matches_torch(M, N, K, waves):
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
