@@ -35,6 +35,7 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
@@ -104,9 +105,9 @@ __device__ __forceinline__ void read_frags(const char* half, int row0, int r16, 
 #pragma unroll
   for (int i = 0; i < NF; ++i) {
     const int row = row0 + i * 16 + r16;
-    const int4 lo = *reinterpret_cast<const int4*>(half + swz(row, 2 * h));
-    const int4 hi = *reinterpret_cast<const int4*>(half + swz(row, 2 * h + 1));
-    f[i] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    const i32x4 lo = *reinterpret_cast<const i32x4*>(half + swz(row, 2 * h));
+    const i32x4 hi = *reinterpret_cast<const i32x4*>(half + swz(row, 2 * h + 1));
+    f[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);  // register concat, no element moves
   }
 }
 

@@ -5,7 +5,7 @@
     commtest [-n N] <args...>
                       exact check / bandwidth sweep of a comm backend (dlnb commtest)
     launch -n N <program ...>   generic N-rank launcher (utils/launch.py)
-    sweep | plots | report | plan | roofline | measure | gemm-bench | clock-check |
+    sweep | plots | report | plan | schedule-sim | roofline | measure | gemm-bench | clock-check |
     prof-summary | download-models
                       the tools, each with its own --help
 
@@ -28,6 +28,7 @@ TOOLS = {
     "plots": "dlnetbench_amd.tools.plots",
     "report": "dlnetbench_amd.utils.report",
     "plan": "dlnetbench_amd.parallel.plan",
+    "schedule-sim": "dlnetbench_amd.parallel.schedule_sim",
     "roofline": "dlnetbench_amd.models.roofline",
     "measure": "dlnetbench_amd.models.measure",
     "gemm-bench": "dlnetbench_amd.tools.gemm_bench",
