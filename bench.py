@@ -137,7 +137,8 @@ def main() -> int:
         "scaling": "weak",
         "vs_baseline": round(ms / BASELINE_MS, 4) if a.model == DEFAULT_MODEL else None,
         "dtype": "bf16",
-        "data": "synthetic (random-init buffers; compute = MFMA GEMM stand-in bounded to the table durations)",
+        "data": ("synthetic (random-init buffers; compute = MFMA GEMM stand-in bounded to the table durations)"
+                 if a.compute == "gemm" else f"synthetic (random-init buffers; compute mode {a.compute})"),
         "config": {
             "model": a.model,
             "global_batch": int(g["local_batch_size"]) * world,
