@@ -374,3 +374,32 @@ def test_interleaved_1f1b(w, S, mb, V, data_dir):
         assert len(r["pp_comm_time"]) == 2 * 2 * mb * V  # one per chunk forward / backward, 2 runs
         for rt in r["runtimes"]:
             assert rt * 1e3 >= floor * 0.98
+
+
+def _fails(n, prog, *args):
+    code, outs = launch.launch(n, [os.path.join(BIN, prog), *map(str, args), "--quiet"], timeout=60, capture=True)
+    return code, "".join(o or "" for o in outs)
+
+
+def test_extension_argument_checks(data_dir):
+    code, out = _fails(4, "hybrid_2d", "tiny_deep_8_bfloat16", 4, 2, data_dir, "--pp-schedule", "interleaved")
+    assert code != 0 and "num_microbatches 2 must be a multiple of num_stages 4" in out
+    code, out = _fails(2, "hybrid_2d", "tiny_dense_8_bfloat16", 2, 2, data_dir, "--pp-schedule", "interleaved",
+                       "--pp-virtual", 4)
+    assert code != 0 and "must be divisible by stages*virtual 8" in out
+    code, out = _fails(4, "hybrid_4d", "tiny_moe_8_bfloat16", 1, 2, 2, 2, data_dir, "--ep-overlap")
+    assert code != 0 and "--ep-overlap is not supported with tensor parallelism" in out
+    code, out = _fails(4, "hybrid_4d", "tiny_moe_8_bfloat16", 1, 2, 2, 3, data_dir)
+    assert code != 0
+    code, out = _fails(2, "hybrid_cp", "tiny_dense_8_bfloat16", 2, data_dir, "--cp-algo", "bogus")
+    assert code != 0 and "--cp-algo must be ring or ulysses" in out
+
+
+def test_extensions_other_wire_dtypes_and_reference_schedule(data_dir):
+    d = run(2, "dp", "tiny_dense_8_bfloat16", 3, data_dir, "-w", 0, "-r", 1, "--zero", 2, "--wire-dtype", "fp32")
+    assert d["global"]["param_allgather_msg_size_bytes"] == -(-333335 // 2) * 2 * 4
+    d = run(2, "hybrid_cp", "tiny_dense_8_bfloat16", 2, data_dir, "-w", 0, "-r", 1, "--schedule", "reference")
+    assert d["global"]["dlnb"]["schedule"] == "reference"
+    d = run(4, "hybrid_4d", "tiny_moe_8_bfloat16", 2, 2, 2, 1, data_dir, "-w", 0, "-r", 1, "--pp-schedule", "interleaved",
+            "--pp-virtual", 2)
+    assert d["global"]["pp_virtual_stages"] == 2
