@@ -35,7 +35,7 @@ for step in "$@"; do
     pmcfsdp)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       # counter collection serialises dispatches: eager enqueue, 20 ms slices
-      run pmc_fsdp 400 env DLNB_GEMM_SLICE_US=20000 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_fsdp -o fsdp -- python3 bench.py --steps 1 --warmup 0 --no-graph ;;
+      run pmc_fsdp 400 env DLNB_GEMM_SLICE_US=20000 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU_MFMA_MOPS_BF16 GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d gpurun_out/pmc_fsdp -o fsdp -- python3 bench.py --steps 1 --warmup 0 --no-graph ;;
     pmc)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       run pmc_gemm 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_gemm -o gemm -- python3 -m dlnetbench_amd.tools.gemm_bench --shapes 8192x14336x4096 --rounds 2 --iters 5 ;;
