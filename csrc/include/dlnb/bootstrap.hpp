@@ -37,17 +37,20 @@ class Store {
   virtual void finish() {}
 };
 
-// In-process store for world_size == 1.
+// In-process store: world_size == 1, or the rank threads of a loopback job.
 class LocalStore : public Store {
  public:
   void set(const std::string& key, const std::string& value) override;
   std::string get(const std::string& key) override;
   long long add(const std::string& key, long long delta) override;
+  // Every blocked and later get() throws (a rank thread of the job failed).
+  void abort(const std::string& why);
 
  private:
   std::mutex mu_;
   std::condition_variable cv_;
   std::map<std::string, std::string> kv_;
+  std::string aborted_;
 };
 
 // TCP store. The server side (rank 0) runs an accept thread plus one thread
@@ -109,11 +112,18 @@ class HostGroup {
 // Reads rank/world from the environment (DLNB_*, torchrun, OMPI, PMI, Slurm),
 // connects to (or hosts) the store and derives local rank from hostnames
 // when the launcher did not provide it.
+struct LoopbackHub;
 struct Bootstrap {
   RankInfo info;
   std::shared_ptr<Store> store;
   std::unique_ptr<HostGroup> world;
+  std::shared_ptr<LoopbackHub> hub;  // loopback backend: shared by the job's rank threads
 };
+
+// Rank `rank` of an in-process loopback job of `world` threads that share
+// `store` and `hub` (--backend loopback --ranks N).
+std::unique_ptr<Bootstrap> bootstrap_loopback(int rank, int world, std::shared_ptr<LocalStore> store,
+                                              std::shared_ptr<LoopbackHub> hub);
 
 // store_addr: "host:port" (empty = from env DLNB_STORE_ADDR, else
 // MASTER_ADDR:(MASTER_PORT+1), else 127.0.0.1:29600).

@@ -82,6 +82,23 @@ std::unique_ptr<CommFactory> make_shm_factory(HostGroup& world, Device& dev);
 // Own kernels over IPC-mapped peer windows (one node); see dlnb/xgmi.hpp.
 std::unique_ptr<CommFactory> make_xgmi_factory(HostGroup& world, Device& dev);
 
+// Loopback: N ranks as threads of one process on one device (GPU or CPU),
+// sharing one LoopbackHub. Collectives are issued by the last rank to
+// arrive, on its own stream, after waiting on every other rank's "ready"
+// event; the others wait on its "done" event. Host enqueue order therefore
+// orders every dependency, so no stream can wait on work queued behind it
+// even when all ranks' streams share the device's few hardware queues.
+struct LoopbackHub;
+std::shared_ptr<LoopbackHub> make_loopback_hub(int ranks, double timeout_s);
+// Wakes every rank blocked in the hub with an error (a rank thread failed).
+void loopback_abort(LoopbackHub& hub, const std::string& why);
+std::unique_ptr<CommFactory> make_loopback_factory(HostGroup& world, Device& dev, std::shared_ptr<LoopbackHub> hub);
+
+// Host-memory helpers of the CPU backends (multi-threaded for large sizes).
+// dst[i] = sum over srcs of src[i] (fp32 accumulation); dst may alias a src.
+void host_reduce_sum(DType t, void* dst, const std::vector<const char*>& srcs, size_t count);
+void host_copy(void* dst, const void* src, size_t bytes);
+
 // Bytes moved per rank for bus-bandwidth accounting (nccl-tests convention):
 // busbw = algbw * factor(kind, n).
 double busbw_factor(CollKind k, int n);

@@ -47,7 +47,8 @@ struct Options {
   bool help = false;
 
   // dlnb extensions
-  std::string backend = "auto";   // auto | rccl | cpu
+  std::string backend = "auto";   // auto | rccl | xgmi | cpu | loopback
+  int ranks = 2;                  // loopback: in-process ranks (threads) sharing one device
   std::string compute = "auto";   // auto | sleep | spin | gemm | flops
   std::string wire_dtype = "bf16";
   std::string compute_dtype = "auto";  // auto (from stats Dtype) | bf16 | fp8

@@ -78,5 +78,13 @@ void launch_send(const Peers& p, const char* buf, size_t bytes, int dst, size_t 
 void launch_recv(const Peers& p, char* buf, size_t bytes, int src, size_t off, uint32_t n, uint32_t target,
                  int blocks, void* stream);
 
+// Loopback backend (all ranks in one process on one device): for i < count,
+// dsts[d][i] = sum over s of srcs[s][i] (fp32 accumulation, one rounding;
+// ns == 1 is a bit-exact copy to nd destinations). In place safe: every
+// element is read from all sources before any destination is written.
+constexpr int kMaxLocal = 16;
+void launch_local_reduce(char* const* dsts, int nd, const char* const* srcs, int ns, size_t count, DType t,
+                         void* stream);
+
 }  // namespace xgmi
 }  // namespace dlnb

@@ -7,6 +7,8 @@
 // traffic at the same time. Reductions accumulate in fp32 and round once.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "dlnb/xgmi.hpp"
 
 #define DLNB_HIP_CHECK(expr)                                                       \
@@ -449,6 +451,56 @@ __global__ void __launch_bounds__(T) recv_kernel(Peers P, char* buf, size_t byte
   }
 }
 
+struct LocalArgs {
+  const char* src[kMaxLocal];
+  char* dst[kMaxLocal];
+  int ns, nd;
+  size_t count;  // elements
+};
+
+// Grid-stride over 16-B vectors (VEC: every pointer 16-B aligned), then the
+// element tail; a copy (ns == 1) moves raw vectors, no dtype round trip.
+template <DType D, bool VEC>
+__global__ void __launch_bounds__(T) local_reduce_kernel(LocalArgs a) {
+  using E = Elt<D>;
+  const size_t stride = static_cast<size_t>(gridDim.x) * T;
+  const size_t tid = static_cast<size_t>(blockIdx.x) * T + threadIdx.x;
+  const size_t nv = VEC ? a.count / E::N : 0;
+  for (size_t i = tid; i < nv; i += stride) {
+    uint4 v = V(a.src[0])[i];
+    if (a.ns > 1) {
+      float acc[E::N], f[E::N];
+      E::unpack(v, acc);
+      for (int s = 1; s < a.ns; ++s) {
+        E::unpack(V(a.src[s])[i], f);
+#pragma unroll
+        for (int k = 0; k < E::N; ++k) acc[k] += f[k];
+      }
+      v = E::pack(acc);
+    }
+    for (int d = 0; d < a.nd; ++d) V(a.dst[d])[i] = v;
+  }
+  const size_t es = sizeof(uint4) / E::N;
+  for (size_t i = nv * E::N + tid; i < a.count; i += stride) {
+    if (a.ns == 1) {
+      for (int d = 0; d < a.nd; ++d)
+        for (size_t b = 0; b < es; ++b) a.dst[d][i * es + b] = a.src[0][i * es + b];
+      continue;
+    }
+    float x = 0.f;
+    for (int s = 0; s < a.ns; ++s) x += E::ld(a.src[s], i);
+    for (int d = 0; d < a.nd; ++d) E::st(a.dst[d], i, x);
+  }
+}
+
+template <DType D>
+void local_reduce_typed(const LocalArgs& a, bool vec, int blocks, hipStream_t s) {
+  if (vec)
+    local_reduce_kernel<D, true><<<blocks, T, 0, s>>>(a);
+  else
+    local_reduce_kernel<D, false><<<blocks, T, 0, s>>>(a);
+}
+
 #define DLNB_XGMI_TYPED(KERNEL)                                                                       \
   switch (c.dtype) {                                                                                 \
     case DType::BF16: KERNEL<DType::BF16><<<blocks, T, 0, s>>>(p, c); break;                         \
@@ -482,6 +534,38 @@ void launch_coll(Op op, const Peers& p, const CollPiece& c, int blocks, void* st
     case Op::AllReduceTwoShot:
       DLNB_REQUIRE(c.bytes % 16 == 0, "xgmi: two-shot piece must be a multiple of 16 B");
       DLNB_XGMI_TYPED(ar2_kernel) break;
+  }
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
+void launch_local_reduce(char* const* dsts, int nd, const char* const* srcs, int ns, size_t count, DType t,
+                         void* stream) {
+  DLNB_REQUIRE(ns >= 1 && ns <= kMaxLocal && nd >= 1 && nd <= kMaxLocal,
+               "local reduce: " << ns << " sources / " << nd << " destinations (1.." << kMaxLocal << ")");
+  if (count == 0) return;
+  LocalArgs a{};
+  a.ns = ns;
+  a.nd = nd;
+  a.count = count;
+  bool vec = true;
+  for (int i = 0; i < ns; ++i) {
+    a.src[i] = srcs[i];
+    vec = vec && (reinterpret_cast<uintptr_t>(srcs[i]) & 15u) == 0;
+  }
+  for (int i = 0; i < nd; ++i) {
+    a.dst[i] = dsts[i];
+    vec = vec && (reinterpret_cast<uintptr_t>(dsts[i]) & 15u) == 0;
+  }
+  const size_t per_vec = 16 / dtype_size(t);
+  const size_t work = vec ? std::max<size_t>(1, count / per_vec) : count;
+  const int blocks = static_cast<int>(std::min<size_t>(2048, std::max<size_t>(1, (work + 4 * T - 1) / (4 * T))));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (t) {
+    case DType::BF16: local_reduce_typed<DType::BF16>(a, vec, blocks, s); break;
+    case DType::FP16: local_reduce_typed<DType::FP16>(a, vec, blocks, s); break;
+    case DType::FP32: local_reduce_typed<DType::FP32>(a, vec, blocks, s); break;
+    case DType::FP8_E4M3: local_reduce_typed<DType::FP8_E4M3>(a, vec, blocks, s); break;
+    case DType::FP8_E5M2: local_reduce_typed<DType::FP8_E5M2>(a, vec, blocks, s); break;
   }
   DLNB_HIP_CHECK(hipGetLastError());
 }

@@ -76,9 +76,16 @@ void LocalStore::set(const std::string& key, const std::string& value) {
 
 std::string LocalStore::get(const std::string& key) {
   std::unique_lock<std::mutex> g(mu_);
-  if (!cv_.wait_for(g, std::chrono::seconds(600), [&] { return kv_.count(key) > 0; }))
+  if (!cv_.wait_for(g, std::chrono::seconds(600), [&] { return kv_.count(key) > 0 || !aborted_.empty(); }))
     DLNB_THROW("local store: timeout waiting for key " << key);
+  if (!kv_.count(key)) DLNB_THROW("local store: abandoned waiting for key " << key << ": " << aborted_);
   return kv_[key];
+}
+
+void LocalStore::abort(const std::string& why) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (aborted_.empty()) aborted_ = why.empty() ? "aborted" : why;
+  cv_.notify_all();
 }
 
 long long LocalStore::add(const std::string& key, long long delta) {
@@ -343,6 +350,20 @@ int first_env_int(std::initializer_list<const char*> names, int dflt) {
 }
 
 }  // namespace
+
+std::unique_ptr<Bootstrap> bootstrap_loopback(int rank, int world, std::shared_ptr<LocalStore> store,
+                                              std::shared_ptr<LoopbackHub> hub) {
+  std::unique_ptr<Bootstrap> b(new Bootstrap());
+  b->info.rank = rank;
+  b->info.world_size = world;
+  b->info.local_rank = rank;
+  b->info.local_size = world;
+  b->info.hostname = get_hostname();
+  b->store = store;
+  b->world.reset(new HostGroup(store, rank, world));
+  b->hub = std::move(hub);
+  return b;
+}
 
 std::unique_ptr<Bootstrap> bootstrap_from_env(const std::string& store_addr_in) {
   std::unique_ptr<Bootstrap> b(new Bootstrap());

@@ -441,4 +441,10 @@ std::unique_ptr<CommFactory> make_shm_factory(HostGroup& world, Device& dev) {
   return std::unique_ptr<CommFactory>(new ShmFactory(world, dev));
 }
 
+void host_reduce_sum(DType t, void* dst, const std::vector<const char*>& srcs, size_t count) {
+  par_reduce_sum(t, dst, srcs, 0, count);
+}
+
+void host_copy(void* dst, const void* src, size_t bytes) { par_copy(dst, src, bytes); }
+
 }  // namespace dlnb

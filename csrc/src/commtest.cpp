@@ -16,6 +16,8 @@
 #include <cstdio>
 #include <cstring>
 #include <iostream>
+#include <algorithm>
+#include <thread>
 #include <sstream>
 
 #include "dlnb/strategy.hpp"
@@ -148,7 +150,7 @@ struct Tester {
 int commtest_main(int argc, char** argv) {
   std::string backend = "auto", devices, dtype = "bf16", sizes_s, json_path;
   bool bench = false;
-  int iters = 20, warmup = 5;
+  int iters = 20, warmup = 5, ranks = 2;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto val = [&](const char* what) -> std::string {
@@ -162,17 +164,21 @@ int commtest_main(int argc, char** argv) {
     else if (a == "--bench") bench = true;
     else if (a == "--iters") iters = std::stoi(val("--iters"));
     else if (a == "--warmup") warmup = std::stoi(val("--warmup"));
+    else if (a == "--ranks") ranks = std::stoi(val("--ranks"));
     else if (a == "--json") json_path = val("--json");
     else if (a == "-h" || a == "--help") {
-      std::cout << "Usage: dlnb commtest [--backend auto|rccl|xgmi|cpu] [-d 0,1,..] [--dtype bf16|fp16|fp32|fp8_e4m3|"
-                   "fp8_e5m2]\n                     [--sizes n1,n2,..] [--bench] [--iters N] [--warmup N]\n"
+      std::cout << "Usage: dlnb commtest [--backend auto|rccl|xgmi|cpu|loopback|loopback-cpu] [--ranks N] [-d 0,1,..]\n"
+                   "                     [--dtype bf16|fp16|fp32|fp8_e4m3|fp8_e5m2]\n"
+                   "                     [--sizes n1,n2,..] [--bench] [--iters N] [--warmup N]\n"
                    "  sizes are elements per rank; check mode verifies every collective exactly\n";
       return 0;
     } else DLNB_THROW("unknown option " << a);
   }
+  auto body = [&](std::unique_ptr<Bootstrap> boot) -> int {
   Context ctx;
-  ctx.boot = bootstrap_from_env("");
-  backend = select_backend(ctx, backend, devices);
+  ctx.boot = std::move(boot);
+  const std::string be = select_backend(ctx, backend, devices);
+  (void)be;
   const DType t = parse_dtype(dtype);
   const int W = ctx.world(), me = ctx.rank();
   std::vector<size_t> sizes;
@@ -280,6 +286,26 @@ int commtest_main(int argc, char** argv) {
   ctx.hg().barrier();
   ctx.hg().store().finish();
   return total_fail == 0 ? 0 : 3;
+  };
+  if (backend != "loopback" && backend != "loopback-cpu") return body(bootstrap_from_env(""));
+  // loopback: the ranks are threads of this process (see comm_loopback.cpp)
+  auto store = std::make_shared<LocalStore>();
+  auto hub = make_loopback_hub(ranks, static_cast<double>(env_int("DLNB_STORE_TIMEOUT", 900)));
+  std::vector<int> rc(static_cast<size_t>(ranks), 0);
+  std::vector<std::thread> threads;
+  for (int r = 0; r < ranks; ++r)
+    threads.emplace_back([&, r] {
+      try {
+        rc[static_cast<size_t>(r)] = body(bootstrap_loopback(r, ranks, store, hub));
+      } catch (const std::exception& e) {
+        std::fprintf(stderr, "[commtest] rank %d: %s\n", r, e.what());
+        rc[static_cast<size_t>(r)] = 2;
+        loopback_abort(*hub, e.what());
+        store->abort(e.what());
+      }
+    });
+  for (auto& t : threads) t.join();
+  return *std::max_element(rc.begin(), rc.end());
 }
 
 }  // namespace dlnb

@@ -74,7 +74,9 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  -d, --devices LIST     comma-separated device ids indexed by local rank\n"
      << "  -m, --min_exectime S   run at least S seconds (overrides --runs)\n"
      << "  -h, --help             this help\n"
-     << "  --backend B            auto | rccl | xgmi | cpu\n"
+     << "  --backend B            auto | rccl | xgmi | cpu | loopback | loopback-cpu\n"
+     << "  --ranks N              loopback: ranks run as threads of this process on one GPU\n"
+     << "                         (loopback-cpu: on the CPU device), default 2\n"
      << "  --compute C            auto | sleep | spin | gemm | gemm-work | flops\n"
      << "  --wire-dtype T         bf16 | fp16 | fp32 | fp8 (collective element type)\n"
      << "  --compute-dtype T      auto | bf16 | fp8 (GEMM operand type for gemm/flops)\n"
@@ -139,6 +141,8 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
       o.min_exectime = to_double(val("min_exectime"), "min_exectime");
     } else if (is("--backend")) {
       o.backend = val("backend");
+    } else if (is("--ranks")) {
+      o.ranks = to_int(val("ranks"), "ranks");
     } else if (is("--compute")) {
       o.compute = val("compute");
     } else if (is("--wire-dtype") || is("--dtype")) {

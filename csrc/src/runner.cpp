@@ -14,6 +14,7 @@
 #include <fstream>
 #include <iostream>
 #include <map>
+#include <mutex>
 #include <sstream>
 #include <thread>
 
@@ -175,7 +176,8 @@ bool file_exists(const std::string& p) {
 std::string select_backend(Context& ctx, const std::string& requested, const std::string& devices) {
   const RankInfo& ri = ctx.boot->info;
   std::string backend = requested;
-  const int ngpu = gpu_device_count();
+  const bool in_process = backend == "loopback" || backend == "loopback-cpu";
+  const int ngpu = in_process ? 0 : gpu_device_count();
   if (backend == "auto") backend = ngpu > 0 ? "rccl" : "cpu";
   if (backend == "rccl" || backend == "xgmi") {
     DLNB_REQUIRE(ngpu > 0, "--backend " << backend << " requested but no GPU is visible");
@@ -191,16 +193,81 @@ std::string select_backend(Context& ctx, const std::string& requested, const std
   } else if (backend == "cpu") {
     ctx.dev = make_cpu_device();
     ctx.comms = make_shm_factory(ctx.hg(), *ctx.dev);
+  } else if (backend == "loopback" || backend == "loopback-cpu") {
+    DLNB_REQUIRE(ctx.boot->hub, "--backend " << backend << " runs inside one process (run_benchmark starts the rank threads)");
+    if (backend == "loopback-cpu") {
+      // CPU device only: no HIP call at all (GPU-less hosts and CPU tests)
+      ctx.dev = make_cpu_device();
+    } else {
+      // Every rank on the same GPU: the one given by -d (default 0).
+      const int ngpu = gpu_device_count();
+      DLNB_REQUIRE(ngpu > 0, "--backend loopback needs a GPU (loopback-cpu runs the ranks on the CPU device)");
+      std::vector<int> list = parse_device_list(devices);
+      const int dev_index = list.empty() ? 0 : list[0];
+      for (int d : list)
+        DLNB_REQUIRE(d == dev_index, "--backend loopback puts every rank on one device (-d " << devices << ")");
+      DLNB_REQUIRE(dev_index >= 0 && dev_index < ngpu, "device id " << dev_index << " out of range");
+      ctx.dev = make_gpu_device(dev_index);
+    }
+    ctx.comms = make_loopback_factory(ctx.hg(), *ctx.dev, ctx.boot->hub);
   } else {
-    DLNB_THROW("unknown backend '" << backend << "' (auto, rccl, xgmi, cpu)");
+    DLNB_THROW("unknown backend '" << backend << "' (auto, rccl, xgmi, cpu, loopback, loopback-cpu)");
   }
   return backend;
 }
 
+namespace {
+
+Json run_rank(const Options& opt, std::unique_ptr<Bootstrap> boot);
+
+// --backend loopback / loopback-cpu: the job's ranks are threads of this process sharing one
+// LocalStore (host barriers / gathers) and one LoopbackHub (collectives). A
+// failing rank aborts both, so the others leave their waits instead of
+// hanging; the first failure is rethrown.
+Json run_loopback(const Options& opt) {
+  const int n = opt.ranks;
+  DLNB_REQUIRE(n >= 1, "--ranks must be >= 1");
+  DLNB_REQUIRE(env_int("WORLD_SIZE", 1) == 1 && env_int("DLNB_WORLD_SIZE", 1) == 1,
+               "--backend loopback runs all ranks inside one process: launch it once, not under a multi-rank launcher");
+  auto store = std::make_shared<LocalStore>();
+  auto hub = make_loopback_hub(n, static_cast<double>(env_int("DLNB_STORE_TIMEOUT", 900)));
+  std::vector<Json> docs(static_cast<size_t>(n));
+  std::mutex mu;
+  std::string first_error;
+  std::vector<std::thread> threads;
+  for (int r = 0; r < n; ++r) {
+    threads.emplace_back([&, r] {
+      try {
+        docs[static_cast<size_t>(r)] = run_rank(opt, bootstrap_loopback(r, n, store, hub));
+      } catch (const std::exception& e) {
+        const std::string msg = "rank " + std::to_string(r) + ": " + e.what();
+        {
+          std::lock_guard<std::mutex> g(mu);
+          if (first_error.empty()) first_error = msg;
+        }
+        loopback_abort(*hub, msg);
+        store->abort(msg);
+      }
+    });
+  }
+  for (auto& t : threads) t.join();
+  if (!first_error.empty()) throw Error(first_error);
+  return docs[0];
+}
+
+}  // namespace
+
 Json run_benchmark(const Options& opt) {
+  if (opt.backend == "loopback" || opt.backend == "loopback-cpu") return run_loopback(opt);
+  return run_rank(opt, bootstrap_from_env(opt.store_addr));
+}
+
+namespace {
+
+Json run_rank(const Options& opt, std::unique_ptr<Bootstrap> boot) {
   Context ctx;
   ctx.opt = opt;
-  ctx.boot = bootstrap_from_env(opt.store_addr);
+  ctx.boot = std::move(boot);
   const RankInfo& ri = ctx.boot->info;
 
   // ---- backend / device (cpp/utils.hpp:62-117 set_local_device)
@@ -435,6 +502,8 @@ Json run_benchmark(const Options& opt) {
   ctx.hg().store().finish();
   return doc;
 }
+
+}  // namespace
 
 int main_for(StrategyKind kind, int argc, char** argv) {
   Options opt;

@@ -624,8 +624,14 @@ class Pipeline : public Strategy {
   // Link groups of one step (-1 = nothing in that slot).
   void links(int send_f, int recv_b, int send_b, int recv_f) {
     if (S_ == 1) return;
+    // With the wrap link the stages form a ring; stage 0 serves its previous
+    // link first so a backend whose groups complete on the host (loopback)
+    // has no cycle of stages each waiting on its successor. Stream-ordered
+    // backends are indifferent to the order (two independent streams).
+    const bool prev_first = interleaved_ && stage_ == 0;
+    if (prev_first && (send_b >= 0 || recv_f >= 0)) prev_link(send_b, recv_f);
     if (send_f >= 0 || recv_b >= 0) next_link(send_f, recv_b);
-    if (send_b >= 0 || recv_f >= 0) prev_link(send_b, recv_f);
+    if (!prev_first && (send_b >= 0 || recv_f >= 0)) prev_link(send_b, recv_f);
   }
 
   void enqueue_interleaved() {

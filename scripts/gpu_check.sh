@@ -19,6 +19,7 @@ run() {  # name timeout cmd...
 for step in "$@"; do
   case $step in
     pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 170 --timeout-method thread ;;
+    loopback) run loopback_gpu 600 python -u -m pytest tests/test_gpu_strategies.py -m gpu -v -k loopback -p no:cacheprovider --timeout 170 --timeout-method thread ;;
     bench) run bench 300 python bench.py --steps 3 --warmup 1 --json gpurun_out/bench_report.json ;;
     clock) run clock 120 python -m dlnetbench_amd.tools.clock_check ;;
     hwmon) run hwmon 30 bash -c "ls -la /sys/class/drm/card*/device/hwmon/hwmon*/ | head -80" ;;

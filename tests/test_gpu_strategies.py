@@ -87,3 +87,54 @@ def test_dp_zero_on_gpu(zero, data_dir):
     g = doc["global"]
     assert g["zero_stage"] == zero and g["dlnb"]["graph"] > 0
     assert len(doc["ranks"][0]["param_allgather_time"]) == 2 * 4
+
+
+# ---- loopback: N ranks as threads of this process, all on the one MI355X
+# (comm_loopback.cpp; collectives = the multi-source reduce kernel of xgmi.hip)
+
+LOOPBACK_CASES = [
+    ("dp", "tiny_dense_8_bfloat16", (4,), 4),
+    ("fsdp", "tiny_dense_8_bfloat16", (4, 4), 4),
+    ("fsdp", "tiny_dense_8_bfloat16", (4, 4), 8),
+    ("hybrid_2d", "tiny_dense_8_bfloat16", (2, 4), 4),
+    ("hybrid_3d", "tiny_dense_8_bfloat16", (2, 4, 2), 8),
+    ("hybrid_3d_moe", "tiny_moe_8_bfloat16", (2, 4, 2), 8),
+    ("hybrid_cp", "tiny_dense_8_bfloat16", (4,), 4),
+    ("hybrid_4d", "tiny_moe_8_bfloat16", (2, 2, 2, 2), 8),
+]
+
+
+@pytest.mark.parametrize("strategy,model,params,w", LOOPBACK_CASES)
+def test_strategy_loopback_on_gpu(strategy, model, params, w, data_dir):
+    doc = engine.run(strategy, model, *params, base_path=data_dir, warmup=1, runs=2, compute="gemm",
+                     backend="loopback", ranks=w, quiet=True)
+    g = doc["global"]
+    assert g["backend"] == "LOOPBACK" and g["device"] == "GPU" and g["world_size"] == w
+    assert len(doc["ranks"]) == w
+    it = g["dlnb"]["iteration"]
+    assert it["median_ms"] >= 0.9 * it["compute_floor_ms"]
+
+
+def test_commtest_loopback_on_gpu(root):
+    """Exact collectives + P2P through the GPU multi-source reduce kernel (aligned and odd sizes)."""
+    import json
+    import os
+    import subprocess
+    dlnb = os.path.join(root, "build", "bin", "dlnb")
+    for dtype, w in (("bf16", 4), ("fp32", 3), ("fp8_e4m3", 8)):
+        p = subprocess.run([dlnb, "commtest", "--backend", "loopback", "--ranks", str(w), "--dtype", dtype,
+                            "--sizes", "1,7,100,4097,70001,1048583"], capture_output=True, text=True, timeout=100)
+        lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+        assert p.returncode == 0 and lines and lines[0]["ok"], p.stdout[-1500:] + p.stderr[-1500:]
+
+
+def test_fsdp_llama3_8b_loopback_8_ranks_one_gpu(root):
+    """The bench config at W=8 as 8 rank threads on one MI355X: full-size FSDP
+    collectives (per-rank shards of 1/8), compute time scaled down 50x."""
+    doc = engine.run("fsdp", "llama3_8b_16_bfloat16", 32, 8, base_path=root, warmup=1, runs=1,
+                     compute="gemm", backend="loopback", ranks=8, time_scale=0.02, quiet=True)
+    g = doc["global"]
+    assert g["world_size"] == 8 and g["sharding_factor"] == 8 and len(doc["ranks"]) == 8
+    assert g["allgather_msg_size_bytes"] == 250945664 * 2  # the gathered unit, as at N=1
+    it = g["dlnb"]["iteration"]
+    assert it["median_ms"] >= 0.9 * it["compute_floor_ms"]
