@@ -105,8 +105,10 @@ __device__ __forceinline__ void read_frags(const char* half, int row0, int r16, 
 #pragma unroll
   for (int i = 0; i < NF; ++i) {
     const int row = row0 + i * 16 + r16;
-    const i32x4 lo = *reinterpret_cast<const i32x4*>(half + swz(row, 2 * h));
-    const i32x4 hi = *reinterpret_cast<const i32x4*>(half + swz(row, 2 * h + 1));
+    // K chunks h and h + 4 (same order for A and B): conflict-free under the
+    // swizzle, where chunks 2h, 2h + 1 are 2-way on every ds_read_b128
+    const i32x4 lo = *reinterpret_cast<const i32x4*>(half + swz(row, h));
+    const i32x4 hi = *reinterpret_cast<const i32x4*>(half + swz(row, h + 4));
     f[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);  // register concat, no element moves
   }
 }

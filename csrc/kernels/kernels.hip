@@ -256,23 +256,24 @@ __device__ __forceinline__ void ktile_mfma(const char* __restrict__ At, const ch
   } else {
     // fp8 e4m3 through the MX-scaled MFMA (16x16x128, unit E8M0 scales =
     // 127): one instruction covers the whole 128-byte K-tile at twice the
-    // non-scaled fp8 rate. Lane l holds 32 consecutive K bytes (chunks
-    // 2h, 2h+1) of its row; A and B use the same K order, which is all
-    // the product needs (checked exactly by scripts/probes/
-    // mfma_f8f6f4_layout.hip and tests/test_gpu_kernels.py).
+    // non-scaled fp8 rate. Lane group h holds K chunks h and h + 4 of its
+    // row (not 2h, 2h+1: with the (row >> 1) swizzle those put rows r and
+    // r + 4 of one ds_read_b128 lane group on the same banks, 2-way on
+    // every read); A and B use the same K order, which is all the product
+    // needs (checked exactly by tests/test_gpu_kernels.py).
     i32x8 bfr[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int row = wn * WTN + j * 16 + r16;
-      const int4 lo = *reinterpret_cast<const int4*>(Bt + swz(row, 2 * h));
-      const int4 hi = *reinterpret_cast<const int4*>(Bt + swz(row, 2 * h + 1));
+      const int4 lo = *reinterpret_cast<const int4*>(Bt + swz(row, h));
+      const int4 hi = *reinterpret_cast<const int4*>(Bt + swz(row, h + 4));
       bfr[j] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int row = wm * 128 + i * 16 + r16;
-      const int4 lo = *reinterpret_cast<const int4*>(At + swz(row, 2 * h));
-      const int4 hi = *reinterpret_cast<const int4*>(At + swz(row, 2 * h + 1));
+      const int4 lo = *reinterpret_cast<const int4*>(At + swz(row, h));
+      const int4 hi = *reinterpret_cast<const int4*>(At + swz(row, h + 4));
       const i32x8 af = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
