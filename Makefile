@@ -24,7 +24,7 @@ LOOPS    := dp_loop fsdp_loop hybrid_2d_loop hybrid_3d_loop hybrid_3d_moe_loop h
 LIB      := $(BUILD)/libdlnb.so
 PYLIB    := dlnetbench_amd/_lib/libdlnb.so
 
-.PHONY: all lib apps clean asan probes
+.PHONY: all lib apps clean asan tsan probes
 all: lib apps
 
 lib: $(PYLIB)
@@ -66,5 +66,11 @@ asan:
 	$(MAKE) BUILD=build-asan OPT="-O1 -g -fno-omit-frame-pointer -Xarch_host -fsanitize=address" \
 	  LDLIBS="$(LDLIBS) -fsanitize=address" PYLIB=build-asan/unused.so apps
 
+# Host ThreadSanitizer build into build-tsan/: the loopback backend's rank
+# threads, the CPU device's worker-thread streams and the energy sampler.
+tsan:
+	$(MAKE) BUILD=build-tsan OPT="-O1 -g -fno-omit-frame-pointer -Xarch_host -fsanitize=thread" \
+	  LDLIBS="$(LDLIBS) -fsanitize=thread" PYLIB=build-tsan/unused.so apps
+
 clean:
-	rm -rf $(BUILD) build-asan $(PYLIB)
+	rm -rf $(BUILD) build-asan build-tsan $(PYLIB)

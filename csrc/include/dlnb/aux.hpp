@@ -17,7 +17,9 @@
 //     timeout / async-error detection and the launcher's teardown.
 #pragma once
 
+#include <atomic>
 #include <memory>
+#include <mutex>
 #include <string>
 
 namespace dlnb {
@@ -38,13 +40,14 @@ class Tracer {
  public:
   static Tracer& get();
   void enable(bool on);
-  bool enabled() const { return on_; }
+  bool enabled() const { return on_.load(std::memory_order_acquire); }
   void push(const char* name);
   void pop();
   void mark(const char* name);
 
  private:
-  bool on_ = false;
+  std::atomic<bool> on_{false};
+  std::mutex mu_;
   void* lib_ = nullptr;
   int (*push_)(const char*) = nullptr;
   int (*pop_)() = nullptr;

@@ -196,28 +196,31 @@ Tracer& Tracer::get() {
   return t;
 }
 
+// Process-wide; the rank threads of a loopback job all call enable() with the
+// same value, so the flag is set once and never toggled under a live range.
 void Tracer::enable(bool on) {
-  on_ = false;
-  if (!on) return;
-  if (!lib_) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (on && !lib_) {
     lib_ = dlopen("libroctx64.so", RTLD_NOW | RTLD_GLOBAL);
     if (!lib_) lib_ = dlopen("/opt/rocm/lib/libroctx64.so", RTLD_NOW | RTLD_GLOBAL);
-    if (!lib_) return;
-    push_ = reinterpret_cast<int (*)(const char*)>(dlsym(lib_, "roctxRangePushA"));
-    pop_ = reinterpret_cast<int (*)()>(dlsym(lib_, "roctxRangePop"));
-    mark_ = reinterpret_cast<void (*)(const char*)>(dlsym(lib_, "roctxMarkA"));
+    if (lib_) {
+      push_ = reinterpret_cast<int (*)(const char*)>(dlsym(lib_, "roctxRangePushA"));
+      pop_ = reinterpret_cast<int (*)()>(dlsym(lib_, "roctxRangePop"));
+      mark_ = reinterpret_cast<void (*)(const char*)>(dlsym(lib_, "roctxMarkA"));
+    }
   }
-  on_ = push_ && pop_;
+  const bool want = on && push_ && pop_;
+  if (on_.load(std::memory_order_relaxed) != want) on_.store(want, std::memory_order_release);
 }
 
 void Tracer::push(const char* name) {
-  if (on_) push_(name);
+  if (on_.load(std::memory_order_acquire)) push_(name);
 }
 void Tracer::pop() {
-  if (on_) pop_();
+  if (on_.load(std::memory_order_acquire)) pop_();
 }
 void Tracer::mark(const char* name) {
-  if (on_ && mark_) mark_(name);
+  if (on_.load(std::memory_order_acquire) && mark_) mark_(name);
 }
 
 // ---------------------------------------------------------- fault injector
