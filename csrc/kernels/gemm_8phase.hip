@@ -417,11 +417,15 @@ void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N
   auto* a = static_cast<const char*>(A);
   auto* b = static_cast<const char*>(B);
   auto* cc = static_cast<__bf16*>(C);
-  // bf16 only: the fp8 MX body plus the deadline bookkeeping spills inside
-  // the K-loop (256 VGPRs); fp8 deadline work stays on gemm_tn_256_kernel.
-  DLNB_REQUIRE(in_t == DType::BF16, "gemm 8-phase deadline: bf16 only");
-  hipLaunchKernelGGL((gemm_8phase_kernel<false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
-                     ticks, slice_end, tstart);
+  // fp8: the MX body plus the deadline bookkeeping needs 35 VGPRs of spill
+  // space, all of it in the per-tile code around the K-loop (the K-loop
+  // itself has no scratch access), i.e. a few reloads per 32 K-tiles.
+  if (in_t == DType::BF16)
+    hipLaunchKernelGGL((gemm_8phase_kernel<false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
+                       ticks, slice_end, tstart);
+  else
+    hipLaunchKernelGGL((gemm_8phase_kernel<true, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
+                       ticks, slice_end, tstart);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 8-phase deadline launch failed: " << hipGetErrorString(e));
 }

@@ -655,7 +655,7 @@ void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K
   if (slice_end == 0) slice_end = ticks;
   DLNB_REQUIRE(gemm_shape_ok(M, N, K, in_t), "gemm_tn_deadline: unsupported shape");
   DLNB_REQUIRE(slot != nullptr && grid > 0 && epoch > 0 && epoch < 65536, "gemm_tn_deadline: bad slot/grid/epoch");
-  if (gemm_8phase_enabled() && in_t == DType::BF16 && gemm_8phase_shape_ok(M, N, K, in_t)) {
+  if (gemm_8phase_enabled() && gemm_8phase_shape_ok(M, N, K, in_t)) {
     gemm_tn_8phase_deadline(A, B, C, M, N, K, in_t, ticks, slot, epoch, grid, stream, slice_end, tstart);
     return;
   }

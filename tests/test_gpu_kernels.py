@@ -97,12 +97,15 @@ def test_deadline_kernels_hit_duration(fn):
         assert us / 1e3 * 0.97 <= ms <= us / 1e3 * 1.10 + 0.05, (us, times)
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
 @pytest.mark.parametrize("us", [100.0, 2000.0, 30000.0])
-def test_deadline_gemm_duration(us):
+def test_deadline_gemm_duration(us, dtype):
     a = torch.empty(8192, 4096, device="cuda", dtype=torch.bfloat16)
     b = torch.empty(14336, 4096, device="cuda", dtype=torch.bfloat16)
     gemm.fill_random_(a, 1)
     gemm.fill_random_(b, 2)
+    if dtype == "fp8":
+        a, b = a.to(torch.float8_e4m3fn), b.to(torch.float8_e4m3fn)
     c = torch.empty(8192, 14336, device="cuda", dtype=torch.bfloat16)
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
