@@ -153,6 +153,22 @@ def test_asan_build_is_clean(prog, args, root, data_dir):
     assert code == 0 and "AddressSanitizer" not in text, text[-3000:]
 
 
+@pytest.mark.parametrize("prog,args,extra", [("fsdp", ["tiny_dense_8_bfloat16", "4", "4"], []),
+                                             ("hybrid_2d", ["tiny_deep_8_bfloat16", "4", "8"],
+                                              ["--pp-schedule", "interleaved"]),
+                                             ("hybrid_3d_moe", ["tiny_moe_8_bfloat16", "2", "4", "2"], ["--ep-overlap"])])
+def test_tsan_loopback_threads_race_free(prog, args, extra, root, data_dir):
+    """Host ThreadSanitizer build (make tsan): 8 loopback rank threads on the CPU device, no data races."""
+    b = os.path.join(root, "build-tsan", "bin", prog)
+    if not os.path.exists(b):
+        pytest.skip("make tsan not built")
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "DLNB_RANK", "DLNB_WORLD_SIZE")}
+    env["TSAN_OPTIONS"] = "halt_on_error=1"
+    p = subprocess.run([b, *args, data_dir, *extra, "--backend", "loopback-cpu", "--ranks", "8", "--quiet",
+                        "-w", "1", "-r", "2"], capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0 and "ThreadSanitizer" not in p.stderr, p.stderr[-3000:]
+
+
 def test_graph_needs_gpu(bindir, data_dir):
     p = subprocess.run([os.path.join(bindir, "dp"), "tiny_dense_8_bfloat16", "2", data_dir, "--backend",
                         "cpu", "--graph", "-w", "0", "-r", "1"], capture_output=True, text=True)
