@@ -86,5 +86,14 @@ constexpr int kMaxLocal = 16;
 void launch_local_reduce(char* const* dsts, int nd, const char* const* srcs, int ns, size_t count, DType t,
                          void* stream);
 
+// One launch for a whole loopback collective of W ranks (send[r] / recv[r]
+// per rank, blk elements per rank block):
+//   AllGather:     recv[j][i*blk + e] = send[i][e]
+//   ReduceScatter: recv[j][e]         = sum_i send[i][j*blk + e]  (fp32 accumulation)
+//   AllToAll:      recv[j][i*blk + e] = send[i][j*blk + e]        (out of place)
+enum class LocalColl : int { AllGather, ReduceScatter, AllToAll };
+void launch_local_coll(LocalColl op, char* const* recv, const char* const* send, int W, size_t blk, DType t,
+                       void* stream);
+
 }  // namespace xgmi
 }  // namespace dlnb

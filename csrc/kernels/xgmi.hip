@@ -493,6 +493,75 @@ __global__ void __launch_bounds__(T) local_reduce_kernel(LocalArgs a) {
   }
 }
 
+struct CollArgs {
+  const char* send[kMaxLocal];
+  char* recv[kMaxLocal];
+  int W;
+  size_t blk;  // elements per rank block
+};
+
+// blockIdx.y = the rank block this block works on: the source rank i
+// (all-gather, all-to-all) or the destination rank j (reduce-scatter).
+template <DType D, LocalColl OP, bool VEC>
+__global__ void __launch_bounds__(T) local_coll_kernel(CollArgs a) {
+  using E = Elt<D>;
+  const int b = blockIdx.y;
+  const size_t stride = static_cast<size_t>(gridDim.x) * T;
+  const size_t tid = static_cast<size_t>(blockIdx.x) * T + threadIdx.x;
+  constexpr size_t es = sizeof(uint4) / E::N;
+  const size_t bb = a.blk * es;  // bytes per rank block
+  const size_t nv = VEC ? a.blk / E::N : 0;
+  for (size_t v = tid; v < nv; v += stride) {
+    if constexpr (OP == LocalColl::AllGather) {
+      const uint4 x = V(a.send[b])[v];
+      for (int j = 0; j < a.W; ++j) V(a.recv[j] + b * bb)[v] = x;
+    } else if constexpr (OP == LocalColl::ReduceScatter) {
+      float acc[E::N], f[E::N];
+      E::unpack(V(a.send[0] + b * bb)[v], acc);
+      for (int i = 1; i < a.W; ++i) {
+        E::unpack(V(a.send[i] + b * bb)[v], f);
+#pragma unroll
+        for (int k = 0; k < E::N; ++k) acc[k] += f[k];
+      }
+      V(a.recv[b])[v] = E::pack(acc);
+    } else {
+      for (int j = 0; j < a.W; ++j) V(a.recv[j] + b * bb)[v] = V(a.send[b] + j * bb)[v];
+    }
+  }
+  for (size_t e = nv * E::N + tid; e < a.blk; e += stride) {
+    if constexpr (OP == LocalColl::ReduceScatter) {
+      float x = 0.f;
+      for (int i = 0; i < a.W; ++i) x += E::ld(a.send[i] + b * bb, e);
+      E::st(a.recv[b], e, x);
+    } else {
+      for (int j = 0; j < a.W; ++j) {
+        const char* src = OP == LocalColl::AllGather ? a.send[b] : a.send[b] + j * bb;
+        char* dst = a.recv[j] + b * bb;
+        for (size_t k = 0; k < es; ++k) dst[e * es + k] = src[e * es + k];
+      }
+    }
+  }
+}
+
+template <DType D, LocalColl OP>
+void local_coll_typed(const CollArgs& a, bool vec, dim3 grid, hipStream_t s) {
+  if (vec)
+    local_coll_kernel<D, OP, true><<<grid, T, 0, s>>>(a);
+  else
+    local_coll_kernel<D, OP, false><<<grid, T, 0, s>>>(a);
+}
+
+template <LocalColl OP>
+void local_coll_dtype(const CollArgs& a, DType t, bool vec, dim3 grid, hipStream_t s) {
+  switch (t) {
+    case DType::BF16: local_coll_typed<DType::BF16, OP>(a, vec, grid, s); break;
+    case DType::FP16: local_coll_typed<DType::FP16, OP>(a, vec, grid, s); break;
+    case DType::FP32: local_coll_typed<DType::FP32, OP>(a, vec, grid, s); break;
+    case DType::FP8_E4M3: local_coll_typed<DType::FP8_E4M3, OP>(a, vec, grid, s); break;
+    case DType::FP8_E5M2: local_coll_typed<DType::FP8_E5M2, OP>(a, vec, grid, s); break;
+  }
+}
+
 template <DType D>
 void local_reduce_typed(const LocalArgs& a, bool vec, int blocks, hipStream_t s) {
   if (vec)
@@ -566,6 +635,33 @@ void launch_local_reduce(char* const* dsts, int nd, const char* const* srcs, int
     case DType::FP32: local_reduce_typed<DType::FP32>(a, vec, blocks, s); break;
     case DType::FP8_E4M3: local_reduce_typed<DType::FP8_E4M3>(a, vec, blocks, s); break;
     case DType::FP8_E5M2: local_reduce_typed<DType::FP8_E5M2>(a, vec, blocks, s); break;
+  }
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
+void launch_local_coll(LocalColl op, char* const* recv, const char* const* send, int W, size_t blk, DType t,
+                       void* stream) {
+  DLNB_REQUIRE(W >= 1 && W <= kMaxLocal, "local collective: " << W << " ranks (1.." << kMaxLocal << ")");
+  if (blk == 0) return;
+  CollArgs a{};
+  a.W = W;
+  a.blk = blk;
+  const size_t es = dtype_size(t);
+  bool vec = (blk * es) % 16 == 0;
+  for (int i = 0; i < W; ++i) {
+    a.send[i] = send[i];
+    a.recv[i] = recv[i];
+    vec = vec && (reinterpret_cast<uintptr_t>(send[i]) & 15u) == 0 && (reinterpret_cast<uintptr_t>(recv[i]) & 15u) == 0;
+  }
+  const size_t work = vec ? std::max<size_t>(1, blk * es / 16) : blk;
+  // ~2048 blocks in total across the W rank blocks
+  const size_t per = std::max<size_t>(1, std::min<size_t>((work + 4 * T - 1) / (4 * T), 2048 / W));
+  const dim3 grid(static_cast<unsigned>(per), static_cast<unsigned>(W));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (op) {
+    case LocalColl::AllGather: local_coll_dtype<LocalColl::AllGather>(a, t, vec, grid, s); break;
+    case LocalColl::ReduceScatter: local_coll_dtype<LocalColl::ReduceScatter>(a, t, vec, grid, s); break;
+    case LocalColl::AllToAll: local_coll_dtype<LocalColl::AllToAll>(a, t, vec, grid, s); break;
   }
   DLNB_HIP_CHECK(hipGetLastError());
 }

@@ -248,6 +248,18 @@ class LoopbackComm : public Communicator {
     const size_t n = static_cast<size_t>(g.n), blk = count * dtype_size(t);
     std::vector<const char*> srcs;
     std::vector<char*> dsts;
+    if (dev_.kind() == DeviceKind::GPU && kind != CollKind::AllReduce && count > 0) {
+      // one launch for the whole collective (instead of n or n^2 pieces)
+      for (auto& a : g.args) {
+        srcs.push_back(a.send);
+        dsts.push_back(a.recv);
+      }
+      const xgmi::LocalColl op = kind == CollKind::AllGather       ? xgmi::LocalColl::AllGather
+                                 : kind == CollKind::ReduceScatter ? xgmi::LocalColl::ReduceScatter
+                                                                   : xgmi::LocalColl::AllToAll;
+      xgmi::launch_local_coll(op, dsts.data(), srcs.data(), g.n, count, t, s.native());
+      return;
+    }
     switch (kind) {
       case CollKind::AllReduce:
         for (auto& a : g.args) {
