@@ -248,6 +248,12 @@ def main(argv=None) -> int:
     ap.add_argument("--wire", default="bf16")
     ap.add_argument("--zero", type=int, default=0, help="dp: ZeRO stage 0|1|2")
     ap.add_argument("--cp-algo", default="ring", choices=["ring", "ulysses"])
+    ap.add_argument("--predict", action="store_true",
+                    help="dp / fsdp: add the xGMI cost-model prediction (parallel/xgmi_model.py) at W = 1, 2, 4, 8")
+    ap.add_argument("--link-gbps", type=float, default=153.0, help="xGMI bandwidth per link and direction")
+    ap.add_argument("--eta", type=float, default=0.75, help="achieved fraction of the link bandwidth")
+    ap.add_argument("--alpha-us", type=float, default=15.0, help="latency per collective")
+    ap.add_argument("--algo", default="direct", choices=["direct", "ring"])
     a = ap.parse_args(argv)
     st = load_stats(os.path.join(a.base, "model_stats", a.model + ".txt"))
     if a.strategy == "dp":
@@ -268,7 +274,22 @@ def main(argv=None) -> int:
             experts = a.params[3] if len(a.params) > 3 else 1
             pl = plan_hybrid(st, a.world, a.strategy, a.params[0], a.params[1], inner, L, wire=a.wire,
                              experts=experts)
-    print(json.dumps(pl.to_json(), indent=1))
+    doc = pl.to_json()
+    if a.predict and a.strategy in ("dp", "fsdp"):
+        from . import xgmi_model as xm
+        lm = xm.LinkModel(a.link_gbps, a.eta, a.alpha_us)
+        pred = {}
+        for w in (1, 2, 4, 8):
+            if a.strategy == "dp":
+                pred[str(w)] = xm.predict_dp(st, w, a.params[0], lm, a.wire, a.algo)
+            elif w % a.params[1] == 0 or a.params[1] == a.world:
+                F = w if a.params[1] == a.world else a.params[1]  # fully sharded runs shard over the job
+                pred[str(w)] = xm.predict_fsdp(st, w, a.params[0], F, lm, a.wire, a.algo)
+        doc["xgmi_prediction"] = {"model": {"link_gbps": a.link_gbps, "eta": a.eta, "alpha_us": a.alpha_us,
+                                            "algo": a.algo}, "by_world": pred}
+        if a.strategy == "dp":
+            doc["xgmi_prediction"]["suggested_buckets_at_world"] = xm.suggest_buckets(st, a.world, lm, a.wire)
+    print(json.dumps(doc, indent=1))
     return 0
 
 

@@ -1,4 +1,5 @@
 """Layouts and message sizes: golden values from SURVEY.md §2.4 / BASELINE.md."""
+import json
 import os
 
 import pytest
@@ -145,3 +146,51 @@ def test_schedule_model_no_deadlock_and_floor(sched, V, S, mb, semantics):
     t, stuck = sim.simulate(sim.build(S, mb, V, 1.0, 2.0, sched), semantics)
     assert not stuck
     assert t == pytest.approx(sim.floor(S, mb, V, 1.0, 2.0))
+
+
+# ---- xGMI cost model (dlnetbench_amd/parallel/xgmi_model.py)
+
+def test_xgmi_model_collective_times():
+    from dlnetbench_amd.parallel.xgmi_model import LinkModel
+    m = LinkModel(link_gbps=100.0, eta=1.0, alpha_us=0.0)
+    S = 8e9  # bytes
+    assert m.coll_us("allgather", S, 1) == 0.0
+    # direct: S / n over each link; ring: (n - 1) / n * S over one link
+    assert m.coll_us("allgather", S, 8) == pytest.approx(S / 8 / 1e5)
+    assert m.coll_us("allgather", S, 8, "ring") == pytest.approx(S * 7 / 8 / 1e5)
+    assert m.coll_us("allreduce", S, 8) == pytest.approx(2 * m.coll_us("reduce_scatter", S, 8))
+    assert m.coll_us("sendrecv", S, 2) == pytest.approx(S / 1e5)
+    with pytest.raises(ValueError):
+        m.coll_us("allgather", S, 16)
+
+
+def test_xgmi_model_predictions(root):
+    from dlnetbench_amd.parallel import xgmi_model as xm
+    st = load_stats(os.path.join(root, "model_stats", "llama3_8b_16_bfloat16.txt"))
+    m = xm.LinkModel()
+    p1 = xm.predict_fsdp(st, 1, 32, 1, m)
+    assert p1["exposed_ms"] == pytest.approx(0.0, abs=1e-9)
+    exposed = [xm.predict_fsdp(st, w, 32, w, m)["exposed_ms"] for w in (2, 4, 8)]
+    # more links per group -> less exposed time; always a small fraction of the floor
+    assert exposed[0] > exposed[1] > exposed[2] > 0
+    assert max(exposed) < 0.01 * p1["floor_ms"]
+    # a ring over one link per direction exposes more than the direct all-link algorithm
+    assert xm.predict_fsdp(st, 8, 32, 8, m, algo="ring")["exposed_ms"] > exposed[2]
+    # slower links can only add exposed time
+    slow = xm.LinkModel(link_gbps=10.0)
+    assert xm.predict_fsdp(st, 8, 32, 8, slow)["exposed_ms"] > exposed[2]
+    # dp: iteration >= floor, bucket suggestion is the argmin of the candidates
+    vit = load_stats(os.path.join(root, "model_stats", "vit_h_32_float8.txt"))
+    best = xm.suggest_buckets(vit, 8, m)
+    for nb in (1, 2, 4, 8, 16):
+        p = xm.predict_dp(vit, 8, nb, m)
+        assert p["iter_ms"] >= p["floor_ms"] - 1e-9
+        assert best["iter_ms"] <= p["iter_ms"] + 1e-9
+
+
+def test_plan_cli_predict(capsys, root):
+    from dlnetbench_amd.parallel import plan
+    assert plan.main(["fsdp", "llama3_8b_16_bfloat16", "32", "8", "--world", "8", "--base", root, "--predict"]) == 0
+    d = json.loads(capsys.readouterr().out)
+    by = d["xgmi_prediction"]["by_world"]
+    assert set(by) == {"1", "2", "4", "8"} and by["1"]["exposed_ms"] == pytest.approx(0.0, abs=1e-9)
