@@ -58,6 +58,7 @@ struct Options {
   std::string pp_schedule = "gpipe";          // gpipe (reference) | 1f1b | interleaved
   int pp_virtual = 2;                         // interleaved: model chunks (virtual stages) per stage
   bool ep_overlap = false;  // moe: overlap each half-microbatch's all-to-all with the other half's compute
+  double ep_imbalance = 0;  // moe: Zipf exponent of the expert-rank load (0 = uniform all-to-all)
   int dp_buckets = 1;  // hybrids: DP all-reduce buckets overlapped with the last backward
   bool in_place = false;
   // dp: ZeRO stage. 0 = replicated (reference), 1 = optimizer state sharded

@@ -87,6 +87,8 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "                         one-forward-one-backward, or interleaved 1F1B over --pp-virtual V chunks per stage\n"
      << "  --pp-virtual V         interleaved: model chunks per stage (default 2)\n"
      << "  --ep-overlap           hybrid_3d_moe: two half-microbatches, each one's all-to-all under the other's compute\n"
+     << "  --ep-imbalance A       moe: skewed expert load, rank j of an EP group gets a 1/(j+1)^A share of\n"
+     << "                         every dispatch (all-to-allv over grouped send/recv); 0 = uniform (reference)\n"
      << "  --dp-buckets K         hybrids: DP all-reduce buckets overlapped with the last backward\n"
      << "                         (hybrid_cp: gradient buckets by layer, overlapped with the backward)\n"
      << "  --cp-algo ring|ulysses hybrid_cp: KV blocks around a P2P ring, or all-to-alls over heads\n"
@@ -157,6 +159,9 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
       o.sequence_parallel = true;
     } else if (a == "--ep-overlap") {
       o.ep_overlap = true;
+    } else if (is("--ep-imbalance")) {
+      o.ep_imbalance = to_double(val("ep-imbalance"), "ep-imbalance");
+      if (o.ep_imbalance < 0) DLNB_THROW("--ep-imbalance must be >= 0");
     } else if (is("--pp-schedule")) {
       o.pp_schedule = val("pp-schedule");
     } else if (is("--pp-virtual")) {

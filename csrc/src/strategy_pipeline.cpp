@@ -29,6 +29,8 @@
 //   * the DP all-reduce can be split into --dp-buckets buckets that overlap
 //     the last microbatch's backward;
 //   * S = 1 is valid (no P2P), unlike the reference.
+#include <cmath>
+
 #include "dlnb/strategy.hpp"
 
 namespace dlnb {
@@ -81,6 +83,8 @@ class Pipeline : public Strategy {
     interleaved_ = o.pp_schedule == "interleaved";
     V_ = interleaved_ ? o.pp_virtual : 1;
     ep_overlap_ = o.ep_overlap && has_ep_ && !reference_;
+    skew_ = has_ep_ && E_ > 1 && o.ep_imbalance > 0;
+    DLNB_REQUIRE(!(skew_ && ep_overlap_), "--ep-imbalance and --ep-overlap cannot be combined");
     DLNB_REQUIRE(!(ep_overlap_ && has_tp_), "--ep-overlap is not supported with tensor parallelism (hybrid_4d)");
     DLNB_REQUIRE(!((one_f_one_b_ || interleaved_) && reference_), "--pp-schedule " << o.pp_schedule
                                                                                    << " needs --schedule overlap");
@@ -135,6 +139,20 @@ class Pipeline : public Strategy {
       const int top_k = 2;  // hybrid_3d_moe.cpp:357
       a2a_ = (spmb_ * st.seq_len * top_k * st.embedded_dim) / E_ / T_;
       if (has_tp_) tp_ar_ = pipe_ / T_;
+      if (has_ep_ && E_ > 1 && o.ep_imbalance > 0) {
+        // Expert-load skew: every rank sends the same a2a_*E_ elements per
+        // dispatch, split over the EP ranks by Zipf weights 1/(j+1)^A, so EP
+        // rank 0 (the hot experts) receives the most; the combine that
+        // follows each dispatch sends the tokens back (the transpose).
+        std::vector<double> w(static_cast<size_t>(E_));
+        double sw = 0;
+        for (int j = 0; j < E_; ++j) sw += (w[static_cast<size_t>(j)] = std::pow(1.0 + j, -o.ep_imbalance));
+        const uint64_t total = a2a_ * static_cast<uint64_t>(E_);
+        uint64_t used = 0;
+        skew_counts_.assign(static_cast<size_t>(E_), 0);
+        for (int j = 0; j < E_; ++j) used += (skew_counts_[static_cast<size_t>(j)] = static_cast<uint64_t>(total * w[static_cast<size_t>(j)] / sw));
+        skew_counts_[0] += total - used;
+      }
     }
 
     sp_ = has_tp_ && o.sequence_parallel;
@@ -191,8 +209,9 @@ class Pipeline : public Strategy {
       if (has_ep_) {
         std::vector<int> m;
         for (int e = 0; e < E_; ++e) m.push_back(base + e * T_ + tp_id_);
+        const uint64_t cap = skew_counts_.empty() ? a2a_ * E_ : std::max<uint64_t>(a2a_ * E_, skew_counts_[0]);
         ep_comm_ = ctx.comms->create("ep/" + where + "/" + std::to_string(tp_id_), m,
-                                     std::max<uint64_t>(a2a_ * E_, ne_) * es_, false);
+                                     std::max<uint64_t>(cap, ne_) * es_, !skew_counts_.empty());
       }
     }
     {
@@ -224,8 +243,10 @@ class Pipeline : public Strategy {
       dev.fill_random(tp_buf_.data(), tp_shard_ * T_, ctx.wire, 4300, *compute_);
     }
     if (has_ep_) {
-      ep_send_ = dev.alloc(a2a_ * E_ * es_);
-      ep_recv_ = dev.alloc(a2a_ * E_ * es_);
+      // skew: the hot rank receives E_ * skew_counts_[0] in a dispatch
+      const uint64_t n = skew_counts_.empty() ? a2a_ * E_ : std::max<uint64_t>(a2a_ * E_, skew_counts_[0] * E_);
+      ep_send_ = dev.alloc(n * es_);
+      ep_recv_ = dev.alloc(n * es_);
       dev.fill_random(ep_send_.data(), a2a_ * E_, ctx.wire, 4400, *compute_);
       if (ep_overlap_) {
         // The half-microbatch all-to-alls share the DP lane instead of a
@@ -370,8 +391,33 @@ class Pipeline : public Strategy {
 
   void ep_alltoall() {
     int t = timers_->begin(*compute_);
-    ep_comm_->all_to_all(ep_send_.data(), ep_recv_.data(), a2a_, ctx_->wire, *compute_);
+    if (skew_)
+      ep_alltoallv();
+    else
+      ep_comm_->all_to_all(ep_send_.data(), ep_recv_.data(), a2a_, ctx_->wire, *compute_);
     timers_->end(t, *compute_, "ep_comm_time");
+  }
+
+  // --ep-imbalance: all-to-allv as one group of sends / receives. Even calls
+  // are dispatches (to EP rank j: skew_counts_[j]), odd calls the matching
+  // combines (every peer sends this rank's share back). The block for this
+  // rank itself stays local.
+  void ep_alltoallv() {
+    const bool dispatch = (skew_call_++ & 1) == 0;
+    const int me = ep_id_;
+    ep_comm_->group_start();
+    size_t so = 0, ro = 0;
+    for (int j = 0; j < E_; ++j) {
+      const uint64_t send_n = dispatch ? skew_counts_[static_cast<size_t>(j)] : skew_counts_[static_cast<size_t>(me)];
+      const uint64_t recv_n = dispatch ? skew_counts_[static_cast<size_t>(me)] : skew_counts_[static_cast<size_t>(j)];
+      if (j != me) {
+        if (send_n) ep_comm_->send(ep_send_.at(so * es_), send_n, ctx_->wire, j, *compute_);
+        if (recv_n) ep_comm_->recv(ep_recv_.at(ro * es_), recv_n, ctx_->wire, j, *compute_);
+      }
+      so += send_n;
+      ro += recv_n;
+    }
+    ep_comm_->group_end();
   }
 
   // Half-microbatch all-to-all (--ep-overlap): half hh owns its own slice of
@@ -756,6 +802,12 @@ class Pipeline : public Strategy {
     if (has_ep_) {
       g["ep_alltoall_size_bytes"] = a2a_ * es_;
       g["ep_allreduce_size_bytes"] = ne_ * es_;
+      if (skew_) {
+        g["ep_imbalance"] = ctx.opt.ep_imbalance;
+        Json c = Json::array();
+        for (uint64_t v : skew_counts_) c.push_back(static_cast<double>(v * es_));
+        g["ep_dispatch_bytes_per_peer"] = c;  // sent by every rank to EP rank j
+      }
     }
     g["dp_allreduce_size_bytes"] = dp_ar_ * es_;
     g["pp_schedule"] = ctx.opt.pp_schedule;
@@ -800,6 +852,9 @@ class Pipeline : public Strategy {
   bool one_f_one_b_ = false, interleaved_ = false;
   int V_ = 1, layers_per_chunk_ = 0;
   bool ep_overlap_ = false;
+  bool skew_ = false;                   // --ep-imbalance > 0
+  std::vector<uint64_t> skew_counts_;   // elements every rank dispatches to EP rank j
+  uint64_t skew_call_ = 0;
   Stream* ep_stream_ = nullptr;  // = dp_stream_ (see setup)
   std::unique_ptr<Event> chunk_done_[2], a2a_done_[2];
   uint64_t spmb_ = 0, pipe_ = 0, dp_ar_ = 0, tp_ar_ = 0, ne_ = 0, a2a_ = 0;

@@ -7,6 +7,7 @@ keys, timer counts, and timing sanity (an iteration can not
 be shorter than its compute).
 """
 import os
+import subprocess
 
 import pytest
 
@@ -403,3 +404,24 @@ def test_extensions_other_wire_dtypes_and_reference_schedule(data_dir):
     d = run(4, "hybrid_4d", "tiny_moe_8_bfloat16", 2, 2, 2, 1, data_dir, "-w", 0, "-r", 1, "--pp-schedule", "interleaved",
             "--pp-virtual", 2)
     assert d["global"]["pp_virtual_stages"] == 2
+
+
+@pytest.mark.parametrize("w,params,alpha", [(4, (1, 2, 4), 1.0), (8, (2, 2, 4), 2.0)])
+def test_moe_expert_imbalance(w, params, alpha, data_dir):
+    """--ep-imbalance: Zipf-skewed dispatch as an all-to-allv (grouped send/recv)."""
+    d = run(w, "hybrid_3d_moe", "tiny_moe_8_bfloat16", *params, data_dir, "-w", 1, "-r", 2, "--ep-imbalance", alpha)
+    g = d["global"]
+    E = params[2]
+    per = g["ep_dispatch_bytes_per_peer"]
+    assert g["ep_imbalance"] == alpha and len(per) == E
+    assert all(a > b for a, b in zip(per, per[1:]))  # EP rank 0 hosts the hot experts
+    assert sum(per) == g["ep_alltoall_size_bytes"] * E  # same tokens as the uniform all-to-all
+    assert per[0] / per[-1] == pytest.approx(E ** alpha, rel=0.01)
+    for r in d["ranks"]:
+        assert r["ep_comm_time"] and all(t >= 0 for t in r["ep_comm_time"])
+
+
+def test_moe_expert_imbalance_argument_checks(data_dir):
+    p = subprocess.run([os.path.join(BIN, "hybrid_3d_moe"), "tiny_moe_8_bfloat16", "1", "2", "1", data_dir,
+                        "--ep-imbalance", "-1"], capture_output=True, text=True)
+    assert p.returncode == 1 and "ep-imbalance" in p.stderr

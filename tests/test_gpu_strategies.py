@@ -104,6 +104,13 @@ LOOPBACK_CASES = [
 ]
 
 
+def test_moe_expert_imbalance_loopback_on_gpu(data_dir):
+    doc = engine.run("hybrid_3d_moe", "tiny_moe_8_bfloat16", 1, 2, 4, base_path=data_dir, warmup=1, runs=2,
+                     compute="gemm", backend="loopback", ranks=4, ep_imbalance=1.0, quiet=True)
+    per = doc["global"]["ep_dispatch_bytes_per_peer"]
+    assert len(per) == 4 and per[0] > per[-1]
+
+
 @pytest.mark.parametrize("strategy,model,params,w", LOOPBACK_CASES)
 def test_strategy_loopback_on_gpu(strategy, model, params, w, data_dir):
     doc = engine.run(strategy, model, *params, base_path=data_dir, warmup=1, runs=2, compute="gemm",
