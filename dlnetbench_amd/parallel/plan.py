@@ -129,9 +129,25 @@ def plan_fsdp(st: ModelStats, world: int, U: int, F: int, wire: str = "bf16") ->
     return p
 
 
+def ep_dispatch_counts(a2a: int, E: int, alpha: float) -> List[int]:
+    """--ep-imbalance: elements every rank dispatches to EP rank j (Zipf 1/(j+1)^alpha
+    of the uniform total a2a*E; the remainder goes to rank 0), as strategy_pipeline.cpp."""
+    total = a2a * E
+    if alpha <= 0 or E <= 1:
+        return [a2a] * E
+    w = [(1.0 + j) ** -alpha for j in range(E)]
+    sw = sum(w)
+    c = [int(total * x / sw) for x in w]
+    c[0] += total - sum(c)
+    return c
+
+
 def plan_hybrid(st: ModelStats, world: int, kind: str, S: int, mb: int, inner: int = 1, layers: int = 0,
-                wire: str = "bf16", tp_granularity: str = "microbatch", experts: int = 1) -> Plan:
-    """hybrid_4d: inner = T (tensor shards), experts = E (expert shards); TP fastest, then EP."""
+                wire: str = "bf16", tp_granularity: str = "microbatch", experts: int = 1,
+                ep_imbalance: float = 0.0) -> Plan:
+    """hybrid_4d: inner = T (tensor shards), experts = E (expert shards); TP fastest, then EP.
+    ep_imbalance > 0 (MoE): the all-to-all becomes an all-to-allv; the message's
+    wire_bytes stay the uniform total and `ep_dispatch_elements_per_peer` gives the split."""
     if kind == "hybrid_4d":
         return _plan_4d(st, world, S, mb, inner, experts, layers, wire, tp_granularity)
     es = WIRE_BYTES[wire]
@@ -164,6 +180,8 @@ def plan_hybrid(st: ModelStats, world: int, kind: str, S: int, mb: int, inner: i
         dp_ar = ne + ((P - st.non_expert_size) // S) // inner
         a2a = (spmb * st.seq_len * 2 * st.hidden) // inner
         p.messages.append(Message("ep_alltoall", "alltoall", inner, a2a, 2 * (layers // S) * mb * 2, a2a * inner * es))
+        if ep_imbalance > 0:
+            params["ep_dispatch_elements_per_peer"] = ep_dispatch_counts(a2a, inner, ep_imbalance)
         p.messages.append(Message("ep_nonexpert_allreduce", "allreduce", inner, ne, 1, ne * es))
     p.messages.append(Message("dp_allreduce", "allreduce", world // (S * inner), dp_ar, 1, dp_ar * es))
     p.memory_bytes = (8 * pipe + 2 * dp_ar) * es
@@ -248,6 +266,7 @@ def main(argv=None) -> int:
     ap.add_argument("--wire", default="bf16")
     ap.add_argument("--zero", type=int, default=0, help="dp: ZeRO stage 0|1|2")
     ap.add_argument("--cp-algo", default="ring", choices=["ring", "ulysses"])
+    ap.add_argument("--ep-imbalance", type=float, default=0.0, help="hybrid_3d_moe: Zipf exponent of the expert load")
     ap.add_argument("--predict", action="store_true",
                     help="dp / fsdp: add the xGMI cost-model prediction (parallel/xgmi_model.py) at W = 1, 2, 4, 8")
     ap.add_argument("--link-gbps", type=float, default=153.0, help="xGMI bandwidth per link and direction")
@@ -273,7 +292,7 @@ def main(argv=None) -> int:
             inner = a.params[2] if len(a.params) > 2 else 1
             experts = a.params[3] if len(a.params) > 3 else 1
             pl = plan_hybrid(st, a.world, a.strategy, a.params[0], a.params[1], inner, L, wire=a.wire,
-                             experts=experts)
+                             experts=experts, ep_imbalance=a.ep_imbalance)
     doc = pl.to_json()
     if a.predict and a.strategy in ("dp", "fsdp"):
         from . import xgmi_model as xm

@@ -139,7 +139,9 @@ def hybrid_dataframe(doc: dict, network: str = "mi355x"):
             row = {"network": network, "section": doc["section"], "model_name": g["model_name"],
                    "world_size": g["world_size"], "num_stages": g["num_stages"],
                    "num_microbatches": g["num_microbatches"], "dp_size": g["dp_size"], "rank": r["rank"],
-                   "stage_id": r.get("stage_id"), "run": i, "runtime": r["runtimes"][i]}
+                   "stage_id": r.get("stage_id"), "run": i, "runtime": r["runtimes"][i],
+                   "pp_schedule": g.get("pp_schedule", "gpipe"), "ep_imbalance": g.get("ep_imbalance", 0.0),
+                   "ep_id": r.get("ep_id")}
             for k in keys:
                 if k in r and r[k]:
                     per = len(r[k]) // runs

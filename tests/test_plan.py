@@ -194,3 +194,22 @@ def test_plan_cli_predict(capsys, root):
     d = json.loads(capsys.readouterr().out)
     by = d["xgmi_prediction"]["by_world"]
     assert set(by) == {"1", "2", "4", "8"} and by["1"]["exposed_ms"] == pytest.approx(0.0, abs=1e-9)
+
+
+def test_ep_dispatch_counts_match_the_native_run(data_dir):
+    """The planner's all-to-allv split equals what the native driver reports."""
+    import subprocess
+    bin_ = os.path.join(os.path.dirname(data_dir), "..", "build", "bin", "hybrid_3d_moe")
+    st = load_stats(os.path.join(data_dir, "model_stats", "tiny_moe_8_bfloat16.txt"))
+    pl = P.plan_hybrid(st, 4, "hybrid_3d_moe", 1, 2, 4, 4, ep_imbalance=1.0)
+    counts = pl.params["ep_dispatch_elements_per_peer"]
+    assert sum(counts) == pl.messages[0].elements * 4 and counts == sorted(counts, reverse=True)
+    assert P.ep_dispatch_counts(100, 4, 0.0) == [100] * 4
+    if not os.path.exists(bin_):
+        pytest.skip("native binaries not built")
+    p = subprocess.run([bin_, "tiny_moe_8_bfloat16", "1", "2", "4", data_dir, "--backend", "loopback-cpu", "--ranks",
+                        "4", "--ep-imbalance", "1.0", "-w", "0", "-r", "1", "--quiet"], capture_output=True, text=True,
+                       timeout=120, env={k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE")})
+    from dlnetbench_amd.utils import report
+    doc = next(iter(report.parse_output(p.stdout).values()))
+    assert doc["global"]["ep_dispatch_bytes_per_peer"] == [c * 2 for c in counts]
