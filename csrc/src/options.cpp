@@ -254,8 +254,9 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
                    o.num_cp_shards >= 1,
                "parallelism degrees must be >= 1");
   DLNB_REQUIRE(o.schedule == "overlap" || o.schedule == "reference", "--schedule must be overlap or reference");
-  DLNB_REQUIRE(o.pp_schedule == "gpipe" || o.pp_schedule == "1f1b" || o.pp_schedule == "interleaved",
-               "--pp-schedule must be gpipe, 1f1b or interleaved");
+  DLNB_REQUIRE(o.pp_schedule == "gpipe" || o.pp_schedule == "1f1b" || o.pp_schedule == "interleaved" ||
+                   o.pp_schedule == "dualpipe",
+               "--pp-schedule must be gpipe, 1f1b, interleaved or dualpipe");
   DLNB_REQUIRE(o.tp_granularity == "microbatch" || o.tp_granularity == "layer",
                "--tp-granularity must be microbatch or layer");
   DLNB_REQUIRE(o.comm_lanes == "single" || o.comm_lanes == "split", "--comm-lanes must be single or split");

@@ -81,13 +81,20 @@ class Pipeline : public Strategy {
     reference_ = o.schedule == "reference";
     one_f_one_b_ = o.pp_schedule == "1f1b";
     interleaved_ = o.pp_schedule == "interleaved";
+    dualpipe_ = o.pp_schedule == "dualpipe";
     V_ = interleaved_ ? o.pp_virtual : 1;
     ep_overlap_ = o.ep_overlap && has_ep_ && !reference_;
     skew_ = has_ep_ && E_ > 1 && o.ep_imbalance > 0;
     DLNB_REQUIRE(!(skew_ && ep_overlap_), "--ep-imbalance and --ep-overlap cannot be combined");
     DLNB_REQUIRE(!(ep_overlap_ && has_tp_), "--ep-overlap is not supported with tensor parallelism (hybrid_4d)");
-    DLNB_REQUIRE(!((one_f_one_b_ || interleaved_) && reference_), "--pp-schedule " << o.pp_schedule
-                                                                                   << " needs --schedule overlap");
+    DLNB_REQUIRE(!((one_f_one_b_ || interleaved_ || dualpipe_) && reference_),
+                 "--pp-schedule " << o.pp_schedule << " needs --schedule overlap");
+    if (dualpipe_) {
+      DLNB_REQUIRE(S_ >= 2 && S_ % 2 == 0, "--pp-schedule dualpipe needs an even number of stages (got " << S_ << ")");
+      DLNB_REQUIRE(mb_ % 2 == 0, "--pp-schedule dualpipe needs an even number of microbatches (half enter at each end)");
+      DLNB_REQUIRE(o.dp_buckets == 1, "--pp-schedule dualpipe does not split the DP all-reduce (--dp-buckets 1)");
+      DLNB_REQUIRE(!ep_overlap_, "--pp-schedule dualpipe cannot be combined with --ep-overlap");
+    }
     DLNB_REQUIRE(V_ >= 1, "--pp-virtual must be >= 1");
     DLNB_REQUIRE(ctx.have_arch, "hybrid strategies need models/<model>.json (layer count)");
     L_ = static_cast<int>(ctx.arch.num_layers);
@@ -155,6 +162,12 @@ class Pipeline : public Strategy {
       }
     }
 
+    if (dualpipe_) {
+      // every rank holds two chunks: stage s of the "down" copy and stage
+      // S-1-s of the "up" copy, so its gradients (and non-expert part) double
+      dp_ar_ *= 2;
+      ne_ *= 2;
+    }
     sp_ = has_tp_ && o.sequence_parallel;
     tp_shard_ = has_tp_ ? (tp_ar_ + T_ - 1) / T_ : 0;
     Device& dev = *ctx.dev;
@@ -219,6 +232,17 @@ class Pipeline : public Strategy {
       const int nbk = o.dp_buckets;
       dp_comm_ = ctx.comms->create(nm, dp_group(rank, inner_, S_, W), (dp_ar_ / nbk + 1) * es_, false);
       dp_stream_ = dev.create_stream(true);
+    }
+    if (dualpipe_) {
+      // Stage s and stage S-1-s hold the same two chunks (one per copy): their
+      // gradients are summed over this pair before the DP all-reduce.
+      const int lo = std::min(stage_, S_ - 1 - stage_);
+      std::vector<int> pair = {pp[lo], pp[S_ - 1 - lo]};
+      mirror_comm_ = ctx.comms->create("pp/mirror/" + std::to_string(dp_id_) + "/" + std::to_string(inner_id_) + "/" +
+                                           std::to_string(lo),
+                                       pair, dp_ar_ * es_, false);
+      build_dualpipe();
+      for (int k = 0; k < 2 * mb_; ++k) dpbuf_.push_back(dev.alloc(pipe_ * es_));
     }
 
     // Buffers.
@@ -288,6 +312,7 @@ class Pipeline : public Strategy {
     for (const char* k : {"pp_comm_time", "dp_comm_time", "pp_send_time", "pp_recv_time", "dp_exposed_time"})
       timers_->ensure(k);
     if (has_tp_) timers_->ensure("tp_comm_time");
+    if (dualpipe_) timers_->ensure("pp_mirror_time");
     if (sp_) {
       timers_->ensure("tp_ag_time");
       timers_->ensure("tp_rs_time");
@@ -515,6 +540,12 @@ class Pipeline : public Strategy {
     if (nbk == 1 || reference_) {
       compute_->record(*bucket_ready_[0]);
       dp_stream_->wait(*bucket_ready_[0]);
+      if (mirror_comm_) {
+        void* g = grad_.data();
+        int tm = timers_->begin(*dp_stream_);
+        mirror_comm_->all_reduce(g, g, dp_ar_, t, *dp_stream_);
+        timers_->end(tm, *dp_stream_, "pp_mirror_time");
+      }
       dp_allreduce_bucket(0, 1);
     }
     dp_stream_->record(*dp_done_);
@@ -708,8 +739,172 @@ class Pipeline : public Strategy {
     finish_iteration();
   }
 
+  // ---------------------------------------------------------- DualPipe
+  // Bidirectional pipeline (DeepSeek-V3's DualPipe, without its intra-chunk
+  // attention/MLP split): every rank holds stage s of a "down" copy of the
+  // model and stage S-1-s of an "up" copy; mb/2 microbatches enter at stage 0
+  // and mb/2 at stage S-1, so the pipeline fills from both ends and each
+  // link carries activations and gradients both ways at once. The order is a
+  // tick schedule every rank computes identically: per tick each rank runs at
+  // most one op, a backward if one is ready (oldest first), else a forward
+  // within its 1F1B in-flight cap (S - position in that copy), the direction
+  // with fewer forwards issued first. Each op's output is sent at the end of
+  // its tick and received by the neighbour at that same tick boundary into a
+  // buffer of its own, so every boundary's send/receive groups pair up among
+  // themselves (next link, then previous link: a chain, no cycle) - also for
+  // backends whose groups complete on the host. Stages s and S-1-s sum their
+  // gradients (pair all-reduce) before the DP all-reduce.
+  struct DpOp {
+    int dir = -1;  // 0 down, 1 up, -1 idle
+    int mb = 0;
+    bool bwd = false;
+  };
+
+  int dp_pos(int s, int dir) const { return dir == 0 ? s : S_ - 1 - s; }
+
+  void build_dualpipe() {
+    const int H = mb_ / 2;
+    // done tick per (stage, dir, mb) for F and B; -1 = not yet
+    std::vector<int> fdone(static_cast<size_t>(S_ * 2 * H), -1), bdone(fdone.size(), -1);
+    auto idx = [&](int s, int d, int i) { return static_cast<size_t>((s * 2 + d) * H + i); };
+    std::vector<int> nf(static_cast<size_t>(S_ * 2), 0), nb(nf.size(), 0);
+    dp_ticks_.clear();
+    int remaining = S_ * 2 * H * 2;
+    for (int t = 0; remaining > 0; ++t) {
+      DLNB_REQUIRE(t < 16 * (mb_ + S_) + 64, "dualpipe schedule did not converge");
+      std::vector<DpOp> row(static_cast<size_t>(S_));
+      for (int s = 0; s < S_; ++s) {
+        DpOp best;
+        // backward: oldest ready microbatch over both directions
+        for (int d = 0; d < 2; ++d) {
+          const int i = nb[static_cast<size_t>(s * 2 + d)];
+          if (i >= nf[static_cast<size_t>(s * 2 + d)]) continue;
+          const int fd = fdone[idx(s, d, i)];
+          if (fd < 0 || fd >= t) continue;
+          if (dp_pos(s, d) < S_ - 1) {
+            const int down = d == 0 ? s + 1 : s - 1;  // the next stage of this copy
+            const int bd = bdone[idx(down, d, i)];
+            if (bd < 0 || bd >= t) continue;
+          }
+          if (best.dir < 0 || i < best.mb) best = DpOp{d, i, true};
+        }
+        if (best.dir < 0) {
+          // forward: the direction with fewer forwards issued (ties: the copy
+          // whose first stage is nearer)
+          int order[2] = {0, 1};
+          const int f0 = nf[static_cast<size_t>(s * 2)], f1 = nf[static_cast<size_t>(s * 2 + 1)];
+          if (f1 < f0 || (f1 == f0 && dp_pos(s, 1) < dp_pos(s, 0))) std::swap(order[0], order[1]);
+          for (int d : order) {
+            const int i = nf[static_cast<size_t>(s * 2 + d)];
+            if (i >= H) continue;
+            if (i - nb[static_cast<size_t>(s * 2 + d)] >= S_ - dp_pos(s, d)) continue;  // in-flight cap
+            if (dp_pos(s, d) > 0) {
+              const int up = d == 0 ? s - 1 : s + 1;
+              const int fu = fdone[idx(up, d, i)];
+              if (fu < 0 || fu >= t) continue;
+            }
+            best = DpOp{d, i, false};
+            break;
+          }
+        }
+        if (best.dir >= 0) {
+          if (best.bwd) {
+            bdone[idx(s, best.dir, best.mb)] = t;
+            ++nb[static_cast<size_t>(s * 2 + best.dir)];
+          } else {
+            fdone[idx(s, best.dir, best.mb)] = t;
+            ++nf[static_cast<size_t>(s * 2 + best.dir)];
+          }
+          --remaining;
+        }
+        row[static_cast<size_t>(s)] = best;
+      }
+      dp_ticks_.push_back(row);
+    }
+    // compute-only makespan of this order (the strategy's floor)
+    std::vector<double> ffin(fdone.size(), 0), bfin(fdone.size(), 0), free_at(static_cast<size_t>(S_), 0);
+    double span = 0;
+    for (const auto& row : dp_ticks_)
+      for (int s = 0; s < S_; ++s) {
+        const DpOp& op = row[static_cast<size_t>(s)];
+        if (op.dir < 0) continue;
+        double start = free_at[static_cast<size_t>(s)];
+        const int d = op.dir, i = op.mb;
+        if (!op.bwd) {
+          if (dp_pos(s, d) > 0) start = std::max(start, ffin[idx(d == 0 ? s - 1 : s + 1, d, i)]);
+          ffin[idx(s, d, i)] = start + fwd_mb_us_;
+          free_at[static_cast<size_t>(s)] = ffin[idx(s, d, i)];
+        } else {
+          start = std::max(start, ffin[idx(s, d, i)]);
+          if (dp_pos(s, d) < S_ - 1) start = std::max(start, bfin[idx(d == 0 ? s + 1 : s - 1, d, i)]);
+          bfin[idx(s, d, i)] = start + bwd_mb_us_;
+          free_at[static_cast<size_t>(s)] = bfin[idx(s, d, i)];
+        }
+        span = std::max(span, free_at[static_cast<size_t>(s)]);
+      }
+    dp_floor_us_ = span;
+  }
+
+  // Event / buffer slot of (dir, mb): activations [0, mb), gradients [mb, 2 mb).
+  int dp_slot(int dir, int i) const { return dir * (mb_ / 2) + i; }
+
+  // One link's group at a tick boundary: what this rank's op of the tick
+  // sends over it, and what the neighbour's op of the tick sends to us.
+  void dualpipe_link(bool next, const DpOp& mine, const DpOp& theirs) {
+    Communicator* c = next ? next_.get() : prev_.get();
+    if (!c) return;
+    Stream& ls = next ? *next_stream_ : *prev_stream_;
+    const int peer = next ? next_peer_ : prev_peer_;
+    // our output travels towards `next` for down-forwards and up-backwards
+    const bool send = mine.dir >= 0 && ((mine.dir == 0) != mine.bwd) == next &&
+                      (mine.bwd ? dp_pos(stage_, mine.dir) > 0 : dp_pos(stage_, mine.dir) < S_ - 1);
+    const int nstage = stage_ + (next ? 1 : -1);
+    const bool recv = theirs.dir >= 0 && ((theirs.dir == 0) != theirs.bwd) == !next &&
+                      (theirs.bwd ? dp_pos(nstage, theirs.dir) > 0 : dp_pos(nstage, theirs.dir) < S_ - 1);
+    if (!send && !recv) return;
+    const DType t = ctx_->wire;
+    if (send) ls.wait(mine.bwd ? *bwd_done_[dp_slot(mine.dir, mine.mb)] : *fwd_done_[dp_slot(mine.dir, mine.mb)]);
+    int tk = timers_->begin(ls);
+    c->group_start();
+    if (send) c->send(next ? act_out_[0].data() : grad_out_[0].data(), pipe_, t, peer, ls);
+    const int slot = recv ? dp_slot(theirs.dir, theirs.mb) : 0;
+    if (recv) c->recv(dpbuf_[static_cast<size_t>(theirs.bwd ? mb_ + slot : slot)].data(), pipe_, t, peer, ls);
+    c->group_end();
+    timers_->end(tk, ls, send ? "pp_send_time" : "pp_recv_time");
+    if (recv) ls.record(theirs.bwd ? *recv_b_[slot] : *recv_f_[slot]);
+  }
+
+  void enqueue_dualpipe() {
+    for (const auto& row : dp_ticks_) {
+      const DpOp& op = row[static_cast<size_t>(stage_)];
+      if (op.dir >= 0) {
+        const int slot = dp_slot(op.dir, op.mb);
+        if (!op.bwd) {
+          if (dp_pos(stage_, op.dir) > 0)
+            timers_->stall(*compute_, *recv_f_[slot], "pp_comm_time");
+          else
+            timers_->add("pp_comm_time", 0.0);
+          micro_compute(fwd_mb_us_, fwd_mb_flops_);
+          compute_->record(*fwd_done_[slot]);
+        } else {
+          if (dp_pos(stage_, op.dir) < S_ - 1)
+            timers_->stall(*compute_, *recv_b_[slot], "pp_comm_time");
+          else
+            timers_->add("pp_comm_time", 0.0);
+          micro_compute(bwd_mb_us_, bwd_mb_flops_);
+          compute_->record(*bwd_done_[slot]);
+        }
+      }
+      if (next_) dualpipe_link(true, op, row[static_cast<size_t>(stage_ + 1)]);
+      if (prev_) dualpipe_link(false, op, row[static_cast<size_t>(stage_ - 1)]);
+    }
+    finish_iteration();
+  }
+
   void enqueue_iteration() override {
-    if (interleaved_)
+    if (dualpipe_)
+      enqueue_dualpipe();
+    else if (interleaved_)
       enqueue_interleaved();
     else if (one_f_one_b_)
       enqueue_1f1b();
@@ -755,6 +950,7 @@ class Pipeline : public Strategy {
 
   double compute_floor_us(const Context&) const override {
     // GPipe / 1F1B: (mb + S - 1)(f + b); interleaved: the bubble / V
+    if (dualpipe_) return dp_floor_us_;
     return (mb_ + static_cast<double>(S_ - 1) / V_) * (fwd_mb_us_ + bwd_mb_us_);
   }
 
@@ -812,6 +1008,7 @@ class Pipeline : public Strategy {
     g["dp_allreduce_size_bytes"] = dp_ar_ * es_;
     g["pp_schedule"] = ctx.opt.pp_schedule;
     if (interleaved_) g["pp_virtual_stages"] = V_;
+    if (dualpipe_) g["dualpipe_ticks"] = static_cast<uint64_t>(dp_ticks_.size());
     if (has_ep_) g["ep_overlap"] = ep_overlap_;
     if (has_tp_) g["tp_granularity"] = ctx.opt.tp_granularity;
     g["device"] = ctx.dev->kind() == DeviceKind::CPU ? "CPU" : "GPU";
@@ -832,6 +1029,7 @@ class Pipeline : public Strategy {
     r["pp_send_time"] = timers_->values_json("pp_send_time");
     r["pp_recv_time"] = timers_->values_json("pp_recv_time");
     r["dp_exposed_time"] = timers_->values_json("dp_exposed_time");
+    if (dualpipe_) r["pp_mirror_time"] = timers_->values_json("pp_mirror_time");
     r["stage_id"] = stage_;
     if (has_tp_) r["tp_id"] = tp_id_;
     if (has_ep_) r["ep_id"] = ep_id_;
@@ -849,7 +1047,11 @@ class Pipeline : public Strategy {
   bool has_tp_ = false, has_ep_ = false, sp_ = false;
   uint64_t tp_shard_ = 0;  // ceil(tp_ar_ / T): sequence-parallel shard
   bool reference_ = false;
-  bool one_f_one_b_ = false, interleaved_ = false;
+  bool one_f_one_b_ = false, interleaved_ = false, dualpipe_ = false;
+  std::vector<std::vector<DpOp>> dp_ticks_;  // [tick][stage]
+  double dp_floor_us_ = 0;
+  std::vector<Buffer> dpbuf_;  // receive buffers per (dir, microbatch): activations, then gradients
+  std::unique_ptr<Communicator> mirror_comm_;
   int V_ = 1, layers_per_chunk_ = 0;
   bool ep_overlap_ = false;
   bool skew_ = false;                   // --ep-imbalance > 0

@@ -118,6 +118,7 @@ XGMI_STRATS = [  # strategy, model, positional args, extra flags, ranks
     ("hybrid_3d", "tiny_dense_8_bfloat16", ["2", "2", "2"], ["--sequence-parallel"], 4),
     ("hybrid_2d", "tiny_deep_8_bfloat16", ["2", "4"], ["--pp-schedule", "interleaved"], 2),
     ("hybrid_3d_moe", "tiny_moe_8_bfloat16", ["1", "2", "2"], ["--ep-imbalance", "1.0"], 2),
+    ("hybrid_2d", "tiny_deep_8_bfloat16", ["2", "4"], ["--pp-schedule", "dualpipe"], 2),
 ]
 
 

@@ -425,3 +425,35 @@ def test_moe_expert_imbalance_argument_checks(data_dir):
     p = subprocess.run([os.path.join(BIN, "hybrid_3d_moe"), "tiny_moe_8_bfloat16", "1", "2", "1", data_dir,
                         "--ep-imbalance", "-1"], capture_output=True, text=True)
     assert p.returncode == 1 and "ep-imbalance" in p.stderr
+
+
+@pytest.mark.parametrize("w,prog,model,params", [(2, "hybrid_2d", "tiny_deep_8_bfloat16", (2, 4)),
+                                                 (4, "hybrid_2d", "tiny_deep_8_bfloat16", (4, 8)),
+                                                 (8, "hybrid_2d", "tiny_deep_8_bfloat16", (4, 8)),
+                                                 (8, "hybrid_3d", "tiny_dense_8_bfloat16", (2, 4, 2)),
+                                                 (8, "hybrid_3d_moe", "tiny_moe_8_bfloat16", (2, 4, 2))])
+def test_dualpipe(w, prog, model, params, data_dir):
+    """--pp-schedule dualpipe: bidirectional pipeline, mirrored stage pairs sum their gradients."""
+    d = run(w, prog, model, *params, data_dir, "-w", 1, "-r", 2, "--pp-schedule", "dualpipe")
+    g = d["global"]
+    assert g["pp_schedule"] == "dualpipe" and g["dualpipe_ticks"] >= params[1]
+    it = g["dlnb"]["iteration"]
+    S, mb = params[0], params[1]
+    f, b = g["fwd_rt_per_microbatch"], g["bwd_rt_per_microbatch"]
+    # the schedule's compute floor: at least mb (f + b), and below 1F1B's (mb + S - 1)(f + b) for S >= 4
+    assert it["compute_floor_ms"] * 1e3 >= mb * (f + b) - 1e-6
+    if S >= 4:
+        assert it["compute_floor_ms"] * 1e3 < (mb + S - 1) * (f + b)
+    for r in d["ranks"]:
+        assert len(r["pp_mirror_time"]) == 2 and len(r["runtimes"]) == 2
+
+
+@pytest.mark.parametrize("params,extra,msg", [((3, 6), [], "even number of stages"),
+                                              ((2, 3), [], "even number of microbatches"),
+                                              ((2, 4), ["--dp-buckets", "2"], "dp-buckets")])
+def test_dualpipe_argument_checks(params, extra, msg, data_dir):
+    code, outs = launch.launch(params[0], [os.path.join(BIN, "hybrid_2d"), "tiny_deep_8_bfloat16",
+                                           *map(str, params), data_dir, "--pp-schedule", "dualpipe", *extra,
+                                           "--quiet"], timeout=60, capture=True)
+    text = "".join(o or "" for o in outs)
+    assert code != 0 and msg in text, text[-2000:]

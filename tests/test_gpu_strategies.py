@@ -104,6 +104,14 @@ LOOPBACK_CASES = [
 ]
 
 
+def test_dualpipe_loopback_on_gpu(data_dir):
+    doc = engine.run("hybrid_2d", "tiny_deep_8_bfloat16", 4, 8, base_path=data_dir, warmup=1, runs=2,
+                     compute="gemm", backend="loopback", ranks=4, pp_schedule="dualpipe", quiet=True)
+    g = doc["global"]
+    assert g["pp_schedule"] == "dualpipe" and len(doc["ranks"]) == 4
+    assert g["dlnb"]["iteration"]["median_ms"] >= 0.9 * g["dlnb"]["iteration"]["compute_floor_ms"]
+
+
 def test_moe_expert_imbalance_loopback_on_gpu(data_dir):
     doc = engine.run("hybrid_3d_moe", "tiny_moe_8_bfloat16", 1, 2, 4, base_path=data_dir, warmup=1, runs=2,
                      compute="gemm", backend="loopback", ranks=4, ep_imbalance=1.0, quiet=True)

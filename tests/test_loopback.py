@@ -132,6 +132,8 @@ def test_hybrid_2d_deep_pipeline_loopback(sched, data_dir):
     ("hybrid_cp", "tiny_dense_8_bfloat16", (4,), 4, ("--cp-algo", "ulysses")),
     ("hybrid_3d_moe", "tiny_moe_8_bfloat16", (1, 2, 4), 4, ("--ep-imbalance", "1.0")),
     ("hybrid_4d", "tiny_moe_8_bfloat16", (2, 2, 2, 2), 8, ("--ep-imbalance", "1.5")),
+    ("hybrid_2d", "tiny_deep_8_bfloat16", (4, 8), 8, ("--pp-schedule", "dualpipe")),
+    ("hybrid_3d_moe", "tiny_moe_8_bfloat16", (2, 4, 2), 8, ("--pp-schedule", "dualpipe", "--ep-imbalance", "1")),
 ])
 def test_hybrids_loopback(prog, model, params, w, extra, data_dir):
     d = run(w, prog, model, *params, data_dir, "-w", 1, "-r", 2, *extra)
