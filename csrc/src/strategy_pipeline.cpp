@@ -746,13 +746,16 @@ class Pipeline : public Strategy {
   // and mb/2 at stage S-1, so the pipeline fills from both ends and each
   // link carries activations and gradients both ways at once. The order is a
   // tick schedule every rank computes identically: per tick each rank runs at
-  // most one op, a backward if one is ready (oldest first), else a forward
-  // within its 1F1B in-flight cap (S - position in that copy), the direction
-  // with fewer forwards issued first. Each op's output is sent at the end of
-  // its tick and received by the neighbour at that same tick boundary into a
-  // buffer of its own, so every boundary's send/receive groups pair up among
-  // themselves (next link, then previous link: a chain, no cycle) - also for
-  // backends whose groups complete on the host. Stages s and S-1-s sum their
+  // most one op - a forward within its 1F1B in-flight cap (S - position in
+  // that copy: at most S + 1 activations per rank, DualPipe's budget), the
+  // copy with fewer forwards issued first, else a backward (oldest first).
+  // Forward-first comes within a few (f + b) of mb (f + b) + (S/2 - 1)(f + b)
+  // and beats 1F1B's (mb + S - 1)(f + b) (schedule_sim.py); backward-first
+  // stalls the steady state. Each op's output is sent at the end of its tick
+  // and received by the neighbour at that same tick boundary into a buffer of
+  // its own, so every boundary's send/receive groups pair up among themselves
+  // (next link, then previous link: a chain, no cycle) - also for backends
+  // whose groups complete on the host. Stages s and S-1-s sum their
   // gradients (pair all-reduce) before the DP all-reduce.
   struct DpOp {
     int dir = -1;  // 0 down, 1 up, -1 idle
@@ -775,21 +778,8 @@ class Pipeline : public Strategy {
       std::vector<DpOp> row(static_cast<size_t>(S_));
       for (int s = 0; s < S_; ++s) {
         DpOp best;
-        // backward: oldest ready microbatch over both directions
-        for (int d = 0; d < 2; ++d) {
-          const int i = nb[static_cast<size_t>(s * 2 + d)];
-          if (i >= nf[static_cast<size_t>(s * 2 + d)]) continue;
-          const int fd = fdone[idx(s, d, i)];
-          if (fd < 0 || fd >= t) continue;
-          if (dp_pos(s, d) < S_ - 1) {
-            const int down = d == 0 ? s + 1 : s - 1;  // the next stage of this copy
-            const int bd = bdone[idx(down, d, i)];
-            if (bd < 0 || bd >= t) continue;
-          }
-          if (best.dir < 0 || i < best.mb) best = DpOp{d, i, true};
-        }
-        if (best.dir < 0) {
-          // forward: the direction with fewer forwards issued (ties: the copy
+        {
+          // forward first: the direction with fewer forwards issued (ties: the copy
           // whose first stage is nearer)
           int order[2] = {0, 1};
           const int f0 = nf[static_cast<size_t>(s * 2)], f1 = nf[static_cast<size_t>(s * 2 + 1)];
@@ -805,6 +795,21 @@ class Pipeline : public Strategy {
             }
             best = DpOp{d, i, false};
             break;
+          }
+        }
+        if (best.dir < 0) {
+          // else a backward: the oldest ready microbatch over both directions
+          for (int d = 0; d < 2; ++d) {
+            const int i = nb[static_cast<size_t>(s * 2 + d)];
+            if (i >= nf[static_cast<size_t>(s * 2 + d)]) continue;
+            const int fd = fdone[idx(s, d, i)];
+            if (fd < 0 || fd >= t) continue;
+            if (dp_pos(s, d) < S_ - 1) {
+              const int down = d == 0 ? s + 1 : s - 1;  // the next stage of this copy
+              const int bd = bdone[idx(down, d, i)];
+              if (bd < 0 || bd >= t) continue;
+            }
+            if (best.dir < 0 || i < best.mb) best = DpOp{d, i, true};
           }
         }
         if (best.dir >= 0) {

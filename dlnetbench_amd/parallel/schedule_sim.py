@@ -1,7 +1,7 @@
 """Discrete-event model of the pipeline schedules' enqueue logic.
 
 Mirrors csrc/src/strategy_pipeline.cpp (enqueue_gpipe / enqueue_1f1b /
-enqueue_interleaved): per rank a compute stream and two link streams (prev,
+enqueue_interleaved / enqueue_dualpipe): per rank a compute stream and two link streams (prev,
 next) executing their operations in order; compute waits on receive events
 and on the send of the buffer it overwrites; a link operation is a group of
 at most one send and one receive that completes when every matching
@@ -130,6 +130,135 @@ def build(S: int, mb: int, V: int, f: float, b: float, sched: str) -> Dict[Tuple
                 nxt(-1, j) if s < S - 1 else None
                 bwd(j)
                 prv(j, -1) if s > 0 else None
+    return streams
+
+
+def dualpipe_ticks(S: int, mb: int) -> List[List[tuple]]:
+    """The DualPipe tick schedule (build_dualpipe in strategy_pipeline.cpp): row t holds, per stage, None or
+    (dir, microbatch, is_backward). dir 0 = the "down" copy (stage s at position s), 1 = the "up" copy
+    (position S-1-s); mb/2 microbatches per copy. A forward within the 1F1B in-flight cap S - position
+    (the copy with fewer forwards issued first), else the oldest ready backward."""
+    H = mb // 2
+
+    def pos(s, d):
+        return s if d == 0 else S - 1 - s
+
+    fdone, bdone = {}, {}
+    nf = [[0, 0] for _ in range(S)]
+    nb = [[0, 0] for _ in range(S)]
+    ticks, remaining, t = [], S * 2 * H * 2, 0
+    while remaining:
+        assert t < 16 * (mb + S) + 64, "dualpipe schedule did not converge"
+        row = []
+        for s in range(S):
+            best = None
+            order = [0, 1]
+            if nf[s][1] < nf[s][0] or (nf[s][1] == nf[s][0] and pos(s, 1) < pos(s, 0)):
+                order = [1, 0]
+            for d in order:
+                i = nf[s][d]
+                if i >= H or i - nb[s][d] >= S - pos(s, d):
+                    continue
+                if pos(s, d) > 0 and fdone.get((s - 1 if d == 0 else s + 1, d, i), t) >= t:
+                    continue
+                best = (d, i, False)
+                break
+            if best is None:
+                for d in (0, 1):
+                    i = nb[s][d]
+                    if i >= nf[s][d] or fdone.get((s, d, i), t) >= t:
+                        continue
+                    if pos(s, d) < S - 1 and bdone.get((s + 1 if d == 0 else s - 1, d, i), t) >= t:
+                        continue
+                    if best is None or i < best[1]:
+                        best = (d, i, True)
+            if best is not None:
+                d, i, bw = best
+                if bw:
+                    bdone[(s, d, i)] = t
+                    nb[s][d] += 1
+                else:
+                    fdone[(s, d, i)] = t
+                    nf[s][d] += 1
+                remaining -= 1
+            row.append(best)
+        ticks.append(row)
+        t += 1
+    return ticks
+
+
+def dualpipe_floor(S: int, mb: int, f: float, b: float) -> float:
+    """Compute-only makespan of the tick order (the driver's compute_floor_us for dualpipe)."""
+    ffin, bfin, free, span = {}, {}, [0.0] * S, 0.0
+    for row in dualpipe_ticks(S, mb):
+        for s, op in enumerate(row):
+            if op is None:
+                continue
+            d, i, bw = op
+            start = free[s]
+            up, down = (s - 1, s + 1) if d == 0 else (s + 1, s - 1)
+            pos = s if d == 0 else S - 1 - s
+            if not bw:
+                if pos > 0:
+                    start = max(start, ffin[(up, d, i)])
+                ffin[(s, d, i)] = free[s] = start + f
+            else:
+                start = max(start, ffin[(s, d, i)])
+                if pos < S - 1:
+                    start = max(start, bfin[(down, d, i)])
+                bfin[(s, d, i)] = free[s] = start + b
+            span = max(span, free[s])
+    return span
+
+
+def build_dualpipe(S: int, mb: int, f: float, b: float) -> Dict[Tuple[int, str], List[dict]]:
+    """Streams of enqueue_dualpipe: per tick the rank's op on the compute stream (waiting on its input's
+    receive), then the next-link group, then the previous-link group - each at most one send (this rank's
+    op output) and one receive (the neighbour's op output of the same tick, into a buffer of its own).
+    One FIFO channel per link direction, as one communicator per link carries every message type."""
+    streams: Dict[Tuple[int, str], List[dict]] = {}
+    H = mb // 2
+
+    def pos(s, d):
+        return s if d == 0 else S - 1 - s
+
+    def travels(s, op, towards_next):  # does op's output at stage s go over that link?
+        if op is None:
+            return False
+        d, _, bw = op
+        if ((d == 0) != bw) != towards_next:
+            return False
+        return pos(s, d) > 0 if bw else pos(s, d) < S - 1
+
+    for row in dualpipe_ticks(S, mb):
+        for s in range(S):
+            op = row[s]
+            if op is not None:
+                d, i, bw = op
+                k = d * H + i
+                needs = (pos(s, d) < S - 1) if bw else (pos(s, d) > 0)
+                waits = [(s, "recvB" if bw else "recvF", k)] if needs else []
+                streams.setdefault((s, "c"), []).append(
+                    {"dur": b if bw else f, "waits": waits, "rec": [(s, "bdone" if bw else "fdone", k)]})
+            for nxt, st in ((True, "n"), (False, "p")):
+                peer = s + 1 if nxt else s - 1
+                if not 0 <= peer < S:
+                    continue
+                theirs = row[peer]
+                send, recv = travels(s, op, nxt), travels(peer, theirs, not nxt)
+                if not (send or recv):
+                    continue
+                waits, p2p, rec = [], [], []
+                if send:
+                    d, i, bw = op
+                    waits.append((s, "bdone" if bw else "fdone", d * H + i))
+                    p2p.append(("send", "L", peer))
+                    rec.append((s, "sent", (d, i, bw)))
+                if recv:
+                    d, i, bw = theirs
+                    p2p.append(("recv", "L", peer))
+                    rec.append((s, "recvB" if bw else "recvF", d * H + i))
+                streams.setdefault((s, st), []).append({"dur": 0.0, "waits": waits, "rec": rec, "p2p": p2p})
     return streams
 
 
@@ -266,6 +395,10 @@ def main(argv=None) -> int:
         t, stuck = simulate(build(a.stages, a.microbatches, V, a.fwd, a.bwd, sched))
         print(f"{sched:12s} V={V}: makespan {t:.3f}  floor {floor(a.stages, a.microbatches, V, a.fwd, a.bwd):.3f}"
               + (f"  DEADLOCK {stuck[:4]}" if stuck else ""))
+    if a.stages % 2 == 0 and a.microbatches % 2 == 0:
+        t, stuck = simulate(build_dualpipe(a.stages, a.microbatches, a.fwd, a.bwd))
+        print(f"{'dualpipe':12s} V=1: makespan {t:.3f}  floor "
+              f"{dualpipe_floor(a.stages, a.microbatches, a.fwd, a.bwd):.3f}" + (f"  DEADLOCK {stuck[:4]}" if stuck else ""))
     return 0
 
 

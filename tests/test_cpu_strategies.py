@@ -457,3 +457,16 @@ def test_dualpipe_argument_checks(params, extra, msg, data_dir):
                                            "--quiet"], timeout=60, capture=True)
     text = "".join(o or "" for o in outs)
     assert code != 0 and msg in text, text[-2000:]
+
+
+def test_dualpipe_native_floor_matches_model(data_dir):
+    """The native driver's tick count and compute floor equal the Python model's for the same f, b."""
+    from dlnetbench_amd.parallel import schedule_sim as sim
+    S, mb = 4, 8
+    d = run(S, "hybrid_2d", "tiny_deep_8_bfloat16", S, mb, data_dir, "-w", 1, "-r", 1, "--pp-schedule", "dualpipe")
+    g = d["global"]
+    f, b = g["fwd_rt_per_microbatch"], g["bwd_rt_per_microbatch"]
+    assert g["dualpipe_ticks"] == len(sim.dualpipe_ticks(S, mb))
+    scale = g["dlnb"].get("time_scale", 1.0) if isinstance(g["dlnb"], dict) else 1.0
+    assert g["dlnb"]["iteration"]["compute_floor_ms"] * 1e3 == pytest.approx(sim.dualpipe_floor(S, mb, f, b) * scale,
+                                                                             rel=1e-6)

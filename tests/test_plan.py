@@ -148,6 +148,32 @@ def test_schedule_model_no_deadlock_and_floor(sched, V, S, mb, semantics):
     assert t == pytest.approx(sim.floor(S, mb, V, 1.0, 2.0))
 
 
+@pytest.mark.parametrize("semantics", ["rendezvous", "buffered"])
+@pytest.mark.parametrize("S,mb", [(2, 2), (2, 4), (4, 4), (4, 8), (4, 16), (6, 12), (8, 8), (8, 16), (8, 32), (16, 32)])
+def test_dualpipe_model_no_deadlock_and_beats_1f1b(S, mb, semantics):
+    """DualPipe's tick order (build_dualpipe in strategy_pipeline.cpp) never deadlocks, reaches its own compute
+    floor when links cost nothing, and that floor sits between the bubble-free mb (f + b) and 1F1B's
+    (mb + S - 1)(f + b), within 3 (f + b) of the ideal mb (f + b) + (S/2 - 1)(f + b)."""
+    from dlnetbench_amd.parallel import schedule_sim as sim
+    f, b = 1.0, 2.0
+    t, stuck = sim.simulate(sim.build_dualpipe(S, mb, f, b), semantics)
+    assert not stuck
+    fl = sim.dualpipe_floor(S, mb, f, b)
+    assert t == pytest.approx(fl)
+    assert mb * (f + b) <= fl < sim.floor(S, mb, 1, f, b)
+    if mb >= S:
+        assert fl <= (mb + S // 2 - 1) * (f + b) + 3 * (f + b)
+    # every rank runs 2 (f + b) per microbatch pair, and at most S + 1 activations are in flight per rank
+    ticks = sim.dualpipe_ticks(S, mb)
+    for s in range(S):
+        live, peak = 0, 0
+        for row in ticks:
+            if row[s] is not None:
+                live += -1 if row[s][2] else 1
+                peak = max(peak, live)
+        assert live == 0 and peak <= S + 1
+
+
 # ---- xGMI cost model (dlnetbench_amd/parallel/xgmi_model.py)
 
 def test_xgmi_model_collective_times():
