@@ -323,6 +323,8 @@ class Pipeline : public Strategy {
     }
     if (prev_ || next_) stats_.push_back({"sendrecv", CollKind::SendRecv, 2, static_cast<double>(pipe_ * es_), "pp_send_time"});
     stats_.push_back({"dp_allreduce", CollKind::AllReduce, dp_size_, static_cast<double>(dp_ar_ / o.dp_buckets * es_), "dp_comm_time"});
+    if (dualpipe_)
+      stats_.push_back({"pp_mirror_allreduce", CollKind::AllReduce, 2, static_cast<double>(dp_ar_ * es_), "pp_mirror_time"});
     if (has_tp_ && !sp_)
       stats_.push_back({"tp_allreduce", CollKind::AllReduce, T_, static_cast<double>(tp_ar_ * es_), "tp_comm_time"});
     if (has_tp_ && sp_) {

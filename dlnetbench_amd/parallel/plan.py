@@ -144,12 +144,16 @@ def ep_dispatch_counts(a2a: int, E: int, alpha: float) -> List[int]:
 
 def plan_hybrid(st: ModelStats, world: int, kind: str, S: int, mb: int, inner: int = 1, layers: int = 0,
                 wire: str = "bf16", tp_granularity: str = "microbatch", experts: int = 1,
-                ep_imbalance: float = 0.0) -> Plan:
+                ep_imbalance: float = 0.0, pp_schedule: str = "gpipe", pp_virtual: int = 1) -> Plan:
     """hybrid_4d: inner = T (tensor shards), experts = E (expert shards); TP fastest, then EP.
+    pp_schedule dualpipe (csrc/src/strategy_pipeline.cpp build_dualpipe): every rank holds two stage
+    chunks, so its gradient (and non-expert part) doubles and mirrored stages s, S-1-s all-reduce it
+    pairwise before the DP all-reduce. `compute_floor_us` is the schedule's makespan with free links.
     ep_imbalance > 0 (MoE): the all-to-all becomes an all-to-allv; the message's
     wire_bytes stay the uniform total and `ep_dispatch_elements_per_peer` gives the split."""
     if kind == "hybrid_4d":
-        return _plan_4d(st, world, S, mb, inner, experts, layers, wire, tp_granularity)
+        p = _plan_4d(st, world, S, mb, inner, experts, layers, wire, tp_granularity)
+        return _apply_pp_schedule(p, S, mb, pp_schedule, pp_virtual, WIRE_BYTES[wire])
     es = WIRE_BYTES[wire]
     if layers and layers % S:
         raise ValueError("num_layers must be divisible by num_stages")
@@ -185,6 +189,27 @@ def plan_hybrid(st: ModelStats, world: int, kind: str, S: int, mb: int, inner: i
         p.messages.append(Message("ep_nonexpert_allreduce", "allreduce", inner, ne, 1, ne * es))
     p.messages.append(Message("dp_allreduce", "allreduce", world // (S * inner), dp_ar, 1, dp_ar * es))
     p.memory_bytes = (8 * pipe + 2 * dp_ar) * es
+    return _apply_pp_schedule(p, S, mb, pp_schedule, pp_virtual, es)
+
+
+def _apply_pp_schedule(p: Plan, S: int, mb: int, sched: str, V: int, es: int) -> Plan:
+    from . import schedule_sim as sim
+    f, b = p.compute_per_unit_us["fwd_per_microbatch"], p.compute_per_unit_us["bwd_per_microbatch"]
+    p.params["pp_schedule"] = sched
+    if sched == "dualpipe":
+        if S % 2 or mb % 2:
+            raise ValueError("dualpipe needs an even number of stages and of microbatches")
+        for m in p.messages:
+            if m.name in ("dp_allreduce", "ep_nonexpert_allreduce"):
+                m.elements *= 2
+                m.wire_bytes *= 2
+        dp = next(m for m in p.messages if m.name == "dp_allreduce")
+        p.messages.append(Message("pp_mirror_allreduce", "allreduce", 2, dp.elements, 1, dp.elements * es))
+        p.memory_bytes += dp.elements * es  # the second chunk's gradient + buffer: 2 x the old dp_ar
+        p.compute_per_unit_us["compute_floor_us"] = sim.dualpipe_floor(S, mb, f, b)
+    else:
+        v = V if sched == "interleaved" else 1
+        p.compute_per_unit_us["compute_floor_us"] = sim.floor(S, mb, v, f, b)
     return p
 
 
@@ -267,6 +292,8 @@ def main(argv=None) -> int:
     ap.add_argument("--zero", type=int, default=0, help="dp: ZeRO stage 0|1|2")
     ap.add_argument("--cp-algo", default="ring", choices=["ring", "ulysses"])
     ap.add_argument("--ep-imbalance", type=float, default=0.0, help="hybrid_3d_moe: Zipf exponent of the expert load")
+    ap.add_argument("--pp-schedule", default="gpipe", choices=["gpipe", "1f1b", "interleaved", "dualpipe"])
+    ap.add_argument("--pp-virtual", type=int, default=2, help="interleaved: model chunks per stage")
     ap.add_argument("--predict", action="store_true",
                     help="dp / fsdp: add the xGMI cost-model prediction (parallel/xgmi_model.py) at W = 1, 2, 4, 8")
     ap.add_argument("--link-gbps", type=float, default=153.0, help="xGMI bandwidth per link and direction")
@@ -292,7 +319,8 @@ def main(argv=None) -> int:
             inner = a.params[2] if len(a.params) > 2 else 1
             experts = a.params[3] if len(a.params) > 3 else 1
             pl = plan_hybrid(st, a.world, a.strategy, a.params[0], a.params[1], inner, L, wire=a.wire,
-                             experts=experts, ep_imbalance=a.ep_imbalance)
+                             experts=experts, ep_imbalance=a.ep_imbalance, pp_schedule=a.pp_schedule,
+                             pp_virtual=a.pp_virtual)
     doc = pl.to_json()
     if a.predict and a.strategy in ("dp", "fsdp"):
         from . import xgmi_model as xm

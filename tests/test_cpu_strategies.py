@@ -470,3 +470,26 @@ def test_dualpipe_native_floor_matches_model(data_dir):
     scale = g["dlnb"].get("time_scale", 1.0) if isinstance(g["dlnb"], dict) else 1.0
     assert g["dlnb"]["iteration"]["compute_floor_ms"] * 1e3 == pytest.approx(sim.dualpipe_floor(S, mb, f, b) * scale,
                                                                              rel=1e-6)
+
+
+@pytest.mark.parametrize("w,prog,model,params", [(4, "hybrid_2d", "tiny_deep_8_bfloat16", (4, 8)),
+                                                 (8, "hybrid_3d_moe", "tiny_moe_8_bfloat16", (2, 4, 2))])
+def test_dualpipe_planner_matches_native(w, prog, model, params, data_dir):
+    """plan.py --pp-schedule dualpipe: doubled DP gradient, pair all-reduce and compute floor as the native run."""
+    import json as _json
+    from dlnetbench_amd.parallel import plan as P
+    from dlnetbench_amd.utils.stats import load_stats
+    d = run(w, prog, model, *params, data_dir, "-w", 1, "-r", 1, "--pp-schedule", "dualpipe")
+    st = load_stats(os.path.join(data_dir, "model_stats", model + ".txt"))
+    with open(os.path.join(data_dir, "models", model.rsplit("_", 2)[0] + ".json")) as f:
+        arch = _json.load(f)
+    L = arch.get("num_encoder_blocks", 0) + arch.get("num_decoder_blocks", 0)
+    inner = params[2] if len(params) > 2 else 1
+    pl = P.plan_hybrid(st, w, prog, params[0], params[1], inner, L, pp_schedule="dualpipe")
+    msgs = {m.name: m for m in pl.messages}
+    comm = d["ranks"][0]["comm"]
+    assert comm["dp_allreduce"]["bytes_per_op"] == msgs["dp_allreduce"].wire_bytes
+    assert comm["pp_mirror_allreduce"]["bytes_per_op"] == msgs["pp_mirror_allreduce"].wire_bytes
+    assert comm["pp_mirror_allreduce"]["nranks"] == 2
+    floor_ms = d["global"]["dlnb"]["iteration"]["compute_floor_ms"]
+    assert pl.compute_per_unit_us["compute_floor_us"] / 1e3 == pytest.approx(floor_ms, rel=1e-6)
