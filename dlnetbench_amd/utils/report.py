@@ -132,7 +132,8 @@ def hybrid_dataframe(doc: dict, network: str = "mi355x"):
     import pandas as pd
     g = doc["global"]
     rows = []
-    keys = [k for k in ("pp_comm_time", "dp_comm_time", "tp_comm_time", "ep_comm_time", "dp_ep_comm_time")]
+    keys = [k for k in ("pp_comm_time", "dp_comm_time", "tp_comm_time", "ep_comm_time", "dp_ep_comm_time",
+                        "pp_mirror_time")]
     for r in doc["ranks"]:
         runs = len(r["runtimes"])
         for i in range(runs):

@@ -74,6 +74,11 @@ def test_report_dataframes(tmp_path, bindir, data_dir):
     assert code == 0
     df = report.hybrid_dataframe(report.parse_output(outs[0])["dp_pp_tp_ep"])
     assert len(df) == 4 * 2 and {"tp_comm_time", "ep_comm_time"} <= set(df.columns)
+    code, outs = launch.launch(4, [os.path.join(bindir, "hybrid_2d"), "tiny_deep_8_bfloat16", "4", "8", data_dir,
+                                   "--quiet", "-w", "0", "-r", "2", "--pp-schedule", "dualpipe"], timeout=60, capture=True)
+    assert code == 0
+    df = report.hybrid_dataframe(report.parse_output(outs[0])["dp_pp"])
+    assert len(df) == 4 * 2 and (df["pp_schedule"] == "dualpipe").all() and "pp_mirror_time" in df.columns
 
 
 def test_plots(tmp_path, bindir):
