@@ -467,9 +467,7 @@ def test_dualpipe_native_floor_matches_model(data_dir):
     g = d["global"]
     f, b = g["fwd_rt_per_microbatch"], g["bwd_rt_per_microbatch"]
     assert g["dualpipe_ticks"] == len(sim.dualpipe_ticks(S, mb))
-    scale = g["dlnb"].get("time_scale", 1.0) if isinstance(g["dlnb"], dict) else 1.0
-    assert g["dlnb"]["iteration"]["compute_floor_ms"] * 1e3 == pytest.approx(sim.dualpipe_floor(S, mb, f, b) * scale,
-                                                                             rel=1e-6)
+    assert g["dlnb"]["iteration"]["compute_floor_ms"] * 1e3 == pytest.approx(sim.dualpipe_floor(S, mb, f, b), rel=1e-6)
 
 
 @pytest.mark.parametrize("w,prog,model,params", [(4, "hybrid_2d", "tiny_deep_8_bfloat16", (4, 8)),
