@@ -243,6 +243,7 @@ class Pipeline : public Strategy {
                                        pair, dp_ar_ * es_, false);
       build_dualpipe();
       for (int k = 0; k < 2 * mb_; ++k) dpbuf_.push_back(dev.alloc(pipe_ * es_));
+      mirror_ready_ = dev.create_event();
     }
 
     // Buffers.
@@ -324,7 +325,7 @@ class Pipeline : public Strategy {
     if (prev_ || next_) stats_.push_back({"sendrecv", CollKind::SendRecv, 2, static_cast<double>(pipe_ * es_), "pp_send_time"});
     stats_.push_back({"dp_allreduce", CollKind::AllReduce, dp_size_, static_cast<double>(dp_ar_ / o.dp_buckets * es_), "dp_comm_time"});
     if (dualpipe_)
-      stats_.push_back({"pp_mirror_allreduce", CollKind::AllReduce, 2, static_cast<double>(dp_ar_ * es_), "pp_mirror_time"});
+      stats_.push_back({"pp_mirror_allreduce", CollKind::AllReduce, 2, static_cast<double>(dp_ar_ / 2 * es_), "pp_mirror_time"});
     if (has_tp_ && !sp_)
       stats_.push_back({"tp_allreduce", CollKind::AllReduce, T_, static_cast<double>(tp_ar_ * es_), "tp_comm_time"});
     if (has_tp_ && sp_) {
@@ -543,9 +544,12 @@ class Pipeline : public Strategy {
       compute_->record(*bucket_ready_[0]);
       dp_stream_->wait(*bucket_ready_[0]);
       if (mirror_comm_) {
-        void* g = grad_.data();
+        // the half whose chunks finish last (model stage min(s, S-1-s)); the
+        // other half was reduced mid-backward (enqueue_dualpipe)
+        const size_t half = dp_ar_ / 2;
+        void* g = static_cast<char*>(grad_.data()) + half * es_;
         int tm = timers_->begin(*dp_stream_);
-        mirror_comm_->all_reduce(g, g, dp_ar_, t, *dp_stream_);
+        mirror_comm_->all_reduce(g, g, dp_ar_ - half, t, *dp_stream_);
         timers_->end(tm, *dp_stream_, "pp_mirror_time");
       }
       dp_allreduce_bucket(0, 1);
@@ -850,6 +854,14 @@ class Pipeline : public Strategy {
         span = std::max(span, free_at[static_cast<size_t>(s)]);
       }
     dp_floor_us_ = span;
+    // The pair's gradient of model stage max(s, S-1-s) is final once the
+    // chunks holding it (down copy on the higher rank, up copy on the lower:
+    // both at position >= S/2, early in their backward chains) have run their
+    // last backward; both ranks reduce it at the end of that same tick, so the
+    // all-reduce overlaps the rest of the backward and host-side rendezvous
+    // stays tick-ordered.
+    const int lo = std::min(stage_, S_ - 1 - stage_), hi = S_ - 1 - lo;
+    mirror_early_tick_ = std::max(bdone[idx(lo, 1, H - 1)], bdone[idx(hi, 0, H - 1)]);
   }
 
   // Event / buffer slot of (dir, mb): activations [0, mb), gradients [mb, 2 mb).
@@ -882,6 +894,7 @@ class Pipeline : public Strategy {
   }
 
   void enqueue_dualpipe() {
+    int tick = 0;
     for (const auto& row : dp_ticks_) {
       const DpOp& op = row[static_cast<size_t>(stage_)];
       if (op.dir >= 0) {
@@ -904,6 +917,15 @@ class Pipeline : public Strategy {
       }
       if (next_) dualpipe_link(true, op, row[static_cast<size_t>(stage_ + 1)]);
       if (prev_) dualpipe_link(false, op, row[static_cast<size_t>(stage_ - 1)]);
+      if (tick == mirror_early_tick_) {
+        compute_->record(*mirror_ready_);
+        dp_stream_->wait(*mirror_ready_);
+        void* g = grad_.data();
+        int tm = timers_->begin(*dp_stream_);
+        mirror_comm_->all_reduce(g, g, dp_ar_ / 2, ctx_->wire, *dp_stream_);
+        timers_->end(tm, *dp_stream_, "pp_mirror_time");
+      }
+      ++tick;
     }
     finish_iteration();
   }
@@ -1057,6 +1079,8 @@ class Pipeline : public Strategy {
   bool one_f_one_b_ = false, interleaved_ = false, dualpipe_ = false;
   std::vector<std::vector<DpOp>> dp_ticks_;  // [tick][stage]
   double dp_floor_us_ = 0;
+  int mirror_early_tick_ = -1;  // tick after which the first half of the mirror all-reduce is issued
+  std::unique_ptr<Event> mirror_ready_;
   std::vector<Buffer> dpbuf_;  // receive buffers per (dir, microbatch): activations, then gradients
   std::unique_ptr<Communicator> mirror_comm_;
   int V_ = 1, layers_per_chunk_ = 0;

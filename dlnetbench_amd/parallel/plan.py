@@ -148,7 +148,7 @@ def plan_hybrid(st: ModelStats, world: int, kind: str, S: int, mb: int, inner: i
     """hybrid_4d: inner = T (tensor shards), experts = E (expert shards); TP fastest, then EP.
     pp_schedule dualpipe (csrc/src/strategy_pipeline.cpp build_dualpipe): every rank holds two stage
     chunks, so its gradient (and non-expert part) doubles and mirrored stages s, S-1-s all-reduce it
-    pairwise before the DP all-reduce. `compute_floor_us` is the schedule's makespan with free links.
+    pairwise (in two halves) before the DP all-reduce. `compute_floor_us` is the schedule's makespan with free links.
     ep_imbalance > 0 (MoE): the all-to-all becomes an all-to-allv; the message's
     wire_bytes stay the uniform total and `ep_dispatch_elements_per_peer` gives the split."""
     if kind == "hybrid_4d":
@@ -204,7 +204,8 @@ def _apply_pp_schedule(p: Plan, S: int, mb: int, sched: str, V: int, es: int) ->
                 m.elements *= 2
                 m.wire_bytes *= 2
         dp = next(m for m in p.messages if m.name == "dp_allreduce")
-        p.messages.append(Message("pp_mirror_allreduce", "allreduce", 2, dp.elements, 1, dp.elements * es))
+        # two halves: the early-finishing model stage mid-backward, the other after the last backward
+        p.messages.append(Message("pp_mirror_allreduce", "allreduce", 2, dp.elements // 2, 2, dp.elements // 2 * es))
         p.memory_bytes += dp.elements * es  # the second chunk's gradient + buffer: 2 x the old dp_ar
         p.compute_per_unit_us["compute_floor_us"] = sim.dualpipe_floor(S, mb, f, b)
     else:
