@@ -323,7 +323,8 @@ class Pipeline : public Strategy {
       timers_->ensure("dp_ep_comm_time");
     }
     if (prev_ || next_) stats_.push_back({"sendrecv", CollKind::SendRecv, 2, static_cast<double>(pipe_ * es_), "pp_send_time"});
-    stats_.push_back({"dp_allreduce", CollKind::AllReduce, dp_size_, static_cast<double>(dp_ar_ / o.dp_buckets * es_), "dp_comm_time"});
+    stats_.push_back({"dp_allreduce", CollKind::AllReduce, dp_size_,
+                      static_cast<double>(dp_ar_ / (dualpipe_ ? 2 : o.dp_buckets) * es_), "dp_comm_time"});
     if (dualpipe_)
       stats_.push_back({"pp_mirror_allreduce", CollKind::AllReduce, 2, static_cast<double>(dp_ar_ / 2 * es_), "pp_mirror_time"});
     if (has_tp_ && !sp_)
@@ -551,8 +552,10 @@ class Pipeline : public Strategy {
         int tm = timers_->begin(*dp_stream_);
         mirror_comm_->all_reduce(g, g, dp_ar_ - half, t, *dp_stream_);
         timers_->end(tm, *dp_stream_, "pp_mirror_time");
+        dp_allreduce_bucket(1, 2);
+      } else {
+        dp_allreduce_bucket(0, 1);
       }
-      dp_allreduce_bucket(0, 1);
     }
     dp_stream_->record(*dp_done_);
     timers_->stall(*compute_, *dp_done_, "dp_exposed_time");
@@ -924,6 +927,7 @@ class Pipeline : public Strategy {
         int tm = timers_->begin(*dp_stream_);
         mirror_comm_->all_reduce(g, g, dp_ar_ / 2, ctx_->wire, *dp_stream_);
         timers_->end(tm, *dp_stream_, "pp_mirror_time");
+        dp_allreduce_bucket(0, 2);  // and that half's DP all-reduce right behind it
       }
       ++tick;
     }

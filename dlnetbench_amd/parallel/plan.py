@@ -200,13 +200,15 @@ def _apply_pp_schedule(p: Plan, S: int, mb: int, sched: str, V: int, es: int) ->
         if S % 2 or mb % 2:
             raise ValueError("dualpipe needs an even number of stages and of microbatches")
         for m in p.messages:
-            if m.name in ("dp_allreduce", "ep_nonexpert_allreduce"):
+            if m.name == "ep_nonexpert_allreduce":
                 m.elements *= 2
                 m.wire_bytes *= 2
         dp = next(m for m in p.messages if m.name == "dp_allreduce")
-        # two halves: the early-finishing model stage mid-backward, the other after the last backward
-        p.messages.append(Message("pp_mirror_allreduce", "allreduce", 2, dp.elements // 2, 2, dp.elements // 2 * es))
-        p.memory_bytes += dp.elements * es  # the second chunk's gradient + buffer: 2 x the old dp_ar
+        p.memory_bytes += 2 * dp.elements * es  # the second chunk's gradient + buffer
+        # the doubled gradient is synchronised in two halves (the early-finishing model stage mid-backward,
+        # the other after the last backward), each a pair all-reduce followed by its DP all-reduce
+        dp.calls_per_iter = 2
+        p.messages.append(Message("pp_mirror_allreduce", "allreduce", 2, dp.elements, 2, dp.elements * es))
         p.compute_per_unit_us["compute_floor_us"] = sim.dualpipe_floor(S, mb, f, b)
     else:
         v = V if sched == "interleaved" else 1
