@@ -6,8 +6,27 @@ Llama-3-8B FSDP proxy (model_stats/llama3_8b_16_bfloat16.txt: local batch
 16, seq 8192, 8.03 B parameters, B200-roofline fwd/bwd times of the
 reference's tables), 32 FSDP units, sharding factor = N (fully sharded over
 the GPUs of the job), bf16 on the wire, compute = hand-written MFMA GEMMs
-calibrated to the table's times. One process per GPU; under torchrun every
+bounded to the table's times. One process per GPU; under torchrun every
 rank runs this file. Weak scaling: each GPU keeps its local batch of 16.
+
+The headline is compute-bound by construction (2.8 s of compute against
+~40 ms of all-link collectives at N = 8), so three secondary measurements
+ride along as extra keys of the same JSON line:
+
+* ``comm_bound``: the ViT-H/32 fp8 data-parallel proxy (BASELINE config 5,
+  model_stats/vit_h_32_float8.txt: 7.13 ms of compute, a 1.26 GB bf16
+  gradient all-reduce in 8 buckets) - the one baseline config where
+  communication dominates; iteration time, exposed communication
+  (barrier_time) and all-reduce bus bandwidth.
+* ``comm_bound.gemm_work``: the same with fixed-work compute (the GEMM count
+  calibrated to the table time with nothing else running), so collective
+  interference shows up as a longer iteration and ``compute_stretch`` > 1.
+* ``compute_stretch``: the headline FSDP configuration with fixed-work
+  compute for a few iterations (task time under the concurrent
+  all-gathers / reduce-scatters over the uncontended time).
+
+At N = 1 a "collective" is a local device copy: bus bandwidth is reported
+as null (nccl-tests convention: nothing crosses a link).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        (N > 1: torchrun --nproc-per-node N ... bench.py --gpus N ...)
@@ -16,10 +35,10 @@ Prints one JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
-import time
 import json
 import os
 import sys
+from typing import Any, Dict, Optional
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -30,16 +49,18 @@ METRIC = "proxy iter time (ms) + effective GB/s, Llama-3-8B DP/FSDP at 1/2/4/8 M
 # ideal overlap would hit on any hardware.
 BASELINE_MS = 2814.74976
 DEFAULT_MODEL = "llama3_8b_16_bfloat16"
+C5_MODEL = "vit_h_32_float8"
 
 
 def _store_env(world: int, rank: int, attempt: str = "") -> None:
     """Point the native runtime's TCP rendezvous store at this torchrun job.
 
     Single node (the bench's case): rank 0's store binds an ephemeral port
-    and publishes host:port in a file named after torchrun's MASTER_PORT and
-    the launcher's pid (all local workers of one job share the elastic agent
-    as parent, so a stale file from an earlier job is never read); the other
-    ranks poll that file (DLNB_STORE_FILE). Multi-node: MASTER_PORT + 1."""
+    and publishes host:port in a file named after torchrun's MASTER_PORT, the
+    launcher's pid and the phase (`attempt`: every benchmark run of this
+    process rendezvouses on a fresh store, so a file from an earlier phase or
+    job is never read); the other ranks poll that file (DLNB_STORE_FILE).
+    Multi-node: MASTER_PORT + 1 + phase index."""
     os.environ.pop("DLNB_STORE_ADDR", None)
     os.environ.pop("DLNB_STORE_FILE", None)
     if world == 1:
@@ -47,13 +68,33 @@ def _store_env(world: int, rank: int, attempt: str = "") -> None:
     host = os.environ.get("MASTER_ADDR", "127.0.0.1")
     port = int(os.environ.get("MASTER_PORT", "29500"))
     if int(os.environ.get("LOCAL_WORLD_SIZE", world)) != world:
-        os.environ["DLNB_STORE_ADDR"] = f"{host}:{port + 1 + (1 if attempt else 0)}"
+        phase = sum(ord(c) for c in attempt) % 97 if attempt else 0
+        os.environ["DLNB_STORE_ADDR"] = f"{host}:{port + 1 + phase}"
         return
     path = f"/tmp/dlnb_bench_store_{port}_{os.getppid()}{attempt}"
     os.environ["DLNB_STORE_FILE"] = path
     if rank == 0:
         import atexit
         atexit.register(lambda: os.path.exists(path) and os.remove(path))
+
+
+def _busbw(doc: dict, kind: str, world: int) -> Optional[float]:
+    """Mean over ranks of one collective's bus bandwidth; None at 1 rank."""
+    if world <= 1:
+        return None
+    vals = [r["comm"][kind]["busbw_GBps"] for r in doc["ranks"] if "busbw_GBps" in r["comm"].get(kind, {})]
+    return round(sum(vals) / len(vals), 2) if vals else None
+
+
+def _algbw(doc: dict, kind: str) -> Optional[float]:
+    vals = [r["comm"][kind]["algbw_GBps"] for r in doc["ranks"] if "algbw_GBps" in r["comm"].get(kind, {})]
+    return round(sum(vals) / len(vals), 2) if vals else None
+
+
+def _mean_of(doc: dict, key: str) -> Optional[float]:
+    """Mean over ranks and runs of a per-rank timer (seconds) -> ms."""
+    vals = [v for r in doc["ranks"] for v in r.get(key, [])]
+    return round(sum(vals) / len(vals) * 1e3, 4) if vals else None
 
 
 def main() -> int:
@@ -70,7 +111,15 @@ def main() -> int:
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--devices", default=None,
                     help="device list by local rank, e.g. 0,0 to put 2 ranks on one GPU (xgmi backend tests)")
-    ap.add_argument("--json", default=None, help="also write the full report here (rank 0)")
+    ap.add_argument("--base-path", default=ROOT, help="directory holding model_stats/ and models/")
+    ap.add_argument("--time-scale", type=float, default=None, help="scale every compute duration (tests)")
+    ap.add_argument("--c5-model", default=C5_MODEL, help="comm-bound DP secondary ('none' skips it)")
+    ap.add_argument("--c5-buckets", type=int, default=8)
+    ap.add_argument("--c5-steps", type=int, default=50)
+    ap.add_argument("--c5-wire", default="bf16", help="wire dtype of the comm-bound all-reduce")
+    ap.add_argument("--stretch-steps", type=int, default=2,
+                    help="fixed-work FSDP iterations for compute_stretch (0 skips)")
+    ap.add_argument("--json", default=None, help="also write the full headline report here (rank 0)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -80,35 +129,80 @@ def main() -> int:
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     # Everything below is native (HIP + RCCL from /opt/rocm); torch is not needed.
     os.environ.setdefault("DLNB_NO_TORCH", "1")
-    _store_env(world, rank)
 
     from dlnetbench_amd import engine
     from dlnetbench_amd.utils.stats import load_stats
-    st = load_stats(os.path.join(ROOT, "model_stats", a.model + ".txt"))
+    st = load_stats(os.path.join(a.base_path, "model_stats", a.model + ".txt"))
+    on_gpu = a.backend in ("auto", "rccl", "xgmi")
+    use_graph = a.graph and on_gpu and a.schedule == "overlap"
+
+    def run(phase: str, strategy: str, model: str, *params: int, graph: bool, **kw: Any) -> dict:
+        _store_env(world, rank, phase)
+        return engine.run(strategy, model, *params, base_path=a.base_path, backend=a.backend, silent=True,
+                          devices=a.devices, time_scale=a.time_scale, graph=graph or None, **kw)
+
     # The result line must be the only stdout line: route whatever the native
     # libraries print (e.g. RCCL's banner) to stderr while the benchmark runs.
-    graph = a.graph and a.backend in ("auto", "rccl") and a.schedule == "overlap"
-
-    def attempt(use_graph: bool):
-        return engine.run("fsdp", a.model, a.units, world, base_path=ROOT, warmup=a.warmup, runs=a.steps,
-                          compute=a.compute, schedule=a.schedule, backend=a.backend, wire_dtype="bf16",
-                          silent=True, json=a.json, graph=use_graph or None, devices=a.devices)
-
     sys.stdout.flush()
     saved = os.dup(1)
     os.dup2(2, 1)
+    extra: Dict[str, Any] = {}
     try:
+        fsdp_kw = dict(schedule=a.schedule, wire_dtype="bf16")
         try:
-            doc = attempt(graph)
+            doc = run("", "fsdp", a.model, a.units, world, graph=use_graph, warmup=a.warmup, runs=a.steps,
+                      compute=a.compute, json=a.json, **fsdp_kw)
         except RuntimeError as e:
-            if not graph:
+            if not use_graph:
                 raise
             # Graph capture is symmetric across ranks, so every rank takes this
             # path; the retry rendezvouses on a fresh store.
             print(f"[bench] HIP graph run failed ({e}); retrying with per-iteration enqueue", file=sys.stderr)
-            graph = False
-            _store_env(world, rank, ".retry")
-            doc = attempt(False)
+            use_graph = False
+            doc = run(".retry", "fsdp", a.model, a.units, world, graph=False, warmup=a.warmup, runs=a.steps,
+                      compute=a.compute, json=a.json, **fsdp_kw)
+        # Secondary measurements: failures are reported, never fatal to the headline.
+        if a.c5_model != "none":
+            c5: Dict[str, Any] = {}
+            try:
+                d = run(".c5", "dp", a.c5_model, a.c5_buckets, graph=use_graph, warmup=5, runs=a.c5_steps,
+                        compute=a.compute, wire_dtype=a.c5_wire)
+                it = d["global"]["dlnb"]["iteration"]
+                c5.update({
+                    "model": a.c5_model, "strategy": f"dp{world}", "num_buckets": a.c5_buckets,
+                    "wire_dtype": a.c5_wire, "compute": a.compute,
+                    "compute_dtype": d["global"]["dlnb"]["compute"].get("gemm_dtype", "auto"),
+                    "ms_per_step": round(it["timed_ms_per_iter"], 4), "median_ms": round(it["median_ms"], 4),
+                    "floor_ms": round(it["compute_floor_ms"], 4),
+                    "exposed_comm_ms": _mean_of(d, "barrier_time"),
+                    "allreduce_bytes": d["global"]["msg_size_avg_bytes"] * a.c5_buckets,
+                    "allreduce_busbw_GBps": _busbw(d, "allreduce", world),
+                    "allreduce_algbw_GBps": _algbw(d, "allreduce"),
+                    "transport": "link" if world > 1 else "local-copy",
+                    "backend": d["global"]["backend"],
+                })
+            except Exception as e:  # noqa: BLE001
+                c5["error"] = str(e)[:300]
+            if a.stretch_steps > 0 and on_gpu:
+                try:
+                    d = run(".c5w", "dp", a.c5_model, a.c5_buckets, graph=use_graph, warmup=5, runs=a.c5_steps,
+                            compute="gemm-work", wire_dtype=a.c5_wire)
+                    it = d["global"]["dlnb"]["iteration"]
+                    c5["gemm_work"] = {"ms_per_step": round(it["timed_ms_per_iter"], 4),
+                                       "median_ms": round(it["median_ms"], 4),
+                                       "exposed_comm_ms": _mean_of(d, "barrier_time"),
+                                       "compute_stretch": d["global"]["dlnb"].get("compute_stretch")}
+                except Exception as e:  # noqa: BLE001
+                    c5["gemm_work"] = {"error": str(e)[:300]}
+            extra["comm_bound"] = c5
+        if a.stretch_steps > 0 and on_gpu:
+            try:
+                d = run(".work", "fsdp", a.model, a.units, world, graph=use_graph, warmup=1, runs=a.stretch_steps,
+                        compute="gemm-work", **fsdp_kw)
+                extra["compute_stretch"] = d["global"]["dlnb"].get("compute_stretch")
+                extra["gemm_work_ms_per_step"] = round(d["global"]["dlnb"]["iteration"]["timed_ms_per_iter"], 3)
+            except Exception as e:  # noqa: BLE001
+                extra["compute_stretch_error"] = str(e)[:300]
     finally:
         sys.stdout.flush()
         os.dup2(saved, 1)
@@ -118,12 +212,6 @@ def main() -> int:
     g = doc["global"]
     it = g["dlnb"]["iteration"]
     ms = it["timed_ms_per_iter"]
-    # effective bus bandwidth of the FSDP collectives (mean over ranks)
-    bw = {}
-    for kind in ("allgather", "reduce_scatter"):
-        vals = [r["comm"][kind]["busbw_GBps"] for r in doc["ranks"] if "busbw_GBps" in r["comm"].get(kind, {})]
-        if vals:
-            bw[kind] = sum(vals) / len(vals)
     exposed = ms - it["compute_floor_ms"]
     out = {
         "metric": METRIC,
@@ -135,7 +223,7 @@ def main() -> int:
         "ms_per_step": round(ms, 3),
         "higher_is_better": False,
         "scaling": "weak",
-        "vs_baseline": round(ms / BASELINE_MS, 4) if a.model == DEFAULT_MODEL else None,
+        "vs_baseline": round(ms / BASELINE_MS, 4) if a.model == DEFAULT_MODEL and a.time_scale is None else None,
         "dtype": "bf16",
         "data": ("synthetic (random-init buffers; compute = MFMA GEMM stand-in bounded to the table durations)"
                  if a.compute == "gemm" else f"synthetic (random-init buffers; compute mode {a.compute})"),
@@ -149,14 +237,17 @@ def main() -> int:
             "compute": a.compute,
             "schedule": a.schedule,
             "backend": g["backend"],
-            "hip_graph": bool(graph),
+            "hip_graph": bool(use_graph),
         },
-        "effective_busbw_GBps": {k: round(v, 2) for k, v in bw.items()},
+        # null at N = 1: a 1-rank all-gather / reduce-scatter is a local copy
+        "effective_busbw_GBps": {k: _busbw(doc, k, world) for k in ("allgather", "reduce_scatter")},
         "exposed_comm_ms": round(exposed, 3),
         "median_ms": round(it["median_ms"], 3),
         "baseline_ms": BASELINE_MS,
         "baseline_note": "derived reference floor (BASELINE.md C2: fwd+bwd of llama3_8b_16_bfloat16); lower is better",
+        "rccl_cta_budget": g["dlnb"].get("rccl_cta_budget"),
     }
+    out.update(extra)
     print(json.dumps(out), flush=True)
     return 0
 

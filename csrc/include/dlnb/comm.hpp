@@ -72,9 +72,11 @@ class CommFactory {
   // `members` are world ranks (this rank must be one of them); `name` must
   // be unique per group and identical on all members. capacity_bytes is the
   // largest single message (CPU backend staging size); need_p2p requests
-  // point-to-point mailboxes.
+  // point-to-point mailboxes. max_ctas > 0 caps the thread blocks one
+  // collective kernel of this communicator may use (RCCL ncclConfig_t
+  // maxCTAs; the other backends size their own kernels and ignore it).
   virtual std::unique_ptr<Communicator> create(const std::string& name, const std::vector<int>& members,
-                                               size_t capacity_bytes, bool need_p2p) = 0;
+                                               size_t capacity_bytes, bool need_p2p, int max_ctas = 0) = 0;
 };
 
 std::unique_ptr<CommFactory> make_rccl_factory(HostGroup& world, Device& dev);

@@ -28,6 +28,7 @@
 
 #include "dlnb/device.hpp"
 #include "dlnb/json.hpp"
+#include "dlnb/timers.hpp"
 
 namespace dlnb {
 
@@ -62,6 +63,12 @@ class ComputeEngine {
   // Graph mode: enqueue on s a reset of whatever per-task device state the
   // engine keys by epoch (a replayed graph repeats the captured epochs).
   virtual void reset_clocks(Stream& s) { (void)s; }
+  // Fixed-work modes (gemm-work, flops): time every compute task on the
+  // device into t ("compute_task_time") next to its table duration
+  // ("compute_task_table"), so the runner can report how much collectives
+  // running beside the compute stretch it (compute_stretch). Deadline modes
+  // last exactly the table time by construction and record nothing.
+  virtual void set_task_timers(TimerSet* t) { (void)t; }
   virtual Json describe() const = 0;
   virtual ComputeMode mode() const = 0;
 };

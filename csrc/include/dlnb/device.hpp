@@ -160,6 +160,11 @@ class CpuStream : public Stream {
 };
 
 std::unique_ptr<Device> make_cpu_device();
+// Process-wide: when on, CPU-stream event waits give up and queued CPU-stream
+// tasks are dropped, so worker threads blocked on a failed loopback rank's
+// events drain and every rank thread can unwind (loopback_abort sets it;
+// a new loopback job clears it).
+void abort_cpu_waits(bool on);
 
 // GPU device (HIP). local_index picks the visible device.
 std::unique_ptr<Device> make_gpu_device(int local_index);

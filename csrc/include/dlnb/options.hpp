@@ -77,6 +77,9 @@ struct Options {
   bool silent = false;  // print nothing (library use, e.g. bench.py)
   bool trace = false;   // roctx ranges around iterations and phases
   int comm_cus = 32;    // CUs left free by the persistent compute for collectives
+  // RCCL maxCTAs per communicator on a comm lane: -1 = comm_cus / lanes
+  // (runner.cpp, collective_lanes), 0 = RCCL's default, N = N.
+  int rccl_max_ctas = -1;
   // fsdp: "single" = every collective of a rank on one in-order comm lane
   // (deadlock-free across communicators), "split" = one lane per collective
   // kind so all-gather / reduce-scatter / replica all-reduce run concurrently.

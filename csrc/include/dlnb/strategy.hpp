@@ -34,6 +34,9 @@ struct Context {
   bool have_arch = false;
   ModelArch arch;
   DType wire = DType::BF16;
+  // RCCL CTA cap for communicators whose collectives run on a comm lane
+  // (a stream beside the compute); 0 = library default.
+  int lane_ctas = 0;
   int rank() const { return boot->info.rank; }
   int world() const { return boot->info.world_size; }
   HostGroup& hg() { return *boot->world; }
@@ -88,6 +91,15 @@ std::unique_ptr<Strategy> make_dp();
 std::unique_ptr<Strategy> make_fsdp();
 std::unique_ptr<Strategy> make_pipeline(StrategyKind kind);  // hybrid_2d / 3d / 3d_moe
 std::unique_ptr<Strategy> make_cp();                          // hybrid_cp (extension)
+
+// Upper bound on the comm lanes (streams other than the compute stream that
+// carry collectives) a rank of this configuration keeps live at once: dp 1;
+// fsdp 1 (--comm-lanes single) or 2 + (replicas > 1) (split); hybrid_cp 2;
+// pipelines 3 when S > 1 (prev link, next link, DP lane - which also carries
+// the DualPipe mirror and --ep-overlap all-to-alls) else 1. Collectives on
+// the compute stream (TP all-reduce, EP all-to-all) never overlap the GEMM
+// and are not counted.
+int collective_lanes(const Options& o, int world);
 
 // Creates ctx.dev + ctx.comms for a backend (auto | rccl | xgmi | cpu);
 // GPU ranks take device list[local_rank] ("-d 0,1,..", default all GPUs).

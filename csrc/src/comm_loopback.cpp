@@ -124,6 +124,7 @@ std::shared_ptr<LoopbackHub> make_loopback_hub(int ranks, double timeout_s) {
 }
 
 void loopback_abort(LoopbackHub& hub, const std::string& why) {
+  abort_cpu_waits(true);  // loopback-cpu: release worker threads blocked on the failed rank's events
   std::lock_guard<std::mutex> g(hub.mu);
   if (!hub.aborted) {
     hub.aborted = true;
@@ -384,7 +385,7 @@ class LoopbackFactory : public CommFactory {
   }
   std::string backend_name() const override { return "LOOPBACK"; }
   std::unique_ptr<Communicator> create(const std::string& name, const std::vector<int>& members, size_t,
-                                       bool) override {
+                                       bool, int) override {
     DLNB_REQUIRE(!members.empty() && members.size() <= static_cast<size_t>(xgmi::kMaxLocal),
                  "loopback: group " << name << " of " << members.size() << " ranks");
     std::shared_ptr<Group> g;

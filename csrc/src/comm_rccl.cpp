@@ -37,7 +37,8 @@ hipStream_t hs(Stream& s) { return static_cast<hipStream_t>(s.native()); }
 
 class RcclComm : public Communicator {
  public:
-  RcclComm(const std::string& name, const std::vector<int>& members, int my_world_rank, HostGroup& world) {
+  RcclComm(const std::string& name, const std::vector<int>& members, int my_world_rank, HostGroup& world,
+           int max_ctas) {
     name_ = name;
     members_ = members;
     size_ = static_cast<int>(members.size());
@@ -58,7 +59,14 @@ class RcclComm : public Communicator {
       DLNB_REQUIRE(v.size() == sizeof(id), "bad unique id size for " << name);
       std::memcpy(&id, v.data(), sizeof(id));
     }
-    DLNB_NCCL_CHECK(ncclCommInitRank(&comm_, size_, id, rank_));
+    // CTA budget (runner.cpp: lanes x max_ctas <= the CUs the persistent
+    // compute leaves free), so every block of every concurrently live
+    // collective finds a CU and no kernel of one communicator can hold CUs
+    // that a peer's kernel of another communicator waits for.
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    if (max_ctas > 0) cfg.maxCTAs = max_ctas;
+    cfg.commName = name_.c_str();
+    DLNB_NCCL_CHECK(ncclCommInitRankConfig(&comm_, size_, id, rank_, &cfg));
   }
   ~RcclComm() override {
     if (comm_) (void)ncclCommDestroy(comm_);
@@ -109,9 +117,9 @@ class RcclFactory : public CommFactory {
   }
   std::string backend_name() const override { return "RCCL"; }
   std::unique_ptr<Communicator> create(const std::string& name, const std::vector<int>& members, size_t,
-                                       bool) override {
+                                       bool, int max_ctas) override {
     (void)hipSetDevice(dev_.index());
-    return std::unique_ptr<Communicator>(new RcclComm(name, members, world_.rank(), world_));
+    return std::unique_ptr<Communicator>(new RcclComm(name, members, world_.rank(), world_, max_ctas));
   }
 
  private:
@@ -126,7 +134,9 @@ std::unique_ptr<CommFactory> make_rccl_factory(HostGroup& world, Device& dev) {
 }
 
 double busbw_factor(CollKind k, int n) {
-  if (n <= 1) return 1.0;
+  // nccl-tests convention: a 1-rank collective moves nothing over a link
+  // (RCCL runs it as a local device copy), so its bus bandwidth is 0.
+  if (n <= 1) return 0.0;
   switch (k) {
     case CollKind::AllReduce: return 2.0 * (n - 1) / n;
     case CollKind::AllGather:

@@ -426,7 +426,7 @@ class ShmFactory : public CommFactory {
   }
   std::string backend_name() const override { return "CPU-SHM"; }
   std::unique_ptr<Communicator> create(const std::string& name, const std::vector<int>& members, size_t cap,
-                                       bool p2p) override {
+                                       bool p2p, int) override {
     return std::unique_ptr<Communicator>(new ShmComm(name, members, world_.rank(), world_, job_, cap, p2p));
   }
 

@@ -374,7 +374,7 @@ class XgmiFactory : public CommFactory {
   }
   std::string backend_name() const override { return "XGMI"; }
   std::unique_ptr<Communicator> create(const std::string& name, const std::vector<int>& members,
-                                       size_t capacity_bytes, bool need_p2p) override {
+                                       size_t capacity_bytes, bool need_p2p, int) override {
     return std::unique_ptr<Communicator>(
         new XgmiComm(name, members, world_.rank(), world_, capacity_bytes, need_p2p));
   }

@@ -135,6 +135,8 @@ class GpuCompute : public ComputeEngine {
       }
       return;
     }
+    // Fixed-work modes from here on: bracket the task with device stamps.
+    const int tok = task_timers_ && d > 0 ? task_timers_->begin(s) : -1;
     if (mode_ == ComputeMode::Flops) {
       double f = flops * scale_;
       for (const auto& lv : levels_) {
@@ -142,6 +144,7 @@ class GpuCompute : public ComputeEngine {
         for (long i = 0; i < n; ++i) launch(lv.M, s);
         f -= static_cast<double>(n) * lv.flops;
       }
+      end_task(tok, s, flops * scale_ / levels_.front().flops * levels_.front().us);
       return;
     }
     // gemm-work: greedy fill of the duration with calibrated launches, then spin.
@@ -152,6 +155,11 @@ class GpuCompute : public ComputeEngine {
       rem -= static_cast<double>(n) * lv.us;
     }
     if (rem > 1.0) kernels::busy_spin(ticks(rem), cus_, s.native());
+    end_task(tok, s, d);
+  }
+
+  void set_task_timers(TimerSet* t) override {
+    if (mode_ == ComputeMode::GemmWork || mode_ == ComputeMode::Flops) task_timers_ = t;
   }
 
   Json describe() const override {
@@ -185,6 +193,14 @@ class GpuCompute : public ComputeEngine {
 
  private:
   uint64_t ticks(double us) const { return static_cast<uint64_t>(us * 1e-6 * hz_ + 0.5); }
+
+  // table_us: the task's uncontended duration (gemm-work: the table time;
+  // flops: the calibrated time of its FLOPs at the largest GEMM level).
+  void end_task(int tok, Stream& s, double table_us) {
+    if (tok < 0) return;
+    task_timers_->end(tok, s, "compute_task_time");
+    task_timers_->add("compute_task_table", table_us * 1e-6);
+  }
 
   void launch(int M, Stream& s) {
     kernels::gemm_tn(A_.data(), B_.data(), C_.data(), M, N_, K_, K_, K_, N_, dtype_, s.native());
@@ -254,6 +270,7 @@ class GpuCompute : public ComputeEngine {
   int K_ = 4096, N_ = 16384;
   Buffer A_, B_, C_;
   std::vector<GemmLevel> levels_;
+  TimerSet* task_timers_ = nullptr;
 };
 
 }  // namespace

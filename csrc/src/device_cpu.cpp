@@ -2,6 +2,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -79,9 +80,16 @@ void CpuEvent::complete(uint64_t gen) {
   cv_.notify_all();
 }
 
+namespace {
+std::atomic<bool> g_abort_waits{false};
+}
+
+void abort_cpu_waits(bool on) { g_abort_waits.store(on); }
+
 void CpuEvent::wait_for(uint64_t gen) {
   std::unique_lock<std::mutex> g(mu_);
-  cv_.wait(g, [&] { return completed_ >= gen; });
+  while (!cv_.wait_for(g, std::chrono::milliseconds(20), [&] { return completed_ >= gen; }))
+    if (g_abort_waits.load()) return;
 }
 
 double CpuEvent::time_s() {
@@ -123,7 +131,7 @@ void CpuStream::run() {
       q_.pop_front();
     }
     try {
-      fn();
+      if (!g_abort_waits.load()) fn();
     } catch (const std::exception& e) {
       // A failed task would leave peers and other streams waiting forever:
       // fail the whole rank loudly (the launcher tears the job down).

@@ -106,6 +106,8 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  --silent               print nothing (the report is returned to the caller)\n"
      << "  --trace                emit roctx ranges (rocprofv3 --marker-trace)\n"
      << "  --comm-cus N           CUs the gemm compute leaves free for collectives (default 32)\n"
+     << "  --rccl-max-ctas N      RCCL blocks per collective on each comm lane (default: comm-cus / lanes;\n"
+     << "                         0 = RCCL's own choice)\n"
      << "  --comm-lanes single|split  fsdp: all collectives on one ordered lane (default) or one per kind\n"
      << "  --graph                capture one iteration into a HIP graph, replay it every iteration (rccl)\n"
      << "env: DLNB_TIMEOUT (s, hang detection), DLNB_INJECT_FAULT=rank=R,iter=I,mode=exit|hang|throw,\n"
@@ -192,6 +194,8 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
       o.topology = false;
     } else if (is("--comm-cus")) {
       o.comm_cus = to_int(val("comm-cus"), "comm-cus");
+    } else if (is("--rccl-max-ctas")) {
+      o.rccl_max_ctas = to_int(val("rccl-max-ctas"), "rccl-max-ctas");
     } else if (a == "--graph") {
       o.graph = true;
     } else if (is("--comm-lanes")) {

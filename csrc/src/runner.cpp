@@ -67,6 +67,9 @@ Json comm_stats_json(const std::vector<CommStat>& stats, const TimerSet& t) {
     double tot = 0;
     for (double x : v) tot += x;
     e["total_s"] = tot;
+    // A 1-rank group moves nothing over a link: its "collective" is a local
+    // device copy (or nothing), so it reports busbw 0 and says so.
+    e["transport"] = s.nranks > 1 ? "link" : "local-copy";
     if (!v.empty() && tot > 0) {
       double algbw = s.bytes_per_op * v.size() / tot / 1e9;
       e["algbw_GBps"] = algbw;
@@ -173,6 +176,19 @@ bool file_exists(const std::string& p) {
 
 }  // namespace
 
+int collective_lanes(const Options& o, int world) {
+  switch (o.strategy) {
+    case StrategyKind::DP: return 1;
+    case StrategyKind::FSDP: {
+      const int F = std::max(1, o.sharding_factor);
+      const bool replicas = world / F > 1;
+      return o.comm_lanes == "split" ? 2 + (replicas ? 1 : 0) : 1;
+    }
+    case StrategyKind::HybridCP: return 2;
+    default: return o.num_stages > 1 ? 3 : 1;
+  }
+}
+
 std::string select_backend(Context& ctx, const std::string& requested, const std::string& devices) {
   const RankInfo& ri = ctx.boot->info;
   std::string backend = requested;
@@ -231,6 +247,7 @@ Json run_loopback(const Options& opt) {
                "--backend loopback runs all ranks inside one process: launch it once, not under a multi-rank launcher");
   auto store = std::make_shared<LocalStore>();
   auto hub = make_loopback_hub(n, static_cast<double>(env_int("DLNB_STORE_TIMEOUT", 900)));
+  abort_cpu_waits(false);
   std::vector<Json> docs(static_cast<size_t>(n));
   std::mutex mu;
   std::string first_error;
@@ -264,10 +281,29 @@ Json run_benchmark(const Options& opt) {
 
 namespace {
 
+Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& strat);
+
 Json run_rank(const Options& opt, std::unique_ptr<Bootstrap> boot) {
+  // ctx and the strategy outlive the try block: a failing loopback rank
+  // aborts the hub (waking its peers' waits) BEFORE its streams are torn
+  // down - their destructors drain queued work that may wait on those peers.
   Context ctx;
   ctx.opt = opt;
   ctx.boot = std::move(boot);
+  std::unique_ptr<Strategy> strat;
+  try {
+    return run_rank_impl(opt, ctx, strat);
+  } catch (const std::exception& e) {
+    if (ctx.boot->hub) {
+      const std::string msg = "rank " + std::to_string(ctx.boot->info.rank) + ": " + e.what();
+      loopback_abort(*ctx.boot->hub, msg);
+      if (auto* ls = dynamic_cast<LocalStore*>(ctx.boot->store.get())) ls->abort(msg);
+    }
+    throw;
+  }
+}
+
+Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& strat) {
   const RankInfo& ri = ctx.boot->info;
 
   // ---- backend / device (cpp/utils.hpp:62-117 set_local_device)
@@ -307,11 +343,31 @@ Json run_rank(const Options& opt, std::unique_ptr<Bootstrap> boot) {
   FaultInjector fault(ri.rank);
   long long iter_no = 0;
 
-  auto strat = make_strategy(opt.strategy);
+  // ---- RCCL CTA budget: every comm lane's collective kernel must find CUs
+  // beside the persistent compute (which leaves comm_cus CUs free), so
+  // lanes x maxCTAs <= comm_cus; else blocks of one communicator's kernel can
+  // sit in the queue while another communicator's kernel holds the free CUs
+  // spinning on a peer that waits for them.
+  const int lanes = collective_lanes(opt, ri.world_size);
+  const bool rccl = backend == "rccl";
+  const bool gemm_compute = ctx.compute->mode() == ComputeMode::Gemm;
+  if (rccl) {
+    if (opt.rccl_max_ctas >= 0)
+      ctx.lane_ctas = opt.rccl_max_ctas;
+    else
+      ctx.lane_ctas = gemm_compute ? std::max(1, opt.comm_cus / lanes) : 0;
+    if (ctx.lane_ctas > 0 && gemm_compute && lanes * ctx.lane_ctas > opt.comm_cus && ri.rank == 0)
+      std::cerr << "[dlnb] warning: " << lanes << " comm lanes x " << ctx.lane_ctas << " RCCL CTAs > --comm-cus "
+                << opt.comm_cus << ": concurrent collectives may not all fit beside the compute" << std::endl;
+  }
+  strat = make_strategy(opt.strategy);
   {
     TraceRange tr("dlnb:setup");
     strat->setup(ctx);
   }
+  DLNB_REQUIRE(strat->streams().size() - 1 <= static_cast<size_t>(lanes),
+               strategy_name(opt.strategy) << " uses " << strat->streams().size() - 1
+                                           << " comm streams but collective_lanes() budgets " << lanes);
   if (ctx.dev->kind() == DeviceKind::GPU) {
     // More streams than hardware queues makes HIP share an in-order queue
     // between two streams: a collective spinning on its peers can then hold
@@ -325,6 +381,7 @@ Json run_rank(const Options& opt, std::unique_ptr<Bootstrap> boot) {
   TimerSet& T = *strat->timers();
   const char* rkey = strat->runtime_key();
   T.ensure(rkey);
+  ctx.compute->set_task_timers(&T);
 
   // ---- HIP graph: capture one iteration, replay it every iteration
   std::unique_ptr<GraphExec> graph;
@@ -423,6 +480,15 @@ Json run_rank(const Options& opt, std::unique_ptr<Bootstrap> boot) {
   rank["device_name"] = ctx.dev->name();
   rank["device_index"] = ctx.dev->index();
   rank["comm"] = strat->comm_summary();
+  // Fixed-work compute: measured task time / uncontended (table) time over
+  // the timed runs. > 1 means the collectives running beside the compute
+  // (HBM traffic, CUs, power) slowed it down.
+  const double task_s = T.sum("compute_task_time"), table_s = T.sum("compute_task_table");
+  if (!T.get("compute_task_time").empty() && table_s > 0) {
+    rank["compute_stretch"] = task_s / table_s;
+    rank["compute_task_s"] = task_s;
+    rank["compute_table_s"] = table_s;
+  }
   auto all = ctx.hg().allgather(rank.dump());
 
   Json g = strat->global_json();
@@ -440,6 +506,15 @@ Json run_rank(const Options& opt, std::unique_ptr<Bootstrap> boot) {
   ext["warmup_times"] = Json(warm);
   ext["timed_region_s"] = timed_region;
   ext["energy_source"] = meter->source();
+  {
+    Json b = Json::object();
+    b["lanes"] = lanes;
+    b["comm_cus"] = opt.comm_cus;
+    b["max_ctas_per_lane"] = ctx.lane_ctas;  // 0 = RCCL default
+    b["applies"] = rccl;
+    b["fits"] = !rccl || !gemm_compute || ctx.lane_ctas == 0 ? true : lanes * ctx.lane_ctas <= opt.comm_cus;
+    ext["rccl_cta_budget"] = b;
+  }
   {
     // Collective-library knobs of this run (the reference recorded them as
     // SbatchMan job variables, plots/parser.py:151-154).
@@ -473,6 +548,12 @@ Json run_rank(const Options& opt, std::unique_ptr<Bootstrap> boot) {
   double floor_us = strat->compute_floor_us(ctx);
   it["compute_floor_ms"] = floor_us / 1e3 * opt.time_scale;
   ext["iteration"] = it;
+  {
+    double worst = 0;
+    for (const auto& rj : ranks)
+      if (rj.contains("compute_stretch")) worst = std::max(worst, rj.at("compute_stretch").as_double());
+    if (worst > 0) ext["compute_stretch"] = worst;  // max over ranks
+  }
   g["dlnb"] = ext;
 
   doc["section"] = strat->section_id();

@@ -91,7 +91,7 @@ class ContextParallel : public Strategy {
     for (int i = 0; i < C_; ++i) cp_members.push_back(dp_id_ * C_ + i);
     if (C_ > 1) {
       size_t cap = (ring_ ? 2 * kv_ : C_ * std::max(qkv_peer_, out_peer_)) * es_;
-      cp_comm_ = ctx.comms->create("cp/" + std::to_string(dp_id_), cp_members, cap, ring_);
+      cp_comm_ = ctx.comms->create("cp/" + std::to_string(dp_id_), cp_members, cap, ring_, ctx.lane_ctas);
     }
     // Gradient buckets by layer (backward order); bucket k = layers
     // [k*L/nbk, (k+1)*L/nbk) counted from the last layer.
@@ -99,7 +99,7 @@ class ContextParallel : public Strategy {
     for (int b = 0; b < nbk_; ++b) bucket_.push_back(P / nbk_ + (static_cast<uint64_t>(b) < P % nbk_ ? 1 : 0));
     std::vector<int> all;
     for (int r = 0; r < W; ++r) all.push_back(r);
-    dp_comm_ = ctx.comms->create("cpdp/world", all, bucket_[0] * es_, false);
+    dp_comm_ = ctx.comms->create("cpdp/world", all, bucket_[0] * es_, false, ctx.lane_ctas);
 
     compute_ = dev.create_stream(false);
     cp_stream_ = dev.create_stream(true);

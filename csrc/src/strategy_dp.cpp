@@ -53,7 +53,7 @@ class DataParallel : public Strategy {
     for (uint64_t sz : sizes_) shard_.push_back((sz + W_ - 1) / W_);
     std::vector<int> all;
     for (int r = 0; r < ctx.world(); ++r) all.push_back(r);
-    comm_ = ctx.comms->create("dp/world", all, (zero_ ? shard_[0] * W_ : sizes_[0]) * es_, false);
+    comm_ = ctx.comms->create("dp/world", all, (zero_ ? shard_[0] * W_ : sizes_[0]) * es_, false, ctx.lane_ctas);
     compute_ = dev.create_stream(false);
     comm_stream_ = dev.create_stream(true);
     // Out-of-place like the reference unless asked (or forced by memory).

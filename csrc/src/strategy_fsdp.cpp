@@ -80,13 +80,13 @@ class Fsdp : public Strategy {
       lanes_.push_back(std::move(s));
       return lanes_.back().get();
     };
-    ag_comm_ = own_comm(ctx.comms->create("fsdp/unit/" + std::to_string(rank / F_), unit_members, unit_bytes, false));
+    ag_comm_ = own_comm(ctx.comms->create("fsdp/unit/" + std::to_string(rank / F_), unit_members, unit_bytes, false, ctx.lane_ctas));
     rs_comm_ = split ? own_comm(ctx.comms->create("fsdp/unit_rs/" + std::to_string(rank / F_), unit_members,
-                                                  unit_bytes, false))
+                                                  unit_bytes, false, ctx.lane_ctas))
                      : ag_comm_;
     if (R_ > 1)
       ar_comm_ = own_comm(
-          ctx.comms->create("fsdp/replica/" + std::to_string(rank % F_), rep_members, max_shard_ * es_, false));
+          ctx.comms->create("fsdp/replica/" + std::to_string(rank % F_), rep_members, max_shard_ * es_, false, ctx.lane_ctas));
 
     compute_ = dev.create_stream(false);
     ag_stream_ = own_stream(dev.create_stream(true));

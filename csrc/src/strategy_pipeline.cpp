@@ -180,7 +180,7 @@ class Pipeline : public Strategy {
     for (int s = 0; s + 1 < S_; ++s) {
       if (stage_ == s || stage_ == s + 1) {
         std::string nm = "pp/link/" + std::to_string(dp_id_) + "/" + std::to_string(inner_id_) + "/" + std::to_string(s);
-        auto comm = ctx.comms->create(nm, {pp[s], pp[s + 1]}, pipe_ * es_, true);
+        auto comm = ctx.comms->create(nm, {pp[s], pp[s + 1]}, pipe_ * es_, true, ctx.lane_ctas);
         if (stage_ == s) {
           next_ = std::move(comm);
           next_peer_ = 1;
@@ -195,7 +195,7 @@ class Pipeline : public Strategy {
       // feeds chunk c+1 of stage 0 over a wrap link.
       if (stage_ == S_ - 1 || stage_ == 0) {
         std::string nm = "pp/wrap/" + std::to_string(dp_id_) + "/" + std::to_string(inner_id_);
-        auto comm = ctx.comms->create(nm, {pp[S_ - 1], pp[0]}, pipe_ * es_, true);
+        auto comm = ctx.comms->create(nm, {pp[S_ - 1], pp[0]}, pipe_ * es_, true, ctx.lane_ctas);
         if (stage_ == S_ - 1) {
           next_ = std::move(comm);
           next_peer_ = 1;
@@ -224,13 +224,14 @@ class Pipeline : public Strategy {
         for (int e = 0; e < E_; ++e) m.push_back(base + e * T_ + tp_id_);
         const uint64_t cap = skew_counts_.empty() ? a2a_ * E_ : std::max<uint64_t>(a2a_ * E_, skew_counts_[0]);
         ep_comm_ = ctx.comms->create("ep/" + where + "/" + std::to_string(tp_id_), m,
-                                     std::max<uint64_t>(cap, ne_) * es_, !skew_counts_.empty());
+                                     std::max<uint64_t>(cap, ne_) * es_, !skew_counts_.empty(),
+                                     o.ep_overlap ? ctx.lane_ctas : 0);  // --ep-overlap: on the DP lane
       }
     }
     {
       std::string nm = "dp/" + std::to_string(stage_) + "/" + std::to_string(inner_id_);
       const int nbk = o.dp_buckets;
-      dp_comm_ = ctx.comms->create(nm, dp_group(rank, inner_, S_, W), (dp_ar_ / nbk + 1) * es_, false);
+      dp_comm_ = ctx.comms->create(nm, dp_group(rank, inner_, S_, W), (dp_ar_ / nbk + 1) * es_, false, ctx.lane_ctas);
       dp_stream_ = dev.create_stream(true);
     }
     if (dualpipe_) {
@@ -240,7 +241,7 @@ class Pipeline : public Strategy {
       std::vector<int> pair = {pp[lo], pp[S_ - 1 - lo]};
       mirror_comm_ = ctx.comms->create("pp/mirror/" + std::to_string(dp_id_) + "/" + std::to_string(inner_id_) + "/" +
                                            std::to_string(lo),
-                                       pair, dp_ar_ * es_, false);
+                                       pair, dp_ar_ * es_, false, ctx.lane_ctas);
       build_dualpipe();
       for (int k = 0; k < 2 * mb_; ++k) dpbuf_.push_back(dev.alloc(pipe_ * es_));
       mirror_ready_ = dev.create_event();
@@ -544,7 +545,13 @@ class Pipeline : public Strategy {
     if (nbk == 1 || reference_) {
       compute_->record(*bucket_ready_[0]);
       dp_stream_->wait(*bucket_ready_[0]);
-      if (mirror_comm_) {
+      if (mirror_comm_ && mirror_early_tick_ < 0) {
+        // MoE: the whole pair gradient after the EP all-reduce
+        int tm = timers_->begin(*dp_stream_);
+        mirror_comm_->all_reduce(grad_.data(), grad_.data(), dp_ar_, t, *dp_stream_);
+        timers_->end(tm, *dp_stream_, "pp_mirror_time");
+        dp_allreduce_bucket(0, 1);
+      } else if (mirror_comm_) {
         // the half whose chunks finish last (model stage min(s, S-1-s)); the
         // other half was reduced mid-backward (enqueue_dualpipe)
         const size_t half = dp_ar_ / 2;
@@ -865,6 +872,16 @@ class Pipeline : public Strategy {
     // stays tick-ordered.
     const int lo = std::min(stage_, S_ - 1 - stage_), hi = S_ - 1 - lo;
     mirror_early_tick_ = std::max(bdone[idx(lo, 1, H - 1)], bdone[idx(hi, 0, H - 1)]);
+    // With EP the non-expert gradients [0, ne_) - which span the early half -
+    // are first all-reduced over the EP group on the compute stream at the end
+    // of the backward (reference order: EP, then DP); an early pair / DP
+    // all-reduce of that range would race it. MoE syncs the whole gradient
+    // after the backward instead.
+    if (has_ep_) mirror_early_tick_ = -1;
+    for (size_t k = 0; k < dp_ticks_.size(); ++k) {
+      const DpOp& op = dp_ticks_[k][static_cast<size_t>(stage_)];
+      if (op.dir >= 0 && op.bwd) last_bwd_tick_ = static_cast<int>(k);
+    }
   }
 
   // Event / buffer slot of (dir, mb): activations [0, mb), gradients [mb, 2 mb).
@@ -977,6 +994,7 @@ class Pipeline : public Strategy {
     }
     if (tp_comm_) cs.push_back(tp_comm_.get());
     if (ep_comm_) cs.push_back(ep_comm_.get());
+    if (mirror_comm_) cs.push_back(mirror_comm_.get());
     sync_streams(ss, cs, *ctx_->dev);
     timers_->resolve();
   }
@@ -1062,7 +1080,11 @@ class Pipeline : public Strategy {
     r["pp_send_time"] = timers_->values_json("pp_send_time");
     r["pp_recv_time"] = timers_->values_json("pp_recv_time");
     r["dp_exposed_time"] = timers_->values_json("dp_exposed_time");
-    if (dualpipe_) r["pp_mirror_time"] = timers_->values_json("pp_mirror_time");
+    if (dualpipe_) {
+      r["pp_mirror_time"] = timers_->values_json("pp_mirror_time");
+      r["dualpipe_early_sync_tick"] = mirror_early_tick_;  // -1: whole gradient after the backward (MoE)
+      r["dualpipe_last_backward_tick"] = last_bwd_tick_;
+    }
     r["stage_id"] = stage_;
     if (has_tp_) r["tp_id"] = tp_id_;
     if (has_ep_) r["ep_id"] = ep_id_;
@@ -1083,7 +1105,8 @@ class Pipeline : public Strategy {
   bool one_f_one_b_ = false, interleaved_ = false, dualpipe_ = false;
   std::vector<std::vector<DpOp>> dp_ticks_;  // [tick][stage]
   double dp_floor_us_ = 0;
-  int mirror_early_tick_ = -1;  // tick after which the first half of the mirror all-reduce is issued
+  int mirror_early_tick_ = -1;  // tick after which the first half of the mirror all-reduce is issued (-1: none)
+  int last_bwd_tick_ = -1;      // this stage's last backward tick (dualpipe)
   std::unique_ptr<Event> mirror_ready_;
   std::vector<Buffer> dpbuf_;  // receive buffers per (dir, microbatch): activations, then gradients
   std::unique_ptr<Communicator> mirror_comm_;

@@ -29,7 +29,7 @@ _FLAG = {
     "dp_buckets": "--dp-buckets", "max_loop_iters": "--max-loop-iters", "time_scale": "--time-scale",
     "json": "--json", "store": "--store", "stats_file": "--stats-file", "comm_cus": "--comm-cus",
     "comm_lanes": "--comm-lanes", "pp_schedule": "--pp-schedule", "zero": "--zero", "cp_algo": "--cp-algo", "pp_virtual": "--pp-virtual",
-    "ranks": "--ranks", "ep_imbalance": "--ep-imbalance",
+    "ranks": "--ranks", "ep_imbalance": "--ep-imbalance", "rccl_max_ctas": "--rccl-max-ctas",
 }
 _BOOL = {"in_place": "--in-place", "optimizer": "--optimizer", "loop": "--loop", "quiet": "--quiet",
          "silent": "--silent", "graph": "--graph", "trace": "--trace", "ep_overlap": "--ep-overlap",

@@ -273,9 +273,11 @@ def plan_cp(st: ModelStats, world: int, C: int, layers: int, heads: int, kv_head
 
 
 def busbw_factor(op: str, n: int) -> float:
-    """nccl-tests bus-bandwidth factor (BASELINE.md 'Metric definitions')."""
+    """nccl-tests bus-bandwidth factor (BASELINE.md 'Metric definitions').
+
+    0 for a single rank: nothing crosses a link (the op is a local copy)."""
     if n <= 1:
-        return 1.0
+        return 0.0
     if op == "allreduce":
         return 2.0 * (n - 1) / n
     if op in ("allgather", "reduce_scatter", "alltoall"):

@@ -1,0 +1,103 @@
+"""bench.py's driver contract: the N > 1 launch (torchrun, one process per
+rank, native TCP rendezvous through the store file), exactly one JSON line
+from rank 0, honest bus bandwidth (null at 1 rank) and the secondary
+comm-bound / compute-stretch blocks. CPU backend here; the GPU variant runs
+the same file at N = 1 on the box."""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DATA = os.path.join(ROOT, "tests", "data")
+TINY = ["--model", "tiny_dense_8_bfloat16", "--base-path", DATA, "--c5-model", "tiny_dense_8_bfloat16",
+        "--units", "4", "--c5-steps", "3"]
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _json_lines(out: str):
+    return [json.loads(ln) for ln in out.splitlines() if ln.strip().startswith("{")]
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_torchrun_cpu(n, tmp_path):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(n), "--steps", "2", "--warmup", "1", "--backend", "cpu", "--compute", "sleep"] + TINY
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=str(tmp_path),
+                       env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout  # rank 0 only, nothing else on stdout
+    o = lines[0]
+    assert o["n_gpus"] == n and o["steps"] == 2 and o["warmup"] == 1
+    assert o["config"]["parallelism"] == f"fsdp{n}" and o["config"]["sharding_factor"] == n
+    assert o["config"]["global_batch"] == 8 * n
+    assert o["higher_is_better"] is False and o["scaling"] == "weak"
+    assert o["ms_per_step"] == o["value"] > 0
+    assert o["effective_busbw_GBps"]["allgather"] > 0 and o["effective_busbw_GBps"]["reduce_scatter"] > 0
+    c5 = o["comm_bound"]
+    assert "error" not in c5, c5
+    assert c5["strategy"] == f"dp{n}" and c5["transport"] == "link" and c5["allreduce_busbw_GBps"] > 0
+    assert c5["floor_ms"] == pytest.approx(6.0) and c5["ms_per_step"] >= c5["floor_ms"] * 0.9
+    assert c5["exposed_comm_ms"] is not None
+    assert o["rccl_cta_budget"]["lanes"] == 1
+
+
+def test_bench_single_rank_reports_no_bus_bandwidth(tmp_path):
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "0",
+                        "--backend", "cpu", "--compute", "sleep"] + TINY,
+                       capture_output=True, text=True, timeout=120, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1
+    o = lines[0]
+    assert o["n_gpus"] == 1
+    # a 1-rank all-gather / reduce-scatter / all-reduce is a local copy: no link bandwidth
+    assert o["effective_busbw_GBps"] == {"allgather": None, "reduce_scatter": None}
+    assert o["comm_bound"]["allreduce_busbw_GBps"] is None and o["comm_bound"]["transport"] == "local-copy"
+
+
+def test_busbw_zero_for_one_rank_in_report(data_dir):
+    sys.path.insert(0, ROOT)
+    from dlnetbench_amd import engine
+    d = engine.run("dp", "tiny_dense_8_bfloat16", 4, base_path=data_dir, backend="cpu", compute="sleep", warmup=0,
+                   runs=2, silent=True)
+    c = d["ranks"][0]["comm"]["allreduce"]
+    assert c["transport"] == "local-copy" and c["busbw_GBps"] == 0.0
+    b = d["global"]["dlnb"]["rccl_cta_budget"]
+    assert b == {"lanes": 1, "comm_cus": 32, "max_ctas_per_lane": 0, "applies": False, "fits": True}
+
+
+@pytest.mark.gpu
+def test_bench_gpu_single_rank_secondaries(tmp_path):
+    """bench.py at N = 1 on the GPU with the tiny model: headline + comm-bound
+    block + fixed-work compute stretch, one JSON line."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1"] + TINY,
+                       capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    o = lines[0]
+    assert o["config"]["backend"] == "RCCL" and o["config"]["hip_graph"] is True
+    assert o["effective_busbw_GBps"] == {"allgather": None, "reduce_scatter": None}
+    c5 = o["comm_bound"]
+    assert "error" not in c5, c5
+    assert c5["transport"] == "local-copy" and c5["allreduce_busbw_GBps"] is None
+    assert c5["ms_per_step"] >= 0.9 * c5["floor_ms"]
+    assert 0.8 < c5["gemm_work"]["compute_stretch"] < 1.5, c5
+    assert 0.8 < o["compute_stretch"] < 1.5, o
+    assert o["rccl_cta_budget"]["applies"] and o["rccl_cta_budget"]["max_ctas_per_lane"] == 32

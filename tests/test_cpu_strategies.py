@@ -444,9 +444,19 @@ def test_dualpipe(w, prog, model, params, data_dir):
     assert it["compute_floor_ms"] * 1e3 >= mb * (f + b) - 1e-6
     if S >= 4:
         assert it["compute_floor_ms"] * 1e3 < (mb + S - 1) * (f + b)
+    moe = prog == "hybrid_3d_moe"
     for r in d["ranks"]:
-        # two mirror all-reduces per iteration: the early half mid-backward, the rest at the end
-        assert len(r["pp_mirror_time"]) == 2 * 2 and len(r["runtimes"]) == 2
+        assert len(r["runtimes"]) == 2
+        if moe:
+            # EP all-reduce of the non-expert gradients first, then the whole pair / DP sync
+            assert r["dualpipe_early_sync_tick"] == -1
+            assert len(r["pp_mirror_time"]) == 2 and len(r["dp_comm_time"]) == 2
+        else:
+            # two mirror all-reduces and two DP all-reduces per iteration: the
+            # early half is issued mid-backward (before this stage's last
+            # backward tick), the rest after the backward
+            assert len(r["pp_mirror_time"]) == 2 * 2 and len(r["dp_comm_time"]) == 2 * 2
+            assert 0 <= r["dualpipe_early_sync_tick"] < r["dualpipe_last_backward_tick"]
 
 
 @pytest.mark.parametrize("params,extra,msg", [((3, 6), [], "even number of stages"),

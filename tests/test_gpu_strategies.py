@@ -153,3 +153,37 @@ def test_fsdp_llama3_8b_loopback_8_ranks_one_gpu(root):
     assert g["allgather_msg_size_bytes"] == 250945664 * 2  # the gathered unit, as at N=1
     it = g["dlnb"]["iteration"]
     assert it["median_ms"] >= 0.9 * it["compute_floor_ms"]
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_compute_stretch_fixed_work(graph, data_dir):
+    """gemm-work compute times every task on the device: measured / uncontended
+    time is reported per rank and as the max over ranks (global.dlnb)."""
+    doc = engine.run("fsdp", "tiny_dense_8_bfloat16", 4, 1, base_path=data_dir, warmup=1, runs=3,
+                     compute="gemm-work", backend="rccl", quiet=True, graph=graph or None)
+    s = doc["global"]["dlnb"]["compute_stretch"]
+    r = doc["ranks"][0]
+    assert r["compute_task_s"] > 0 and r["compute_table_s"] > 0
+    assert s == pytest.approx(r["compute_stretch"])
+    # 1 rank: the only contention is the local copies; the calibrated GEMM
+    # count reproduces the table time to within launch gaps
+    assert 0.8 < s < 1.5, s
+    # deadline compute lasts the table time by construction: nothing to report
+    doc = engine.run("fsdp", "tiny_dense_8_bfloat16", 4, 1, base_path=data_dir, warmup=1, runs=2,
+                     compute="gemm", backend="rccl", quiet=True)
+    assert "compute_stretch" not in doc["global"]["dlnb"]
+
+
+def test_rccl_cta_budget(data_dir):
+    doc = engine.run("dp", "tiny_dense_8_bfloat16", 4, base_path=data_dir, warmup=1, runs=2, compute="gemm",
+                     backend="rccl", quiet=True)
+    assert doc["global"]["dlnb"]["rccl_cta_budget"] == {"lanes": 1, "comm_cus": 32, "max_ctas_per_lane": 32,
+                                                         "applies": True, "fits": True}
+    doc = engine.run("hybrid_cp", "tiny_dense_8_bfloat16", 1, base_path=data_dir, warmup=1, runs=2,
+                     compute="gemm", backend="rccl", quiet=True, comm_cus=48)
+    b = doc["global"]["dlnb"]["rccl_cta_budget"]
+    assert b["lanes"] == 2 and b["max_ctas_per_lane"] == 24 and b["fits"]
+    doc = engine.run("dp", "tiny_dense_8_bfloat16", 4, base_path=data_dir, warmup=1, runs=2, compute="gemm",
+                     backend="rccl", quiet=True, rccl_max_ctas=64)
+    b = doc["global"]["dlnb"]["rccl_cta_budget"]
+    assert b["max_ctas_per_lane"] == 64 and not b["fits"]

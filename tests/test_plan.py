@@ -88,7 +88,7 @@ def test_busbw_factors():
     assert P.busbw_factor("allreduce", 8) == pytest.approx(1.75)
     assert P.busbw_factor("allgather", 8) == pytest.approx(0.875)
     assert P.busbw_factor("sendrecv", 2) == 1.0
-    assert P.busbw_factor("allreduce", 1) == 1.0
+    assert P.busbw_factor("allreduce", 1) == 0.0
 
 
 def test_invalid_layouts(stats):
