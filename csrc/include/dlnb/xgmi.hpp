@@ -14,6 +14,14 @@
 // order on the peer guarantees piece k-2 is fully consumed when any of its
 // blocks reached piece k-1's flags).
 //
+// Sequence numbers live on the device: a collective's epoch (and with it the
+// parity region) and a point-to-point message's number are read from
+// per-communicator counters in the rank's own flag page when the kernel
+// starts, and the last block of the kernel to finish advances them. Kernel
+// arguments therefore carry no sequence state, so a captured HIP graph that
+// is replayed issues fresh epochs on every replay exactly like eager launches
+// (every member still issues the same sequence of kernels per communicator).
+//
 // Reference equivalent: none (the reference only calls NCCL/RCCL/MPI,
 // cpp/proxy_classes.hpp:135-253); this is new MI355X-native capability.
 #pragma once
@@ -34,8 +42,15 @@ constexpr int kThreads = 512;
 constexpr size_t kFlagColl = 0;                                    // [phase 2][src 8][block 256]
 constexpr size_t kFlagP2PSeq = 2 * kMaxRanks * kMaxBlocks;         // [src 8][block 256]
 constexpr size_t kFlagP2PConsumed = kFlagP2PSeq + kMaxRanks * kMaxBlocks;  // [dst 8]
-constexpr size_t kFlagP2PCount = kFlagP2PConsumed + 64;            // [src 8] local block counters
-constexpr size_t kFlagWords = kFlagP2PCount + 64;
+// Local-only control words (never touched by peers):
+constexpr size_t kCtl = kFlagP2PConsumed + 64;
+constexpr size_t kCtlCollEpoch = kCtl;           // last finished collective epoch
+constexpr size_t kCtlCollDone = kCtl + 1;        // blocks of the running collective that finished
+constexpr size_t kCtlSendSeq = kCtl + 16;        // [dst 8] last message number sent to dst
+constexpr size_t kCtlSendDone = kCtl + 32;       // [dst 8] finished blocks of the running send
+constexpr size_t kCtlRecvSeq = kCtl + 48;        // [src 8] last message number received from src
+constexpr size_t kCtlRecvDone = kCtl + 64;       // [src 8] finished blocks of the running receive
+constexpr size_t kFlagWords = kCtl + 80;
 constexpr size_t kFlagBytes = 64 * 1024;
 
 struct Peers {
@@ -56,10 +71,9 @@ struct CollPiece {
   size_t bytes;        // bytes per rank block of this piece
   size_t send_stride;  // bytes between rank blocks in send (RS, A2A)
   size_t recv_stride;  // bytes between rank blocks in recv (AG, A2A)
-  size_t region;       // parity region offset in the windows
+  size_t region;       // bytes per parity region (epoch e uses region (e & 1))
   size_t slot;         // bytes between source slots inside the region
   size_t ag_off;       // two-shot: offset of the all-gather slots inside the region
-  uint32_t epoch;
   DType dtype;
 };
 
@@ -68,15 +82,14 @@ int blocks_for(size_t bytes, int max_blocks);
 
 void launch_coll(Op op, const Peers& p, const CollPiece& c, int blocks, void* stream);
 
-// Point-to-point: message n (1-based) of the (me -> dst) channel goes to
-// parity region n & 1 of dst's window at offset `off`; the sender waits until
-// dst consumed message n-2.
-void launch_send(const Peers& p, const char* buf, size_t bytes, int dst, size_t off, uint32_t n, int blocks,
+// Point-to-point: message n (1-based, counted on the device) of the
+// (me -> dst) channel goes to dst's window at `off + (n & 1) * slot`; the
+// sender waits until dst consumed message n-2. The receiver's last block to
+// finish signals "consumed n" back to the sender.
+void launch_send(const Peers& p, const char* buf, size_t bytes, int dst, size_t off, size_t slot, int blocks,
                  void* stream);
-// `target` = cumulative number of receive blocks on the (src -> me) channel
-// after this message (the last block to finish signals "consumed").
-void launch_recv(const Peers& p, char* buf, size_t bytes, int src, size_t off, uint32_t n, uint32_t target,
-                 int blocks, void* stream);
+void launch_recv(const Peers& p, char* buf, size_t bytes, int src, size_t off, size_t slot, int blocks,
+                 void* stream);
 
 // Loopback backend (all ranks in one process on one device): for i < count,
 // dsts[d][i] = sum over s of srcs[s][i] (fp32 accumulation, one rounding;

@@ -47,13 +47,16 @@ __device__ __forceinline__ uint32_t sys_load(uint32_t* p) {
 
 // Spin until *f >= v (wrap-safe). Every wait has an exit: the host's abort
 // word or the timeout (which also raises the error word), so a dead peer
-// never leaves a grid that cannot drain.
+// never leaves a grid that cannot drain. Once any wait of the communicator
+// timed out, the later ones give up at their first check instead of each
+// waiting out the full timeout (the queued work then drains in moments).
 __device__ void wait_geq(uint32_t* f, uint32_t v, const Peers& P) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (unsigned k = 1; static_cast<int>(sys_load(f) - v) < 0; ++k) {
     __builtin_amdgcn_s_sleep(1);
     if ((k & 255u) == 0) {
       if (__hip_atomic_load(P.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
+      if (__hip_atomic_load(P.error_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return;
       if (__builtin_amdgcn_s_memrealtime() - t0 > P.timeout_ticks) {
         __hip_atomic_store(P.error_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
@@ -64,6 +67,32 @@ __device__ void wait_geq(uint32_t* f, uint32_t v, const Peers& P) {
 
 __device__ __forceinline__ uint32_t* coll_flag(const Peers& P, int owner, int phase, int src) {
   return P.flags[owner] + kFlagColl + (static_cast<size_t>(phase) * kMaxRanks + src) * kMaxBlocks + blockIdx.x;
+}
+
+// Sequence number of this kernel on a counter of the rank's own flag page:
+// the value the previous kernel on the communicator published, plus one.
+// Every block reads it before any block of the kernel can finish (the last
+// block to finish is the one that advances it), so all blocks agree.
+__device__ __forceinline__ uint32_t begin_seq(const Peers& P, size_t word) {
+  __shared__ uint32_t seq;
+  if (threadIdx.x == 0)
+    seq = __hip_atomic_load(P.flags[P.rank] + word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  __syncthreads();
+  return seq;
+}
+
+// Count this block as finished; the last one resets the block counter and
+// publishes `seq` for the next kernel (stream order makes it visible there).
+// Returns true in thread 0 of the last block.
+__device__ __forceinline__ bool end_seq(const Peers& P, size_t word, size_t done, uint32_t seq) {
+  __syncthreads();
+  if (threadIdx.x != 0) return false;
+  uint32_t* f = P.flags[P.rank];
+  const uint32_t old = __hip_atomic_fetch_add(f + done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (old + 1 != gridDim.x) return false;
+  __hip_atomic_store(f + done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(f + word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
 }
 
 // This block's window stores are visible system-wide -> raise one flag per
@@ -285,32 +314,37 @@ __device__ __forceinline__ void push_all(const Peers& P, const uint4* __restrict
 }
 
 __global__ void __launch_bounds__(T) ag_kernel(Peers P, CollPiece c) {
+  const uint32_t ep = begin_seq(P, kCtlCollEpoch);
+  const size_t rg = (ep & 1) * c.region;
   const size_t nv = c.bytes / 16;
   size_t lo, hi;
   blk_range(nv, lo, hi);
   char* own = c.recv + static_cast<size_t>(P.rank) * c.recv_stride;
   const bool in_place = own == c.send;
   // push my block into slot[rank] of every peer's window (+ my own recv)
-  push_all(P, V(c.send), c.region + c.slot * P.rank, in_place ? nullptr : V(own), lo, hi);
-  for (int j = 1; j < P.nranks; ++j) copy_tail(P.win[peer_at(P, j)] + c.region + c.slot * P.rank, c.send, nv * 16, c.bytes);
+  push_all(P, V(c.send), rg + c.slot * P.rank, in_place ? nullptr : V(own), lo, hi);
+  for (int j = 1; j < P.nranks; ++j) copy_tail(P.win[peer_at(P, j)] + rg + c.slot * P.rank, c.send, nv * 16, c.bytes);
   if (!in_place) copy_tail(own, c.send, nv * 16, c.bytes);
-  exchange(P, 0, c.epoch);
+  exchange(P, 0, ep);
   for (int j = 1; j < P.nranks; ++j) {
     const int src = peer_at(P, P.nranks - j);
-    const char* w = P.win[P.rank] + c.region + c.slot * src;
+    const char* w = P.win[P.rank] + rg + c.slot * src;
     char* d = c.recv + static_cast<size_t>(src) * c.recv_stride;
     copy_vec(V(d), V(w), lo, hi);
     copy_tail(d, w, nv * 16, c.bytes);
   }
+  end_seq(P, kCtlCollEpoch, kCtlCollDone, ep);
 }
 
 __global__ void __launch_bounds__(T) a2a_kernel(Peers P, CollPiece c) {
+  const uint32_t ep = begin_seq(P, kCtlCollEpoch);
+  const size_t rg = (ep & 1) * c.region;
   const size_t nv = c.bytes / 16;
   size_t lo, hi;
   blk_range(nv, lo, hi);
   for (int j = 1; j < P.nranks; ++j) {
     const int p = peer_at(P, j);
-    char* w = P.win[p] + c.region + c.slot * P.rank;
+    char* w = P.win[p] + rg + c.slot * P.rank;
     const char* s = c.send + static_cast<size_t>(p) * c.send_stride;
     copy_vec(V(w), V(s), lo, hi);
     copy_tail(w, s, nv * 16, c.bytes);
@@ -321,61 +355,70 @@ __global__ void __launch_bounds__(T) a2a_kernel(Peers P, CollPiece c) {
     copy_vec(V(d), V(s), lo, hi);
     copy_tail(d, s, nv * 16, c.bytes);
   }
-  exchange(P, 0, c.epoch);
+  exchange(P, 0, ep);
   for (int j = 1; j < P.nranks; ++j) {
     const int src = peer_at(P, P.nranks - j);
-    const char* w = P.win[P.rank] + c.region + c.slot * src;
+    const char* w = P.win[P.rank] + rg + c.slot * src;
     char* d = c.recv + static_cast<size_t>(src) * c.recv_stride;
     copy_vec(V(d), V(w), lo, hi);
     copy_tail(d, w, nv * 16, c.bytes);
   }
+  end_seq(P, kCtlCollEpoch, kCtlCollDone, ep);
 }
 
 template <DType D>
 __global__ void __launch_bounds__(T) rs_kernel(Peers P, CollPiece c) {
+  const uint32_t ep = begin_seq(P, kCtlCollEpoch);
+  const size_t rg = (ep & 1) * c.region;
   const size_t es = sizeof(uint4) / Elt<D>::N;
   const size_t nv = c.bytes / 16;
   size_t lo, hi;
   blk_range(nv, lo, hi);
   for (int j = 1; j < P.nranks; ++j) {
     const int p = peer_at(P, j);
-    char* w = P.win[p] + c.region + c.slot * P.rank;
+    char* w = P.win[p] + rg + c.slot * P.rank;
     const char* s = c.send + static_cast<size_t>(p) * c.send_stride;
     copy_vec(V(w), V(s), lo, hi);
     copy_tail(w, s, nv * 16, c.bytes);
   }
-  exchange(P, 0, c.epoch);
+  exchange(P, 0, ep);
   const uint4* srcs[kMaxRanks];
   const char* srcb[kMaxRanks];
   srcb[0] = c.send + static_cast<size_t>(P.rank) * c.send_stride;
-  for (int j = 1; j < P.nranks; ++j) srcb[j] = P.win[P.rank] + c.region + c.slot * peer_at(P, j);
+  for (int j = 1; j < P.nranks; ++j) srcb[j] = P.win[P.rank] + rg + c.slot * peer_at(P, j);
   for (int j = 0; j < P.nranks; ++j) srcs[j] = V(srcb[j]);
   reduce_vec<D>(V(c.recv), srcs, P.nranks, lo, hi);
   reduce_tail<D>(c.recv, srcb, P.nranks, nv * 16 / es, c.bytes / es);
+  end_seq(P, kCtlCollEpoch, kCtlCollDone, ep);
 }
 
 template <DType D>
 __global__ void __launch_bounds__(T) ar1_kernel(Peers P, CollPiece c) {
+  const uint32_t ep = begin_seq(P, kCtlCollEpoch);
+  const size_t rg = (ep & 1) * c.region;
   const size_t es = sizeof(uint4) / Elt<D>::N;
   const size_t nv = c.bytes / 16;
   size_t lo, hi;
   blk_range(nv, lo, hi);
-  push_all(P, V(c.send), c.region + c.slot * P.rank, nullptr, lo, hi);
-  for (int j = 1; j < P.nranks; ++j) copy_tail(P.win[peer_at(P, j)] + c.region + c.slot * P.rank, c.send, nv * 16, c.bytes);
-  exchange(P, 0, c.epoch);
+  push_all(P, V(c.send), rg + c.slot * P.rank, nullptr, lo, hi);
+  for (int j = 1; j < P.nranks; ++j) copy_tail(P.win[peer_at(P, j)] + rg + c.slot * P.rank, c.send, nv * 16, c.bytes);
+  exchange(P, 0, ep);
   // every rank sums in the same (rank) order -> bitwise identical results
   const uint4* srcs[kMaxRanks];
   const char* srcb[kMaxRanks];
-  for (int r = 0; r < P.nranks; ++r) srcb[r] = r == P.rank ? c.send : P.win[P.rank] + c.region + c.slot * r;
+  for (int r = 0; r < P.nranks; ++r) srcb[r] = r == P.rank ? c.send : P.win[P.rank] + rg + c.slot * r;
   for (int r = 0; r < P.nranks; ++r) srcs[r] = V(srcb[r]);
   reduce_vec<D>(V(c.recv), srcs, P.nranks, lo, hi);
   reduce_tail<D>(c.recv, srcb, P.nranks, nv * 16 / es, c.bytes / es);
+  end_seq(P, kCtlCollEpoch, kCtlCollDone, ep);
 }
 
 // Two-shot (reduce-scatter + all-gather inside one kernel). c.bytes is a
 // multiple of 16; chunk p = vectors [p*cv, min((p+1)*cv, nv)).
 template <DType D>
 __global__ void __launch_bounds__(T) ar2_kernel(Peers P, CollPiece c) {
+  const uint32_t ep = begin_seq(P, kCtlCollEpoch);
+  const size_t rg = (ep & 1) * c.region;
   const size_t nv = c.bytes / 16;
   const size_t cv = (nv + P.nranks - 1) / P.nranks;
   size_t lo, hi;  // this block's slice of a chunk
@@ -384,15 +427,15 @@ __global__ void __launch_bounds__(T) ar2_kernel(Peers P, CollPiece c) {
   // 1. chunk p -> peer p's RS slot[rank]
   for (int j = 1; j < P.nranks; ++j) {
     const int p = peer_at(P, j);
-    copy_vec(V(P.win[p] + c.region + c.slot * P.rank), V(c.send) + p * cv, lo, chunk_hi(p, hi));
+    copy_vec(V(P.win[p] + rg + c.slot * P.rank), V(c.send) + p * cv, lo, chunk_hi(p, hi));
   }
-  exchange(P, 0, c.epoch);
+  exchange(P, 0, ep);
   // 2. reduce my chunk (rank order), write it to recv and to every peer's AG slot[rank]
   const uint4* srcs[kMaxRanks];
   for (int r = 0; r < P.nranks; ++r)
-    srcs[r] = r == P.rank ? V(c.send) + P.rank * cv : V(P.win[P.rank] + c.region + c.slot * r);
+    srcs[r] = r == P.rank ? V(c.send) + P.rank * cv : V(P.win[P.rank] + rg + c.slot * r);
   uint4* outs[kMaxRanks];
-  for (int j = 1; j < P.nranks; ++j) outs[j - 1] = V(P.win[peer_at(P, j)] + c.region + c.ag_off + c.slot * P.rank);
+  for (int j = 1; j < P.nranks; ++j) outs[j - 1] = V(P.win[peer_at(P, j)] + rg + c.ag_off + c.slot * P.rank);
   // srcs are chunk-relative; recv chunk rank
   {
     using E = Elt<D>;
@@ -411,44 +454,44 @@ __global__ void __launch_bounds__(T) ar2_kernel(Peers P, CollPiece c) {
       for (int o = 0; o + 1 < P.nranks; ++o) outs[o][i] = r;
     }
   }
-  exchange(P, 1, c.epoch);
+  exchange(P, 1, ep);
   // 3. copy the peers' reduced chunks out of my AG slots
   for (int j = 1; j < P.nranks; ++j) {
     const int src = peer_at(P, P.nranks - j);
-    copy_vec(V(c.recv) + src * cv, V(P.win[P.rank] + c.region + c.ag_off + c.slot * src), lo, chunk_hi(src, hi));
+    copy_vec(V(c.recv) + src * cv, V(P.win[P.rank] + rg + c.ag_off + c.slot * src), lo, chunk_hi(src, hi));
   }
+  end_seq(P, kCtlCollEpoch, kCtlCollDone, ep);
 }
 
 __global__ void __launch_bounds__(T) send_kernel(Peers P, const char* buf, size_t bytes, int dst, size_t off,
-                                                 uint32_t n) {
+                                                 size_t slot) {
+  const uint32_t n = begin_seq(P, kCtlSendSeq + dst);
   if (threadIdx.x == 0 && n > 2) wait_geq(P.flags[P.rank] + kFlagP2PConsumed + dst, n - 2, P);
   __syncthreads();
   const size_t nv = bytes / 16;
   size_t lo, hi;
   blk_range(nv, lo, hi);
-  char* w = P.win[dst] + off;
+  char* w = P.win[dst] + off + (n & 1) * slot;
   copy_vec(V(w), V(buf), lo, hi);
   copy_tail(w, buf, nv * 16, bytes);
   __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) sys_store(P.flags[dst] + kFlagP2PSeq + static_cast<size_t>(P.rank) * kMaxBlocks + blockIdx.x, n);
+  end_seq(P, kCtlSendSeq + dst, kCtlSendDone + dst, n);
 }
 
-__global__ void __launch_bounds__(T) recv_kernel(Peers P, char* buf, size_t bytes, int src, size_t off, uint32_t n,
-                                                 uint32_t target) {
+__global__ void __launch_bounds__(T) recv_kernel(Peers P, char* buf, size_t bytes, int src, size_t off, size_t slot) {
+  const uint32_t n = begin_seq(P, kCtlRecvSeq + src);
   if (threadIdx.x == 0) wait_geq(P.flags[P.rank] + kFlagP2PSeq + static_cast<size_t>(src) * kMaxBlocks + blockIdx.x, n, P);
   __syncthreads();
   const size_t nv = bytes / 16;
   size_t lo, hi;
   blk_range(nv, lo, hi);
-  const char* w = P.win[P.rank] + off;
+  const char* w = P.win[P.rank] + off + (n & 1) * slot;
   copy_vec(V(buf), V(w), lo, hi);
   copy_tail(buf, w, nv * 16, bytes);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t old = atomicAdd(P.flags[P.rank] + kFlagP2PCount + src, 1u);
-    if (old + 1 == target) sys_store(P.flags[src] + kFlagP2PConsumed + P.rank, n);
-  }
+  // the last block to finish tells the sender that message n was consumed
+  if (end_seq(P, kCtlRecvSeq + src, kCtlRecvDone + src, n)) sys_store(P.flags[src] + kFlagP2PConsumed + P.rank, n);
 }
 
 struct LocalArgs {
@@ -666,15 +709,15 @@ void launch_local_coll(LocalColl op, char* const* recv, const char* const* send,
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
-void launch_send(const Peers& p, const char* buf, size_t bytes, int dst, size_t off, uint32_t n, int blocks,
+void launch_send(const Peers& p, const char* buf, size_t bytes, int dst, size_t off, size_t slot, int blocks,
                  void* stream) {
-  send_kernel<<<blocks, T, 0, static_cast<hipStream_t>(stream)>>>(p, buf, bytes, dst, off, n);
+  send_kernel<<<blocks, T, 0, static_cast<hipStream_t>(stream)>>>(p, buf, bytes, dst, off, slot);
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
-void launch_recv(const Peers& p, char* buf, size_t bytes, int src, size_t off, uint32_t n, uint32_t target,
-                 int blocks, void* stream) {
-  recv_kernel<<<blocks, T, 0, static_cast<hipStream_t>(stream)>>>(p, buf, bytes, src, off, n, target);
+void launch_recv(const Peers& p, char* buf, size_t bytes, int src, size_t off, size_t slot, int blocks,
+                 void* stream) {
+  recv_kernel<<<blocks, T, 0, static_cast<hipStream_t>(stream)>>>(p, buf, bytes, src, off, slot);
   DLNB_HIP_CHECK(hipGetLastError());
 }
 

@@ -5,10 +5,12 @@
 // uncached device memory, publishes hipIpcMemHandles through the job's TCP
 // store and opens every peer's handles; the members must share one node
 // (xGMI). Each operation is cut into pieces that fit one parity region of
-// the windows and each piece is one kernel on the caller's stream, tagged
-// with a per-communicator epoch (identical on all members because every
-// member issues the same sequence of operations on a communicator - the
-// same rule RCCL has). Ops on one communicator must be stream-ordered.
+// the windows and each piece is one kernel on the caller's stream. The
+// kernel takes its epoch from a per-communicator counter in device memory
+// (identical on all members because every member issues the same sequence
+// of operations on a communicator - the same rule RCCL has), so the ops
+// capture into HIP graphs and replay with fresh epochs. Ops on one
+// communicator must be stream-ordered.
 //
 // Selection: --backend xgmi (GPU only). Several ranks may share one GPU
 // (-d 0,0): IPC works within a device, which is how the kernels are tested
@@ -147,9 +149,6 @@ class XgmiComm : public Communicator {
     const std::string done = key.str() + "opened";
     if (world.store().add(done, 1) == size_) world.store().set(done + "/go", "1");
     world.store().get(done + "/go");
-    sent_.assign(static_cast<size_t>(size_), 0);
-    recvd_.assign(static_cast<size_t>(size_), 0);
-    recv_blocks_.assign(static_cast<size_t>(size_), 0);
   }
 
   ~XgmiComm() override {
@@ -302,17 +301,15 @@ class XgmiComm : public Communicator {
     const size_t n = o.bytes == 0 ? 0 : std::min(p2p_slot_, o.bytes - off);
     const size_t p = static_cast<size_t>(o.peer);
     const int nb = xgmi::blocks_for(n, max_blocks_);
+    // source s's two slots (message parity) in the receiver's window
     if (o.is_send) {
-      const uint32_t seq = ++sent_[p];
-      const size_t woff = p2p_off_ + (static_cast<size_t>(rank_) * 2 + (seq & 1)) * p2p_slot_;
-      xgmi::launch_send(peers_, o.buf + off, n, o.peer, woff, seq, nb, hs(*o.s));
-      debug("send", seq, n, *o.s);
+      const size_t woff = p2p_off_ + static_cast<size_t>(rank_) * 2 * p2p_slot_;
+      xgmi::launch_send(peers_, o.buf + off, n, o.peer, woff, p2p_slot_, nb, hs(*o.s));
+      debug("send", n, *o.s);
     } else {
-      const uint32_t seq = ++recvd_[p];
-      recv_blocks_[p] += static_cast<uint32_t>(nb);
-      const size_t woff = p2p_off_ + (p * 2 + (seq & 1)) * p2p_slot_;
-      xgmi::launch_recv(peers_, o.buf + off, n, o.peer, woff, seq, recv_blocks_[p], nb, hs(*o.s));
-      debug("recv", seq, n, *o.s);
+      const size_t woff = p2p_off_ + p * 2 * p2p_slot_;
+      xgmi::launch_recv(peers_, o.buf + off, n, o.peer, woff, p2p_slot_, nb, hs(*o.s));
+      debug("recv", n, *o.s);
     }
   }
 
@@ -326,30 +323,31 @@ class XgmiComm : public Communicator {
     CollPiece c;
     std::memset(&c, 0, sizeof(c));
     c.dtype = t;
-    c.epoch = ++epoch_;
-    c.region = (epoch_ & 1) * region_;
+    c.region = region_;
     return c;
   }
   void launch(Op op, const CollPiece& c, Stream& s) {
     xgmi::launch_coll(op, peers_, c, xgmi::blocks_for(c.bytes, max_blocks_), hs(s));
-    debug("coll", c.epoch, c.bytes, s);
+    debug("coll", c.bytes, s);
   }
   // DLNB_XGMI_DEBUG=1: synchronise after every kernel and dump the flags.
-  void debug(const char* what, uint32_t tag, size_t bytes, Stream& s) {
+  void debug(const char* what, size_t bytes, Stream& s) {
     static const bool on = env_int("DLNB_XGMI_DEBUG", 0) != 0;
     if (!on) return;
     DLNB_HIP_CHECK(hipStreamSynchronize(hs(s)));
     std::vector<uint32_t> f(xgmi::kFlagWords);
     DLNB_HIP_CHECK(hipMemcpy(f.data(), flags_, f.size() * 4, hipMemcpyDeviceToHost));
-    std::fprintf(stderr, "[xgmi-debug] %s r%d %s tag=%u bytes=%zu err=%u coll0=[", name_.c_str(), rank_, what, tag,
-                 bytes, host_words_[16]);
+    std::fprintf(stderr, "[xgmi-debug] %s r%d %s epoch=%u bytes=%zu err=%u coll0=[", name_.c_str(), rank_, what,
+                 f[xgmi::kCtlCollEpoch], bytes, host_words_[16]);
     for (int r = 0; r < size_; ++r) std::fprintf(stderr, "%u ", f[xgmi::kFlagColl + r * xgmi::kMaxBlocks]);
     std::fprintf(stderr, "] seq0=[");
     for (int r = 0; r < size_; ++r) std::fprintf(stderr, "%u ", f[xgmi::kFlagP2PSeq + r * xgmi::kMaxBlocks]);
     std::fprintf(stderr, "] consumed=[");
     for (int r = 0; r < size_; ++r) std::fprintf(stderr, "%u ", f[xgmi::kFlagP2PConsumed + r]);
-    std::fprintf(stderr, "] count=[");
-    for (int r = 0; r < size_; ++r) std::fprintf(stderr, "%u ", f[xgmi::kFlagP2PCount + r]);
+    std::fprintf(stderr, "] sent=[");
+    for (int r = 0; r < size_; ++r) std::fprintf(stderr, "%u ", f[xgmi::kCtlSendSeq + r]);
+    std::fprintf(stderr, "] received=[");
+    for (int r = 0; r < size_; ++r) std::fprintf(stderr, "%u ", f[xgmi::kCtlRecvSeq + r]);
     std::fprintf(stderr, "]\n");
   }
 
@@ -361,8 +359,6 @@ class XgmiComm : public Communicator {
   uint32_t* host_words_ = nullptr;  // [0] abort, [16] error
   std::vector<void*> opened_;
   xgmi::Peers peers_;
-  uint32_t epoch_ = 0;
-  std::vector<uint32_t> sent_, recvd_, recv_blocks_;
   bool in_group_ = false;
   std::vector<P2POp> pending_;
 };

@@ -1,7 +1,7 @@
 // dlnb commtest: correctness and bandwidth of every collective of a backend.
 //
 //   dlnb commtest [--backend auto|rccl|xgmi|cpu] [-d 0,1,..] [--dtype bf16]
-//                 [--sizes 1,7,4096,...] [--bench] [--iters N] [--warmup N]
+//                 [--sizes 1,7,4096,...] [--bench] [--iters N] [--warmup N] [--graph]
 //
 // Check mode (default): every rank fills its buffers with exact small
 // integers v(rank, i), runs all-reduce (out-of-place and in-place),
@@ -10,6 +10,11 @@
 // (exact in every wire dtype at <= 8 ranks). Bench mode prints algbw/busbw
 // per collective and size (nccl-tests conventions, SURVEY.md §5 "Metrics"),
 // so RCCL and the xgmi kernels can be compared on one node.
+//
+// --graph (GPU): check mode captures every collective of a size plus the ring
+// send/recv into one HIP graph and replays it three times with new inputs
+// uploaded between replays (each replay must see fresh sequence numbers);
+// bench mode captures the timed loop of one op and replays it.
 //
 // Reference equivalent: none (DLNetBench relies on nccl-tests externally).
 #include <chrono>
@@ -129,6 +134,58 @@ struct Tester {
     if (failures != before) std::fprintf(stderr, "[commtest] rank %d: n=%zu FAILED\n", me, n);
   }
 
+  // One graph holding all collectives of size n and a ring send/recv,
+  // replayed `reps` times; inputs change between replays, outputs are
+  // compared after each.
+  void check_graph(Communicator& link, size_t n, int reps) {
+    const long long before = failures;
+    const size_t nb = std::max<size_t>(1, n * W * es);
+    Buffer ar_in = ctx.dev->alloc(nb), ar_out = ctx.dev->alloc(nb), ar_ip = ctx.dev->alloc(nb);
+    Buffer ag_out = ctx.dev->alloc(nb), blk_in = ctx.dev->alloc(nb), rs_out = ctx.dev->alloc(nb);
+    Buffer a2a_out = ctx.dev->alloc(nb), p_in = ctx.dev->alloc(nb), p_out = ctx.dev->alloc(nb);
+    const int next = (me + 1) % W, prev = (me + W - 1) % W;
+    auto g = ctx.dev->capture(s, {}, [&] {
+      comm.all_reduce(ar_in.data(), ar_out.data(), n, t, s);
+      comm.all_reduce(ar_ip.data(), ar_ip.data(), n, t, s);
+      comm.all_gather(ar_in.data(), ag_out.data(), n, t, s);
+      comm.reduce_scatter(blk_in.data(), rs_out.data(), n, t, s);
+      comm.all_to_all(blk_in.data(), a2a_out.data(), n, t, s);
+      if (W > 1) {
+        link.group_start();
+        link.send(p_in.data(), n, t, next, s);
+        link.recv(p_out.data(), n, t, prev, s);
+        link.group_end();
+      }
+    });
+    for (int rep = 0; rep < reps; ++rep) {
+      // rank r's inputs at replay rep: v(r, rep + i)
+      const size_t o = static_cast<size_t>(rep);
+      upload(ar_in, pattern(me, o, n));
+      upload(ar_ip, pattern(me, o, n));
+      upload(blk_in, pattern(me, o, n * W));
+      upload(p_in, pattern(me, o, n));
+      g->launch(s);
+      auto got = download(ar_out, n * es);
+      for (size_t i = 0; i < n; ++i) expect("graph all_reduce", n, got, i, sum_over_ranks(o + i));
+      got = download(ar_ip, n * es);
+      for (size_t i = 0; i < n; ++i) expect("graph all_reduce(in-place)", n, got, i, sum_over_ranks(o + i));
+      got = download(ag_out, n * W * es);
+      for (int r = 0; r < W; ++r)
+        for (size_t i = 0; i < n; ++i) expect("graph all_gather", n, got, r * n + i, val(r, o + i, t));
+      got = download(rs_out, n * es);
+      for (size_t i = 0; i < n; ++i) expect("graph reduce_scatter", n, got, i, sum_over_ranks(o + me * n + i));
+      got = download(a2a_out, n * W * es);
+      for (int p = 0; p < W; ++p)
+        for (size_t i = 0; i < n; ++i) expect("graph all_to_all", n, got, p * n + i, val(p, o + me * n + i, t));
+      if (W > 1) {
+        got = download(p_out, n * es);
+        for (size_t i = 0; i < n; ++i) expect("graph send/recv", n, got, i, val(prev, o + i, t));
+      }
+    }
+    s.synchronize();
+    if (failures != before) std::fprintf(stderr, "[commtest] rank %d: graph n=%zu FAILED\n", me, n);
+  }
+
   void check_p2p(Communicator& link, size_t n) {
     if (W < 2) return;
     Buffer a = ctx.dev->alloc(std::max<size_t>(1, n * es)), b = ctx.dev->alloc(std::max<size_t>(1, n * es));
@@ -149,7 +206,7 @@ struct Tester {
 
 int commtest_main(int argc, char** argv) {
   std::string backend = "auto", devices, dtype = "bf16", sizes_s, json_path;
-  bool bench = false;
+  bool bench = false, graph = false;
   int iters = 20, warmup = 5, ranks = 2;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -162,6 +219,7 @@ int commtest_main(int argc, char** argv) {
     else if (a == "--dtype") dtype = val("--dtype");
     else if (a == "--sizes") sizes_s = val("--sizes");
     else if (a == "--bench") bench = true;
+    else if (a == "--graph") graph = true;
     else if (a == "--iters") iters = std::stoi(val("--iters"));
     else if (a == "--warmup") warmup = std::stoi(val("--warmup"));
     else if (a == "--ranks") ranks = std::stoi(val("--ranks"));
@@ -169,8 +227,9 @@ int commtest_main(int argc, char** argv) {
     else if (a == "-h" || a == "--help") {
       std::cout << "Usage: dlnb commtest [--backend auto|rccl|xgmi|cpu|loopback|loopback-cpu] [--ranks N] [-d 0,1,..]\n"
                    "                     [--dtype bf16|fp16|fp32|fp8_e4m3|fp8_e5m2]\n"
-                   "                     [--sizes n1,n2,..] [--bench] [--iters N] [--warmup N]\n"
-                   "  sizes are elements per rank; check mode verifies every collective exactly\n";
+                   "                     [--sizes n1,n2,..] [--bench] [--iters N] [--warmup N] [--graph]\n"
+                   "  sizes are elements per rank; check mode verifies every collective exactly\n"
+                   "  --graph: capture the operations into a HIP graph and replay it (rccl, xgmi)\n";
       return 0;
     } else DLNB_THROW("unknown option " << a);
   }
@@ -178,7 +237,7 @@ int commtest_main(int argc, char** argv) {
   Context ctx;
   ctx.boot = std::move(boot);
   const std::string be = select_backend(ctx, backend, devices);
-  (void)be;
+  DLNB_REQUIRE(!graph || be == "rccl" || be == "xgmi", "commtest --graph needs --backend rccl or xgmi");
   const DType t = parse_dtype(dtype);
   const int W = ctx.world(), me = ctx.rank();
   std::vector<size_t> sizes;
@@ -205,6 +264,10 @@ int commtest_main(int argc, char** argv) {
     for (size_t n : sizes) {
       const double t0 = now();
       if (verbose) std::fprintf(stderr, "[commtest] rank %d: collectives n=%zu\n", me, n);
+      if (graph) {
+        T.check_graph(*link, n, 3);
+        continue;
+      }
       T.check(n);
       const double t1 = now();
       if (verbose) std::fprintf(stderr, "[commtest] rank %d: send/recv n=%zu (collectives took %.3f s)\n", me, n, t1 - t0);
@@ -224,6 +287,7 @@ int commtest_main(int argc, char** argv) {
       Json j = Json::object();
       j["commtest"] = "check";
       j["backend"] = comm->backend_name();
+      j["graph"] = graph;
       j["world_size"] = W;
       j["dtype"] = dtype_name(t);
       Json sz = Json::array();
@@ -255,11 +319,19 @@ int commtest_main(int argc, char** argv) {
             default: comm->all_to_all(a.data(), b.data(), n, t, *stream); break;
           }
         };
+        std::unique_ptr<GraphExec> g;
+        if (graph)
+          g = ctx.dev->capture(*stream, {}, [&] {
+            for (int it = 0; it < iters; ++it) op();
+          });
         for (int w = 0; w < warmup; ++w) op();
         stream->synchronize();
         ctx.hg().barrier();
         const double t0 = now();
-        for (int it = 0; it < iters; ++it) op();
+        if (g)
+          g->launch(*stream);
+        else
+          for (int it = 0; it < iters; ++it) op();
         stream->synchronize();
         const double dt = ctx.hg().allreduce_max(now() - t0) / iters;
         // algorithm bytes per rank (nccl-tests): AR/RS/A2A n*W... AG output
@@ -269,6 +341,7 @@ int commtest_main(int argc, char** argv) {
           Json j = Json::object();
           j["commtest"] = "bench";
           j["backend"] = comm->backend_name();
+          j["graph"] = graph;
           j["op"] = k.name;
           j["world_size"] = W;
           j["dtype"] = dtype_name(t);

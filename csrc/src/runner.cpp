@@ -387,8 +387,9 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   std::unique_ptr<GraphExec> graph;
   if (opt.graph) {
     DLNB_REQUIRE(ctx.dev->kind() == DeviceKind::GPU, "--graph needs a GPU");
-    DLNB_REQUIRE(backend == "rccl", "--graph needs --backend rccl (the xgmi kernels tag every piece with a fresh "
-                                    "epoch, which a replayed graph would repeat)");
+    // xgmi kernels take their epochs from device-side counters, so a replayed
+    // graph issues fresh ones; the loopback backends synchronise on the host.
+    DLNB_REQUIRE(backend == "rccl" || backend == "xgmi", "--graph needs --backend rccl or xgmi");
     DLNB_REQUIRE(strat->capturable(), "--graph cannot capture --schedule reference (it blocks the host)");
     std::vector<Stream*> ss = strat->streams();
     std::vector<Stream*> others(ss.begin() + 1, ss.end());

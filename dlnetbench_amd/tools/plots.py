@@ -10,13 +10,22 @@ colour/marker maps, zoom insets, :15-209). Inputs here are sweep JSONL files
     python -m dlnetbench_amd.tools.plots scaling results.jsonl -o scaling.png
     python -m dlnetbench_amd.tools.plots barrier results.jsonl -o barrier.png
     python -m dlnetbench_amd.tools.plots pareto results.jsonl -o pareto.png
+    python -m dlnetbench_amd.tools.plots knobs results.jsonl -o knobs.png [--metric barrier]
+    python -m dlnetbench_amd.tools.plots knobs-pareto results.jsonl -o knobs_pareto.png
+
+Collective-library knobs (the reference's PROTOCOL x ALGO and THREADS x
+CHANNELS axes, plot_dp.py:23-26) are read from each sweep point's
+environment: NCCL_PROTO, NCCL_ALGO, NCCL_NTHREADS and NCCL_MIN_NCHANNELS /
+NCCL_MAX_NCHANNELS for RCCL, DLNB_XGMI_BLOCKS for the xgmi kernels (their
+"channels"); a knob a point does not set shows as "default".
 """
 from __future__ import annotations
 
 import argparse
+import itertools
 import json
 import re
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 _UNITS = ["B", "KiB", "MiB", "GiB", "TiB"]
 
@@ -51,6 +60,195 @@ def pareto_front(points: Sequence[Tuple[float, float]]) -> List[int]:
             front.append(i)
             best_y = points[i][1]
     return front
+
+
+# ---------------------------------------------------------------- style maps
+# (py_utils.py:8-13, :123-132)
+
+MARKERS = ["o", "s", "^", "d", "v", "P", "*", "X", ">", "<", "h", "p"]
+LINESTYLES = ["-", ":", "-.", "--"]
+COLORS = ["#1f77b4", "#ff7f0e", "#2ca02c", "#d62728", "#9467bd", "#8c564b", "#e377c2", "#7f7f7f", "#bcbd22",
+          "#17becf"]
+
+
+def create_color_map(values: Sequence) -> Dict:
+    """One colour per value, cycling through a 10-colour palette."""
+    return {v: c for v, c in zip(values, itertools.cycle(COLORS))}
+
+
+def create_marker_map(values: Sequence) -> Dict:
+    return {v: m for v, m in zip(values, itertools.cycle(MARKERS))}
+
+
+def create_linestyle_map(values: Sequence) -> Dict:
+    return {v: ls for v, ls in zip(values, itertools.cycle(LINESTYLES))}
+
+
+def add_zoom_inset(ax, zoom_region: Tuple[float, float, float, float],
+                   inset_position: Tuple[float, float, float, float] = (0.6, 0.6, 0.35, 0.35),
+                   draw_rect: bool = True):
+    """Magnified copy of the lines and scatter points of `ax` inside zoom_region
+    = (x1, x2, y1, y2), drawn at inset_position (axes fractions x0, y0, w, h),
+    with a dashed rectangle marking the region on the main axes
+    (py_utils.add_zoom_inset). Returns the inset axes."""
+    from matplotlib.patches import Rectangle
+    x1, x2, y1, y2 = zoom_region
+    axins = ax.inset_axes(list(inset_position))
+    for line in ax.get_lines():
+        axins.plot(line.get_xdata(), line.get_ydata(), color=line.get_color(), linestyle=line.get_linestyle(),
+                   linewidth=line.get_linewidth(), marker=line.get_marker(), markersize=line.get_markersize(),
+                   alpha=line.get_alpha())
+    for coll in ax.collections:
+        offs = coll.get_offsets()
+        if len(offs):
+            axins.scatter(offs[:, 0], offs[:, 1], c=coll.get_facecolors(), s=coll.get_sizes(),
+                          marker=(coll.get_paths()[0] if coll.get_paths() else "o"))
+    axins.set_xlim(x1, x2)
+    axins.set_ylim(y1, y2)
+    axins.tick_params(labelsize=6)
+    axins.grid(alpha=0.3)
+    if draw_rect:
+        ax.add_patch(Rectangle((x1, y1), x2 - x1, y2 - y1, fill=False, edgecolor="black", linestyle="dashed",
+                               linewidth=1))
+    return axins
+
+
+# ---------------------------------------------------------------- knobs
+
+def knobs(rec: dict) -> Dict[str, str]:
+    """Collective-library knobs of one sweep record (see the module doc)."""
+    env = {k: str(v) for k, v in rec.get("point", {}).get("env", {}).items()}
+    ch = env.get("NCCL_MAX_NCHANNELS") or env.get("NCCL_MIN_NCHANNELS") or env.get("DLNB_XGMI_BLOCKS")
+    return {"protocol": env.get("NCCL_PROTO", "default"), "algorithm": env.get("NCCL_ALGO", "default"),
+            "threads": env.get("NCCL_NTHREADS", "default"), "channels": ch or "default"}
+
+
+def _knob_sort_key(v: str):
+    return (0, float(v), "") if re.fullmatch(r"[0-9.]+", v) else (1, 0.0, v)
+
+
+def knob_table(recs: List[dict], metric: str = "runtime") -> List[dict]:
+    """One row per record: model, world size, knobs, and the metric in ms
+    (runtime = median iteration; barrier = mean exposed all-reduce wait)."""
+    rows = []
+    for r in recs:
+        rep = r["report"]
+        g = rep["global"]
+        if metric == "barrier":
+            vals = [b * 1e3 for rk in rep["ranks"] for b in rk.get("barrier_time", [])]
+            if not vals:
+                continue
+            y = sum(vals) / len(vals)
+        else:
+            y = g["dlnb"]["iteration"]["median_ms"]
+        e = [x for rk in rep["ranks"] for x in rk.get("energy_consumed", [])]
+        runs = max(1, len(rep["ranks"][0].get("energy_consumed", []))) if e else 1
+        rows.append(dict(knobs(r), model=g.get("model_name"), world=g.get("world_size"), value_ms=y,
+                         energy_J=(sum(e) / runs) if e else None,
+                         msg_bytes=g.get("msg_size_avg_bytes") or g.get("allgather_msg_size_bytes")))
+    return rows
+
+
+def plot_knobs(recs: List[dict], out: str, metric: str = "runtime") -> Dict[Tuple[str, str], int]:
+    """Protocol x algorithm facets (rows x columns); inside each facet the
+    metric against world size, one line per threads x channels combination
+    (plot_dp.py:23-26 knob grid). Returns {(protocol, algorithm): points}."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    rows = knob_table(recs, metric)
+    protos = sorted({r["protocol"] for r in rows}, key=_knob_sort_key) or ["default"]
+    algos = sorted({r["algorithm"] for r in rows}, key=_knob_sort_key) or ["default"]
+    tcs = sorted({(r["threads"], r["channels"]) for r in rows},
+                 key=lambda t: (_knob_sort_key(t[0]), _knob_sort_key(t[1])))
+    colors, marks = create_color_map(tcs), create_marker_map(tcs)
+    fig, axes = plt.subplots(len(protos), len(algos), figsize=(4.2 * len(algos), 3.4 * len(protos)), squeeze=False,
+                             sharex=True, sharey=True)
+    counts: Dict[Tuple[str, str], int] = {}
+    for i, pr in enumerate(protos):
+        for j, al in enumerate(algos):
+            ax = axes[i][j]
+            sub = [r for r in rows if r["protocol"] == pr and r["algorithm"] == al]
+            counts[(pr, al)] = len(sub)
+            for tc in tcs:
+                pts = sorted((r["world"], r["value_ms"]) for r in sub if (r["threads"], r["channels"]) == tc)
+                if pts:
+                    ax.plot([p[0] for p in pts], [p[1] for p in pts], marker=marks[tc], color=colors[tc],
+                            label=f"T{tc[0]} x C{tc[1]}")
+            ax.set_title(f"{pr} x {al}", fontsize=9)
+            ax.set_xscale("log", base=2)
+            ax.grid(alpha=0.3)
+            if i == len(protos) - 1:
+                ax.set_xlabel("GPUs")
+            if j == 0:
+                ax.set_ylabel("barrier time (ms)" if metric == "barrier" else "iteration (ms)")
+    handles, labels = axes[0][0].get_legend_handles_labels()
+    for ax in axes.flat:
+        h, l = ax.get_legend_handles_labels()
+        for hh, ll in zip(h, l):
+            if ll not in labels:
+                handles.append(hh)
+                labels.append(ll)
+    if handles:
+        fig.legend(handles, labels, loc="center right", fontsize=7, title="threads x channels")
+    fig.tight_layout(rect=(0, 0, 0.85, 1))
+    fig.savefig(out, dpi=150)
+    plt.close(fig)
+    return counts
+
+
+def pareto_staircase(points: Sequence[Tuple[float, float]]) -> List[Tuple[float, float]]:
+    """Vertices of the staircase through the Pareto front (minimise both),
+    sorted by x (plots_pareto_energy.py draw_pareto_frontier)."""
+    fr = sorted(points[i] for i in pareto_front(points))
+    out: List[Tuple[float, float]] = []
+    for k, (x, y) in enumerate(fr):
+        if k:
+            out.append((x, fr[k - 1][1]))
+        out.append((x, y))
+    return out
+
+
+def plot_knobs_pareto(recs: List[dict], out: str) -> Dict[str, int]:
+    """Energy vs runtime per model (one subplot each): colour = protocol x
+    algorithm, marker = threads x channels, staircase Pareto frontier
+    (plots_pareto_energy.py:107-234). Returns {model: points}."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    from matplotlib.lines import Line2D
+    rows = [r for r in knob_table(recs) if r["energy_J"] is not None]
+    models = sorted({r["model"] for r in rows}) or ["(no energy data)"]
+    pa = sorted({f"{r['protocol']} x {r['algorithm']}" for r in rows})
+    tc = sorted({f"T{r['threads']} x C{r['channels']}" for r in rows})
+    colors, marks = create_color_map(pa), create_marker_map(tc)
+    fig, axes = plt.subplots(1, len(models), figsize=(6.5 * len(models), 5), squeeze=False)
+    counts: Dict[str, int] = {}
+    for ax, m in zip(axes[0], models):
+        sub = [r for r in rows if r["model"] == m]
+        counts[m] = len(sub)
+        for r in sub:
+            ax.scatter(r["energy_J"], r["value_ms"], color=colors[f"{r['protocol']} x {r['algorithm']}"],
+                       marker=marks[f"T{r['threads']} x C{r['channels']}"], s=70, edgecolor="black", linewidth=0.6,
+                       alpha=0.8, zorder=5)
+        stair = pareto_staircase([(r["energy_J"], r["value_ms"]) for r in sub])
+        if len(stair) > 1:
+            ax.plot([p[0] for p in stair], [p[1] for p in stair], color="red", lw=2, zorder=10)
+        msg = sub[0]["msg_bytes"] if sub else None
+        ax.set_title(f"{m}" + (f" (message {format_bytes(msg)})" if msg else ""), fontsize=10)
+        ax.set_xlabel("energy per iteration, all ranks (J)")
+        ax.set_ylabel("iteration time (ms)")
+        ax.grid(alpha=0.3)
+    items = [Line2D([0], [0], color="red", lw=2, label="Pareto frontier")]
+    items += [Line2D([0], [0], marker="o", color="w", markerfacecolor=colors[p], markeredgecolor="black",
+                     label=p) for p in pa]
+    items += [Line2D([0], [0], marker=marks[t], color="w", markerfacecolor="gray", markeredgecolor="black",
+                     label=t) for t in tc]
+    fig.legend(handles=items, loc="center right", fontsize=7)
+    fig.tight_layout(rect=(0, 0, 0.82, 1))
+    fig.savefig(out, dpi=150)
+    plt.close(fig)
+    return counts
 
 
 def load_records(path: str) -> List[dict]:
@@ -148,12 +346,17 @@ def plot_pareto(recs: List[dict], out: str) -> None:
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("kind", choices=["scaling", "barrier", "pareto"])
+    ap.add_argument("kind", choices=["scaling", "barrier", "pareto", "knobs", "knobs-pareto"])
     ap.add_argument("inputs", nargs="+")
     ap.add_argument("-o", "--out", default="plot.png")
+    ap.add_argument("--metric", choices=["runtime", "barrier"], default="runtime", help="knobs: y axis")
     a = ap.parse_args(argv)
     recs = [r for p in a.inputs for r in load_records(p)]
-    {"scaling": plot_scaling, "barrier": plot_barrier, "pareto": plot_pareto}[a.kind](recs, a.out)
+    if a.kind == "knobs":
+        plot_knobs(recs, a.out, a.metric)
+    else:
+        {"scaling": plot_scaling, "barrier": plot_barrier, "pareto": plot_pareto,
+         "knobs-pareto": plot_knobs_pareto}[a.kind](recs, a.out)
     print(a.out)
     return 0
 

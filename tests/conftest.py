@@ -29,8 +29,23 @@ def pytest_sessionstart(session):
     if not all(os.path.exists(p) for p in need) and not os.environ.get("PYTEST_XDIST_WORKER"):
         subprocess.run(["make", "-C", ROOT, f"-j{min(16, os.cpu_count() or 4)}"], check=True,
                        stdout=subprocess.DEVNULL)
-    # An existing host-ASan build is brought up to date (incremental) so its
-    # tests never run stale binaries.
-    if os.path.isdir(os.path.join(ROOT, "build-asan", "bin")) and not os.environ.get("PYTEST_XDIST_WORKER"):
-        subprocess.run(["make", "-C", ROOT, f"-j{min(16, os.cpu_count() or 4)}", "asan"], check=False,
-                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+
+
+def _sanitizer_build(kind: str) -> str:
+    """`make asan` / `make tsan` into build-<kind>/ (incremental: the first
+    session compiles the tree once, later ones only what changed) and return
+    its bin directory. A failing build fails the tests that need it."""
+    import subprocess
+    p = subprocess.run(["make", "-C", ROOT, f"-j{min(16, os.cpu_count() or 4)}", kind], capture_output=True, text=True)
+    assert p.returncode == 0, f"make {kind} failed:\n" + p.stdout[-2000:] + p.stderr[-3000:]
+    return os.path.join(ROOT, f"build-{kind}", "bin")
+
+
+@pytest.fixture(scope="session")
+def asan_bindir():
+    return _sanitizer_build("asan")
+
+
+@pytest.fixture(scope="session")
+def tsan_bindir():
+    return _sanitizer_build("tsan")

@@ -85,6 +85,26 @@ def test_xgmi_kernels_exact(w, dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("w,dtype", [(2, "bf16"), (4, "bf16"), (3, "fp32")])
+def test_xgmi_graph_replay_exact(w, dtype):
+    """The collectives and a ring send/recv captured into one HIP graph and replayed 3 times with new
+    inputs: the kernels take their epochs / message numbers from device counters, so every replay must
+    synchronise afresh (a repeated epoch would let a rank read a peer's previous data)."""
+    _need_gpu()
+    devs = ",".join(["0"] * w)
+    out = commtest(w, "--backend", "xgmi", "-d", devs, "--dtype", dtype, "--graph", "--sizes", "1,100,4097,300007",
+                   env_extra=SMALL_WINDOWS)
+    assert out[0]["ok"] and out[0]["graph"] is True, out
+
+
+@pytest.mark.gpu
+def test_rccl_graph_replay_exact():
+    _need_gpu()
+    out = commtest(1, "--backend", "rccl", "--graph", "--sizes", "1,4097")
+    assert out[0]["ok"] and out[0]["graph"] is True
+
+
+@pytest.mark.gpu
 def test_xgmi_default_windows_large_message():
     _need_gpu()
     out = commtest(2, "--backend", "xgmi", "-d", "0,0", "--sizes", "33554441", env_extra={"DLNB_XGMI_TIMEOUT_S": "60"})
@@ -135,6 +155,32 @@ def test_strategies_on_xgmi(strategy, model, params, extra, w, tmp_path):
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
     d = json.loads(out.read_text())
     assert d["global"]["backend"] == "XGMI" and len(d["ranks"]) == w
+
+
+XGMI_GRAPH_STRATS = [
+    ("dp", "tiny_dense_8_bfloat16", ["4"], [], 2),
+    ("fsdp", "tiny_dense_8_bfloat16", ["4", "4"], [], 4),
+    ("hybrid_2d", "tiny_dense_8_bfloat16", ["2", "4"], ["--pp-schedule", "1f1b"], 2),
+    ("hybrid_3d_moe", "tiny_moe_8_bfloat16", ["2", "2", "2"], [], 4),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy,model,params,extra,w", XGMI_GRAPH_STRATS)
+def test_strategies_on_xgmi_graph(strategy, model, params, extra, w, tmp_path):
+    """One captured iteration replayed (--graph) over the xgmi kernels, ranks sharing one MI355X."""
+    _need_gpu()
+    out = tmp_path / "r.json"
+    data = os.path.join(ROOT, "tests", "data")
+    args = [os.path.join(ROOT, "build", "bin", strategy), model, *params, data, *extra, "-w", "1", "-r", "3",
+            "--backend", "xgmi", "-d", ",".join(["0"] * w), "--compute", "spin", "--graph", "--quiet",
+            "--json", str(out)]
+    p = launch(w, args, {"DLNB_XGMI_TIMEOUT_S": "60"})
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    d = json.loads(out.read_text())
+    assert d["global"]["backend"] == "XGMI" and d["global"]["dlnb"]["graph"] > 0
+    for r in d["ranks"]:
+        assert not r.get("async_error"), r
 
 
 @pytest.mark.gpu

@@ -15,18 +15,28 @@ def need_gpu():
 from dlnetbench_amd.ops import gemm  # noqa: E402
 
 
+def assert_close_bf16_out(c, ref):
+    """fp32-accumulated GEMM with a bf16 output: every element within one bf16
+    rounding of the fp32 reference (2^-8 relative) plus 1e-3 of the RMS of the
+    reference for accumulation-order differences. A dropped or doubled K tile
+    moves elements by O(rms) and fails this."""
+    err = (c.float() - ref).abs()
+    bound = ref.abs() * 2.0 ** -8 + 1e-3 * ref.pow(2).mean().sqrt().item()
+    worst = (err - bound).max().item()
+    assert worst <= 0, f"max excess {worst}, max err {err.max().item()}, rms {ref.pow(2).mean().sqrt().item()}"
+
+
 @pytest.mark.parametrize("waves", [0, 1, 2, 3, 6, 8, 4])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 512, 128), (512, 256, 1024), (768, 1280, 640),
-                                   (2048, 1024, 4096), (256, 256, 192), (512, 768, 320)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 512, 128), (512, 512, 64), (768, 256, 128),
+                                   (512, 256, 1024), (768, 1280, 640), (2048, 1024, 4096), (256, 256, 192),
+                                   (512, 768, 320)])
 def test_gemm_bf16_matches_torch(M, N, K, waves):
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
     b = torch.randn(N, K, device="cuda", generator=g).to(torch.bfloat16)
     c = gemm.gemm_tn(a, b, waves=waves)
     torch.cuda.synchronize()
-    ref = a.float() @ b.float().t()
-    tol = 2e-2 * ref.abs().max().item() + 1e-2
-    assert (c.float() - ref).abs().max().item() < tol
+    assert_close_bf16_out(c, a.float() @ b.float().t())
 
 
 @pytest.mark.parametrize("waves", [0, 3, 6])
@@ -43,16 +53,15 @@ def test_gemm_bf16_identity_asymmetric(waves):
 
 @pytest.mark.skipif(not hasattr(torch, "float8_e4m3fn"), reason="torch without float8")
 @pytest.mark.parametrize("waves", [0, 1, 2, 3, 6, 8, 4])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 768, 512), (1024, 512, 2048)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 256, 128), (256, 512, 256), (512, 768, 512),
+                                   (1024, 512, 2048)])
 def test_gemm_fp8_matches_torch(M, N, K, waves):
     g = torch.Generator(device="cuda").manual_seed(7 + M)
     a = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(torch.float8_e4m3fn)
     b = (torch.randn(N, K, device="cuda", generator=g) * 0.5).to(torch.float8_e4m3fn)
     c = gemm.gemm_tn(a, b, waves=waves)
     torch.cuda.synchronize()
-    ref = a.float() @ b.float().t()
-    tol = 2e-2 * ref.abs().max().item() + 1e-2
-    assert (c.float() - ref).abs().max().item() < tol
+    assert_close_bf16_out(c, a.float() @ b.float().t())
 
 
 def test_fill_random_uniform():

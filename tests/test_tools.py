@@ -90,6 +90,66 @@ def test_plots(tmp_path, bindir):
         assert png.exists() and png.stat().st_size > 1000
 
 
+def test_knob_plots(tmp_path, bindir, data_dir):
+    """Protocol x algorithm facets with threads x channels series, and the per-model energy Pareto
+    (plot_dp.py:23-26, plots_pareto_energy.py:107-234): a real 2-point knob sweep on the CPU backend,
+    then synthetic copies filling a 2 x 2 x 2 knob grid with known values."""
+    import copy
+    spec = {"base_path": data_dir, "points": [
+        {"strategy": "dp", "model": "tiny_dense_8_bfloat16", "params": [2], "world": [2],
+         "opts": {"warmup": 0, "runs": 2, "backend": "cpu"},
+         "env": {"NCCL_PROTO": ["Simple", "LL128"], "NCCL_ALGO": "Ring"}}]}
+    sf = tmp_path / "spec.json"
+    sf.write_text(json.dumps(spec))
+    out = tmp_path / "r.jsonl"
+    assert sweep.main([str(sf), "--out", str(out), "--bin", bindir]) == 0
+    recs = plots.load_records(str(out))
+    assert [plots.knobs(r)["protocol"] for r in recs] == ["Simple", "LL128"]
+    assert plots.knobs(recs[0]) == {"protocol": "Simple", "algorithm": "Ring", "threads": "default",
+                                    "channels": "default"}
+    grid = []
+    for proto in ("Simple", "LL128"):
+        for algo in ("Ring", "Tree"):
+            for nt in ("256", "512"):
+                for w in (2, 4):
+                    r = copy.deepcopy(recs[0])
+                    r["point"]["env"] = {"NCCL_PROTO": proto, "NCCL_ALGO": algo, "NCCL_NTHREADS": nt,
+                                         "NCCL_MAX_NCHANNELS": "8"}
+                    r["report"]["global"]["world_size"] = w
+                    r["report"]["global"]["dlnb"]["iteration"]["median_ms"] = 10.0 + w + (nt == "512")
+                    for rk in r["report"]["ranks"]:
+                        rk["energy_consumed"] = [5.0 + (algo == "Tree")] * 2
+                    grid.append(r)
+    gf = tmp_path / "grid.jsonl"
+    gf.write_text("\n".join(json.dumps(r) for r in grid) + "\n")
+    counts = plots.plot_knobs(grid, str(tmp_path / "k.png"))
+    assert counts == {(p, a): 4 for p in ("LL128", "Simple") for a in ("Ring", "Tree")}
+    assert plots.plot_knobs(grid, str(tmp_path / "kb.png"), metric="barrier")[("Simple", "Ring")] == 4
+    assert plots.plot_knobs_pareto(grid, str(tmp_path / "p.png")) == {"tiny_dense_8_bfloat16": 16}
+    for kind, extra in (("knobs", []), ("knobs", ["--metric", "barrier"]), ("knobs-pareto", [])):
+        png = tmp_path / f"cli_{kind}.png"
+        assert plots.main([kind, str(gf), "-o", str(png), *extra]) == 0 and png.stat().st_size > 1000
+
+
+def test_zoom_inset_and_style_maps(tmp_path):
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    fig, ax = plt.subplots()
+    ax.plot([1, 2, 3, 4], [10, 1, 1.1, 1.2], marker="o")
+    ax.scatter([2.5], [1.05])
+    ins = plots.add_zoom_inset(ax, (1.8, 4.2, 0.9, 1.3))
+    assert ins.get_xlim() == (1.8, 4.2) and ins.get_ylim() == (0.9, 1.3)
+    assert len(ins.get_lines()) == 1 and len(ins.collections) == 1
+    assert len(ax.patches) == 1  # the dashed zoom rectangle
+    fig.savefig(tmp_path / "z.png")
+    cm = plots.create_color_map(range(12))
+    assert cm[0] == cm[10] != cm[1]
+    assert plots.create_marker_map(["a", "b"]) == {"a": "o", "b": "s"}
+    assert plots.create_linestyle_map(range(5))[4] == "-"
+    assert plots.pareto_staircase([(1, 5), (2, 3), (4, 1), (3, 4)]) == [(1, 5), (2, 5), (2, 3), (4, 3), (4, 1)]
+
+
 def test_plot_utils():
     assert plots.format_bytes(1536) == "1.5 KiB"
     assert plots.format_bytes(512) == "512 B"
@@ -146,11 +206,9 @@ def test_plan_cli(capsys, root):
 @pytest.mark.parametrize("prog,args", [("fsdp", ["tiny_dense_8_bfloat16", "4", "2"]),
                                        ("hybrid_3d_moe", ["tiny_moe_8_bfloat16", "2", "2", "1"]),
                                        ("hybrid_3d", ["tiny_dense_8_bfloat16", "2", "2", "1"])])
-def test_asan_build_is_clean(prog, args, root, data_dir):
-    """Host AddressSanitizer build (make asan): no memory errors in the runtime."""
-    b = os.path.join(root, "build-asan", "bin", prog)
-    if not os.path.exists(b):
-        pytest.skip("make asan not built")
+def test_asan_build_is_clean(prog, args, asan_bindir, data_dir):
+    """Host AddressSanitizer build (make asan, built on demand): no memory errors in the runtime."""
+    b = os.path.join(asan_bindir, prog)
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1")
     code, outs = launch.launch(2, [b, *args, data_dir, "--quiet", "-w", "1", "-r", "2"], timeout=120,
                                capture=True, env=env)
@@ -162,11 +220,10 @@ def test_asan_build_is_clean(prog, args, root, data_dir):
                                              ("hybrid_2d", ["tiny_deep_8_bfloat16", "4", "8"],
                                               ["--pp-schedule", "interleaved"]),
                                              ("hybrid_3d_moe", ["tiny_moe_8_bfloat16", "2", "4", "2"], ["--ep-overlap"])])
-def test_tsan_loopback_threads_race_free(prog, args, extra, root, data_dir):
-    """Host ThreadSanitizer build (make tsan): 8 loopback rank threads on the CPU device, no data races."""
-    b = os.path.join(root, "build-tsan", "bin", prog)
-    if not os.path.exists(b):
-        pytest.skip("make tsan not built")
+def test_tsan_loopback_threads_race_free(prog, args, extra, tsan_bindir, data_dir):
+    """Host ThreadSanitizer build (make tsan, built on demand): 8 loopback rank threads on the CPU device,
+    no data races."""
+    b = os.path.join(tsan_bindir, prog)
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "DLNB_RANK", "DLNB_WORLD_SIZE")}
     env["TSAN_OPTIONS"] = "halt_on_error=1"
     p = subprocess.run([b, *args, data_dir, *extra, "--backend", "loopback-cpu", "--ranks", "8", "--quiet",
