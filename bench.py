@@ -24,6 +24,11 @@ ride along as extra keys of the same JSON line:
 * ``compute_stretch``: the headline FSDP configuration with fixed-work
   compute for a few iterations (task time under the concurrent
   all-gathers / reduce-scatters over the uncontended time).
+* ``comm_bound_xgmi`` (N > 1): the comm-bound ViT-H DP run again over our
+  own xGMI collective kernels (``--backend xgmi``, HIP graph) instead of
+  RCCL, with the RCCL/xgmi time ratio. It runs last, in a child process per
+  rank with a short device-wait timeout, so a failure there can only cost
+  this block, never the headline.
 
 At N = 1 a "collective" is a local device copy: bus bandwidth is reported
 as null (nccl-tests convention: nothing crosses a link).
@@ -37,6 +42,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 from typing import Any, Dict, Optional
 
@@ -97,6 +103,42 @@ def _mean_of(doc: dict, key: str) -> Optional[float]:
     return round(sum(vals) / len(vals) * 1e3, 4) if vals else None
 
 
+def _xgmi_ab(a: argparse.Namespace, world: int, rank: int, c5: dict) -> Dict[str, Any]:
+    """The comm-bound DP secondary over the xgmi backend (HIP graph), run by
+    the native binary as a child of every rank."""
+    from dlnetbench_amd import engine
+    _store_env(world, rank, ".xgmi")
+    out = f"/tmp/dlnb_bench_xgmi_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}.json"
+    args = engine.build_args("dp", a.c5_model, a.c5_buckets, base_path=a.base_path, warmup=5, runs=a.c5_steps,
+                             compute=a.compute, wire_dtype=a.c5_wire, backend="xgmi", graph=True,
+                             devices=a.devices, time_scale=a.time_scale, quiet=True,
+                             json=out if rank == 0 else None)
+    env = dict(os.environ, DLNB_XGMI_TIMEOUT_S=os.environ.get("DLNB_XGMI_TIMEOUT_S", "20"))
+    res: Dict[str, Any] = {"backend": "XGMI", "hip_graph": True}
+    try:
+        p = subprocess.run([os.path.join(ROOT, "build", "bin", "dp"), *args], env=env, timeout=240,
+                           stdout=sys.stderr, stderr=subprocess.PIPE, text=True)
+        if p.returncode != 0:
+            return {"error": f"exit {p.returncode}: " + (p.stderr or "")[-300:]}
+        if rank != 0:
+            return res
+        with open(out) as f:
+            d = json.load(f)
+        os.remove(out)
+        it = d["global"]["dlnb"]["iteration"]
+        res.update({"ms_per_step": round(it["timed_ms_per_iter"], 4), "median_ms": round(it["median_ms"], 4),
+                    "exposed_comm_ms": _mean_of(d, "barrier_time"),
+                    "allreduce_busbw_GBps": _busbw(d, "allreduce", world),
+                    "allreduce_algbw_GBps": _algbw(d, "allreduce")})
+        if c5.get("ms_per_step"):
+            # > 1: the xgmi kernels finish the comm-bound step faster than the comm_bound block's backend
+            res["speedup_vs_comm_bound"] = round(c5["ms_per_step"] / res["ms_per_step"], 4)
+            res["comm_bound_backend"] = c5.get("backend")
+    except Exception as e:  # noqa: BLE001
+        res = {"error": str(e)[:300]}
+    return res
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -119,6 +161,8 @@ def main() -> int:
     ap.add_argument("--c5-wire", default="bf16", help="wire dtype of the comm-bound all-reduce")
     ap.add_argument("--stretch-steps", type=int, default=2,
                     help="fixed-work FSDP iterations for compute_stretch (0 skips)")
+    ap.add_argument("--xgmi-ab", choices=["auto", "on", "off"], default="auto",
+                    help="comm_bound_xgmi secondary (auto: when N > 1 on the GPU)")
     ap.add_argument("--json", default=None, help="also write the full headline report here (rank 0)")
     a = ap.parse_args()
 
@@ -207,6 +251,9 @@ def main() -> int:
         sys.stdout.flush()
         os.dup2(saved, 1)
         os.close(saved)
+    # xgmi A/B last, in child processes (see the module docstring).
+    if a.c5_model != "none" and on_gpu and (a.xgmi_ab == "on" or (a.xgmi_ab == "auto" and world > 1)):
+        extra["comm_bound_xgmi"] = _xgmi_ab(a, world, rank, extra.get("comm_bound", {}))
     if rank != 0:
         return 0
     g = doc["global"]

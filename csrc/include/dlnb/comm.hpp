@@ -9,7 +9,7 @@
 //     WaitAll(n) (the reference's CCL "Barrier" that was not a barrier,
 //     proxy_classes.hpp:189-191, disappears: host barriers live in
 //     HostGroup);
-//   * the backend is chosen at run time (--backend rccl|xgmi|cpu);
+//   * the backend is chosen at run time (--backend rccl|xgmi|mixed|cpu);
 //   * all-to-all maps to ncclAllToAll instead of a hand-rolled
 //     ncclGroupStart + per-peer send/recv loop (proxy_classes.hpp:160-182);
 //   * element type is explicit (the MPI backend's hard-coded MPI_FLOAT,
@@ -83,6 +83,9 @@ std::unique_ptr<CommFactory> make_rccl_factory(HostGroup& world, Device& dev);
 std::unique_ptr<CommFactory> make_shm_factory(HostGroup& world, Device& dev);
 // Own kernels over IPC-mapped peer windows (one node); see dlnb/xgmi.hpp.
 std::unique_ptr<CommFactory> make_xgmi_factory(HostGroup& world, Device& dev);
+// Size-based dispatch: xgmi kernels for small messages inside a node, RCCL
+// otherwise (comm_mixed.cpp).
+std::unique_ptr<CommFactory> make_mixed_factory(HostGroup& world, Device& dev);
 
 // Loopback: N ranks as threads of one process on one device (GPU or CPU),
 // sharing one LoopbackHub. Collectives are issued by the last rank to

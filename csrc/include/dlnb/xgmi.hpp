@@ -35,12 +35,12 @@ namespace dlnb {
 namespace xgmi {
 
 constexpr int kMaxRanks = 8;     // one node: 8 MI355X, fully connected by xGMI
-constexpr int kMaxBlocks = 256;  // per-block flags
+constexpr int kMaxBlocks = 1024;  // per-block flags
 constexpr int kThreads = 512;
 
 // Flag words (uint32) in each rank's flag array.
-constexpr size_t kFlagColl = 0;                                    // [phase 2][src 8][block 256]
-constexpr size_t kFlagP2PSeq = 2 * kMaxRanks * kMaxBlocks;         // [src 8][block 256]
+constexpr size_t kFlagColl = 0;                                    // [phase 2][src 8][block]
+constexpr size_t kFlagP2PSeq = 2 * kMaxRanks * kMaxBlocks;         // [src 8][block]
 constexpr size_t kFlagP2PConsumed = kFlagP2PSeq + kMaxRanks * kMaxBlocks;  // [dst 8]
 // Local-only control words (never touched by peers):
 constexpr size_t kCtl = kFlagP2PConsumed + 64;
@@ -51,7 +51,8 @@ constexpr size_t kCtlSendDone = kCtl + 32;       // [dst 8] finished blocks of t
 constexpr size_t kCtlRecvSeq = kCtl + 48;        // [src 8] last message number received from src
 constexpr size_t kCtlRecvDone = kCtl + 64;       // [src 8] finished blocks of the running receive
 constexpr size_t kFlagWords = kCtl + 80;
-constexpr size_t kFlagBytes = 64 * 1024;
+constexpr size_t kFlagBytes = 128 * 1024;
+static_assert(kFlagWords * 4 <= kFlagBytes, "flag page too small");
 
 struct Peers {
   char* win[kMaxRanks];        // each rank's window, mapped in this process
@@ -61,6 +62,7 @@ struct Peers {
   uint64_t timeout_ticks;      // s_memrealtime ticks (100 MHz) before a wait gives up
   int rank;
   int nranks;
+  int uncached;                // windows + flags in uncached memory (the default; see release_window)
 };
 
 enum class Op : int { AllGather, ReduceScatter, AllReduceOneShot, AllReduceTwoShot, AllToAll };

@@ -25,24 +25,48 @@ namespace {
 constexpr int T = kThreads;
 
 // Flags are raised with a system-scope atomic RMW, not a store: L2 is per
-// XCD and not coherent across XCDs, and a plain (even release) store made
-// through a peer's IPC mapping can sit in the writer's L2 after the release
-// fence has written back the data before it - the waiter, polling its
-// uncached flag word, then spins until that line happens to be evicted
-// (seen as intermittent multi-second stalls with two ranks on one GPU).
-// Atomics execute at the memory side. Epochs only grow, so max == store.
+// XCD and not coherent across XCDs, and a plain store made through a peer's
+// IPC mapping can sit in the writer's L2 - the waiter, polling its flag
+// word, then spins until that line happens to be evicted (seen as
+// intermittent multi-second stalls with two ranks on one GPU). Atomics
+// execute at the memory side. Epochs only grow, so max == store. The RMW
+// itself is relaxed: release_window() orders the data before it.
 __device__ __forceinline__ void sys_store(uint32_t* p, uint32_t v) {
-  __hip_atomic_fetch_max(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_fetch_max(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 // Polled with an idempotent atomic RMW for the same reason: a plain
 // system-scope load can keep hitting a stale line in the poller's own XCD L2.
 // (A compare-and-swap that never matches: LLVM folds an idempotent add/or
-// into a plain load.)
+// into a plain load.) Relaxed: an acquire here would invalidate the whole
+// L2 on every poll; acquire_window() runs once after the wait instead.
 __device__ __forceinline__ uint32_t sys_load(uint32_t* p) {
   uint32_t v = 0xffffffffu;
-  __hip_atomic_compare_exchange_strong(p, &v, 0xffffffffu, __ATOMIC_ACQUIRE, __ATOMIC_ACQUIRE,
+  __hip_atomic_compare_exchange_strong(p, &v, 0xffffffffu, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_SYSTEM);
   return v;
+}
+
+// Make this wave's window stores visible to the peers before a flag is
+// raised. Uncached windows (the default) never hold data in any cache, so
+// completing the stores (vmcnt 0) is all it takes; a system-scope release
+// fence would also write back the whole L2 of the XCD (buffer_wbl2) and,
+// as __threadfence_system() is acquire-release, invalidate it - once per
+// block and piece, costly for every kernel sharing the XCD. Cached windows
+// (DLNB_XGMI_MEM=fine|coarse) keep the full fence.
+__device__ __forceinline__ void release_window(const Peers& P) {
+  if (P.uncached)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+// After the peers' flags were seen: drop this CU's L1 lines (the window
+// slots were read two pieces ago) - the L2 holds no window data when the
+// windows are uncached; cached windows take the full system acquire.
+__device__ __forceinline__ void acquire_window(const Peers& P) {
+  if (P.uncached)
+    asm volatile("buffer_inv sc0" ::: "memory");
+  else
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
 
 // Spin until *f >= v (wrap-safe). Every wait has an exit: the host's abort
@@ -88,22 +112,25 @@ __device__ __forceinline__ bool end_seq(const Peers& P, size_t word, size_t done
   __syncthreads();
   if (threadIdx.x != 0) return false;
   uint32_t* f = P.flags[P.rank];
-  const uint32_t old = __hip_atomic_fetch_add(f + done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  // relaxed: the counters carry no data; the next kernel on the stream reads
+  // them after this kernel's end-of-kernel release
+  const uint32_t old = __hip_atomic_fetch_add(f + done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (old + 1 != gridDim.x) return false;
   __hip_atomic_store(f + done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(f + word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(f + word, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }
 
 // This block's window stores are visible system-wide -> raise one flag per
 // peer -> wait for every peer's flag of the same block and phase.
 __device__ void exchange(const Peers& P, int phase, uint32_t epoch) {
-  __threadfence_system();
+  release_window(P);
   __syncthreads();
   const int t = threadIdx.x;
   if (t < P.nranks && t != P.rank) sys_store(coll_flag(P, t, phase, P.rank), epoch);
   if (t < P.nranks && t != P.rank) wait_geq(coll_flag(P, P.rank, phase, t), epoch, P);
   __syncthreads();
+  acquire_window(P);
 }
 
 __device__ __forceinline__ void blk_range(size_t n, size_t& lo, size_t& hi) {
@@ -474,7 +501,7 @@ __global__ void __launch_bounds__(T) send_kernel(Peers P, const char* buf, size_
   char* w = P.win[dst] + off + (n & 1) * slot;
   copy_vec(V(w), V(buf), lo, hi);
   copy_tail(w, buf, nv * 16, bytes);
-  __threadfence_system();
+  release_window(P);
   __syncthreads();
   if (threadIdx.x == 0) sys_store(P.flags[dst] + kFlagP2PSeq + static_cast<size_t>(P.rank) * kMaxBlocks + blockIdx.x, n);
   end_seq(P, kCtlSendSeq + dst, kCtlSendDone + dst, n);
@@ -484,6 +511,7 @@ __global__ void __launch_bounds__(T) recv_kernel(Peers P, char* buf, size_t byte
   const uint32_t n = begin_seq(P, kCtlRecvSeq + src);
   if (threadIdx.x == 0) wait_geq(P.flags[P.rank] + kFlagP2PSeq + static_cast<size_t>(src) * kMaxBlocks + blockIdx.x, n, P);
   __syncthreads();
+  acquire_window(P);
   const size_t nv = bytes / 16;
   size_t lo, hi;
   blk_range(nv, lo, hi);

@@ -18,7 +18,7 @@
 //
 // Tunables (env): DLNB_XGMI_REGION_MB (per-parity collective region, default
 // 256), DLNB_XGMI_P2P_MB (per-source, per-parity P2P slot, default 128),
-// DLNB_XGMI_BLOCKS (max blocks per kernel, default 64),
+// DLNB_XGMI_BLOCKS (max blocks per kernel, default 256),
 // DLNB_XGMI_ONESHOT_KB (all-reduce one-shot threshold, default 256),
 // DLNB_XGMI_TIMEOUT_S (device-side wait timeout, default 600).
 #include <hip/hip_runtime.h>
@@ -79,7 +79,7 @@ class XgmiComm : public Communicator {
     DLNB_REQUIRE(rank_ >= 0, "rank " << my_world_rank << " is not a member of group " << name);
     DLNB_REQUIRE(size_ <= xgmi::kMaxRanks, "xgmi backend: group " << name << " has " << size_ << " ranks (max "
                                                                  << xgmi::kMaxRanks << ", one node)");
-    max_blocks_ = static_cast<int>(std::max<long long>(1, std::min<long long>(xgmi::kMaxBlocks, env_int("DLNB_XGMI_BLOCKS", 64))));
+    max_blocks_ = static_cast<int>(std::max<long long>(1, std::min<long long>(xgmi::kMaxBlocks, env_int("DLNB_XGMI_BLOCKS", 256))));
     oneshot_ = static_cast<size_t>(env_int("DLNB_XGMI_ONESHOT_KB", 256)) << 10;
     const size_t cap = std::max<size_t>(capacity, 4096);
     // Collective region per parity: AG/RS/A2A need W slots of a piece, the
@@ -145,6 +145,7 @@ class XgmiComm : public Communicator {
     peers_.timeout_ticks = static_cast<uint64_t>(env_int("DLNB_XGMI_TIMEOUT_S", 600)) * 100000000ull;
     peers_.rank = rank_;
     peers_.nranks = size_;
+    peers_.uncached = mem != "coarse" && mem != "fine";
     // Nobody may free its window before every member has mapped it.
     const std::string done = key.str() + "opened";
     if (world.store().add(done, 1) == size_) world.store().set(done + "/go", "1");

@@ -225,7 +225,7 @@ int commtest_main(int argc, char** argv) {
     else if (a == "--ranks") ranks = std::stoi(val("--ranks"));
     else if (a == "--json") json_path = val("--json");
     else if (a == "-h" || a == "--help") {
-      std::cout << "Usage: dlnb commtest [--backend auto|rccl|xgmi|cpu|loopback|loopback-cpu] [--ranks N] [-d 0,1,..]\n"
+      std::cout << "Usage: dlnb commtest [--backend auto|rccl|xgmi|mixed|cpu|loopback|loopback-cpu] [--ranks N] [-d 0,1,..]\n"
                    "                     [--dtype bf16|fp16|fp32|fp8_e4m3|fp8_e5m2]\n"
                    "                     [--sizes n1,n2,..] [--bench] [--iters N] [--warmup N] [--graph]\n"
                    "  sizes are elements per rank; check mode verifies every collective exactly\n"
@@ -237,7 +237,7 @@ int commtest_main(int argc, char** argv) {
   Context ctx;
   ctx.boot = std::move(boot);
   const std::string be = select_backend(ctx, backend, devices);
-  DLNB_REQUIRE(!graph || be == "rccl" || be == "xgmi", "commtest --graph needs --backend rccl or xgmi");
+  DLNB_REQUIRE(!graph || be == "rccl" || be == "xgmi" || be == "mixed", "commtest --graph needs a GPU backend");
   const DType t = parse_dtype(dtype);
   const int W = ctx.world(), me = ctx.rank();
   std::vector<size_t> sizes;
@@ -305,14 +305,18 @@ int commtest_main(int argc, char** argv) {
       const char* name;
       CollKind kind;
     };
+    // "copy": one device-to-device copy of the rank's n elements (the local
+    // HBM roofline the collectives' kernels are compared against).
     const K kinds[] = {{"all_reduce", CollKind::AllReduce},
                        {"all_gather", CollKind::AllGather},
                        {"reduce_scatter", CollKind::ReduceScatter},
-                       {"all_to_all", CollKind::AllToAll}};
+                       {"all_to_all", CollKind::AllToAll},
+                       {"copy", CollKind::SendRecv}};
     for (size_t n : sizes) {
       for (const K& k : kinds) {
         auto op = [&] {
           switch (k.kind) {
+            case CollKind::SendRecv: ctx.dev->copy_async(b.data(), a.data(), n * es, *stream); break;
             case CollKind::AllReduce: comm->all_reduce(a.data(), b.data(), n, t, *stream); break;
             case CollKind::AllGather: comm->all_gather(a.data(), b.data(), n, t, *stream); break;
             case CollKind::ReduceScatter: comm->reduce_scatter(a.data(), b.data(), n, t, *stream); break;
@@ -336,7 +340,7 @@ int commtest_main(int argc, char** argv) {
         const double dt = ctx.hg().allreduce_max(now() - t0) / iters;
         // algorithm bytes per rank (nccl-tests): AR/RS/A2A n*W... AG output
         double bytes = static_cast<double>(n) * es;
-        if (k.kind != CollKind::AllReduce) bytes *= W;
+        if (k.kind != CollKind::AllReduce && k.kind != CollKind::SendRecv) bytes *= W;
         if (me == 0) {
           Json j = Json::object();
           j["commtest"] = "bench";
@@ -349,7 +353,7 @@ int commtest_main(int argc, char** argv) {
           j["bytes"] = bytes;
           j["time_us"] = dt * 1e6;
           j["algbw_GBps"] = bytes / dt / 1e9;
-          j["busbw_GBps"] = bytes / dt / 1e9 * busbw_factor(k.kind, W);
+          j["busbw_GBps"] = k.kind == CollKind::SendRecv ? 0.0 : bytes / dt / 1e9 * busbw_factor(k.kind, W);
           std::cout << j.dump() << std::endl;
         }
       }

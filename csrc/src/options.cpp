@@ -74,7 +74,7 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  -d, --devices LIST     comma-separated device ids indexed by local rank\n"
      << "  -m, --min_exectime S   run at least S seconds (overrides --runs)\n"
      << "  -h, --help             this help\n"
-     << "  --backend B            auto | rccl | xgmi | cpu | loopback | loopback-cpu\n"
+     << "  --backend B            auto | rccl | xgmi | mixed | cpu | loopback | loopback-cpu\n"
      << "  --ranks N              loopback: ranks run as threads of this process on one GPU\n"
      << "                         (loopback-cpu: on the CPU device), default 2\n"
      << "  --compute C            auto | sleep | spin | gemm | gemm-work | flops\n"
@@ -109,7 +109,7 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  --rccl-max-ctas N      RCCL blocks per collective on each comm lane (default: comm-cus / lanes;\n"
      << "                         0 = RCCL's own choice)\n"
      << "  --comm-lanes single|split  fsdp: all collectives on one ordered lane (default) or one per kind\n"
-     << "  --graph                capture one iteration into a HIP graph, replay it every iteration (rccl)\n"
+     << "  --graph                capture one iteration into a HIP graph, replay it every iteration (rccl, xgmi, mixed)\n"
      << "env: DLNB_TIMEOUT (s, hang detection), DLNB_INJECT_FAULT=rank=R,iter=I,mode=exit|hang|throw,\n"
      << "     DLNB_STORE_ADDR=host:port, DLNB_NO_ENERGY=1\n";
   return os.str();

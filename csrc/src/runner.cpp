@@ -195,7 +195,7 @@ std::string select_backend(Context& ctx, const std::string& requested, const std
   const bool in_process = backend == "loopback" || backend == "loopback-cpu";
   const int ngpu = in_process ? 0 : gpu_device_count();
   if (backend == "auto") backend = ngpu > 0 ? "rccl" : "cpu";
-  if (backend == "rccl" || backend == "xgmi") {
+  if (backend == "rccl" || backend == "xgmi" || backend == "mixed") {
     DLNB_REQUIRE(ngpu > 0, "--backend " << backend << " requested but no GPU is visible");
     std::vector<int> list = parse_device_list(devices);
     if (list.empty())
@@ -205,7 +205,9 @@ std::string select_backend(Context& ctx, const std::string& requested, const std
     int dev_index = list[static_cast<size_t>(ri.local_rank)];
     DLNB_REQUIRE(dev_index >= 0 && dev_index < ngpu, "device id " << dev_index << " out of range");
     ctx.dev = make_gpu_device(dev_index);
-    ctx.comms = backend == "rccl" ? make_rccl_factory(ctx.hg(), *ctx.dev) : make_xgmi_factory(ctx.hg(), *ctx.dev);
+    ctx.comms = backend == "rccl"    ? make_rccl_factory(ctx.hg(), *ctx.dev)
+                : backend == "xgmi" ? make_xgmi_factory(ctx.hg(), *ctx.dev)
+                                    : make_mixed_factory(ctx.hg(), *ctx.dev);
   } else if (backend == "cpu") {
     ctx.dev = make_cpu_device();
     ctx.comms = make_shm_factory(ctx.hg(), *ctx.dev);
@@ -227,7 +229,7 @@ std::string select_backend(Context& ctx, const std::string& requested, const std
     }
     ctx.comms = make_loopback_factory(ctx.hg(), *ctx.dev, ctx.boot->hub);
   } else {
-    DLNB_THROW("unknown backend '" << backend << "' (auto, rccl, xgmi, cpu, loopback, loopback-cpu)");
+    DLNB_THROW("unknown backend '" << backend << "' (auto, rccl, xgmi, mixed, cpu, loopback, loopback-cpu)");
   }
   return backend;
 }
@@ -349,7 +351,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   // sit in the queue while another communicator's kernel holds the free CUs
   // spinning on a peer that waits for them.
   const int lanes = collective_lanes(opt, ri.world_size);
-  const bool rccl = backend == "rccl";
+  const bool rccl = backend == "rccl" || backend == "mixed";
   const bool gemm_compute = ctx.compute->mode() == ComputeMode::Gemm;
   if (rccl) {
     if (opt.rccl_max_ctas >= 0)
@@ -389,7 +391,8 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     DLNB_REQUIRE(ctx.dev->kind() == DeviceKind::GPU, "--graph needs a GPU");
     // xgmi kernels take their epochs from device-side counters, so a replayed
     // graph issues fresh ones; the loopback backends synchronise on the host.
-    DLNB_REQUIRE(backend == "rccl" || backend == "xgmi", "--graph needs --backend rccl or xgmi");
+    DLNB_REQUIRE(backend == "rccl" || backend == "xgmi" || backend == "mixed",
+                 "--graph needs --backend rccl, xgmi or mixed");
     DLNB_REQUIRE(strat->capturable(), "--graph cannot capture --schedule reference (it blocks the host)");
     std::vector<Stream*> ss = strat->streams();
     std::vector<Stream*> others(ss.begin() + 1, ss.end());

@@ -101,3 +101,27 @@ def test_bench_gpu_single_rank_secondaries(tmp_path):
     assert 0.8 < c5["gemm_work"]["compute_stretch"] < 1.5, c5
     assert 0.8 < o["compute_stretch"] < 1.5, o
     assert o["rccl_cta_budget"]["applies"] and o["rccl_cta_budget"]["max_ctas_per_lane"] == 32
+
+
+@pytest.mark.gpu
+def test_bench_torchrun_xgmi_two_ranks_one_gpu(tmp_path):
+    """The driver's N > 1 launch on the GPU: torchrun, 2 ranks sharing GPU 0 over the xgmi kernels (RCCL
+    refuses two ranks on one device), HIP graph, plus the comm_bound_xgmi child-process secondary."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--backend", "xgmi", "--devices", "0,0"] + TINY
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=str(tmp_path),
+                       env=dict(os.environ, DLNB_XGMI_TIMEOUT_S="60"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    o = lines[0]
+    assert o["n_gpus"] == 2 and o["config"]["backend"] == "XGMI" and o["config"]["hip_graph"] is True
+    assert o["effective_busbw_GBps"]["allgather"] > 0
+    x = o["comm_bound_xgmi"]
+    assert "error" not in x, x
+    assert x["hip_graph"] is True and x["ms_per_step"] > 0 and x["allreduce_busbw_GBps"] > 0
+    assert x["speedup_vs_comm_bound"] > 0 and x["comm_bound_backend"] == "XGMI"

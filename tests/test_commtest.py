@@ -42,9 +42,9 @@ def test_cpu_backend_exact(w, dtype):
 def test_cpu_backend_bench_lines():
     out = commtest(2, "--backend", "cpu", "--bench", "--sizes", "4096,65536", "--iters", "2", "--warmup", "1")
     ops = {(o["op"], o["count"]) for o in out}
-    assert len(ops) == 8
+    assert len(ops) == 10  # 4 collectives + the local copy roofline, 2 sizes
     for o in out:
-        assert o["busbw_GBps"] > 0 and o["time_us"] > 0
+        assert o["time_us"] > 0 and (o["busbw_GBps"] > 0 or o["op"] == "copy")
 
 
 def test_commtest_usage():
@@ -105,6 +105,23 @@ def test_rccl_graph_replay_exact():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("graph", [False, True])
+def test_mixed_backend_single_rank_exact(graph):
+    """--backend mixed (size-based RCCL / xgmi dispatch) at W = 1, the only rank count RCCL allows on one GPU:
+    every op and size routes through the dispatcher and stays exact."""
+    _need_gpu()
+    extra = ["--graph"] if graph else []
+    out = commtest(1, "--backend", "mixed", "--sizes", "1,4097,1048583", *extra, env_extra={"DLNB_MIXED_XGMI_MAX_KB": "64"})
+    assert out[0]["ok"] and out[0]["backend"] == "RCCL", out  # one rank: no xgmi side
+
+
+def test_mixed_backend_needs_gpu():
+    p = subprocess.run([DLNB, "commtest", "--backend", "mixed"], capture_output=True, text=True,
+                       env=dict(os.environ, HIP_VISIBLE_DEVICES="-1"))
+    assert p.returncode != 0 and "no GPU" in p.stderr, p.stderr[-500:]
+
+
+@pytest.mark.gpu
 def test_xgmi_default_windows_large_message():
     _need_gpu()
     out = commtest(2, "--backend", "xgmi", "-d", "0,0", "--sizes", "33554441", env_extra={"DLNB_XGMI_TIMEOUT_S": "60"})
@@ -116,7 +133,7 @@ def test_xgmi_bench_runs():
     _need_gpu()
     out = commtest(2, "--backend", "xgmi", "-d", "0,0", "--bench", "--sizes", "65536,4194304", "--iters", "5",
                    "--warmup", "2", env_extra={"DLNB_XGMI_TIMEOUT_S": "60"})
-    assert len(out) == 8 and all(o["busbw_GBps"] > 0 for o in out)
+    assert len(out) == 10 and all(o["busbw_GBps"] > 0 for o in out if o["op"] != "copy")
 
 
 XGMI_STRATS = [  # strategy, model, positional args, extra flags, ranks

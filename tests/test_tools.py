@@ -246,3 +246,47 @@ def test_unified_cli(tmp_path, data_dir, root):
     assert main(["run", "bogus"]) == 1
     assert main(["nope"]) == 1
     assert main(["plan", "fsdp", "llama3_8b_16_bfloat16", "32", "8", "--world", "8", "--base", root]) == 0
+
+
+def test_prof_merge_folds_counters_into_report(tmp_path):
+    """tools/prof_merge.py: rocprofv3 kernel trace + PMC CSVs -> global.dlnb.counters per kernel class."""
+    from dlnetbench_amd.tools import prof_merge
+    tr = tmp_path / "prof" / "host" / "123"
+    tr.mkdir(parents=True)
+    rows = [("void dlnb::kernels::gemm_8phase_kernel<false, true, false>(...)", 0, 2_000_000),
+            ("void dlnb::kernels::gemm_8phase_kernel<false, true, false>(...)", 3_000_000, 5_000_000),
+            ("ncclDevKernel_Generic_1(ncclDevKernelArgsStorage<4096ul>)", 100, 600_100),
+            ("__amd_rocclr_copyBuffer", 0, 1000),
+            ("void dlnb::xgmi::(anonymous namespace)::ar2_kernel<(dlnb::DType)0>(...)", 0, 50_000)]
+    with open(tr / "x_kernel_trace.csv", "w") as f:
+        f.write("Kind,Agent_Id,Kernel_Name,Start_Timestamp,End_Timestamp\n")
+        for n, s, e in rows:
+            f.write(f'KERNEL_DISPATCH,1,"{n}",{s},{e}\n')
+    pm = tmp_path / "pmc"
+    pm.mkdir()
+    with open(pm / "y_counter_collection.csv", "w") as f:
+        f.write("Dispatch_Id,Agent_Id,Kernel_Name,Counter_Name,Counter_Value,Start_Timestamp,End_Timestamp\n")
+        g = "void dlnb::kernels::gemm_8phase_kernel<false, true, false>(...)"
+        # 1 ms dispatch at 2 GHz: GUI = 2e6 cycles x 8 XCDs; MFMA busy half of 256 CUs x 4 SIMDs
+        f.write(f'1,1,"{g}",GRBM_GUI_ACTIVE,16000000,0,1000000\n')
+        f.write(f'1,1,"{g}",SQ_VALU_MFMA_BUSY_CYCLES,{0.5 * 2e6 * 1024},0,1000000\n')
+        f.write(f'1,1,"{g}",SQ_INSTS_VALU_MFMA_MOPS_BF16,{1e15 * 1e-3 / 512},0,1000000\n')
+        f.write(f'1,1,"{g}",FETCH_SIZE,{4e9 / 1024},0,1000000\n')
+    pm2 = tmp_path / "pmc2"  # a second pass (WRITE_SIZE did not fit the first): 2 ms dispatch
+    pm2.mkdir()
+    with open(pm2 / "z_counter_collection.csv", "w") as f:
+        f.write("Dispatch_Id,Agent_Id,Kernel_Name,Counter_Name,Counter_Value,Start_Timestamp,End_Timestamp\n")
+        f.write(f'1,1,"{g}",WRITE_SIZE,{2e9 / 1024},0,2000000\n')
+    rep_path = tmp_path / "r.json"
+    rep_path.write_text(json.dumps({"section": "fsdp", "global": {"dlnb": {"iteration": {}}}, "ranks": []}))
+    assert prof_merge.main([str(rep_path), str(tmp_path / "prof"), str(pm), str(pm2)]) == 0
+    c = json.loads(rep_path.read_text())["global"]["dlnb"]["counters"]
+    cl = c["classes"]
+    assert cl["compute_gemm"]["calls"] == 2 and cl["compute_gemm"]["time_ms"] == pytest.approx(4.0)
+    assert cl["rccl"]["calls"] == 1 and cl["copy"]["calls"] == 1 and cl["xgmi"]["calls"] == 1
+    assert cl["compute_gemm"]["clock_GHz"] == pytest.approx(2.0)
+    assert cl["compute_gemm"]["mfma_busy"] == pytest.approx(0.5)
+    assert cl["compute_gemm"]["mfma_TFLOPs"] == pytest.approx(1000.0, rel=1e-3)
+    assert cl["compute_gemm"]["hbm_GBps"] == pytest.approx(5000.0, rel=1e-3)
+    assert c["total_kernel_ms"] == pytest.approx(4.0 + 0.6 + 0.001 + 0.05)
+    assert sum(v["time_pct"] for v in cl.values()) == pytest.approx(100.0, abs=0.05)
