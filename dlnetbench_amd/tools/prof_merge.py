@@ -6,7 +6,8 @@ reads a rocprofv3 kernel trace (``--kernel-trace``, ``*kernel_trace.csv``)
 and/or a counter collection (``--pmc``, ``*counter_collection.csv``) of the
 same command, groups kernels into classes and writes, per class: calls,
 kernel time, and — when the counters were collected — MFMA busy fraction,
-MFMA TFLOP/s, HBM bytes read / written and achieved HBM GB/s.
+MFMA TFLOP/s, and the bytes read / written beyond the L2 (TCC <-> data
+fabric: Infinity Cache or HBM; FETCH_SIZE / WRITE_SIZE) with their rate.
 
     rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof -- python3 bench.py --json r.json ...
     rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU_MFMA_MOPS_BF16 --output-format csv \\
@@ -135,10 +136,10 @@ def derive(c: dict) -> dict:
     mops = sum(rate(n) for n in k if n.startswith("SQ_INSTS_VALU_MFMA_MOPS"))
     if mops:
         out["mfma_TFLOPs"] = round(mops * 512 / 1e12, 1)
-    if "FETCH_SIZE" in k or "WRITE_SIZE" in k:
-        out["hbm_read_bytes"] = k.get("FETCH_SIZE", 0.0) * 1024
-        out["hbm_write_bytes"] = k.get("WRITE_SIZE", 0.0) * 1024
-        out["hbm_GBps"] = round((rate("FETCH_SIZE") + rate("WRITE_SIZE")) * 1024 / 1e9, 1)
+    if "FETCH_SIZE" in k or "WRITE_SIZE" in k:  # L2 misses / write-backs to the fabric (MALL or HBM)
+        out["fabric_read_bytes"] = k.get("FETCH_SIZE", 0.0) * 1024
+        out["fabric_write_bytes"] = k.get("WRITE_SIZE", 0.0) * 1024
+        out["fabric_GBps"] = round((rate("FETCH_SIZE") + rate("WRITE_SIZE")) * 1024 / 1e9, 1)
     if k:
         out["counters"] = dict(k)
     return out

@@ -287,6 +287,6 @@ def test_prof_merge_folds_counters_into_report(tmp_path):
     assert cl["compute_gemm"]["clock_GHz"] == pytest.approx(2.0)
     assert cl["compute_gemm"]["mfma_busy"] == pytest.approx(0.5)
     assert cl["compute_gemm"]["mfma_TFLOPs"] == pytest.approx(1000.0, rel=1e-3)
-    assert cl["compute_gemm"]["hbm_GBps"] == pytest.approx(5000.0, rel=1e-3)
+    assert cl["compute_gemm"]["fabric_GBps"] == pytest.approx(5000.0, rel=1e-3)
     assert c["total_kernel_ms"] == pytest.approx(4.0 + 0.6 + 0.001 + 0.05)
     assert sum(v["time_pct"] for v in cl.values()) == pytest.approx(100.0, abs=0.05)
