@@ -373,6 +373,239 @@ __global__ void __launch_bounds__(512, 1)
   }
 }
 
+// ---------------------------------------------------------------------------
+// Streaming persistent variant (the deadline compute, DL only).
+//
+// The per-tile kernel above fills the pipeline at the start of every tile
+// (six half-tiles staged, the first MFMA waits for two of them) and drains it
+// over the last two K-tiles. In the persistent deadline kernel a block runs
+// tile after tile, so here the K-tiles of consecutive tiles form ONE stream:
+// global K-tile g = r * nk + v of the block's r-th tile, LDS buffer g & 1,
+// and the phases of the last two K-tiles of tile r stage K-tiles 0 and 1 of
+// tile r + 1 exactly as the steady state would. Right after phase 3 of a
+// tile's last K-tile the wave converts and stores its accumulators and zeroes
+// them (32 stores per thread), then continues into the next tile's K-tile 0,
+// whose half-tiles are already in flight. The 32 stores sit in the in-order
+// vmcnt queue between the half-tiles, so that K-tile's four waits count them
+// (vmcnt(40) instead of 8; from its successor on the stores are older than
+// every half-tile waited for and the count is 8 again). The two counts are a
+// uniform branch per phase: a second copy of the K-tile body in the loop
+// spills ~160 VGPRs. That branch is why this kernel only pays at short K
+// (gemm_tn_8phase_deadline picks it for <= 16 K-tiles).
+template <bool FP8>
+__device__ __forceinline__ void store_tile(const Ctx& c, __bf16* __restrict__ C, int ldc, int tm, int tn,
+                                           f32x4 (&acc)[2][2][4][2]) {
+  // This lane's element offset in the tile, made opaque so the compiler
+  // cannot hoist the 32 store addresses out of the K-loop (they would stay
+  // live across it and spill).
+  size_t lane = static_cast<size_t>(c.wr * 64 + c.r16) * ldc + c.wc * 32 + 4 * c.h;
+  asm volatile("" : "+v"(lane));
+  __bf16* base = C + static_cast<size_t>(tm) * kT * ldc + static_cast<size_t>(tn) * kT + lane;
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const f32x4 a = acc[qm][qn][i][j];
+          bf16x4 o;
+          o[0] = static_cast<__bf16>(a[0]);
+          o[1] = static_cast<__bf16>(a[1]);
+          o[2] = static_cast<__bf16>(a[2]);
+          o[3] = static_cast<__bf16>(a[3]);
+          *reinterpret_cast<bf16x4*>(base + static_cast<size_t>(qm * 128 + i * 16) * ldc + qn * 128 + j * 16) = o;
+          acc[qm][qn][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+}
+
+// Tile coordinates of linear tile index b (GROUP-ed M order, as tile()).
+__device__ __forceinline__ void tile_coords(int b, int nt_m, int nt_n, int& tm, int& tn) {
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * nt_n;
+  const int first_m = (b / per_group) * GROUP;
+  const int gsz = min(nt_m - first_m, GROUP);
+  tm = first_m + (b % per_group) % gsz;
+  tn = (b % per_group) / gsz;
+}
+
+struct StreamCtx {
+  const char* A;
+  const char* B;
+  int nt_m, nt_n, T, nk;
+  // the tile being computed (0) and the next one (1); named, not an array:
+  // a runtime-indexed array would live in scratch
+  const char *Ab0, *Ab1, *Bb0, *Bb1;
+};
+
+// Half-tile `slot` of stream K-tile t (t - base in [0, 2 nk): this tile or the next).
+__device__ __forceinline__ void stage_g(const Ctx& c, const StreamCtx& sc, int t, int base, int slot) {
+  const int nxt = t - base >= sc.nk;
+  const int kt = t - base - nxt * sc.nk;
+  const bool isA = slot == kA0 || slot == kA1;
+  const int hi = slot == kA1 || slot == kB1;
+  const char* ab = nxt ? sc.Ab1 : sc.Ab0;
+  const char* bb = nxt ? sc.Bb1 : sc.Bb0;
+  const char* src = (isA ? ab + static_cast<size_t>(hi) * 128 * c.lda : bb + static_cast<size_t>(hi) * 128 * c.ldb) +
+                    static_cast<size_t>(kt) * kRB;
+  stage_half(src, isA ? c.lda : c.ldb, c.smem + (t & 1) * kBuf + slot * kHalf, c.w, c.lane);
+}
+
+// Phase Q of stream K-tile g (g - base = K-tile of the current tile). Same
+// body as phase<FP8, true, false, Q, ...> with stream staging.
+template <bool FP8, int Q, typename AF, typename BF>
+__device__ __forceinline__ bool sphase(const Ctx& c, const StreamCtx& sc, int g, int base, bool after_store, AF& fa,
+                                       BF& b0r, BF& b1r, f32x4 (&acc)[2][2][4][2], const Deadline& d, uint64_t& now) {
+  const char* cur = c.smem + (g & 1) * kBuf;
+  if constexpr (Q == 0) {
+    read_frags<FP8, 2>(cur + kB0 * kHalf, c.wc * 32, c.r16, c.h, b0r);
+    __builtin_amdgcn_sched_barrier(0);
+    read_frags<FP8, 4>(cur + kA0 * kHalf, c.wr * 64, c.r16, c.h, fa);
+  } else if constexpr (Q == 1) {
+    read_frags<FP8, 2>(cur + kB1 * kHalf, c.wc * 32, c.r16, c.h, b1r);
+  } else if constexpr (Q == 2) {
+    read_frags<FP8, 4>(cur + kA1 * kHalf, c.wr * 64, c.r16, c.h, fa);
+    now = __builtin_amdgcn_s_memrealtime();
+  } else {
+    if (d.tid == 0) {
+      const uint64_t el = (now - d.t0) & ((1ull << 48) - 1);
+      d.flag[g & 1] = el >= d.ticks || el >= d.slice_end;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  }
+  if constexpr (Q == 0) stage_g(c, sc, g + 1, base, kB1);
+  if constexpr (Q == 1) stage_g(c, sc, g + 1, base, kA1);
+  if constexpr (Q == 2) stage_g(c, sc, g + 2, base, kA0);
+  if constexpr (Q == 3) stage_g(c, sc, g + 2, base, kB0);
+  // a uniform branch on the wait count, not a second instance of the whole
+  // K-tile body (two bodies in one loop spill ~160 VGPRs)
+  if (after_store)
+    wait_vm<40>();
+  else
+    wait_vm<8>();
+  raw_barrier();
+  bool stop = false;
+  if constexpr (Q == 3) stop = __builtin_amdgcn_readfirstlane(d.flag[g & 1]) != 0;
+  __builtin_amdgcn_s_setprio(1);
+  if constexpr (Q == 0) mfma_quadrant(acc[0][0], fa, b0r);
+  if constexpr (Q == 1) mfma_quadrant(acc[0][1], fa, b1r);
+  if constexpr (Q == 2) mfma_quadrant(acc[1][1], fa, b1r);
+  if constexpr (Q == 3) mfma_quadrant(acc[1][0], fa, b0r);
+  __builtin_amdgcn_s_setprio(0);
+  raw_barrier();
+  return stop;
+}
+
+template <bool FP8>
+__device__ __forceinline__ bool sktile(const Ctx& c, const StreamCtx& sc, int g, int base, bool after_store,
+                                       Frags<FP8>& f, f32x4 (&acc)[2][2][4][2], const Deadline& d) {
+  uint64_t now = 0;
+  sphase<FP8, 0>(c, sc, g, base, after_store, f.a, f.bx, f.by, acc, d, now);
+  sphase<FP8, 1>(c, sc, g, base, after_store, f.a, f.bx, f.by, acc, d, now);
+  sphase<FP8, 2>(c, sc, g, base, after_store, f.a, f.bx, f.by, acc, d, now);
+  return sphase<FP8, 3>(c, sc, g, base, after_store, f.a, f.bx, f.by, acc, d, now);
+}
+
+template <bool FP8>
+__global__ void __launch_bounds__(512, 1)
+    gemm_8phase_stream_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M,
+                              int N, int K, int lda, int ldb, int ldc, uint64_t* __restrict__ slot, uint32_t epoch,
+                              uint64_t ticks, uint64_t slice_end, uint64_t* __restrict__ tstart) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + 16];  // ONE array: staging + deadline flags
+  const int tid = threadIdx.x;
+  Ctx c;
+  c.lane = tid & 63;
+  c.w = tid >> 6;
+  c.wr = c.w >> 2;
+  c.wc = c.w & 3;
+  c.r16 = c.lane & 15;
+  c.h = c.lane >> 4;
+  c.smem = smem;
+  constexpr int esz = FP8 ? 1 : 2;
+  c.lda = static_cast<size_t>(lda) * esz;
+  c.ldb = static_cast<size_t>(ldb) * esz;
+  Deadline d{0, ticks, slice_end, (lds_flag_t*)(smem + 2 * kBuf), tid};
+  {
+    constexpr uint64_t kMask48 = (1ull << 48) - 1;
+    if (tid == 0) {
+      const uint64_t raw = __builtin_amdgcn_s_memrealtime();
+      const uint64_t mine = (static_cast<uint64_t>(epoch) << 48) | (raw & kMask48);
+      uint64_t cur = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while ((cur >> 48) != epoch) {
+        if (__hip_atomic_compare_exchange_strong(slot, &cur, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          cur = mine;
+          if (tstart) __hip_atomic_store(tstart, raw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+      }
+      d.t0 = cur & kMask48;
+    }
+  }
+  StreamCtx sc;
+  sc.A = A;
+  sc.B = B;
+  sc.nt_m = M / kT;
+  sc.nt_n = N / kT;
+  sc.T = sc.nt_m * sc.nt_n;
+  sc.nk = (K * esz) / kRB;  // >= 2 (host checks)
+  int tm0, tn0, tm1, tn1;
+  int round = 0;
+  tile_coords(xcd_remap(blockIdx.x % sc.T, sc.T), sc.nt_m, sc.nt_n, tm0, tn0);
+  tile_coords(xcd_remap((blockIdx.x + gridDim.x) % sc.T, sc.T), sc.nt_m, sc.nt_n, tm1, tn1);
+  sc.Ab0 = A + static_cast<size_t>(tm0) * kT * c.lda;
+  sc.Bb0 = B + static_cast<size_t>(tn0) * kT * c.ldb;
+  sc.Ab1 = A + static_cast<size_t>(tm1) * kT * c.lda;
+  sc.Bb1 = B + static_cast<size_t>(tn1) * kT * c.ldb;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+    for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[qm][qn][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  Frags<FP8> f;
+
+  // Prologue (stream K-tiles 0 and 1), steady-state issue order.
+  stage_g(c, sc, 0, 0, kA0);
+  stage_g(c, sc, 0, 0, kB0);
+  stage_g(c, sc, 0, 0, kB1);
+  stage_g(c, sc, 0, 0, kA1);
+  stage_g(c, sc, 1, 0, kA0);
+  stage_g(c, sc, 1, 0, kB0);
+  wait_vm<8>();
+  raw_barrier();
+  if (c.wr == 1) raw_barrier();  // wave row 1 runs one barrier behind
+
+  int g = 0;     // stream K-tile
+  int base = 0;  // stream index of the current tile's K-tile 0
+  bool stop = false;
+  while (!stop) {
+    // K-tile 0 of a tile after the first: the previous tile's 32 stores are in flight
+    stop = sktile<FP8>(c, sc, g, base, g == base && base > 0, f, acc, d);
+    ++g;
+    if (!stop && g == base + sc.nk) {  // tile done: store, advance the tile window
+      store_tile<FP8>(c, C, ldc, tm0, tn0, acc);
+      base = g;
+      ++round;
+      tm0 = tm1;
+      tn0 = tn1;
+      sc.Ab0 = sc.Ab1;
+      sc.Bb0 = sc.Bb1;
+      tile_coords(xcd_remap((blockIdx.x + (round + 1) * gridDim.x) % sc.T, sc.T), sc.nt_m, sc.nt_n, tm1, tn1);
+      sc.Ab1 = A + static_cast<size_t>(tm1) * kT * c.lda;
+      sc.Bb1 = B + static_cast<size_t>(tn1) * kT * c.ldb;
+    }
+  }
+  // stopped (partial tile discarded): drain every staged half-tile, re-align the rows
+  wait_vm<0>();
+  if (c.wr == 0) raw_barrier();
+}
+
 }  // namespace
 
 bool gemm_8phase_shape_ok(int M, int N, int K, DType in_t) {
@@ -417,10 +650,23 @@ void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N
   auto* a = static_cast<const char*>(A);
   auto* b = static_cast<const char*>(B);
   auto* cc = static_cast<__bf16*>(C);
-  // fp8: the MX body plus the deadline bookkeeping needs 35 VGPRs of spill
-  // space, all of it in the per-tile code around the K-loop (the K-loop
-  // itself has no scratch access), i.e. a few reloads per 32 K-tiles.
-  if (in_t == DType::BF16)
+  // Short K (<= 16 K-tiles, e.g. ViT-H's FFN at fp8: 10) -> the streaming
+  // kernel: the per-tile pipeline fill / drain is a large share of a tile
+  // there (+15 % TF/s at 8192 x 5120 x 1280 fp8). Long K -> the per-tile loop:
+  // the streaming kernel's per-phase branch on the wait count costs more than
+  // the fill it hides (-8..-14 % at K = 4096; profiles/gemm_deadline_stream_r2.md).
+  // DLNB_GEMM_STREAM=0|1 forces either.
+  const int nk = static_cast<int>(static_cast<size_t>(K) * dtype_size(in_t) / kRB);
+  const long long force = env_int("DLNB_GEMM_STREAM", -1);
+  const bool stream_on = force >= 0 ? force != 0 : nk <= 16;
+  if (stream_on) {
+    if (in_t == DType::BF16)
+      hipLaunchKernelGGL((gemm_8phase_stream_kernel<false>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
+                         ticks, slice_end, tstart);
+    else
+      hipLaunchKernelGGL((gemm_8phase_stream_kernel<true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
+                         ticks, slice_end, tstart);
+  } else if (in_t == DType::BF16)
     hipLaunchKernelGGL((gemm_8phase_kernel<false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
                        ticks, slice_end, tstart);
   else

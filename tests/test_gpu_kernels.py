@@ -130,3 +130,31 @@ def test_deadline_gemm_duration(us, dtype):
         times.append(e0.elapsed_time(e1))
     ms = sorted(times)[2]
     assert us / 1e3 <= ms * 1.01 and ms <= us / 1e3 * 1.05 + 0.03, (us, times)
+
+
+@pytest.mark.parametrize("stream", ["0", "1"])
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+@pytest.mark.parametrize("M,N,K,grid", [(1024, 768, 512, 3), (512, 512, 256, 1), (256, 256, 256, 2),
+                                        (768, 512, 1280, 0)])
+def test_deadline_gemm_numerics(M, N, K, grid, dtype, stream, monkeypatch):
+    """The persistent deadline GEMM (the bench's compute), both kernels: the per-tile loop and the
+    streaming one that runs a block's tiles as one K-tile stream (the next tile's first K-tiles are
+    staged while the current one finishes). With a deadline long enough for several passes every tile
+    of C holds a complete product: each one equals A.B^T. Small grids make every block cross many tile
+    boundaries (grid 0 = the default, CUs - 32)."""
+    monkeypatch.setenv("DLNB_GEMM_STREAM", stream)
+    if dtype == "fp8" and not hasattr(torch, "float8_e4m3fn"):
+        pytest.skip("torch without float8")
+    g = torch.Generator(device="cuda").manual_seed(M * 3 + N + K)
+    a = torch.randn(M, K, device="cuda", generator=g)
+    b = torch.randn(N, K, device="cuda", generator=g)
+    if dtype == "fp8":
+        a, b = (a * 0.5).to(torch.float8_e4m3fn), (b * 0.5).to(torch.float8_e4m3fn)
+    else:
+        a, b = a.to(torch.bfloat16), b.to(torch.bfloat16)
+    c = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+    stamp = torch.zeros(8, dtype=torch.int64, device="cuda")
+    gemm.gemm_deadline_us(a, b, c, 3000.0, stamp, grid=grid)
+    torch.cuda.synchronize()
+    assert not torch.isnan(c.float()).any(), "some tile was never stored"
+    assert_close_bf16_out(c, a.float() @ b.float().t())
