@@ -52,6 +52,16 @@ class Communicator {
   virtual void recv(void* buf, size_t count, DType t, int peer, Stream& s) = 0;
   virtual void group_start() {}
   virtual void group_end() {}
+  // Zero-copy registration (collective: every member registers its buffer
+  // of the same role, in the same order). A backend that moves data with
+  // its own kernels can then read a peer's registered send buffer and write
+  // a peer's registered receive buffer directly instead of staging through
+  // its windows; an operation takes the direct path when its buffers are
+  // registered, so registrations and their use must be symmetric across
+  // members (the ncclCommRegister rule). wants_peer_buffers(): allocate
+  // such buffers with Device::alloc_peer and register them.
+  virtual bool wants_peer_buffers() const { return false; }
+  virtual void register_buffer(void* p, size_t bytes) { (void)p, (void)bytes; }
   // Returns a non-empty description if the backend detected an
   // asynchronous failure (peer death, network error).
   virtual std::string async_error() { return ""; }

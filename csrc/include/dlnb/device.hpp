@@ -55,7 +55,9 @@ class GraphExec {
 class Buffer {
  public:
   Buffer() = default;
-  Buffer(Device* dev, size_t bytes);
+  // peer = true: memory peers may read and write directly over xGMI
+  // (Device::raw_alloc_peer; see Communicator::register_buffer).
+  Buffer(Device* dev, size_t bytes, bool peer = false);
   ~Buffer();
   Buffer(const Buffer&) = delete;
   Buffer& operator=(const Buffer&) = delete;
@@ -90,6 +92,11 @@ class Device {
   // Milliseconds from a to b; both must have completed.
   virtual double elapsed_ms(Event& a, Event& b) = 0;
   virtual void* raw_alloc(size_t bytes) = 0;
+  // Zeroed memory that other GPUs' kernels access directly through IPC
+  // mappings (GPU: uncached, so a peer's stores are never shadowed by a stale
+  // line in this device's L2 and this device's stores reach memory when
+  // they complete). Freed with raw_free. CPU: plain memory.
+  virtual void* raw_alloc_peer(size_t bytes) { return raw_alloc(bytes); }
   virtual void raw_free(void* p, size_t bytes) = 0;
   // Fill with deterministic pseudo-random values of type t in [-1, 1)
   // (random data keeps the MFMA units at realistic clocks, unlike zeros).
@@ -115,6 +122,7 @@ class Device {
                                              const std::function<void()>& enqueue);
 
   Buffer alloc(size_t bytes) { return Buffer(this, bytes); }
+  Buffer alloc_peer(size_t bytes) { return Buffer(this, bytes, true); }
 };
 
 // ---- CPU implementation (also used by the GPU-less tests) ----

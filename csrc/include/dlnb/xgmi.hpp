@@ -79,6 +79,27 @@ struct CollPiece {
   DType dtype;
 };
 
+// Zero-copy collectives on registered buffers (Communicator::register_buffer):
+// one kernel per operation, no window staging. Every block owns the same
+// slice on all ranks; its phase-0 flags say "ready" (this rank's kernel has
+// started, so everything its stream did to its buffers before is complete)
+// and its phase-1 flags "done with your buffers" (the kernel - and with it
+// the next use of the buffers on that rank - cannot finish before every peer
+// is done reading / writing them).
+//   AllGather:     dst[r] = rank r's receive buffer at this rank's block; src[me] = send
+//   ReduceScatter: src[r] = rank r's send buffer at this rank's block; out = receive buffer
+//   AllReduce:     src[r] = rank r's send buffer, dst[r] = rank r's receive buffer (may alias);
+//                  rank me sums chunk me of every src and writes it into every dst
+enum class DirectOp : int { AllGather, ReduceScatter, AllReduce };
+struct DirectPiece {
+  const char* src[kMaxRanks];
+  char* dst[kMaxRanks];
+  char* out;
+  size_t bytes;  // AG / RS: bytes per rank block; AR: the whole message (multiple of 16)
+  DType dtype;
+};
+void launch_direct(DirectOp op, const Peers& p, const DirectPiece& c, int blocks, void* stream);
+
 // Number of blocks a piece of `bytes` per rank uses (identical on all ranks).
 int blocks_for(size_t bytes, int max_blocks);
 

@@ -490,6 +490,91 @@ __global__ void __launch_bounds__(T) ar2_kernel(Peers P, CollPiece c) {
   end_seq(P, kCtlCollEpoch, kCtlCollDone, ep);
 }
 
+// ------------------------------------------------ zero-copy (registered)
+
+// dst[j][i] = src[i] for every rank j (own first, then rank-staggered), 4
+// loads in flight per thread.
+__device__ __forceinline__ void push_ptrs(const Peers& P, const uint4* __restrict__ src, uint4* const* dst, size_t lo,
+                                          size_t hi) {
+  size_t i = lo + threadIdx.x;
+  for (; i + 3 * T < hi; i += 4 * T) {
+    uint4 v[4] = {src[i], src[i + T], src[i + 2 * T], src[i + 3 * T]};
+    for (int j = 0; j < P.nranks; ++j) {
+      uint4* d = dst[peer_at(P, j)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) d[i + u * T] = v[u];
+    }
+  }
+  for (; i < hi; i += T) {
+    const uint4 v = src[i];
+    for (int j = 0; j < P.nranks; ++j) dst[peer_at(P, j)][i] = v;
+  }
+}
+
+__global__ void __launch_bounds__(T) ag_direct_kernel(Peers P, DirectPiece c) {
+  const uint32_t ep = begin_seq(P, kCtlCollEpoch);
+  exchange(P, 0, ep);  // every rank's receive buffer is free
+  const size_t nv = c.bytes / 16;
+  size_t lo, hi;
+  blk_range(nv, lo, hi);
+  uint4* dst[kMaxRanks];
+  for (int r = 0; r < P.nranks; ++r) dst[r] = V(c.dst[r]);
+  push_ptrs(P, V(c.src[P.rank]), dst, lo, hi);
+  for (int r = 0; r < P.nranks; ++r) copy_tail(c.dst[r], c.src[P.rank], nv * 16, c.bytes);
+  exchange(P, 1, ep);  // every rank's block landed in my receive buffer
+  end_seq(P, kCtlCollEpoch, kCtlCollDone, ep);
+}
+
+template <DType D>
+__global__ void __launch_bounds__(T) rs_direct_kernel(Peers P, DirectPiece c) {
+  const size_t es = sizeof(uint4) / Elt<D>::N;
+  const uint32_t ep = begin_seq(P, kCtlCollEpoch);
+  exchange(P, 0, ep);  // every rank's send buffer holds its data
+  const size_t nv = c.bytes / 16;
+  size_t lo, hi;
+  blk_range(nv, lo, hi);
+  const uint4* srcs[kMaxRanks];
+  for (int r = 0; r < P.nranks; ++r) srcs[r] = V(c.src[r]);  // rank order: identical sums everywhere
+  reduce_vec<D>(V(c.out), srcs, P.nranks, lo, hi);
+  reduce_tail<D>(c.out, c.src, P.nranks, nv * 16 / es, c.bytes / es);
+  exchange(P, 1, ep);  // every rank is done reading my send buffer
+  end_seq(P, kCtlCollEpoch, kCtlCollDone, ep);
+}
+
+template <DType D>
+__global__ void __launch_bounds__(T) ar_direct_kernel(Peers P, DirectPiece c) {
+  using E = Elt<D>;
+  const uint32_t ep = begin_seq(P, kCtlCollEpoch);
+  exchange(P, 0, ep);
+  const size_t nv = c.bytes / 16;
+  const size_t cv = (nv + P.nranks - 1) / P.nranks;
+  const size_t c0 = min(nv, static_cast<size_t>(P.rank) * cv), c1 = min(nv, c0 + cv);
+  size_t lo, hi;
+  blk_range(c1 - c0, lo, hi);
+  const uint4* srcs[kMaxRanks];
+  uint4* dst[kMaxRanks];
+  for (int r = 0; r < P.nranks; ++r) {
+    srcs[r] = V(c.src[r]) + c0;
+    dst[r] = V(c.dst[r]) + c0;
+  }
+  // chunk `rank` of every send buffer, summed in rank order, into chunk
+  // `rank` of every receive buffer (only this rank reads or writes that
+  // chunk anywhere, so send and receive may alias)
+  for (size_t i = lo + threadIdx.x; i < hi; i += T) {
+    float acc[E::N], f[E::N];
+    E::unpack(srcs[0][i], acc);
+    for (int r = 1; r < P.nranks; ++r) {
+      E::unpack(srcs[r][i], f);
+#pragma unroll
+      for (int k = 0; k < E::N; ++k) acc[k] += f[k];
+    }
+    const uint4 v = E::pack(acc);
+    for (int j = 0; j < P.nranks; ++j) dst[peer_at(P, j)][i] = v;
+  }
+  exchange(P, 1, ep);
+  end_seq(P, kCtlCollEpoch, kCtlCollDone, ep);
+}
+
 __global__ void __launch_bounds__(T) send_kernel(Peers P, const char* buf, size_t bytes, int dst, size_t off,
                                                  size_t slot) {
   const uint32_t n = begin_seq(P, kCtlSendSeq + dst);
@@ -674,6 +759,20 @@ void launch_coll(Op op, const Peers& p, const CollPiece& c, int blocks, void* st
     case Op::AllReduceTwoShot:
       DLNB_REQUIRE(c.bytes % 16 == 0, "xgmi: two-shot piece must be a multiple of 16 B");
       DLNB_XGMI_TYPED(ar2_kernel) break;
+  }
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
+void launch_direct(DirectOp op, const Peers& p, const DirectPiece& c, int blocks, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  DLNB_REQUIRE(blocks >= 1 && blocks <= kMaxBlocks, "xgmi: bad block count " << blocks);
+  DLNB_REQUIRE(p.nranks >= 1 && p.nranks <= kMaxRanks, "xgmi: bad group size " << p.nranks);
+  switch (op) {
+    case DirectOp::AllGather: ag_direct_kernel<<<blocks, T, 0, s>>>(p, c); break;
+    case DirectOp::ReduceScatter: DLNB_XGMI_TYPED(rs_direct_kernel) break;
+    case DirectOp::AllReduce:
+      DLNB_REQUIRE(c.bytes % 16 == 0, "xgmi: direct all-reduce needs a multiple of 16 B");
+      DLNB_XGMI_TYPED(ar_direct_kernel) break;
   }
   DLNB_HIP_CHECK(hipGetLastError());
 }

@@ -69,9 +69,10 @@ hipStream_t hs(Stream& s) { return static_cast<hipStream_t>(s.native()); }
 class XgmiComm : public Communicator {
  public:
   XgmiComm(const std::string& name, const std::vector<int>& members, int my_world_rank, HostGroup& world,
-           size_t capacity, bool p2p) {
+           size_t capacity, bool p2p, int max_ctas) {
     name_ = name;
     members_ = members;
+    world_ = &world;
     size_ = static_cast<int>(members.size());
     rank_ = -1;
     for (int i = 0; i < size_; ++i)
@@ -80,6 +81,10 @@ class XgmiComm : public Communicator {
     DLNB_REQUIRE(size_ <= xgmi::kMaxRanks, "xgmi backend: group " << name << " has " << size_ << " ranks (max "
                                                                  << xgmi::kMaxRanks << ", one node)");
     max_blocks_ = static_cast<int>(std::max<long long>(1, std::min<long long>(xgmi::kMaxBlocks, env_int("DLNB_XGMI_BLOCKS", 256))));
+    // CU budget of this comm lane (runner.cpp): 4 of these blocks fit a CU
+    // beside nothing else, so the lane's kernels never need more CUs than
+    // the budget even when several lanes' kernels are live at once.
+    if (max_ctas > 0) max_blocks_ = std::min(max_blocks_, 4 * max_ctas);
     oneshot_ = static_cast<size_t>(env_int("DLNB_XGMI_ONESHOT_KB", 256)) << 10;
     const size_t cap = std::max<size_t>(capacity, 4096);
     // Collective region per parity: AG/RS/A2A need W slots of a piece, the
@@ -162,8 +167,59 @@ class XgmiComm : public Communicator {
 
   std::string backend_name() const override { return "XGMI"; }
 
+  bool wants_peer_buffers() const override { return size_ > 1; }
+
+  // Collective: every member maps every other member's buffer of this
+  // registration (the k-th registration of each member pairs with the k-th of
+  // the others). The buffer must be an allocation of its own (Device::alloc_peer).
+  void register_buffer(void* p, size_t bytes) override {
+    Reg r;
+    std::memset(&r, 0, sizeof(r));
+    r.local = static_cast<char*>(p);
+    r.bytes = bytes;
+    r.peer[rank_] = r.local;
+    if (size_ > 1) {
+      hipIpcMemHandle_t h;
+      DLNB_HIP_CHECK(hipIpcGetMemHandle(&h, p));
+      std::ostringstream key;
+      key << "xgmi/" << name_ << "/";
+      for (int m : members_) key << m << ",";
+      key << "reg" << regs_.size() << "/";
+      world_->store().set(key.str() + std::to_string(rank_), hex(&h, sizeof(h)) + " " + std::to_string(bytes));
+      for (int q = 0; q < size_; ++q) {
+        if (q == rank_) continue;
+        std::istringstream in(world_->store().get(key.str() + std::to_string(q)));
+        std::string sh;
+        size_t qb = 0;
+        in >> sh >> qb;
+        DLNB_REQUIRE(qb == bytes, "xgmi: registration " << regs_.size() << " of " << name_ << ": rank " << q
+                                                         << " registered " << qb << " B, this rank " << bytes);
+        hipIpcMemHandle_t ph;
+        unhex(sh, &ph, sizeof(ph));
+        void* a = nullptr;
+        DLNB_HIP_CHECK(hipIpcOpenMemHandle(&a, ph, hipIpcMemLazyEnablePeerAccess));
+        r.peer[q] = static_cast<char*>(a);
+        opened_.push_back(a);
+      }
+      // nobody may free the buffer before every member mapped it (freeing is
+      // stream-ordered after the last use anyway; this orders the setup)
+      const std::string done = key.str() + "opened";
+      if (world_->store().add(done, 1) == size_) world_->store().set(done + "/go", "1");
+      world_->store().get(done + "/go");
+    }
+    regs_.push_back(r);
+  }
+
   void all_gather(const void* send, void* recv, size_t send_count, DType t, Stream& s) override {
     const size_t es = dtype_size(t), bytes = send_count * es;
+    size_t off = 0;
+    if (const Reg* r = size_ > 1 && bytes > 0 ? find(recv, bytes * size_, off) : nullptr) {
+      xgmi::DirectPiece c = direct(t, bytes);
+      c.src[rank_] = static_cast<const char*>(send);
+      for (int q = 0; q < size_; ++q) c.dst[q] = r->peer[q] + off + static_cast<size_t>(rank_) * bytes;
+      launch_direct(xgmi::DirectOp::AllGather, c, bytes, s);
+      return;
+    }
     const size_t piece = piece_bytes(region_ / size_, es);
     for (size_t off = 0; off < bytes; off += piece) {
       CollPiece c = base(t);
@@ -178,6 +234,14 @@ class XgmiComm : public Communicator {
 
   void reduce_scatter(const void* send, void* recv, size_t recv_count, DType t, Stream& s) override {
     const size_t es = dtype_size(t), bytes = recv_count * es;
+    size_t off = 0;
+    if (const Reg* r = size_ > 1 && bytes > 0 ? find(send, bytes * size_, off) : nullptr) {
+      xgmi::DirectPiece c = direct(t, bytes);
+      for (int q = 0; q < size_; ++q) c.src[q] = r->peer[q] + off + static_cast<size_t>(rank_) * bytes;
+      c.out = static_cast<char*>(recv);
+      launch_direct(xgmi::DirectOp::ReduceScatter, c, bytes, s);
+      return;
+    }
     const size_t piece = piece_bytes(region_ / size_, es);
     for (size_t off = 0; off < bytes; off += piece) {
       CollPiece c = base(t);
@@ -215,6 +279,21 @@ class XgmiComm : public Communicator {
     }
     // One-shot for latency-bound sizes: every rank pushes the whole buffer.
     const size_t one_max = std::min(oneshot_, piece_bytes(region_ / size_, es));
+    // Registered send and receive buffers, above the one-shot range: rank r
+    // sums chunk r straight out of every peer's send buffer and writes it
+    // into every peer's receive buffer (no window staging).
+    size_t offs = 0, offr = 0;
+    const Reg* rs = bytes > one_max && bytes % 16 == 0 ? find(send, bytes, offs) : nullptr;
+    const Reg* rr = rs ? find(recv, bytes, offr) : nullptr;
+    if (rs && rr) {
+      xgmi::DirectPiece c = direct(t, bytes);
+      for (int q = 0; q < size_; ++q) {
+        c.src[q] = rs->peer[q] + offs;
+        c.dst[q] = rr->peer[q] + offr;
+      }
+      launch_direct(xgmi::DirectOp::AllReduce, c, bytes / size_, s);
+      return;
+    }
     if (bytes <= one_max) {
       CollPiece c = base(t);
       c.bytes = bytes;
@@ -314,6 +393,35 @@ class XgmiComm : public Communicator {
     }
   }
 
+  struct Reg {
+    char* local;
+    size_t bytes;
+    char* peer[xgmi::kMaxRanks];  // each member's buffer of this registration, mapped here
+  };
+  // The registration holding [p, p + n) on this rank (offset returned).
+  const Reg* find(const void* p, size_t n, size_t& off) const {
+    const char* c = static_cast<const char*>(p);
+    for (const Reg& r : regs_)
+      if (c >= r.local && c + n <= r.local + r.bytes) {
+        off = static_cast<size_t>(c - r.local);
+        return &r;
+      }
+    return nullptr;
+  }
+  xgmi::DirectPiece direct(DType t, size_t bytes) const {
+    xgmi::DirectPiece c;
+    std::memset(&c, 0, sizeof(c));
+    c.dtype = t;
+    c.bytes = bytes;
+    return c;
+  }
+  // `work` = bytes each rank moves per block slice group (blocks_for's unit)
+  void launch_direct(xgmi::DirectOp op, const xgmi::DirectPiece& c, size_t work, Stream& s) {
+    xgmi::launch_direct(op, peers_, c, xgmi::blocks_for(work, max_blocks_), hs(s));
+    ++direct_ops_;
+    debug("direct", c.bytes, s);
+  }
+
   // Largest piece (bytes per rank block) fitting `slot_cap`, element aligned.
   static size_t piece_bytes(size_t slot_cap, size_t es) {
     size_t p = (slot_cap / 256) * 256;
@@ -360,6 +468,9 @@ class XgmiComm : public Communicator {
   uint32_t* host_words_ = nullptr;  // [0] abort, [16] error
   std::vector<void*> opened_;
   xgmi::Peers peers_;
+  HostGroup* world_ = nullptr;
+  std::vector<Reg> regs_;
+  size_t direct_ops_ = 0;
   bool in_group_ = false;
   std::vector<P2POp> pending_;
 };
@@ -371,9 +482,9 @@ class XgmiFactory : public CommFactory {
   }
   std::string backend_name() const override { return "XGMI"; }
   std::unique_ptr<Communicator> create(const std::string& name, const std::vector<int>& members,
-                                       size_t capacity_bytes, bool need_p2p, int) override {
+                                       size_t capacity_bytes, bool need_p2p, int max_ctas) override {
     return std::unique_ptr<Communicator>(
-        new XgmiComm(name, members, world_.rank(), world_, capacity_bytes, need_p2p));
+        new XgmiComm(name, members, world_.rank(), world_, capacity_bytes, need_p2p, max_ctas));
   }
 
  private:

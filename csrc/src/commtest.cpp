@@ -11,6 +11,10 @@
 // per collective and size (nccl-tests conventions, SURVEY.md §5 "Metrics"),
 // so RCCL and the xgmi kernels can be compared on one node.
 //
+// --registered: the buffers are peer memory (Device::alloc_peer) registered
+// with the communicator, so backends with zero-copy paths (xgmi) read and
+// write peers' buffers directly instead of staging through their windows.
+//
 // --graph (GPU): check mode captures every collective of a size plus the ring
 // send/recv into one HIP graph and replays it three times with new inputs
 // uploaded between replays (each replay must see fresh sequence numbers);
@@ -70,14 +74,28 @@ struct Tester {
   size_t es;
   int W, me;
   long long failures = 0;
+  // --registered: buffers of the maximum size, registered once (a
+  // registration pairs buffers by order across ranks, so they are not
+  // re-created per size); take(i) hands out buffer i of the pool.
+  std::vector<Buffer> pool;
+  // Buffer i of at least `bytes`: a fresh allocation kept in `keep`, or the
+  // registered pool's buffer i.
+  void* get(std::vector<Buffer>& keep, size_t bytes, size_t i) {
+    if (pool.empty()) {
+      keep.push_back(ctx.dev->alloc(std::max<size_t>(1, bytes)));
+      return keep.back().data();
+    }
+    DLNB_REQUIRE(i < pool.size() && bytes <= pool[i].bytes(), "commtest: registered pool too small");
+    return pool[i].data();
+  }
 
-  void upload(Buffer& b, const std::vector<char>& h) {
-    ctx.dev->copy_async(b.data(), h.data(), h.size(), s);
+  void upload(void* b, const std::vector<char>& h) {
+    ctx.dev->copy_async(b, h.data(), h.size(), s);
     s.synchronize();
   }
-  std::vector<char> download(const Buffer& b, size_t bytes) {
+  std::vector<char> download(const void* b, size_t bytes) {
     std::vector<char> h(bytes);
-    ctx.dev->copy_async(h.data(), b.data(), bytes, s);
+    ctx.dev->copy_async(h.data(), b, bytes, s);
     s.synchronize();
     return h;
   }
@@ -103,30 +121,32 @@ struct Tester {
 
   void check(size_t n) {
     const long long before = failures;
-    Buffer a = ctx.dev->alloc(std::max<size_t>(1, n * W * es)), b = ctx.dev->alloc(std::max<size_t>(1, n * W * es));
+    std::vector<Buffer> keep;
+    void* a = get(keep, n * W * es, 0);
+    void* b = get(keep, n * W * es, 1);
     // all-reduce out of place
     upload(a, pattern(me, 0, n));
-    comm.all_reduce(a.data(), b.data(), n, t, s);
+    comm.all_reduce(a, b, n, t, s);
     auto got = download(b, n * es);
     for (size_t i = 0; i < n; ++i) expect("all_reduce", n, got, i, sum_over_ranks(i));
     // all-reduce in place
-    comm.all_reduce(a.data(), a.data(), n, t, s);
+    comm.all_reduce(a, a, n, t, s);
     got = download(a, n * es);
     for (size_t i = 0; i < n; ++i) expect("all_reduce(in-place)", n, got, i, sum_over_ranks(i));
     // all-gather
     upload(a, pattern(me, 0, n));
-    comm.all_gather(a.data(), b.data(), n, t, s);
+    comm.all_gather(a, b, n, t, s);
     got = download(b, n * W * es);
     for (int r = 0; r < W; ++r)
       for (size_t i = 0; i < n; ++i) expect("all_gather", n, got, r * n + i, val(r, i, t));
     // reduce-scatter: send has W blocks of n, element j = v(me, j)
     upload(a, pattern(me, 0, n * W));
-    comm.reduce_scatter(a.data(), b.data(), n, t, s);
+    comm.reduce_scatter(a, b, n, t, s);
     got = download(b, n * es);
     for (size_t i = 0; i < n; ++i) expect("reduce_scatter", n, got, i, sum_over_ranks(me * n + i));
     // all-to-all: block p of rank r's send = v(r, p*n + i) -> recv block p on me = v(p, me*n + i)
     upload(a, pattern(me, 0, n * W));
-    comm.all_to_all(a.data(), b.data(), n, t, s);
+    comm.all_to_all(a, b, n, t, s);
     got = download(b, n * W * es);
     for (int p = 0; p < W; ++p)
       for (size_t i = 0; i < n; ++i) expect("all_to_all", n, got, p * n + i, val(p, me * n + i, t));
@@ -139,21 +159,22 @@ struct Tester {
   // compared after each.
   void check_graph(Communicator& link, size_t n, int reps) {
     const long long before = failures;
-    const size_t nb = std::max<size_t>(1, n * W * es);
-    Buffer ar_in = ctx.dev->alloc(nb), ar_out = ctx.dev->alloc(nb), ar_ip = ctx.dev->alloc(nb);
-    Buffer ag_out = ctx.dev->alloc(nb), blk_in = ctx.dev->alloc(nb), rs_out = ctx.dev->alloc(nb);
-    Buffer a2a_out = ctx.dev->alloc(nb), p_in = ctx.dev->alloc(nb), p_out = ctx.dev->alloc(nb);
+    const size_t nb = n * W * es;
+    std::vector<Buffer> keep;
+    void *ar_in = get(keep, nb, 0), *ar_out = get(keep, nb, 1), *ar_ip = get(keep, nb, 2);
+    void *ag_out = get(keep, nb, 3), *blk_in = get(keep, nb, 4), *rs_out = get(keep, nb, 5);
+    void *a2a_out = get(keep, nb, 6), *p_in = get(keep, nb, 7), *p_out = get(keep, nb, 8);
     const int next = (me + 1) % W, prev = (me + W - 1) % W;
     auto g = ctx.dev->capture(s, {}, [&] {
-      comm.all_reduce(ar_in.data(), ar_out.data(), n, t, s);
-      comm.all_reduce(ar_ip.data(), ar_ip.data(), n, t, s);
-      comm.all_gather(ar_in.data(), ag_out.data(), n, t, s);
-      comm.reduce_scatter(blk_in.data(), rs_out.data(), n, t, s);
-      comm.all_to_all(blk_in.data(), a2a_out.data(), n, t, s);
+      comm.all_reduce(ar_in, ar_out, n, t, s);
+      comm.all_reduce(ar_ip, ar_ip, n, t, s);
+      comm.all_gather(ar_in, ag_out, n, t, s);
+      comm.reduce_scatter(blk_in, rs_out, n, t, s);
+      comm.all_to_all(blk_in, a2a_out, n, t, s);
       if (W > 1) {
         link.group_start();
-        link.send(p_in.data(), n, t, next, s);
-        link.recv(p_out.data(), n, t, prev, s);
+        link.send(p_in, n, t, next, s);
+        link.recv(p_out, n, t, prev, s);
         link.group_end();
       }
     });
@@ -188,13 +209,15 @@ struct Tester {
 
   void check_p2p(Communicator& link, size_t n) {
     if (W < 2) return;
-    Buffer a = ctx.dev->alloc(std::max<size_t>(1, n * es)), b = ctx.dev->alloc(std::max<size_t>(1, n * es));
+    std::vector<Buffer> keep;
+    void* a = get(keep, n * es, 0);
+    void* b = get(keep, n * es, 1);
     const int next = (me + 1) % W, prev = (me + W - 1) % W;
     for (int rep = 0; rep < 3; ++rep) {  // several messages: exercises the double-buffered slots
       upload(a, pattern(me, static_cast<size_t>(rep), n));
       link.group_start();
-      link.send(a.data(), n, t, next, s);
-      link.recv(b.data(), n, t, prev, s);
+      link.send(a, n, t, next, s);
+      link.recv(b, n, t, prev, s);
       link.group_end();
       auto got = download(b, n * es);
       for (size_t i = 0; i < n; ++i) expect("send/recv", n, got, i, val(prev, rep + i, t));
@@ -206,7 +229,7 @@ struct Tester {
 
 int commtest_main(int argc, char** argv) {
   std::string backend = "auto", devices, dtype = "bf16", sizes_s, json_path;
-  bool bench = false, graph = false;
+  bool bench = false, graph = false, registered = false;
   int iters = 20, warmup = 5, ranks = 2;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -220,6 +243,7 @@ int commtest_main(int argc, char** argv) {
     else if (a == "--sizes") sizes_s = val("--sizes");
     else if (a == "--bench") bench = true;
     else if (a == "--graph") graph = true;
+    else if (a == "--registered") registered = true;
     else if (a == "--iters") iters = std::stoi(val("--iters"));
     else if (a == "--warmup") warmup = std::stoi(val("--warmup"));
     else if (a == "--ranks") ranks = std::stoi(val("--ranks"));
@@ -229,7 +253,8 @@ int commtest_main(int argc, char** argv) {
                    "                     [--dtype bf16|fp16|fp32|fp8_e4m3|fp8_e5m2]\n"
                    "                     [--sizes n1,n2,..] [--bench] [--iters N] [--warmup N] [--graph]\n"
                    "  sizes are elements per rank; check mode verifies every collective exactly\n"
-                   "  --graph: capture the operations into a HIP graph and replay it (rccl, xgmi)\n";
+                   "  --graph: capture the operations into a HIP graph and replay it (rccl, xgmi)\n"
+                   "  --registered: peer-memory buffers registered with the communicator (zero-copy paths)\n";
       return 0;
     } else DLNB_THROW("unknown option " << a);
   }
@@ -258,6 +283,13 @@ int commtest_main(int argc, char** argv) {
   auto link = ctx.comms->create("commtest/link", all, maxn * es, true);
   auto stream = ctx.dev->create_stream(true);
   Tester T{ctx, *comm, *stream, t, es, W, me};
+  const bool reg = registered && comm->wants_peer_buffers();
+  if (reg && !bench) {
+    for (int i = 0; i < 9; ++i) {
+      T.pool.push_back(ctx.dev->alloc_peer(std::max<size_t>(16, maxn * W * es)));
+      comm->register_buffer(T.pool.back().data(), T.pool.back().bytes());
+    }
+  }
   long long total_fail = 0;
   if (!bench) {
     const bool verbose = env_int("DLNB_COMMTEST_VERBOSE", 0) != 0;
@@ -288,6 +320,7 @@ int commtest_main(int argc, char** argv) {
       j["commtest"] = "check";
       j["backend"] = comm->backend_name();
       j["graph"] = graph;
+      j["registered"] = reg;
       j["world_size"] = W;
       j["dtype"] = dtype_name(t);
       Json sz = Json::array();
@@ -298,7 +331,12 @@ int commtest_main(int argc, char** argv) {
       std::cout << j.dump() << std::endl;
     }
   } else {
-    Buffer a = ctx.dev->alloc(maxn * W * es), b = ctx.dev->alloc(maxn * W * es);
+    Buffer a = reg ? ctx.dev->alloc_peer(maxn * W * es) : ctx.dev->alloc(maxn * W * es);
+    Buffer b = reg ? ctx.dev->alloc_peer(maxn * W * es) : ctx.dev->alloc(maxn * W * es);
+    if (reg) {
+      comm->register_buffer(a.data(), a.bytes());
+      comm->register_buffer(b.data(), b.bytes());
+    }
     ctx.dev->fill_random(a.data(), maxn * W, t, 7 + me, *stream);
     stream->synchronize();
     struct K {
@@ -346,6 +384,7 @@ int commtest_main(int argc, char** argv) {
           j["commtest"] = "bench";
           j["backend"] = comm->backend_name();
           j["graph"] = graph;
+          j["registered"] = reg;
           j["op"] = k.name;
           j["world_size"] = W;
           j["dtype"] = dtype_name(t);

@@ -37,8 +37,8 @@ void precise_sleep_us(double us) {
 
 // ------------------------------------------------------------------ Buffer
 
-Buffer::Buffer(Device* dev, size_t bytes) : dev_(dev), bytes_(bytes) {
-  ptr_ = bytes ? dev->raw_alloc(bytes) : nullptr;
+Buffer::Buffer(Device* dev, size_t bytes, bool peer) : dev_(dev), bytes_(bytes) {
+  ptr_ = bytes ? (peer ? dev->raw_alloc_peer(bytes) : dev->raw_alloc(bytes)) : nullptr;
 }
 
 Buffer::~Buffer() {

@@ -118,6 +118,16 @@ class GpuDevice : public Device {
     DLNB_HIP_CHECK(hipStreamSynchronize(nullptr));
     return p;
   }
+  void* raw_alloc_peer(size_t bytes) override {
+    void* p = nullptr;
+    hipError_t e = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached);
+    if (e != hipSuccess)
+      DLNB_THROW("hipExtMallocWithFlags(" << bytes << " B, uncached) failed on device " << idx_ << ": "
+                                          << hipGetErrorString(e));
+    DLNB_HIP_CHECK(hipMemset(p, 0, bytes));
+    DLNB_HIP_CHECK(hipStreamSynchronize(nullptr));
+    return p;
+  }
   void raw_free(void* p, size_t) override { (void)hipFree(p); }
   void fill_random(void* p, size_t count, DType t, uint64_t seed, Stream& s) override {
     kernels::fill_random(p, count, t, seed, s.native());

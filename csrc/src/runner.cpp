@@ -351,7 +351,9 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   // sit in the queue while another communicator's kernel holds the free CUs
   // spinning on a peer that waits for them.
   const int lanes = collective_lanes(opt, ri.world_size);
-  const bool rccl = backend == "rccl" || backend == "mixed";
+  // xgmi kernels are budgeted too: a lane's kernel gets 4 blocks (512
+  // threads, no LDS) per budgeted CU (comm_xgmi.cpp).
+  const bool rccl = backend == "rccl" || backend == "mixed" || backend == "xgmi";
   const bool gemm_compute = ctx.compute->mode() == ComputeMode::Gemm;
   if (rccl) {
     if (opt.rccl_max_ctas >= 0)

@@ -60,16 +60,25 @@ class DataParallel : public Strategy {
     size_t need = static_cast<size_t>(P_) * es_ * 2;
     in_place_ = o.in_place || (dev.kind() == DeviceKind::GPU && need > dev.free_memory() * 0.85);
     if (zero_ == 2) in_place_ = false;  // the reduce-scatter writes a separate shard
+    // Zero-copy (xgmi): gradient buckets and all-reduce outputs in peer
+    // memory, registered with the communicator, so the collectives read and
+    // write peers' buffers directly (see Communicator::register_buffer).
+    const bool peer = comm_->wants_peer_buffers();
+    auto buf = [&](size_t bytes, bool reg) {
+      Buffer b = peer && reg ? dev.alloc_peer(bytes) : dev.alloc(bytes);
+      if (peer && reg) comm_->register_buffer(b.data(), bytes);
+      return b;
+    };
     for (int i = 0; i < nb_; ++i) {
       const uint64_t n = zero_ ? shard_[i] * W_ : sizes_[i];  // padded for ZeRO
-      grads_.push_back(dev.alloc(n * es_));
-      if (!in_place_) sums_.push_back(dev.alloc((zero_ == 2 ? shard_[i] : n) * es_));
+      grads_.push_back(buf(n * es_, true));
+      if (!in_place_) sums_.push_back(buf((zero_ == 2 ? shard_[i] : n) * es_, zero_ != 2));
       ready_.push_back(dev.create_event());
       dev.fill_random(grads_.back().data(), n, ctx.wire, 1000 + i, *compute_);
       if (zero_) {
         pshard_.push_back(dev.alloc(shard_[i] * es_));
         mshard_.push_back(dev.alloc(shard_[i] * es_));
-        pfull_.push_back(dev.alloc(shard_[i] * W_ * es_));
+        pfull_.push_back(buf(shard_[i] * W_ * es_, true));
         dev.fill_random(pshard_.back().data(), shard_[i], ctx.wire, 2000 + i, *compute_);
         opt_done_.push_back(dev.create_event());
       }

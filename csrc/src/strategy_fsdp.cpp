@@ -98,10 +98,16 @@ class Fsdp : public Strategy {
       grads_.push_back(dev.alloc(shard_[u] * es_));
       dev.fill_random(params_.back().data(), shard_[u], ctx.wire, 2000 + u, *compute_);
     }
+    // Zero-copy: with a backend that moves data with its own kernels (xgmi),
+    // peers write their shards straight into the gather buffers and read
+    // their blocks straight out of the full-gradient buffers.
+    const bool ag_peer = ag_comm_->wants_peer_buffers(), rs_peer = rs_comm_->wants_peer_buffers();
     for (int b = 0; b < 2; ++b) {
-      gathered_[b] = dev.alloc(unit_bytes);
-      full_grad_[b] = dev.alloc(unit_bytes);
+      gathered_[b] = ag_peer ? dev.alloc_peer(unit_bytes) : dev.alloc(unit_bytes);
+      full_grad_[b] = rs_peer ? dev.alloc_peer(unit_bytes) : dev.alloc(unit_bytes);
       dev.fill_random(full_grad_[b].data(), max_shard_ * F_, ctx.wire, 3000 + b, *compute_);
+      if (ag_peer) ag_comm_->register_buffer(gathered_[b].data(), unit_bytes);
+      if (rs_peer) rs_comm_->register_buffer(full_grad_[b].data(), unit_bytes);
     }
     auto mk = [&](std::vector<std::unique_ptr<Event>>& v) {
       for (int u = 0; u < U_; ++u) v.push_back(dev.create_event());

@@ -5,6 +5,7 @@
 # plus the local D2D copy roofline. Each memory type is first checked exactly
 # (the bench only runs if it passes). Output: gpurun_out/xgmi_sweep.jsonl
 # usage: scripts/xgmi_sweep.sh [W] [mem types] [block caps] [sizes]
+# EXTRA="--registered" runs the zero-copy paths (registered peer buffers).
 set -u
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0 DLNB_XGMI_TIMEOUT_S=20
@@ -28,10 +29,10 @@ for l in sys.stdin:
 }
 for mem in $MEMS; do
   export DLNB_XGMI_MEM=$mem
-  DLNB_XGMI_REGION_MB=1 DLNB_XGMI_P2P_MB=1 run "{'mem':'$mem','W':$W,'check':'eager'}" 120 --sizes 1,100,4097,300007,1048583
-  run "{'mem':'$mem','W':$W,'check':'graph'}" 120 --graph --sizes 1,4097,1048583
+  DLNB_XGMI_REGION_MB=1 DLNB_XGMI_P2P_MB=1 run "{'mem':'$mem','W':$W,'check':'eager'}" 120 --sizes 1,100,4097,300000,1048583 ${EXTRA:-}
+  run "{'mem':'$mem','W':$W,'check':'graph'}" 120 --graph --sizes 1,4097,1048583 ${EXTRA:-}
   if ! tail -2 $OUT | grep -q '"ok": true'; then echo "$mem: check failed, no bench" >> gpurun_out/xgmi_sweep_steps.log; continue; fi
   for b in $BLOCKS; do
-    DLNB_XGMI_BLOCKS=$b run "{'mem':'$mem','W':$W,'blocks':$b}" 200 --bench --graph --iters 10 --warmup 3 --sizes $SIZES
+    DLNB_XGMI_BLOCKS=$b run "{'mem':'$mem','W':$W,'blocks':$b,'extra':'${EXTRA:-}'}" 200 --bench --graph --iters 10 --warmup 3 --sizes $SIZES ${EXTRA:-}
   done
 done

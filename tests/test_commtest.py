@@ -98,6 +98,22 @@ def test_xgmi_graph_replay_exact(w, dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("w,dtype,graph", [(2, "bf16", False), (4, "bf16", False), (3, "fp32", False),
+                                           (2, "fp8_e4m3", False), (2, "bf16", True), (4, "fp16", True)])
+def test_xgmi_registered_zero_copy_exact(w, dtype, graph):
+    """--registered: peer-memory buffers registered with the communicator, so all-gather writes straight
+    into every rank's receive buffer, reduce-scatter reads straight out of every rank's send buffer and the
+    all-reduce (16-B multiples above the one-shot range) does both - no window staging. Exact, eager and
+    graph-replayed; the odd sizes take the staged paths on the same buffers."""
+    _need_gpu()
+    devs = ",".join(["0"] * w)
+    extra = ["--graph"] if graph else []
+    out = commtest(w, "--backend", "xgmi", "-d", devs, "--dtype", dtype, "--registered", *extra,
+                   "--sizes", "1,100,4097,65536,300000,1048583,2097152", env_extra=SMALL_WINDOWS)
+    assert out[0]["ok"] and out[0]["registered"] is True, out
+
+
+@pytest.mark.gpu
 def test_rccl_graph_replay_exact():
     _need_gpu()
     out = commtest(1, "--backend", "rccl", "--graph", "--sizes", "1,4097")
