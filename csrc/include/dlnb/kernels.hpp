@@ -53,7 +53,7 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
              void* stream, int waves = 0);
 bool gemm_8phase_shape_ok(int M, int N, int K, DType in_t);
 void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
-                    void* stream, bool balanced = false);
+                    void* stream, bool balanced = false, bool uniform = false);
 void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
                              uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
                              uint64_t* tstart);

@@ -90,7 +90,8 @@ struct CollPiece {
 //   ReduceScatter: src[r] = rank r's send buffer at this rank's block; out = receive buffer
 //   AllReduce:     src[r] = rank r's send buffer, dst[r] = rank r's receive buffer (may alias);
 //                  rank me sums chunk me of every src and writes it into every dst
-enum class DirectOp : int { AllGather, ReduceScatter, AllReduce };
+//   AllToAll:      src[me] = send (W blocks); dst[r] = rank r's receive buffer at this rank's block
+enum class DirectOp : int { AllGather, ReduceScatter, AllReduce, AllToAll };
 struct DirectPiece {
   const char* src[kMaxRanks];
   char* dst[kMaxRanks];

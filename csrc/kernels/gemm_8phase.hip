@@ -136,14 +136,16 @@ struct Ctx {
   size_t lda, ldb;  // bytes
   char* smem;
   int w, lane, wr, wc, r16, h;
+  int last_kt;  // uniform K-loop: staging of K-tiles past the last one re-reads it (never consumed)
 };
 
 // Where half-tile `slot` of K-tile t comes from / goes to.
 __device__ __forceinline__ void stage(const Ctx& c, int t, int slot) {
+  const int tk = min(t, c.last_kt);  // == t except for the uniform loop's two overrun K-tiles
   const bool isA = slot == kA0 || slot == kA1;
   const int hi = slot == kA1 || slot == kB1;
   const char* src = (isA ? c.Ab + static_cast<size_t>(hi) * 128 * c.lda : c.Bb + static_cast<size_t>(hi) * 128 * c.ldb) +
-                    static_cast<size_t>(t) * kRB;
+                    static_cast<size_t>(tk) * kRB;
   stage_half(src, isA ? c.lda : c.ldb, c.smem + (t & 1) * kBuf + slot * kHalf, c.w, c.lane);
 }
 
@@ -244,7 +246,7 @@ __device__ __forceinline__ bool tail(const Ctx& c, int v, Frags<FP8>& f, f32x4 (
 
 // One 256 x 256 tile of C. Returns false if the deadline stopped it (no
 // store; every staged load has been waited for).
-template <bool FP8, bool DL, bool BAL>
+template <bool FP8, bool DL, bool BAL, bool UNI = false>
 __device__ __forceinline__ bool tile(Ctx& c, const char* __restrict__ A, const char* __restrict__ B,
                                      __bf16* __restrict__ C, int M, int N, int K, int ldc, int b, const Deadline& d) {
   const int nt_m = M / kT, nt_n = N / kT;
@@ -258,6 +260,7 @@ __device__ __forceinline__ bool tile(Ctx& c, const char* __restrict__ A, const c
   c.Ab = A + static_cast<size_t>(tm) * kT * c.lda;
   c.Bb = B + static_cast<size_t>(tn) * kT * c.ldb;
   const int nk = (K * esz) / kRB;  // >= 2 (host checks)
+  c.last_kt = UNI ? nk - 1 : 1 << 30;
 
   f32x4 acc[2][2][4][2];
 #pragma unroll
@@ -285,7 +288,20 @@ __device__ __forceinline__ bool tile(Ctx& c, const char* __restrict__ A, const c
 
   bool stop = false;
   int v = 0;
-  if constexpr (!BAL) {
+  if constexpr (UNI) {
+    // One K-tile body for the whole loop (no tail instantiations: less
+    // register pressure): the last two K-tiles stage two K-tiles past the
+    // end (clamped to the last one: L2 hits, never read), drained below.
+    if constexpr (!BAL) {
+      for (; v < nk && !stop; ++v) stop = ktile<FP8, DL, false, 0, 8, 8, 8, 8, true, true>(c, v, f, acc, d);
+    } else {
+      for (; v < nk && !stop; v += 2) {
+        stop = ktile<FP8, DL, true, 0, 8, 8, 8, 8, true, true>(c, v, f, acc, d);
+        if (!stop) stop = ktile<FP8, DL, true, 1, 8, 8, 8, 8, true, true>(c, v + 1, f, acc, d);
+      }
+    }
+    wait_vm<0>();
+  } else if constexpr (!BAL) {
     for (; v < nk - 2 && !stop; ++v) stop = ktile<FP8, DL, false, 0, 8, 8, 8, 8, true, true>(c, v, f, acc, d);
     if (!stop) stop = tail<FP8, DL, false, 0>(c, v, f, acc, d);
   } else {
@@ -330,7 +346,7 @@ __device__ __forceinline__ bool tile(Ctx& c, const char* __restrict__ A, const c
 // compute with the contract of gemm_tn_256_kernel's deadline mode
 // (kernels.hip): grid <= resident blocks walks the tiles round-robin and
 // stops min(ticks, slice_end) after t0, agreed per epoch through *slot.
-template <bool FP8, bool DL, bool BAL = false>
+template <bool FP8, bool DL, bool BAL = false, bool UNI = false>
 __global__ void __launch_bounds__(512, 1)
     gemm_8phase_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
                        int K, int lda, int ldb, int ldc, uint64_t* __restrict__ slot, uint32_t epoch, uint64_t ticks,
@@ -351,7 +367,7 @@ __global__ void __launch_bounds__(512, 1)
   const int T = (M / kT) * (N / kT);
   Deadline d{0, ticks, slice_end, (lds_flag_t*)(smem + 2 * kBuf), tid};
   if constexpr (!DL) {
-    tile<FP8, false, BAL>(c, A, B, C, M, N, K, ldc, xcd_remap(blockIdx.x, T), d);
+    tile<FP8, false, BAL, UNI>(c, A, B, C, M, N, K, ldc, xcd_remap(blockIdx.x, T), d);
   } else {
     constexpr uint64_t kMask48 = (1ull << 48) - 1;
     if (tid == 0) {
@@ -369,7 +385,8 @@ __global__ void __launch_bounds__(512, 1)
       d.t0 = cur & kMask48;  // only thread 0 reads the clock
     }
     for (int round = 0;; ++round)
-      if (!tile<FP8, true, BAL>(c, A, B, C, M, N, K, ldc, xcd_remap((blockIdx.x + round * gridDim.x) % T, T), d)) return;
+      if (!tile<FP8, true, BAL, UNI>(c, A, B, C, M, N, K, ldc, xcd_remap((blockIdx.x + round * gridDim.x) % T, T), d))
+        return;
   }
 }
 
@@ -614,7 +631,7 @@ bool gemm_8phase_shape_ok(int M, int N, int K, DType in_t) {
 }
 
 void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
-                    void* stream, bool balanced) {
+                    void* stream, bool balanced, bool uniform) {
   DLNB_REQUIRE(gemm_8phase_shape_ok(M, N, K, in_t), "gemm 8-phase: unsupported shape M=" << M << " N=" << N << " K=" << K);
   const int tiles = (M / kT) * (N / kT);
   hipStream_t st = static_cast<hipStream_t>(stream);
@@ -623,6 +640,26 @@ void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, 
   auto* cc = static_cast<__bf16*>(C);
   // the balanced schedule is unrolled by two K-tiles: even K-tile counts only
   balanced = balanced && ((static_cast<size_t>(K) * dtype_size(in_t) / kRB) % 2 == 0);
+  if (uniform) {
+    if (in_t == DType::FP8_E4M3) {
+      if (balanced)
+        hipLaunchKernelGGL((gemm_8phase_kernel<true, false, true, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb,
+                           ldc, nullptr, 0u, 0ull, 0ull, nullptr);
+      else
+        hipLaunchKernelGGL((gemm_8phase_kernel<true, false, false, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda,
+                           ldb, ldc, nullptr, 0u, 0ull, 0ull, nullptr);
+    } else {
+      if (balanced)
+        hipLaunchKernelGGL((gemm_8phase_kernel<false, false, true, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda,
+                           ldb, ldc, nullptr, 0u, 0ull, 0ull, nullptr);
+      else
+        hipLaunchKernelGGL((gemm_8phase_kernel<false, false, false, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda,
+                           ldb, ldc, nullptr, 0u, 0ull, 0ull, nullptr);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) DLNB_THROW("gemm 8-phase launch failed: " << hipGetErrorString(e));
+    return;
+  }
   if (in_t == DType::FP8_E4M3) {
     if (balanced)
       hipLaunchKernelGGL((gemm_8phase_kernel<true, false, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc,
@@ -666,12 +703,19 @@ void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N
     else
       hipLaunchKernelGGL((gemm_8phase_stream_kernel<true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
                          ticks, slice_end, tstart);
-  } else if (in_t == DType::BF16)
+  } else if (in_t == DType::BF16) {
     hipLaunchKernelGGL((gemm_8phase_kernel<false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
                        ticks, slice_end, tstart);
-  else
+  } else if (env_int("DLNB_GEMM_FP8_DL_UNIFORM", 1) != 0) {
+    // fp8: one uniform K-tile body (the tail K-tiles stage past the end
+    // instead of their own instantiations): 254 VGPRs, no spills (the
+    // per-tile fp8 deadline kernel with a tail carries 35 spilled VGPRs)
+    hipLaunchKernelGGL((gemm_8phase_kernel<true, true, false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot,
+                       epoch, ticks, slice_end, tstart);
+  } else {
     hipLaunchKernelGGL((gemm_8phase_kernel<true, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
                        ticks, slice_end, tstart);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 8-phase deadline launch failed: " << hipGetErrorString(e));
 }

@@ -633,13 +633,18 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
                    reinterpret_cast<uintptr_t>(C) % 8 == 0,
                "gemm_tn: misaligned base pointers");
   const int tiles = (M / kTile) * (N / kTile);
-  DLNB_REQUIRE(waves == 0 || waves == 1 || waves == 2 || waves == 3 || waves == 4 || waves == 6 || waves == 8,
-               "gemm_tn: variant must be 0, 1, 2, 3, 4, 6 or 8");
-  if (waves == 0 && gemm_8phase_enabled()) waves = in_t == DType::BF16 ? 6 : 3;  // bf16: balanced reads
-  if ((waves == 3 || waves == 6) && gemm_8phase_shape_ok(M, N, K, in_t)) {  // (one K-tile: falls back)
-    gemm_tn_8phase(A, B, C, M, N, K, lda, ldb, ldc, in_t, stream, waves == 6);
+  DLNB_REQUIRE(waves == 0 || waves == 1 || waves == 2 || waves == 3 || waves == 4 || waves == 6 || waves == 7 ||
+                   waves == 8 || waves == 9,
+               "gemm_tn: variant must be 0, 1, 2, 3, 4, 6, 7, 8 or 9");
+  // bf16: balanced reads; fp8: balanced reads + one uniform K-tile body (no
+  // spills: +7-12 % over the plain 8-phase fp8 kernel, profiles/gemm_bench_r2.md)
+  if (waves == 0 && gemm_8phase_enabled()) waves = in_t == DType::BF16 ? 6 : 7;
+  // 7 / 9: the 8-phase kernels (balanced / plain) with one uniform K-tile body
+  if ((waves == 3 || waves == 6 || waves == 7 || waves == 9) && gemm_8phase_shape_ok(M, N, K, in_t)) {
+    gemm_tn_8phase(A, B, C, M, N, K, lda, ldb, ldc, in_t, stream, waves == 6 || waves == 7, waves == 7 || waves == 9);
     return;
   }
+  if (waves == 7 || waves == 9) waves = 3;
   if (waves == 0) {
     // bf16: the software-pipelined 8-wave body (+3-6 % over the plain one,
     // profiles/gemm_bench_r1.md); fp8: the plain MX body.

@@ -525,6 +525,23 @@ __global__ void __launch_bounds__(T) ag_direct_kernel(Peers P, DirectPiece c) {
   end_seq(P, kCtlCollEpoch, kCtlCollDone, ep);
 }
 
+__global__ void __launch_bounds__(T) a2a_direct_kernel(Peers P, DirectPiece c) {
+  const uint32_t ep = begin_seq(P, kCtlCollEpoch);
+  exchange(P, 0, ep);  // every rank's receive buffer is free
+  const size_t nv = c.bytes / 16;
+  size_t lo, hi;
+  blk_range(nv, lo, hi);
+  // block j of my send -> slot `rank` of rank j's receive buffer (own first, then staggered)
+  for (int j = 0; j < P.nranks; ++j) {
+    const int r = peer_at(P, j);
+    const char* s = c.src[P.rank] + static_cast<size_t>(r) * c.bytes;
+    copy_vec(V(c.dst[r]), V(s), lo, hi);
+    copy_tail(c.dst[r], s, nv * 16, c.bytes);
+  }
+  exchange(P, 1, ep);  // every rank's block for me landed
+  end_seq(P, kCtlCollEpoch, kCtlCollDone, ep);
+}
+
 template <DType D>
 __global__ void __launch_bounds__(T) rs_direct_kernel(Peers P, DirectPiece c) {
   const size_t es = sizeof(uint4) / Elt<D>::N;
@@ -769,6 +786,7 @@ void launch_direct(DirectOp op, const Peers& p, const DirectPiece& c, int blocks
   DLNB_REQUIRE(p.nranks >= 1 && p.nranks <= kMaxRanks, "xgmi: bad group size " << p.nranks);
   switch (op) {
     case DirectOp::AllGather: ag_direct_kernel<<<blocks, T, 0, s>>>(p, c); break;
+    case DirectOp::AllToAll: a2a_direct_kernel<<<blocks, T, 0, s>>>(p, c); break;
     case DirectOp::ReduceScatter: DLNB_XGMI_TYPED(rs_direct_kernel) break;
     case DirectOp::AllReduce:
       DLNB_REQUIRE(c.bytes % 16 == 0, "xgmi: direct all-reduce needs a multiple of 16 B");

@@ -257,6 +257,14 @@ class XgmiComm : public Communicator {
   void all_to_all(const void* send, void* recv, size_t count, DType t, Stream& s) override {
     DLNB_REQUIRE(send != recv, "xgmi all_to_all is out-of-place only");
     const size_t es = dtype_size(t), bytes = count * es;
+    size_t off = 0;
+    if (const Reg* r = size_ > 1 && bytes > 0 ? find(recv, bytes * size_, off) : nullptr) {
+      xgmi::DirectPiece c = direct(t, bytes);
+      c.src[rank_] = static_cast<const char*>(send);
+      for (int q = 0; q < size_; ++q) c.dst[q] = r->peer[q] + off + static_cast<size_t>(rank_) * bytes;
+      launch_direct(xgmi::DirectOp::AllToAll, c, bytes, s);
+      return;
+    }
     const size_t piece = piece_bytes(region_ / size_, es);
     for (size_t off = 0; off < bytes; off += piece) {
       CollPiece c = base(t);

@@ -260,9 +260,16 @@ class Pipeline : public Strategy {
         dev.fill_random(act_out_[b].data(), pipe_, ctx.wire, 4100 + b, *compute_);
       }
     }
-    grad_ = dev.alloc(dp_ar_ * es_);
+    // Zero-copy (xgmi): the DP gradient (and its all-reduce output) and the
+    // expert receive buffer are peer memory registered with their groups.
+    const bool dp_peer = dp_comm_->wants_peer_buffers();
+    grad_ = dp_peer ? dev.alloc_peer(dp_ar_ * es_) : dev.alloc(dp_ar_ * es_);
     dev.fill_random(grad_.data(), dp_ar_, ctx.wire, 4200, *compute_);
-    if (!o.in_place) sum_grad_ = dev.alloc(dp_ar_ * es_);
+    if (!o.in_place) sum_grad_ = dp_peer ? dev.alloc_peer(dp_ar_ * es_) : dev.alloc(dp_ar_ * es_);
+    if (dp_peer) {
+      dp_comm_->register_buffer(grad_.data(), grad_.bytes());
+      if (!o.in_place) dp_comm_->register_buffer(sum_grad_.data(), sum_grad_.bytes());
+    }
     if (has_tp_) {
       tp_buf_ = dev.alloc(tp_shard_ * T_ * es_);
       tp_res_ = dev.alloc(tp_shard_ * T_ * es_);
@@ -272,7 +279,9 @@ class Pipeline : public Strategy {
       // skew: the hot rank receives E_ * skew_counts_[0] in a dispatch
       const uint64_t n = skew_counts_.empty() ? a2a_ * E_ : std::max<uint64_t>(a2a_ * E_, skew_counts_[0] * E_);
       ep_send_ = dev.alloc(n * es_);
-      ep_recv_ = dev.alloc(n * es_);
+      const bool ep_peer = ep_comm_->wants_peer_buffers();
+      ep_recv_ = ep_peer ? dev.alloc_peer(n * es_) : dev.alloc(n * es_);
+      if (ep_peer) ep_comm_->register_buffer(ep_recv_.data(), ep_recv_.bytes());
       dev.fill_random(ep_send_.data(), a2a_ * E_, ctx.wire, 4400, *compute_);
       if (ep_overlap_) {
         // The half-microbatch all-to-alls share the DP lane instead of a

@@ -32,5 +32,5 @@ for d in sorted(glob.glob(os.path.join(root, "*_s[0-9]"))):
         rows.append((fl / t / 1e12, gui / 1e9, busy))
     if rows:
         tf = sorted(r[0] for r in rows)
-        print(f"| {dt} | {shape} | { {'s0': 'per-tile', 's1': 'stream'}.get(s, 'probe ' + s)} | {tf[0]:.0f}-{tf[-1]:.0f} | "
+        print(f"| {dt} | {shape} | { {'s0': 'per-tile', 's1': 'stream', 's2': 'per-tile uniform'}.get(s, 'probe ' + s)} | {tf[0]:.0f}-{tf[-1]:.0f} | "
               f"{sum(r[1] for r in rows) / len(rows):.2f} | {sum(r[2] for r in rows) / len(rows):.3f} |")
