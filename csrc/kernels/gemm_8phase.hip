@@ -687,15 +687,17 @@ void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N
   auto* a = static_cast<const char*>(A);
   auto* b = static_cast<const char*>(B);
   auto* cc = static_cast<__bf16*>(C);
-  // Short K (<= 16 K-tiles, e.g. ViT-H's FFN at fp8: 10) -> the streaming
-  // kernel: the per-tile pipeline fill / drain is a large share of a tile
-  // there (+15 % TF/s at 8192 x 5120 x 1280 fp8). Long K -> the per-tile loop:
-  // the streaming kernel's per-phase branch on the wait count costs more than
-  // the fill it hides (-8..-14 % at K = 4096; profiles/gemm_deadline_stream_r2.md).
-  // DLNB_GEMM_STREAM=0|1 forces either.
+  // fp8: the per-tile loop with one uniform K-tile body (no spills): fastest
+  // at every measured K (+7 % at K = 4096, +24 % at the ViT-H FFN's K = 1280
+  // over the loop with tail instantiations, +8 % over the streaming kernel).
+  // bf16, short K (<= 16 K-tiles): the streaming kernel, whose per-tile
+  // pipeline fill / drain savings outweigh its per-phase wait-count branch
+  // only there; long K: the per-tile loop (profiles/gemm_deadline_stream_r2.md).
+  // DLNB_GEMM_STREAM=0|1 and DLNB_GEMM_FP8_DL_UNIFORM=0|1 force a choice.
   const int nk = static_cast<int>(static_cast<size_t>(K) * dtype_size(in_t) / kRB);
   const long long force = env_int("DLNB_GEMM_STREAM", -1);
-  const bool stream_on = force >= 0 ? force != 0 : nk <= 16;
+  const bool fp8_uniform = in_t != DType::BF16 && env_int("DLNB_GEMM_FP8_DL_UNIFORM", 1) != 0;
+  const bool stream_on = force >= 0 ? force != 0 : (!fp8_uniform && nk <= 16);
   if (stream_on) {
     if (in_t == DType::BF16)
       hipLaunchKernelGGL((gemm_8phase_stream_kernel<false>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
@@ -706,7 +708,7 @@ void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N
   } else if (in_t == DType::BF16) {
     hipLaunchKernelGGL((gemm_8phase_kernel<false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
                        ticks, slice_end, tstart);
-  } else if (env_int("DLNB_GEMM_FP8_DL_UNIFORM", 1) != 0) {
+  } else if (fp8_uniform) {
     // fp8: one uniform K-tile body (the tail K-tiles stage past the end
     // instead of their own instantiations): 254 VGPRs, no spills (the
     // per-tile fp8 deadline kernel with a tail carries 35 spilled VGPRs)
