@@ -112,12 +112,18 @@ class ContextParallel : public Strategy {
         }
       } else {
         a2a_send_ = dev.alloc(C_ * std::max(qkv_peer_, out_peer_) * es_);
-        a2a_recv_ = dev.alloc(C_ * std::max(qkv_peer_, out_peer_) * es_);
+        // zero-copy (xgmi): peers write their blocks straight into a2a_recv_
+        const bool peer = cp_comm_->wants_peer_buffers();
+        const size_t rb = C_ * std::max(qkv_peer_, out_peer_) * es_;
+        a2a_recv_ = peer ? dev.alloc_peer(rb) : dev.alloc(rb);
+        if (peer) cp_comm_->register_buffer(a2a_recv_.data(), rb);
         dev.fill_random(a2a_send_.data(), C_ * std::max(qkv_peer_, out_peer_), ctx.wire, 5100, *compute_);
       }
     }
+    const bool dp_peer = dp_comm_->wants_peer_buffers();  // in-place bucket all-reduces, zero-copy on xgmi
     for (int b = 0; b < nbk_; ++b) {
-      grads_.push_back(dev.alloc(bucket_[b] * es_));
+      grads_.push_back(dp_peer ? dev.alloc_peer(bucket_[b] * es_) : dev.alloc(bucket_[b] * es_));
+      if (dp_peer) dp_comm_->register_buffer(grads_.back().data(), bucket_[b] * es_);
       dev.fill_random(grads_.back().data(), bucket_[b], ctx.wire, 5200 + b, *compute_);
       bucket_ready_.push_back(dev.create_event());
     }

@@ -305,6 +305,10 @@ def main(argv=None) -> int:
     ap.add_argument("--eta", type=float, default=0.75, help="achieved fraction of the link bandwidth")
     ap.add_argument("--alpha-us", type=float, default=15.0, help="latency per collective")
     ap.add_argument("--algo", default="direct", choices=["direct", "ring"])
+    ap.add_argument("--buffers", default="rccl", choices=["rccl", "staged", "registered"],
+                    help="--predict: add the local HBM traffic of the xgmi kernels' window (staged) or "
+                         "zero-copy (registered) data path")
+    ap.add_argument("--hbm-gbps", type=float, default=5000.0, help="--predict: local HBM rate of those kernels")
     a = ap.parse_args(argv)
     st = load_stats(os.path.join(a.base, "model_stats", a.model + ".txt"))
     if a.strategy == "dp":
@@ -329,7 +333,7 @@ def main(argv=None) -> int:
     doc = pl.to_json()
     if a.predict and a.strategy in ("dp", "fsdp"):
         from . import xgmi_model as xm
-        lm = xm.LinkModel(a.link_gbps, a.eta, a.alpha_us)
+        lm = xm.LinkModel(a.link_gbps, a.eta, a.alpha_us, buffers=a.buffers, hbm_gbps=a.hbm_gbps)
         pred = {}
         for w in (1, 2, 4, 8):
             if a.strategy == "dp":
@@ -338,7 +342,8 @@ def main(argv=None) -> int:
                 F = w if a.params[1] == a.world else a.params[1]  # fully sharded runs shard over the job
                 pred[str(w)] = xm.predict_fsdp(st, w, a.params[0], F, lm, a.wire, a.algo)
         doc["xgmi_prediction"] = {"model": {"link_gbps": a.link_gbps, "eta": a.eta, "alpha_us": a.alpha_us,
-                                            "algo": a.algo}, "by_world": pred}
+                                            "algo": a.algo, "buffers": a.buffers, "hbm_gbps": a.hbm_gbps},
+                                  "by_world": pred}
         if a.strategy == "dp":
             doc["xgmi_prediction"]["suggested_buckets_at_world"] = xm.suggest_buckets(st, a.world, lm, a.wire)
     print(json.dumps(doc, indent=1))

@@ -17,6 +17,13 @@ collective achieves, alpha the per-collective latency. The defaults (153 GB/s,
 0.75, 15 us) are assumptions to be replaced by `dlnb commtest --bench`
 numbers from an 8-GPU node (--link-gbps / --eta / --alpha-us).
 
+With our own kernels (`buffers` = "staged" for the xgmi backend's window
+path, "registered" for its zero-copy path) a collective also moves local HBM
+bytes, which can bound it before the links do: the per-rank traffic of each
+kernel's data path (scripts/xgmi_roofline.py, measured at 81-104 % of the
+D2D copy rate on one MI355X: profiles/xgmi_roofline_r2.md) over `hbm_gbps`,
+and t = max(link time, HBM time) + alpha. "rccl" (default) is links only.
+
 `predict_dp` / `predict_fsdp` replay the strategies' overlap schedules
 (csrc/src/strategy_dp.cpp, strategy_fsdp.cpp: one in-order comm lane, a
 collective waits for the compute that produced its data) with these times
@@ -40,6 +47,19 @@ class LinkModel:
     eta: float = 0.75
     alpha_us: float = 15.0
     gpus_per_node: int = 8
+    buffers: str = "rccl"      # rccl | staged | registered (the xgmi kernels' data paths)
+    hbm_gbps: float = 5000.0   # local HBM rate the kernels' copies reach (D2D copies: ~6 TB/s)
+
+    def local_bytes(self, op: str, nbytes: float, n: int) -> float:
+        """Local HBM bytes one rank's xgmi kernel moves (0 for rccl)."""
+        if self.buffers == "rccl" or n <= 1:
+            return 0.0
+        blk = nbytes / n  # per-rank block of the gathered / reduced buffer
+        if self.buffers == "registered":
+            return {"allgather": blk * (n + 1), "reduce_scatter": blk * (n + 1), "alltoall": blk * (4 * n - 2),
+                    "allreduce": 2.0 * nbytes, "sendrecv": 2.0 * nbytes}[op]
+        return {"allgather": blk * (3 * n - 1), "reduce_scatter": blk * (3 * n - 1), "alltoall": blk * (4 * n - 2),
+                "allreduce": nbytes * (6 * n - 4) / n, "sendrecv": 2.0 * nbytes}[op]
 
     def _bw(self) -> float:  # bytes per microsecond on one link
         return self.link_gbps * 1e3 * self.eta
@@ -53,15 +73,16 @@ class LinkModel:
         if n > self.gpus_per_node:
             raise ValueError("the model covers one node (at most %d GPUs per group)" % self.gpus_per_node)
         bw = self._bw()
+        if op not in ("sendrecv", "allreduce", "allgather", "reduce_scatter", "alltoall"):
+            raise ValueError(f"unknown op {op!r}")
+        hbm = self.local_bytes(op, nbytes, n) / (self.hbm_gbps * 1e3)  # us
         if op == "sendrecv":
-            return nbytes / bw + self.alpha_us
+            return max(nbytes / bw, hbm) + self.alpha_us
         per_link = nbytes / n if algo == "direct" else nbytes * (n - 1) / n
         steps = 1 if algo == "direct" else (n - 1)
         if op == "allreduce":
-            return 2 * per_link / bw + 2 * steps * self.alpha_us
-        if op in ("allgather", "reduce_scatter", "alltoall"):
-            return per_link / bw + steps * self.alpha_us
-        raise ValueError(f"unknown op {op!r}")
+            return max(2 * per_link / bw, hbm) + 2 * steps * self.alpha_us
+        return max(per_link / bw, hbm) + steps * self.alpha_us
 
 
 def predict_dp(st: ModelStats, world: int, nb: int, model: LinkModel, wire: str = "bf16",

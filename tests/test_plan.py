@@ -190,6 +190,23 @@ def test_xgmi_model_collective_times():
         m.coll_us("allgather", S, 16)
 
 
+def test_xgmi_model_local_hbm_term():
+    """Own-kernel data paths: staged (window) kernels move n(3W-1) local bytes per all-gather block, registered
+    (zero-copy) ones n(W+1); when that exceeds the link time it bounds the collective."""
+    from dlnetbench_amd.parallel.xgmi_model import LinkModel
+    S = 8e9  # gathered bytes: 1 GB per rank block at n = 8
+    links = LinkModel(link_gbps=1000.0, eta=1.0, alpha_us=0.0)  # fast links: HBM-bound below
+    st = LinkModel(link_gbps=1000.0, eta=1.0, alpha_us=0.0, buffers="staged", hbm_gbps=5000.0)
+    rg = LinkModel(link_gbps=1000.0, eta=1.0, alpha_us=0.0, buffers="registered", hbm_gbps=5000.0)
+    assert links.coll_us("allgather", S, 8) == pytest.approx(1e9 / 1e6)        # 1 GB per link at 1 TB/s
+    assert st.local_bytes("allgather", S, 8) == pytest.approx(1e9 * 23)
+    assert st.coll_us("allgather", S, 8) == pytest.approx(23e9 / 5e6)          # HBM-bound: 4.6 ms
+    assert rg.coll_us("allgather", S, 8) == pytest.approx(9e9 / 5e6)           # 1.8 ms
+    assert rg.coll_us("allreduce", 1e9, 8) == pytest.approx(2e9 / 5e6)
+    slow = LinkModel(link_gbps=10.0, eta=1.0, alpha_us=0.0, buffers="registered")
+    assert slow.coll_us("allgather", S, 8) == pytest.approx(1e9 / 1e4)         # link-bound again
+
+
 def test_xgmi_model_predictions(root):
     from dlnetbench_amd.parallel import xgmi_model as xm
     st = load_stats(os.path.join(root, "model_stats", "llama3_8b_16_bfloat16.txt"))
