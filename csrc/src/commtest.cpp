@@ -341,20 +341,34 @@ int commtest_main(int argc, char** argv) {
     stream->synchronize();
     struct K {
       const char* name;
-      CollKind kind;
+      CollKind kind;  // bus-bandwidth accounting
+      bool copy;      // the local D2D copy roofline, not a collective
     };
     // "copy": one device-to-device copy of the rank's n elements (the local
-    // HBM roofline the collectives' kernels are compared against).
-    const K kinds[] = {{"all_reduce", CollKind::AllReduce},
-                       {"all_gather", CollKind::AllGather},
-                       {"reduce_scatter", CollKind::ReduceScatter},
-                       {"all_to_all", CollKind::AllToAll},
-                       {"copy", CollKind::SendRecv}};
+    // HBM roofline the collectives' kernels are compared against);
+    // "sendrecv": a ring exchange on the point-to-point communicator (send n
+    // to the next rank, receive n from the previous one: nccl-tests sendrecv).
+    std::vector<K> kinds = {{"all_reduce", CollKind::AllReduce, false},
+                            {"all_gather", CollKind::AllGather, false},
+                            {"reduce_scatter", CollKind::ReduceScatter, false},
+                            {"all_to_all", CollKind::AllToAll, false},
+                            {"copy", CollKind::SendRecv, true}};
+    if (W > 1) kinds.push_back({"sendrecv", CollKind::SendRecv, false});
+    const int next = (me + 1) % W, prev = (me + W - 1) % W;
     for (size_t n : sizes) {
       for (const K& k : kinds) {
         auto op = [&] {
+          if (k.copy) {
+            ctx.dev->copy_async(b.data(), a.data(), n * es, *stream);
+            return;
+          }
           switch (k.kind) {
-            case CollKind::SendRecv: ctx.dev->copy_async(b.data(), a.data(), n * es, *stream); break;
+            case CollKind::SendRecv:
+              link->group_start();
+              link->send(a.data(), n, t, next, *stream);
+              link->recv(b.data(), n, t, prev, *stream);
+              link->group_end();
+              break;
             case CollKind::AllReduce: comm->all_reduce(a.data(), b.data(), n, t, *stream); break;
             case CollKind::AllGather: comm->all_gather(a.data(), b.data(), n, t, *stream); break;
             case CollKind::ReduceScatter: comm->reduce_scatter(a.data(), b.data(), n, t, *stream); break;
@@ -392,7 +406,7 @@ int commtest_main(int argc, char** argv) {
           j["bytes"] = bytes;
           j["time_us"] = dt * 1e6;
           j["algbw_GBps"] = bytes / dt / 1e9;
-          j["busbw_GBps"] = k.kind == CollKind::SendRecv ? 0.0 : bytes / dt / 1e9 * busbw_factor(k.kind, W);
+          j["busbw_GBps"] = k.copy ? 0.0 : bytes / dt / 1e9 * busbw_factor(k.kind, W);
           std::cout << j.dump() << std::endl;
         }
       }

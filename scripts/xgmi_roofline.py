@@ -8,6 +8,7 @@ rank and operation the kernels' traffic is fixed by their data path
   reduce_scatter  push W-1 blocks, reduce W sources into recv         n(3W-1)
   all_to_all      push W-1 blocks, own block, copy W-1 slots out      n(4W-2)
   all_reduce      two-shot: scatter, reduce + broadcast, copy out     n(6W-4)/W  (n = whole message)
+  sendrecv        ring: push n into the next rank's window, copy n out of mine   4n
   copy            hipMemcpyAsync D2D                                  2n
 With registered buffers (EXTRA=--registered: zero-copy paths) the same ops move
   all_gather      one load, W stores straight into every rank's receive buffer  n(W+1)
@@ -30,7 +31,7 @@ def traffic(op, n, W, registered=False):
     if registered and op == "all_reduce" and n > 256 * 1024 and n % 16 == 0:
         return 2 * n
     return {"all_gather": n * (3 * W - 1), "reduce_scatter": n * (3 * W - 1), "all_to_all": n * (4 * W - 2),
-            "all_reduce": n * (6 * W - 4) / W, "copy": 2 * n}[op]
+            "all_reduce": n * (6 * W - 4) / W, "sendrecv": 4 * n, "copy": 2 * n}[op]
 
 
 def main():
@@ -44,7 +45,7 @@ def main():
         if r.get("commtest") != "bench" or (a.blocks and r.get("blocks") != a.blocks):
             continue
         W, op, count = r["W"], r["op"], r["count"]
-        es = r["bytes"] / count / (1 if op in ("all_reduce", "copy") else W)
+        es = r["bytes"] / count / (1 if op in ("all_reduce", "copy", "sendrecv") else W)
         n = count * es
         t = r["time_us"] * 1e-6
         reg = "--registered" in (r.get("extra") or "")

@@ -42,7 +42,7 @@ def test_cpu_backend_exact(w, dtype):
 def test_cpu_backend_bench_lines():
     out = commtest(2, "--backend", "cpu", "--bench", "--sizes", "4096,65536", "--iters", "2", "--warmup", "1")
     ops = {(o["op"], o["count"]) for o in out}
-    assert len(ops) == 10  # 4 collectives + the local copy roofline, 2 sizes
+    assert len(ops) == 12  # 4 collectives + ring send/recv + the local copy roofline, 2 sizes
     for o in out:
         assert o["time_us"] > 0 and (o["busbw_GBps"] > 0 or o["op"] == "copy")
 
@@ -149,7 +149,7 @@ def test_xgmi_bench_runs():
     _need_gpu()
     out = commtest(2, "--backend", "xgmi", "-d", "0,0", "--bench", "--sizes", "65536,4194304", "--iters", "5",
                    "--warmup", "2", env_extra={"DLNB_XGMI_TIMEOUT_S": "60"})
-    assert len(out) == 10 and all(o["busbw_GBps"] > 0 for o in out if o["op"] != "copy")
+    assert len(out) == 12 and all(o["busbw_GBps"] > 0 for o in out if o["op"] != "copy")
 
 
 XGMI_STRATS = [  # strategy, model, positional args, extra flags, ranks

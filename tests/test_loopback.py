@@ -69,7 +69,8 @@ def test_commtest_loopback_bench():
                        cwd=ROOT)
     lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert p.returncode == 0, p.stderr[-2000:]
-    assert {ln["op"] for ln in lines} == {"all_reduce", "all_gather", "reduce_scatter", "all_to_all", "copy"}
+    assert {ln["op"] for ln in lines} == {"all_reduce", "all_gather", "reduce_scatter", "all_to_all", "copy",
+                                          "sendrecv"}
     assert all(ln["busbw_GBps"] > 0 for ln in lines if ln["op"] != "copy")
 
 
