@@ -97,6 +97,14 @@ def _algbw(doc: dict, kind: str) -> Optional[float]:
     return round(sum(vals) / len(vals), 2) if vals else None
 
 
+def _energy(doc: dict) -> Optional[Dict[str, float]]:
+    per_rank = [sum(r["energy_consumed"]) / len(r["energy_consumed"]) for r in doc["ranks"]
+                if r.get("energy_consumed")]
+    if not per_rank or not any(per_rank):
+        return None
+    return {"all_gpus": round(sum(per_rank), 2), "per_gpu": round(sum(per_rank) / len(per_rank), 2)}
+
+
 def _mean_of(doc: dict, key: str) -> Optional[float]:
     """Mean over ranks and runs of a per-rank timer (seconds) -> ms."""
     vals = [v for r in doc["ranks"] for v in r.get(key, [])]
@@ -293,6 +301,10 @@ def main() -> int:
         "baseline_ms": BASELINE_MS,
         "baseline_note": "derived reference floor (BASELINE.md C2: fwd+bwd of llama3_8b_16_bfloat16); lower is better",
         "rccl_cta_budget": g["dlnb"].get("rccl_cta_budget"),
+        # energy per step (J): hwmon / amd-smi power sampled every 5 ms on every GPU
+        # (the reference's energy_consumed, plots_pareto_energy.py); sum over GPUs and mean per GPU
+        "energy_J_per_step": _energy(doc),
+        "energy_source": g["dlnb"].get("energy_source"),
     }
     out.update(extra)
     print(json.dumps(out), flush=True)

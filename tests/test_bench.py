@@ -101,6 +101,8 @@ def test_bench_gpu_single_rank_secondaries(tmp_path):
     assert 0.8 < c5["gemm_work"]["compute_stretch"] < 1.5, c5
     assert 0.8 < o["compute_stretch"] < 1.5, o
     assert o["rccl_cta_budget"]["applies"] and o["rccl_cta_budget"]["max_ctas_per_lane"] == 32
+    # energy: the GPU's power sensor integrated over each step (hundreds of W x the step time)
+    assert o["energy_J_per_step"] is None or o["energy_J_per_step"]["per_gpu"] > 0
 
 
 @pytest.mark.gpu
