@@ -248,9 +248,10 @@ __device__ __forceinline__ bool tail(const Ctx& c, int v, Frags<FP8>& f, f32x4 (
 // store; every staged load has been waited for).
 template <bool FP8, bool DL, bool BAL, bool UNI = false>
 __device__ __forceinline__ bool tile(Ctx& c, const char* __restrict__ A, const char* __restrict__ B,
-                                     __bf16* __restrict__ C, int M, int N, int K, int ldc, int b, const Deadline& d) {
+                                     __bf16* __restrict__ C, int M, int N, int K, int ldc, int b, const Deadline& d,
+                                     int GROUP = 8) {
   const int nt_m = M / kT, nt_n = N / kT;
-  constexpr int GROUP = 8;  // GROUP M-tiles share their B panels in L2
+  // GROUP M-tiles share their B panels in L2
   const int per_group = GROUP * nt_n;
   const int first_m = (b / per_group) * GROUP;
   const int gsz = min(nt_m - first_m, GROUP);
@@ -350,7 +351,7 @@ template <bool FP8, bool DL, bool BAL = false, bool UNI = false>
 __global__ void __launch_bounds__(512, 1)
     gemm_8phase_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
                        int K, int lda, int ldb, int ldc, uint64_t* __restrict__ slot, uint32_t epoch, uint64_t ticks,
-                       uint64_t slice_end, uint64_t* __restrict__ tstart) {
+                       uint64_t slice_end, uint64_t* __restrict__ tstart, int group = 8) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + 16];  // ONE array: staging + deadline flags
   const int tid = threadIdx.x;
   Ctx c;
@@ -367,7 +368,7 @@ __global__ void __launch_bounds__(512, 1)
   const int T = (M / kT) * (N / kT);
   Deadline d{0, ticks, slice_end, (lds_flag_t*)(smem + 2 * kBuf), tid};
   if constexpr (!DL) {
-    tile<FP8, false, BAL, UNI>(c, A, B, C, M, N, K, ldc, xcd_remap(blockIdx.x, T), d);
+    tile<FP8, false, BAL, UNI>(c, A, B, C, M, N, K, ldc, xcd_remap(blockIdx.x, T), d, group);
   } else {
     constexpr uint64_t kMask48 = (1ull << 48) - 1;
     if (tid == 0) {
@@ -634,6 +635,8 @@ void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, 
                     void* stream, bool balanced, bool uniform) {
   DLNB_REQUIRE(gemm_8phase_shape_ok(M, N, K, in_t), "gemm 8-phase: unsupported shape M=" << M << " N=" << N << " K=" << K);
   const int tiles = (M / kT) * (N / kT);
+  // M-tiles per L2 group of the tile order (DLNB_GEMM_GROUP, experiments)
+  const int group = static_cast<int>(std::max<long long>(1, env_int("DLNB_GEMM_GROUP", 8)));
   hipStream_t st = static_cast<hipStream_t>(stream);
   auto* a = static_cast<const char*>(A);
   auto* b = static_cast<const char*>(B);
@@ -644,17 +647,17 @@ void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, 
     if (in_t == DType::FP8_E4M3) {
       if (balanced)
         hipLaunchKernelGGL((gemm_8phase_kernel<true, false, true, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb,
-                           ldc, nullptr, 0u, 0ull, 0ull, nullptr);
+                           ldc, nullptr, 0u, 0ull, 0ull, nullptr, group);
       else
         hipLaunchKernelGGL((gemm_8phase_kernel<true, false, false, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda,
-                           ldb, ldc, nullptr, 0u, 0ull, 0ull, nullptr);
+                           ldb, ldc, nullptr, 0u, 0ull, 0ull, nullptr, group);
     } else {
       if (balanced)
         hipLaunchKernelGGL((gemm_8phase_kernel<false, false, true, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda,
-                           ldb, ldc, nullptr, 0u, 0ull, 0ull, nullptr);
+                           ldb, ldc, nullptr, 0u, 0ull, 0ull, nullptr, group);
       else
         hipLaunchKernelGGL((gemm_8phase_kernel<false, false, false, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda,
-                           ldb, ldc, nullptr, 0u, 0ull, 0ull, nullptr);
+                           ldb, ldc, nullptr, 0u, 0ull, 0ull, nullptr, group);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) DLNB_THROW("gemm 8-phase launch failed: " << hipGetErrorString(e));
@@ -663,14 +666,14 @@ void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, 
   if (in_t == DType::FP8_E4M3) {
     if (balanced)
       hipLaunchKernelGGL((gemm_8phase_kernel<true, false, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc,
-                         nullptr, 0u, 0ull, 0ull, nullptr);
+                         nullptr, 0u, 0ull, 0ull, nullptr, group);
     else
       hipLaunchKernelGGL((gemm_8phase_kernel<true, false>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc, nullptr,
                          0u, 0ull, 0ull, nullptr);
   } else {
     if (balanced)
       hipLaunchKernelGGL((gemm_8phase_kernel<false, false, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc,
-                         nullptr, 0u, 0ull, 0ull, nullptr);
+                         nullptr, 0u, 0ull, 0ull, nullptr, group);
     else
       hipLaunchKernelGGL((gemm_8phase_kernel<false, false>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc, nullptr,
                          0u, 0ull, 0ull, nullptr);
