@@ -2,6 +2,10 @@
 //
 // Every group gets an RCCL communicator; groups whose members share one node
 // also get an xgmi communicator with windows sized to the dispatch threshold.
+// A single-node group whose largest message (the capacity the strategy
+// declares) fits under the threshold gets the xgmi communicator only (every
+// operation would go there anyway); that is also what lets the dispatcher run
+// with several ranks on one GPU, which RCCL refuses.
 // Each operation goes to xgmi when its per-rank message is at most
 // DLNB_MIXED_XGMI_MAX_KB (default 2048 KiB: the latency-bound range, where a
 // one-shot kernel that writes to all 7 peers at once and exchanges one flag
@@ -34,12 +38,13 @@ class MixedComm : public Communicator {
  public:
   MixedComm(std::unique_ptr<Communicator> big, std::unique_ptr<Communicator> small, size_t max_small)
       : big_(std::move(big)), small_(std::move(small)), max_small_(max_small) {
-    name_ = big_->name();
-    members_ = big_->members();
-    rank_ = big_->rank();
-    size_ = big_->size();
+    Communicator& any = big_ ? *big_ : *small_;
+    name_ = any.name();
+    members_ = any.members();
+    rank_ = any.rank();
+    size_ = any.size();
   }
-  std::string backend_name() const override { return small_ ? "RCCL+XGMI" : "RCCL"; }
+  std::string backend_name() const override { return !small_ ? "RCCL" : big_ ? "RCCL+XGMI" : "XGMI"; }
 
   void all_reduce(const void* send, void* recv, size_t count, DType t, Stream& s) override {
     pick(count * dtype_size(t)).all_reduce(send, recv, count, t, s);
@@ -52,7 +57,7 @@ class MixedComm : public Communicator {
   }
   void all_to_all(const void* send, void* recv, size_t count, DType t, Stream& s) override {
     // xgmi all-to-all is out-of-place only
-    Communicator& c = send == recv ? *big_ : pick(count * dtype_size(t));
+    Communicator& c = send == recv && big_ ? *big_ : pick(count * dtype_size(t));
     c.all_to_all(send, recv, count, t, s);
   }
   void send(const void* buf, size_t count, DType t, int peer, Stream& s) override {
@@ -73,12 +78,12 @@ class MixedComm : public Communicator {
     c.group_end();
   }
   std::string async_error() override {
-    std::string e = big_->async_error();
+    std::string e = big_ ? big_->async_error() : "";
     if (e.empty() && small_) e = small_->async_error();
     return e;
   }
   void abort() override {
-    big_->abort();
+    if (big_) big_->abort();
     if (small_) small_->abort();
   }
 
@@ -91,7 +96,9 @@ class MixedComm : public Communicator {
     int peer;
     Stream* s;
   };
-  Communicator& pick(size_t bytes) { return small_ && bytes <= max_small_ ? *small_ : *big_; }
+  // (no RCCL side: the group's messages all fit the threshold; the xgmi
+  // communicator still cuts a larger one into window pieces)
+  Communicator& pick(size_t bytes) { return small_ && (bytes <= max_small_ || !big_) ? *small_ : *big_; }
   static void issue(Communicator& c, const P2P& o) {
     if (o.is_send)
       c.send(o.buf, o.count, o.t, o.peer, *o.s);
@@ -121,10 +128,10 @@ class MixedFactory : public CommFactory {
   std::string backend_name() const override { return "RCCL+XGMI"; }
   std::unique_ptr<Communicator> create(const std::string& name, const std::vector<int>& members, size_t capacity_bytes,
                                        bool need_p2p, int max_ctas) override {
-    auto big = rccl_->create(name, members, capacity_bytes, need_p2p, max_ctas);
-    std::unique_ptr<Communicator> small;
+    std::unique_ptr<Communicator> big, small;
     if (max_small_ > 0 && members.size() > 1 && one_node(name, members))
       small = xgmi_->create("mixed/" + name, members, std::min(capacity_bytes, max_small_), need_p2p, max_ctas);
+    if (!small || capacity_bytes > max_small_) big = rccl_->create(name, members, capacity_bytes, need_p2p, max_ctas);
     return std::unique_ptr<Communicator>(new MixedComm(std::move(big), std::move(small), max_small_));
   }
 

@@ -131,6 +131,37 @@ def test_mixed_backend_single_rank_exact(graph):
     assert out[0]["ok"] and out[0]["backend"] == "RCCL", out  # one rank: no xgmi side
 
 
+MIXED_ALL_XGMI = {"DLNB_MIXED_XGMI_MAX_KB": str(8 << 20), "DLNB_XGMI_TIMEOUT_S": "60"}
+
+
+@pytest.mark.gpu
+def test_mixed_backend_two_ranks_xgmi_side():
+    """--backend mixed with 2 ranks on one GPU: with a threshold above every message the groups need no RCCL
+    side (RCCL refuses two ranks on one device), so the dispatcher's routing of collectives and grouped
+    point-to-point runs end to end through its xgmi side, exactly."""
+    _need_gpu()
+    out = commtest(2, "--backend", "mixed", "-d", "0,0", "--sizes", "1,4097,300000", env_extra=MIXED_ALL_XGMI)
+    assert out[0]["ok"] and out[0]["backend"] == "XGMI", out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy,model,params,extra,w", [
+    ("fsdp", "tiny_dense_8_bfloat16", ["4", "2"], ["--graph"], 2),
+    ("hybrid_3d_moe", "tiny_moe_8_bfloat16", ["1", "2", "2"], [], 2)])
+def test_strategies_on_mixed_two_ranks(strategy, model, params, extra, w, tmp_path):
+    _need_gpu()
+    out = tmp_path / "r.json"
+    data = os.path.join(ROOT, "tests", "data")
+    args = [os.path.join(ROOT, "build", "bin", strategy), model, *params, data, *extra, "-w", "1", "-r", "2",
+            "--backend", "mixed", "-d", ",".join(["0"] * w), "--compute", "spin", "--quiet", "--json", str(out)]
+    p = launch(w, args, MIXED_ALL_XGMI)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    d = json.loads(out.read_text())
+    # the reported group: fsdp's unit group (2 ranks: xgmi side); hybrid_3d_moe's DP group has 1 rank here
+    # (RCCL at one rank) while its 2-rank EP group runs on the xgmi side
+    assert d["global"]["backend"] == ("XGMI" if strategy == "fsdp" else "RCCL") and len(d["ranks"]) == w
+
+
 def test_mixed_backend_needs_gpu():
     p = subprocess.run([DLNB, "commtest", "--backend", "mixed"], capture_output=True, text=True,
                        env=dict(os.environ, HIP_VISIBLE_DEVICES="-1"))
