@@ -52,6 +52,10 @@ bool gemm_shape_ok(int M, int N, int K, DType in_t);
 void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
              void* stream, int waves = 0);
 bool gemm_8phase_shape_ok(int M, int N, int K, DType in_t);
+// 5 = one wave per SIMD, 128 x 128 of C per wave (gemm_4wave.hip; bf16, K % 64 == 0).
+bool gemm_4wave_shape_ok(int M, int N, int K, DType in_t);
+void gemm_tn_4wave(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                   void* stream);
 void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
                     void* stream, bool balanced = false, bool uniform = false);
 void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,

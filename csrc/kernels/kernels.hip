@@ -633,9 +633,19 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
                    reinterpret_cast<uintptr_t>(C) % 8 == 0,
                "gemm_tn: misaligned base pointers");
   const int tiles = (M / kTile) * (N / kTile);
-  DLNB_REQUIRE(waves == 0 || waves == 1 || waves == 2 || waves == 3 || waves == 4 || waves == 6 || waves == 7 ||
-                   waves == 8 || waves == 9,
-               "gemm_tn: variant must be 0, 1, 2, 3, 4, 6, 7, 8 or 9");
+  DLNB_REQUIRE(waves >= 0 && waves <= 9, "gemm_tn: variant must be 0..9");
+  // bf16 default: the one-wave-per-SIMD kernel (0.94x hipBLASLt at 8192^3,
+  // +3-8 % over the 8-phase kernel) except at long K, where its shorter
+  // prefetch distance loses to the 8-phase kernel (profiles/gemm_bench_r2.md)
+  if (waves == 0 && in_t == DType::BF16 && gemm_8phase_enabled() && K < 12288 && gemm_4wave_shape_ok(M, N, K, in_t))
+    waves = 5;
+  if (waves == 5) {
+    if (gemm_4wave_shape_ok(M, N, K, in_t)) {
+      gemm_tn_4wave(A, B, C, M, N, K, lda, ldb, ldc, stream);
+      return;
+    }
+    waves = 0;  // fp8 / K not a multiple of 64: the default
+  }
   // bf16: balanced reads; fp8: balanced reads + one uniform K-tile body (no
   // spills: +7-12 % over the plain 8-phase fp8 kernel, profiles/gemm_bench_r2.md)
   if (waves == 0 && gemm_8phase_enabled()) waves = in_t == DType::BF16 ? 6 : 7;

@@ -26,7 +26,7 @@ def main(argv=None) -> int:
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--variants", default=None, help="comma list of gemm_tn variants (default: 2,3,6 bf16; 8,3 fp8)")
+    ap.add_argument("--variants", default=None, help="comma list of gemm_tn variants (default: 5,6 bf16; 7,3 fp8)")
     a = ap.parse_args(argv)
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float8_e4m3fn
     for shp in a.shapes.split(","):
@@ -38,7 +38,7 @@ def main(argv=None) -> int:
         C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         flop = 2.0 * M * N * K
 
-        variants = [int(v) for v in (a.variants or ("2,3,6" if a.dtype == "bf16" else "8,3")).split(",")]
+        variants = [int(v) for v in (a.variants or ("5,6" if a.dtype == "bf16" else "7,3")).split(",")]
 
         def mk(v):
             return lambda: gemm.gemm_tn(A, B, C, waves=v)
