@@ -60,19 +60,29 @@ __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// One half-tile: 16 wave-instructions of global_load_lds_dwordx4, 2 per wave.
-// The swizzle is applied to the per-lane source address (LDS writes are
-// lane-linear): LDS slot q of row r holds chunk q ^ ((r >> 1) & 7).
-__device__ __forceinline__ void stage_half(const char* __restrict__ g, size_t ld, char* lds, int w, int lane) {
+// One half-tile: 16 wave-instructions of buffer_load_dwordx4 ... lds, 2 per
+// wave (instruction i*8 + w: rows 8 (i*8 + w) .. +7, 128 B each). The swizzle
+// is applied to the per-lane source offset (LDS writes are lane-linear): LDS
+// slot q of row r holds chunk q ^ ((r >> 1) & 7). The lane offset
+// (lane_offset) is loop-invariant; the half-tile's first row is the
+// (scalar) resource base and the K-tile the scalar offset, so staging costs
+// no per-lane address arithmetic (the per-lane 64-bit global_load_lds
+// addresses it replaces cost 10 % in the one-wave-per-SIMD kernel,
+// profiles/gemm_bench_r2.md).
+__device__ __forceinline__ void stage_half(const char* base, int voff, size_t ld, int soff, char* lds, int w) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), 0, 0x7ffffff0, 0x00020000);
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int inst = i * 8 + w;
-    const int slot = inst * 64 + lane;
-    const int r = slot >> 3;
-    const int c = (slot & 7) ^ ((r >> 1) & 7);
-    __builtin_amdgcn_global_load_lds((gbl_ptr_t)(g + static_cast<size_t>(r) * ld + (c << 4)),
-                                     (lds_ptr_t)(lds + inst * 1024), 16, 0, 0);
-  }
+  for (int i = 0; i < 2; ++i)  // instruction 1 = instruction 0 + 64 rows (same swizzle phase): a scalar offset
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(lds + (i * 8 + w) * 1024), 16, voff,
+                                             soff + i * 64 * static_cast<int>(ld), 0, 0);
+}
+
+// The lane's offset within its first staging instruction (w * 64 + lane).
+__device__ __forceinline__ int lane_offset(size_t ld, int w, int lane) {
+  const int slot = w * 64 + lane;
+  const int r = slot >> 3;
+  const int q = (slot & 7) ^ ((r >> 1) & 7);
+  return static_cast<int>(r * ld) + (q << 4);
 }
 
 __device__ __forceinline__ int xcd_remap(int b, int T) {
@@ -137,6 +147,7 @@ struct Ctx {
   char* smem;
   int w, lane, wr, wc, r16, h;
   int last_kt;  // uniform K-loop: staging of K-tiles past the last one re-reads it (never consumed)
+  int voffA, voffB;  // staging lane offsets (lane_offset)
 };
 
 // Where half-tile `slot` of K-tile t comes from / goes to.
@@ -144,9 +155,8 @@ __device__ __forceinline__ void stage(const Ctx& c, int t, int slot) {
   const int tk = min(t, c.last_kt);  // == t except for the uniform loop's two overrun K-tiles
   const bool isA = slot == kA0 || slot == kA1;
   const int hi = slot == kA1 || slot == kB1;
-  const char* src = (isA ? c.Ab + static_cast<size_t>(hi) * 128 * c.lda : c.Bb + static_cast<size_t>(hi) * 128 * c.ldb) +
-                    static_cast<size_t>(tk) * kRB;
-  stage_half(src, isA ? c.lda : c.ldb, c.smem + (t & 1) * kBuf + slot * kHalf, c.w, c.lane);
+  const char* base = isA ? c.Ab + static_cast<size_t>(hi) * 128 * c.lda : c.Bb + static_cast<size_t>(hi) * 128 * c.ldb;
+  stage_half(base, isA ? c.voffA : c.voffB, isA ? c.lda : c.ldb, tk * kRB, c.smem + (t & 1) * kBuf + slot * kHalf, c.w);
 }
 
 // Deadline state of the persistent variant: thread 0 (wave row 0) reads the
@@ -356,7 +366,7 @@ __global__ void __launch_bounds__(512, 1)
   const int tid = threadIdx.x;
   Ctx c;
   c.lane = tid & 63;
-  c.w = tid >> 6;
+  c.w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: staging LDS addresses stay scalar
   c.wr = c.w >> 2;  // waves w and w+4 share a SIMD: one per wave row
   c.wc = c.w & 3;
   c.r16 = c.lane & 15;
@@ -365,6 +375,8 @@ __global__ void __launch_bounds__(512, 1)
   constexpr int esz = FP8 ? 1 : 2;
   c.lda = static_cast<size_t>(lda) * esz;
   c.ldb = static_cast<size_t>(ldb) * esz;
+  c.voffA = lane_offset(c.lda, c.w, c.lane);
+  c.voffB = lane_offset(c.ldb, c.w, c.lane);
   const int T = (M / kT) * (N / kT);
   Deadline d{0, ticks, slice_end, (lds_flag_t*)(smem + 2 * kBuf), tid};
   if constexpr (!DL) {
@@ -465,9 +477,8 @@ __device__ __forceinline__ void stage_g(const Ctx& c, const StreamCtx& sc, int t
   const int hi = slot == kA1 || slot == kB1;
   const char* ab = nxt ? sc.Ab1 : sc.Ab0;
   const char* bb = nxt ? sc.Bb1 : sc.Bb0;
-  const char* src = (isA ? ab + static_cast<size_t>(hi) * 128 * c.lda : bb + static_cast<size_t>(hi) * 128 * c.ldb) +
-                    static_cast<size_t>(kt) * kRB;
-  stage_half(src, isA ? c.lda : c.ldb, c.smem + (t & 1) * kBuf + slot * kHalf, c.w, c.lane);
+  const char* src = isA ? ab + static_cast<size_t>(hi) * 128 * c.lda : bb + static_cast<size_t>(hi) * 128 * c.ldb;
+  stage_half(src, isA ? c.voffA : c.voffB, isA ? c.lda : c.ldb, kt * kRB, c.smem + (t & 1) * kBuf + slot * kHalf, c.w);
 }
 
 // Phase Q of stream K-tile g (g - base = K-tile of the current tile). Same
@@ -534,7 +545,7 @@ __global__ void __launch_bounds__(512, 1)
   const int tid = threadIdx.x;
   Ctx c;
   c.lane = tid & 63;
-  c.w = tid >> 6;
+  c.w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: staging LDS addresses stay scalar
   c.wr = c.w >> 2;
   c.wc = c.w & 3;
   c.r16 = c.lane & 15;
@@ -543,6 +554,8 @@ __global__ void __launch_bounds__(512, 1)
   constexpr int esz = FP8 ? 1 : 2;
   c.lda = static_cast<size_t>(lda) * esz;
   c.ldb = static_cast<size_t>(ldb) * esz;
+  c.voffA = lane_offset(c.lda, c.w, c.lane);
+  c.voffB = lane_offset(c.ldb, c.w, c.lane);
   Deadline d{0, ticks, slice_end, (lds_flag_t*)(smem + 2 * kBuf), tid};
   {
     constexpr uint64_t kMask48 = (1ull << 48) - 1;

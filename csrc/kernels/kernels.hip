@@ -634,11 +634,6 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
                "gemm_tn: misaligned base pointers");
   const int tiles = (M / kTile) * (N / kTile);
   DLNB_REQUIRE(waves >= 0 && waves <= 9, "gemm_tn: variant must be 0..9");
-  // bf16 default: the one-wave-per-SIMD kernel (0.94x hipBLASLt at 8192^3,
-  // +3-8 % over the 8-phase kernel) except at long K, where its shorter
-  // prefetch distance loses to the 8-phase kernel (profiles/gemm_bench_r2.md)
-  if (waves == 0 && in_t == DType::BF16 && gemm_8phase_enabled() && K < 12288 && gemm_4wave_shape_ok(M, N, K, in_t))
-    waves = 5;
   if (waves == 5) {
     if (gemm_4wave_shape_ok(M, N, K, in_t)) {
       gemm_tn_4wave(A, B, C, M, N, K, lda, ldb, ldc, stream);
@@ -646,9 +641,9 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
     }
     waves = 0;  // fp8 / K not a multiple of 64: the default
   }
-  // bf16: balanced reads; fp8: balanced reads + one uniform K-tile body (no
-  // spills: +7-12 % over the plain 8-phase fp8 kernel, profiles/gemm_bench_r2.md)
-  if (waves == 0 && gemm_8phase_enabled()) waves = in_t == DType::BF16 ? 6 : 7;
+  // bf16: balanced reads; fp8: one uniform K-tile body (no spills; with the
+  // buffer_load staging the balanced fp8 build spills again, profiles/gemm_bench_r2.md)
+  if (waves == 0 && gemm_8phase_enabled()) waves = in_t == DType::BF16 ? 6 : 9;
   // 7 / 9: the 8-phase kernels (balanced / plain) with one uniform K-tile body
   if ((waves == 3 || waves == 6 || waves == 7 || waves == 9) && gemm_8phase_shape_ok(M, N, K, in_t)) {
     gemm_tn_8phase(A, B, C, M, N, K, lda, ldb, ldc, in_t, stream, waves == 6 || waves == 7, waves == 7 || waves == 9);
