@@ -38,7 +38,11 @@ def lib() -> ctypes.CDLL:
             pass
     if not os.path.exists(LIB_PATH):
         raise NativeError(f"{LIB_PATH} is missing: build it with `make` (or __graft_entry__.build())")
-    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    # RTLD_LOCAL: with RTLD_GLOBAL, the library's (and its HIP / RCCL
+    # dependencies') exported symbols interposed on extension modules dlopen'ed
+    # later in the process - the hypothesis pytest plugin's native module
+    # segfaulted on import at the end of a full test session (exit 139)
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_LOCAL)
     c_int, c_size, c_vp, c_dbl, c_float = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_double, ctypes.c_float
     L.dlnb_version.restype = ctypes.c_char_p
     L.dlnb_last_error.restype = ctypes.c_char_p
