@@ -56,6 +56,10 @@ bool gemm_8phase_shape_ok(int M, int N, int K, DType in_t);
 bool gemm_4wave_shape_ok(int M, int N, int K, DType in_t);
 void gemm_tn_4wave(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                    void* stream);
+//   fp8: gemm_4wave_fp8.hip (MX MFMA, K % 256 == 0).
+bool gemm_4wave_fp8_shape_ok(int M, int N, int K, DType in_t);
+void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                       void* stream);
 void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
                     void* stream, bool balanced = false, bool uniform = false);
 void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,

@@ -1,0 +1,275 @@
+// One-wave-per-SIMD MX-fp8 GEMM for gfx950: C[M,N] (bf16) = A[M,K] . B[N,K]^T,
+// A and B OCP fp8 e4m3, unit E8M0 scales (v_mfma_scale_f32_16x16x128_f8f6f4).
+//
+// Why a 4-wave fp8 kernel: in the 8-phase kernel (gemm_8phase.hip) an fp8
+// phase is only 8 MX MFMAs per wave between two barriers, and the waves spend
+// 30 % of their time at barriers / waitcnt (PMC at 8192 x 14336 x 4096; the
+// MX MFMA runs twice the FLOPs of a bf16 one in the same time, so the
+// per-barrier cost doubles relative to compute). Here one K-tile (128 fp8 =
+// one MX MFMA K) is 64 MFMAs per wave with two barriers.
+//
+//   * 4 waves, one per SIMD, 128 x 128 of C per wave: 64 accumulators = all
+//     256 AGPRs, MFMAs as inline asm on tied "+a" operands (see
+//     gemm_4wave.hip for why).
+//   * Fragments: a[i] (A rows wr*128 + 16 i + r16) single-buffered - a[i] of
+//     K-tile t+1 is read into a[i]'s registers once row i of K-tile t is done;
+//     b[j] double-buffered (two sets alternate per K-tile). 64 + 128 VGPRs.
+//     A lane's 32 bytes of K are chunks h and h + 4 of its row (the 8-phase
+//     kernel's conflict-free fp8 order).
+//   * K-tile t, MFMAs row-major (row i: 8 MFMAs on a[i]):
+//       start    vmcnt(8) (B(t+1) landed) + barrier
+//       rows 0-3 read B(t+1) into the other B set (16 ds_reads), stage B(t+2)
+//                (8 buffer_load ... lds, every other MFMA pair)
+//       mid      vmcnt(8) (A(t+1) landed) + lgkmcnt(0) + barrier (every wave's
+//                A(t) reads, issued during K-tile t-1, are done: A(t+2) may
+//                overwrite them)
+//       rows 4-7 read A(t+1) (a[0..3] at once, a[4..6] after their rows; a[7]
+//                in K-tile t+1's first MFMA pair), stage A(t+2)
+//     so every staged operand half has a full K-tile of load latency before
+//     its wait, and loads / reads are spread evenly (8 + 16 per half).
+//   * LDS: two 64 KiB K-tile buffers of four 128-row half-tiles (A0 A1 B0 B1),
+//     the 8-phase kernel's XOR-swizzled image; staging by buffer_load ... lds
+//     with loop-invariant lane offsets (K-tile and row block in the scalar
+//     offset). Uniform loop: the last K-tiles stage / read clamped copies of
+//     the last one (never used).
+//
+// Variant 5 of dlnb::kernels::gemm_tn for fp8 (K a multiple of 256 bytes).
+#include <hip/hip_runtime.h>
+
+#include "dlnb/kernels.hpp"
+
+namespace dlnb {
+namespace kernels {
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+constexpr int kT = 256;           // block tile
+constexpr int kRB = 128;          // bytes of K per K-tile row
+constexpr int kHalf = 128 * kRB;  // half-tile: 16 KiB
+constexpr int kBuf = 4 * kHalf;   // A0 A1 B0 B1
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ int xcd_remap(int b, int T) {
+  const int q = T / 8, r = T % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+struct CtxF {
+  __amdgpu_buffer_rsrc_t ra, rb;  // A / B rows of the block tile
+  int voffA, voffB;               // lane offset within a staging instruction
+  int lda, ldb;                   // bytes
+  char* smem;
+  int w, last_kt;
+};
+
+// Piece p (0..7) of operand op's (0 A, 1 B) half-tiles of K-tile kt (clamped
+// to the last one): half p / 4, this wave's wave-instruction (p % 4) * 4 + w
+// (8 rows x 128 B; instruction i covers rows 32 i + 8 w + lane / 8 of the half).
+__device__ __forceinline__ void stage_piece(const CtxF& c, int kt, int op, int p) {
+  const int half = p >> 2, i = p & 3;
+  const int tk = min(kt, c.last_kt);
+  const int ld = op ? c.ldb : c.lda;
+  char* lds = c.smem + (kt & 1) * kBuf + (op * 2 + half) * kHalf + (i * 4 + c.w) * 1024;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(op ? c.rb : c.ra, (lds_ptr_t)lds, 16, op ? c.voffB : c.voffA,
+                                           tk * kRB + (half * 128 + i * 32) * ld, 0, 0);
+}
+
+// One 16-B half of fragment f (rows 16 f + r16 of a half-tile): part 0 = K
+// chunk h, part 1 = chunk h + 4 (lane offsets offl / offh).
+__device__ __forceinline__ i32x4 read_part(const char* half, int offl, int offh, int f, int part) {
+  return *reinterpret_cast<const i32x4*>(half + (part ? offh : offl) + f * 2048);
+}
+
+struct FragF {
+  i32x4 lo, hi;
+  __device__ __forceinline__ i32x8 v() const { return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7); }
+};
+
+// acc += b . a^T (MX fp8, unit scales), accumulator pinned to AGPRs. ZERO:
+// srcC = 0 (first K-tile).
+template <bool ZERO>
+__device__ __forceinline__ void mfma(f32x4& acc, const FragF& b, const FragF& a, int scale) {
+  const i32x8 bv = b.v(), av = a.v();
+  if constexpr (ZERO)
+    asm("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, 0, %3, %3 op_sel_hi:[0,0,0]"
+        : "=a"(acc)
+        : "v"(bv), "v"(av), "v"(scale));
+  else
+    asm("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
+        : "+a"(acc)
+        : "v"(bv), "v"(av), "v"(scale));
+}
+
+// K-tile t (PAR = t & 1: b[PAR] is this K-tile's B set, b[1 - PAR] receives
+// K-tile t+1's).
+template <int PAR, bool FIRST>
+__device__ __forceinline__ void ktile(const CtxF& c, int t, int wr, int wc, int offl, int offh, FragF (&a)[8],
+                                      FragF (&b)[2][8], f32x4 (&acc)[8][8], int scale) {
+  const char* cbuf = c.smem + (t & 1) * kBuf;
+  const char* nbuf = c.smem + ((t + 1) & 1) * kBuf;
+  const char* na = nbuf + wr * kHalf;
+  const char* nb = nbuf + (2 + wc) * kHalf;
+  wait_vm<8>();  // B(t+1) landed (A(t+1) may be in flight)
+  raw_barrier();
+#pragma unroll
+  for (int g = 0; g < 32; ++g) {
+    const int i = g >> 2, j = (g & 3) * 2;
+    if (g == 16) {
+      wait_vm<8>();                        // A(t+1) landed (B(t+2) may be in flight)
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's A(t) reads are done
+      raw_barrier();
+    }
+    mfma<FIRST>(acc[i][j], b[PAR][j], a[i], scale);
+    mfma<FIRST>(acc[i][j + 1], b[PAR][j + 1], a[i], scale);
+    // a[7] of THIS K-tile: read here, not right after the MFMA that last read
+    // the previous a[7] (its K-tile's A region is restaged only after the mid
+    // barrier, which waits for this read)
+    if (!FIRST && g == 0) a[7].lo = read_part(cbuf + wr * kHalf, offl, offh, 7, 0);
+    if (!FIRST && g == 1) a[7].hi = read_part(cbuf + wr * kHalf, offl, offh, 7, 1);
+    if (g < 16) {
+      // B(t+1): fragment g / 2, part g % 2
+      if ((g & 1) == 0)
+        b[1 - PAR][g >> 1].lo = read_part(nb, offl, offh, g >> 1, 0);
+      else
+        b[1 - PAR][g >> 1].hi = read_part(nb, offl, offh, g >> 1, 1);
+      if (g & 1) stage_piece(c, t + 2, 1, g >> 1);
+    } else {
+      // A(t+1): a[0..1] in pairs 16-19, a[2..3] 20-23, a[4..5] 24-27 (rows 4, 5
+      // done), a[6] 28-29 (row 6 done); a[7] in K-tile t+1's first pair
+      const int k = g - 16;
+      if (k < 14) {
+        if ((k & 1) == 0)
+          a[k >> 1].lo = read_part(na, offl, offh, k >> 1, 0);
+        else
+          a[k >> 1].hi = read_part(na, offl, offh, k >> 1, 1);
+      }
+      if (g & 1) stage_piece(c, t + 2, 0, (g - 16) >> 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+__global__ void __launch_bounds__(256, 1)
+    gemm_4wave_fp8_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
+                          int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];  // 128 KiB, one array
+  const int tid = threadIdx.x;
+  CtxF c;
+  const int lane = tid & 63;
+  c.w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = c.w >> 1, wc = c.w & 1;
+  const int r16 = lane & 15, h = lane >> 4;
+  c.smem = smem;
+  c.lda = lda;  // fp8: elements = bytes
+  c.ldb = ldb;
+  const int nt_m = M / kT, nt_n = N / kT, T = nt_m * nt_n;
+  const int bid = xcd_remap(blockIdx.x, T);
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * nt_n;
+  const int first_m = (bid / per_group) * GROUP;
+  const int gsz = min(nt_m - first_m, GROUP);
+  const int tm = first_m + (bid % per_group) % gsz;
+  const int tn = (bid % per_group) / gsz;
+  c.ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(A) + static_cast<size_t>(tm) * kT * lda, 0, 0x7ffffff0,
+                                           0x00020000);
+  c.rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(B) + static_cast<size_t>(tn) * kT * ldb, 0, 0x7ffffff0,
+                                           0x00020000);
+  {
+    const int r = c.w * 8 + (lane >> 3);  // row within instruction 0 of a half
+    const int q = (lane & 7) ^ ((r >> 1) & 7);
+    c.voffA = r * lda + (q << 4);
+    c.voffB = r * ldb + (q << 4);
+  }
+  const int nk = K / kRB;  // K-tiles (even, >= 2: host-checked)
+  c.last_kt = nk - 1;
+  const int x = (r16 >> 1) & 7;
+  const int offl = r16 * kRB + ((h ^ x) << 4), offh = offl ^ 64;  // chunk h + 4 = offset bit 6 flipped
+  int scale = 127;  // E8M0 1.0
+  asm volatile("" : "+v"(scale));
+
+  f32x4 acc[8][8];
+  FragF a[8], b[2][8];
+
+  // Prologue: B(0) A(0) B(1) A(1); K-tile 0 landed -> its fragments.
+#pragma unroll
+  for (int p = 0; p < 8; ++p) stage_piece(c, 0, 1, p);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) stage_piece(c, 0, 0, p);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) stage_piece(c, 1, 1, p);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) stage_piece(c, 1, 0, p);
+  wait_vm<16>();
+  raw_barrier();
+#pragma unroll
+  for (int f = 0; f < 8; ++f) {
+    a[f].lo = read_part(smem + wr * kHalf, offl, offh, f, 0);
+    a[f].hi = read_part(smem + wr * kHalf, offl, offh, f, 1);
+    b[0][f].lo = read_part(smem + (2 + wc) * kHalf, offl, offh, f, 0);
+    b[0][f].hi = read_part(smem + (2 + wc) * kHalf, offl, offh, f, 1);
+  }
+  ktile<0, true>(c, 0, wr, wc, offl, offh, a, b, acc, scale);
+  for (int t = 1; t < nk - 1; t += 2) {
+    ktile<1, false>(c, t, wr, wc, offl, offh, a, b, acc, scale);
+    ktile<0, false>(c, t + 1, wr, wc, offl, offh, a, b, acc, scale);
+  }
+  ktile<1, false>(c, nk - 1, wr, wc, offl, offh, a, b, acc, scale);
+  wait_vm<0>();  // the clamped staging copies
+  // MFMA D -> v_accvgpr_read wait states (tied: no reader hoisted above it)
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
+               : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[7][4]),
+                 "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7]));
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int m = tm * kT + wr * 128 + i * 16 + r16;
+      const int n = tn * kT + wc * 128 + j * 16 + 4 * h;
+      const f32x4 v = acc[i][j];
+      bf16x4 o;
+      o[0] = static_cast<__bf16>(v[0]);
+      o[1] = static_cast<__bf16>(v[1]);
+      o[2] = static_cast<__bf16>(v[2]);
+      o[3] = static_cast<__bf16>(v[3]);
+      *reinterpret_cast<bf16x4*>(C + static_cast<size_t>(m) * ldc + n) = o;
+    }
+}
+
+}  // namespace
+
+bool gemm_4wave_fp8_shape_ok(int M, int N, int K, DType in_t) {
+  return in_t == DType::FP8_E4M3 && gemm_shape_ok(M, N, K, in_t) && K % 256 == 0 && K >= 256;
+}
+
+void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                       void* stream) {
+  DLNB_REQUIRE(gemm_4wave_fp8_shape_ok(M, N, K, DType::FP8_E4M3),
+               "gemm 4-wave fp8: unsupported shape M=" << M << " N=" << N << " K=" << K);
+  const int tiles = (M / kT) * (N / kT);
+  hipLaunchKernelGGL(gemm_4wave_fp8_kernel, tiles, 256, 0, static_cast<hipStream_t>(stream),
+                     static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda,
+                     ldb, ldc);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) DLNB_THROW("gemm 4-wave fp8 launch failed: " << hipGetErrorString(e));
+}
+
+}  // namespace kernels
+}  // namespace dlnb

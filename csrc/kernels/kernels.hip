@@ -634,12 +634,19 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
                "gemm_tn: misaligned base pointers");
   const int tiles = (M / kTile) * (N / kTile);
   DLNB_REQUIRE(waves >= 0 && waves <= 9, "gemm_tn: variant must be 0..9");
+  // fp8 default: the one-wave-per-SIMD MX kernel where it applies (+5-7 % over
+  // the uniform 8-phase kernel, profiles/gemm_bench_r2.md)
+  if (waves == 0 && gemm_8phase_enabled() && gemm_4wave_fp8_shape_ok(M, N, K, in_t)) waves = 5;
   if (waves == 5) {
     if (gemm_4wave_shape_ok(M, N, K, in_t)) {
       gemm_tn_4wave(A, B, C, M, N, K, lda, ldb, ldc, stream);
       return;
     }
-    waves = 0;  // fp8 / K not a multiple of 64: the default
+    if (gemm_4wave_fp8_shape_ok(M, N, K, in_t)) {
+      gemm_tn_4wave_fp8(A, B, C, M, N, K, lda, ldb, ldc, stream);
+      return;
+    }
+    waves = 0;  // shapes the 4-wave kernels do not take: the default
   }
   // bf16: balanced reads; fp8: one uniform K-tile body (no spills; with the
   // buffer_load staging the balanced fp8 build spills again, profiles/gemm_bench_r2.md)

@@ -1,11 +1,14 @@
-"""8192^3 GEMM launches for PMC runs: our variants (waves selector) from argv[1], 10 launches each;
-argv[2] = bf16 (default) | fp8; variant "t" = torch (hipBLASLt: matmul / _scaled_mm)."""
+"""GEMM launches for PMC runs: our variants (waves selector) from argv[1], 10 launches each;
+argv[2] = bf16 (default) | fp8; argv[3] = MxNxK (default 8192^3); variant "t" = torch (hipBLASLt:
+matmul / _scaled_mm)."""
 import sys
 import torch
 sys.path.insert(0, ".")
 from dlnetbench_amd.ops import gemm
 
 M = N = K = 8192
+if len(sys.argv) > 3:
+    M, N, K = (int(x) for x in sys.argv[3].split("x"))
 dt = sys.argv[2] if len(sys.argv) > 2 else "bf16"
 a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
 b = torch.empty(N, K, device="cuda", dtype=torch.bfloat16)

@@ -29,8 +29,9 @@ for nm, c in acc.items():
     t = sum(c["dur_ns"]) / len(c["dur_ns"])
     gui = mean.get("GRBM_GUI_ACTIVE", 0) / 8
     out = {"kernel": nm, "n": len(c["dur_ns"]), "ms": round(t / 1e6, 3), "clk_GHz": round(gui / t, 3) if t else 0}
-    if "SQ_INSTS_VALU_MFMA_MOPS_BF16" in mean:
-        out["TFLOPs"] = round(mean["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512 / t / 1e3, 1)
+    for mops in ("SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_INSTS_VALU_MFMA_MOPS_F8"):
+        if mops in mean:
+            out["TFLOPs"] = round(mean[mops] * 512 / t / 1e3, 1)
     for k, v in sorted(mean.items()):
         if k not in ("dur_ns", "GRBM_GUI_ACTIVE"):
             out[k] = round(v / gui, 3) if gui else v  # per GPU-clock cycle
