@@ -60,6 +60,9 @@ void gemm_tn_4wave(const void* A, const void* B, void* C, int M, int N, int K, i
 bool gemm_4wave_fp8_shape_ok(int M, int N, int K, DType in_t);
 void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                        void* stream);
+void gemm_tn_4wave_fp8_deadline(const void* A, const void* B, void* C, int M, int N, int K, uint64_t ticks,
+                                uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
+                                uint64_t* tstart);
 void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
                     void* stream, bool balanced = false, bool uniform = false);
 void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,

@@ -36,6 +36,8 @@
 // Variant 5 of dlnb::kernels::gemm_tn for fp8 (K a multiple of 256 bytes).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "dlnb/kernels.hpp"
 
 namespace dlnb {
@@ -117,24 +119,51 @@ __device__ __forceinline__ void mfma(f32x4& acc, const FragF& b, const FragF& a,
         : "v"(bv), "v"(av), "v"(scale));
 }
 
+// Deadline state (DL kernels, the compute stand-in): the clock is read at the
+// start of every K-tile and thread 0 writes the stop decision into an LDS flag
+// (typed LDS pointer: a generic one becomes a FLAT store that waits vmcnt(0))
+// before the K-tile's mid barrier; every wave reads it right after that
+// barrier, so all waves leave at the same point. flag[t & 1] is next written
+// two K-tiles later, after two more barriers.
+typedef __attribute__((address_space(3))) volatile int lds_flag_t;
+struct DeadlineF {
+  uint64_t t0, ticks, slice_end;
+  lds_flag_t* flag;
+  int tid;
+};
+
 // K-tile t (PAR = t & 1: b[PAR] is this K-tile's B set, b[1 - PAR] receives
-// K-tile t+1's).
-template <int PAR, bool FIRST>
-__device__ __forceinline__ void ktile(const CtxF& c, int t, int wr, int wc, int offl, int offh, FragF (&a)[8],
-                                      FragF (&b)[2][8], f32x4 (&acc)[8][8], int scale) {
+// K-tile t+1's). READ7: read this K-tile's a[7] (every K-tile but a tile's
+// first, whose fragments the prologue read). Returns (DL) whether the
+// deadline has passed; a stopped K-tile has issued every load it would have.
+template <int PAR, bool FIRST, bool DL>
+__device__ __forceinline__ bool ktile(const CtxF& c, int t, int wr, int wc, int offl, int offh, FragF (&a)[8],
+                                      FragF (&b)[2][8], f32x4 (&acc)[8][8], int scale, const DeadlineF& d) {
   const char* cbuf = c.smem + (t & 1) * kBuf;
   const char* nbuf = c.smem + ((t + 1) & 1) * kBuf;
   const char* na = nbuf + wr * kHalf;
   const char* nb = nbuf + (2 + wc) * kHalf;
   wait_vm<8>();  // B(t+1) landed (A(t+1) may be in flight)
   raw_barrier();
+  bool stop = false;
+  uint64_t now = 0;
 #pragma unroll
   for (int g = 0; g < 32; ++g) {
     const int i = g >> 2, j = (g & 3) * 2;
+    if constexpr (DL) {
+      // clock read early (scalar-memory latency hidden behind 15 MFMA pairs),
+      // flag written late; the mid wait's lgkmcnt(0) lands it before the barrier
+      if (g == 0) now = __builtin_amdgcn_s_memrealtime();
+      if (g == 15 && d.tid == 0) {
+        const uint64_t el = (now - d.t0) & ((1ull << 48) - 1);
+        d.flag[t & 1] = el >= d.ticks || el >= d.slice_end;
+      }
+    }
     if (g == 16) {
       wait_vm<8>();                        // A(t+1) landed (B(t+2) may be in flight)
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's A(t) reads are done
       raw_barrier();
+      if constexpr (DL) stop = __builtin_amdgcn_readfirstlane(d.flag[t & 1]) != 0;
     }
     mfma<FIRST>(acc[i][j], b[PAR][j], a[i], scale);
     mfma<FIRST>(acc[i][j + 1], b[PAR][j + 1], a[i], scale);
@@ -164,39 +193,21 @@ __device__ __forceinline__ void ktile(const CtxF& c, int t, int wr, int wc, int 
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+  return stop;
 }
 
-__global__ void __launch_bounds__(256, 1)
-    gemm_4wave_fp8_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
-                          int K, int lda, int ldb, int ldc) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];  // 128 KiB, one array
-  const int tid = threadIdx.x;
-  CtxF c;
-  const int lane = tid & 63;
-  c.w = __builtin_amdgcn_readfirstlane(tid >> 6);
+// One 256 x 256 tile of C. Returns false if the deadline stopped it (no
+// store; every staged load has been waited for).
+template <bool DL>
+__device__ __forceinline__ bool tile4(CtxF& c, const char* __restrict__ A, const char* __restrict__ B,
+                                      __bf16* __restrict__ C, int lda, int ldb, int ldc, int K, int tm, int tn,
+                                      int lane, const DeadlineF& d) {
   const int wr = c.w >> 1, wc = c.w & 1;
   const int r16 = lane & 15, h = lane >> 4;
-  c.smem = smem;
-  c.lda = lda;  // fp8: elements = bytes
-  c.ldb = ldb;
-  const int nt_m = M / kT, nt_n = N / kT, T = nt_m * nt_n;
-  const int bid = xcd_remap(blockIdx.x, T);
-  constexpr int GROUP = 8;
-  const int per_group = GROUP * nt_n;
-  const int first_m = (bid / per_group) * GROUP;
-  const int gsz = min(nt_m - first_m, GROUP);
-  const int tm = first_m + (bid % per_group) % gsz;
-  const int tn = (bid % per_group) / gsz;
   c.ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(A) + static_cast<size_t>(tm) * kT * lda, 0, 0x7ffffff0,
                                            0x00020000);
   c.rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(B) + static_cast<size_t>(tn) * kT * ldb, 0, 0x7ffffff0,
                                            0x00020000);
-  {
-    const int r = c.w * 8 + (lane >> 3);  // row within instruction 0 of a half
-    const int q = (lane & 7) ^ ((r >> 1) & 7);
-    c.voffA = r * lda + (q << 4);
-    c.voffB = r * ldb + (q << 4);
-  }
   const int nk = K / kRB;  // K-tiles (even, >= 2: host-checked)
   c.last_kt = nk - 1;
   const int x = (r16 >> 1) & 7;
@@ -220,23 +231,30 @@ __global__ void __launch_bounds__(256, 1)
   raw_barrier();
 #pragma unroll
   for (int f = 0; f < 8; ++f) {
-    a[f].lo = read_part(smem + wr * kHalf, offl, offh, f, 0);
-    a[f].hi = read_part(smem + wr * kHalf, offl, offh, f, 1);
-    b[0][f].lo = read_part(smem + (2 + wc) * kHalf, offl, offh, f, 0);
-    b[0][f].hi = read_part(smem + (2 + wc) * kHalf, offl, offh, f, 1);
+    a[f].lo = read_part(c.smem + wr * kHalf, offl, offh, f, 0);
+    a[f].hi = read_part(c.smem + wr * kHalf, offl, offh, f, 1);
+    b[0][f].lo = read_part(c.smem + (2 + wc) * kHalf, offl, offh, f, 0);
+    b[0][f].hi = read_part(c.smem + (2 + wc) * kHalf, offl, offh, f, 1);
   }
-  ktile<0, true>(c, 0, wr, wc, offl, offh, a, b, acc, scale);
-  for (int t = 1; t < nk - 1; t += 2) {
-    ktile<1, false>(c, t, wr, wc, offl, offh, a, b, acc, scale);
-    ktile<0, false>(c, t + 1, wr, wc, offl, offh, a, b, acc, scale);
+  bool stop = ktile<0, true, DL>(c, 0, wr, wc, offl, offh, a, b, acc, scale, d);
+  for (int t = 1; t < nk - 1 && !stop; t += 2) {
+    stop = ktile<1, false, DL>(c, t, wr, wc, offl, offh, a, b, acc, scale, d);
+    if (!stop) stop = ktile<0, false, DL>(c, t + 1, wr, wc, offl, offh, a, b, acc, scale, d);
   }
-  ktile<1, false>(c, nk - 1, wr, wc, offl, offh, a, b, acc, scale);
-  wait_vm<0>();  // the clamped staging copies
+  if (!stop) stop = ktile<1, false, DL>(c, nk - 1, wr, wc, offl, offh, a, b, acc, scale, d);
+  wait_vm<0>();  // the clamped staging copies (or, stopped, everything in flight)
+  // Every wave passes this barrier before the next tile's prologue restages
+  // K-tile 1's buffer, whose last reads (the clamped K-tile nk) were this
+  // K-tile's; and a stopped block leaves with nothing in flight.
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  raw_barrier();
+  if constexpr (DL) {
+    if (stop) return false;
+  }
   // MFMA D -> v_accvgpr_read wait states (tied: no reader hoisted above it)
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
                : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[7][4]),
                  "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7]));
-
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -251,6 +269,67 @@ __global__ void __launch_bounds__(256, 1)
       o[3] = static_cast<__bf16>(v[3]);
       *reinterpret_cast<bf16x4*>(C + static_cast<size_t>(m) * ldc + n) = o;
     }
+  return true;
+}
+
+__device__ __forceinline__ void tile_coords(int bid, int nt_m, int nt_n, int group, int& tm, int& tn) {
+  const int per_group = group * nt_n;  // group M-tiles share their B panels in L2
+  const int first_m = (bid / per_group) * group;
+  const int gsz = min(nt_m - first_m, group);
+  tm = first_m + (bid % per_group) % gsz;
+  tn = (bid % per_group) / gsz;
+}
+
+// DL = false: one launch, grid = tiles. DL = true: persistent stand-in
+// compute with gemm_tn_deadline's contract (kernels.hip): grid <= resident
+// blocks walks the tiles round-robin and stops min(ticks, slice_end) after t0,
+// agreed per epoch through *slot.
+template <bool DL>
+__global__ void __launch_bounds__(256, 1)
+    gemm_4wave_fp8_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
+                          int K, int lda, int ldb, int ldc, int group, uint64_t* __restrict__ slot, uint32_t epoch,
+                          uint64_t ticks, uint64_t slice_end, uint64_t* __restrict__ tstart) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + 16];  // ONE array: staging + deadline flags
+  const int tid = threadIdx.x;
+  CtxF c;
+  const int lane = tid & 63;
+  c.w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  c.smem = smem;
+  c.lda = lda;  // fp8: elements = bytes
+  c.ldb = ldb;
+  {
+    const int r = c.w * 8 + (lane >> 3);  // row within instruction 0 of a half
+    const int q = (lane & 7) ^ ((r >> 1) & 7);
+    c.voffA = r * lda + (q << 4);
+    c.voffB = r * ldb + (q << 4);
+  }
+  const int nt_m = M / kT, nt_n = N / kT, T = nt_m * nt_n;
+  DeadlineF d{0, ticks, slice_end, (lds_flag_t*)(smem + 2 * kBuf), tid};
+  int tm, tn;
+  if constexpr (!DL) {
+    tile_coords(xcd_remap(blockIdx.x, T), nt_m, nt_n, group, tm, tn);
+    tile4<false>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d);
+  } else {
+    constexpr uint64_t kMask48 = (1ull << 48) - 1;
+    if (tid == 0) {
+      const uint64_t raw = __builtin_amdgcn_s_memrealtime();
+      const uint64_t mine = (static_cast<uint64_t>(epoch) << 48) | (raw & kMask48);
+      uint64_t cur = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while ((cur >> 48) != epoch) {
+        if (__hip_atomic_compare_exchange_strong(slot, &cur, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          cur = mine;
+          if (tstart) __hip_atomic_store(tstart, raw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+      }
+      d.t0 = cur & kMask48;  // only thread 0 reads the clock
+    }
+    for (int round = 0;; ++round) {
+      tile_coords(xcd_remap((blockIdx.x + round * gridDim.x) % T, T), nt_m, nt_n, group, tm, tn);
+      if (!tile4<true>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d)) return;
+    }
+  }
 }
 
 }  // namespace
@@ -264,11 +343,23 @@ void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int 
   DLNB_REQUIRE(gemm_4wave_fp8_shape_ok(M, N, K, DType::FP8_E4M3),
                "gemm 4-wave fp8: unsupported shape M=" << M << " N=" << N << " K=" << K);
   const int tiles = (M / kT) * (N / kT);
-  hipLaunchKernelGGL(gemm_4wave_fp8_kernel, tiles, 256, 0, static_cast<hipStream_t>(stream),
+  static const int group = static_cast<int>(std::max<long long>(1, env_int("DLNB_GEMM_GROUP", 8)));
+  hipLaunchKernelGGL(gemm_4wave_fp8_kernel<false>, tiles, 256, 0, static_cast<hipStream_t>(stream),
                      static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda,
-                     ldb, ldc);
+                     ldb, ldc, group, nullptr, 0u, 0ull, 0ull, nullptr);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 4-wave fp8 launch failed: " << hipGetErrorString(e));
+}
+
+void gemm_tn_4wave_fp8_deadline(const void* A, const void* B, void* C, int M, int N, int K, uint64_t ticks,
+                                uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
+                                uint64_t* tstart) {
+  DLNB_REQUIRE(gemm_4wave_fp8_shape_ok(M, N, K, DType::FP8_E4M3), "gemm 4-wave fp8 deadline: unsupported shape");
+  hipLaunchKernelGGL(gemm_4wave_fp8_kernel<true>, grid, 256, 0, static_cast<hipStream_t>(stream),
+                     static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, K, K,
+                     N, 8, slot, epoch, ticks, slice_end, tstart);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) DLNB_THROW("gemm 4-wave fp8 deadline launch failed: " << hipGetErrorString(e));
 }
 
 }  // namespace kernels

@@ -672,6 +672,11 @@ void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K
   if (slice_end == 0) slice_end = ticks;
   DLNB_REQUIRE(gemm_shape_ok(M, N, K, in_t), "gemm_tn_deadline: unsupported shape");
   DLNB_REQUIRE(slot != nullptr && grid > 0 && epoch > 0 && epoch < 65536, "gemm_tn_deadline: bad slot/grid/epoch");
+  // fp8: the one-wave-per-SIMD MX kernel where it applies (DLNB_GEMM_FP8_DL_4WAVE=0: the 8-phase one)
+  if (gemm_8phase_enabled() && gemm_4wave_fp8_shape_ok(M, N, K, in_t) && env_int("DLNB_GEMM_FP8_DL_4WAVE", 1) != 0) {
+    gemm_tn_4wave_fp8_deadline(A, B, C, M, N, K, ticks, slot, epoch, grid, stream, slice_end, tstart);
+    return;
+  }
   if (gemm_8phase_enabled() && gemm_8phase_shape_ok(M, N, K, in_t)) {
     gemm_tn_8phase_deadline(A, B, C, M, N, K, in_t, ticks, slot, epoch, grid, stream, slice_end, tstart);
     return;
