@@ -709,7 +709,7 @@ void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N
   // bf16, short K (<= 16 K-tiles): the streaming kernel, whose per-tile
   // pipeline fill / drain savings outweigh its per-phase wait-count branch
   // only there; long K: the per-tile loop (profiles/gemm_deadline_stream_r2.md).
-  // DLNB_GEMM_STREAM=0|1 and DLNB_GEMM_FP8_DL_UNIFORM=0|1 force a choice.
+  // DLNB_GEMM_STREAM=0|1, DLNB_GEMM_FP8_DL_UNIFORM=0|1 and DLNB_GEMM_BF16_DL_BAL=0|1 force a choice.
   const int nk = static_cast<int>(static_cast<size_t>(K) * dtype_size(in_t) / kRB);
   const long long force = env_int("DLNB_GEMM_STREAM", -1);
   const bool fp8_uniform = in_t != DType::BF16 && env_int("DLNB_GEMM_FP8_DL_UNIFORM", 1) != 0;
@@ -721,6 +721,11 @@ void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N
     else
       hipLaunchKernelGGL((gemm_8phase_stream_kernel<true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
                          ticks, slice_end, tstart);
+  } else if (in_t == DType::BF16 && nk % 2 == 0 && env_int("DLNB_GEMM_BF16_DL_BAL", 1) != 0) {
+    // bf16, long K: balanced reads (236 VGPRs, no spills with the buffer_load
+    // staging): 1354 vs 1288 TF/s sustained (scripts/probes/deadline_rate_bal.sh)
+    hipLaunchKernelGGL((gemm_8phase_kernel<false, true, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot,
+                       epoch, ticks, slice_end, tstart);
   } else if (in_t == DType::BF16) {
     hipLaunchKernelGGL((gemm_8phase_kernel<false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
                        ticks, slice_end, tstart);
