@@ -204,6 +204,19 @@ __device__ __forceinline__ bool tile4(CtxF& c, const char* __restrict__ A, const
                                       int lane, const DeadlineF& d) {
   const int wr = c.w >> 1, wc = c.w & 1;
   const int r16 = lane & 15, h = lane >> 4;
+  if constexpr (DL) {
+    // Tile boundary check: a deadline that passes during the previous tile's
+    // epilogue must not cost a whole prologue + first K-tile (measured: 512
+    // instead of 500 us per 500-us slice at the ViT-H FFN shape). flag[2] is
+    // rewritten only after this tile's last barrier.
+    if (d.tid == 0) {
+      const uint64_t el = (__builtin_amdgcn_s_memrealtime() - d.t0) & ((1ull << 48) - 1);
+      d.flag[2] = el >= d.ticks || el >= d.slice_end;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    raw_barrier();
+    if (__builtin_amdgcn_readfirstlane(d.flag[2]) != 0) return false;
+  }
   c.ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(A) + static_cast<size_t>(tm) * kT * lda, 0, 0x7ffffff0,
                                            0x00020000);
   c.rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(B) + static_cast<size_t>(tn) * kT * ldb, 0, 0x7ffffff0,

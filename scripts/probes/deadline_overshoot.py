@@ -1,32 +1,36 @@
-"""Where a deadline GEMM's extra time goes: device-clock stamps around gemm_deadline_us.
-
-For each launch: s0 = stamp before, t0 = first block's start (the epoch slot's low 48 bits),
-s1 = stamp after. start latency = t0 - s0, overshoot = s1 - (t0 + ticks). 100 MHz ticks -> us.
-DLNB_GEMM_8PHASE=0|1 selects the kernel."""
+"""Deadline accuracy of the persistent GEMM stand-in per shape: event-timed duration of
+gemm_deadline_us(500 us) (median of 20), for bf16 and fp8 at the llama3-8B FFN and ViT-H FFN
+shapes. Prints one JSON line per case."""
+import json
+import statistics
 import sys
-import torch
-sys.path.insert(0, ".")
-from dlnetbench_amd.ops import gemm
 
-a = torch.empty(8192, 4096, device="cuda", dtype=torch.bfloat16)
-b = torch.empty(14336, 4096, device="cuda", dtype=torch.bfloat16)
-gemm.fill_random_(a, 1)
-gemm.fill_random_(b, 2)
-c = torch.empty(8192, 14336, device="cuda", dtype=torch.bfloat16)
-slot = torch.zeros(8, dtype=torch.int64, device="cuda")
-st = torch.zeros(8, dtype=torch.int64, device="cuda")
-for us in (100.0, 500.0, 2000.0):
-    lat, over = [], []
-    for rep in range(8):
-        gemm.stamp_(st, 0)
-        gemm.gemm_deadline_us(a, b, c, us, slot)
-        gemm.stamp_(st, 1)
-        torch.cuda.synchronize()
-        s0, s1 = st[0].item(), st[1].item()
-        t0 = slot[0].item() & ((1 << 48) - 1)
-        s0 &= (1 << 48) - 1
-        s1 &= (1 << 48) - 1
-        lat.append((t0 - s0) / 100.0)
-        over.append((s1 - t0) / 100.0 - us)
-    print(f"us={us}: start latency {sorted(lat)[4]:.2f} us (min {min(lat):.2f}), "
-          f"overshoot median {sorted(over)[4]:.2f} us (min {min(over):.2f}, max {max(over):.2f})", flush=True)
+import torch
+
+sys.path.insert(0, ".")
+from dlnetbench_amd.ops import gemm  # noqa: E402
+
+US = 500.0
+for dt in ("bf16", "fp8"):
+    for (M, N, K) in ((8192, 14336, 4096), (8192, 5120, 1280), (8192, 1280, 5120)):
+        a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
+        b = torch.empty(N, K, device="cuda", dtype=torch.bfloat16)
+        gemm.fill_random_(a, 1)
+        gemm.fill_random_(b, 2)
+        if dt == "fp8":
+            a, b = a.to(torch.float8_e4m3fn), b.to(torch.float8_e4m3fn)
+        c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        stamp = torch.zeros(8, dtype=torch.int64, device="cuda")
+        s = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(3):
+            gemm.gemm_deadline_us(a, b, c, US, stamp)
+        t = []
+        for _ in range(20):
+            e0.record(s)
+            gemm.gemm_deadline_us(a, b, c, US, stamp)
+            e1.record(s)
+            torch.cuda.synchronize()
+            t.append(e0.elapsed_time(e1) * 1e3)
+        print(json.dumps({"dtype": dt, "shape": f"{M}x{N}x{K}", "target_us": US, "median_us": round(statistics.median(t), 1),
+                          "max_us": round(max(t), 1)}), flush=True)
