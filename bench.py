@@ -124,7 +124,9 @@ def _xgmi_ab(a: argparse.Namespace, world: int, rank: int, c5: dict) -> Dict[str
     env = dict(os.environ, DLNB_XGMI_TIMEOUT_S=os.environ.get("DLNB_XGMI_TIMEOUT_S", "20"))
     res: Dict[str, Any] = {"backend": "XGMI", "hip_graph": True}
     try:
-        p = subprocess.run([os.path.join(ROOT, "build", "bin", "dp"), *args], env=env, timeout=240,
+        # ~10 s expected (55 iterations of ~7.5 ms + setup); bounded well below any driver limit so a
+        # first-time cross-device xgmi failure costs a minute and the headline line still prints
+        p = subprocess.run([os.path.join(ROOT, "build", "bin", "dp"), *args], env=env, timeout=90,
                            stdout=sys.stderr, stderr=subprocess.PIPE, text=True)
         if p.returncode != 0:
             return {"error": f"exit {p.returncode}: " + (p.stderr or "")[-300:]}
