@@ -45,9 +45,11 @@ bool gemm_shape_ok(int M, int N, int K, DType in_t);
 // double buffered, 2 = the same with software-pipelined fragment reads
 // (bf16), 1 = 8 waves with a 3-deep A ring (160 KiB LDS), 4 = 4 waves (1 per
 // SIMD, 128x128 per wave), 6 = 8-phase with balanced fragment reads (bf16;
-// even K-tile counts, else 3); 0 = the default: 6 (bf16) / 3 (fp8) where it
-// applies (>= 2 K-tiles), else 2 for bf16 / 8 for fp8 (ring if
-// DLNB_GEMM_RING=1, 4 waves if DLNB_GEMM_WAVES=4).
+// even K-tile counts, else 3), 7 / 9 = 8-phase balanced / plain with one
+// uniform K-tile body, 5 = one wave per SIMD with AGPR accumulators (below);
+// 0 = the default: bf16 6, fp8 5 (K % 256 == 0) else 9, where they apply
+// (>= 2 K-tiles), else 2 for bf16 / 8 for fp8 (ring if DLNB_GEMM_RING=1, 4
+// waves if DLNB_GEMM_WAVES=4).
 // 3 = the 8-phase ping-pong schedule (gemm_8phase.hip; needs >= 2 K-tiles).
 void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
              void* stream, int waves = 0);
