@@ -151,17 +151,21 @@ __device__ __forceinline__ bool ktile(const CtxF& c, int t, int wr, int wc, int 
   for (int g = 0; g < 32; ++g) {
     const int i = g >> 2, j = (g & 3) * 2;
     if constexpr (DL) {
-      // clock read early (scalar-memory latency hidden behind 15 MFMA pairs),
-      // flag written late; the mid wait's lgkmcnt(0) lands it before the barrier
+      // clock read early (scalar-memory latency hidden behind 8 MFMA pairs);
+      // the flag write is followed by exactly 8 LDS reads (pairs 8-15), so the
+      // mid wait's lgkmcnt(8) lands it before the barrier
       if (g == 0) now = __builtin_amdgcn_s_memrealtime();
-      if (g == 15 && d.tid == 0) {
+      if (g == 8 && d.tid == 0) {
         const uint64_t el = (now - d.t0) & ((1ull << 48) - 1);
         d.flag[t & 1] = el >= d.ticks || el >= d.slice_end;
       }
     }
     if (g == 16) {
-      wait_vm<8>();                        // A(t+1) landed (B(t+2) may be in flight)
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's A(t) reads are done
+      wait_vm<8>();  // A(t+1) landed (B(t+2) may be in flight)
+      // lgkmcnt(8): this wave's A(t) reads (the last, a[7], in pairs 0-1) are
+      // done; the B(t+1) reads of pairs 8-15 may still be in flight (lgkmcnt(0)
+      // here stalled on the reads just issued)
+      __builtin_amdgcn_s_waitcnt(0xc87f);
       raw_barrier();
       if constexpr (DL) stop = __builtin_amdgcn_readfirstlane(d.flag[t & 1]) != 0;
     }
