@@ -75,10 +75,12 @@ __device__ __forceinline__ int xcd_remap(int b, int T) {
 
 struct CtxF {
   __amdgpu_buffer_rsrc_t ra, rb;  // A / B rows of the block tile
+  __amdgpu_buffer_rsrc_t ran, rbn;  // the next tile's (streaming kernel; has_next)
   int voffA, voffB;               // lane offset within a staging instruction
   int lda, ldb;                   // bytes
   char* smem;
   int w, last_kt;
+  int has_next = 0;  // K-tiles past the last stage the next tile's K-tiles 0, 1 (else clamped copies)
 };
 
 // Piece p (0..7) of operand op's (0 A, 1 B) half-tiles of K-tile kt (clamped
@@ -86,10 +88,13 @@ struct CtxF {
 // (8 rows x 128 B; instruction i covers rows 32 i + 8 w + lane / 8 of the half).
 __device__ __forceinline__ void stage_piece(const CtxF& c, int kt, int op, int p) {
   const int half = p >> 2, i = p & 3;
-  const int tk = min(kt, c.last_kt);
+  const bool past = kt > c.last_kt;
+  const bool nxt = past && c.has_next;  // the next tile's K-tile kt - nk (same buffer parity: nk even)
+  const int tk = nxt ? kt - c.last_kt - 1 : min(kt, c.last_kt);
   const int ld = op ? c.ldb : c.lda;
   char* lds = c.smem + (kt & 1) * kBuf + (op * 2 + half) * kHalf + (i * 4 + c.w) * 1024;
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(op ? c.rb : c.ra, (lds_ptr_t)lds, 16, op ? c.voffB : c.voffA,
+  const __amdgpu_buffer_rsrc_t rs = op ? (nxt ? c.rbn : c.rb) : (nxt ? c.ran : c.ra);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)lds, 16, op ? c.voffB : c.voffA,
                                            tk * kRB + (half * 128 + i * 32) * ld, 0, 0);
 }
 
@@ -136,14 +141,23 @@ struct DeadlineF {
 // K-tile t+1's). READ7: read this K-tile's a[7] (every K-tile but a tile's
 // first, whose fragments the prologue read). Returns (DL) whether the
 // deadline has passed; a stopped K-tile has issued every load it would have.
-template <int PAR, bool FIRST, bool DL>
+// READ7: read this K-tile's a[7] (false only for a tile whose prologue read
+// every fragment). VM < 0 (the streaming kernel's K-tile 0): the two vmcnt
+// waits are 63 when after_store (the previous tile's 64 stores are younger
+// than the loads waited for and would not fit the counter), else 8 - a
+// uniform branch, not a second instantiation of the K-tile body.
+template <int PAR, bool FIRST, bool DL, bool READ7 = !FIRST, int VM = 8>
 __device__ __forceinline__ bool ktile(const CtxF& c, int t, int wr, int wc, int offl, int offh, FragF (&a)[8],
-                                      FragF (&b)[2][8], f32x4 (&acc)[8][8], int scale, const DeadlineF& d) {
+                                      FragF (&b)[2][8], f32x4 (&acc)[8][8], int scale, const DeadlineF& d,
+                                      bool after_store = false) {
   const char* cbuf = c.smem + (t & 1) * kBuf;
   const char* nbuf = c.smem + ((t + 1) & 1) * kBuf;
   const char* na = nbuf + wr * kHalf;
   const char* nb = nbuf + (2 + wc) * kHalf;
-  wait_vm<8>();  // B(t+1) landed (A(t+1) may be in flight)
+  if (VM >= 0 || !after_store)  // B(t+1) landed (A(t+1) may be in flight)
+    wait_vm<(VM >= 0 ? VM : 8)>();
+  else
+    wait_vm<63>();
   raw_barrier();
   bool stop = false;
   uint64_t now = 0;
@@ -161,7 +175,10 @@ __device__ __forceinline__ bool ktile(const CtxF& c, int t, int wr, int wc, int 
       }
     }
     if (g == 16) {
-      wait_vm<8>();  // A(t+1) landed (B(t+2) may be in flight)
+      if (VM >= 0 || !after_store)  // A(t+1) landed (B(t+2) may be in flight)
+        wait_vm<(VM >= 0 ? VM : 8)>();
+      else
+        wait_vm<63>();
       // lgkmcnt(8): this wave's A(t) reads (the last, a[7], in pairs 0-1) are
       // done; the B(t+1) reads of pairs 8-15 may still be in flight (lgkmcnt(0)
       // here stalled on the reads just issued)
@@ -174,8 +191,8 @@ __device__ __forceinline__ bool ktile(const CtxF& c, int t, int wr, int wc, int 
     // a[7] of THIS K-tile: read here, not right after the MFMA that last read
     // the previous a[7] (its K-tile's A region is restaged only after the mid
     // barrier, which waits for this read)
-    if (!FIRST && g == 0) a[7].lo = read_part(cbuf + wr * kHalf, offl, offh, 7, 0);
-    if (!FIRST && g == 1) a[7].hi = read_part(cbuf + wr * kHalf, offl, offh, 7, 1);
+    if (READ7 && g == 0) a[7].lo = read_part(cbuf + wr * kHalf, offl, offh, 7, 0);
+    if (READ7 && g == 1) a[7].hi = read_part(cbuf + wr * kHalf, offl, offh, 7, 1);
     if (g < 16) {
       // B(t+1): fragment g / 2, part g % 2
       if ((g & 1) == 0)
@@ -349,6 +366,129 @@ __global__ void __launch_bounds__(256, 1)
   }
 }
 
+
+// Streaming one-shot kernel (persistent: grid <= tiles, block b computes tiles
+// b, b + grid, ...). A block's tiles form one K-tile stream: the last two
+// K-tiles of a tile stage the next tile's K-tiles 0 and 1 and the last one
+// reads its K-tile-0 fragments, so the next tile starts without a prologue
+// (no exposed load latency); the 64 accumulator stores of a tile sit between
+// its last K-tile and the next tile's first, whose waits use vmcnt(63).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const char* base, int tile_row, int ld) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base) + static_cast<size_t>(tile_row) * kT * ld, 0,
+                                           0x7ffffff0, 0x00020000);
+}
+
+__global__ void __launch_bounds__(256, 1)
+    gemm_4wave_fp8_stream_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C,
+                                 int M, int N, int K, int lda, int ldb, int ldc, int group) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
+  const int tid = threadIdx.x;
+  CtxF c;
+  const int lane = tid & 63;
+  c.w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = c.w >> 1, wc = c.w & 1;
+  const int r16 = lane & 15, h = lane >> 4;
+  c.smem = smem;
+  c.lda = lda;
+  c.ldb = ldb;
+  {
+    const int r = c.w * 8 + (lane >> 3);
+    const int q = (lane & 7) ^ ((r >> 1) & 7);
+    c.voffA = r * lda + (q << 4);
+    c.voffB = r * ldb + (q << 4);
+  }
+  const int nt_m = M / kT, nt_n = N / kT, T = nt_m * nt_n;
+  const int G = gridDim.x;
+  int cur = blockIdx.x;  // host: grid <= T
+  int tm, tn, tmn = 0, tnn = 0;
+  tile_coords(xcd_remap(cur, T), nt_m, nt_n, group, tm, tn);
+  c.ra = rows_rsrc(A, tm, lda);
+  c.rb = rows_rsrc(B, tn, ldb);
+  c.has_next = cur + G < T;
+  if (c.has_next) {
+    tile_coords(xcd_remap(cur + G, T), nt_m, nt_n, group, tmn, tnn);
+    c.ran = rows_rsrc(A, tmn, lda);
+    c.rbn = rows_rsrc(B, tnn, ldb);
+  }
+  const int nk = K / kRB;  // even, >= 2
+  c.last_kt = nk - 1;
+  const int x = (r16 >> 1) & 7;
+  const int offl = r16 * kRB + ((h ^ x) << 4), offh = offl ^ 64;
+  int scale = 127;
+  asm volatile("" : "+v"(scale));
+  const DeadlineF d{0, 0, 0, nullptr, tid};
+
+  f32x4 acc[8][8];
+  FragF a[8], b[2][8];
+
+#pragma unroll
+  for (int p = 0; p < 8; ++p) stage_piece(c, 0, 1, p);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) stage_piece(c, 0, 0, p);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) stage_piece(c, 1, 1, p);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) stage_piece(c, 1, 0, p);
+  wait_vm<16>();
+  raw_barrier();
+#pragma unroll
+  for (int f = 0; f < 8; ++f) {
+    a[f].lo = read_part(smem + wr * kHalf, offl, offh, f, 0);
+    a[f].hi = read_part(smem + wr * kHalf, offl, offh, f, 1);
+    b[0][f].lo = read_part(smem + (2 + wc) * kHalf, offl, offh, f, 0);
+    b[0][f].hi = read_part(smem + (2 + wc) * kHalf, offl, offh, f, 1);
+  }
+  bool first = true;
+  for (;;) {
+    // (the first tile re-reads the a[7] its prologue read: same data)
+    ktile<0, true, false, true, -1>(c, 0, wr, wc, offl, offh, a, b, acc, scale, d, !first);
+    for (int t = 1; t < nk - 1; t += 2) {
+      ktile<1, false, false>(c, t, wr, wc, offl, offh, a, b, acc, scale, d);
+      ktile<0, false, false>(c, t + 1, wr, wc, offl, offh, a, b, acc, scale, d);
+    }
+    ktile<1, false, false>(c, nk - 1, wr, wc, offl, offh, a, b, acc, scale, d);
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
+                 : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[7][4]),
+                   "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7]));
+    {
+      // the lane's element offset made opaque, so the compiler cannot hoist
+      // the 64 store addresses out of the tile loop (they would stay live
+      // across it and spill)
+      size_t lo = static_cast<size_t>(wr * 128 + r16) * ldc + wc * 128 + 4 * h;
+      asm volatile("" : "+v"(lo));
+      __bf16* base = C + static_cast<size_t>(tm) * kT * ldc + static_cast<size_t>(tn) * kT + lo;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const f32x4 v = acc[i][j];
+          bf16x4 o;
+          o[0] = static_cast<__bf16>(v[0]);
+          o[1] = static_cast<__bf16>(v[1]);
+          o[2] = static_cast<__bf16>(v[2]);
+          o[3] = static_cast<__bf16>(v[3]);
+          *reinterpret_cast<bf16x4*>(base + static_cast<size_t>(i * 16) * ldc + j * 16) = o;
+        }
+    }
+    if (!c.has_next) break;
+    // advance the stream: the next tile's K-tiles 0, 1 are staged, its K-tile-0
+    // fragments (but a[7]) read
+    cur += G;
+    tm = tmn;
+    tn = tnn;
+    c.ra = c.ran;
+    c.rb = c.rbn;
+    c.has_next = cur + G < T;
+    if (c.has_next) {
+      tile_coords(xcd_remap(cur + G, T), nt_m, nt_n, group, tmn, tnn);
+      c.ran = rows_rsrc(A, tmn, lda);
+      c.rbn = rows_rsrc(B, tnn, ldb);
+    }
+    first = false;
+  }
+  wait_vm<0>();  // the last tile's clamped staging copies
+}
+
 }  // namespace
 
 bool gemm_4wave_fp8_shape_ok(int M, int N, int K, DType in_t) {
@@ -361,6 +501,21 @@ void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int 
                "gemm 4-wave fp8: unsupported shape M=" << M << " N=" << N << " K=" << K);
   const int tiles = (M / kT) * (N / kT);
   static const int group = static_cast<int>(std::max<long long>(1, env_int("DLNB_GEMM_GROUP", 8)));
+  // more tiles than CUs: the streaming persistent kernel, one block per CU
+  // (+1-5 %, profiles/gemm_bench_r2.md); DLNB_GEMM_FP8_STREAM=0: a block per tile
+  const bool stream_on = env_int("DLNB_GEMM_FP8_STREAM", 1) != 0;
+  static const int cus = [] {
+    int dev = 0;
+    return hipGetDevice(&dev) == hipSuccess ? num_cus(dev) : 256;
+  }();
+  if (stream_on && tiles > cus) {
+    hipLaunchKernelGGL(gemm_4wave_fp8_stream_kernel, cus, 256, 0, static_cast<hipStream_t>(stream),
+                       static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K,
+                       lda, ldb, ldc, group);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) DLNB_THROW("gemm 4-wave fp8 stream launch failed: " << hipGetErrorString(e));
+    return;
+  }
   hipLaunchKernelGGL(gemm_4wave_fp8_kernel<false>, tiles, 256, 0, static_cast<hipStream_t>(stream),
                      static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda,
                      ldb, ldc, group, nullptr, 0u, 0ull, 0ull, nullptr);

@@ -64,6 +64,22 @@ def test_gemm_fp8_matches_torch(M, N, K, waves):
     assert_close_bf16_out(c, a.float() @ b.float().t())
 
 
+@pytest.mark.skipif(not hasattr(torch, "float8_e4m3fn"), reason="torch without float8")
+@pytest.mark.parametrize("stream", ["0", "1"])
+@pytest.mark.parametrize("M,N,K", [(4096, 4352, 512), (8192, 8192, 256), (2048, 8448, 1280)])
+def test_gemm_fp8_many_tiles(M, N, K, stream, monkeypatch):
+    """More tiles than CUs: the one-wave-per-SIMD fp8 kernel one block per tile (stream 0) and as the
+    streaming persistent kernel (stream 1: a block's tiles as one K-tile stream, the next tile's first
+    K-tiles staged during the current one's last, K = 256 the 2-K-tile minimum)."""
+    monkeypatch.setenv("DLNB_GEMM_FP8_STREAM", stream)
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    a = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(torch.float8_e4m3fn)
+    b = (torch.randn(N, K, device="cuda", generator=g) * 0.5).to(torch.float8_e4m3fn)
+    c = gemm.gemm_tn(a, b)
+    torch.cuda.synchronize()
+    assert_close_bf16_out(c, a.float() @ b.float().t())
+
+
 def test_fill_random_uniform():
     t = torch.empty(1 << 20, device="cuda", dtype=torch.bfloat16)
     gemm.fill_random_(t, seed=3)
