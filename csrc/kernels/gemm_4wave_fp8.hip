@@ -31,7 +31,12 @@
 //     the 8-phase kernel's XOR-swizzled image; staging by buffer_load ... lds
 //     with loop-invariant lane offsets (K-tile and row block in the scalar
 //     offset). Uniform loop: the last K-tiles stage / read clamped copies of
-//     the last one (never used).
+//     the last one (never used) - or, in the streaming kernel, the next
+//     tile's first K-tiles.
+//   * Kernels: gemm_4wave_fp8_kernel<false> (a block per tile),
+//     gemm_4wave_fp8_stream_kernel (persistent, a block's tiles as one K-tile
+//     stream; the one-shot default with more tiles than CUs) and
+//     gemm_4wave_fp8_kernel<true> (the persistent deadline compute stand-in).
 //
 // Variant 5 of dlnb::kernels::gemm_tn for fp8 (K a multiple of 256 bytes).
 #include <hip/hip_runtime.h>
@@ -217,6 +222,50 @@ __device__ __forceinline__ bool ktile(const CtxF& c, int t, int wr, int wc, int 
   return stop;
 }
 
+// A tile's prologue: stage B(0) A(0) B(1) A(1); once K-tile 0 has landed,
+// read all of its fragments (a[], b[0]).
+__device__ __forceinline__ void prologue(const CtxF& c, int wr, int wc, int offl, int offh, FragF (&a)[8],
+                                         FragF (&b)[2][8]) {
+#pragma unroll
+  for (int k = 0; k < 32; ++k) stage_piece(c, k >> 4, ((k >> 3) & 1) ^ 1, k & 7);  // kt, op (B first), piece
+  wait_vm<16>();
+  raw_barrier();
+#pragma unroll
+  for (int f = 0; f < 8; ++f) {
+    a[f].lo = read_part(c.smem + wr * kHalf, offl, offh, f, 0);
+    a[f].hi = read_part(c.smem + wr * kHalf, offl, offh, f, 1);
+    b[0][f].lo = read_part(c.smem + (2 + wc) * kHalf, offl, offh, f, 0);
+    b[0][f].hi = read_part(c.smem + (2 + wc) * kHalf, offl, offh, f, 1);
+  }
+}
+
+// Convert and store a tile's accumulators: lane holds C[m = .. + r16][n = ..
+// + 4h + 0..3] of each fragment. The MFMA D -> v_accvgpr_read wait states
+// come first (tied to the last row, so no read is hoisted above them); the
+// lane's element offset is made opaque so the 64 store addresses are not
+// hoisted out of a tile loop (they would stay live across it and spill).
+__device__ __forceinline__ void store_tile(f32x4 (&acc)[8][8], __bf16* __restrict__ C, int ldc, int tm, int tn, int wr,
+                                           int wc, int r16, int h) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
+               : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[7][4]),
+                 "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7]));
+  size_t lo = static_cast<size_t>(wr * 128 + r16) * ldc + wc * 128 + 4 * h;
+  asm volatile("" : "+v"(lo));
+  __bf16* base = C + static_cast<size_t>(tm) * kT * ldc + static_cast<size_t>(tn) * kT + lo;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f32x4 v = acc[i][j];
+      bf16x4 o;
+      o[0] = static_cast<__bf16>(v[0]);
+      o[1] = static_cast<__bf16>(v[1]);
+      o[2] = static_cast<__bf16>(v[2]);
+      o[3] = static_cast<__bf16>(v[3]);
+      *reinterpret_cast<bf16x4*>(base + static_cast<size_t>(i * 16) * ldc + j * 16) = o;
+    }
+}
+
 // One 256 x 256 tile of C. Returns false if the deadline stopped it (no
 // store; every staged load has been waited for).
 template <bool DL>
@@ -252,24 +301,7 @@ __device__ __forceinline__ bool tile4(CtxF& c, const char* __restrict__ A, const
   f32x4 acc[8][8];
   FragF a[8], b[2][8];
 
-  // Prologue: B(0) A(0) B(1) A(1); K-tile 0 landed -> its fragments.
-#pragma unroll
-  for (int p = 0; p < 8; ++p) stage_piece(c, 0, 1, p);
-#pragma unroll
-  for (int p = 0; p < 8; ++p) stage_piece(c, 0, 0, p);
-#pragma unroll
-  for (int p = 0; p < 8; ++p) stage_piece(c, 1, 1, p);
-#pragma unroll
-  for (int p = 0; p < 8; ++p) stage_piece(c, 1, 0, p);
-  wait_vm<16>();
-  raw_barrier();
-#pragma unroll
-  for (int f = 0; f < 8; ++f) {
-    a[f].lo = read_part(c.smem + wr * kHalf, offl, offh, f, 0);
-    a[f].hi = read_part(c.smem + wr * kHalf, offl, offh, f, 1);
-    b[0][f].lo = read_part(c.smem + (2 + wc) * kHalf, offl, offh, f, 0);
-    b[0][f].hi = read_part(c.smem + (2 + wc) * kHalf, offl, offh, f, 1);
-  }
+  prologue(c, wr, wc, offl, offh, a, b);
   bool stop = ktile<0, true, DL>(c, 0, wr, wc, offl, offh, a, b, acc, scale, d);
   for (int t = 1; t < nk - 1 && !stop; t += 2) {
     stop = ktile<1, false, DL>(c, t, wr, wc, offl, offh, a, b, acc, scale, d);
@@ -285,24 +317,7 @@ __device__ __forceinline__ bool tile4(CtxF& c, const char* __restrict__ A, const
   if constexpr (DL) {
     if (stop) return false;
   }
-  // MFMA D -> v_accvgpr_read wait states (tied: no reader hoisted above it)
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
-               : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[7][4]),
-                 "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7]));
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int m = tm * kT + wr * 128 + i * 16 + r16;
-      const int n = tn * kT + wc * 128 + j * 16 + 4 * h;
-      const f32x4 v = acc[i][j];
-      bf16x4 o;
-      o[0] = static_cast<__bf16>(v[0]);
-      o[1] = static_cast<__bf16>(v[1]);
-      o[2] = static_cast<__bf16>(v[2]);
-      o[3] = static_cast<__bf16>(v[3]);
-      *reinterpret_cast<bf16x4*>(C + static_cast<size_t>(m) * ldc + n) = o;
-    }
+  store_tile(acc, C, ldc, tm, tn, wr, wc, r16, h);
   return true;
 }
 
@@ -421,23 +436,7 @@ __global__ void __launch_bounds__(256, 1)
   f32x4 acc[8][8];
   FragF a[8], b[2][8];
 
-#pragma unroll
-  for (int p = 0; p < 8; ++p) stage_piece(c, 0, 1, p);
-#pragma unroll
-  for (int p = 0; p < 8; ++p) stage_piece(c, 0, 0, p);
-#pragma unroll
-  for (int p = 0; p < 8; ++p) stage_piece(c, 1, 1, p);
-#pragma unroll
-  for (int p = 0; p < 8; ++p) stage_piece(c, 1, 0, p);
-  wait_vm<16>();
-  raw_barrier();
-#pragma unroll
-  for (int f = 0; f < 8; ++f) {
-    a[f].lo = read_part(smem + wr * kHalf, offl, offh, f, 0);
-    a[f].hi = read_part(smem + wr * kHalf, offl, offh, f, 1);
-    b[0][f].lo = read_part(smem + (2 + wc) * kHalf, offl, offh, f, 0);
-    b[0][f].hi = read_part(smem + (2 + wc) * kHalf, offl, offh, f, 1);
-  }
+  prologue(c, wr, wc, offl, offh, a, b);
   bool first = true;
   for (;;) {
     // (the first tile re-reads the a[7] its prologue read: same data)
@@ -447,29 +446,7 @@ __global__ void __launch_bounds__(256, 1)
       ktile<0, false, false>(c, t + 1, wr, wc, offl, offh, a, b, acc, scale, d);
     }
     ktile<1, false, false>(c, nk - 1, wr, wc, offl, offh, a, b, acc, scale, d);
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
-                 : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[7][4]),
-                   "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7]));
-    {
-      // the lane's element offset made opaque, so the compiler cannot hoist
-      // the 64 store addresses out of the tile loop (they would stay live
-      // across it and spill)
-      size_t lo = static_cast<size_t>(wr * 128 + r16) * ldc + wc * 128 + 4 * h;
-      asm volatile("" : "+v"(lo));
-      __bf16* base = C + static_cast<size_t>(tm) * kT * ldc + static_cast<size_t>(tn) * kT + lo;
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const f32x4 v = acc[i][j];
-          bf16x4 o;
-          o[0] = static_cast<__bf16>(v[0]);
-          o[1] = static_cast<__bf16>(v[1]);
-          o[2] = static_cast<__bf16>(v[2]);
-          o[3] = static_cast<__bf16>(v[3]);
-          *reinterpret_cast<bf16x4*>(base + static_cast<size_t>(i * 16) * ldc + j * 16) = o;
-        }
-    }
+    store_tile(acc, C, ldc, tm, tn, wr, wc, r16, h);
     if (!c.has_next) break;
     // advance the stream: the next tile's K-tiles 0, 1 are staged, its K-tile-0
     // fragments (but a[7]) read
