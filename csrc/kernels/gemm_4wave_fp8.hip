@@ -329,6 +329,25 @@ __device__ __forceinline__ void tile_coords(int bid, int nt_m, int nt_n, int gro
   tn = (bid % per_group) / gsz;
 }
 
+// The deadline's t0, agreed per task epoch: the first block to arrive
+// publishes its start {epoch:16 | t0:48} in *slot (and stamps *tstart); every
+// other block of that epoch reads it back.
+__device__ __forceinline__ uint64_t agree_t0(uint64_t* slot, uint32_t epoch, uint64_t* tstart) {
+  constexpr uint64_t kMask48 = (1ull << 48) - 1;
+  const uint64_t raw = __builtin_amdgcn_s_memrealtime();
+  const uint64_t mine = (static_cast<uint64_t>(epoch) << 48) | (raw & kMask48);
+  uint64_t cur = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while ((cur >> 48) != epoch) {
+    if (__hip_atomic_compare_exchange_strong(slot, &cur, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)) {
+      cur = mine;
+      if (tstart) __hip_atomic_store(tstart, raw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+  }
+  return cur & kMask48;
+}
+
 // DL = false: one launch, grid = tiles. DL = true: persistent stand-in
 // compute with gemm_tn_deadline's contract (kernels.hip): grid <= resident
 // blocks walks the tiles round-robin and stops min(ticks, slice_end) after t0,
@@ -359,21 +378,7 @@ __global__ void __launch_bounds__(256, 1)
     tile_coords(xcd_remap(blockIdx.x, T), nt_m, nt_n, group, tm, tn);
     tile4<false>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d);
   } else {
-    constexpr uint64_t kMask48 = (1ull << 48) - 1;
-    if (tid == 0) {
-      const uint64_t raw = __builtin_amdgcn_s_memrealtime();
-      const uint64_t mine = (static_cast<uint64_t>(epoch) << 48) | (raw & kMask48);
-      uint64_t cur = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      while ((cur >> 48) != epoch) {
-        if (__hip_atomic_compare_exchange_strong(slot, &cur, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT)) {
-          cur = mine;
-          if (tstart) __hip_atomic_store(tstart, raw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-      }
-      d.t0 = cur & kMask48;  // only thread 0 reads the clock
-    }
+    if (tid == 0) d.t0 = agree_t0(slot, epoch, tstart);  // only thread 0 reads the clock
     for (int round = 0;; ++round) {
       tile_coords(xcd_remap((blockIdx.x + round * gridDim.x) % T, T), nt_m, nt_n, group, tm, tn);
       if (!tile4<true>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d)) return;
@@ -382,21 +387,26 @@ __global__ void __launch_bounds__(256, 1)
 }
 
 
-// Streaming one-shot kernel (persistent: grid <= tiles, block b computes tiles
-// b, b + grid, ...). A block's tiles form one K-tile stream: the last two
-// K-tiles of a tile stage the next tile's K-tiles 0 and 1 and the last one
-// reads its K-tile-0 fragments, so the next tile starts without a prologue
-// (no exposed load latency); the 64 accumulator stores of a tile sit between
-// its last K-tile and the next tile's first, whose waits use vmcnt(63).
+// Streaming kernel (persistent: block b computes tiles b, b + grid, ...; DL:
+// round-robin over the tile space until the deadline). A block's tiles form
+// one K-tile stream: the last two K-tiles of a tile stage the next tile's
+// K-tiles 0 and 1 and the last one reads its K-tile-0 fragments, so the next
+// tile starts without a prologue (no exposed load latency); the 64
+// accumulator stores of a tile sit between its last K-tile and the next
+// tile's first, whose waits use vmcnt(63). DL: a stop (decided at a mid
+// K-tile barrier, uniform over the block) drains the loads in flight and
+// leaves without storing.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const char* base, int tile_row, int ld) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base) + static_cast<size_t>(tile_row) * kT * ld, 0,
                                            0x7ffffff0, 0x00020000);
 }
 
+template <bool DL>
 __global__ void __launch_bounds__(256, 1)
     gemm_4wave_fp8_stream_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C,
-                                 int M, int N, int K, int lda, int ldb, int ldc, int group) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
+                                 int M, int N, int K, int lda, int ldb, int ldc, int group, uint64_t* __restrict__ slot,
+                                 uint32_t epoch, uint64_t ticks, uint64_t slice_end, uint64_t* __restrict__ tstart) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + 16];  // ONE array: staging + deadline flags
   const int tid = threadIdx.x;
   CtxF c;
   const int lane = tid & 63;
@@ -414,14 +424,21 @@ __global__ void __launch_bounds__(256, 1)
   }
   const int nt_m = M / kT, nt_n = N / kT, T = nt_m * nt_n;
   const int G = gridDim.x;
-  int cur = blockIdx.x;  // host: grid <= T
+  DeadlineF d{0, ticks, slice_end, (lds_flag_t*)(smem + 2 * kBuf), tid};
+  if constexpr (DL) {
+    if (tid == 0) d.t0 = agree_t0(slot, epoch, tstart);  // only thread 0 reads the clock
+  }
+  // one-shot: grid <= T (host), the stream ends after the block's last tile;
+  // DL: tile indices wrap, the stream never ends before the deadline
+  int cur = DL ? blockIdx.x % T : blockIdx.x;
+  auto next_of = [&](int t) { return DL ? (t + G) % T : t + G; };
   int tm, tn, tmn = 0, tnn = 0;
   tile_coords(xcd_remap(cur, T), nt_m, nt_n, group, tm, tn);
   c.ra = rows_rsrc(A, tm, lda);
   c.rb = rows_rsrc(B, tn, ldb);
-  c.has_next = cur + G < T;
+  c.has_next = DL || next_of(cur) < T;
   if (c.has_next) {
-    tile_coords(xcd_remap(cur + G, T), nt_m, nt_n, group, tmn, tnn);
+    tile_coords(xcd_remap(next_of(cur), T), nt_m, nt_n, group, tmn, tnn);
     c.ran = rows_rsrc(A, tmn, lda);
     c.rbn = rows_rsrc(B, tnn, ldb);
   }
@@ -431,39 +448,39 @@ __global__ void __launch_bounds__(256, 1)
   const int offl = r16 * kRB + ((h ^ x) << 4), offh = offl ^ 64;
   int scale = 127;
   asm volatile("" : "+v"(scale));
-  const DeadlineF d{0, 0, 0, nullptr, tid};
 
   f32x4 acc[8][8];
   FragF a[8], b[2][8];
 
   prologue(c, wr, wc, offl, offh, a, b);
-  bool first = true;
+  bool first = true, stop = false;
   for (;;) {
     // (the first tile re-reads the a[7] its prologue read: same data)
-    ktile<0, true, false, true, -1>(c, 0, wr, wc, offl, offh, a, b, acc, scale, d, !first);
-    for (int t = 1; t < nk - 1; t += 2) {
-      ktile<1, false, false>(c, t, wr, wc, offl, offh, a, b, acc, scale, d);
-      ktile<0, false, false>(c, t + 1, wr, wc, offl, offh, a, b, acc, scale, d);
+    stop = ktile<0, true, DL, true, -1>(c, 0, wr, wc, offl, offh, a, b, acc, scale, d, !first);
+    for (int t = 1; t < nk - 1 && !stop; t += 2) {
+      stop = ktile<1, false, DL>(c, t, wr, wc, offl, offh, a, b, acc, scale, d);
+      if (!stop) stop = ktile<0, false, DL>(c, t + 1, wr, wc, offl, offh, a, b, acc, scale, d);
     }
-    ktile<1, false, false>(c, nk - 1, wr, wc, offl, offh, a, b, acc, scale, d);
+    if (!stop) stop = ktile<1, false, DL>(c, nk - 1, wr, wc, offl, offh, a, b, acc, scale, d);
+    if (DL && stop) break;  // partial tile: the stand-in result is not needed
     store_tile(acc, C, ldc, tm, tn, wr, wc, r16, h);
     if (!c.has_next) break;
     // advance the stream: the next tile's K-tiles 0, 1 are staged, its K-tile-0
     // fragments (but a[7]) read
-    cur += G;
+    cur = next_of(cur);
     tm = tmn;
     tn = tnn;
     c.ra = c.ran;
     c.rb = c.rbn;
-    c.has_next = cur + G < T;
+    c.has_next = DL || next_of(cur) < T;
     if (c.has_next) {
-      tile_coords(xcd_remap(cur + G, T), nt_m, nt_n, group, tmn, tnn);
+      tile_coords(xcd_remap(next_of(cur), T), nt_m, nt_n, group, tmn, tnn);
       c.ran = rows_rsrc(A, tmn, lda);
       c.rbn = rows_rsrc(B, tnn, ldb);
     }
     first = false;
   }
-  wait_vm<0>();  // the last tile's clamped staging copies
+  wait_vm<0>();  // the clamped / next-tile staging still in flight
 }
 
 }  // namespace
@@ -486,9 +503,9 @@ void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int 
     return hipGetDevice(&dev) == hipSuccess ? num_cus(dev) : 256;
   }();
   if (stream_on && tiles > cus) {
-    hipLaunchKernelGGL(gemm_4wave_fp8_stream_kernel, cus, 256, 0, static_cast<hipStream_t>(stream),
+    hipLaunchKernelGGL(gemm_4wave_fp8_stream_kernel<false>, cus, 256, 0, static_cast<hipStream_t>(stream),
                        static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K,
-                       lda, ldb, ldc, group);
+                       lda, ldb, ldc, group, nullptr, 0u, 0ull, 0ull, nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) DLNB_THROW("gemm 4-wave fp8 stream launch failed: " << hipGetErrorString(e));
     return;
@@ -504,6 +521,18 @@ void gemm_tn_4wave_fp8_deadline(const void* A, const void* B, void* C, int M, in
                                 uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
                                 uint64_t* tstart) {
   DLNB_REQUIRE(gemm_4wave_fp8_shape_ok(M, N, K, DType::FP8_E4M3), "gemm 4-wave fp8 deadline: unsupported shape");
+  // DLNB_GEMM_FP8_DL_STREAM=1: the streaming deadline kernel. Power-bound on
+  // the 224 CUs, it runs +5 % MFMA per clock at a 5 % lower clock: the same
+  // 2620-2630 TF/s as the per-tile kernel (0 spills vs 6), which stays the
+  // default (scripts/probes/deadline_rate_fp8_stream.sh)
+  if (env_int("DLNB_GEMM_FP8_DL_STREAM", 0) != 0) {
+    hipLaunchKernelGGL(gemm_4wave_fp8_stream_kernel<true>, grid, 256, 0, static_cast<hipStream_t>(stream),
+                       static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, K,
+                       K, N, 8, slot, epoch, ticks, slice_end, tstart);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) DLNB_THROW("gemm 4-wave fp8 deadline launch failed: " << hipGetErrorString(e));
+    return;
+  }
   hipLaunchKernelGGL(gemm_4wave_fp8_kernel<true>, grid, 256, 0, static_cast<hipStream_t>(stream),
                      static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, K, K,
                      N, 8, slot, epoch, ticks, slice_end, tstart);

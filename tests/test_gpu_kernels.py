@@ -148,8 +148,7 @@ def test_deadline_gemm_duration(us, dtype):
     assert us / 1e3 <= ms * 1.01 and ms <= us / 1e3 * 1.05 + 0.03, (us, times)
 
 
-@pytest.mark.parametrize("alt", ["0", "1"])
-@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+@pytest.mark.parametrize("dtype,alt", [("bf16", "0"), ("bf16", "1"), ("fp8", "0"), ("fp8", "1"), ("fp8", "2")])
 @pytest.mark.parametrize("M,N,K,grid", [(1024, 768, 512, 3), (512, 512, 256, 1), (256, 256, 256, 2),
                                         (768, 512, 1280, 0)])
 def test_deadline_gemm_numerics(M, N, K, grid, dtype, alt, monkeypatch):
@@ -158,9 +157,11 @@ def test_deadline_gemm_numerics(M, N, K, grid, dtype, alt, monkeypatch):
     tile's first K-tiles are staged while the current one finishes); fp8 the one-wave-per-SIMD MX
     kernel (alt 0) and the 8-phase one (alt 1). With a deadline long enough for several passes every
     tile of C holds a complete product: each one equals A.B^T. Small grids make every block cross many
-    tile boundaries (grid 0 = the default, CUs - 32)."""
+    tile boundaries (grid 0 = the default, CUs - 32). alt 2: fp8 the streaming one-wave-per-SIMD
+    deadline kernel (a block's tiles as one K-tile stream)."""
     monkeypatch.setenv("DLNB_GEMM_STREAM", alt if dtype == "bf16" else "0")
-    monkeypatch.setenv("DLNB_GEMM_FP8_DL_4WAVE", "1" if alt == "0" else "0")
+    monkeypatch.setenv("DLNB_GEMM_FP8_DL_4WAVE", "0" if alt == "1" else "1")
+    monkeypatch.setenv("DLNB_GEMM_FP8_DL_STREAM", "1" if alt == "2" else "0")
     if dtype == "fp8" and not hasattr(torch, "float8_e4m3fn"):
         pytest.skip("torch without float8")
     g = torch.Generator(device="cuda").manual_seed(M * 3 + N + K)
