@@ -74,9 +74,10 @@ int dlnb_gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int
   });
 }
 
-int dlnb_gemm_tn_waves(const void* A, const void* B, void* C, int M, int N, int K, int dtype, int waves, void* stream) {
+int dlnb_gemm_tn_waves(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, int dtype,
+                       int waves, void* stream) {
   return guard([&] {
-    dlnb::kernels::gemm_tn(A, B, C, M, N, K, K, K, N, static_cast<dlnb::DType>(dtype), stream, waves);
+    dlnb::kernels::gemm_tn(A, B, C, M, N, K, lda, ldb, ldc, static_cast<dlnb::DType>(dtype), stream, waves);
   });
 }
 

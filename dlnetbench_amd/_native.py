@@ -54,7 +54,7 @@ def lib() -> ctypes.CDLL:
     L.dlnb_parse_stats.restype = c_int
     L.dlnb_fill_random.argtypes = [c_vp, c_size, c_int, ctypes.c_ulonglong, c_vp]
     L.dlnb_gemm_tn.argtypes = [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]
-    L.dlnb_gemm_tn_waves.argtypes = [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp]
+    L.dlnb_gemm_tn_waves.argtypes = [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]
     L.dlnb_gemm_deadline_us.argtypes = [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_dbl, c_int, c_vp, c_int, c_vp]
     L.dlnb_gemm_shape_ok.argtypes = [c_int, c_int, c_int, c_int]
     L.dlnb_idle_wait_us.argtypes = [c_dbl, c_int, c_vp]

@@ -17,8 +17,10 @@ def _stream(t):
 def gemm_tn(a, b, out=None, waves: int = 0):
     """C[M,N] (bf16) = A[M,K] @ B[N,K]^T with the 256x256 MFMA kernel.
 
-    a, b: bf16 or float8_e4m3fn (OCP) CUDA tensors, row-major, K contiguous.
-    M and N must be multiples of 256; K*elem_size a multiple of 128 bytes.
+    a, b: bf16 or float8_e4m3fn (OCP) CUDA tensors, row-major with K contiguous;
+    rows may be strided (a view of a wider matrix: leading dimension = stride(0)).
+    M and N must be multiples of 256; K*elem_size a multiple of 128 bytes;
+    rows 16-byte aligned. out (optional) may be row-strided the same way.
     """
     import torch
     if a.dtype != b.dtype:
@@ -33,17 +35,18 @@ def gemm_tn(a, b, out=None, waves: int = 0):
     N, K2 = b.shape
     if K != K2:
         raise ValueError("K mismatch")
-    if not a.is_contiguous() or not b.is_contiguous():
-        raise ValueError("a and b must be contiguous")
+    if a.stride(1) != 1 or b.stride(1) != 1:
+        raise ValueError("a and b must be K-contiguous (row-major)")
     L = _native.lib()
     if not L.dlnb_gemm_shape_ok(M, N, K, dt):
         raise ValueError(f"unsupported shape M={M} N={N} K={K} (M,N % 256, K bytes % 128)")
     if out is None:
         out = torch.empty((M, N), device=a.device, dtype=torch.bfloat16)
-    if waves:
-        _native.check(L.dlnb_gemm_tn_waves(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, dt, waves, _stream(a)))
-    else:
-        _native.check(L.dlnb_gemm_tn(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, K, K, N, dt, _stream(a)))
+    if out.stride(1) != 1:
+        raise ValueError("out must be row-major")
+    lda, ldb, ldc = a.stride(0), b.stride(0), out.stride(0)
+    _native.check(L.dlnb_gemm_tn_waves(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, lda, ldb, ldc, dt, waves,
+                                       _stream(a)))
     return out
 
 

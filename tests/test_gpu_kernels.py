@@ -80,6 +80,29 @@ def test_gemm_fp8_many_tiles(M, N, K, stream, monkeypatch):
     assert_close_bf16_out(c, a.float() @ b.float().t())
 
 
+@pytest.mark.parametrize("dtype,waves", [("bf16", 0), ("bf16", 5), ("bf16", 3), ("fp8", 0), ("fp8", 5), ("fp8", 9)])
+def test_gemm_strided_operands(dtype, waves):
+    """Row-strided A, B and C (views of wider matrices: leading dimensions > K, > N): the staging lane
+    offsets and buffer resources use the leading dimensions, not K."""
+    if dtype == "fp8" and not hasattr(torch, "float8_e4m3fn"):
+        pytest.skip("torch without float8")
+    M, N, K = 512, 768, 512
+    g = torch.Generator(device="cuda").manual_seed(11)
+    A = torch.randn(M, K + 320, device="cuda", generator=g) * 0.5
+    B = torch.randn(N, K + 192, device="cuda", generator=g) * 0.5
+    if dtype == "fp8":
+        A, B = A.to(torch.float8_e4m3fn), B.to(torch.float8_e4m3fn)
+    else:
+        A, B = A.to(torch.bfloat16), B.to(torch.bfloat16)
+    a, b = A[:, 64:64 + K], B[:, 128:128 + K]
+    Cbig = torch.full((M, N + 256), float("nan"), device="cuda", dtype=torch.bfloat16)
+    c = Cbig[:, :N]
+    gemm.gemm_tn(a, b, c, waves=waves)
+    torch.cuda.synchronize()
+    assert_close_bf16_out(c, a.float() @ b.float().t())
+    assert torch.isnan(Cbig[:, N:].float()).all(), "wrote outside C"
+
+
 def test_fill_random_uniform():
     t = torch.empty(1 << 20, device="cuda", dtype=torch.bfloat16)
     gemm.fill_random_(t, seed=3)
