@@ -20,9 +20,9 @@
 //       start    vmcnt(8) (B(t+1) landed) + barrier
 //       rows 0-3 read B(t+1) into the other B set (16 ds_reads), stage B(t+2)
 //                (8 buffer_load ... lds, every other MFMA pair)
-//       mid      vmcnt(8) (A(t+1) landed) + lgkmcnt(0) + barrier (every wave's
-//                A(t) reads, issued during K-tile t-1, are done: A(t+2) may
-//                overwrite them)
+//       mid      vmcnt(8) (A(t+1) landed) + lgkmcnt(8) + barrier (every wave's
+//                A(t) reads - the last, a[7], in this K-tile's first MFMA pair -
+//                are done: A(t+2) may overwrite them)
 //       rows 4-7 read A(t+1) (a[0..3] at once, a[4..6] after their rows; a[7]
 //                in K-tile t+1's first MFMA pair), stage A(t+2)
 //     so every staged operand half has a full K-tile of load latency before
@@ -34,9 +34,10 @@
 //     the last one (never used) - or, in the streaming kernel, the next
 //     tile's first K-tiles.
 //   * Kernels: gemm_4wave_fp8_kernel<false> (a block per tile),
-//     gemm_4wave_fp8_stream_kernel (persistent, a block's tiles as one K-tile
-//     stream; the one-shot default with more tiles than CUs) and
-//     gemm_4wave_fp8_kernel<true> (the persistent deadline compute stand-in).
+//     gemm_4wave_fp8_stream_kernel<false> (persistent, a block's tiles as one
+//     K-tile stream; the one-shot default with more tiles than CUs),
+//     gemm_4wave_fp8_kernel<true> (the persistent deadline compute stand-in)
+//     and gemm_4wave_fp8_stream_kernel<true> (its streaming variant, opt-in).
 //
 // Variant 5 of dlnb::kernels::gemm_tn for fp8 (K a multiple of 256 bytes).
 #include <hip/hip_runtime.h>
