@@ -181,6 +181,10 @@ def main() -> int:
     if world != a.gpus:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # An iteration takes ~3 s: a collective that has not completed within
+    # 3 minutes is hung - abort it and fall back (graph retry / error key)
+    # instead of waiting out the runtime's 15-minute default.
+    os.environ.setdefault("DLNB_TIMEOUT", "180")
     # Everything below is native (HIP + RCCL from /opt/rocm); torch is not needed.
     os.environ.setdefault("DLNB_NO_TORCH", "1")
 

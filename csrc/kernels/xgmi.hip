@@ -51,8 +51,13 @@ __device__ __forceinline__ uint32_t sys_load(uint32_t* p) {
 // completing the stores (vmcnt 0) is all it takes; a system-scope release
 // fence would also write back the whole L2 of the XCD (buffer_wbl2) and,
 // as __threadfence_system() is acquire-release, invalidate it - once per
-// block and piece, costly for every kernel sharing the XCD. Cached windows
-// (DLNB_XGMI_MEM=fine|coarse) keep the full fence.
+// block and piece, costly for every kernel sharing the XCD. This holds for a
+// peer on another GPU too: gfx950's system-scope release is exactly that
+// L2 write-back followed by vmcnt(0), and the write-back has nothing to do
+// for MTYPE-UC lines - a store's vmcnt slot is returned only once the write
+// is acknowledged by the memory it targets (local HBM or, through xGMI, the
+// peer's). Cached windows (DLNB_XGMI_MEM=fine|coarse) keep the full fence,
+// which is also the escape hatch if a platform ever acknowledges earlier.
 __device__ __forceinline__ void release_window(const Peers& P) {
   if (P.uncached)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
