@@ -59,6 +59,16 @@ class ComputeEngine {
     run(s, us, flops);
   }
   virtual bool stamps_task_start() const { return false; }
+  // A task that continues the previous task on s: the caller guarantees that
+  // nothing but event records was enqueued on s in between (no waits, no
+  // collectives), so the two are one stretch of compute. The gemm (deadline)
+  // mode then ends it at the previous task's deadline + us on the clock the
+  // stretch started with, so a kernel-boundary gap between the two is
+  // absorbed rather than added (a replayed HIP graph puts consecutive kernels
+  // of a stream on different hardware queues: ~10 us per hop, measured in
+  // profiles/graph_queues_r2.md). The compute still lasts the table's total.
+  // Other modes: run().
+  virtual void run_chained(Stream& s, double us, double flops) { run(s, us, flops); }
   virtual uint64_t task_ticks(double us) const { (void)us; return 0; }
   // Graph mode: enqueue on s a reset of whatever per-task device state the
   // engine keys by epoch (a replayed graph repeats the captured epochs).

@@ -104,8 +104,31 @@ class GpuCompute : public ComputeEngine {
   uint64_t task_ticks(double us) const override { return ticks(us * scale_); }
   void run(Stream& s, double us, double flops) override { run_stamped(s, us, flops, nullptr); }
 
+  void run_chained(Stream& s, double us, double flops) override {
+    if (mode_ == ComputeMode::Gemm && us * scale_ >= 20.0) {
+      uint64_t* slot = slot_for(s);
+      auto it = chain_end_.find(slot);
+      if (it != chain_end_.end() && it->second > 0) {
+        // Same epoch, so the same t0: this task's slices end at the previous
+        // task's deadline + its own duration on the clock the chain started.
+        const uint64_t base = it->second, total = base + ticks(us * scale_);
+        const uint64_t slice = std::max<uint64_t>(ticks(slice_us_), 1);
+        for (uint64_t end = base + slice;; end += slice) {
+          kernels::gemm_tn_deadline(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, total, slot, epoch_[slot],
+                                    grid_, s.native(), std::min(end, total), nullptr);
+          if (end >= total) break;
+        }
+        it->second = total;
+        ++chained_;
+        return;
+      }
+    }
+    run(s, us, flops);
+  }
+
   void run_stamped(Stream& s, double us, double flops, uint64_t* start) override {
     double d = us * scale_;
+    if (mode_ == ComputeMode::Gemm) chain_end_[slot_for(s)] = 0;  // a chain restarts at every unchained task
     if (mode_ == ComputeMode::Sleep) {
       if (d > 0) kernels::idle_wait(ticks(d), s.native());
       return;
@@ -133,6 +156,7 @@ class GpuCompute : public ComputeEngine {
                                   grid_, s.native(), std::min(end, total), end == slice ? start : nullptr);
         if (end >= total) break;
       }
+      chain_end_[slot_for(s)] = total;
       return;
     }
     // Fixed-work modes from here on: bracket the task with device stamps.
@@ -172,6 +196,7 @@ class GpuCompute : public ComputeEngine {
       j["deadline_grid"] = grid_;
       j["comm_reserved_cus"] = cus_ - grid_;
       j["deadline_slice_us"] = slice_us_;
+      j["chained_tasks"] = chained_;  // enqueued so far (a captured graph counts its one iteration)
     }
     if (!levels_.empty()) {
       j["gemm_dtype"] = dtype_name(dtype_);
@@ -262,6 +287,8 @@ class GpuCompute : public ComputeEngine {
   Buffer slots_;
   std::map<Stream*, size_t> slot_of_;
   std::map<uint64_t*, uint32_t> epoch_;
+  std::map<uint64_t*, uint64_t> chain_end_;  // deadline (ticks after t0) of the stream's last task, 0: no chain
+  long chained_ = 0;                         // tasks that continued a chain (describe())
   int grid_ = 256;
   double slice_us_ = 500;
   double hz_ = 1e8;

@@ -114,7 +114,8 @@ class DataParallel : public Strategy {
     const int me = comm_->rank();
     ce.run(*compute_, fwd_us_, fwd_flops_);
     for (int i = 0; i < nb_; ++i) {
-      ce.run(*compute_, bwd_us_per_bucket_, bwd_flops_per_bucket_);
+      // only event records on compute_ since the forward: one stretch of compute
+      ce.run_chained(*compute_, bwd_us_per_bucket_, bwd_flops_per_bucket_);
       compute_->record(*ready_[i]);
       comm_stream_->wait(*ready_[i]);
       const uint64_t n = shard_[i] * W_;
@@ -156,7 +157,8 @@ class DataParallel : public Strategy {
     ComputeEngine& ce = *ctx.compute;
     ce.run(*compute_, fwd_us_, fwd_flops_);
     for (int i = 0; i < nb_; ++i) {
-      ce.run(*compute_, bwd_us_per_bucket_, bwd_flops_per_bucket_);
+      // only event records on compute_ since the forward: one stretch of compute
+      ce.run_chained(*compute_, bwd_us_per_bucket_, bwd_flops_per_bucket_);
       compute_->record(*ready_[i]);
       comm_stream_->wait(*ready_[i]);
       int t = timers_->begin(*comm_stream_);

@@ -187,3 +187,17 @@ def test_rccl_cta_budget(data_dir):
                      backend="rccl", quiet=True, rccl_max_ctas=64)
     b = doc["global"]["dlnb"]["rccl_cta_budget"]
     assert b["max_ctas_per_lane"] == 64 and not b["fits"]
+
+
+def test_dp_backward_buckets_chain_deadline(root):
+    """DP's backward buckets continue the forward's deadline clock (run_chained):
+    the comm-bound ViT-H step (bench.py's comm_bound block) lasts the table's
+    compute plus the last bucket's exposed all-reduce and the iteration
+    boundary, not plus ~10 us per bucket boundary (7.46 ms before, 7.29 after)."""
+    doc = engine.run("dp", "vit_h_32_float8", 8, base_path=root, warmup=3, runs=10, compute="gemm",
+                     backend="rccl", graph=True, quiet=True)
+    d = doc["global"]["dlnb"]
+    it = d["iteration"]
+    assert d["compute"]["chained_tasks"] >= 8
+    floor = it["compute_floor_ms"]
+    assert floor <= it["median_ms"] < floor + 0.3, (it["median_ms"], floor)
