@@ -18,6 +18,10 @@ ride along as extra keys of the same JSON line:
   gradient all-reduce in 8 buckets) - the one baseline config where
   communication dominates; iteration time, exposed communication
   (barrier_time) and all-reduce bus bandwidth.
+* ``comm_bound.rccl_default_ctas``: the same step with RCCL choosing its own
+  CTA count instead of the ``maxCTAs`` cap that fits every comm lane into
+  the 32 CUs the deadline compute leaves free (what the budget costs the
+  all-reduce over the links).
 * ``comm_bound.gemm_work``: the same with fixed-work compute (the GEMM count
   calibrated to the table time with nothing else running), so collective
   interference shows up as a longer iteration and ``compute_stretch`` > 1.
@@ -169,6 +173,8 @@ def main() -> int:
     ap.add_argument("--c5-buckets", type=int, default=8)
     ap.add_argument("--c5-steps", type=int, default=50)
     ap.add_argument("--c5-wire", default="bf16", help="wire dtype of the comm-bound all-reduce")
+    ap.add_argument("--no-c5-ctas-ab", dest="c5_ctas_ab", action="store_false",
+                    help="skip the comm-bound rerun with RCCL's default CTA count")
     ap.add_argument("--stretch-steps", type=int, default=2,
                     help="fixed-work FSDP iterations for compute_stretch (0 skips)")
     ap.add_argument("--xgmi-ab", choices=["auto", "on", "off"], default="auto",
@@ -241,6 +247,21 @@ def main() -> int:
                 })
             except Exception as e:  # noqa: BLE001
                 c5["error"] = str(e)[:300]
+            if on_gpu and c5.get("backend") == "RCCL" and a.c5_ctas_ab:
+                # The same step with RCCL's own CTA count (no maxCTAs cap from the
+                # comm-CU budget): one comm lane cannot deadlock against another, so
+                # this shows what the 32-CU budget costs the all-reduce over the links.
+                try:
+                    d = run(".c5c", "dp", a.c5_model, a.c5_buckets, graph=use_graph, warmup=5, runs=a.c5_steps,
+                            compute=a.compute, wire_dtype=a.c5_wire, rccl_max_ctas=0)
+                    it = d["global"]["dlnb"]["iteration"]
+                    c5["rccl_default_ctas"] = {"ms_per_step": round(it["timed_ms_per_iter"], 4),
+                                               "median_ms": round(it["median_ms"], 4),
+                                               "exposed_comm_ms": _mean_of(d, "barrier_time"),
+                                               "allreduce_busbw_GBps": _busbw(d, "allreduce", world),
+                                               "allreduce_algbw_GBps": _algbw(d, "allreduce")}
+                except Exception as e:  # noqa: BLE001
+                    c5["rccl_default_ctas"] = {"error": str(e)[:300]}
             if a.stretch_steps > 0 and on_gpu:
                 try:
                     d = run(".c5w", "dp", a.c5_model, a.c5_buckets, graph=use_graph, warmup=5, runs=a.c5_steps,

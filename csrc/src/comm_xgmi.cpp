@@ -66,6 +66,14 @@ void unhex(const std::string& s, void* p, size_t n) {
 
 hipStream_t hs(Stream& s) { return static_cast<hipStream_t>(s.native()); }
 
+// PCI bus id of a device ("0000:a4:00.0"): how a peer names its GPU in the
+// store record, independent of each process's device ordinals.
+std::string pci_id(int dev) {
+  char buf[64] = {0};
+  if (hipDeviceGetPCIBusId(buf, sizeof(buf), dev) != hipSuccess) return "?";
+  return buf;
+}
+
 class XgmiComm : public Communicator {
  public:
   XgmiComm(const std::string& name, const std::vector<int>& members, int my_world_rank, HostGroup& world,
@@ -119,7 +127,7 @@ class XgmiComm : public Communicator {
     std::ostringstream key;
     key << "xgmi/" << name << "/";
     for (int m : members) key << m << ",";
-    const std::string me = get_hostname() + " " + hex(&hw, sizeof(hw)) + " " + hex(&hf, sizeof(hf));
+    const std::string me = get_hostname() + " " + hex(&hw, sizeof(hw)) + " " + hex(&hf, sizeof(hf)) + " " + pci_id(dev_);
     world.store().set(key.str() + std::to_string(rank_), me);
     std::memset(&peers_, 0, sizeof(peers_));
     for (int r = 0; r < size_; ++r) {
@@ -129,10 +137,11 @@ class XgmiComm : public Communicator {
         continue;
       }
       std::istringstream in(world.store().get(key.str() + std::to_string(r)));
-      std::string host, sw, sf;
-      in >> host >> sw >> sf;
+      std::string host, sw, sf, pci;
+      in >> host >> sw >> sf >> pci;
       DLNB_REQUIRE(host == get_hostname(), "xgmi backend: group " << name << " spans hosts (" << host << " and "
                                                                   << get_hostname() << "); use --backend rccl");
+      require_peer_access(name, r, pci);
       hipIpcMemHandle_t pw, pf;
       unhex(sw, &pw, sizeof(pw));
       unhex(sf, &pf, sizeof(pf));
@@ -366,6 +375,28 @@ class XgmiComm : public Communicator {
   void abort() override { __atomic_store_n(host_words_, 1u, __ATOMIC_RELEASE); }
 
  private:
+  // Before any kernel touches a peer window: a member on another GPU must be
+  // reachable by peer access (xGMI), or the first load from its window faults
+  // the device instead of failing this setup. Ranks sharing one GPU (the
+  // 1-GPU test setup) need nothing; a peer GPU outside this process's visible
+  // set cannot be checked here and is left to the IPC mapping.
+  void require_peer_access(const std::string& name, int r, const std::string& pci) {
+    int peer_dev = -1;
+    if (pci == "?" || hipDeviceGetByPCIBusId(&peer_dev, pci.c_str()) != hipSuccess || peer_dev == dev_) {
+      (void)hipGetLastError();
+      return;
+    }
+    int ok = 0;
+    DLNB_HIP_CHECK(hipDeviceCanAccessPeer(&ok, dev_, peer_dev));
+    DLNB_REQUIRE(ok, "xgmi backend: group " << name << ": GPU " << dev_ << " cannot access the GPU of member " << r
+                                            << " (" << pci << ", device " << peer_dev
+                                            << ") by peer access; use --backend rccl");
+    hipError_t e = hipDeviceEnablePeerAccess(peer_dev, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+      DLNB_THROW("xgmi backend: hipDeviceEnablePeerAccess(" << peer_dev << ") failed: " << hipGetErrorString(e));
+    (void)hipGetLastError();
+  }
+
   struct P2POp {
     bool is_send;
     char* buf;

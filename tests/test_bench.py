@@ -101,6 +101,10 @@ def test_bench_gpu_single_rank_secondaries(tmp_path):
     assert 0.8 < c5["gemm_work"]["compute_stretch"] < 1.5, c5
     assert 0.8 < o["compute_stretch"] < 1.5, o
     assert o["rccl_cta_budget"]["applies"] and o["rccl_cta_budget"]["max_ctas_per_lane"] == 32
+    # the comm-bound step again with RCCL's own CTA count (no maxCTAs cap)
+    u = c5["rccl_default_ctas"]
+    assert "error" not in u, u
+    assert u["ms_per_step"] >= 0.9 * c5["floor_ms"] and u["allreduce_busbw_GBps"] is None
     # energy: the GPU's power sensor integrated over each step (hundreds of W x the step time)
     assert o["energy_J_per_step"] is None or o["energy_J_per_step"]["per_gpu"] > 0
 
