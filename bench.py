@@ -33,6 +33,10 @@ ride along as extra keys of the same JSON line:
   RCCL, with the RCCL/xgmi time ratio. It runs last, in a child process per
   rank with a short device-wait timeout, so a failure there can only cost
   this block, never the headline.
+* ``headline_xgmi`` (N > 1): the headline FSDP step itself over the xgmi
+  kernels (zero-copy all-gather / reduce-scatter into registered buffers),
+  with its effective bus bandwidth as a ratio of the headline's (RCCL).
+  Also a child process per rank, after ``comm_bound_xgmi``.
 
 At N = 1 a "collective" is a local device copy: bus bandwidth is reported
 as null (nccl-tests convention: nothing crosses a link).
@@ -115,30 +119,40 @@ def _mean_of(doc: dict, key: str) -> Optional[float]:
     return round(sum(vals) / len(vals) * 1e3, 4) if vals else None
 
 
-def _xgmi_ab(a: argparse.Namespace, world: int, rank: int, c5: dict) -> Dict[str, Any]:
-    """The comm-bound DP secondary over the xgmi backend (HIP graph), run by
-    the native binary as a child of every rank."""
+def _xgmi_child(a: argparse.Namespace, world: int, rank: int, tag: str, strategy: str, model: str,
+                params: tuple, timeout: float, **kw: Any) -> Dict[str, Any]:
+    """One benchmark run over the xgmi backend (HIP graph) by the native binary
+    as a child of every rank; rank 0 returns the child's report document."""
     from dlnetbench_amd import engine
-    _store_env(world, rank, ".xgmi")
-    out = f"/tmp/dlnb_bench_xgmi_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}.json"
-    args = engine.build_args("dp", a.c5_model, a.c5_buckets, base_path=a.base_path, warmup=5, runs=a.c5_steps,
-                             compute=a.compute, wire_dtype=a.c5_wire, backend="xgmi", graph=True,
-                             devices=a.devices, time_scale=a.time_scale, quiet=True,
-                             json=out if rank == 0 else None)
+    _store_env(world, rank, tag)
+    out = f"/tmp/dlnb_bench{tag}_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}.json"
+    args = engine.build_args(strategy, model, *params, base_path=a.base_path, compute=a.compute, backend="xgmi",
+                             graph=True, devices=a.devices, time_scale=a.time_scale, quiet=True,
+                             json=out if rank == 0 else None, **kw)
     env = dict(os.environ, DLNB_XGMI_TIMEOUT_S=os.environ.get("DLNB_XGMI_TIMEOUT_S", "20"))
+    # bounded well below any driver limit, so a first-time cross-device xgmi
+    # failure costs a minute or two and the headline line still prints
+    p = subprocess.run([os.path.join(ROOT, "build", "bin", strategy), *args], env=env, timeout=timeout,
+                       stdout=sys.stderr, stderr=subprocess.PIPE, text=True)
+    if p.returncode != 0:
+        raise RuntimeError(f"exit {p.returncode}: " + (p.stderr or "")[-300:])
+    if rank != 0:
+        return {}
+    with open(out) as f:
+        d = json.load(f)
+    os.remove(out)
+    return d
+
+
+def _xgmi_ab(a: argparse.Namespace, world: int, rank: int, c5: dict) -> Dict[str, Any]:
+    """The comm-bound DP secondary over the xgmi backend (HIP graph)."""
     res: Dict[str, Any] = {"backend": "XGMI", "hip_graph": True}
     try:
-        # ~10 s expected (55 iterations of ~7.5 ms + setup); bounded well below any driver limit so a
-        # first-time cross-device xgmi failure costs a minute and the headline line still prints
-        p = subprocess.run([os.path.join(ROOT, "build", "bin", "dp"), *args], env=env, timeout=90,
-                           stdout=sys.stderr, stderr=subprocess.PIPE, text=True)
-        if p.returncode != 0:
-            return {"error": f"exit {p.returncode}: " + (p.stderr or "")[-300:]}
+        # ~10 s expected (55 iterations of ~7.5 ms + setup)
+        d = _xgmi_child(a, world, rank, ".xgmi", "dp", a.c5_model, (a.c5_buckets,), 90, warmup=5,
+                        runs=a.c5_steps, wire_dtype=a.c5_wire)
         if rank != 0:
             return res
-        with open(out) as f:
-            d = json.load(f)
-        os.remove(out)
         it = d["global"]["dlnb"]["iteration"]
         res.update({"ms_per_step": round(it["timed_ms_per_iter"], 4), "median_ms": round(it["median_ms"], 4),
                     "exposed_comm_ms": _mean_of(d, "barrier_time"),
@@ -148,6 +162,30 @@ def _xgmi_ab(a: argparse.Namespace, world: int, rank: int, c5: dict) -> Dict[str
             # > 1: the xgmi kernels finish the comm-bound step faster than the comm_bound block's backend
             res["speedup_vs_comm_bound"] = round(c5["ms_per_step"] / res["ms_per_step"], 4)
             res["comm_bound_backend"] = c5.get("backend")
+    except Exception as e:  # noqa: BLE001
+        res = {"error": str(e)[:300]}
+    return res
+
+
+def _headline_xgmi(a: argparse.Namespace, world: int, rank: int, doc: dict) -> Dict[str, Any]:
+    """The headline FSDP step itself over the xgmi kernels (zero-copy
+    all-gather / reduce-scatter into registered buffers): its effective bus
+    bandwidth next to the headline's, under the same deadline compute."""
+    res: Dict[str, Any] = {"backend": "XGMI", "hip_graph": True}
+    try:
+        # ~4 iterations of ~2.8 s + setup
+        d = _xgmi_child(a, world, rank, ".xgmih", "fsdp", a.model, (a.units, world), 150, warmup=1,
+                        runs=a.xgmi_headline_steps, schedule=a.schedule, wire_dtype="bf16")
+        if rank != 0:
+            return res
+        it = d["global"]["dlnb"]["iteration"]
+        res.update({"ms_per_step": round(it["timed_ms_per_iter"], 3), "median_ms": round(it["median_ms"], 3),
+                    "exposed_comm_ms": round(it["timed_ms_per_iter"] - it["compute_floor_ms"], 3),
+                    "effective_busbw_GBps": {k: _busbw(d, k, world) for k in ("allgather", "reduce_scatter")}})
+        base = {k: _busbw(doc, k, world) for k in ("allgather", "reduce_scatter")}
+        res["busbw_ratio_vs_headline"] = {k: round(res["effective_busbw_GBps"][k] / v, 4)
+                                          for k, v in base.items() if v and res["effective_busbw_GBps"][k]}
+        res["headline_backend"] = doc["global"]["backend"]
     except Exception as e:  # noqa: BLE001
         res = {"error": str(e)[:300]}
     return res
@@ -178,7 +216,9 @@ def main() -> int:
     ap.add_argument("--stretch-steps", type=int, default=2,
                     help="fixed-work FSDP iterations for compute_stretch (0 skips)")
     ap.add_argument("--xgmi-ab", choices=["auto", "on", "off"], default="auto",
-                    help="comm_bound_xgmi secondary (auto: when N > 1 on the GPU)")
+                    help="comm_bound_xgmi / headline_xgmi secondaries (auto: when N > 1 on the GPU)")
+    ap.add_argument("--xgmi-headline-steps", type=int, default=2,
+                    help="timed steps of the headline_xgmi secondary (0 skips it)")
     ap.add_argument("--json", default=None, help="also write the full headline report here (rank 0)")
     a = ap.parse_args()
 
@@ -287,8 +327,11 @@ def main() -> int:
         os.dup2(saved, 1)
         os.close(saved)
     # xgmi A/B last, in child processes (see the module docstring).
-    if a.c5_model != "none" and on_gpu and (a.xgmi_ab == "on" or (a.xgmi_ab == "auto" and world > 1)):
+    xgmi_on = on_gpu and (a.xgmi_ab == "on" or (a.xgmi_ab == "auto" and world > 1))
+    if a.c5_model != "none" and xgmi_on:
         extra["comm_bound_xgmi"] = _xgmi_ab(a, world, rank, extra.get("comm_bound", {}))
+    if xgmi_on and a.xgmi_headline_steps > 0:
+        extra["headline_xgmi"] = _headline_xgmi(a, world, rank, doc)
     if rank != 0:
         return 0
     g = doc["global"]

@@ -131,3 +131,7 @@ def test_bench_torchrun_xgmi_two_ranks_one_gpu(tmp_path):
     assert "error" not in x, x
     assert x["hip_graph"] is True and x["ms_per_step"] > 0 and x["allreduce_busbw_GBps"] > 0
     assert x["speedup_vs_comm_bound"] > 0 and x["comm_bound_backend"] == "XGMI"
+    h = o["headline_xgmi"]
+    assert "error" not in h, h
+    assert h["ms_per_step"] > 0 and h["effective_busbw_GBps"]["allgather"] > 0
+    assert h["busbw_ratio_vs_headline"]["allgather"] > 0 and h["headline_backend"] == "XGMI"
