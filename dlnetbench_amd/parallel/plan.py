@@ -19,10 +19,9 @@ from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 from dataclasses import asdict, dataclass, field
-from typing import Dict, List, Optional
+from typing import Dict, List
 
 from ..utils.stats import ModelStats, load_stats
 

@@ -25,7 +25,7 @@ import argparse
 import itertools
 import json
 import re
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, List, Sequence, Tuple
 
 _UNITS = ["B", "KiB", "MiB", "GiB", "TiB"]
 

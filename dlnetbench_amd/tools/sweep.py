@@ -29,7 +29,7 @@ import json
 import os
 import sys
 import time
-from typing import Dict, Iterator, List
+from typing import Iterator, List
 
 from ..engine import build_args
 from ..utils import launch, report
