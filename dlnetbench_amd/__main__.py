@@ -6,7 +6,7 @@
                       exact check / bandwidth sweep of a comm backend (dlnb commtest)
     launch -n N <program ...>   generic N-rank launcher (utils/launch.py)
     sweep | plots | report | plan | schedule-sim | roofline | measure | gemm-bench | clock-check |
-    prof-summary | download-models
+    prof-summary | bench-report | download-models
                       the tools, each with its own --help
 
 The reference spreads these over Makefile targets, SbatchMan jobs and loose
@@ -34,6 +34,7 @@ TOOLS = {
     "gemm-bench": "dlnetbench_amd.tools.gemm_bench",
     "clock-check": "dlnetbench_amd.tools.clock_check",
     "prof-summary": "dlnetbench_amd.tools.prof_summary",
+    "bench-report": "dlnetbench_amd.tools.bench_report",
     "download-models": "dlnetbench_amd.tools.download_models",
 }
 

@@ -1,0 +1,123 @@
+"""Scaling table from bench.py result lines (one JSON line per GPU count).
+
+    python -m dlnetbench_amd bench-report BENCH_N1.json BENCH_N8.json ...
+    python -m dlnetbench_amd bench-report runs.jsonl --csv scaling.csv
+
+Every input holds bench.py JSON lines (a file with one line, a JSONL of
+several, or a JSON array of them); other lines are skipped, so a captured
+stdout works as is. Rows are sorted by ``n_gpus``. Columns: the headline
+iteration and its weak-scaling efficiency against the smallest N
+(T_min / T_N; the headline keeps per-GPU work fixed), the headline's
+all-gather / reduce-scatter bus bandwidth, and the secondary blocks when
+present: the comm-bound ViT-H DP step (RCCL, RCCL without the CTA cap, our
+xgmi kernels) and the headline FSDP step over xgmi as a busbw ratio to RCCL.
+
+Reference equivalent: the scaling plots of plots/plot_dp.py:80-145 start
+from the per-run DataFrame; this is the same view for the bench contract's
+one-line-per-run output.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from typing import Any, Dict, Iterable, List, Optional
+
+
+def _lines(text: str) -> Iterable[Dict[str, Any]]:
+    text = text.strip()
+    if text.startswith("["):
+        for d in json.loads(text):
+            if isinstance(d, dict):
+                yield d
+        return
+    for ln in text.splitlines():
+        ln = ln.strip()
+        if not ln.startswith("{"):
+            continue
+        try:
+            d = json.loads(ln)
+        except json.JSONDecodeError:
+            continue
+        if isinstance(d, dict):
+            yield d
+
+
+def load(paths: List[str]) -> List[Dict[str, Any]]:
+    """bench.py result lines (dicts with "metric" and "n_gpus") from the inputs, sorted by n_gpus."""
+    out = []
+    for p in paths:
+        with (sys.stdin if p == "-" else open(p)) as f:
+            out += [d for d in _lines(f.read()) if "metric" in d and "n_gpus" in d and "value" in d]
+    return sorted(out, key=lambda d: d["n_gpus"])
+
+
+def _get(d: Optional[dict], *keys: str) -> Any:
+    for k in keys:
+        if not isinstance(d, dict):
+            return None
+        d = d.get(k)
+    return d
+
+
+def rows(lines: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
+    if not lines:
+        return []
+    t0 = lines[0]["ms_per_step"]
+    out = []
+    for d in lines:
+        ms = d["ms_per_step"]
+        r = {
+            "n_gpus": d["n_gpus"],
+            "ms_per_step": ms,
+            "efficiency": round(t0 / ms, 4) if ms else None,
+            "exposed_comm_ms": d.get("exposed_comm_ms"),
+            "ag_busbw_GBps": _get(d, "effective_busbw_GBps", "allgather"),
+            "rs_busbw_GBps": _get(d, "effective_busbw_GBps", "reduce_scatter"),
+            "c5_ms": _get(d, "comm_bound", "ms_per_step"),
+            "c5_busbw_GBps": _get(d, "comm_bound", "allreduce_busbw_GBps"),
+            "c5_uncapped_ms": _get(d, "comm_bound", "rccl_default_ctas", "ms_per_step"),
+            "c5_xgmi_ms": _get(d, "comm_bound_xgmi", "ms_per_step"),
+            "c5_xgmi_speedup": _get(d, "comm_bound_xgmi", "speedup_vs_comm_bound"),
+            "fsdp_xgmi_ag_ratio": _get(d, "headline_xgmi", "busbw_ratio_vs_headline", "allgather"),
+            "fsdp_xgmi_rs_ratio": _get(d, "headline_xgmi", "busbw_ratio_vs_headline", "reduce_scatter"),
+        }
+        out.append(r)
+    return out
+
+
+def _fmt(v: Any) -> str:
+    if v is None:
+        return "—"
+    if isinstance(v, float):
+        return f"{v:.4g}" if abs(v) < 100 else f"{v:.1f}"
+    return str(v)
+
+
+def markdown(rs: List[Dict[str, Any]]) -> str:
+    if not rs:
+        return "(no bench.py result lines)\n"
+    cols = list(rs[0].keys())
+    out = ["| " + " | ".join(cols) + " |", "|" + "---:|" * len(cols)]
+    out += ["| " + " | ".join(_fmt(r[c]) for c in cols) + " |" for r in rs]
+    return "\n".join(out) + "\n"
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("inputs", nargs="+", help="files with bench.py JSON lines ('-' = stdin)")
+    ap.add_argument("--csv", default=None, help="also write the table as CSV")
+    a = ap.parse_args(argv)
+    rs = rows(load(a.inputs))
+    sys.stdout.write(markdown(rs))
+    if a.csv and rs:
+        import csv
+        with open(a.csv, "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=list(rs[0].keys()))
+            w.writeheader()
+            w.writerows(rs)
+    return 0 if rs else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,58 @@
+"""tools/bench_report.py: scaling table from bench.py result lines."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from dlnetbench_amd.tools import bench_report  # noqa: E402
+
+
+def _line(n, ms, ag=None, c5=None, xgmi=None, hx=None):
+    d = {"metric": "m", "value": ms, "unit": "ms", "n_gpus": n, "ms_per_step": ms, "exposed_comm_ms": ms - 2814.75,
+         "effective_busbw_GBps": {"allgather": ag, "reduce_scatter": ag}}
+    if c5 is not None:
+        d["comm_bound"] = {"ms_per_step": c5, "allreduce_busbw_GBps": None if n == 1 else 300.0,
+                           "rccl_default_ctas": {"ms_per_step": c5 - 0.5}}
+    if xgmi is not None:
+        d["comm_bound_xgmi"] = {"ms_per_step": xgmi, "speedup_vs_comm_bound": round(c5 / xgmi, 4)}
+    if hx is not None:
+        d["headline_xgmi"] = {"busbw_ratio_vs_headline": {"allgather": hx, "reduce_scatter": hx}}
+    return json.dumps(d)
+
+
+def test_scaling_rows_sorted_with_efficiency(tmp_path):
+    # stdout of three runs in arbitrary order, with non-JSON noise (banners) in between
+    p = tmp_path / "runs.txt"
+    p.write_text("\n".join([
+        "RCCL version 2.x", _line(8, 2830.0, ag=250.0, c5=9.0, xgmi=7.5, hx=1.3),
+        _line(1, 2816.5, c5=7.25), "{not json", _line(2, 2820.0, ag=110.0, c5=14.5, xgmi=14.2, hx=1.05)]))
+    rs = bench_report.rows(bench_report.load([str(p)]))
+    assert [r["n_gpus"] for r in rs] == [1, 2, 8]
+    assert rs[0]["efficiency"] == 1.0
+    assert rs[2]["efficiency"] == round(2816.5 / 2830.0, 4)
+    assert rs[0]["ag_busbw_GBps"] is None and rs[2]["ag_busbw_GBps"] == 250.0
+    assert rs[2]["c5_uncapped_ms"] == 8.5 and rs[2]["c5_xgmi_speedup"] == round(9.0 / 7.5, 4)
+    assert rs[2]["fsdp_xgmi_ag_ratio"] == 1.3 and rs[0]["c5_xgmi_ms"] is None
+    md = bench_report.markdown(rs)
+    assert md.count("\n") == 5 and "| 8 |" in md and "—" in md
+
+
+def test_cli_json_array_and_csv(tmp_path, capsys):
+    p = tmp_path / "a.json"
+    p.write_text("[" + ",".join([_line(4, 2818.0, ag=180.0), _line(1, 2816.0)]) + "]")
+    out = tmp_path / "s.csv"
+    assert bench_report.main([str(p), "--csv", str(out)]) == 0
+    text = capsys.readouterr().out
+    assert text.splitlines()[0].startswith("| n_gpus | ms_per_step | efficiency")
+    rows = out.read_text().splitlines()
+    assert rows[0].startswith("n_gpus,ms_per_step,efficiency") and len(rows) == 3
+
+
+def test_no_lines_is_an_error(tmp_path):
+    p = tmp_path / "empty.txt"
+    p.write_text("nothing here\n")
+    assert bench_report.main([str(p)]) == 1
