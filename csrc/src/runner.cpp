@@ -9,6 +9,9 @@
 // divides a world-sum by the warm-up count, cpp/utils.hpp:127-128) and takes
 // the max over ranks; loop mode is a run-time flag (or a *_loop argv[0]).
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <fstream>
@@ -263,6 +266,8 @@ Json run_loopback(const Options& opt) {
   abort_cpu_waits(false);
   std::vector<Json> docs(static_cast<size_t>(n));
   std::mutex mu;
+  std::condition_variable done_cv;
+  int done = 0;
   std::string first_error;
   std::vector<std::thread> threads;
   for (int r = 0; r < n; ++r) {
@@ -278,7 +283,27 @@ Json run_loopback(const Options& opt) {
         loopback_abort(*hub, msg);
         store->abort(msg);
       }
+      std::lock_guard<std::mutex> g(mu);
+      ++done;
+      done_cv.notify_all();
     });
+  }
+  {
+    // After the first failure the other rank threads get a bounded grace
+    // period to leave their waits and tear down; a thread still blocked then
+    // (a wait that missed the abort under heavy host load: seen ~1 in 25
+    // runs with 12 jobs on 8 CPUs) must not hold the job forever, so the
+    // process ends with the rank's error, as a multi-process job would.
+    const double grace_s = static_cast<double>(env_int("DLNB_LOOPBACK_ABORT_GRACE_S", 10));
+    std::unique_lock<std::mutex> g(mu);
+    done_cv.wait(g, [&] { return done == n || !first_error.empty(); });
+    if (done < n &&
+        !done_cv.wait_for(g, std::chrono::duration<double>(grace_s), [&] { return done == n; })) {
+      std::fprintf(stderr, "[dlnb] error: %s\n[dlnb] %d of %d rank threads still blocked %.0f s after the failure; exiting\n",
+                   first_error.c_str(), n - done, n, grace_s);
+      std::fflush(stderr);
+      std::_Exit(2);
+    }
   }
   for (auto& t : threads) t.join();
   if (!first_error.empty()) throw Error(first_error);
