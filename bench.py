@@ -64,6 +64,10 @@ METRIC = "proxy iter time (ms) + effective GB/s, Llama-3-8B DP/FSDP at 1/2/4/8 M
 BASELINE_MS = 2814.74976
 DEFAULT_MODEL = "llama3_8b_16_bfloat16"
 C5_MODEL = "vit_h_32_float8"
+# BASELINE configs C3 / C4 (8 GPUs): llama3_70b hybrid_3d S=2 mb=4 T=4 and
+# mixtral hybrid_3d_moe S=2 mb=16 EP=4; GPipe floors 3.81 s and 13.56 s.
+C3_MODEL, C3_PARAMS = "llama3_70b_16_bfloat16", "2,4,4"
+C4_MODEL, C4_PARAMS = "mixtral_8x7b_16_bfloat16", "2,16,4"
 
 
 def _store_env(world: int, rank: int, attempt: str = "") -> None:
@@ -97,7 +101,7 @@ def _busbw(doc: dict, kind: str, world: int) -> Optional[float]:
     if world <= 1:
         return None
     vals = [r["comm"][kind]["busbw_GBps"] for r in doc["ranks"] if "busbw_GBps" in r["comm"].get(kind, {})]
-    return round(sum(vals) / len(vals), 2) if vals else None
+    return float(f"{sum(vals) / len(vals):.4g}") if vals else None
 
 
 def _algbw(doc: dict, kind: str) -> Optional[float]:
@@ -119,18 +123,19 @@ def _mean_of(doc: dict, key: str) -> Optional[float]:
     return round(sum(vals) / len(vals) * 1e3, 4) if vals else None
 
 
-def _xgmi_child(a: argparse.Namespace, world: int, rank: int, tag: str, strategy: str, model: str,
-                params: tuple, timeout: float, **kw: Any) -> Dict[str, Any]:
-    """One benchmark run over the xgmi backend (HIP graph) by the native binary
-    as a child of every rank; rank 0 returns the child's report document."""
+def _child_run(a: argparse.Namespace, world: int, rank: int, tag: str, strategy: str, model: str,
+               params: tuple, timeout: float, backend: str = "xgmi", graph: bool = True,
+               **kw: Any) -> Dict[str, Any]:
+    """One benchmark run by the native binary as a child of every rank (its
+    own rendezvous, a bounded wall time); rank 0 returns the child's report."""
     from dlnetbench_amd import engine
     _store_env(world, rank, tag)
     out = f"/tmp/dlnb_bench{tag}_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}.json"
-    args = engine.build_args(strategy, model, *params, base_path=a.base_path, compute=a.compute, backend="xgmi",
-                             graph=True, devices=a.devices, time_scale=a.time_scale, quiet=True,
+    args = engine.build_args(strategy, model, *params, base_path=a.base_path, backend=backend,
+                             graph=graph or None, devices=a.devices, time_scale=a.time_scale, quiet=True,
                              json=out if rank == 0 else None, **kw)
     env = dict(os.environ, DLNB_XGMI_TIMEOUT_S=os.environ.get("DLNB_XGMI_TIMEOUT_S", "20"))
-    # bounded well below any driver limit, so a first-time cross-device xgmi
+    # bounded well below any driver limit, so a first-time cross-device
     # failure costs a minute or two and the headline line still prints
     p = subprocess.run([os.path.join(ROOT, "build", "bin", strategy), *args], env=env, timeout=timeout,
                        stdout=sys.stderr, stderr=subprocess.PIPE, text=True)
@@ -142,6 +147,99 @@ def _xgmi_child(a: argparse.Namespace, world: int, rank: int, tag: str, strategy
         d = json.load(f)
     os.remove(out)
     return d
+
+
+def _xgmi_child(a: argparse.Namespace, world: int, rank: int, tag: str, strategy: str, model: str,
+                params: tuple, timeout: float, **kw: Any) -> Dict[str, Any]:
+    """One benchmark run over the xgmi backend (HIP graph) as a child of every rank."""
+    return _child_run(a, world, rank, tag, strategy, model, params, timeout, backend="xgmi", graph=True,
+                      compute=a.compute, **kw)
+
+
+def _exact_backends(a: argparse.Namespace) -> str:
+    """Backends the exactness pass checks: the CPU backend on CPU runs; on the
+    GPU RCCL and the xgmi kernels, or xgmi alone when ranks share a GPU (RCCL
+    refuses that)."""
+    if a.backend == "cpu":
+        return "cpu"
+    devs = [d for d in (a.devices or "").split(",") if d.strip()]
+    shared = len(devs) != len(set(devs))
+    if a.backend == "xgmi" or shared:
+        return "xgmi"
+    return "rccl,xgmi"
+
+
+def _exactness(a: argparse.Namespace, world: int, rank: int) -> Dict[str, Any]:
+    """Before any timed phase of a multi-rank job: every collective (all-reduce
+    in and out of place, all-gather, reduce-scatter, all-to-all, ring
+    send/recv) of every backend the bench times, eager and graph-replayed
+    (xgmi also zero-copy registered), bf16 and fp8, at 3 sizes, checked
+    exactly across the real ranks (`dlnb commtest --suite`, a child of every
+    rank). xgmi runs with the vmcnt release first and the system-scope one if
+    that fails. Returns the suite report (identical on every rank: its
+    verdicts are all-reduced)."""
+    _store_env(world, rank, ".exact")
+    out = f"/tmp/dlnb_bench.exact_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}_{rank}.json"
+    cmd = [os.path.join(ROOT, "build", "bin", "dlnb"), "commtest", "--suite", "--backends", _exact_backends(a),
+           "--dtypes", a.exact_dtypes, "--sizes", a.exact_sizes, "--release-fallback", "--json", out]
+    if a.devices:
+        cmd += ["-d", a.devices]
+    env = dict(os.environ, DLNB_XGMI_TIMEOUT_S=os.environ.get("DLNB_EXACT_XGMI_TIMEOUT_S", "10"),
+               DLNB_STORE_TIMEOUT=str(int(a.exact_timeout)))
+    p = subprocess.run(cmd, env=env, timeout=a.exact_timeout, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       text=True)
+    if not os.path.exists(out):
+        raise RuntimeError(f"exit {p.returncode}: " + (p.stderr or "")[-300:])
+    with open(out) as f:
+        d = json.load(f)
+    os.remove(out)
+    return d
+
+
+def _exact_block(a: argparse.Namespace, world: int, rank: int) -> Dict[str, Any]:
+    res: Dict[str, Any] = {}
+    try:
+        d = _exactness(a, world, rank)
+        res = {"exact": d["exact"], "exact_detail": {
+            "ok": d["ok"], "seconds": round(d["seconds"], 2), "sizes": d["sizes"], "xgmi_release": d["xgmi_release"],
+            "rccl_nranks": d["rccl_nranks"], "world_size": d["world_size"],
+            "failed": [f"{r['backend']}/{r['mode']}/{r['dtype']}" + (f"/{r['release']}" if r.get("release") else "")
+                       for r in d["results"] if not r["ok"]]}}
+    except Exception as e:  # noqa: BLE001
+        res = {"exact": {}, "exact_detail": {"error": str(e)[:300]}}
+    return res
+
+
+def _hybrid_block(a: argparse.Namespace, world: int, rank: int, tag: str, strategy: str, model: str,
+                  params: tuple, floor_note: str) -> Dict[str, Any]:
+    """One BASELINE hybrid config (C3 hybrid_3d / C4 hybrid_3d_moe) on the job's
+    GPUs over RCCL: 1 warm-up + 1 timed iteration in a child process, its
+    time against the GPipe compute floor and its per-group communication."""
+    res: Dict[str, Any] = {"model": model, "strategy": strategy, "params": list(params), "backend": "RCCL"}
+    try:
+        d = _child_run(a, world, rank, tag, strategy, model, params, a.hybrid_timeout, backend=a.hybrid_backend,
+                       graph=False, compute=a.compute, warmup=1, runs=1)
+        if rank != 0:
+            return res
+        g, it = d["global"], d["global"]["dlnb"]["iteration"]
+        res.update({"ms_per_step": round(it["timed_ms_per_iter"], 3), "median_ms": round(it["median_ms"], 3),
+                    "floor_ms": round(it["compute_floor_ms"], 3), "floor_note": floor_note,
+                    "vs_floor": round(it["timed_ms_per_iter"] / it["compute_floor_ms"], 4)
+                    if it["compute_floor_ms"] else None,
+                    "backend": g["backend"], "rccl_nranks": g["dlnb"].get("rccl_nranks")})
+        for k in ("pp_comm_time", "dp_comm_time", "tp_comm_time", "ep_comm_time", "dp_ep_comm_time"):
+            v = _mean_of(d, k)
+            if v is not None:
+                res[k + "_ms"] = v
+        bw = {}
+        for k in ("tp_allreduce", "ep_alltoall", "dp_allreduce", "sendrecv"):
+            b = _busbw(d, k, world)
+            if b is not None:
+                bw[k] = b
+        res["busbw_GBps"] = bw
+    except Exception as e:  # noqa: BLE001
+        res["error"] = str(e)[:300]
+    return res
 
 
 def _xgmi_ab(a: argparse.Namespace, world: int, rank: int, c5: dict) -> Dict[str, Any]:
@@ -219,8 +317,22 @@ def main() -> int:
                     help="comm_bound_xgmi / headline_xgmi secondaries (auto: when N > 1 on the GPU)")
     ap.add_argument("--xgmi-headline-steps", type=int, default=2,
                     help="timed steps of the headline_xgmi secondary (0 skips it)")
+    ap.add_argument("--exact", choices=["auto", "on", "off"], default="auto",
+                    help="exactness pass of every timed backend across the ranks before timing (auto: N > 1)")
+    ap.add_argument("--exact-dtypes", default="bf16,fp8_e4m3")
+    ap.add_argument("--exact-sizes", default="4097,300000,2097157",
+                    help="elements per rank: one-shot with a ragged tail, two-shot / zero-copy, multi-piece")
+    ap.add_argument("--exact-timeout", type=float, default=120.0)
+    ap.add_argument("--hybrids", choices=["auto", "on", "off"], default="auto",
+                    help="BASELINE C3 hybrid_3d / C4 hybrid_3d_moe blocks (auto: N == 8 on the GPU)")
+    ap.add_argument("--c3-model", default=C3_MODEL)
+    ap.add_argument("--c3", default=C3_PARAMS, help="hybrid_3d num_stages,num_microbatches,num_tensor_shards")
+    ap.add_argument("--c4-model", default=C4_MODEL)
+    ap.add_argument("--c4", default=C4_PARAMS, help="hybrid_3d_moe num_stages,num_microbatches,num_expert_shards")
+    ap.add_argument("--hybrid-timeout", type=float, default=150.0)
     ap.add_argument("--json", default=None, help="also write the full headline report here (rank 0)")
     a = ap.parse_args()
+    a.hybrid_backend = "rccl" if a.backend == "auto" else a.backend
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -233,6 +345,15 @@ def main() -> int:
     os.environ.setdefault("DLNB_TIMEOUT", "180")
     # Everything below is native (HIP + RCCL from /opt/rocm); torch is not needed.
     os.environ.setdefault("DLNB_NO_TORCH", "1")
+    # Multi-rank: prove the collectives exact on these ranks before timing them.
+    # (every rank gets the same all-reduced verdict, so all ranks take the
+    # same decisions below)
+    exact: Dict[str, Any] = {}
+    if a.exact == "on" or (a.exact == "auto" and world > 1):
+        exact = _exact_block(a, world, rank)
+        if rank == 0:
+            print(f"[bench] exactness: {json.dumps(exact)}", file=sys.stderr)
+    xgmi_exact_ok = not exact or bool(exact.get("exact", {}).get("xgmi", False))
 
     from dlnetbench_amd import engine
     from dlnetbench_amd.utils.stats import load_stats
@@ -326,12 +447,22 @@ def main() -> int:
         sys.stdout.flush()
         os.dup2(saved, 1)
         os.close(saved)
-    # xgmi A/B last, in child processes (see the module docstring).
+    # BASELINE C3 / C4 hybrids (8 GPUs), each a child process per rank.
+    if a.hybrids == "on" or (a.hybrids == "auto" and world == 8 and on_gpu):
+        c3 = tuple(int(x) for x in a.c3.split(","))
+        c4 = tuple(int(x) for x in a.c4.split(","))
+        extra["hybrid_3d"] = _hybrid_block(a, world, rank, ".c3", "hybrid_3d", a.c3_model, c3,
+                                           "GPipe (mb + S - 1)(f_mb + b_mb), BASELINE.md C3")
+        extra["hybrid_3d_moe"] = _hybrid_block(a, world, rank, ".c4", "hybrid_3d_moe", a.c4_model, c4,
+                                               "GPipe (mb + S - 1)(f_mb + b_mb), BASELINE.md C4")
+    # xgmi A/B last, in child processes (see the module docstring); skipped
+    # when the exactness pass found the xgmi kernels wrong on these ranks.
     xgmi_on = on_gpu and (a.xgmi_ab == "on" or (a.xgmi_ab == "auto" and world > 1))
+    skip = {"error": "skipped: the xgmi exactness check failed on these ranks (see exact_detail)"}
     if a.c5_model != "none" and xgmi_on:
-        extra["comm_bound_xgmi"] = _xgmi_ab(a, world, rank, extra.get("comm_bound", {}))
+        extra["comm_bound_xgmi"] = _xgmi_ab(a, world, rank, extra.get("comm_bound", {})) if xgmi_exact_ok else skip
     if xgmi_on and a.xgmi_headline_steps > 0:
-        extra["headline_xgmi"] = _headline_xgmi(a, world, rank, doc)
+        extra["headline_xgmi"] = _headline_xgmi(a, world, rank, doc) if xgmi_exact_ok else skip
     if rank != 0:
         return 0
     g = doc["global"]
@@ -375,7 +506,12 @@ def main() -> int:
         # (the reference's energy_consumed, plots_pareto_energy.py); sum over GPUs and mean per GPU
         "energy_J_per_step": _energy(doc),
         "energy_source": g["dlnb"].get("energy_source"),
+        # ncclCommCount of every RCCL communicator of the headline run: proof
+        # that RCCL formed an N-rank group
+        "rccl_nranks": g["dlnb"].get("rccl_nranks"),
+        "runtime": g["dlnb"].get("runtime"),
     }
+    out.update(exact)
     out.update(extra)
     print(json.dumps(out), flush=True)
     return 0

@@ -66,6 +66,10 @@ class Communicator {
   // asynchronous failure (peer death, network error).
   virtual std::string async_error() { return ""; }
   virtual void abort() {}
+  // Ranks the underlying library says the communicator has (RCCL:
+  // ncclCommCount), -1 when the backend has no such library object. Reported
+  // so a multi-GPU run shows that RCCL really formed an N-rank communicator.
+  virtual int library_nranks() { return -1; }
 
  protected:
   int rank_ = 0;

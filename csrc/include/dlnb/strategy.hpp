@@ -24,11 +24,21 @@
 
 namespace dlnb {
 
+// One communicator the run created (recorded by select_backend's factory):
+// group name, member count and the library's own rank count.
+struct CommRecord {
+  std::string name;
+  std::string backend;
+  int nranks;
+  int library_nranks;  // RCCL: ncclCommCount; -1 for backends without one
+};
+
 struct Context {
   Options opt;
   std::unique_ptr<Bootstrap> boot;
   std::unique_ptr<Device> dev;
   std::unique_ptr<CommFactory> comms;
+  std::vector<CommRecord> comm_log;
   std::unique_ptr<ComputeEngine> compute;
   ModelStats stats;
   bool have_arch = false;
@@ -108,6 +118,9 @@ std::string select_backend(Context& ctx, const std::string& requested, const std
 
 // Collective correctness / bandwidth tool: dlnb commtest [options].
 int commtest_main(int argc, char** argv);
+// dlnb info: one JSON line with the HIP / RCCL runtime this binary bound and
+// the xgmi kernels' occupancy (blocks per CU) on the visible GPU.
+int info_main(int argc, char** argv);
 
 // Runs a whole benchmark (bootstrap -> setup -> warmup -> timed runs ->
 // report). Returns the report document (rank 0 has the gathered ranks).
@@ -131,6 +144,14 @@ struct CommStat {
 Json comm_stats_json(const std::vector<CommStat>& stats, const TimerSet& t);
 
 void print_topology(Context& ctx);
+
+// HIP runtime / RCCL this process is bound to: versions and the shared
+// objects they were loaded from (comm_rccl.cpp).
+Json runtime_info();
+
+// The communicator log as report JSON: "communicators" (every group) and
+// "rccl_nranks" (group name -> ncclCommCount, RCCL groups only).
+Json comm_log_json(const std::vector<CommRecord>& log);
 
 // Elementwise SGD-momentum over a bf16 shard (the optional --optimizer step).
 void optimizer_step(Context& ctx, Stream& s, void* param, void* mom, const void* grad, size_t n);

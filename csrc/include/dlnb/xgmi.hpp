@@ -28,6 +28,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <vector>
 
 #include "dlnb/common.hpp"
 
@@ -63,7 +64,22 @@ struct Peers {
   int rank;
   int nranks;
   int uncached;                // windows + flags in uncached memory (the default; see release_window)
+  int release_system;          // DLNB_XGMI_RELEASE=system: system-scope release/acquire even when uncached
 };
+
+// Blocks of a peer-waiting kernel that fit one CU (every such kernel is
+// register-capped for this; see DLNB_XGMI_KERNEL in xgmi.hip).
+constexpr int kBlocksPerCU = 4;
+
+// Occupancy (blocks per CU, hipOccupancyMaxActiveBlocksPerMultiprocessor)
+// of every peer-waiting kernel and dtype on the current device, as
+// {"rs_kernel<fp8_e4m3>", n} pairs; min_blocks_per_cu() is the smallest.
+struct KernelOccupancy {
+  const char* name;
+  int blocks_per_cu;
+};
+std::vector<KernelOccupancy> occupancy();
+int min_blocks_per_cu();
 
 enum class Op : int { AllGather, ReduceScatter, AllReduceOneShot, AllReduceTwoShot, AllToAll };
 

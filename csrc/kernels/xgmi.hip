@@ -24,6 +24,15 @@ namespace {
 
 constexpr int T = kThreads;
 
+// Every kernel that waits on peers is capped at 64 registers per lane: 8 of
+// its waves then fit a SIMD, i.e. kBlocksPerCU blocks of 512 threads per CU,
+// which is what the CU budget of a comm lane is computed from
+// (comm_xgmi.cpp). Uncapped, the fp8 reductions took 70-72 VGPRs (7 waves /
+// SIMD = 3 blocks per CU), so a lane of 4 * max_ctas blocks needed a third
+// more CUs than budgeted - blocks of one lane could then queue behind a
+// spinning kernel of another (tests/test_tools.py checks the code object).
+#define DLNB_XGMI_KERNEL __global__ void __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8)))
+
 // Flags are raised with a system-scope atomic RMW, not a store: L2 is per
 // XCD and not coherent across XCDs, and a plain store made through a peer's
 // IPC mapping can sit in the writer's L2 - the waiter, polling its flag
@@ -57,18 +66,21 @@ __device__ __forceinline__ uint32_t sys_load(uint32_t* p) {
 // for MTYPE-UC lines - a store's vmcnt slot is returned only once the write
 // is acknowledged by the memory it targets (local HBM or, through xGMI, the
 // peer's). Cached windows (DLNB_XGMI_MEM=fine|coarse) keep the full fence,
-// which is also the escape hatch if a platform ever acknowledges earlier.
+// and so does DLNB_XGMI_RELEASE=system on uncached windows: the escape hatch
+// if a platform ever acknowledges a remote store earlier (the bench's
+// multi-GPU exactness pass runs vmcnt first and system if that fails).
 __device__ __forceinline__ void release_window(const Peers& P) {
-  if (P.uncached)
+  if (P.uncached && !P.release_system)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 // After the peers' flags were seen: drop this CU's L1 lines (the window
 // slots were read two pieces ago) - the L2 holds no window data when the
-// windows are uncached; cached windows take the full system acquire.
+// windows are uncached; cached windows (or the system release mode) take
+// the full system-scope acquire.
 __device__ __forceinline__ void acquire_window(const Peers& P) {
-  if (P.uncached)
+  if (P.uncached && !P.release_system)
     asm volatile("buffer_inv sc0" ::: "memory");
   else
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -288,18 +300,33 @@ struct Elt<DType::FP8_E4M3> : Fp8<false> {};
 template <>
 struct Elt<DType::FP8_E5M2> : Fp8<true> {};
 
+// Loops over ranks are unrolled to kMaxRanks with a guard, never indexed by
+// a run-time count: the per-rank pointer arrays then stay in (scalar)
+// registers instead of going to scratch under the 64-register cap.
+
+// Sum of vector i over the first ns sources, unpacked into acc (fp32).
+template <DType D>
+__device__ __forceinline__ void sum_vec(float* acc, const uint4* const* srcs, int ns, size_t i) {
+  using E = Elt<D>;
+  float f[E::N];
+  E::unpack(srcs[0][i], acc);
+#pragma unroll
+  for (int s = 1; s < kMaxRanks; ++s) {
+    if (s < ns) {
+      E::unpack(srcs[s][i], f);
+#pragma unroll
+      for (int k = 0; k < E::N; ++k) acc[k] += f[k];
+    }
+  }
+}
+
 // out[i] = sum over srcs of vector i, for i in [lo, hi).
 template <DType D>
 __device__ __forceinline__ void reduce_vec(uint4* out, const uint4* const* srcs, int ns, size_t lo, size_t hi) {
   using E = Elt<D>;
   for (size_t i = lo + threadIdx.x; i < hi; i += T) {
-    float acc[E::N], f[E::N];
-    E::unpack(srcs[0][i], acc);
-    for (int s = 1; s < ns; ++s) {
-      E::unpack(srcs[s][i], f);
-#pragma unroll
-      for (int k = 0; k < E::N; ++k) acc[k] += f[k];
-    }
+    float acc[E::N];
+    sum_vec<D>(acc, srcs, ns, i);
     out[i] = E::pack(acc);
   }
 }
@@ -311,7 +338,9 @@ __device__ __forceinline__ void reduce_tail(char* out, const char* const* srcs, 
   if (blockIdx.x != gridDim.x - 1) return;
   for (size_t i = e0 + threadIdx.x; i < e1; i += T) {
     float a = 0.f;
-    for (int s = 0; s < ns; ++s) a += E::ld(srcs[s], i);
+#pragma unroll
+    for (int s = 0; s < kMaxRanks; ++s)
+      if (s < ns) a += E::ld(srcs[s], i);
     E::st(out, i, a);
   }
 }
@@ -319,6 +348,9 @@ __device__ __forceinline__ void reduce_tail(char* out, const char* const* srcs, 
 // --------------------------------------------------------------- kernels
 
 __device__ __forceinline__ int peer_at(const Peers& P, int j) { return (P.rank + j) % P.nranks; }
+
+// for (r = 0; r < n; ++r) unrolled to kMaxRanks (see sum_vec)
+#define DLNB_FOR_RANKS(r, lo, n) _Pragma("unroll") for (int r = (lo); r < kMaxRanks; ++r) if (r < (n))
 
 // Push vectors [lo, hi) of src to slot `slot_off` of every peer's window
 // (and to `own` unless null): 4 loads in flight per thread, each loaded
@@ -345,7 +377,7 @@ __device__ __forceinline__ void push_all(const Peers& P, const uint4* __restrict
   }
 }
 
-__global__ void __launch_bounds__(T) ag_kernel(Peers P, CollPiece c) {
+DLNB_XGMI_KERNEL ag_kernel(Peers P, CollPiece c) {
   const uint32_t ep = begin_seq(P, kCtlCollEpoch);
   const size_t rg = (ep & 1) * c.region;
   const size_t nv = c.bytes / 16;
@@ -368,7 +400,7 @@ __global__ void __launch_bounds__(T) ag_kernel(Peers P, CollPiece c) {
   end_seq(P, kCtlCollEpoch, kCtlCollDone, ep);
 }
 
-__global__ void __launch_bounds__(T) a2a_kernel(Peers P, CollPiece c) {
+DLNB_XGMI_KERNEL a2a_kernel(Peers P, CollPiece c) {
   const uint32_t ep = begin_seq(P, kCtlCollEpoch);
   const size_t rg = (ep & 1) * c.region;
   const size_t nv = c.bytes / 16;
@@ -399,7 +431,7 @@ __global__ void __launch_bounds__(T) a2a_kernel(Peers P, CollPiece c) {
 }
 
 template <DType D>
-__global__ void __launch_bounds__(T) rs_kernel(Peers P, CollPiece c) {
+DLNB_XGMI_KERNEL rs_kernel(Peers P, CollPiece c) {
   const uint32_t ep = begin_seq(P, kCtlCollEpoch);
   const size_t rg = (ep & 1) * c.region;
   const size_t es = sizeof(uint4) / Elt<D>::N;
@@ -417,15 +449,15 @@ __global__ void __launch_bounds__(T) rs_kernel(Peers P, CollPiece c) {
   const uint4* srcs[kMaxRanks];
   const char* srcb[kMaxRanks];
   srcb[0] = c.send + static_cast<size_t>(P.rank) * c.send_stride;
-  for (int j = 1; j < P.nranks; ++j) srcb[j] = P.win[P.rank] + rg + c.slot * peer_at(P, j);
-  for (int j = 0; j < P.nranks; ++j) srcs[j] = V(srcb[j]);
+  DLNB_FOR_RANKS(j, 1, P.nranks) srcb[j] = P.win[P.rank] + rg + c.slot * peer_at(P, j);
+  DLNB_FOR_RANKS(j, 0, P.nranks) srcs[j] = V(srcb[j]);
   reduce_vec<D>(V(c.recv), srcs, P.nranks, lo, hi);
   reduce_tail<D>(c.recv, srcb, P.nranks, nv * 16 / es, c.bytes / es);
   end_seq(P, kCtlCollEpoch, kCtlCollDone, ep);
 }
 
 template <DType D>
-__global__ void __launch_bounds__(T) ar1_kernel(Peers P, CollPiece c) {
+DLNB_XGMI_KERNEL ar1_kernel(Peers P, CollPiece c) {
   const uint32_t ep = begin_seq(P, kCtlCollEpoch);
   const size_t rg = (ep & 1) * c.region;
   const size_t es = sizeof(uint4) / Elt<D>::N;
@@ -438,8 +470,8 @@ __global__ void __launch_bounds__(T) ar1_kernel(Peers P, CollPiece c) {
   // every rank sums in the same (rank) order -> bitwise identical results
   const uint4* srcs[kMaxRanks];
   const char* srcb[kMaxRanks];
-  for (int r = 0; r < P.nranks; ++r) srcb[r] = r == P.rank ? c.send : P.win[P.rank] + rg + c.slot * r;
-  for (int r = 0; r < P.nranks; ++r) srcs[r] = V(srcb[r]);
+  DLNB_FOR_RANKS(r, 0, P.nranks) srcb[r] = r == P.rank ? c.send : P.win[P.rank] + rg + c.slot * r;
+  DLNB_FOR_RANKS(r, 0, P.nranks) srcs[r] = V(srcb[r]);
   reduce_vec<D>(V(c.recv), srcs, P.nranks, lo, hi);
   reduce_tail<D>(c.recv, srcb, P.nranks, nv * 16 / es, c.bytes / es);
   end_seq(P, kCtlCollEpoch, kCtlCollDone, ep);
@@ -448,7 +480,7 @@ __global__ void __launch_bounds__(T) ar1_kernel(Peers P, CollPiece c) {
 // Two-shot (reduce-scatter + all-gather inside one kernel). c.bytes is a
 // multiple of 16; chunk p = vectors [p*cv, min((p+1)*cv, nv)).
 template <DType D>
-__global__ void __launch_bounds__(T) ar2_kernel(Peers P, CollPiece c) {
+DLNB_XGMI_KERNEL ar2_kernel(Peers P, CollPiece c) {
   const uint32_t ep = begin_seq(P, kCtlCollEpoch);
   const size_t rg = (ep & 1) * c.region;
   const size_t nv = c.bytes / 16;
@@ -464,26 +496,20 @@ __global__ void __launch_bounds__(T) ar2_kernel(Peers P, CollPiece c) {
   exchange(P, 0, ep);
   // 2. reduce my chunk (rank order), write it to recv and to every peer's AG slot[rank]
   const uint4* srcs[kMaxRanks];
-  for (int r = 0; r < P.nranks; ++r)
-    srcs[r] = r == P.rank ? V(c.send) + P.rank * cv : V(P.win[P.rank] + rg + c.slot * r);
+  DLNB_FOR_RANKS(r, 0, P.nranks) srcs[r] = r == P.rank ? V(c.send) + P.rank * cv : V(P.win[P.rank] + rg + c.slot * r);
   uint4* outs[kMaxRanks];
-  for (int j = 1; j < P.nranks; ++j) outs[j - 1] = V(P.win[peer_at(P, j)] + rg + c.ag_off + c.slot * P.rank);
+  DLNB_FOR_RANKS(j, 1, P.nranks) outs[j - 1] = V(P.win[peer_at(P, j)] + rg + c.ag_off + c.slot * P.rank);
   // srcs are chunk-relative; recv chunk rank
   {
     using E = Elt<D>;
     const size_t h = chunk_hi(P.rank, hi);
     uint4* out = V(c.recv) + P.rank * cv;
     for (size_t i = lo + threadIdx.x; i < h; i += T) {
-      float acc[E::N], f[E::N];
-      E::unpack(srcs[0][i], acc);
-      for (int s = 1; s < P.nranks; ++s) {
-        E::unpack(srcs[s][i], f);
-#pragma unroll
-        for (int k = 0; k < E::N; ++k) acc[k] += f[k];
-      }
+      float acc[E::N];
+      sum_vec<D>(acc, srcs, P.nranks, i);
       uint4 r = E::pack(acc);
       out[i] = r;
-      for (int o = 0; o + 1 < P.nranks; ++o) outs[o][i] = r;
+      DLNB_FOR_RANKS(o, 0, P.nranks - 1) outs[o][i] = r;
     }
   }
   exchange(P, 1, ep);
@@ -499,38 +525,36 @@ __global__ void __launch_bounds__(T) ar2_kernel(Peers P, CollPiece c) {
 
 // dst[j][i] = src[i] for every rank j (own first, then rank-staggered), 4
 // loads in flight per thread.
-__device__ __forceinline__ void push_ptrs(const Peers& P, const uint4* __restrict__ src, uint4* const* dst, size_t lo,
+__device__ __forceinline__ void push_ptrs(const Peers& P, const uint4* __restrict__ src, char* const* dst, size_t lo,
                                           size_t hi) {
   size_t i = lo + threadIdx.x;
   for (; i + 3 * T < hi; i += 4 * T) {
     uint4 v[4] = {src[i], src[i + T], src[i + 2 * T], src[i + 3 * T]};
     for (int j = 0; j < P.nranks; ++j) {
-      uint4* d = dst[peer_at(P, j)];
+      uint4* d = V(dst[peer_at(P, j)]);
 #pragma unroll
       for (int u = 0; u < 4; ++u) d[i + u * T] = v[u];
     }
   }
   for (; i < hi; i += T) {
     const uint4 v = src[i];
-    for (int j = 0; j < P.nranks; ++j) dst[peer_at(P, j)][i] = v;
+    for (int j = 0; j < P.nranks; ++j) V(dst[peer_at(P, j)])[i] = v;
   }
 }
 
-__global__ void __launch_bounds__(T) ag_direct_kernel(Peers P, DirectPiece c) {
+DLNB_XGMI_KERNEL ag_direct_kernel(Peers P, DirectPiece c) {
   const uint32_t ep = begin_seq(P, kCtlCollEpoch);
   exchange(P, 0, ep);  // every rank's receive buffer is free
   const size_t nv = c.bytes / 16;
   size_t lo, hi;
   blk_range(nv, lo, hi);
-  uint4* dst[kMaxRanks];
-  for (int r = 0; r < P.nranks; ++r) dst[r] = V(c.dst[r]);
-  push_ptrs(P, V(c.src[P.rank]), dst, lo, hi);
+  push_ptrs(P, V(c.src[P.rank]), c.dst, lo, hi);
   for (int r = 0; r < P.nranks; ++r) copy_tail(c.dst[r], c.src[P.rank], nv * 16, c.bytes);
   exchange(P, 1, ep);  // every rank's block landed in my receive buffer
   end_seq(P, kCtlCollEpoch, kCtlCollDone, ep);
 }
 
-__global__ void __launch_bounds__(T) a2a_direct_kernel(Peers P, DirectPiece c) {
+DLNB_XGMI_KERNEL a2a_direct_kernel(Peers P, DirectPiece c) {
   const uint32_t ep = begin_seq(P, kCtlCollEpoch);
   exchange(P, 0, ep);  // every rank's receive buffer is free
   const size_t nv = c.bytes / 16;
@@ -548,7 +572,7 @@ __global__ void __launch_bounds__(T) a2a_direct_kernel(Peers P, DirectPiece c) {
 }
 
 template <DType D>
-__global__ void __launch_bounds__(T) rs_direct_kernel(Peers P, DirectPiece c) {
+DLNB_XGMI_KERNEL rs_direct_kernel(Peers P, DirectPiece c) {
   const size_t es = sizeof(uint4) / Elt<D>::N;
   const uint32_t ep = begin_seq(P, kCtlCollEpoch);
   exchange(P, 0, ep);  // every rank's send buffer holds its data
@@ -556,7 +580,7 @@ __global__ void __launch_bounds__(T) rs_direct_kernel(Peers P, DirectPiece c) {
   size_t lo, hi;
   blk_range(nv, lo, hi);
   const uint4* srcs[kMaxRanks];
-  for (int r = 0; r < P.nranks; ++r) srcs[r] = V(c.src[r]);  // rank order: identical sums everywhere
+  DLNB_FOR_RANKS(r, 0, P.nranks) srcs[r] = V(c.src[r]);  // rank order: identical sums everywhere
   reduce_vec<D>(V(c.out), srcs, P.nranks, lo, hi);
   reduce_tail<D>(c.out, c.src, P.nranks, nv * 16 / es, c.bytes / es);
   exchange(P, 1, ep);  // every rank is done reading my send buffer
@@ -564,7 +588,7 @@ __global__ void __launch_bounds__(T) rs_direct_kernel(Peers P, DirectPiece c) {
 }
 
 template <DType D>
-__global__ void __launch_bounds__(T) ar_direct_kernel(Peers P, DirectPiece c) {
+DLNB_XGMI_KERNEL ar_direct_kernel(Peers P, DirectPiece c) {
   using E = Elt<D>;
   const uint32_t ep = begin_seq(P, kCtlCollEpoch);
   exchange(P, 0, ep);
@@ -574,30 +598,21 @@ __global__ void __launch_bounds__(T) ar_direct_kernel(Peers P, DirectPiece c) {
   size_t lo, hi;
   blk_range(c1 - c0, lo, hi);
   const uint4* srcs[kMaxRanks];
-  uint4* dst[kMaxRanks];
-  for (int r = 0; r < P.nranks; ++r) {
-    srcs[r] = V(c.src[r]) + c0;
-    dst[r] = V(c.dst[r]) + c0;
-  }
+  DLNB_FOR_RANKS(r, 0, P.nranks) srcs[r] = V(c.src[r]) + c0;
   // chunk `rank` of every send buffer, summed in rank order, into chunk
   // `rank` of every receive buffer (only this rank reads or writes that
   // chunk anywhere, so send and receive may alias)
   for (size_t i = lo + threadIdx.x; i < hi; i += T) {
-    float acc[E::N], f[E::N];
-    E::unpack(srcs[0][i], acc);
-    for (int r = 1; r < P.nranks; ++r) {
-      E::unpack(srcs[r][i], f);
-#pragma unroll
-      for (int k = 0; k < E::N; ++k) acc[k] += f[k];
-    }
+    float acc[E::N];
+    sum_vec<D>(acc, srcs, P.nranks, i);
     const uint4 v = E::pack(acc);
-    for (int j = 0; j < P.nranks; ++j) dst[peer_at(P, j)][i] = v;
+    for (int j = 0; j < P.nranks; ++j) (V(c.dst[peer_at(P, j)]) + c0)[i] = v;
   }
   exchange(P, 1, ep);
   end_seq(P, kCtlCollEpoch, kCtlCollDone, ep);
 }
 
-__global__ void __launch_bounds__(T) send_kernel(Peers P, const char* buf, size_t bytes, int dst, size_t off,
+DLNB_XGMI_KERNEL send_kernel(Peers P, const char* buf, size_t bytes, int dst, size_t off,
                                                  size_t slot) {
   const uint32_t n = begin_seq(P, kCtlSendSeq + dst);
   if (threadIdx.x == 0 && n > 2) wait_geq(P.flags[P.rank] + kFlagP2PConsumed + dst, n - 2, P);
@@ -614,7 +629,7 @@ __global__ void __launch_bounds__(T) send_kernel(Peers P, const char* buf, size_
   end_seq(P, kCtlSendSeq + dst, kCtlSendDone + dst, n);
 }
 
-__global__ void __launch_bounds__(T) recv_kernel(Peers P, char* buf, size_t bytes, int src, size_t off, size_t slot) {
+DLNB_XGMI_KERNEL recv_kernel(Peers P, char* buf, size_t bytes, int src, size_t off, size_t slot) {
   const uint32_t n = begin_seq(P, kCtlRecvSeq + src);
   if (threadIdx.x == 0) wait_geq(P.flags[P.rank] + kFlagP2PSeq + static_cast<size_t>(src) * kMaxBlocks + blockIdx.x, n, P);
   __syncthreads();
@@ -857,6 +872,49 @@ void launch_local_coll(LocalColl op, char* const* recv, const char* const* send,
     case LocalColl::AllToAll: local_coll_dtype<LocalColl::AllToAll>(a, t, vec, grid, s); break;
   }
   DLNB_HIP_CHECK(hipGetLastError());
+}
+
+namespace {
+
+template <typename K>
+void occ(std::vector<KernelOccupancy>& out, const char* name, K kernel) {
+  int n = 0;
+  DLNB_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, T, 0));
+  out.push_back({name, n});
+}
+
+#define DLNB_XGMI_OCC_TYPED(KERNEL)                                \
+  occ(v, #KERNEL "<bf16>", KERNEL<DType::BF16>);                   \
+  occ(v, #KERNEL "<fp16>", KERNEL<DType::FP16>);                   \
+  occ(v, #KERNEL "<fp32>", KERNEL<DType::FP32>);                   \
+  occ(v, #KERNEL "<fp8_e4m3>", KERNEL<DType::FP8_E4M3>);           \
+  occ(v, #KERNEL "<fp8_e5m2>", KERNEL<DType::FP8_E5M2>);
+
+}  // namespace
+
+std::vector<KernelOccupancy> occupancy() {
+  std::vector<KernelOccupancy> v;
+  occ(v, "ag_kernel", ag_kernel);
+  occ(v, "a2a_kernel", a2a_kernel);
+  occ(v, "ag_direct_kernel", ag_direct_kernel);
+  occ(v, "a2a_direct_kernel", a2a_direct_kernel);
+  occ(v, "send_kernel", send_kernel);
+  occ(v, "recv_kernel", recv_kernel);
+  DLNB_XGMI_OCC_TYPED(rs_kernel)
+  DLNB_XGMI_OCC_TYPED(ar1_kernel)
+  DLNB_XGMI_OCC_TYPED(ar2_kernel)
+  DLNB_XGMI_OCC_TYPED(rs_direct_kernel)
+  DLNB_XGMI_OCC_TYPED(ar_direct_kernel)
+  return v;
+}
+
+int min_blocks_per_cu() {
+  static int cached = [] {
+    int m = kBlocksPerCU;
+    for (const auto& k : occupancy()) m = std::min(m, k.blocks_per_cu);
+    return std::max(1, m);
+  }();
+  return cached;
 }
 
 void launch_send(const Peers& p, const char* buf, size_t bytes, int dst, size_t off, size_t slot, int blocks,

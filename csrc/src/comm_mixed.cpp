@@ -56,7 +56,8 @@ class MixedComm : public Communicator {
     pick(recv_count * dtype_size(t)).reduce_scatter(send, recv, recv_count, t, s);
   }
   void all_to_all(const void* send, void* recv, size_t count, DType t, Stream& s) override {
-    // xgmi all-to-all is out-of-place only
+    // in place: RCCL when there is one (xgmi stages in-place all-to-alls
+    // through its windows, never the zero-copy path)
     Communicator& c = send == recv && big_ ? *big_ : pick(count * dtype_size(t));
     c.all_to_all(send, recv, count, t, s);
   }
@@ -86,6 +87,7 @@ class MixedComm : public Communicator {
     if (big_) big_->abort();
     if (small_) small_->abort();
   }
+  int library_nranks() override { return big_ ? big_->library_nranks() : -1; }
 
  private:
   struct P2P {

@@ -7,10 +7,13 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
+
 #include <cstring>
 #include <sstream>
 
 #include "dlnb/comm.hpp"
+#include "dlnb/json.hpp"
 
 #define DLNB_NCCL_CHECK(expr)                                                            \
   do {                                                                                   \
@@ -105,6 +108,11 @@ class RcclComm : public Communicator {
       comm_ = nullptr;
     }
   }
+  int library_nranks() override {
+    int n = -1;
+    if (comm_ && ncclCommCount(comm_, &n) != ncclSuccess) n = -1;
+    return n;
+  }
 
  private:
   ncclComm_t comm_ = nullptr;
@@ -131,6 +139,33 @@ class RcclFactory : public CommFactory {
 
 std::unique_ptr<CommFactory> make_rccl_factory(HostGroup& world, Device& dev) {
   return std::unique_ptr<CommFactory>(new RcclFactory(world, dev));
+}
+
+namespace {
+std::string lib_of(const void* sym) {
+  Dl_info info;
+  if (dladdr(sym, &info) && info.dli_fname) return info.dli_fname;
+  return "?";
+}
+}  // namespace
+
+Json runtime_info() {
+  // Which HIP runtime and RCCL this process bound (a process that imported
+  // torch first binds torch's bundled copies; the CLI binaries and bench.py,
+  // which never import torch, bind /opt/rocm's).
+  Json j = Json::object();
+  int v = 0;
+  if (ncclGetVersion(&v) == ncclSuccess) {
+    j["rccl_version_code"] = v;
+    std::ostringstream s;
+    s << v / 10000 << "." << (v / 100) % 100 << "." << v % 100;
+    j["rccl_version"] = s.str();
+  }
+  j["librccl"] = lib_of(reinterpret_cast<const void*>(&ncclGetVersion));
+  int hv = 0;
+  if (hipRuntimeGetVersion(&hv) == hipSuccess) j["hip_runtime_version"] = hv;
+  j["libamdhip64"] = lib_of(reinterpret_cast<const void*>(&hipRuntimeGetVersion));
+  return j;
 }
 
 double busbw_factor(CollKind k, int n) {

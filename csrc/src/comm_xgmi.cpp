@@ -89,10 +89,12 @@ class XgmiComm : public Communicator {
     DLNB_REQUIRE(size_ <= xgmi::kMaxRanks, "xgmi backend: group " << name << " has " << size_ << " ranks (max "
                                                                  << xgmi::kMaxRanks << ", one node)");
     max_blocks_ = static_cast<int>(std::max<long long>(1, std::min<long long>(xgmi::kMaxBlocks, env_int("DLNB_XGMI_BLOCKS", 256))));
-    // CU budget of this comm lane (runner.cpp): 4 of these blocks fit a CU
-    // beside nothing else, so the lane's kernels never need more CUs than
-    // the budget even when several lanes' kernels are live at once.
-    if (max_ctas > 0) max_blocks_ = std::min(max_blocks_, 4 * max_ctas);
+    // CU budget of this comm lane (runner.cpp): blocks_per_cu of these
+    // blocks fit a CU beside nothing else (the measured occupancy of the
+    // least-occupant kernel; every kernel is register-capped for 4), so the
+    // lane's kernels never need more CUs than the budget even when several
+    // lanes' kernels are live at once.
+    if (max_ctas > 0) max_blocks_ = std::min(max_blocks_, xgmi::min_blocks_per_cu() * max_ctas);
     oneshot_ = static_cast<size_t>(env_int("DLNB_XGMI_ONESHOT_KB", 256)) << 10;
     const size_t cap = std::max<size_t>(capacity, 4096);
     // Collective region per parity: AG/RS/A2A need W slots of a piece, the
@@ -160,6 +162,9 @@ class XgmiComm : public Communicator {
     peers_.rank = rank_;
     peers_.nranks = size_;
     peers_.uncached = mem != "coarse" && mem != "fine";
+    const std::string rel = env_or("DLNB_XGMI_RELEASE", "vmcnt");
+    DLNB_REQUIRE(rel == "vmcnt" || rel == "system", "DLNB_XGMI_RELEASE must be vmcnt or system (got " << rel << ")");
+    peers_.release_system = rel == "system";
     // Nobody may free its window before every member has mapped it.
     const std::string done = key.str() + "opened";
     if (world.store().add(done, 1) == size_) world.store().set(done + "/go", "1");
@@ -264,10 +269,13 @@ class XgmiComm : public Communicator {
   }
 
   void all_to_all(const void* send, void* recv, size_t count, DType t, Stream& s) override {
-    DLNB_REQUIRE(send != recv, "xgmi all_to_all is out-of-place only");
     const size_t es = dtype_size(t), bytes = count * es;
     size_t off = 0;
-    if (const Reg* r = size_ > 1 && bytes > 0 ? find(recv, bytes * size_, off) : nullptr) {
+    // In place goes through the windows: each block reads its slice of every
+    // send block before the exchange and writes the same slice of the receive
+    // blocks after it, while the zero-copy path writes peers' receive buffers
+    // that may still be their unread send buffers.
+    if (const Reg* r = size_ > 1 && bytes > 0 && send != recv ? find(recv, bytes * size_, off) : nullptr) {
       xgmi::DirectPiece c = direct(t, bytes);
       c.src[rank_] = static_cast<const char*>(send);
       for (int q = 0; q < size_; ++q) c.dst[q] = r->peer[q] + off + static_cast<size_t>(rank_) * bytes;

@@ -23,13 +23,16 @@
 // Reference equivalent: none (DLNetBench relies on nccl-tests externally).
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <iostream>
 #include <algorithm>
 #include <thread>
 #include <sstream>
 
 #include "dlnb/strategy.hpp"
+#include "dlnb/xgmi.hpp"
 
 namespace dlnb {
 
@@ -76,17 +79,19 @@ struct Tester {
   long long failures = 0;
   // --registered: buffers of the maximum size, registered once (a
   // registration pairs buffers by order across ranks, so they are not
-  // re-created per size); take(i) hands out buffer i of the pool.
-  std::vector<Buffer> pool;
+  // re-created per size); get(.., i) hands out buffer i of the pool.
+  std::vector<Buffer>* pool = nullptr;
+  // also check an in-place all-to-all (backends that support it: xgmi)
+  bool inplace_a2a = false;
   // Buffer i of at least `bytes`: a fresh allocation kept in `keep`, or the
   // registered pool's buffer i.
   void* get(std::vector<Buffer>& keep, size_t bytes, size_t i) {
-    if (pool.empty()) {
+    if (!pool || pool->empty()) {
       keep.push_back(ctx.dev->alloc(std::max<size_t>(1, bytes)));
       return keep.back().data();
     }
-    DLNB_REQUIRE(i < pool.size() && bytes <= pool[i].bytes(), "commtest: registered pool too small");
-    return pool[i].data();
+    DLNB_REQUIRE(i < pool->size() && bytes <= (*pool)[i].bytes(), "commtest: registered pool too small");
+    return (*pool)[i].data();
   }
 
   void upload(void* b, const std::vector<char>& h) {
@@ -150,6 +155,13 @@ struct Tester {
     got = download(b, n * W * es);
     for (int p = 0; p < W; ++p)
       for (size_t i = 0; i < n; ++i) expect("all_to_all", n, got, p * n + i, val(p, me * n + i, t));
+    if (inplace_a2a) {
+      upload(a, pattern(me, 0, n * W));
+      comm.all_to_all(a, a, n, t, s);
+      got = download(a, n * W * es);
+      for (int p = 0; p < W; ++p)
+        for (size_t i = 0; i < n; ++i) expect("all_to_all(in-place)", n, got, p * n + i, val(p, me * n + i, t));
+    }
     s.synchronize();
     if (failures != before) std::fprintf(stderr, "[commtest] rank %d: n=%zu FAILED\n", me, n);
   }
@@ -225,11 +237,197 @@ struct Tester {
   }
 };
 
+std::unique_ptr<CommFactory> factory_for(Context& ctx, const std::string& b) {
+  if (b == "rccl") return make_rccl_factory(ctx.hg(), *ctx.dev);
+  if (b == "xgmi") return make_xgmi_factory(ctx.hg(), *ctx.dev);
+  if (b == "mixed") return make_mixed_factory(ctx.hg(), *ctx.dev);
+  if (b == "cpu") return make_shm_factory(ctx.hg(), *ctx.dev);
+  DLNB_THROW("commtest --suite: unknown backend " << b << " (rccl, xgmi, mixed, cpu)");
+}
+
+// Modes a backend is checked in: eager enqueue and HIP-graph replay; xgmi
+// also with registered (zero-copy) buffers, eager and replayed.
+std::vector<std::string> suite_modes(const std::string& b) {
+  if (b == "xgmi") return {"staged", "registered", "graph", "registered_graph"};
+  if (b == "cpu") return {"eager"};
+  return {"eager", "graph"};
+}
+
+// --suite: the exactness pass of a multi-GPU job (bench.py runs it as a
+// child of every rank before any timed phase). For each backend, mode and
+// wire dtype it checks every collective plus a ring send/recv at every size
+// exactly, and reports one JSON line (rank 0): per-combination results,
+// "exact": {backend: ok, backend_mode: ok}, the xgmi release mode that
+// passed and the RCCL communicator's own rank count (ncclCommCount).
+// xgmi runs with DLNB_XGMI_RELEASE as set (default vmcnt); with
+// --release-fallback a failing xgmi backend is re-checked with the
+// system-scope release/acquire.
+int run_suite(Context& ctx, const std::vector<std::string>& backends, const std::vector<std::string>& dtypes,
+              std::vector<size_t> sizes, bool fallback, const std::string& json_path) {
+  const int W = ctx.world(), me = ctx.rank();
+  if (sizes.empty()) sizes = {4097, 300000, (size_t(1) << 21) + 5};
+  size_t maxn = 1, maxes = 1;
+  for (size_t n : sizes) maxn = std::max(maxn, n);
+  std::vector<DType> types;
+  for (const auto& d : dtypes) {
+    types.push_back(parse_dtype(d));
+    maxes = std::max(maxes, dtype_size(types.back()));
+  }
+  std::vector<int> all;
+  for (int r = 0; r < W; ++r) all.push_back(r);
+  const double t_start = now();
+  Json results = Json::array();
+  Json exact = Json::object();
+  Json release_used = nullptr;
+  int rccl_nranks = -1;
+  auto stream = ctx.dev->create_stream(true);
+  int uid = 0;
+  for (const std::string& b : backends) {
+    std::vector<std::string> releases = {""};
+    if (b == "xgmi" || b == "mixed") {
+      releases = {env_or("DLNB_XGMI_RELEASE", "vmcnt")};
+      if (fallback && releases[0] != "system") releases.push_back("system");
+    }
+    const std::string saved_release = env_or("DLNB_XGMI_RELEASE", "");
+    bool backend_ok = false;
+    Json per_mode = Json::object();
+    for (const std::string& rel : releases) {
+      if (!rel.empty()) setenv("DLNB_XGMI_RELEASE", rel.c_str(), 1);
+      auto fac = factory_for(ctx, b);
+      backend_ok = true;
+      per_mode = Json::object();
+      // registered and unregistered modes use separate communicators (a
+      // registration is permanent); graph and eager share one.
+      for (bool want_reg : {false, true}) {
+        std::vector<std::string> modes;
+        for (const auto& m : suite_modes(b))
+          if ((m.find("registered") != std::string::npos) == want_reg) modes.push_back(m);
+        if (modes.empty()) continue;
+        const std::string tag = "suite/" + std::to_string(uid++) + "/" + b;
+        auto comm = fac->create(tag + "/world", all, maxn * W * maxes, false);
+        auto link = fac->create(tag + "/link", all, maxn * maxes, true);
+        if (b == "rccl" && comm->library_nranks() >= 0) rccl_nranks = comm->library_nranks();
+        std::vector<Buffer> pool;
+        if (want_reg && comm->wants_peer_buffers()) {
+          for (int i = 0; i < 9; ++i) {
+            pool.push_back(ctx.dev->alloc_peer(std::max<size_t>(16, maxn * W * maxes)));
+            comm->register_buffer(pool.back().data(), pool.back().bytes());
+          }
+        }
+        for (const std::string& mode : modes) {
+          const bool graph = mode.find("graph") != std::string::npos;
+          bool mode_ok = true;
+          for (DType t : types) {
+            const double t0 = now();
+            Tester T{ctx, *comm, *stream, t, dtype_size(t), W, me};
+            T.pool = pool.empty() ? nullptr : &pool;
+            T.inplace_a2a = comm->backend_name() == "XGMI";
+            std::string error;
+            try {
+              for (size_t n : sizes) {
+                if (graph) {
+                  T.check_graph(*link, n, 3);
+                } else {
+                  T.check(n);
+                  T.check_p2p(*link, n);
+                }
+              }
+              stream->synchronize();
+            } catch (const std::exception& e) {
+              error = e.what();
+              ++T.failures;
+            }
+            for (Communicator* c : {comm.get(), link.get()}) {
+              std::string err = c->async_error();
+              if (!err.empty()) {
+                if (error.empty()) error = err;
+                ++T.failures;
+              }
+            }
+            const long long fails = static_cast<long long>(ctx.hg().allreduce_sum(static_cast<double>(T.failures)));
+            const bool ok = fails == 0;
+            mode_ok = mode_ok && ok;
+            if (!ok) std::fprintf(stderr, "[commtest] suite %s/%s/%s%s%s: %lld failures %s\n", b.c_str(), mode.c_str(),
+                                  dtype_name(t), rel.empty() ? "" : " release=", rel.c_str(), fails, error.c_str());
+            Json r = Json::object();
+            r["backend"] = b;
+            r["mode"] = mode;
+            r["dtype"] = dtype_name(t);
+            if (!rel.empty()) r["release"] = rel;
+            r["ok"] = ok;
+            r["failures"] = fails;
+            r["seconds"] = now() - t0;
+            if (!error.empty()) r["error"] = error.substr(0, 200);
+            results.push_back(r);
+          }
+          per_mode[b + "_" + mode] = mode_ok;
+          backend_ok = backend_ok && mode_ok;
+        }
+        stream->synchronize();
+        ctx.hg().barrier();  // nobody frees a registered buffer a peer still maps
+      }
+      if (backend_ok) {
+        if (!rel.empty()) release_used = rel;
+        break;
+      }
+    }
+    if (!saved_release.empty())
+      setenv("DLNB_XGMI_RELEASE", saved_release.c_str(), 1);
+    else
+      unsetenv("DLNB_XGMI_RELEASE");
+    exact[b] = backend_ok;
+    for (const auto& kv : per_mode.items()) exact[kv.first] = kv.second;
+  }
+  bool all_ok = true;
+  for (const auto& kv : exact.items()) all_ok = all_ok && kv.second.as_bool();
+  // The verdicts are all-reduced, so every rank holds the same report; each
+  // writes --json (so every rank of a job can act on it), rank 0 prints it.
+  Json j = Json::object();
+  j["commtest"] = "suite";
+  j["world_size"] = W;
+  j["rank"] = me;
+  Json sz = Json::array();
+  for (size_t n : sizes) sz.push_back(static_cast<double>(n));
+  j["sizes"] = sz;
+  j["exact"] = exact;
+  j["ok"] = all_ok;
+  j["xgmi_release"] = release_used;
+  j["rccl_nranks"] = rccl_nranks;
+  j["results"] = results;
+  j["seconds"] = now() - t_start;
+  if (ctx.dev->kind() == DeviceKind::GPU) j["runtime"] = runtime_info();
+  if (me == 0) std::cout << j.dump() << std::endl;
+  if (!json_path.empty()) {
+    std::ofstream f(json_path);
+    f << j.dump(1) << "\n";
+  }
+  return all_ok ? 0 : 3;
+}
+
 }  // namespace
 
+int info_main(int argc, char** argv) {
+  (void)argc, (void)argv;
+  Json j = Json::object();
+  j["version"] = "dlnetbench_amd 0.1.0 (gfx950)";
+  const int ngpu = gpu_device_count();
+  j["gpus"] = ngpu;
+  if (ngpu > 0) {
+    j["runtime"] = runtime_info();
+    Json occ = Json::object();
+    for (const auto& k : xgmi::occupancy()) occ[k.name] = k.blocks_per_cu;
+    j["xgmi_occupancy_blocks_per_cu"] = occ;
+    j["xgmi_min_blocks_per_cu"] = xgmi::min_blocks_per_cu();
+    j["xgmi_threads_per_block"] = xgmi::kThreads;
+  }
+  std::cout << j.dump() << std::endl;
+  return 0;
+}
+
 int commtest_main(int argc, char** argv) {
-  std::string backend = "auto", devices, dtype = "bf16", sizes_s, json_path;
-  bool bench = false, graph = false, registered = false;
+  std::string backend = "auto", devices, dtype = "bf16", sizes_s, json_path, backends_s = "rccl,xgmi",
+              dtypes_s = "bf16,fp8_e4m3";
+  bool bench = false, graph = false, registered = false, suite = false, fallback = false;
   int iters = 20, warmup = 5, ranks = 2;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -244,6 +442,10 @@ int commtest_main(int argc, char** argv) {
     else if (a == "--bench") bench = true;
     else if (a == "--graph") graph = true;
     else if (a == "--registered") registered = true;
+    else if (a == "--suite") suite = true;
+    else if (a == "--backends") backends_s = val("--backends");
+    else if (a == "--dtypes") dtypes_s = val("--dtypes");
+    else if (a == "--release-fallback") fallback = true;
     else if (a == "--iters") iters = std::stoi(val("--iters"));
     else if (a == "--warmup") warmup = std::stoi(val("--warmup"));
     else if (a == "--ranks") ranks = std::stoi(val("--ranks"));
@@ -254,13 +456,31 @@ int commtest_main(int argc, char** argv) {
                    "                     [--sizes n1,n2,..] [--bench] [--iters N] [--warmup N] [--graph]\n"
                    "  sizes are elements per rank; check mode verifies every collective exactly\n"
                    "  --graph: capture the operations into a HIP graph and replay it (rccl, xgmi)\n"
-                   "  --registered: peer-memory buffers registered with the communicator (zero-copy paths)\n";
+                   "  --registered: peer-memory buffers registered with the communicator (zero-copy paths)\n"
+                   "       dlnb commtest --suite [--backends rccl,xgmi] [--dtypes bf16,fp8_e4m3] [--sizes ..]\n"
+                   "                     [--release-fallback] [--json PATH]\n"
+                   "  exactness pass over every backend x mode (eager/graph, xgmi staged/registered) x dtype;\n"
+                   "  one JSON line with \"exact\": {backend: ok, ...}, the xgmi release mode and ncclCommCount\n";
       return 0;
     } else DLNB_THROW("unknown option " << a);
   }
   auto body = [&](std::unique_ptr<Bootstrap> boot) -> int {
   Context ctx;
   ctx.boot = std::move(boot);
+  if (suite) {
+    std::vector<std::string> bs, ds;
+    for (auto& x : split(backends_s, ',')) bs.push_back(trim(x));
+    for (auto& x : split(dtypes_s, ',')) ds.push_back(trim(x));
+    DLNB_REQUIRE(!bs.empty(), "commtest --suite: no backends");
+    std::vector<size_t> sz;
+    if (!sizes_s.empty())
+      for (auto& x : split(sizes_s, ',')) sz.push_back(static_cast<size_t>(std::stoull(x)));
+    select_backend(ctx, bs[0], devices);
+    const int rc = run_suite(ctx, bs, ds, sz, fallback, json_path);
+    ctx.hg().barrier();
+    ctx.hg().store().finish();
+    return rc;
+  }
   const std::string be = select_backend(ctx, backend, devices);
   DLNB_REQUIRE(!graph || be == "rccl" || be == "xgmi" || be == "mixed", "commtest --graph needs a GPU backend");
   const DType t = parse_dtype(dtype);
@@ -283,12 +503,15 @@ int commtest_main(int argc, char** argv) {
   auto link = ctx.comms->create("commtest/link", all, maxn * es, true);
   auto stream = ctx.dev->create_stream(true);
   Tester T{ctx, *comm, *stream, t, es, W, me};
+  T.inplace_a2a = comm->backend_name() == "XGMI";
   const bool reg = registered && comm->wants_peer_buffers();
+  std::vector<Buffer> pool;
   if (reg && !bench) {
     for (int i = 0; i < 9; ++i) {
-      T.pool.push_back(ctx.dev->alloc_peer(std::max<size_t>(16, maxn * W * es)));
-      comm->register_buffer(T.pool.back().data(), T.pool.back().bytes());
+      pool.push_back(ctx.dev->alloc_peer(std::max<size_t>(16, maxn * W * es)));
+      comm->register_buffer(pool.back().data(), pool.back().bytes());
     }
+    T.pool = &pool;
   }
   long long total_fail = 0;
   if (!bench) {

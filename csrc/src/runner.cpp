@@ -28,6 +28,7 @@ extern char** environ;
 #include "dlnb/aux.hpp"
 #include "dlnb/kernels.hpp"
 #include "dlnb/strategy.hpp"
+#include "dlnb/xgmi.hpp"
 
 namespace dlnb {
 
@@ -190,6 +191,47 @@ bool file_exists(const std::string& p) {
 
 }  // namespace
 
+namespace {
+
+// Wraps the backend's factory and logs every communicator it creates (name,
+// members, the library's own rank count) into ctx.comm_log for the report.
+class RecordingFactory : public CommFactory {
+ public:
+  RecordingFactory(std::unique_ptr<CommFactory> inner, std::vector<CommRecord>* log)
+      : inner_(std::move(inner)), log_(log) {}
+  std::string backend_name() const override { return inner_->backend_name(); }
+  std::unique_ptr<Communicator> create(const std::string& name, const std::vector<int>& members,
+                                       size_t capacity_bytes, bool need_p2p, int max_ctas) override {
+    auto c = inner_->create(name, members, capacity_bytes, need_p2p, max_ctas);
+    log_->push_back({name, c->backend_name(), c->size(), c->library_nranks()});
+    return c;
+  }
+
+ private:
+  std::unique_ptr<CommFactory> inner_;
+  std::vector<CommRecord>* log_;
+};
+
+}  // namespace
+
+Json comm_log_json(const std::vector<CommRecord>& log) {
+  Json out = Json::object();
+  Json all = Json::array();
+  Json rccl = Json::object();
+  for (const auto& r : log) {
+    Json e = Json::object();
+    e["name"] = r.name;
+    e["backend"] = r.backend;
+    e["nranks"] = r.nranks;
+    e["library_nranks"] = r.library_nranks;
+    all.push_back(e);
+    if (r.library_nranks >= 0) rccl[r.name] = r.library_nranks;
+  }
+  out["communicators"] = all;
+  out["rccl_nranks"] = rccl;
+  return out;
+}
+
 int collective_lanes(const Options& o, int world) {
   switch (o.strategy) {
     case StrategyKind::DP: return 1;
@@ -245,6 +287,7 @@ std::string select_backend(Context& ctx, const std::string& requested, const std
   } else {
     DLNB_THROW("unknown backend '" << backend << "' (auto, rccl, xgmi, mixed, cpu, loopback, loopback-cpu)");
   }
+  ctx.comms.reset(new RecordingFactory(std::move(ctx.comms), &ctx.comm_log));
   return backend;
 }
 
@@ -555,7 +598,20 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     b["max_ctas_per_lane"] = ctx.lane_ctas;  // 0 = RCCL default
     b["applies"] = rccl;
     b["fits"] = !rccl || !gemm_compute || ctx.lane_ctas == 0 ? true : lanes * ctx.lane_ctas <= opt.comm_cus;
+    if (backend == "xgmi" || backend == "mixed") {
+      // xgmi kernels: blocks per lane = blocks_per_cu x max_ctas, so a lane
+      // occupies max_ctas CUs at the measured occupancy
+      const int bpc = xgmi::min_blocks_per_cu();
+      b["xgmi_blocks_per_cu"] = bpc;
+      b["xgmi_blocks_per_lane"] = ctx.lane_ctas > 0 ? bpc * ctx.lane_ctas : 0;
+    }
     ext["rccl_cta_budget"] = b;
+  }
+  {
+    Json cl = comm_log_json(ctx.comm_log);
+    ext["communicators"] = cl.at("communicators");
+    ext["rccl_nranks"] = cl.at("rccl_nranks");
+    if (ctx.dev->kind() == DeviceKind::GPU) ext["runtime"] = runtime_info();
   }
   {
     // Collective-library knobs of this run (the reference recorded them as

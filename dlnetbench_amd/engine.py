@@ -8,9 +8,15 @@ reference's key names plus ``global["dlnb"]`` extras.
 """
 from __future__ import annotations
 
-from typing import Any, Dict, List
+import json
+import os
+import subprocess
+import tempfile
+from typing import Any, Dict, List, Optional
 
 from . import _native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 POSITIONAL = {
     "dp": ["num_buckets"],
@@ -59,3 +65,32 @@ def build_args(strategy: str, model: str, *params: int, base_path: str = ".", to
 
 def run(strategy: str, model: str, *params: int, **kw: Any) -> Dict[str, Any]:
     return _native.run_raw(strategy, build_args(strategy, model, *params, **kw))
+
+
+def run_native(strategy: str, model: str, *params: int, timeout: float = 600, env: Optional[Dict[str, str]] = None,
+               **kw: Any) -> Dict[str, Any]:
+    """Run one rank of a benchmark in a child process of the native binary
+    (build/bin/<strategy>) and return its report document.
+
+    The binary never imports torch, so it binds /opt/rocm's HIP runtime and
+    RCCL - the stack bench.py measures - even when this process has torch
+    (and with it torch's bundled HIP / RCCL) loaded. Raises NativeError with
+    the tail of the child's stderr if it fails."""
+    binary = os.path.join(ROOT, "build", "bin", strategy)
+    if not os.path.exists(binary):
+        raise _native.NativeError(f"{binary} is missing: build it with `make`")
+    fd, out = tempfile.mkstemp(prefix="dlnb_report_", suffix=".json")
+    os.close(fd)
+    try:
+        kw.setdefault("silent", True)
+        args = build_args(strategy, model, *params, json=out, **kw)
+        e = dict(os.environ, DLNB_NO_TORCH="1")
+        e.update(env or {})
+        p = subprocess.run([binary, *args], capture_output=True, text=True, timeout=timeout, env=e)
+        if p.returncode != 0:
+            raise _native.NativeError(f"{strategy} exited {p.returncode}: {(p.stderr or '')[-1500:]}")
+        with open(out) as f:
+            return json.load(f)
+    finally:
+        if os.path.exists(out):
+            os.remove(out)

@@ -16,7 +16,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DATA = os.path.join(ROOT, "tests", "data")
 TINY = ["--model", "tiny_dense_8_bfloat16", "--base-path", DATA, "--c5-model", "tiny_dense_8_bfloat16",
-        "--units", "4", "--c5-steps", "3"]
+        "--units", "4", "--c5-steps", "3", "--exact-sizes", "4097,30000"]
 
 
 def _free_port() -> int:
@@ -52,6 +52,39 @@ def test_bench_torchrun_cpu(n, tmp_path):
     assert c5["floor_ms"] == pytest.approx(6.0) and c5["ms_per_step"] >= c5["floor_ms"] * 0.9
     assert c5["exposed_comm_ms"] is not None
     assert o["rccl_cta_budget"]["lanes"] == 1
+    # the multi-rank exactness pass ran before the timed phases, on every rank
+    assert o["exact"] == {"cpu": True, "cpu_eager": True}, o.get("exact_detail")
+    d = o["exact_detail"]
+    assert d["ok"] and d["world_size"] == n and d["failed"] == [] and d["sizes"] == [4097, 30000]
+    assert d["rccl_nranks"] == -1 and o["rccl_nranks"] == {}  # no RCCL on the CPU backend
+
+
+def test_bench_hybrid_blocks_eight_ranks_cpu(tmp_path):
+    """The N = 8 driver path with the BASELINE C3 / C4 hybrid blocks (hybrid_3d
+    S=2 mb=4 T=4, hybrid_3d_moe S=2 mb=8 EP=4 on tiny models), 8 processes on
+    the shared-memory backend."""
+    n = 8
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(n), "--steps", "1", "--warmup", "0", "--backend", "cpu", "--compute", "sleep",
+           "--hybrids", "on", "--c3-model", "tiny_deep_8_bfloat16", "--c3", "2,4,4",
+           "--c4-model", "tiny_moe_8_bfloat16", "--c4", "2,8,4", "--exact", "off", "--c5-model", "none"] + TINY[:6]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=str(tmp_path),
+                       env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    o = lines[0]
+    h3, h4 = o["hybrid_3d"], o["hybrid_3d_moe"]
+    for h in (h3, h4):
+        assert "error" not in h, h
+        assert h["ms_per_step"] >= 0.9 * h["floor_ms"] > 0 and h["vs_floor"] > 0.9
+        assert h["pp_comm_time_ms"] is not None and h["dp_comm_time_ms"] is not None
+    assert h3["params"] == [2, 4, 4] and h3["tp_comm_time_ms"] is not None and h3["busbw_GBps"]["tp_allreduce"] > 0
+    assert h4["params"] == [2, 8, 4] and h4["ep_comm_time_ms"] is not None and h4["busbw_GBps"]["ep_alltoall"] > 0
+    # GPipe floor (mb + S - 1)(f_mb + b_mb): hybrid_3d f_mb = fwd / S / (mb T)
+    assert h3["floor_ms"] == pytest.approx((4 + 1) * (2.0 + 4.0) / 2 / (4 * 4), rel=1e-3)
+    assert h4["floor_ms"] == pytest.approx((8 + 1) * (2.0 + 4.0) / 2 / 8, rel=1e-3)
 
 
 def test_bench_single_rank_reports_no_bus_bandwidth(tmp_path):

@@ -268,3 +268,32 @@ def test_interleaved_shrinks_the_bubble_on_gpu(tmp_path):
         med[name] = (it["median_ms"], it["compute_floor_ms"])
     assert med["il"][0] < med["1f1b"][0], med
     assert med["il"][0] >= 0.98 * med["il"][1], med
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("release", ["vmcnt", "system"])
+def test_xgmi_exactness_suite_two_ranks_one_gpu(release):
+    """bench.py's multi-GPU exactness pass (commtest --suite) over the xgmi
+    kernels with 2 ranks sharing the GPU: staged, registered (zero-copy),
+    graph-replayed and registered + replayed, bf16 and fp8, 3 sizes, in both
+    release modes of the uncached windows."""
+    _need_gpu()
+    out = commtest(2, "--suite", "--backends", "xgmi", "-d", "0,0", "--dtypes", "bf16,fp8_e4m3",
+                   env_extra={"DLNB_XGMI_RELEASE": release, "DLNB_XGMI_TIMEOUT_S": "30"})
+    s = out[0]
+    assert s["commtest"] == "suite" and s["world_size"] == 2
+    assert s["ok"] and s["exact"]["xgmi"] is True and s["xgmi_release"] == release, s
+    for m in ("staged", "registered", "graph", "registered_graph"):
+        assert s["exact"]["xgmi_" + m] is True
+    assert len(s["results"]) == 8 and all(r["release"] == release for r in s["results"])
+    assert s["seconds"] < 60
+
+
+@pytest.mark.gpu
+def test_rccl_exactness_suite_single_rank():
+    """The suite's RCCL half at 1 rank (RCCL refuses 2 ranks on one GPU):
+    eager + graph, bf16 + fp8, and ncclCommCount reported."""
+    _need_gpu()
+    s = commtest(1, "--suite", "--backends", "rccl", "--dtypes", "bf16,fp8_e4m3")[0]
+    assert s["ok"] and s["exact"] == {"rccl": True, "rccl_eager": True, "rccl_graph": True}, s
+    assert s["rccl_nranks"] == 1 and s["runtime"]["librccl"].startswith("/opt/rocm")

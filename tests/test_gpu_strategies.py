@@ -1,4 +1,9 @@
-"""Every strategy end to end on one MI355X (RCCL, 1-rank groups, GEMM compute)."""
+"""Every strategy end to end on one MI355X (RCCL, 1-rank groups, GEMM compute).
+
+Each run is a child process of the native binary (engine.run_native), which
+never imports torch: it binds /opt/rocm's HIP runtime and RCCL, the stack
+bench.py measures, not the copies bundled with the torch this process loads
+(test_runs_bind_the_bench_runtime checks that)."""
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -28,7 +33,7 @@ CASES = [
 @pytest.mark.parametrize("strategy,model,params", CASES)
 @pytest.mark.parametrize("compute", ["gemm", "sleep"])
 def test_strategy_runs_on_gpu(strategy, model, params, compute, data_dir):
-    doc = engine.run(strategy, model, *params, base_path=data_dir, warmup=1, runs=2, compute=compute,
+    doc = engine.run_native(strategy, model, *params, base_path=data_dir, warmup=1, runs=2, compute=compute,
                      backend="rccl", quiet=True)
     g = doc["global"]
     assert g["backend"] == "RCCL" and g["device"] == "GPU"
@@ -46,7 +51,7 @@ def test_strategy_runs_on_gpu(strategy, model, params, compute, data_dir):
 
 def test_fsdp_llama3_8b_single_gpu_iteration(root):
     """The bench config at N=1 with time scaled down 20x (memory + collectives full size)."""
-    doc = engine.run("fsdp", "llama3_8b_16_bfloat16", 32, 1, base_path=root, warmup=1, runs=1,
+    doc = engine.run_native("fsdp", "llama3_8b_16_bfloat16", 32, 1, base_path=root, warmup=1, runs=1,
                      compute="gemm", backend="rccl", time_scale=0.05, quiet=True)
     it = doc["global"]["dlnb"]["iteration"]
     assert it["median_ms"] >= 0.9 * it["compute_floor_ms"]
@@ -67,7 +72,7 @@ def test_measured_stats_generator(tmp_path):
 @pytest.mark.parametrize("strategy,model,params", CASES)
 def test_strategy_hip_graph_replay(strategy, model, params, data_dir):
     """--graph: one captured iteration replayed per run, timings like eager enqueue."""
-    doc = engine.run(strategy, model, *params, base_path=data_dir, warmup=1, runs=3, compute="gemm",
+    doc = engine.run_native(strategy, model, *params, base_path=data_dir, warmup=1, runs=3, compute="gemm",
                      backend="rccl", quiet=True, graph=True)
     g = doc["global"]
     assert g["dlnb"]["graph"] > 0
@@ -82,7 +87,7 @@ def test_strategy_hip_graph_replay(strategy, model, params, data_dir):
 
 @pytest.mark.parametrize("zero", [1, 2])
 def test_dp_zero_on_gpu(zero, data_dir):
-    doc = engine.run("dp", "tiny_dense_8_bfloat16", 4, base_path=data_dir, warmup=1, runs=2, compute="gemm",
+    doc = engine.run_native("dp", "tiny_dense_8_bfloat16", 4, base_path=data_dir, warmup=1, runs=2, compute="gemm",
                      backend="rccl", quiet=True, zero=zero, graph=True)
     g = doc["global"]
     assert g["zero_stage"] == zero and g["dlnb"]["graph"] > 0
@@ -105,7 +110,7 @@ LOOPBACK_CASES = [
 
 
 def test_dualpipe_loopback_on_gpu(data_dir):
-    doc = engine.run("hybrid_2d", "tiny_deep_8_bfloat16", 4, 8, base_path=data_dir, warmup=1, runs=2,
+    doc = engine.run_native("hybrid_2d", "tiny_deep_8_bfloat16", 4, 8, base_path=data_dir, warmup=1, runs=2,
                      compute="gemm", backend="loopback", ranks=4, pp_schedule="dualpipe", quiet=True)
     g = doc["global"]
     assert g["pp_schedule"] == "dualpipe" and len(doc["ranks"]) == 4
@@ -113,7 +118,7 @@ def test_dualpipe_loopback_on_gpu(data_dir):
 
 
 def test_moe_expert_imbalance_loopback_on_gpu(data_dir):
-    doc = engine.run("hybrid_3d_moe", "tiny_moe_8_bfloat16", 1, 2, 4, base_path=data_dir, warmup=1, runs=2,
+    doc = engine.run_native("hybrid_3d_moe", "tiny_moe_8_bfloat16", 1, 2, 4, base_path=data_dir, warmup=1, runs=2,
                      compute="gemm", backend="loopback", ranks=4, ep_imbalance=1.0, quiet=True)
     per = doc["global"]["ep_dispatch_bytes_per_peer"]
     assert len(per) == 4 and per[0] > per[-1]
@@ -121,7 +126,7 @@ def test_moe_expert_imbalance_loopback_on_gpu(data_dir):
 
 @pytest.mark.parametrize("strategy,model,params,w", LOOPBACK_CASES)
 def test_strategy_loopback_on_gpu(strategy, model, params, w, data_dir):
-    doc = engine.run(strategy, model, *params, base_path=data_dir, warmup=1, runs=2, compute="gemm",
+    doc = engine.run_native(strategy, model, *params, base_path=data_dir, warmup=1, runs=2, compute="gemm",
                      backend="loopback", ranks=w, quiet=True)
     g = doc["global"]
     assert g["backend"] == "LOOPBACK" and g["device"] == "GPU" and g["world_size"] == w
@@ -146,7 +151,7 @@ def test_commtest_loopback_on_gpu(root):
 def test_fsdp_llama3_8b_loopback_8_ranks_one_gpu(root):
     """The bench config at W=8 as 8 rank threads on one MI355X: full-size FSDP
     collectives (per-rank shards of 1/8), compute time scaled down 50x."""
-    doc = engine.run("fsdp", "llama3_8b_16_bfloat16", 32, 8, base_path=root, warmup=1, runs=1,
+    doc = engine.run_native("fsdp", "llama3_8b_16_bfloat16", 32, 8, base_path=root, warmup=1, runs=1,
                      compute="gemm", backend="loopback", ranks=8, time_scale=0.02, quiet=True)
     g = doc["global"]
     assert g["world_size"] == 8 and g["sharding_factor"] == 8 and len(doc["ranks"]) == 8
@@ -159,7 +164,7 @@ def test_fsdp_llama3_8b_loopback_8_ranks_one_gpu(root):
 def test_compute_stretch_fixed_work(graph, data_dir):
     """gemm-work compute times every task on the device: measured / uncontended
     time is reported per rank and as the max over ranks (global.dlnb)."""
-    doc = engine.run("fsdp", "tiny_dense_8_bfloat16", 4, 1, base_path=data_dir, warmup=1, runs=3,
+    doc = engine.run_native("fsdp", "tiny_dense_8_bfloat16", 4, 1, base_path=data_dir, warmup=1, runs=3,
                      compute="gemm-work", backend="rccl", quiet=True, graph=graph or None)
     s = doc["global"]["dlnb"]["compute_stretch"]
     r = doc["ranks"][0]
@@ -169,21 +174,21 @@ def test_compute_stretch_fixed_work(graph, data_dir):
     # count reproduces the table time to within launch gaps
     assert 0.8 < s < 1.5, s
     # deadline compute lasts the table time by construction: nothing to report
-    doc = engine.run("fsdp", "tiny_dense_8_bfloat16", 4, 1, base_path=data_dir, warmup=1, runs=2,
+    doc = engine.run_native("fsdp", "tiny_dense_8_bfloat16", 4, 1, base_path=data_dir, warmup=1, runs=2,
                      compute="gemm", backend="rccl", quiet=True)
     assert "compute_stretch" not in doc["global"]["dlnb"]
 
 
 def test_rccl_cta_budget(data_dir):
-    doc = engine.run("dp", "tiny_dense_8_bfloat16", 4, base_path=data_dir, warmup=1, runs=2, compute="gemm",
+    doc = engine.run_native("dp", "tiny_dense_8_bfloat16", 4, base_path=data_dir, warmup=1, runs=2, compute="gemm",
                      backend="rccl", quiet=True)
     assert doc["global"]["dlnb"]["rccl_cta_budget"] == {"lanes": 1, "comm_cus": 32, "max_ctas_per_lane": 32,
                                                          "applies": True, "fits": True}
-    doc = engine.run("hybrid_cp", "tiny_dense_8_bfloat16", 1, base_path=data_dir, warmup=1, runs=2,
+    doc = engine.run_native("hybrid_cp", "tiny_dense_8_bfloat16", 1, base_path=data_dir, warmup=1, runs=2,
                      compute="gemm", backend="rccl", quiet=True, comm_cus=48)
     b = doc["global"]["dlnb"]["rccl_cta_budget"]
     assert b["lanes"] == 2 and b["max_ctas_per_lane"] == 24 and b["fits"]
-    doc = engine.run("dp", "tiny_dense_8_bfloat16", 4, base_path=data_dir, warmup=1, runs=2, compute="gemm",
+    doc = engine.run_native("dp", "tiny_dense_8_bfloat16", 4, base_path=data_dir, warmup=1, runs=2, compute="gemm",
                      backend="rccl", quiet=True, rccl_max_ctas=64)
     b = doc["global"]["dlnb"]["rccl_cta_budget"]
     assert b["max_ctas_per_lane"] == 64 and not b["fits"]
@@ -194,10 +199,60 @@ def test_dp_backward_buckets_chain_deadline(root):
     the comm-bound ViT-H step (bench.py's comm_bound block) lasts the table's
     compute plus the last bucket's exposed all-reduce and the iteration
     boundary, not plus ~10 us per bucket boundary (7.46 ms before, 7.29 after)."""
-    doc = engine.run("dp", "vit_h_32_float8", 8, base_path=root, warmup=3, runs=10, compute="gemm",
+    doc = engine.run_native("dp", "vit_h_32_float8", 8, base_path=root, warmup=3, runs=10, compute="gemm",
                      backend="rccl", graph=True, quiet=True)
     d = doc["global"]["dlnb"]
     it = d["iteration"]
     assert d["compute"]["chained_tasks"] >= 8
     floor = it["compute_floor_ms"]
     assert floor <= it["median_ms"] < floor + 0.3, (it["median_ms"], floor)
+
+
+def test_runs_bind_the_bench_runtime(data_dir, root, tmp_path):
+    """The strategy runs above and bench.py report the same HIP / RCCL build:
+    /opt/rocm's (the banner bench.py's driver records), not torch's bundled one."""
+    import json
+    import os
+    import subprocess
+    import sys
+    doc = engine.run_native("fsdp", "tiny_dense_8_bfloat16", 4, 1, base_path=data_dir, warmup=1, runs=1,
+                            compute="gemm", backend="rccl", quiet=True)
+    rt = doc["global"]["dlnb"]["runtime"]
+    assert rt["librccl"].startswith("/opt/rocm"), rt
+    assert rt["libamdhip64"].startswith("/opt/rocm"), rt
+    nr = doc["global"]["dlnb"]["rccl_nranks"]
+    assert nr and all(v == 1 for v in nr.values()), nr  # ncclCommCount of every 1-rank group
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "1", "--warmup", "0",
+                        "--model", "tiny_dense_8_bfloat16", "--base-path", data_dir, "--units", "4",
+                        "--c5-model", "none", "--stretch-steps", "0"],
+                       capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    o = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert o["runtime"]["rccl_version"] == rt["rccl_version"]
+    assert o["runtime"]["librccl"] == rt["librccl"] and o["runtime"]["hip_runtime_version"] == rt["hip_runtime_version"]
+    info = json.loads(subprocess.run([os.path.join(root, "build", "bin", "dlnb"), "info"], capture_output=True,
+                                     text=True, timeout=60, check=True).stdout)
+    assert info["runtime"]["rccl_version"] == rt["rccl_version"]
+
+
+def test_xgmi_kernel_occupancy_fits_the_cu_budget(root):
+    """Measured occupancy of every xgmi kernel and dtype (hipOccupancy...):
+    at least 4 blocks of 512 threads per CU, so a comm lane of blocks_per_cu x
+    max_ctas blocks needs at most max_ctas CUs, and 1 or 3 live lanes fit the
+    32 CUs the deadline GEMM leaves free."""
+    import json
+    import math
+    import os
+    import subprocess
+    info = json.loads(subprocess.run([os.path.join(root, "build", "bin", "dlnb"), "info"], capture_output=True,
+                                     text=True, timeout=60, check=True).stdout)
+    occ = info["xgmi_occupancy_blocks_per_cu"]
+    assert len(occ) == 31, occ
+    bpc = info["xgmi_min_blocks_per_cu"]
+    assert bpc == 4 and min(occ.values()) >= 4, occ
+    comm_cus = 32
+    for lanes in (1, 3):
+        max_ctas = comm_cus // lanes
+        blocks = bpc * max_ctas
+        for name, b in occ.items():
+            assert lanes * math.ceil(blocks / b) <= comm_cus, (name, lanes, b)

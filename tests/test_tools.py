@@ -290,3 +290,17 @@ def test_prof_merge_folds_counters_into_report(tmp_path):
     assert cl["compute_gemm"]["fabric_GBps"] == pytest.approx(5000.0, rel=1e-3)
     assert c["total_kernel_ms"] == pytest.approx(4.0 + 0.6 + 0.001 + 0.05)
     assert sum(v["time_pct"] for v in cl.values()) == pytest.approx(100.0, abs=0.05)
+
+
+def test_xgmi_kernels_fit_the_cu_budget(root):
+    """Every peer-waiting xgmi kernel fits 4 blocks of 512 threads per CU on
+    registers (<= 64 per lane, no scratch), which the comm-lane CU budget
+    (comm_xgmi.cpp, runner.cpp) assumes; read from the gfx950 code object."""
+    from dlnetbench_amd.tools.kernel_resources import kernel_resources
+    ks = kernel_resources(os.path.join(root, "csrc", "kernels", "xgmi.hip"))
+    peer = [k for k in ks if "local_" not in k["name"]]
+    assert len(peer) == 31, [k["name"] for k in peer]
+    for k in peer:
+        assert k["max_threads"] == 512, k
+        assert k["waves_per_simd"] == 8 and k["blocks_per_cu_regs"] >= 4, k
+        assert k["scratch"] == 0, k
