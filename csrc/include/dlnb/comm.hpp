@@ -111,6 +111,14 @@ struct LoopbackHub;
 std::shared_ptr<LoopbackHub> make_loopback_hub(int ranks, double timeout_s);
 // Wakes every rank blocked in the hub with an error (a rank thread failed).
 void loopback_abort(LoopbackHub& hub, const std::string& why);
+// The job's CPU abort switch (loopback-cpu devices are created with it;
+// loopback_abort sets it).
+AbortFlag loopback_cpu_abort_flag(LoopbackHub& hub);
+// A rank thread is done with the job: its streams are drained, nothing of it
+// is still queued. With `wait`, also blocks (up to timeout_s) until every
+// rank of the job is: a failing rank frees its buffers and events only once
+// no other rank's queued copy or event wait can still reference them.
+void loopback_drained(LoopbackHub& hub, bool wait, double timeout_s);
 std::unique_ptr<CommFactory> make_loopback_factory(HostGroup& world, Device& dev, std::shared_ptr<LoopbackHub> hub);
 
 // Host-memory helpers of the CPU backends (multi-threaded for large sizes).

@@ -16,6 +16,7 @@
 #include <cstdint>
 #include <deque>
 #include <functional>
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -127,10 +128,18 @@ class Device {
 
 // ---- CPU implementation (also used by the GPU-less tests) ----
 
+// Abort switch of one job (loopback-cpu: its LoopbackHub owns it): when set,
+// CPU-stream event waits give up and queued CPU-stream tasks are dropped, so
+// worker threads blocked on a failed rank's events drain and every rank
+// thread can unwind. Scoped to the job's device, so another job in the same
+// process (or a later --backend cpu run) is never affected.
+using AbortFlag = std::shared_ptr<std::atomic<bool>>;
+
 // Generation-counted event with HIP semantics: a wait() captures the most
 // recent record() at enqueue time and blocks until that record completes.
 class CpuEvent : public Event {
  public:
+  explicit CpuEvent(AbortFlag abort = nullptr) : abort_(std::move(abort)) {}
   uint64_t mark_recorded();           // host, at enqueue time
   void complete(uint64_t gen);        // worker, when reached
   uint64_t recorded() ;
@@ -138,6 +147,7 @@ class CpuEvent : public Event {
   double time_s();
 
  private:
+  AbortFlag abort_;
   std::mutex mu_;
   std::condition_variable cv_;
   uint64_t recorded_ = 0;
@@ -145,9 +155,12 @@ class CpuEvent : public Event {
   double t_ = 0;
 };
 
+// Live streams of one CPU device (Device::synchronize drains them all).
+struct CpuStreamRegistry;
+
 class CpuStream : public Stream {
  public:
-  CpuStream();
+  explicit CpuStream(AbortFlag abort = nullptr, std::shared_ptr<CpuStreamRegistry> reg = nullptr);
   ~CpuStream() override;
   void record(Event& e) override;
   void wait(Event& e) override;
@@ -158,6 +171,8 @@ class CpuStream : public Stream {
 
  private:
   void run();
+  AbortFlag abort_;
+  std::shared_ptr<CpuStreamRegistry> reg_;
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<std::function<void()>> q_;
@@ -167,12 +182,8 @@ class CpuStream : public Stream {
   std::thread th_;
 };
 
-std::unique_ptr<Device> make_cpu_device();
-// Process-wide: when on, CPU-stream event waits give up and queued CPU-stream
-// tasks are dropped, so worker threads blocked on a failed loopback rank's
-// events drain and every rank thread can unwind (loopback_abort sets it;
-// a new loopback job clears it).
-void abort_cpu_waits(bool on);
+// CPU device; its streams and events observe `abort` (may be null).
+std::unique_ptr<Device> make_cpu_device(AbortFlag abort = nullptr);
 
 // GPU device (HIP). local_index picks the visible device.
 std::unique_ptr<Device> make_gpu_device(int local_index);

@@ -24,6 +24,7 @@
 // group_start()/group_end() are posted without blocking and completed
 // together at group_end(), which is how the strategies issue paired
 // send/recv exchanges.
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -98,6 +99,8 @@ struct LoopbackHub {
   bool aborted = false;
   std::string why;
   std::map<std::string, std::weak_ptr<Group>> groups;
+  AbortFlag cpu_abort = std::make_shared<std::atomic<bool>>(false);
+  int drained = 0;  // rank threads done with the job (loopback_drained)
 
   // Waits (mu held) until pred() holds; throws on abort or timeout.
   template <typename Pred>
@@ -123,8 +126,18 @@ std::shared_ptr<LoopbackHub> make_loopback_hub(int ranks, double timeout_s) {
   return h;
 }
 
+AbortFlag loopback_cpu_abort_flag(LoopbackHub& hub) { return hub.cpu_abort; }
+
+void loopback_drained(LoopbackHub& hub, bool wait, double timeout_s) {
+  std::unique_lock<std::mutex> g(hub.mu);
+  ++hub.drained;
+  hub.cv.notify_all();
+  if (wait)
+    hub.cv.wait_for(g, std::chrono::duration<double>(timeout_s), [&] { return hub.drained >= hub.ranks; });
+}
+
 void loopback_abort(LoopbackHub& hub, const std::string& why) {
-  abort_cpu_waits(true);  // loopback-cpu: release worker threads blocked on the failed rank's events
+  hub.cpu_abort->store(true);  // loopback-cpu: release worker threads blocked on the failed rank's events
   std::lock_guard<std::mutex> g(hub.mu);
   if (!hub.aborted) {
     hub.aborted = true;

@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <set>
 
 #include "dlnb/device.hpp"
 
@@ -80,16 +81,10 @@ void CpuEvent::complete(uint64_t gen) {
   cv_.notify_all();
 }
 
-namespace {
-std::atomic<bool> g_abort_waits{false};
-}
-
-void abort_cpu_waits(bool on) { g_abort_waits.store(on); }
-
 void CpuEvent::wait_for(uint64_t gen) {
   std::unique_lock<std::mutex> g(mu_);
   while (!cv_.wait_for(g, std::chrono::milliseconds(20), [&] { return completed_ >= gen; }))
-    if (g_abort_waits.load()) return;
+    if (abort_ && abort_->load()) return;
 }
 
 double CpuEvent::time_s() {
@@ -100,9 +95,24 @@ double CpuEvent::time_s() {
 
 // --------------------------------------------------------------- CpuStream
 
-CpuStream::CpuStream() : th_([this] { run(); }) {}
+struct CpuStreamRegistry {
+  std::mutex mu;
+  std::set<CpuStream*> live;
+};
+
+CpuStream::CpuStream(AbortFlag abort, std::shared_ptr<CpuStreamRegistry> reg)
+    : abort_(std::move(abort)), reg_(std::move(reg)), th_([this] { run(); }) {
+  if (reg_) {
+    std::lock_guard<std::mutex> g(reg_->mu);
+    reg_->live.insert(this);
+  }
+}
 
 CpuStream::~CpuStream() {
+  if (reg_) {
+    std::lock_guard<std::mutex> g(reg_->mu);
+    reg_->live.erase(this);
+  }
   {
     std::lock_guard<std::mutex> g(mu_);
     stop_ = true;
@@ -131,7 +141,7 @@ void CpuStream::run() {
       q_.pop_front();
     }
     try {
-      if (!g_abort_waits.load()) fn();
+      if (!abort_ || !abort_->load()) fn();
     } catch (const std::exception& e) {
       // A failed task would leave peers and other streams waiting forever:
       // fail the whole rank loudly (the launcher tears the job down).
@@ -183,11 +193,12 @@ namespace {
 
 class CpuDevice : public Device {
  public:
+  explicit CpuDevice(AbortFlag abort) : abort_(std::move(abort)), reg_(std::make_shared<CpuStreamRegistry>()) {}
   DeviceKind kind() const override { return DeviceKind::CPU; }
   std::string name() const override { return "CPU"; }
   int index() const override { return 0; }
-  std::unique_ptr<Stream> create_stream(bool) override { return std::unique_ptr<Stream>(new CpuStream()); }
-  std::unique_ptr<Event> create_event(bool) override { return std::unique_ptr<Event>(new CpuEvent()); }
+  std::unique_ptr<Stream> create_stream(bool) override { return std::unique_ptr<Stream>(new CpuStream(abort_, reg_)); }
+  std::unique_ptr<Event> create_event(bool) override { return std::unique_ptr<Event>(new CpuEvent(abort_)); }
   double elapsed_ms(Event& a, Event& b) override {
     auto* ea = dynamic_cast<CpuEvent*>(&a);
     auto* eb = dynamic_cast<CpuEvent*>(&b);
@@ -227,7 +238,11 @@ class CpuDevice : public Device {
     dynamic_cast<CpuStream&>(s).enqueue([dst, src, bytes] { std::memcpy(dst, src, bytes); });
   }
   void host_task(Stream& s, std::function<void()> fn) override { dynamic_cast<CpuStream&>(s).enqueue(std::move(fn)); }
-  void synchronize() override {}
+  // Like hipDeviceSynchronize: every live stream of this device drained.
+  void synchronize() override {
+    std::lock_guard<std::mutex> g(reg_->mu);
+    for (CpuStream* s : reg_->live) s->synchronize();
+  }
   uint64_t* alloc_stamps(size_t n) override { return static_cast<uint64_t*>(std::calloc(n, sizeof(uint64_t))); }
   void free_stamps(uint64_t* p, size_t) override { std::free(p); }
   void stamp(Stream& s, uint64_t* slot) override {
@@ -236,11 +251,15 @@ class CpuDevice : public Device {
   double stamp_hz() const override { return 1e9; }
   size_t total_memory() const override { return static_cast<size_t>(sysconf(_SC_PHYS_PAGES)) * sysconf(_SC_PAGE_SIZE); }
   size_t free_memory() const override { return static_cast<size_t>(sysconf(_SC_AVPHYS_PAGES)) * sysconf(_SC_PAGE_SIZE); }
+
+ private:
+  AbortFlag abort_;
+  std::shared_ptr<CpuStreamRegistry> reg_;
 };
 
 }  // namespace
 
-std::unique_ptr<Device> make_cpu_device() { return std::unique_ptr<Device>(new CpuDevice()); }
+std::unique_ptr<Device> make_cpu_device(AbortFlag abort) { return std::unique_ptr<Device>(new CpuDevice(std::move(abort))); }
 
 std::unique_ptr<GraphExec> Device::capture(Stream&, const std::vector<Stream*>&, const std::function<void()>&) {
   DLNB_THROW("--graph needs a GPU device (HIP graphs)");

@@ -9,6 +9,7 @@
 // divides a world-sum by the warm-up count, cpp/utils.hpp:127-128) and takes
 // the max over ranks; loop mode is a run-time flag (or a *_loop argv[0]).
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -271,7 +272,7 @@ std::string select_backend(Context& ctx, const std::string& requested, const std
     DLNB_REQUIRE(ctx.boot->hub, "--backend " << backend << " runs inside one process (run_benchmark starts the rank threads)");
     if (backend == "loopback-cpu") {
       // CPU device only: no HIP call at all (GPU-less hosts and CPU tests)
-      ctx.dev = make_cpu_device();
+      ctx.dev = make_cpu_device(loopback_cpu_abort_flag(*ctx.boot->hub));
     } else {
       // Every rank on the same GPU: the one given by -d (default 0).
       const int ngpu = gpu_device_count();
@@ -295,62 +296,84 @@ namespace {
 
 Json run_rank(const Options& opt, std::unique_ptr<Bootstrap> boot);
 
+// Set by main_for: this process is a CLI binary, not a library host (Python).
+std::atomic<bool> g_cli_process{false};
+
+// State of one loopback job, shared by its rank threads (heap-held so a rank
+// thread that outlives run_loopback - detached after a failure - never
+// touches a dead stack frame).
+struct LoopbackJob {
+  Options opt;
+  std::shared_ptr<LocalStore> store;
+  std::shared_ptr<LoopbackHub> hub;
+  std::vector<Json> docs;
+  std::mutex mu;
+  std::condition_variable done_cv;
+  int done = 0;
+  std::string first_error;
+};
+
 // --backend loopback / loopback-cpu: the job's ranks are threads of this process sharing one
 // LocalStore (host barriers / gathers) and one LoopbackHub (collectives). A
-// failing rank aborts both, so the others leave their waits instead of
-// hanging; the first failure is rethrown.
+// failing rank aborts both (and the job's CPU abort switch), so the others
+// leave their waits instead of hanging; the first failure is rethrown.
 Json run_loopback(const Options& opt) {
   const int n = opt.ranks;
   DLNB_REQUIRE(n >= 1, "--ranks must be >= 1");
   DLNB_REQUIRE(env_int("WORLD_SIZE", 1) == 1 && env_int("DLNB_WORLD_SIZE", 1) == 1,
                "--backend loopback runs all ranks inside one process: launch it once, not under a multi-rank launcher");
-  auto store = std::make_shared<LocalStore>();
-  auto hub = make_loopback_hub(n, static_cast<double>(env_int("DLNB_STORE_TIMEOUT", 900)));
-  abort_cpu_waits(false);
-  std::vector<Json> docs(static_cast<size_t>(n));
-  std::mutex mu;
-  std::condition_variable done_cv;
-  int done = 0;
-  std::string first_error;
+  auto job = std::make_shared<LoopbackJob>();
+  job->opt = opt;
+  job->store = std::make_shared<LocalStore>();
+  job->hub = make_loopback_hub(n, static_cast<double>(env_int("DLNB_STORE_TIMEOUT", 900)));
+  job->docs.resize(static_cast<size_t>(n));
   std::vector<std::thread> threads;
   for (int r = 0; r < n; ++r) {
-    threads.emplace_back([&, r] {
+    threads.emplace_back([job, r, n] {
       try {
-        docs[static_cast<size_t>(r)] = run_rank(opt, bootstrap_loopback(r, n, store, hub));
+        Json d = run_rank(job->opt, bootstrap_loopback(r, n, job->store, job->hub));
+        loopback_drained(*job->hub, false, 0);
+        std::lock_guard<std::mutex> g(job->mu);
+        job->docs[static_cast<size_t>(r)] = std::move(d);
       } catch (const std::exception& e) {
         const std::string msg = "rank " + std::to_string(r) + ": " + e.what();
         {
-          std::lock_guard<std::mutex> g(mu);
-          if (first_error.empty()) first_error = msg;
+          std::lock_guard<std::mutex> g(job->mu);
+          if (job->first_error.empty()) job->first_error = msg;
         }
-        loopback_abort(*hub, msg);
-        store->abort(msg);
+        loopback_abort(*job->hub, msg);
+        job->store->abort(msg);
       }
-      std::lock_guard<std::mutex> g(mu);
-      ++done;
-      done_cv.notify_all();
+      std::lock_guard<std::mutex> g(job->mu);
+      ++job->done;
+      job->done_cv.notify_all();
     });
   }
-  {
-    // After the first failure the other rank threads get a bounded grace
-    // period to leave their waits and tear down; a thread still blocked then
-    // (a wait that missed the abort under heavy host load: seen ~1 in 25
-    // runs with 12 jobs on 8 CPUs) must not hold the job forever, so the
-    // process ends with the rank's error, as a multi-process job would.
-    const double grace_s = static_cast<double>(env_int("DLNB_LOOPBACK_ABORT_GRACE_S", 10));
-    std::unique_lock<std::mutex> g(mu);
-    done_cv.wait(g, [&] { return done == n || !first_error.empty(); });
-    if (done < n &&
-        !done_cv.wait_for(g, std::chrono::duration<double>(grace_s), [&] { return done == n; })) {
-      std::fprintf(stderr, "[dlnb] error: %s\n[dlnb] %d of %d rank threads still blocked %.0f s after the failure; exiting\n",
-                   first_error.c_str(), n - done, n, grace_s);
-      std::fflush(stderr);
-      std::_Exit(2);
-    }
+  // After the first failure the other rank threads get a bounded grace
+  // period to leave their waits and tear down. A thread still blocked then
+  // must not hold the job forever: the CLI process ends with the rank's
+  // error (as a multi-process job would); a library host (Python) gets the
+  // error as an exception, with the stuck threads detached (they only hold
+  // the job's heap state).
+  const double grace_s = static_cast<double>(env_int("DLNB_LOOPBACK_ABORT_GRACE_S", 10));
+  std::unique_lock<std::mutex> g(job->mu);
+  job->done_cv.wait(g, [&] { return job->done == n || !job->first_error.empty(); });
+  if (job->done < n &&
+      !job->done_cv.wait_for(g, std::chrono::duration<double>(grace_s), [&] { return job->done == n; })) {
+    const int stuck = n - job->done;
+    const std::string err = job->first_error;
+    g.unlock();
+    std::fprintf(stderr, "[dlnb] error: %s\n[dlnb] %d of %d rank threads still blocked %.0f s after the failure\n",
+                 err.c_str(), stuck, n, grace_s);
+    std::fflush(stderr);
+    if (g_cli_process.load()) std::_Exit(2);
+    for (auto& t : threads) t.detach();
+    throw Error(err + " (" + std::to_string(stuck) + " rank threads still blocked were detached)");
   }
+  g.unlock();
   for (auto& t : threads) t.join();
-  if (!first_error.empty()) throw Error(first_error);
-  return docs[0];
+  if (!job->first_error.empty()) throw Error(job->first_error);
+  return job->docs[0];
 }
 
 }  // namespace
@@ -379,6 +402,14 @@ Json run_rank(const Options& opt, std::unique_ptr<Bootstrap> boot) {
       const std::string msg = "rank " + std::to_string(ctx.boot->info.rank) + ": " + e.what();
       loopback_abort(*ctx.boot->hub, msg);
       if (auto* ls = dynamic_cast<LocalStore*>(ctx.boot->store.get())) ls->abort(msg);
+      // The other ranks' streams may still hold copies into this rank's
+      // buffers or waits on its events: drain this rank's work, then free
+      // nothing (ctx / strat destructors) until every rank has drained too.
+      try {
+        if (ctx.dev) ctx.dev->synchronize();
+      } catch (const std::exception&) {
+      }
+      loopback_drained(*ctx.boot->hub, true, static_cast<double>(env_int("DLNB_LOOPBACK_ABORT_GRACE_S", 10)));
     }
     throw;
   }
@@ -698,6 +729,7 @@ int main_for(StrategyKind kind, int argc, char** argv) {
     return 0;
   }
   if (ends_with(prog, "_loop")) opt.loop = true;
+  g_cli_process.store(true);
   try {
     run_benchmark(opt);
   } catch (const std::exception& e) {

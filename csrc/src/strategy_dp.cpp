@@ -60,6 +60,12 @@ class DataParallel : public Strategy {
     size_t need = static_cast<size_t>(P_) * es_ * 2;
     in_place_ = o.in_place || (dev.kind() == DeviceKind::GPU && need > dev.free_memory() * 0.85);
     if (zero_ == 2) in_place_ = false;  // the reduce-scatter writes a separate shard
+    // Every rank must take the same decision: it sets how many buffers each
+    // registers with the communicator (xgmi pairs the k-th registration of
+    // every member) and which buffers the collectives read and write. Free
+    // memory differs between ranks (several ranks on one GPU, or near the
+    // threshold), so agree: in place if any rank needs it.
+    in_place_ = ctx.hg().allreduce_max(in_place_ ? 1.0 : 0.0) > 0.5;
     // Zero-copy (xgmi): gradient buckets and all-reduce outputs in peer
     // memory, registered with the communicator, so the collectives read and
     // write peers' buffers directly (see Communicator::register_buffer).

@@ -156,3 +156,47 @@ def test_loopback_refuses_a_multi_process_launch(data_dir):
                         "--ranks", "2", "--quiet"], capture_output=True, text=True, timeout=60,
                        env=_env({"WORLD_SIZE": "2", "RANK": "0"}), cwd=ROOT)
     assert p.returncode == 2 and "one process" in p.stderr
+
+
+_LIBRARY_FAILURE = r"""
+import json, os, sys, time
+sys.path.insert(0, {root!r})
+os.environ["DLNB_NO_TORCH"] = "1"
+from dlnetbench_amd import engine, _native
+data = {data!r}
+os.environ["DLNB_INJECT_FAULT"] = "rank=1,iter=1,mode={mode}"
+t0 = time.time()
+try:
+    engine.run("dp", "tiny_dense_8_bfloat16", 2, base_path=data, backend="loopback-cpu", ranks=3, warmup=1, runs=2,
+               compute="sleep", silent=True)
+    print("NO ERROR")
+except _native.NativeError as e:
+    print("RAISED", time.time() - t0, str(e)[:200])
+del os.environ["DLNB_INJECT_FAULT"]
+# the failed job's abort switch is its own: later runs in this process are unaffected
+d = engine.run("dp", "tiny_dense_8_bfloat16", 2, base_path=data, backend="loopback-cpu", ranks=3, warmup=1, runs=2,
+               compute="sleep", silent=True)
+print(json.dumps({{"ok": d["global"]["dlnb"]["iteration"]["median_ms"]}}))
+d = engine.run("dp", "tiny_dense_8_bfloat16", 2, base_path=data, backend="cpu", warmup=1, runs=2, compute="sleep",
+               silent=True)
+print(json.dumps({{"cpu": d["global"]["dlnb"]["iteration"]["median_ms"]}}))
+"""
+
+
+@pytest.mark.parametrize("mode", ["throw", "hang"])
+def test_loopback_failure_in_library_mode_raises(mode, data_dir, root):
+    """In-process (Python / ctypes) loopback jobs: a failing rank raises
+    NativeError instead of ending the interpreter; a rank thread that never
+    leaves its wait (injected hang) is detached after the grace period; the
+    job-scoped CPU abort switch leaves later runs in the process intact."""
+    env = dict(os.environ, DLNB_STORE_TIMEOUT="3", DLNB_LOOPBACK_ABORT_GRACE_S="1")
+    p = subprocess.run([sys.executable, "-c", _LIBRARY_FAILURE.format(root=root, data=data_dir, mode=mode)],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    lines = p.stdout.splitlines()
+    assert lines[0].startswith("RAISED"), p.stdout
+    if mode == "hang":
+        assert "detached" in lines[0] and float(lines[0].split()[1]) < 30
+    ok = json.loads(lines[1])["ok"]
+    cpu = json.loads(lines[2])["cpu"]
+    assert ok >= 0.9 * 6.0 and cpu >= 0.9 * 6.0  # tiny model: 6 ms of compute per iteration, nothing dropped
