@@ -309,6 +309,9 @@ def main() -> int:
     ap.add_argument("--c5-buckets", type=int, default=8)
     ap.add_argument("--c5-steps", type=int, default=50)
     ap.add_argument("--c5-wire", default="bf16", help="wire dtype of the comm-bound all-reduce")
+    ap.add_argument("--c5-bucket-ratio", type=float, default=0.7,
+                    help="comm_bound.geometric_buckets: the same step with geometric bucket sizes (share r^i per "
+                         "bucket, a small last all-reduce); 0 skips it")
     ap.add_argument("--no-c5-ctas-ab", dest="c5_ctas_ab", action="store_false",
                     help="skip the comm-bound rerun with RCCL's default CTA count")
     ap.add_argument("--stretch-steps", type=int, default=2,
@@ -423,6 +426,20 @@ def main() -> int:
                                                "allreduce_algbw_GBps": _algbw(d, "allreduce")}
                 except Exception as e:  # noqa: BLE001
                     c5["rccl_default_ctas"] = {"error": str(e)[:300]}
+            if 0 < a.c5_bucket_ratio < 1 and "error" not in c5:
+                # opt-in policy: shrink the exposed tail (the last bucket's
+                # all-reduce runs after the backward ends)
+                try:
+                    d = run(".c5g", "dp", a.c5_model, a.c5_buckets, graph=use_graph, warmup=5, runs=a.c5_steps,
+                            compute=a.compute, wire_dtype=a.c5_wire, dp_bucket_ratio=a.c5_bucket_ratio)
+                    it = d["global"]["dlnb"]["iteration"]
+                    c5["geometric_buckets"] = {"bucket_ratio": a.c5_bucket_ratio,
+                                               "ms_per_step": round(it["timed_ms_per_iter"], 4),
+                                               "median_ms": round(it["median_ms"], 4),
+                                               "exposed_comm_ms": _mean_of(d, "barrier_time"),
+                                               "allreduce_busbw_GBps": _busbw(d, "allreduce", world)}
+                except Exception as e:  # noqa: BLE001
+                    c5["geometric_buckets"] = {"error": str(e)[:300]}
             if a.stretch_steps > 0 and on_gpu:
                 try:
                     d = run(".c5w", "dp", a.c5_model, a.c5_buckets, graph=use_graph, warmup=5, runs=a.c5_steps,

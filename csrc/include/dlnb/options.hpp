@@ -59,6 +59,7 @@ struct Options {
   int pp_virtual = 2;                         // interleaved: model chunks (virtual stages) per stage
   bool ep_overlap = false;  // moe: overlap each half-microbatch's all-to-all with the other half's compute
   double ep_imbalance = 0;  // moe: Zipf exponent of the expert-rank load (0 = uniform all-to-all)
+  double dp_bucket_ratio = 1.0;  // dp: geometric bucket sizes (strategy_dp.cpp dp_bucket_sizes)
   int dp_buckets = 1;  // hybrids: DP all-reduce buckets overlapped with the last backward
   bool in_place = false;
   // dp: ZeRO stage. 0 = replicated (reference), 1 = optimizer state sharded

@@ -91,6 +91,9 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "                         every dispatch (all-to-allv over grouped send/recv); 0 = uniform (reference)\n"
      << "  --dp-buckets K         hybrids: DP all-reduce buckets overlapped with the last backward\n"
      << "                         (hybrid_cp: gradient buckets by layer, overlapped with the backward)\n"
+     << "  --dp-bucket-ratio R    dp: bucket i (backward order) holds a share R^i of the parameters, its\n"
+     << "                         backward compute the same share (1 = the reference's P/nb; < 1 shrinks\n"
+     << "                         the tail so the last, exposed all-reduce is small)\n"
      << "  --cp-algo ring|ulysses hybrid_cp: KV blocks around a P2P ring, or all-to-alls over heads\n"
      << "  --in-place             in-place all-reduce (halves DP buffer memory)\n"
      << "  --zero 0|1|2           dp: ZeRO stage (1: sharded optimizer + parameter all-gather, 2: + gradient\n"
@@ -172,6 +175,9 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
       o.cp_algo = val("cp-algo");
     } else if (is("--dp-buckets")) {
       o.dp_buckets = to_int(val("dp-buckets"), "dp-buckets");
+    } else if (is("--dp-bucket-ratio")) {
+      o.dp_bucket_ratio = to_double(val("dp-bucket-ratio"), "dp-bucket-ratio");
+      if (!(o.dp_bucket_ratio > 0 && o.dp_bucket_ratio <= 1)) DLNB_THROW("--dp-bucket-ratio must be in (0, 1]");
     } else if (a == "--in-place") {
       o.in_place = true;
     } else if (is("--zero")) {

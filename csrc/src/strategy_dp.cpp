@@ -28,6 +28,36 @@
 
 namespace dlnb {
 
+// Bucket sizes of a dp run: ratio 1 is the reference's partition (P/nb, the
+// first P%nb buckets one larger, dp.cpp:159-164); ratio r < 1 gives bucket i
+// (backward order) the share r^i / sum_j r^j, floored, the rounding rest
+// going to bucket 0. The weights are built by repeated multiplication and
+// summed in order so dlnetbench_amd/parallel/plan.py dp_bucket_sizes()
+// reproduces them bit for bit.
+std::vector<uint64_t> dp_bucket_sizes(uint64_t P, int nb, double ratio) {
+  std::vector<uint64_t> s;
+  if (ratio >= 1.0) {
+    const uint64_t base = P / nb, rem = P % nb;
+    for (int i = 0; i < nb; ++i) s.push_back(base + (static_cast<uint64_t>(i) < rem ? 1 : 0));
+    return s;
+  }
+  std::vector<double> w(static_cast<size_t>(nb));
+  double x = 1.0, tot = 0.0;
+  for (int i = 0; i < nb; ++i) {
+    w[static_cast<size_t>(i)] = x;
+    x *= ratio;
+  }
+  for (double v : w) tot += v;
+  uint64_t sum = 0;
+  for (double v : w) {
+    s.push_back(static_cast<uint64_t>(std::floor(static_cast<double>(P) * v / tot)));
+    sum += s.back();
+  }
+  s[0] += P - sum;
+  for (uint64_t v : s) DLNB_REQUIRE(v > 0, "--dp-bucket-ratio " << ratio << " leaves an empty bucket of " << nb);
+  return s;
+}
+
 namespace {
 
 class DataParallel : public Strategy {
@@ -39,10 +69,14 @@ class DataParallel : public Strategy {
     nb_ = o.num_buckets;
     P_ = st.model_size;
     DLNB_REQUIRE(P_ >= static_cast<uint64_t>(nb_), "num_buckets (" << nb_ << ") exceeds the parameter count");
-    uint64_t base = P_ / nb_, rem = P_ % nb_;
-    for (int i = 0; i < nb_; ++i) sizes_.push_back(base + (static_cast<uint64_t>(i) < rem ? 1 : 0));
+    ratio_ = o.dp_bucket_ratio;
+    sizes_ = dp_bucket_sizes(P_, nb_, ratio_);
     fwd_us_ = st.avg_forward_time_us;
     bwd_us_per_bucket_ = st.avg_backward_time_us / nb_;
+    // backward compute of bucket i: the reference's bwd/nb, or under a
+    // geometric policy the bucket's share of the parameters
+    for (uint64_t sz : sizes_)
+      bwd_us_.push_back(ratio_ >= 1.0 ? bwd_us_per_bucket_ : st.avg_backward_time_us * sz / static_cast<double>(P_));
     fwd_flops_ = st.forward_flops;
     bwd_flops_per_bucket_ = st.backward_flops / nb_;
 
@@ -53,6 +87,7 @@ class DataParallel : public Strategy {
     for (uint64_t sz : sizes_) shard_.push_back((sz + W_ - 1) / W_);
     std::vector<int> all;
     for (int r = 0; r < ctx.world(); ++r) all.push_back(r);
+    // (bucket 0 is the largest under every policy)
     comm_ = ctx.comms->create("dp/world", all, (zero_ ? shard_[0] * W_ : sizes_[0]) * es_, false, ctx.lane_ctas);
     compute_ = dev.create_stream(false);
     comm_stream_ = dev.create_stream(true);
@@ -100,16 +135,24 @@ class DataParallel : public Strategy {
     timers_.reset(new TimerSet(dev));
     timers_->ensure("barrier_time");
     timers_->ensure("allreduce_time");
+    // bytes per op for the bandwidth summary: the first bucket's (the
+    // reference's msg size) under the even policy, the mean otherwise
+    double op_bytes = 0, shard_bytes = 0;
+    for (int i = 0; i < nb_; ++i) {
+      op_bytes += static_cast<double>((zero_ ? shard_[i] * W_ : sizes_[i]) * es_) / nb_;
+      shard_bytes += static_cast<double>(shard_[i] * W_ * es_) / nb_;
+    }
+    if (ratio_ >= 1.0) {
+      op_bytes = static_cast<double>((zero_ ? shard_[0] * W_ : sizes_[0]) * es_);
+      shard_bytes = static_cast<double>(shard_[0] * W_ * es_);
+    }
     if (zero_ == 2)
-      stats_ = {{"reduce_scatter", CollKind::ReduceScatter, W_, static_cast<double>(shard_[0] * W_ * es_),
-                 "reduce_scatter_time"}};
+      stats_ = {{"reduce_scatter", CollKind::ReduceScatter, W_, shard_bytes, "reduce_scatter_time"}};
     else
-      stats_ = {{"allreduce", CollKind::AllReduce, W_, static_cast<double>((zero_ ? shard_[0] * W_ : sizes_[0]) * es_),
-                 "allreduce_time"}};
+      stats_ = {{"allreduce", CollKind::AllReduce, W_, op_bytes, "allreduce_time"}};
     if (zero_) {
       for (const char* k : {"reduce_scatter_time", "param_allgather_time", "param_allgather_exposed"}) timers_->ensure(k);
-      stats_.push_back({"param_allgather", CollKind::AllGather, W_, static_cast<double>(shard_[0] * W_ * es_),
-                        "param_allgather_time"});
+      stats_.push_back({"param_allgather", CollKind::AllGather, W_, shard_bytes, "param_allgather_time"});
     }
   }
 
@@ -121,7 +164,7 @@ class DataParallel : public Strategy {
     ce.run(*compute_, fwd_us_, fwd_flops_);
     for (int i = 0; i < nb_; ++i) {
       // only event records on compute_ since the forward: one stretch of compute
-      ce.run_chained(*compute_, bwd_us_per_bucket_, bwd_flops_per_bucket_);
+      ce.run_chained(*compute_, bwd_us_[i], bwd_flops_per_bucket_);
       compute_->record(*ready_[i]);
       comm_stream_->wait(*ready_[i]);
       const uint64_t n = shard_[i] * W_;
@@ -164,7 +207,7 @@ class DataParallel : public Strategy {
     ce.run(*compute_, fwd_us_, fwd_flops_);
     for (int i = 0; i < nb_; ++i) {
       // only event records on compute_ since the forward: one stretch of compute
-      ce.run_chained(*compute_, bwd_us_per_bucket_, bwd_flops_per_bucket_);
+      ce.run_chained(*compute_, bwd_us_[i], bwd_flops_per_bucket_);
       compute_->record(*ready_[i]);
       comm_stream_->wait(*ready_[i]);
       int t = timers_->begin(*comm_stream_);
@@ -216,6 +259,13 @@ class DataParallel : public Strategy {
     g["device"] = ctx.dev->kind() == DeviceKind::CPU ? "CPU" : "GPU";
     g["backend"] = comm_->backend_name();
     g["in_place"] = in_place_;
+    g["bucket_ratio"] = ratio_;
+    if (ratio_ < 1.0) {
+      g["bucket_policy"] = "geometric";
+      g["bucket_sizes"] = Json(sizes_);
+    } else {
+      g["bucket_policy"] = "even";
+    }
     g["zero_stage"] = zero_;
     if (zero_) {
       g["shard_size_params"] = shard_[0];
@@ -245,6 +295,8 @@ class DataParallel : public Strategy {
   uint64_t P_ = 0;
   size_t es_ = 2;
   std::vector<uint64_t> sizes_;
+  std::vector<double> bwd_us_;  // backward compute per bucket
+  double ratio_ = 1.0;
   double fwd_us_ = 0, bwd_us_per_bucket_ = 0, fwd_flops_ = 0, bwd_flops_per_bucket_ = 0;
   bool in_place_ = false;
   int zero_ = 0, W_ = 1;

@@ -32,7 +32,7 @@ _FLAG = {
     "warmup": "-w", "runs": "-r", "devices": "-d", "min_exectime": "-m",
     "backend": "--backend", "compute": "--compute", "wire_dtype": "--wire-dtype",
     "compute_dtype": "--compute-dtype", "schedule": "--schedule", "tp_granularity": "--tp-granularity",
-    "dp_buckets": "--dp-buckets", "max_loop_iters": "--max-loop-iters", "time_scale": "--time-scale",
+    "dp_buckets": "--dp-buckets", "dp_bucket_ratio": "--dp-bucket-ratio", "max_loop_iters": "--max-loop-iters", "time_scale": "--time-scale",
     "json": "--json", "store": "--store", "stats_file": "--stats-file", "comm_cus": "--comm-cus",
     "comm_lanes": "--comm-lanes", "pp_schedule": "--pp-schedule", "zero": "--zero", "cp_algo": "--cp-algo", "pp_virtual": "--pp-virtual",
     "ranks": "--ranks", "ep_imbalance": "--ep-imbalance", "rccl_max_ctas": "--rccl-max-ctas",

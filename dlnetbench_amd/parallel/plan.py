@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 from dataclasses import asdict, dataclass, field
 from typing import Dict, List
@@ -85,13 +86,38 @@ def _split(total: int, parts: int) -> List[int]:
     return [base + (1 if i < rem else 0) for i in range(parts)]
 
 
-def plan_dp(st: ModelStats, world: int, nb: int, wire: str = "bf16", zero: int = 0) -> Plan:
+def dp_bucket_sizes(P: int, nb: int, ratio: float = 1.0) -> List[int]:
+    """csrc/src/strategy_dp.cpp dp_bucket_sizes(), bit for bit: ratio 1 is the
+    reference's P/nb partition (cpp/data_parallel/dp.cpp:159-164); ratio r < 1
+    gives bucket i (backward order) floor(P r^i / sum_j r^j), the rest to
+    bucket 0 (a geometric tail: the last, exposed all-reduce is small)."""
+    if ratio >= 1.0:
+        return _split(P, nb)
+    w, x = [], 1.0
+    for _ in range(nb):
+        w.append(x)
+        x *= ratio
+    tot = 0.0
+    for v in w:
+        tot += v
+    s = [int(math.floor(float(P) * v / tot)) for v in w]
+    s[0] += P - sum(s)
+    if min(s) <= 0:
+        raise ValueError(f"--dp-bucket-ratio {ratio} leaves an empty bucket of {nb}")
+    return s
+
+
+def plan_dp(st: ModelStats, world: int, nb: int, wire: str = "bf16", zero: int = 0, ratio: float = 1.0) -> Plan:
     """zero = 1|2: ZeRO extension of csrc/src/strategy_dp.cpp (buckets padded to
-    world * ceil(size / world); stage 2 reduce-scatters instead of all-reducing)."""
+    world * ceil(size / world); stage 2 reduce-scatters instead of all-reducing).
+    ratio < 1: geometric bucket sizes (dp_bucket_sizes), listed per bucket."""
     es = WIRE_BYTES[wire]
-    sizes = _split(st.model_size, nb)
-    p = Plan("dp", world, {"num_buckets": nb, "zero": zero},
+    sizes = dp_bucket_sizes(st.model_size, nb, ratio)
+    p = Plan("dp", world, {"num_buckets": nb, "zero": zero, "bucket_ratio": ratio},
              {"fwd": st.fwd_us, "bwd_per_bucket": st.bwd_us / nb})
+    if ratio < 1.0:
+        p.params["bucket_sizes"] = sizes
+        p.compute_per_unit_us["bwd_per_bucket"] = [st.bwd_us * s / st.model_size for s in sizes]
     if not zero:
         p.messages.append(Message("bucket_allreduce", "allreduce", world, sizes[0], nb, sizes[0] * es))
         p.memory_bytes = 2 * st.model_size * es
@@ -294,6 +320,8 @@ def main(argv=None) -> int:
     ap.add_argument("--base", default=".")
     ap.add_argument("--wire", default="bf16")
     ap.add_argument("--zero", type=int, default=0, help="dp: ZeRO stage 0|1|2")
+    ap.add_argument("--dp-bucket-ratio", type=float, default=1.0,
+                    help="dp: geometric bucket sizes, bucket i holds a share r^i (1 = the reference's P/nb)")
     ap.add_argument("--cp-algo", default="ring", choices=["ring", "ulysses"])
     ap.add_argument("--ep-imbalance", type=float, default=0.0, help="hybrid_3d_moe: Zipf exponent of the expert load")
     ap.add_argument("--pp-schedule", default="gpipe", choices=["gpipe", "1f1b", "interleaved", "dualpipe"])
@@ -311,7 +339,7 @@ def main(argv=None) -> int:
     a = ap.parse_args(argv)
     st = load_stats(os.path.join(a.base, "model_stats", a.model + ".txt"))
     if a.strategy == "dp":
-        pl = plan_dp(st, a.world, *a.params, wire=a.wire, zero=a.zero)
+        pl = plan_dp(st, a.world, *a.params, wire=a.wire, zero=a.zero, ratio=a.dp_bucket_ratio)
     elif a.strategy == "fsdp":
         pl = plan_fsdp(st, a.world, *a.params, wire=a.wire)
     else:
@@ -336,7 +364,7 @@ def main(argv=None) -> int:
         pred = {}
         for w in (1, 2, 4, 8):
             if a.strategy == "dp":
-                pred[str(w)] = xm.predict_dp(st, w, a.params[0], lm, a.wire, a.algo)
+                pred[str(w)] = xm.predict_dp(st, w, a.params[0], lm, a.wire, a.algo, ratio=a.dp_bucket_ratio)
             elif w % a.params[1] == 0 or a.params[1] == a.world:
                 F = w if a.params[1] == a.world else a.params[1]  # fully sharded runs shard over the job
                 pred[str(w)] = xm.predict_fsdp(st, w, a.params[0], F, lm, a.wire, a.algo)

@@ -38,7 +38,7 @@ from dataclasses import dataclass
 from typing import Dict, List
 
 from ..utils.stats import ModelStats
-from .plan import WIRE_BYTES, fsdp_shards, _split
+from .plan import WIRE_BYTES, dp_bucket_sizes, fsdp_shards
 
 
 @dataclass
@@ -86,17 +86,17 @@ class LinkModel:
 
 
 def predict_dp(st: ModelStats, world: int, nb: int, model: LinkModel, wire: str = "bf16",
-               algo: str = "direct") -> Dict[str, float]:
+               algo: str = "direct", ratio: float = 1.0) -> Dict[str, float]:
     """dp: forward, then bucket i's backward followed by its all-reduce on the
     comm lane (strategy_dp.cpp enqueue order); the iteration ends when the
-    last all-reduce is done."""
+    last all-reduce is done. ratio < 1: geometric buckets (--dp-bucket-ratio),
+    each bucket's backward its share of the parameters."""
     es = WIRE_BYTES[wire]
-    sizes = _split(st.model_size, nb)
-    b = st.bwd_us / nb
+    sizes = dp_bucket_sizes(st.model_size, nb, ratio)
     t = st.fwd_us
     lane = 0.0
     for s in sizes:
-        t += b
+        t += st.bwd_us / nb if ratio >= 1.0 else st.bwd_us * s / st.model_size
         lane = max(lane, t) + model.coll_us("allreduce", s * es, world, algo)
     end = max(t, lane)
     floor = st.fwd_us + st.bwd_us

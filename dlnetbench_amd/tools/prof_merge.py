@@ -15,8 +15,17 @@ fabric: Infinity Cache or HBM; FETCH_SIZE / WRITE_SIZE) with their rate.
     python -m dlnetbench_amd.tools.prof_merge r.json gpurun_out/prof gpurun_out/pmc -o r_counters.json
 
 Counter units (rocprofv3 derived metrics): FETCH_SIZE / WRITE_SIZE are KiB;
-MFMA MOPS count 512 FLOPs each; MFMA busy is normalised by
-GRBM_GUI_ACTIVE / 8 XCDs x CUs x 4 SIMDs (MI355X: 256 CUs).
+MFMA MOPS count 512 FLOPs each; MFMA busy is normalised by clock x kernel
+time x CUs x 4 SIMDs (MI355X: 256 CUs).
+
+Clock: GRBM_GUI_ACTIVE counts GPU-busy cycles (x 8 XCDs) over the counter
+collection window of a dispatch, which is longer than the kernel's own start
+/ end stamps by a fixed setup cost - dividing by the kernel time read 2.9-3.5
+GHz for 10-us copy / stamp kernels. The clock is therefore derived only from
+dispatches of at least LONG_DISPATCH_MS (per class when it has some, else
+from every long dispatch of the job, ``clock_source: job``), and a derived
+clock above MAX_CLOCK_GHZ (the MI355X peak is 2.4 GHz) or an MFMA busy
+fraction above 1 raises instead of being reported.
 """
 from __future__ import annotations
 
@@ -32,6 +41,8 @@ from typing import Dict, Iterable, List, Optional
 CUS = 256
 XCDS = 8
 SIMDS = 4
+LONG_DISPATCH_MS = 0.5
+MAX_CLOCK_GHZ = 2.5
 
 # first match wins
 CLASSES = [
@@ -77,7 +88,8 @@ def collect(dirs: List[str]) -> Dict[str, dict]:
     collected in, so rates derived from it are per pass, never diluted."""
     cls: Dict[str, dict] = collections.defaultdict(
         lambda: {"calls": 0, "time_ms": 0.0, "counters": collections.defaultdict(float),
-                 "counter_ms": collections.defaultdict(float), "kernels": collections.Counter()})
+                 "counter_ms": collections.defaultdict(float), "kernels": collections.Counter(),
+                 "gui": []})  # (dispatch ms, GRBM_GUI_ACTIVE) per dispatch
     traced = set()
     for path in _csvs(dirs, "kernel_trace.csv"):
         for r in csv.DictReader(open(path)):
@@ -98,9 +110,11 @@ def collect(dirs: List[str]) -> Dict[str, dict]:
             c["counters"][r["Counter_Name"]] += _f(r.get("Counter_Value"))
             file_names[k].add(r["Counter_Name"])
             key = (r.get("Dispatch_Id"), r.get("Agent_Id"))
+            ms = (_f(r.get("End_Timestamp")) - _f(r.get("Start_Timestamp"))) / 1e6
+            if r["Counter_Name"] == "GRBM_GUI_ACTIVE":
+                c["gui"].append((ms, _f(r.get("Counter_Value"))))
             if key not in seen:
                 seen.add(key)
-                ms = (_f(r.get("End_Timestamp")) - _f(r.get("Start_Timestamp"))) / 1e6
                 file_ms[k] += ms
                 if k not in traced:  # counters without a trace: count the dispatches here
                     c["calls"] += 1
@@ -118,7 +132,20 @@ def _short(name: str) -> str:
     return name[:80]
 
 
-def derive(c: dict) -> dict:
+def long_dispatch_clock(gui: List[tuple]) -> Optional[float]:
+    """Clock (Hz) from the dispatches of at least LONG_DISPATCH_MS:
+    sum(GRBM_GUI_ACTIVE) / XCDs over their summed kernel time; None if none."""
+    long = [(ms, g) for ms, g in gui if ms >= LONG_DISPATCH_MS and g > 0]
+    if not long:
+        return None
+    hz = sum(g for _, g in long) / XCDS / (sum(ms for ms, _ in long) * 1e-3)
+    if hz / 1e9 > MAX_CLOCK_GHZ:
+        raise ValueError(f"derived clock {hz / 1e9:.3f} GHz > {MAX_CLOCK_GHZ} GHz from {len(long)} dispatches "
+                         f">= {LONG_DISPATCH_MS} ms: GRBM_GUI_ACTIVE or the timestamps are not what prof_merge assumes")
+    return hz
+
+
+def derive(c: dict, job_clock: Optional[float] = None) -> dict:
     """Per-class summary with derived rates (only those whose counters exist)."""
     k = c["counters"]
     out = {"calls": c["calls"], "time_ms": round(c["time_ms"], 4),
@@ -128,11 +155,18 @@ def derive(c: dict) -> dict:
         ms = c["counter_ms"].get(name, 0.0)
         return k.get(name, 0.0) / (ms * 1e-3) if ms > 0 else 0.0
 
-    if rate("GRBM_GUI_ACTIVE") > 0:
-        gui = rate("GRBM_GUI_ACTIVE") / XCDS  # cycles per second = clock
-        out["clock_GHz"] = round(gui / 1e9, 3)
+    hz = long_dispatch_clock(c.get("gui", []))
+    source = "class"
+    if hz is None and job_clock and c.get("gui"):
+        hz, source = job_clock, "job"
+    if hz:
+        out["clock_GHz"] = round(hz / 1e9, 3)
+        out["clock_source"] = source
         if "SQ_VALU_MFMA_BUSY_CYCLES" in k:
-            out["mfma_busy"] = round(rate("SQ_VALU_MFMA_BUSY_CYCLES") / (gui * CUS * SIMDS), 4)
+            busy = rate("SQ_VALU_MFMA_BUSY_CYCLES") / (hz * CUS * SIMDS)
+            if busy > 1.0 + 1e-6:
+                raise ValueError(f"MFMA busy fraction {busy:.3f} > 1 (clock {hz / 1e9:.3f} GHz)")
+            out["mfma_busy"] = round(busy, 4)
     mops = sum(rate(n) for n in k if n.startswith("SQ_INSTS_VALU_MFMA_MOPS"))
     if mops:
         out["mfma_TFLOPs"] = round(mops * 512 / 1e12, 1)
@@ -147,7 +181,8 @@ def derive(c: dict) -> dict:
 
 def merge(report: dict, dirs: List[str]) -> dict:
     cls = collect(dirs)
-    classes = {name: derive(c) for name, c in sorted(cls.items())}
+    job_clock = long_dispatch_clock([d for c in cls.values() for d in c["gui"]])
+    classes = {name: derive(c, job_clock) for name, c in sorted(cls.items())}
     total = sum(v["time_ms"] for v in classes.values())
     for v in classes.values():
         v["time_pct"] = round(100.0 * v["time_ms"] / total, 2) if total else 0.0

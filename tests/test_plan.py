@@ -256,3 +256,40 @@ def test_ep_dispatch_counts_match_the_native_run(data_dir):
     from dlnetbench_amd.utils import report
     doc = next(iter(report.parse_output(p.stdout).values()))
     assert doc["global"]["ep_dispatch_bytes_per_peer"] == [c * 2 for c in counts]
+
+
+@pytest.mark.parametrize("nb,ratio", [(8, 0.7), (8, 1.0), (13, 0.55), (4, 0.9)])
+def test_dp_geometric_buckets_match_native(nb, ratio, root):
+    """--dp-bucket-ratio: the native driver's bucket sizes (global.bucket_sizes)
+    equal plan.dp_bucket_sizes bit for bit, sum to P, shrink geometrically; the
+    even policy is the reference's partition."""
+    from dlnetbench_amd import engine
+    from dlnetbench_amd.parallel.plan import dp_bucket_sizes
+    from dlnetbench_amd.utils.stats import load_stats
+    st = load_stats(os.path.join(root, "model_stats", "vit_h_32_float8.txt"))
+    py = dp_bucket_sizes(st.model_size, nb, ratio)
+    assert sum(py) == st.model_size and len(py) == nb
+    d = engine.run("dp", "vit_h_32_float8", nb, base_path=root, backend="loopback-cpu", ranks=1, compute="sleep",
+                   warmup=0, runs=1, time_scale=0.01, silent=True, dp_bucket_ratio=ratio)
+    g = d["global"]
+    assert g["bucket_ratio"] == ratio
+    if ratio < 1:
+        assert g["bucket_policy"] == "geometric" and g["bucket_sizes"] == py
+        assert all(a > b for a, b in zip(py[1:-1], py[2:]))
+    else:
+        assert g["bucket_policy"] == "even" and py == [st.model_size // nb + (i < st.model_size % nb)
+                                                      for i in range(nb)]
+
+
+def test_dp_geometric_tail_shrinks_predicted_n8_step(root):
+    """The xGMI model (plan dp --predict): 8 geometric buckets (r = 0.7) take
+    the predicted ViT-H N = 8 step from ~7.50 ms (even, the last bucket's
+    all-reduce exposed) toward the 7.13 ms floor."""
+    from dlnetbench_amd.parallel import xgmi_model as xm
+    from dlnetbench_amd.utils.stats import load_stats
+    st = load_stats(os.path.join(root, "model_stats", "vit_h_32_float8.txt"))
+    lm = xm.LinkModel()
+    even = xm.predict_dp(st, 8, 8, lm)["iter_ms"]
+    geo = xm.predict_dp(st, 8, 8, lm, ratio=0.7)["iter_ms"]
+    assert even == pytest.approx(7.504, abs=0.01)
+    assert geo == pytest.approx(7.24, abs=0.01) and geo < even

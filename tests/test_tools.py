@@ -304,3 +304,35 @@ def test_xgmi_kernels_fit_the_cu_budget(root):
         assert k["max_threads"] == 512, k
         assert k["waves_per_simd"] == 8 and k["blocks_per_cu_regs"] >= 4, k
         assert k["scratch"] == 0, k
+
+
+def test_prof_merge_clock_from_long_dispatches_only(tmp_path):
+    """GRBM_GUI_ACTIVE over a short dispatch includes the collection window's
+    setup cycles: a 10-us copy kernel must not report a 5 GHz clock. Classes
+    without long dispatches take the job's clock; an impossible clock raises."""
+    from dlnetbench_amd.tools import prof_merge
+    pm = tmp_path / "pmc"
+    pm.mkdir()
+    g = "void dlnb::kernels::gemm_8phase_kernel<false, true, false>(...)"
+    cp = "__amd_rocclr_copyBuffer"
+    with open(pm / "y_counter_collection.csv", "w") as f:
+        f.write("Dispatch_Id,Agent_Id,Kernel_Name,Counter_Name,Counter_Value,Start_Timestamp,End_Timestamp\n")
+        # two long GEMM dispatches at 2.0 GHz (2 ms, 3 ms)
+        for d, ms in ((1, 2.0), (2, 3.0)):
+            f.write(f'{d},1,"{g}",GRBM_GUI_ACTIVE,{8 * 2.0e9 * ms * 1e-3},0,{int(ms * 1e6)}\n')
+            f.write(f'{d},1,"{g}",SQ_VALU_MFMA_BUSY_CYCLES,{0.6 * 2.0e9 * ms * 1e-3 * 1024},0,{int(ms * 1e6)}\n')
+        # 50 short copies of 10 us, each with 30k cycles of window overhead (naive clock: 5 GHz)
+        for d in range(3, 53):
+            f.write(f'{d},1,"{cp}",GRBM_GUI_ACTIVE,{8 * (2.0e9 * 10e-6 + 30000)},0,10000\n')
+    rep = prof_merge.merge({}, [str(pm)])
+    cl = rep["global"]["dlnb"]["counters"]["classes"]
+    assert cl["compute_gemm"]["clock_GHz"] == pytest.approx(2.0) and cl["compute_gemm"]["clock_source"] == "class"
+    assert cl["compute_gemm"]["mfma_busy"] == pytest.approx(0.6)
+    assert cl["copy"]["clock_GHz"] == pytest.approx(2.0) and cl["copy"]["clock_source"] == "job"
+    for c in cl.values():
+        assert c.get("clock_GHz", 0) <= 2.4
+    # a long dispatch whose GUI count implies 3 GHz is rejected, not reported
+    with open(pm / "y_counter_collection.csv", "a") as f:
+        f.write(f'99,1,"{g}",GRBM_GUI_ACTIVE,{8 * 3.0e9 * 10 * 1e-3 * 10},0,10000000\n')
+    with pytest.raises(ValueError, match="GHz"):
+        prof_merge.merge({}, [str(pm)])
