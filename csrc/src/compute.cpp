@@ -92,7 +92,13 @@ class GpuCompute : public ComputeEngine {
       // room (with the whole chip taken, a comm kernel only starts at a
       // compute boundary, and overlap collapses).
       grid_ = std::max(1, cus_ - std::max(0, shape.comm_cus));
-      slice_us_ = static_cast<double>(env_int("DLNB_GEMM_SLICE_US", 500));
+      // One launch per task by default. Cutting a task into relaunched
+      // slices (DLNB_GEMM_SLICE_US > 0) was meant to give collectives CUs at
+      // slice boundaries, which the comm_cus reservation already does; at
+      // 500-us slices every slice also abandons a partial 256 x 256 tile and
+      // pays a prologue: 630 vs 679 TF/s per GHz on the headline
+      // (profiles/slice_ab_r3.md), and a 4x larger graph.
+      slice_us_ = static_cast<double>(env_int("DLNB_GEMM_SLICE_US", 0));
     }
   }
 
@@ -112,7 +118,7 @@ class GpuCompute : public ComputeEngine {
         // Same epoch, so the same t0: this task's slices end at the previous
         // task's deadline + its own duration on the clock the chain started.
         const uint64_t base = it->second, total = base + ticks(us * scale_);
-        const uint64_t slice = std::max<uint64_t>(ticks(slice_us_), 1);
+        const uint64_t slice = slice_us_ > 0 ? std::max<uint64_t>(ticks(slice_us_), 1) : total;
         for (uint64_t end = base + slice;; end += slice) {
           kernels::gemm_tn_deadline(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, total, slot, epoch_[slot],
                                     grid_, s.native(), std::min(end, total), nullptr);
@@ -150,7 +156,7 @@ class GpuCompute : public ComputeEngine {
       uint32_t& ep = epoch_[slot_for(s)];
       ep = ep % 65535 + 1;  // 1..65535, never 0 (a fresh slot reads as epoch 0)
       const uint64_t total = ticks(d);
-      const uint64_t slice = std::max<uint64_t>(ticks(slice_us_), 1);
+      const uint64_t slice = slice_us_ > 0 ? std::max<uint64_t>(ticks(slice_us_), 1) : total;
       for (uint64_t end = slice;; end += slice) {
         kernels::gemm_tn_deadline(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, total, slot_for(s), ep,
                                   grid_, s.native(), std::min(end, total), end == slice ? start : nullptr);

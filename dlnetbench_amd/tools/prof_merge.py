@@ -186,6 +186,13 @@ def merge(report: dict, dirs: List[str]) -> dict:
     total = sum(v["time_ms"] for v in classes.values())
     for v in classes.values():
         v["time_pct"] = round(100.0 * v["time_ms"] / total, 2) if total else 0.0
+    # The deadline GEMM runs on `deadline_grid` CUs (the rest are left to the
+    # collectives): its MFMA busy fraction on the CUs it occupies.
+    grid = report.get("global", {}).get("dlnb", {}).get("compute", {}).get("deadline_grid")
+    cg = classes.get("compute_gemm")
+    if grid and cg and "mfma_busy" in cg:
+        cg["grid_cus"] = grid
+        cg["mfma_busy_on_grid"] = round(cg["mfma_busy"] * CUS / grid, 4)
     g = report.setdefault("global", {}).setdefault("dlnb", {})
     g["counters"] = {"source": [os.path.basename(os.path.normpath(d)) for d in dirs], "total_kernel_ms": round(total, 4),
                      "classes": classes}

@@ -49,12 +49,12 @@ for step in "$@"; do
     counters)
       # bench headline (FSDP, N = 1) with rocprof counters folded into its report (global.dlnb.counters):
       # a kernel trace of the graph-replayed run + two PMC passes (TCC holds FETCH_SIZE or WRITE_SIZE, not
-      # both) of one eagerly enqueued iteration with 20 ms compute slices.
+      # both) of one eagerly enqueued iteration (one deadline launch per task, the default).
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       B="bench.py --c5-model none --stretch-steps 0"
       run cnt_trace 400 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/cnt_trace -o bench -- python3 $B --steps 2 --warmup 1 --json gpurun_out/bench_cnt_report.json
-      run cnt_pmc_a 400 env DLNB_GEMM_SLICE_US=20000 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU_MFMA_MOPS_BF16 FETCH_SIZE --output-format csv -d gpurun_out/cnt_pmc_a -o a -- python3 $B --steps 1 --warmup 0 --no-graph
-      run cnt_pmc_b 400 env DLNB_GEMM_SLICE_US=20000 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/cnt_pmc_b -o b -- python3 $B --steps 1 --warmup 0 --no-graph
+      run cnt_pmc_a 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU_MFMA_MOPS_BF16 FETCH_SIZE --output-format csv -d gpurun_out/cnt_pmc_a -o a -- python3 $B --steps 1 --warmup 0 --no-graph
+      run cnt_pmc_b 400 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/cnt_pmc_b -o b -- python3 $B --steps 1 --warmup 0 --no-graph
       run cnt_merge 60 python -m dlnetbench_amd.tools.prof_merge gpurun_out/bench_cnt_report.json gpurun_out/cnt_trace gpurun_out/cnt_pmc_a gpurun_out/cnt_pmc_b -o gpurun_out/bench_counters.json ;;
     *) echo "unknown step $step" >> gpurun_out/steps.log ;;
   esac

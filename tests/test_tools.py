@@ -336,3 +336,20 @@ def test_prof_merge_clock_from_long_dispatches_only(tmp_path):
         f.write(f'99,1,"{g}",GRBM_GUI_ACTIVE,{8 * 3.0e9 * 10 * 1e-3 * 10},0,10000000\n')
     with pytest.raises(ValueError, match="GHz"):
         prof_merge.merge({}, [str(pm)])
+
+
+def test_prof_merge_busy_on_the_deadline_grid(tmp_path):
+    """The deadline GEMM occupies deadline_grid CUs (224 of 256): its MFMA busy
+    fraction on those CUs is reported next to the whole-chip one."""
+    from dlnetbench_amd.tools import prof_merge
+    pm = tmp_path / "pmc"
+    pm.mkdir()
+    g = "void dlnb::kernels::gemm_8phase_kernel<false, true, true>(...)"
+    with open(pm / "y_counter_collection.csv", "w") as f:
+        f.write("Dispatch_Id,Agent_Id,Kernel_Name,Counter_Name,Counter_Value,Start_Timestamp,End_Timestamp\n")
+        f.write(f'1,1,"{g}",GRBM_GUI_ACTIVE,{8 * 2.0e9 * 1e-3},0,1000000\n')
+        f.write(f'1,1,"{g}",SQ_VALU_MFMA_BUSY_CYCLES,{0.7 * 2.0e9 * 1e-3 * 224 * 4},0,1000000\n')
+    rep = {"global": {"dlnb": {"compute": {"deadline_grid": 224}}}}
+    c = prof_merge.merge(rep, [str(pm)])["global"]["dlnb"]["counters"]["classes"]["compute_gemm"]
+    assert c["mfma_busy"] == pytest.approx(0.7 * 224 / 256) and c["mfma_busy_on_grid"] == pytest.approx(0.7)
+    assert c["grid_cus"] == 224
