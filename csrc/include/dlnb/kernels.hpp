@@ -41,24 +41,21 @@ int num_cus(int device);
 // dimensions in elements, 16-byte aligned rows. in_t is BF16 or FP8_E4M3;
 // C is always bf16.
 bool gemm_shape_ok(int M, int N, int K, DType in_t);
-// waves selects the variant: 8 = 8 waves (2 per SIMD, 128x64 per wave)
-// double buffered, 2 = the same with software-pipelined fragment reads
-// (bf16), 1 = 8 waves with a 3-deep A ring (160 KiB LDS), 4 = 4 waves (1 per
-// SIMD, 128x128 per wave), 6 = 8-phase with balanced fragment reads (bf16;
-// even K-tile counts, else 3), 7 / 9 = 8-phase balanced / plain with one
-// uniform K-tile body, 5 = one wave per SIMD with AGPR accumulators (below);
-// 0 = the default: bf16 6, fp8 5 (K % 256 == 0) else 9, where they apply
-// (>= 2 K-tiles), else 2 for bf16 / 8 for fp8 (ring if DLNB_GEMM_RING=1, 4
-// waves if DLNB_GEMM_WAVES=4).
-// 3 = the 8-phase ping-pong schedule (gemm_8phase.hip; needs >= 2 K-tiles).
+// variant:
+//   0 = the default: fp8 5 where it applies (K % 256 == 0), else 6 where it
+//       applies (>= 2 K-tiles), else 8;
+//   5 = one wave per SIMD, 128 x 128 of C per wave, MX MFMA with AGPR
+//       accumulators (gemm_4wave_fp8.hip; fp8, K % 256 == 0; the streaming
+//       persistent kernel when there are more tiles than CUs);
+//   6 = the 8-phase ping-pong schedule, 8 waves (2 per SIMD, 128 x 64 of C
+//       each; gemm_8phase.hip; bf16 balanced fragment reads when the K-tile
+//       count is even, fp8 one uniform K-tile body; >= 2 K-tiles);
+//   8 = 8 waves double-buffered (kernels.hip; bf16 software-pipelined reads):
+//       any K, the fallback.
+// A variant that does not take a shape falls through to the next that does.
 void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
-             void* stream, int waves = 0);
+             void* stream, int variant = 0);
 bool gemm_8phase_shape_ok(int M, int N, int K, DType in_t);
-// 5 = one wave per SIMD, 128 x 128 of C per wave (gemm_4wave.hip; bf16, K % 64 == 0).
-bool gemm_4wave_shape_ok(int M, int N, int K, DType in_t);
-void gemm_tn_4wave(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
-                   void* stream);
-//   fp8: gemm_4wave_fp8.hip (MX MFMA, K % 256 == 0).
 bool gemm_4wave_fp8_shape_ok(int M, int N, int K, DType in_t);
 void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                        void* stream);
@@ -66,14 +63,10 @@ void gemm_tn_4wave_fp8_deadline(const void* A, const void* B, void* C, int M, in
                                 uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
                                 uint64_t* tstart);
 void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
-                    void* stream, bool balanced = false, bool uniform = false);
+                    void* stream);
 void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
                              uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
                              uint64_t* tstart);
-// Whether the 8-phase schedule is used where it applies (default on;
-// DLNB_GEMM_8PHASE=0 selects the older double-buffered kernel for A/B runs).
-bool gemm_8phase_enabled();
-int gemm_default_waves();
 
 // Persistent deadline variant (the default stand-in compute): a grid of
 // `grid` blocks (<= one per CU: 128 KiB LDS each) walks the M x N tile space
@@ -81,9 +74,9 @@ int gemm_default_waves();
 // s_memrealtime) after t0. t0 is agreed through *slot: the first block of the
 // first launch of `epoch` (1..65535, different from the slot's previous task)
 // CASes {epoch:16 | t0:48} into it; every other block and every later launch
-// with the same epoch reads it. A long task is issued as several launches
-// (slices) with increasing slice_end so that collectives on other streams get
-// CUs at slice boundaries, as they do between a training step's kernels.
+// with the same epoch reads it. A task is one launch by default; with
+// DLNB_GEMM_SLICE_US it is issued as several launches (slices) with
+// increasing slice_end (compute.cpp; profiles/slice_ab_r3.md).
 // Leading dimensions are K, K and N.
 // tstart (optional, host-mapped): the block that claims the epoch stores the
 // task's start (s_memrealtime) there - stall timing without extra kernels.

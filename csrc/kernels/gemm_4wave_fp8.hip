@@ -495,15 +495,14 @@ void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int 
   DLNB_REQUIRE(gemm_4wave_fp8_shape_ok(M, N, K, DType::FP8_E4M3),
                "gemm 4-wave fp8: unsupported shape M=" << M << " N=" << N << " K=" << K);
   const int tiles = (M / kT) * (N / kT);
-  static const int group = static_cast<int>(std::max<long long>(1, env_int("DLNB_GEMM_GROUP", 8)));
+  constexpr int group = 8;  // M-tiles sharing B panels in L2 (4 / 8 / 16 / 32 measured: 8 best)
   // more tiles than CUs: the streaming persistent kernel, one block per CU
-  // (+1-5 %, profiles/gemm_bench_r2.md); DLNB_GEMM_FP8_STREAM=0: a block per tile
-  const bool stream_on = env_int("DLNB_GEMM_FP8_STREAM", 1) != 0;
+  // (+1-5 %, profiles/gemm_bench_r2.md); else a block per tile
   static const int cus = [] {
     int dev = 0;
     return hipGetDevice(&dev) == hipSuccess ? num_cus(dev) : 256;
   }();
-  if (stream_on && tiles > cus) {
+  if (tiles > cus) {
     hipLaunchKernelGGL(gemm_4wave_fp8_stream_kernel<false>, cus, 256, 0, static_cast<hipStream_t>(stream),
                        static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K,
                        lda, ldb, ldc, group, nullptr, 0u, 0ull, 0ull, nullptr);
@@ -522,18 +521,9 @@ void gemm_tn_4wave_fp8_deadline(const void* A, const void* B, void* C, int M, in
                                 uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
                                 uint64_t* tstart) {
   DLNB_REQUIRE(gemm_4wave_fp8_shape_ok(M, N, K, DType::FP8_E4M3), "gemm 4-wave fp8 deadline: unsupported shape");
-  // DLNB_GEMM_FP8_DL_STREAM=1: the streaming deadline kernel. Power-bound on
-  // the 224 CUs, it runs +5 % MFMA per clock at a 5 % lower clock: the same
-  // 2620-2630 TF/s as the per-tile kernel (0 spills vs 6), which stays the
-  // default (scripts/probes/deadline_rate_fp8_stream.sh)
-  if (env_int("DLNB_GEMM_FP8_DL_STREAM", 0) != 0) {
-    hipLaunchKernelGGL(gemm_4wave_fp8_stream_kernel<true>, grid, 256, 0, static_cast<hipStream_t>(stream),
-                       static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, K,
-                       K, N, 8, slot, epoch, ticks, slice_end, tstart);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) DLNB_THROW("gemm 4-wave fp8 deadline launch failed: " << hipGetErrorString(e));
-    return;
-  }
+  // The per-tile kernel. (Its streaming twin ran +5 % MFMA per clock at a 5 %
+  // lower, power-capped clock on the 224 CUs - the same 2620-2630 TF/s - so
+  // it was not kept as a deadline kernel: profiles/gemm_deadline_stream_r2.md.)
   hipLaunchKernelGGL(gemm_4wave_fp8_kernel<true>, grid, 256, 0, static_cast<hipStream_t>(stream),
                      static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, K, K,
                      N, 8, slot, epoch, ticks, slice_end, tstart);

@@ -645,51 +645,27 @@ bool gemm_8phase_shape_ok(int M, int N, int K, DType in_t) {
 }
 
 void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
-                    void* stream, bool balanced, bool uniform) {
+                    void* stream) {
   DLNB_REQUIRE(gemm_8phase_shape_ok(M, N, K, in_t), "gemm 8-phase: unsupported shape M=" << M << " N=" << N << " K=" << K);
   const int tiles = (M / kT) * (N / kT);
-  // M-tiles per L2 group of the tile order (DLNB_GEMM_GROUP, experiments)
-  const int group = static_cast<int>(std::max<long long>(1, env_int("DLNB_GEMM_GROUP", 8)));
+  constexpr int group = 8;  // M-tiles per L2 group of the tile order
   hipStream_t st = static_cast<hipStream_t>(stream);
   auto* a = static_cast<const char*>(A);
   auto* b = static_cast<const char*>(B);
   auto* cc = static_cast<__bf16*>(C);
-  // the balanced schedule is unrolled by two K-tiles: even K-tile counts only
-  balanced = balanced && ((static_cast<size_t>(K) * dtype_size(in_t) / kRB) % 2 == 0);
-  if (uniform) {
-    if (in_t == DType::FP8_E4M3) {
-      if (balanced)
-        hipLaunchKernelGGL((gemm_8phase_kernel<true, false, true, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb,
-                           ldc, nullptr, 0u, 0ull, 0ull, nullptr, group);
-      else
-        hipLaunchKernelGGL((gemm_8phase_kernel<true, false, false, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda,
-                           ldb, ldc, nullptr, 0u, 0ull, 0ull, nullptr, group);
-    } else {
-      if (balanced)
-        hipLaunchKernelGGL((gemm_8phase_kernel<false, false, true, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda,
-                           ldb, ldc, nullptr, 0u, 0ull, 0ull, nullptr, group);
-      else
-        hipLaunchKernelGGL((gemm_8phase_kernel<false, false, false, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda,
-                           ldb, ldc, nullptr, 0u, 0ull, 0ull, nullptr, group);
-    }
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) DLNB_THROW("gemm 8-phase launch failed: " << hipGetErrorString(e));
-    return;
-  }
+  const bool even = (static_cast<size_t>(K) * dtype_size(in_t) / kRB) % 2 == 0;
   if (in_t == DType::FP8_E4M3) {
-    if (balanced)
-      hipLaunchKernelGGL((gemm_8phase_kernel<true, false, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc,
-                         nullptr, 0u, 0ull, 0ull, nullptr, group);
-    else
-      hipLaunchKernelGGL((gemm_8phase_kernel<true, false>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc, nullptr,
-                         0u, 0ull, 0ull, nullptr);
+    // fp8: one uniform K-tile body with plain reads (the balanced fp8 build
+    // spills under the buffer_load staging, profiles/gemm_bench_r2.md)
+    hipLaunchKernelGGL((gemm_8phase_kernel<true, false, false, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb,
+                       ldc, nullptr, 0u, 0ull, 0ull, nullptr, group);
+  } else if (even) {
+    // bf16: balanced fragment reads (unrolled by two K-tiles: even counts)
+    hipLaunchKernelGGL((gemm_8phase_kernel<false, false, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc,
+                       nullptr, 0u, 0ull, 0ull, nullptr, group);
   } else {
-    if (balanced)
-      hipLaunchKernelGGL((gemm_8phase_kernel<false, false, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc,
-                         nullptr, 0u, 0ull, 0ull, nullptr, group);
-    else
-      hipLaunchKernelGGL((gemm_8phase_kernel<false, false>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc, nullptr,
-                         0u, 0ull, 0ull, nullptr);
+    hipLaunchKernelGGL((gemm_8phase_kernel<false, false>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc, nullptr,
+                       0u, 0ull, 0ull, nullptr);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 8-phase launch failed: " << hipGetErrorString(e));
@@ -703,41 +679,30 @@ void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N
   auto* a = static_cast<const char*>(A);
   auto* b = static_cast<const char*>(B);
   auto* cc = static_cast<__bf16*>(C);
-  // fp8: the per-tile loop with one uniform K-tile body (no spills): fastest
-  // at every measured K (+7 % at K = 4096, +24 % at the ViT-H FFN's K = 1280
-  // over the loop with tail instantiations, +8 % over the streaming kernel).
-  // bf16, short K (<= 16 K-tiles): the streaming kernel, whose per-tile
-  // pipeline fill / drain savings outweigh its per-phase wait-count branch
-  // only there; long K: the per-tile loop (profiles/gemm_deadline_stream_r2.md).
-  // DLNB_GEMM_STREAM=0|1, DLNB_GEMM_FP8_DL_UNIFORM=0|1 and DLNB_GEMM_BF16_DL_BAL=0|1 force a choice.
+  // Chosen by shape (profiles/gemm_deadline_stream_r2.md, gemm_bench_r2.md):
+  //   bf16, short K (<= 16 K-tiles): the streaming kernel, whose per-tile
+  //     pipeline fill / drain savings outweigh its per-phase wait-count
+  //     branch only there;
+  //   bf16, long K: the per-tile loop, balanced reads when the K-tile count
+  //     is even (236 VGPRs, no spills: 1354 vs 1288 TF/s sustained), plain
+  //     otherwise;
+  //   fp8 (K not a multiple of 256 bytes, else the 4-wave MX kernel runs):
+  //     the per-tile loop with one uniform K-tile body (no spills; +7 % at
+  //     K = 4096, +24 % at the ViT-H FFN's K = 1280 over the tail
+  //     instantiations, +8 % over the streaming kernel).
   const int nk = static_cast<int>(static_cast<size_t>(K) * dtype_size(in_t) / kRB);
-  const long long force = env_int("DLNB_GEMM_STREAM", -1);
-  const bool fp8_uniform = in_t != DType::BF16 && env_int("DLNB_GEMM_FP8_DL_UNIFORM", 1) != 0;
-  const bool stream_on = force >= 0 ? force != 0 : (!fp8_uniform && nk <= 16);
-  if (stream_on) {
-    if (in_t == DType::BF16)
-      hipLaunchKernelGGL((gemm_8phase_stream_kernel<false>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
-                         ticks, slice_end, tstart);
-    else
-      hipLaunchKernelGGL((gemm_8phase_stream_kernel<true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
-                         ticks, slice_end, tstart);
-  } else if (in_t == DType::BF16 && nk % 2 == 0 && env_int("DLNB_GEMM_BF16_DL_BAL", 1) != 0) {
-    // bf16, long K: balanced reads (236 VGPRs, no spills with the buffer_load
-    // staging): 1354 vs 1288 TF/s sustained (scripts/probes/deadline_rate_bal.sh)
+  if (in_t == DType::BF16 && nk <= 16) {
+    hipLaunchKernelGGL((gemm_8phase_stream_kernel<false>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
+                       ticks, slice_end, tstart);
+  } else if (in_t == DType::BF16 && nk % 2 == 0) {
     hipLaunchKernelGGL((gemm_8phase_kernel<false, true, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot,
                        epoch, ticks, slice_end, tstart);
   } else if (in_t == DType::BF16) {
     hipLaunchKernelGGL((gemm_8phase_kernel<false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
                        ticks, slice_end, tstart);
-  } else if (fp8_uniform) {
-    // fp8: one uniform K-tile body (the tail K-tiles stage past the end
-    // instead of their own instantiations): 254 VGPRs, no spills (the
-    // per-tile fp8 deadline kernel with a tail carries 35 spilled VGPRs)
+  } else {
     hipLaunchKernelGGL((gemm_8phase_kernel<true, true, false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot,
                        epoch, ticks, slice_end, tstart);
-  } else {
-    hipLaunchKernelGGL((gemm_8phase_kernel<true, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
-                       ticks, slice_end, tstart);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 8-phase deadline launch failed: " << hipGetErrorString(e));

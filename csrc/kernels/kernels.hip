@@ -412,71 +412,6 @@ __global__ void __launch_bounds__(128 * WN, WN == 4 ? 2 : 1)
 }
 
 
-// Non-deadline GEMM with a deeper A pipeline: A in a ring of 3 K-tiles, B
-// double-buffered (5 x 32 KiB = the whole 160 KiB LDS). Each K-tile issues
-// B(k+1) then A(k+2) (4 + 4 glds per thread) and, after the MFMAs, waits
-// with a COUNTED vmcnt(4) - only A(k+2) may stay in flight - then a raw
-// s_barrier (a __syncthreads() would drain every glds with vmcnt(0),
-// cdna_hip_programming.md §5 "Pipelining across barriers"). A panels get two
-// K-tiles of latency hiding, B panels (shared by the 8 M-tiles of a tile
-// group, so mostly L2 hits) one. Slots written in iteration k held A(k-1) /
-// B(k-1), whose reads every wave finished before the barrier ending k-1.
-template <bool FP8>
-__global__ void __launch_bounds__(512, 1)
-    gemm_tn_ring_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
-                        int K, int lda, int ldb, int ldc) {
-  __shared__ __attribute__((aligned(16))) char smem[5 * kTileBytes];  // A0 A1 A2 | B0 B1
-  char* const Aring = smem;
-  char* const Bring = smem + 3 * kTileBytes;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  constexpr int NW = 8, WN = 4, FN = 4, WTN = 64;
-  const int wm = w / WN, wn = w % WN;
-  const int nt_m = M / kTile, nt_n = N / kTile, T = nt_m * nt_n;
-  const int b = xcd_remap(blockIdx.x, T);
-  constexpr int GROUP = 8;
-  const int per_group = GROUP * nt_n;
-  const int first_m = (b / per_group) * GROUP;
-  const int gsz = min(nt_m - first_m, GROUP);
-  const int tm = first_m + (b % per_group) % gsz;
-  const int tn = (b % per_group) / gsz;
-  constexpr int esz = FP8 ? 1 : 2;
-  const size_t lda_b = static_cast<size_t>(lda) * esz, ldb_b = static_cast<size_t>(ldb) * esz;
-  const char* Ab = A + static_cast<size_t>(tm) * kTile * lda_b;
-  const char* Bb = B + static_cast<size_t>(tn) * kTile * ldb_b;
-  const int nk = (K * esz) / kRowBytes;
-
-  f32x4 acc[8][FN];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  stage_tile<NW>(Ab, lda_b, Aring, w, lane);
-  stage_tile<NW>(Bb, ldb_b, Bring, w, lane);
-  if (nk > 1) {
-    stage_tile<NW>(Ab + kRowBytes, lda_b, Aring + kTileBytes, w, lane);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-
-  const int r16 = lane & 15, h = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk)
-      stage_tile<NW>(Bb + static_cast<size_t>(kt + 1) * kRowBytes, ldb_b, Bring + ((kt + 1) & 1) * kTileBytes, w, lane);
-    if (kt + 2 < nk)
-      stage_tile<NW>(Ab + static_cast<size_t>(kt + 2) * kRowBytes, lda_b, Aring + ((kt + 2) % 3) * kTileBytes, w, lane);
-    ktile_mfma<FP8, false, FN, WTN>(Aring + (kt % 3) * kTileBytes, Bring + (kt & 1) * kTileBytes, acc, wm, wn, r16, h);
-    if (kt + 2 < nk)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-  store_tile<FN, WTN>(C, ldc, tm, tn, wm, wn, r16, h, acc);
-}
-
 // ------------------------------------------------------------- optimizer
 
 __global__ void sgd_momentum_kernel(__bf16* __restrict__ p, __bf16* __restrict__ m, const __bf16* __restrict__ g,
@@ -573,56 +508,27 @@ void launch_gemm(int grid, const void* A, const void* B, void* C, int M, int N, 
                      slice_end, tstart);
 }
 
-bool gemm_ring_enabled() {
-  // Off by default: measured 7 % slower than the double-buffered kernel for
-  // bf16 and +1 % for fp8 (profiles/gemm_bench_r1.md) - the A latency it
-  // hides is not what limits this kernel.
-  static const bool on = env_int("DLNB_GEMM_RING", 0) != 0;
-  return on;
-}
-
+// The 8-wave double-buffered kernel (variant 8): bf16 with software-pipelined
+// fragment reads, fp8 with the plain MX body. The fallback for shapes the
+// 8-phase / 4-wave kernels do not take (a single K-tile).
 template <bool DEADLINE>
-void dispatch_gemm(int waves, DType in_t, int grid, const void* A, const void* B, void* C, int M, int N, int K,
-                   int lda, int ldb, int ldc, uint64_t* slot, uint32_t epoch, uint64_t ticks, uint64_t slice_end,
-                   hipStream_t st, uint64_t* tstart = nullptr) {
+void dispatch_gemm(DType in_t, int grid, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+                   int ldc, uint64_t* slot, uint32_t epoch, uint64_t ticks, uint64_t slice_end, hipStream_t st,
+                   uint64_t* tstart = nullptr) {
   const bool fp8 = in_t == DType::FP8_E4M3;
-  if (!DEADLINE && waves == 4) {  // (the 4-wave deadline variant would spill: never instantiated)
-    if (fp8)
-      launch_gemm<true, false, 2>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
-    else
-      launch_gemm<false, false, 2>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
-  } else if (!DEADLINE && waves == 2 && !fp8) {
+  if (!DEADLINE && !fp8)
     launch_gemm<false, false, 4, true>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
-  } else if (!DEADLINE && waves == 1) {
-    if (fp8)
-      hipLaunchKernelGGL(gemm_tn_ring_kernel<true>, grid, 512, 0, st, static_cast<const char*>(A),
-                         static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc);
-    else
-      hipLaunchKernelGGL(gemm_tn_ring_kernel<false>, grid, 512, 0, st, static_cast<const char*>(A),
-                         static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc);
-  } else {
-    if (fp8)
-      launch_gemm<true, DEADLINE, 4>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st, tstart);
-    else
-      launch_gemm<false, DEADLINE, 4>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st, tstart);
-  }
+  else if (fp8)
+    launch_gemm<true, DEADLINE, 4>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st, tstart);
+  else
+    launch_gemm<false, DEADLINE, 4>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st, tstart);
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace
 
-bool gemm_8phase_enabled() {
-  static const bool on = env_int("DLNB_GEMM_8PHASE", 1) != 0;
-  return on;
-}
-
-int gemm_default_waves() {
-  static const int w = env_int("DLNB_GEMM_WAVES", 8) == 4 ? 4 : 8;
-  return w;
-}
-
 void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
-             void* stream, int waves) {
+             void* stream, int variant) {
   DLNB_REQUIRE(gemm_shape_ok(M, N, K, in_t), "gemm_tn: unsupported shape M=" << M << " N=" << N << " K=" << K << " dtype="
                                                                               << dtype_name(in_t));
   size_t esz = dtype_size(in_t);
@@ -632,39 +538,22 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
   DLNB_REQUIRE(reinterpret_cast<uintptr_t>(A) % 16 == 0 && reinterpret_cast<uintptr_t>(B) % 16 == 0 &&
                    reinterpret_cast<uintptr_t>(C) % 8 == 0,
                "gemm_tn: misaligned base pointers");
+  DLNB_REQUIRE(variant == 0 || variant == 5 || variant == 6 || variant == 8,
+               "gemm_tn: variant must be 0 (default), 5 (4-wave MX, fp8), 6 (8-phase) or 8 (8-wave)");
   const int tiles = (M / kTile) * (N / kTile);
-  DLNB_REQUIRE(waves >= 0 && waves <= 9, "gemm_tn: variant must be 0..9");
-  // fp8 default: the one-wave-per-SIMD MX kernel where it applies (+5-7 % over
-  // the uniform 8-phase kernel, profiles/gemm_bench_r2.md)
-  if (waves == 0 && gemm_8phase_enabled() && gemm_4wave_fp8_shape_ok(M, N, K, in_t)) waves = 5;
-  if (waves == 5) {
-    if (gemm_4wave_shape_ok(M, N, K, in_t)) {
-      gemm_tn_4wave(A, B, C, M, N, K, lda, ldb, ldc, stream);
-      return;
-    }
-    if (gemm_4wave_fp8_shape_ok(M, N, K, in_t)) {
-      gemm_tn_4wave_fp8(A, B, C, M, N, K, lda, ldb, ldc, stream);
-      return;
-    }
-    waves = 0;  // shapes the 4-wave kernels do not take: the default
-  }
-  // bf16: balanced reads; fp8: one uniform K-tile body (no spills; with the
-  // buffer_load staging the balanced fp8 build spills again, profiles/gemm_bench_r2.md)
-  if (waves == 0 && gemm_8phase_enabled()) waves = in_t == DType::BF16 ? 6 : 9;
-  // 7 / 9: the 8-phase kernels (balanced / plain) with one uniform K-tile body
-  if ((waves == 3 || waves == 6 || waves == 7 || waves == 9) && gemm_8phase_shape_ok(M, N, K, in_t)) {
-    gemm_tn_8phase(A, B, C, M, N, K, lda, ldb, ldc, in_t, stream, waves == 6 || waves == 7, waves == 7 || waves == 9);
+  // 0: fp8 the one-wave-per-SIMD MX kernel where it applies (+5-7 % over the
+  // 8-phase one), else the 8-phase kernel where it applies, else 8 waves
+  if (variant == 0)
+    variant = gemm_4wave_fp8_shape_ok(M, N, K, in_t) ? 5 : gemm_8phase_shape_ok(M, N, K, in_t) ? 6 : 8;
+  if (variant == 5 && gemm_4wave_fp8_shape_ok(M, N, K, in_t)) {
+    gemm_tn_4wave_fp8(A, B, C, M, N, K, lda, ldb, ldc, stream);
     return;
   }
-  if (waves == 7 || waves == 9) waves = 3;
-  if (waves == 0) {
-    // bf16: the software-pipelined 8-wave body (+3-6 % over the plain one,
-    // profiles/gemm_bench_r1.md); fp8: the plain MX body.
-    const int w = gemm_default_waves();
-    waves = gemm_ring_enabled() ? 1 : w == 4 ? 4 : in_t == DType::BF16 ? 2 : 8;
+  if ((variant == 5 || variant == 6) && gemm_8phase_shape_ok(M, N, K, in_t)) {
+    gemm_tn_8phase(A, B, C, M, N, K, lda, ldb, ldc, in_t, stream);
+    return;
   }
-  if (waves == 3 || waves == 6) waves = in_t == DType::BF16 ? 2 : 8;
-  dispatch_gemm<false>(waves, in_t, tiles, A, B, C, M, N, K, lda, ldb, ldc, nullptr, 0u, 0ull, 0ull, S(stream));
+  dispatch_gemm<false>(in_t, tiles, A, B, C, M, N, K, lda, ldb, ldc, nullptr, 0u, 0ull, 0ull, S(stream));
 }
 
 void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
@@ -672,17 +561,17 @@ void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K
   if (slice_end == 0) slice_end = ticks;
   DLNB_REQUIRE(gemm_shape_ok(M, N, K, in_t), "gemm_tn_deadline: unsupported shape");
   DLNB_REQUIRE(slot != nullptr && grid > 0 && epoch > 0 && epoch < 65536, "gemm_tn_deadline: bad slot/grid/epoch");
-  // fp8: the one-wave-per-SIMD MX kernel where it applies (DLNB_GEMM_FP8_DL_4WAVE=0: the 8-phase one)
-  if (gemm_8phase_enabled() && gemm_4wave_fp8_shape_ok(M, N, K, in_t) && env_int("DLNB_GEMM_FP8_DL_4WAVE", 1) != 0) {
+  // fp8: the one-wave-per-SIMD MX kernel where it applies (2665 vs ~2180 TF/s sustained)
+  if (gemm_4wave_fp8_shape_ok(M, N, K, in_t)) {
     gemm_tn_4wave_fp8_deadline(A, B, C, M, N, K, ticks, slot, epoch, grid, stream, slice_end, tstart);
     return;
   }
-  if (gemm_8phase_enabled() && gemm_8phase_shape_ok(M, N, K, in_t)) {
+  if (gemm_8phase_shape_ok(M, N, K, in_t)) {
     gemm_tn_8phase_deadline(A, B, C, M, N, K, in_t, ticks, slot, epoch, grid, stream, slice_end, tstart);
     return;
   }
-  // 8 waves: the 4-wave variant spills once the deadline logic is added.
-  dispatch_gemm<true>(8, in_t, grid, A, B, C, M, N, K, K, K, N, slot, epoch, ticks, slice_end, S(stream), tstart);
+  // 8 waves (a single K-tile)
+  dispatch_gemm<true>(in_t, grid, A, B, C, M, N, K, K, K, N, slot, epoch, ticks, slice_end, S(stream), tstart);
 }
 
 void sgd_momentum_bf16(void* param, void* mom, const void* grad, size_t n, float lr, float beta, void* stream) {

@@ -21,6 +21,8 @@ def gemm_tn(a, b, out=None, waves: int = 0):
     rows may be strided (a view of a wider matrix: leading dimension = stride(0)).
     M and N must be multiples of 256; K*elem_size a multiple of 128 bytes;
     rows 16-byte aligned. out (optional) may be row-strided the same way.
+    waves: the kernel variant (csrc/include/dlnb/kernels.hpp): 0 the default,
+    5 one wave per SIMD MX (fp8), 6 8-phase, 8 8-wave double-buffered.
     """
     import torch
     if a.dtype != b.dtype:

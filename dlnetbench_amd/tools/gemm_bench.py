@@ -1,14 +1,14 @@
 """Throughput of the hand-written MFMA GEMM variants vs torch (hipBLASLt) on MI355X.
 
     python -m dlnetbench_amd.tools.gemm_bench [--shapes 8192x14336x4096,...] [--dtype bf16|fp8]
-                                              [--variants 2,3,8]
+                                              [--variants 0,8]
 
 Interleaves the implementations round by round in one process
 (cdna_hip_programming.md §5.4 rule 24) on random [-1, 1) operands (rule 25)
 and prints TFLOP/s (median, best) as JSON lines, one key per variant
-(``v<n>_tflops_*``, n = the ``waves`` selector of ops.gemm.gemm_tn: 8 = double
-buffered, 2 = software-pipelined fragment reads (bf16 default), 1 = 3-deep A
-ring, 4 = 4 waves, 3 = 8-phase ping-pong, 6 = 8-phase with balanced reads) and ``torch_tflops_*``.
+(``v<n>_tflops_*``, n = the variant of ops.gemm.gemm_tn, csrc/include/dlnb/kernels.hpp:
+0 = the default, 5 = one wave per SIMD MX (fp8), 6 = 8-phase, 8 = 8 waves
+double-buffered) and ``torch_tflops_*``.
 """
 from __future__ import annotations
 
@@ -26,7 +26,7 @@ def main(argv=None) -> int:
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--variants", default=None, help="comma list of gemm_tn variants (default: 5,6 bf16; 7,3 fp8)")
+    ap.add_argument("--variants", default=None, help="comma list of gemm_tn variants (default: 0,8 bf16; 0,6 fp8)")
     a = ap.parse_args(argv)
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float8_e4m3fn
     for shp in a.shapes.split(","):
@@ -38,7 +38,7 @@ def main(argv=None) -> int:
         C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         flop = 2.0 * M * N * K
 
-        variants = [int(v) for v in (a.variants or ("5,6" if a.dtype == "bf16" else "7,3")).split(",")]
+        variants = [int(v) for v in (a.variants or ("0,8" if a.dtype == "bf16" else "0,6")).split(",")]
 
         def mk(v):
             return lambda: gemm.gemm_tn(A, B, C, waves=v)

@@ -26,7 +26,8 @@ def assert_close_bf16_out(c, ref):
     assert worst <= 0, f"max excess {worst}, max err {err.max().item()}, rms {ref.pow(2).mean().sqrt().item()}"
 
 
-@pytest.mark.parametrize("waves", [0, 1, 2, 3, 6, 7, 8, 9, 4, 5])
+# gemm_tn variants (kernels.hpp): 0 default, 5 4-wave MX (fp8), 6 8-phase, 8 8-wave
+@pytest.mark.parametrize("waves", [0, 8])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 512, 128), (512, 512, 64), (768, 256, 128),
                                    (512, 256, 1024), (768, 1280, 640), (2048, 1024, 4096), (256, 256, 192),
                                    (512, 768, 320)])
@@ -39,7 +40,7 @@ def test_gemm_bf16_matches_torch(M, N, K, waves):
     assert_close_bf16_out(c, a.float() @ b.float().t())
 
 
-@pytest.mark.parametrize("waves", [0, 3, 6, 5])
+@pytest.mark.parametrize("waves", [0, 8])
 def test_gemm_bf16_identity_asymmetric(waves):
     # A = I picks rows of B: catches any row/column/quadrant swap in the C write.
     M = N = 256
@@ -52,9 +53,9 @@ def test_gemm_bf16_identity_asymmetric(waves):
 
 
 @pytest.mark.skipif(not hasattr(torch, "float8_e4m3fn"), reason="torch without float8")
-@pytest.mark.parametrize("waves", [0, 1, 2, 3, 6, 7, 8, 9, 4, 5])
+@pytest.mark.parametrize("waves", [0, 6])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 128), (512, 256, 128), (256, 512, 256), (512, 768, 512),
-                                   (1024, 512, 2048)])
+                                   (1024, 512, 2048), (512, 512, 384)])
 def test_gemm_fp8_matches_torch(M, N, K, waves):
     g = torch.Generator(device="cuda").manual_seed(7 + M)
     a = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(torch.float8_e4m3fn)
@@ -65,13 +66,11 @@ def test_gemm_fp8_matches_torch(M, N, K, waves):
 
 
 @pytest.mark.skipif(not hasattr(torch, "float8_e4m3fn"), reason="torch without float8")
-@pytest.mark.parametrize("stream", ["0", "1"])
 @pytest.mark.parametrize("M,N,K", [(4096, 4352, 512), (8192, 8192, 256), (2048, 8448, 1280)])
-def test_gemm_fp8_many_tiles(M, N, K, stream, monkeypatch):
-    """More tiles than CUs: the one-wave-per-SIMD fp8 kernel one block per tile (stream 0) and as the
-    streaming persistent kernel (stream 1: a block's tiles as one K-tile stream, the next tile's first
-    K-tiles staged during the current one's last, K = 256 the 2-K-tile minimum)."""
-    monkeypatch.setenv("DLNB_GEMM_FP8_STREAM", stream)
+def test_gemm_fp8_many_tiles(M, N, K):
+    """More tiles than CUs: the one-wave-per-SIMD fp8 kernel runs as the streaming persistent kernel (a
+    block's tiles as one K-tile stream, the next tile's first K-tiles staged during the current one's
+    last, K = 256 the 2-K-tile minimum); fewer tiles (test_gemm_fp8_matches_torch) a block per tile."""
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     a = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(torch.float8_e4m3fn)
     b = (torch.randn(N, K, device="cuda", generator=g) * 0.5).to(torch.float8_e4m3fn)
@@ -80,7 +79,7 @@ def test_gemm_fp8_many_tiles(M, N, K, stream, monkeypatch):
     assert_close_bf16_out(c, a.float() @ b.float().t())
 
 
-@pytest.mark.parametrize("dtype,waves", [("bf16", 0), ("bf16", 5), ("bf16", 3), ("fp8", 0), ("fp8", 5), ("fp8", 9)])
+@pytest.mark.parametrize("dtype,waves", [("bf16", 0), ("bf16", 8), ("fp8", 0), ("fp8", 6), ("fp8", 8)])
 def test_gemm_strided_operands(dtype, waves):
     """Row-strided A, B and C (views of wider matrices: leading dimensions > K, > N): the staging lane
     offsets and buffer resources use the leading dimensions, not K."""
@@ -171,20 +170,28 @@ def test_deadline_gemm_duration(us, dtype):
     assert us / 1e3 <= ms * 1.01 and ms <= us / 1e3 * 1.05 + 0.03, (us, times)
 
 
-@pytest.mark.parametrize("dtype,alt", [("bf16", "0"), ("bf16", "1"), ("fp8", "0"), ("fp8", "1"), ("fp8", "2")])
-@pytest.mark.parametrize("M,N,K,grid", [(1024, 768, 512, 3), (512, 512, 256, 1), (256, 256, 256, 2),
-                                        (768, 512, 1280, 0)])
-def test_deadline_gemm_numerics(M, N, K, grid, dtype, alt, monkeypatch):
-    """The persistent deadline GEMM (the bench's compute), every kernel: bf16 the per-tile 8-phase loop
-    (alt 0) and the streaming one that runs a block's tiles as one K-tile stream (alt 1: the next
-    tile's first K-tiles are staged while the current one finishes); fp8 the one-wave-per-SIMD MX
-    kernel (alt 0) and the 8-phase one (alt 1). With a deadline long enough for several passes every
-    tile of C holds a complete product: each one equals A.B^T. Small grids make every block cross many
-    tile boundaries (grid 0 = the default, CUs - 32). alt 2: fp8 the streaming one-wave-per-SIMD
-    deadline kernel (a block's tiles as one K-tile stream)."""
-    monkeypatch.setenv("DLNB_GEMM_STREAM", alt if dtype == "bf16" else "0")
-    monkeypatch.setenv("DLNB_GEMM_FP8_DL_4WAVE", "0" if alt == "1" else "1")
-    monkeypatch.setenv("DLNB_GEMM_FP8_DL_STREAM", "1" if alt == "2" else "0")
+# (dtype, M, N, K, grid) -> the deadline kernel the shape selects (kernels.hip gemm_tn_deadline)
+DEADLINE_CASES = [
+    ("bf16", 1024, 768, 512, 3),   # <= 16 K-tiles: the streaming 8-phase kernel
+    ("bf16", 512, 512, 256, 1),
+    ("bf16", 256, 256, 256, 2),
+    ("bf16", 768, 512, 1280, 0),   # 20 K-tiles: the per-tile loop, balanced reads
+    ("bf16", 512, 512, 1216, 2),   # 19 K-tiles (odd): the per-tile loop, plain reads
+    ("bf16", 256, 512, 64, 2),     # 1 K-tile: the 8-wave kernel
+    ("fp8", 1024, 768, 512, 3),    # K % 256 == 0: the one-wave-per-SIMD MX kernel
+    ("fp8", 512, 512, 256, 1),
+    ("fp8", 768, 512, 1280, 0),
+    ("fp8", 512, 768, 384, 2),     # K % 256 != 0: the 8-phase kernel, uniform K-tile body
+    ("fp8", 768, 512, 640, 0),
+    ("fp8", 256, 512, 128, 2),     # 1 K-tile: the 8-wave kernel
+]
+
+
+@pytest.mark.parametrize("dtype,M,N,K,grid", DEADLINE_CASES)
+def test_deadline_gemm_numerics(M, N, K, grid, dtype):
+    """The persistent deadline GEMM (the bench's compute), every kernel the shapes select. With a deadline
+    long enough for several passes every tile of C holds a complete product: each one equals A.B^T.
+    Small grids make every block cross many tile boundaries (grid 0 = the default, CUs - 32)."""
     if dtype == "fp8" and not hasattr(torch, "float8_e4m3fn"):
         pytest.skip("torch without float8")
     g = torch.Generator(device="cuda").manual_seed(M * 3 + N + K)
