@@ -9,8 +9,11 @@ stdout works as is. Rows are sorted by ``n_gpus``. Columns: the headline
 iteration and its weak-scaling efficiency against the smallest N
 (T_min / T_N; the headline keeps per-GPU work fixed), the headline's
 all-gather / reduce-scatter bus bandwidth, and the secondary blocks when
-present: the comm-bound ViT-H DP step (RCCL, RCCL without the CTA cap, our
-xgmi kernels) and the headline FSDP step over xgmi as a busbw ratio to RCCL.
+present: the comm-bound ViT-H DP step (RCCL, RCCL without the CTA cap,
+geometric buckets, our xgmi kernels), the headline FSDP step over xgmi as a
+busbw ratio to RCCL, the multi-rank exactness verdict (RCCL / xgmi, the xgmi
+release mode that passed) with RCCL's own rank count, and the N = 8 hybrid
+configs (C3 hybrid_3d, C4 hybrid_3d_moe) against their GPipe floors.
 
 Reference equivalent: the scaling plots of plots/plot_dp.py:80-145 start
 from the per-run DataFrame; this is the same view for the bench contract's
@@ -77,10 +80,19 @@ def rows(lines: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
             "c5_ms": _get(d, "comm_bound", "ms_per_step"),
             "c5_busbw_GBps": _get(d, "comm_bound", "allreduce_busbw_GBps"),
             "c5_uncapped_ms": _get(d, "comm_bound", "rccl_default_ctas", "ms_per_step"),
+            "c5_geometric_ms": _get(d, "comm_bound", "geometric_buckets", "ms_per_step"),
             "c5_xgmi_ms": _get(d, "comm_bound_xgmi", "ms_per_step"),
             "c5_xgmi_speedup": _get(d, "comm_bound_xgmi", "speedup_vs_comm_bound"),
             "fsdp_xgmi_ag_ratio": _get(d, "headline_xgmi", "busbw_ratio_vs_headline", "allgather"),
             "fsdp_xgmi_rs_ratio": _get(d, "headline_xgmi", "busbw_ratio_vs_headline", "reduce_scatter"),
+            "exact_rccl": _get(d, "exact", "rccl"),
+            "exact_xgmi": _get(d, "exact", "xgmi"),
+            "xgmi_release": _get(d, "exact_detail", "xgmi_release"),
+            "rccl_nranks": max((d.get("rccl_nranks") or {}).values(), default=None),
+            "c3_ms": _get(d, "hybrid_3d", "ms_per_step"),
+            "c3_vs_floor": _get(d, "hybrid_3d", "vs_floor"),
+            "c4_ms": _get(d, "hybrid_3d_moe", "ms_per_step"),
+            "c4_vs_floor": _get(d, "hybrid_3d_moe", "vs_floor"),
         }
         out.append(r)
     return out

@@ -56,3 +56,18 @@ def test_no_lines_is_an_error(tmp_path):
     p = tmp_path / "empty.txt"
     p.write_text("nothing here\n")
     assert bench_report.main([str(p)]) == 1
+
+
+def test_exactness_and_hybrid_columns():
+    d = json.loads(_line(8, 2816.0, ag=300.0, c5=7.4))
+    d["comm_bound"]["geometric_buckets"] = {"ms_per_step": 7.25}
+    d["exact"] = {"rccl": True, "xgmi": False, "rccl_eager": True}
+    d["exact_detail"] = {"xgmi_release": None}
+    d["rccl_nranks"] = {"fsdp/unit/0": 8}
+    d["hybrid_3d"] = {"ms_per_step": 3900.0, "vs_floor": 1.02}
+    d["hybrid_3d_moe"] = {"ms_per_step": 15000.0, "vs_floor": 1.1}
+    r = bench_report.rows([d])[0]
+    assert r["c5_geometric_ms"] == 7.25 and r["exact_rccl"] is True and r["exact_xgmi"] is False
+    assert r["rccl_nranks"] == 8 and r["c3_vs_floor"] == 1.02 and r["c4_ms"] == 15000.0
+    r1 = bench_report.rows([json.loads(_line(1, 2816.0))])[0]
+    assert r1["exact_rccl"] is None and r1["rccl_nranks"] is None and r1["c3_ms"] is None
