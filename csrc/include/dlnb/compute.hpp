@@ -38,8 +38,8 @@ ComputeMode parse_compute_mode(const std::string& s, DeviceKind dev);
 const char* compute_mode_name(ComputeMode m);
 
 struct ComputeShape {
-  int hidden = 4096;  // model hidden size (K of the stand-in GEMM)
-  int ffn = 16384;    // FFN width (N)
+  int hidden = 4096;  // model hidden size (N of the stand-in GEMM: the FFN down projection)
+  int ffn = 16384;    // FFN width (K)
   DType dtype = DType::BF16;
   int comm_cus = 32;  // CUs the persistent compute leaves to collectives
 };

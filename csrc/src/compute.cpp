@@ -80,9 +80,17 @@ class GpuCompute : public ComputeEngine {
     hz_ = kernels::wallclock_hz(dev.index());
     cus_ = kernels::num_cus(dev.index());
     dtype_ = shape.dtype == DType::FP8_E4M3 ? DType::FP8_E4M3 : DType::BF16;
-    const int kmul = dtype_ == DType::FP8_E4M3 ? 128 : 64;
-    K_ = std::max(512, (shape.hidden + kmul - 1) / kmul * kmul);
-    N_ = std::min(32768, std::max(1024, (shape.ffn + 255) / 256 * 256));
+    // The stand-in is the layer's FFN down projection, C[tokens, hidden] =
+    // A[tokens, ffn] . W[hidden, ffn]^T: its long K (the FFN width) keeps
+    // the per-tile pipeline fill / drain of the persistent kernel small. At
+    // the up-projection shape used before (K = hidden) the deadline kernel did
+    // 0.725 -> 0.787 less MFMA busy per clock on its CUs (bf16 llama3_8b) and
+    // 1810 vs 2672 TF/s (fp8 ViT-H, K = 1280) (profiles/deadline_shapes_r3.md).
+    // K: a multiple of 128 (bf16: an even K-tile count, the balanced body) or
+    // 256 bytes (fp8: the one-wave-per-SIMD MX kernel).
+    const int kmul = dtype_ == DType::FP8_E4M3 ? 256 : 128;
+    K_ = std::min(65536, std::max(512, (shape.ffn + kmul - 1) / kmul * kmul));
+    N_ = std::min(32768, std::max(1024, (shape.hidden + 255) / 256 * 256));
     if (mode_ != ComputeMode::Sleep && mode_ != ComputeMode::Spin) calibrate();
     if (mode_ == ComputeMode::Gemm) {
       slots_ = dev_.alloc(kSlots * 64);

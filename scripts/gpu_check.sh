@@ -21,6 +21,7 @@ for step in "$@"; do
     pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 170 --timeout-method thread ;;
     loopback) run loopback_gpu 600 python -u -m pytest tests/test_gpu_strategies.py -m gpu -v -k loopback -p no:cacheprovider --timeout 170 --timeout-method thread ;;
     bench) run bench 300 python bench.py --steps 3 --warmup 1 --json gpurun_out/bench_report.json ;;
+    benchdriver) run bench_driver 400 python bench.py --steps 20 --warmup 5 --json gpurun_out/bench_driver_report.json ;;
     clock) run clock 120 python -m dlnetbench_amd.tools.clock_check ;;
     hwmon) run hwmon 30 bash -c "ls -la /sys/class/drm/card*/device/hwmon/hwmon*/ | head -80" ;;
     benchvariants)

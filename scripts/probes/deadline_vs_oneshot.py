@@ -1,7 +1,7 @@
 """Workload for a PMC comparison of the bf16 deadline GEMM (the headline's
 compute) with the one-shot kernel of the same shape.
 
-    python3 scripts/probes/deadline_vs_oneshot.py oneshot|deadline [M N K]
+    python3 scripts/probes/deadline_vs_oneshot.py oneshot|deadline [M N K [bf16|fp8]]
 
 oneshot: 10 back-to-back gemm_tn launches (variant 0, all CUs);
 deadline: 5 x 20-ms persistent deadline launches on CUs - 32 (the bench's grid).
@@ -16,10 +16,13 @@ from dlnetbench_amd.ops import gemm  # noqa: E402
 
 mode = sys.argv[1]
 M, N, K = (int(x) for x in sys.argv[2:5]) if len(sys.argv) > 4 else (8192, 14336, 4096)
+fp8 = len(sys.argv) > 5 and sys.argv[5] == "fp8"
 a = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
 b = torch.empty(N, K, device="cuda", dtype=torch.bfloat16)
 gemm.fill_random_(a, 1)
 gemm.fill_random_(b, 2)
+if fp8:
+    a, b = a.to(torch.float8_e4m3fn), b.to(torch.float8_e4m3fn)
 c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 if mode == "oneshot":
     for _ in range(10):
