@@ -74,8 +74,8 @@ def test_rccl_single_rank_exact():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("w,dtype", [(1, "bf16"), (2, "bf16"), (2, "fp32"), (2, "fp8_e4m3"), (4, "bf16"),
-                                     (4, "fp16"), (3, "bf16")])
+# (2 ranks, bf16 and fp8 at default windows: test_xgmi_exactness_suite_two_ranks_one_gpu)
+@pytest.mark.parametrize("w,dtype", [(2, "bf16"), (2, "fp32"), (4, "fp16"), (3, "bf16")])
 def test_xgmi_kernels_exact(w, dtype):
     _need_gpu()
     devs = ",".join(["0"] * w)
@@ -85,7 +85,7 @@ def test_xgmi_kernels_exact(w, dtype):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("w,dtype", [(2, "bf16"), (4, "bf16"), (3, "fp32")])
+@pytest.mark.parametrize("w,dtype", [(4, "bf16"), (3, "fp32")])
 def test_xgmi_graph_replay_exact(w, dtype):
     """The collectives and a ring send/recv captured into one HIP graph and replayed 3 times with new
     inputs: the kernels take their epochs / message numbers from device counters, so every replay must
@@ -98,8 +98,7 @@ def test_xgmi_graph_replay_exact(w, dtype):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("w,dtype,graph", [(2, "bf16", False), (4, "bf16", False), (3, "fp32", False),
-                                           (2, "fp8_e4m3", False), (2, "bf16", True), (4, "fp16", True)])
+@pytest.mark.parametrize("w,dtype,graph", [(4, "bf16", False), (3, "fp32", False), (4, "fp16", True)])
 def test_xgmi_registered_zero_copy_exact(w, dtype, graph):
     """--registered: peer-memory buffers registered with the communicator, so all-gather writes straight
     into every rank's receive buffer, reduce-scatter reads straight out of every rank's send buffer and the
@@ -184,16 +183,12 @@ def test_xgmi_bench_runs():
 
 
 XGMI_STRATS = [  # strategy, model, positional args, extra flags, ranks
-    ("dp", "tiny_dense_8_bfloat16", ["2"], [], 2),
+    # (2-rank dp / fsdp / hybrid_2d: the graph-replayed, mixed-backend and torchrun bench tests)
     ("dp", "tiny_dense_8_bfloat16", ["4"], [], 8),
-    ("fsdp", "tiny_dense_8_bfloat16", ["4", "2"], [], 2),
     ("fsdp", "tiny_dense_8_bfloat16", ["4", "2"], [], 4),
     ("fsdp", "tiny_dense_8_bfloat16", ["4", "8"], [], 8),
-    ("hybrid_2d", "tiny_dense_8_bfloat16", ["2", "4"], [], 2),
     ("hybrid_2d", "tiny_dense_8_bfloat16", ["4", "8"], ["--pp-schedule", "1f1b"], 4),
-    ("hybrid_3d", "tiny_dense_8_bfloat16", ["2", "2", "2"], [], 4),
     ("hybrid_3d", "tiny_dense_8_bfloat16", ["2", "4", "2"], ["--pp-schedule", "1f1b"], 8),
-    ("hybrid_3d_moe", "tiny_moe_8_bfloat16", ["1", "2", "2"], [], 2),
     ("hybrid_3d_moe", "tiny_moe_8_bfloat16", ["2", "4", "2"], ["--pp-schedule", "1f1b", "--ep-overlap"], 4),
     ("dp", "tiny_dense_8_bfloat16", ["4"], ["--zero", "2"], 4),
     ("hybrid_cp", "tiny_dense_8_bfloat16", ["2"], [], 4),

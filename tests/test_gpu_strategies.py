@@ -30,8 +30,11 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("strategy,model,params", CASES)
-@pytest.mark.parametrize("compute", ["gemm", "sleep"])
+# every strategy with the MFMA compute; idle-wait compute for one case of each family
+RUNS = [(*c, "gemm") for c in CASES] + [(*c, "sleep") for c in CASES if c[0] in ("fsdp", "hybrid_3d_moe")]
+
+
+@pytest.mark.parametrize("strategy,model,params,compute", RUNS)
 def test_strategy_runs_on_gpu(strategy, model, params, compute, data_dir):
     doc = engine.run_native(strategy, model, *params, base_path=data_dir, warmup=1, runs=2, compute=compute,
                      backend="rccl", quiet=True)
@@ -95,7 +98,9 @@ def test_dp_zero_on_gpu(zero, data_dir):
 
 
 # ---- loopback: N ranks as threads of this process, all on the one MI355X
-# (comm_loopback.cpp; collectives = the multi-source reduce kernel of xgmi.hip)
+# (comm_loopback.cpp; collectives = the multi-source reduce kernel of xgmi.hip).
+# No RCCL is involved, so these run in-process (engine.run): no per-test
+# process start and HIP initialisation.
 
 LOOPBACK_CASES = [
     ("dp", "tiny_dense_8_bfloat16", (4,), 4),
@@ -110,7 +115,7 @@ LOOPBACK_CASES = [
 
 
 def test_dualpipe_loopback_on_gpu(data_dir):
-    doc = engine.run_native("hybrid_2d", "tiny_deep_8_bfloat16", 4, 8, base_path=data_dir, warmup=1, runs=2,
+    doc = engine.run("hybrid_2d", "tiny_deep_8_bfloat16", 4, 8, base_path=data_dir, warmup=1, runs=2,
                      compute="gemm", backend="loopback", ranks=4, pp_schedule="dualpipe", quiet=True)
     g = doc["global"]
     assert g["pp_schedule"] == "dualpipe" and len(doc["ranks"]) == 4
@@ -118,7 +123,7 @@ def test_dualpipe_loopback_on_gpu(data_dir):
 
 
 def test_moe_expert_imbalance_loopback_on_gpu(data_dir):
-    doc = engine.run_native("hybrid_3d_moe", "tiny_moe_8_bfloat16", 1, 2, 4, base_path=data_dir, warmup=1, runs=2,
+    doc = engine.run("hybrid_3d_moe", "tiny_moe_8_bfloat16", 1, 2, 4, base_path=data_dir, warmup=1, runs=2,
                      compute="gemm", backend="loopback", ranks=4, ep_imbalance=1.0, quiet=True)
     per = doc["global"]["ep_dispatch_bytes_per_peer"]
     assert len(per) == 4 and per[0] > per[-1]
@@ -126,7 +131,7 @@ def test_moe_expert_imbalance_loopback_on_gpu(data_dir):
 
 @pytest.mark.parametrize("strategy,model,params,w", LOOPBACK_CASES)
 def test_strategy_loopback_on_gpu(strategy, model, params, w, data_dir):
-    doc = engine.run_native(strategy, model, *params, base_path=data_dir, warmup=1, runs=2, compute="gemm",
+    doc = engine.run(strategy, model, *params, base_path=data_dir, warmup=1, runs=2, compute="gemm",
                      backend="loopback", ranks=w, quiet=True)
     g = doc["global"]
     assert g["backend"] == "LOOPBACK" and g["device"] == "GPU" and g["world_size"] == w
@@ -151,7 +156,7 @@ def test_commtest_loopback_on_gpu(root):
 def test_fsdp_llama3_8b_loopback_8_ranks_one_gpu(root):
     """The bench config at W=8 as 8 rank threads on one MI355X: full-size FSDP
     collectives (per-rank shards of 1/8), compute time scaled down 50x."""
-    doc = engine.run_native("fsdp", "llama3_8b_16_bfloat16", 32, 8, base_path=root, warmup=1, runs=1,
+    doc = engine.run("fsdp", "llama3_8b_16_bfloat16", 32, 8, base_path=root, warmup=1, runs=1,
                      compute="gemm", backend="loopback", ranks=8, time_scale=0.02, quiet=True)
     g = doc["global"]
     assert g["world_size"] == 8 and g["sharding_factor"] == 8 and len(doc["ranks"]) == 8
