@@ -204,15 +204,22 @@ __device__ __forceinline__ bool phase(const Ctx& c, int v, AF& fa, BF& b0r, BF& 
     // latency does not stall wave 0 in front of a barrier
     if constexpr (DL) now = __builtin_amdgcn_s_memrealtime();
   } else {
+    // The flag write comes first: wave 0 then has no LDS read in flight (phase
+    // 2's fragments were consumed by its MFMAs), so the lgkmcnt(0) that
+    // completes the write (and the clock read of phase 2) costs the write's
+    // own latency only. After the BAL reads below it waited for those 4
+    // ds_reads too, once per K-tile in front of the barrier every wave waits
+    // at: 27.6 % of wave time waiting vs 20.8 % for the one-shot kernel
+    // (profiles/deadline_shapes_r3.md).
+    if constexpr (DL) {
+      if (d.tid == 0) {
+        const uint64_t el = (now - d.t0) & ((1ull << 48) - 1);
+        d.flag[v & 1] = el >= d.ticks || el >= d.slice_end;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    }
     if constexpr (BAL) {
       if (has_next) read_frags<FP8, 2>(c.smem + ((v + 1) & 1) * kBuf + kB0 * kHalf, c.wc * 32, c.r16, c.h, b1r);
-    }
-    if constexpr (DL) {
-    if (d.tid == 0) {
-      const uint64_t el = (now - d.t0) & ((1ull << 48) - 1);
-      d.flag[v & 1] = el >= d.ticks || el >= d.slice_end;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
     }
   }
   if constexpr (STAGE) {
