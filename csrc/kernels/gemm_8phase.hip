@@ -160,7 +160,7 @@ __device__ __forceinline__ void stage(const Ctx& c, int t, int slot) {
 }
 
 // Deadline state of the persistent variant: thread 0 (wave row 0) reads the
-// clock in phase 2 of every K-tile, writes the stop
+// clock at the end of phase 2 of every K-tile, writes the stop
 // decision in phase 3 into an LDS flag
 // (completed before its barrier), and every wave reads it after its own first
 // barrier of that phase - the write precedes every read (the rows are one
@@ -200,9 +200,6 @@ __device__ __forceinline__ bool phase(const Ctx& c, int v, AF& fa, BF& b0r, BF& 
     read_frags<FP8, 2>(cur + kB1 * kHalf, c.wc * 32, c.r16, c.h, b1r);
   } else if constexpr (Q == 2) {
     read_frags<FP8, 4>(cur + kA1 * kHalf, c.wr * 64, c.r16, c.h, fa);
-    // the clock is read one phase before its use, so its (scalar-memory)
-    // latency does not stall wave 0 in front of a barrier
-    if constexpr (DL) now = __builtin_amdgcn_s_memrealtime();
   } else {
     // The flag write comes first: wave 0 then has no LDS read in flight (phase
     // 2's fragments were consumed by its MFMAs), so the lgkmcnt(0) that
@@ -230,14 +227,29 @@ __device__ __forceinline__ bool phase(const Ctx& c, int v, AF& fa, BF& b0r, BF& 
   }
   wait_vm<VM>();
   raw_barrier();
-  bool stop = false;
-  if constexpr (DL && Q == 3) stop = __builtin_amdgcn_readfirstlane(d.flag[v & 1]) != 0;
+  // The stop flag is loaded right after the barrier but used only after the
+  // MFMA cluster: its LDS latency (and the wait for the prefetch reads issued
+  // before the barrier, which the same lgkmcnt covers) hides behind the
+  // MFMAs instead of delaying their start once per K-tile.
+  int flag = 0;
+  if constexpr (DL && Q == 3) flag = d.flag[v & 1];
+  __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_setprio(1);
   if constexpr (Q == 0) mfma_quadrant(acc[0][0], fa, b0r);
   if constexpr (Q == 1) mfma_quadrant(acc[0][1], fa, b1r);
   if constexpr (Q == 2) mfma_quadrant(acc[1][1], fa, b1r);
   if constexpr (Q == 3) mfma_quadrant(acc[1][0], fa, b0r);
   __builtin_amdgcn_s_setprio(0);
+  __builtin_amdgcn_sched_barrier(0);
+  // The clock is read at the END of phase 2, once its MFMAs are issued: a
+  // scalar-memory read in flight forces every LDS wait behind it to
+  // lgkmcnt(0) (they complete out of order), and read at the start of phase 2
+  // it made the whole A1 fragment read complete before the phase's first
+  // MFMA. Consumed by wave 0 at the start of phase 3 (its latency hides
+  // behind the barrier between).
+  if constexpr (DL && Q == 2) now = __builtin_amdgcn_s_memrealtime();
+  bool stop = false;
+  if constexpr (DL && Q == 3) stop = __builtin_amdgcn_readfirstlane(flag) != 0;
   raw_barrier();
   return stop;
 }
