@@ -150,7 +150,10 @@ uint16_t float_to_fp16(float f) {
 }
 
 // OCP FP8 e4m3fn: bias 7, no infinities, 0x7f/0xff are NaN, max 448.
-float fp8e4m3_to_float(uint8_t v) {
+// Decoded through a 256-entry table (the host checks of commtest / the shm
+// backend decode millions of elements).
+namespace {
+float fp8e4m3_decode_slow(uint8_t v) {
   int sign = (v >> 7) & 1;
   int exp = (v >> 3) & 0xf;
   int man = v & 7;
@@ -162,24 +165,37 @@ float fp8e4m3_to_float(uint8_t v) {
     r = std::ldexp(1.0f + static_cast<float>(man) / 8.0f, exp - 7);
   return sign ? -r : r;
 }
+struct Fp8e4m3Table {
+  float v[256];
+  Fp8e4m3Table() {
+    for (int c = 0; c < 256; ++c) v[c] = fp8e4m3_decode_slow(static_cast<uint8_t>(c));
+  }
+};
+}  // namespace
 
+float fp8e4m3_to_float(uint8_t v) {
+  static const Fp8e4m3Table t;
+  return t.v[v];
+}
+
+// Round to nearest, ties to even, saturating at +-448 (the conversion the
+// gfx950 cvt instructions do with saturation on).
 uint8_t float_to_fp8e4m3(float f) {
   if (std::isnan(f)) return 0x7f;
   uint8_t sign = std::signbit(f) ? 0x80 : 0;
   float a = std::fabs(f);
   if (a >= 448.0f) return sign | 0x7e;  // saturate to max finite
-  // brute-force nearest (ties to even) over the 127 non-negative codes
-  uint8_t best = 0;
-  float bestd = a;
-  for (int c = 1; c <= 0x7e; ++c) {
-    float v = fp8e4m3_to_float(static_cast<uint8_t>(c));
-    float d = std::fabs(v - a);
-    if (d < bestd || (d == bestd && (c & 1) == 0)) {
-      bestd = d;
-      best = static_cast<uint8_t>(c);
-    }
+  if (a < 0.015625f) {
+    // subnormal range (below 2^-6): code = round(a / 2^-9); 8 is the
+    // smallest normal (exponent 1, mantissa 0), which the same code denotes
+    return sign | static_cast<uint8_t>(std::nearbyint(a * 512.0f));
   }
-  return sign | best;
+  uint32_t u;
+  std::memcpy(&u, &a, 4);
+  // keep 3 mantissa bits, round to nearest even (a carry bumps the exponent)
+  u += 0x7ffffu + ((u >> 20) & 1u);
+  uint32_t code = (u >> 20) - ((127u - 7u) << 3);
+  return sign | static_cast<uint8_t>(std::min<uint32_t>(code, 0x7e));
 }
 
 // OCP FP8 e5m2: bias 15, IEEE-like with inf/NaN.
