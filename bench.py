@@ -210,22 +210,45 @@ def _exact_block(a: argparse.Namespace, world: int, rank: int) -> Dict[str, Any]
     return res
 
 
+def _predicted_ms(a: argparse.Namespace, world: int, strategy: str, model: str, params: tuple,
+                  **kw: Any) -> Optional[float]:
+    """The xGMI cost model's iteration time for this run (parallel/plan.py
+    predict: direct all-link collectives at 75 % of 153 GB/s per link, 15 us
+    each): what the measured value should land near on an 8 x MI355X node.
+    None when compute is time-scaled or the model has no prediction."""
+    if a.time_scale is not None:
+        return None
+    try:
+        from dlnetbench_amd.parallel.plan import predict
+        return round(predict(strategy, model, list(params), world, base=a.base_path, **kw)["iter_ms"], 3)
+    except Exception:  # noqa: BLE001
+        return None
+
+
 def _hybrid_block(a: argparse.Namespace, world: int, rank: int, tag: str, strategy: str, model: str,
-                  params: tuple, floor_note: str) -> Dict[str, Any]:
+                  params: tuple, floor_note: str, ep_overlap: bool = False) -> Dict[str, Any]:
     """One BASELINE hybrid config (C3 hybrid_3d / C4 hybrid_3d_moe) on the job's
     GPUs over RCCL: 1 warm-up + 1 timed iteration in a child process, its
-    time against the GPipe compute floor and its per-group communication."""
+    time against the GPipe compute floor and the xGMI model's prediction, and
+    its per-group communication. ep_overlap: the same config with
+    --ep-overlap (each half-microbatch's all-to-all under the other half's
+    compute instead of on the compute stream)."""
     res: Dict[str, Any] = {"model": model, "strategy": strategy, "params": list(params), "backend": "RCCL"}
+    if ep_overlap:
+        res["ep_overlap"] = True
     try:
         d = _child_run(a, world, rank, tag, strategy, model, params, a.hybrid_timeout, backend=a.hybrid_backend,
-                       graph=False, compute=a.compute, warmup=1, runs=1)
+                       graph=False, compute=a.compute, warmup=1, runs=1, ep_overlap=ep_overlap or None)
         if rank != 0:
             return res
         g, it = d["global"], d["global"]["dlnb"]["iteration"]
+        pred = _predicted_ms(a, world, strategy, model, params, ep_overlap=ep_overlap)
         res.update({"ms_per_step": round(it["timed_ms_per_iter"], 3), "median_ms": round(it["median_ms"], 3),
                     "floor_ms": round(it["compute_floor_ms"], 3), "floor_note": floor_note,
                     "vs_floor": round(it["timed_ms_per_iter"] / it["compute_floor_ms"], 4)
                     if it["compute_floor_ms"] else None,
+                    "predicted_ms": pred,
+                    "vs_predicted": round(it["timed_ms_per_iter"] / pred, 4) if pred else None,
                     "backend": g["backend"], "rccl_nranks": g["dlnb"].get("rccl_nranks")})
         for k in ("pp_comm_time", "dp_comm_time", "tp_comm_time", "ep_comm_time", "dp_ep_comm_time"):
             v = _mean_of(d, k)
@@ -333,6 +356,8 @@ def main() -> int:
     ap.add_argument("--c4-model", default=C4_MODEL)
     ap.add_argument("--c4", default=C4_PARAMS, help="hybrid_3d_moe num_stages,num_microbatches,num_expert_shards")
     ap.add_argument("--hybrid-timeout", type=float, default=150.0)
+    ap.add_argument("--c4-ep-overlap", choices=["on", "off"], default="on",
+                    help="also run C4 with --ep-overlap (the all-to-alls off the compute stream)")
     ap.add_argument("--json", default=None, help="also write the full headline report here (rank 0)")
     a = ap.parse_args()
     a.hybrid_backend = "rccl" if a.backend == "auto" else a.backend
@@ -472,6 +497,12 @@ def main() -> int:
                                            "GPipe (mb + S - 1)(f_mb + b_mb), BASELINE.md C3")
         extra["hybrid_3d_moe"] = _hybrid_block(a, world, rank, ".c4", "hybrid_3d_moe", a.c4_model, c4,
                                                "GPipe (mb + S - 1)(f_mb + b_mb), BASELINE.md C4")
+        if a.c4_ep_overlap == "on":
+            # the MI355X-side schedule for the same config: the 1,024
+            # all-to-alls per iteration leave the compute stream
+            extra["hybrid_3d_moe"]["ep_overlap"] = _hybrid_block(
+                a, world, rank, ".c4o", "hybrid_3d_moe", a.c4_model, c4,
+                "GPipe (mb + S - 1)(f_mb + b_mb), BASELINE.md C4", ep_overlap=True)
     # xgmi A/B last, in child processes (see the module docstring); skipped
     # when the exactness pass found the xgmi kernels wrong on these ranks.
     xgmi_on = on_gpu and (a.xgmi_ab == "on" or (a.xgmi_ab == "auto" and world > 1))
@@ -527,7 +558,14 @@ def main() -> int:
         # that RCCL formed an N-rank group
         "rccl_nranks": g["dlnb"].get("rccl_nranks"),
         "runtime": g["dlnb"].get("runtime"),
+        # the xGMI cost model's iteration at this N (BASELINE.md "Link-model
+        # expectations"): the headline and the comm-bound block should land
+        # near these on an 8 x MI355X node (plus ~1-2 ms of fixed overhead)
+        "predicted_ms": _predicted_ms(a, world, "fsdp", a.model, (a.units, world)),
     }
+    if "comm_bound" in extra and "error" not in extra["comm_bound"]:
+        extra["comm_bound"]["predicted_ms"] = _predicted_ms(a, world, "dp", a.c5_model, (a.c5_buckets,),
+                                                            wire=a.c5_wire)
     out.update(exact)
     out.update(extra)
     print(json.dumps(out), flush=True)

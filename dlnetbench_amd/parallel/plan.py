@@ -310,6 +310,39 @@ def busbw_factor(op: str, n: int) -> float:
     return 1.0
 
 
+def model_layers(base: str, model: str) -> Dict[str, int]:
+    """Layer and head counts of a stats-table model from its architecture JSON
+    (models/<name>.json; the table name without its _<batch>_<dtype> suffix)."""
+    name = model.rsplit("_", 2)[0]
+    with open(os.path.join(base, "models", name + ".json")) as f:
+        arch = json.load(f)
+    heads = arch.get("num_heads", 1)
+    return {"layers": arch.get("num_encoder_blocks", 0) + arch.get("num_decoder_blocks", 0), "heads": heads,
+            "kv_heads": arch.get("dlnb", {}).get("num_kv_heads", heads)}
+
+
+def predict(strategy: str, model: str, params: List[int], world: int, base: str = ".", wire: str = "bf16",
+            algo: str = "direct", ep_overlap: bool = False, pp_schedule: str = "gpipe", pp_virtual: int = 2,
+            dp_bucket_ratio: float = 1.0, **link) -> Dict[str, float]:
+    """xGMI cost-model prediction (xgmi_model.py) of one run at `world` GPUs:
+    dp, fsdp and the pipeline hybrids; `link` overrides LinkModel fields."""
+    from . import xgmi_model as xm
+    st = load_stats(os.path.join(base, "model_stats", model + ".txt"))
+    lm = xm.LinkModel(**link)
+    if strategy == "dp":
+        return xm.predict_dp(st, world, params[0], lm, wire, algo, ratio=dp_bucket_ratio)
+    if strategy == "fsdp":
+        return xm.predict_fsdp(st, world, params[0], params[1], lm, wire, algo)
+    if strategy in ("hybrid_2d", "hybrid_3d", "hybrid_3d_moe", "hybrid_4d"):
+        L = model_layers(base, model)["layers"]
+        inner = params[2] if len(params) > 2 else 1
+        experts = params[3] if len(params) > 3 else 1
+        pl = plan_hybrid(st, world, strategy, params[0], params[1], inner, L, wire=wire, experts=experts,
+                         pp_schedule=pp_schedule, pp_virtual=pp_virtual)
+        return xm.predict_hybrid(pl, lm, algo, pp_virtual, ep_overlap=ep_overlap)
+    raise ValueError(f"no prediction for {strategy}")
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description="Print the messages and memory of a benchmark run")
     ap.add_argument("strategy", choices=["dp", "fsdp", "hybrid_2d", "hybrid_3d", "hybrid_3d_moe", "hybrid_4d",
@@ -327,7 +360,9 @@ def main(argv=None) -> int:
     ap.add_argument("--pp-schedule", default="gpipe", choices=["gpipe", "1f1b", "interleaved", "dualpipe"])
     ap.add_argument("--pp-virtual", type=int, default=2, help="interleaved: model chunks per stage")
     ap.add_argument("--predict", action="store_true",
-                    help="dp / fsdp: add the xGMI cost-model prediction (parallel/xgmi_model.py) at W = 1, 2, 4, 8")
+                    help="add the xGMI cost-model prediction (parallel/xgmi_model.py): dp / fsdp at W = 1, 2, 4, 8, "
+                         "the pipeline hybrids at --world")
+    ap.add_argument("--ep-overlap", action="store_true", help="hybrid_3d_moe --predict: dual-batch all-to-all overlap")
     ap.add_argument("--link-gbps", type=float, default=153.0, help="xGMI bandwidth per link and direction")
     ap.add_argument("--eta", type=float, default=0.75, help="achieved fraction of the link bandwidth")
     ap.add_argument("--alpha-us", type=float, default=15.0, help="latency per collective")
@@ -343,14 +378,10 @@ def main(argv=None) -> int:
     elif a.strategy == "fsdp":
         pl = plan_fsdp(st, a.world, *a.params, wire=a.wire)
     else:
-        base = a.model.rsplit("_", 2)[0]
-        with open(os.path.join(a.base, "models", base + ".json")) as f:
-            arch = json.load(f)
-        L = arch.get("num_encoder_blocks", 0) + arch.get("num_decoder_blocks", 0)
+        ml = model_layers(a.base, a.model)
+        L = ml["layers"]
         if a.strategy == "hybrid_cp":
-            heads = arch.get("num_heads", 1)
-            kv = arch.get("dlnb", {}).get("num_kv_heads", heads)
-            pl = plan_cp(st, a.world, a.params[0], L, heads, kv, a.cp_algo, wire=a.wire)
+            pl = plan_cp(st, a.world, a.params[0], L, ml["heads"], ml["kv_heads"], a.cp_algo, wire=a.wire)
         else:
             inner = a.params[2] if len(a.params) > 2 else 1
             experts = a.params[3] if len(a.params) > 3 else 1
@@ -373,6 +404,14 @@ def main(argv=None) -> int:
                                   "by_world": pred}
         if a.strategy == "dp":
             doc["xgmi_prediction"]["suggested_buckets_at_world"] = xm.suggest_buckets(st, a.world, lm, a.wire)
+    elif a.predict and a.strategy.startswith("hybrid_") and a.strategy != "hybrid_cp":
+        from . import xgmi_model as xm
+        lm = xm.LinkModel(a.link_gbps, a.eta, a.alpha_us, buffers=a.buffers, hbm_gbps=a.hbm_gbps)
+        doc["xgmi_prediction"] = {"model": {"link_gbps": a.link_gbps, "eta": a.eta, "alpha_us": a.alpha_us,
+                                            "algo": a.algo, "buffers": a.buffers, "hbm_gbps": a.hbm_gbps},
+                                  "at_world": a.world,
+                                  "prediction": xm.predict_hybrid(pl, lm, a.algo, a.pp_virtual,
+                                                                  ep_overlap=a.ep_overlap)}
     print(json.dumps(doc, indent=1))
     return 0
 

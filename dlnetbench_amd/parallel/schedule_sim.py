@@ -6,8 +6,10 @@ next) executing their operations in order; compute waits on receive events
 and on the send of the buffer it overwrites; a link operation is a group of
 at most one send and one receive that completes when every matching
 operation (per channel FIFO order) sits at the head of its own stream with
-its waits satisfied. Links cost nothing, so a finished run's makespan is the
-schedule's compute critical path and a stuck run is a deadlock.
+its waits satisfied. By default links cost nothing, so a finished run's
+makespan is the schedule's compute critical path and a stuck run is a
+deadlock; with `link` > 0 every link group takes that long (the xGMI cost
+model's send/recv time: xgmi_model.predict_hybrid).
 
     python -m dlnetbench_amd.parallel.schedule_sim --stages 4 --microbatches 8 --virtual 2
 """
@@ -17,7 +19,8 @@ import argparse
 from typing import Dict, List, Tuple
 
 
-def build(S: int, mb: int, V: int, f: float, b: float, sched: str) -> Dict[Tuple[int, str], List[dict]]:
+def build(S: int, mb: int, V: int, f: float, b: float, sched: str,
+          link: float = 0.0) -> Dict[Tuple[int, str], List[dict]]:
     streams: Dict[Tuple[int, str], List[dict]] = {}
     total = mb * V
 
@@ -67,7 +70,7 @@ def build(S: int, mb: int, V: int, f: float, b: float, sched: str) -> Dict[Tuple
                 if rb >= 2:
                     waits.append((s, "bdone", rb - 2))
                 p2p.append(("recv", "B", (s + 1) % S)); rec.append((s, "recvB", rb))
-            op(s, "n", dur=0.0, waits=waits, rec=rec, p2p=p2p)
+            op(s, "n", dur=link, waits=waits, rec=rec, p2p=p2p)
 
         def prv(sb, rf):  # previous link: send B(sb) to s-1, receive F(rf) from s-1
             if S == 1 or (sb < 0 and rf < 0):
@@ -79,7 +82,7 @@ def build(S: int, mb: int, V: int, f: float, b: float, sched: str) -> Dict[Tuple
                 if rf >= 2:
                     waits.append((s, "fdone", rf - 2))
                 p2p.append(("recv", "F", (s - 1) % S)); rec.append((s, "recvF", rf))
-            op(s, "p", dur=0.0, waits=waits, rec=rec, p2p=p2p)
+            op(s, "p", dur=link, waits=waits, rec=rec, p2p=p2p)
 
         if il:
             w = total if mb == S else min((S - s - 1) * 2 + (V - 1) * S, total)
@@ -211,7 +214,7 @@ def dualpipe_floor(S: int, mb: int, f: float, b: float) -> float:
     return span
 
 
-def build_dualpipe(S: int, mb: int, f: float, b: float) -> Dict[Tuple[int, str], List[dict]]:
+def build_dualpipe(S: int, mb: int, f: float, b: float, link: float = 0.0) -> Dict[Tuple[int, str], List[dict]]:
     """Streams of enqueue_dualpipe: per tick the rank's op on the compute stream (waiting on its input's
     receive), then the next-link group, then the previous-link group - each at most one send (this rank's
     op output) and one receive (the neighbour's op output of the same tick, into a buffer of its own).
@@ -258,7 +261,7 @@ def build_dualpipe(S: int, mb: int, f: float, b: float) -> Dict[Tuple[int, str],
                     d, i, bw = theirs
                     p2p.append(("recv", "L", peer))
                     rec.append((s, "recvB" if bw else "recvF", d * H + i))
-                streams.setdefault((s, st), []).append({"dur": 0.0, "waits": waits, "rec": rec, "p2p": p2p})
+                streams.setdefault((s, st), []).append({"dur": link, "waits": waits, "rec": rec, "p2p": p2p})
     return streams
 
 

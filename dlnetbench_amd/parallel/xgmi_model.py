@@ -27,7 +27,11 @@ and t = max(link time, HBM time) + alpha. "rccl" (default) is links only.
 `predict_dp` / `predict_fsdp` replay the strategies' overlap schedules
 (csrc/src/strategy_dp.cpp, strategy_fsdp.cpp: one in-order comm lane, a
 collective waits for the compute that produced its data) with these times
-and return the predicted iteration time and exposed communication. They are
+and return the predicted iteration time and exposed communication.
+`predict_hybrid` runs the pipeline schedules (schedule_sim, the enqueue
+order of strategy_pipeline.cpp) with every stage-to-stage send/recv taking
+its link time and the TP all-reduces / EP all-to-alls that sit on the
+compute stream added to each microbatch's compute. They are
 the numbers to hold the driver's measured scaling run against, and the way to
 size DP buckets for point-to-point links instead of a switch
 (`suggest_buckets`).
@@ -38,7 +42,7 @@ from dataclasses import dataclass
 from typing import Dict, List
 
 from ..utils.stats import ModelStats
-from .plan import WIRE_BYTES, dp_bucket_sizes, fsdp_shards
+from .plan import WIRE_BYTES, Plan, dp_bucket_sizes, fsdp_shards
 
 
 @dataclass
@@ -160,3 +164,73 @@ def suggest_buckets(st: ModelStats, world: int, model: LinkModel, wire: str = "b
         if best is None or p["iter_ms"] < best[1]["iter_ms"] - 1e-9:
             best = (nb, p)
     return {"num_buckets": best[0], **best[1]}
+
+
+def _ep_overlap_op_us(compute_us: float, n: int, half_us: float) -> float:
+    """One microbatch's compute op under --ep-overlap (strategy_pipeline.cpp
+    micro_compute): n slices of two halves; half hh's all-to-all runs on the EP
+    lane after its compute slice, and its next slice waits for it; the op ends
+    when both halves' last all-to-alls are done."""
+    t_c = t_e = 0.0
+    done = [0.0, 0.0]
+    for i in range(n):
+        for hh in (0, 1):
+            t_c = (t_c if i == 0 else max(t_c, done[hh])) + compute_us / (2 * n)
+            t_e = max(t_e, t_c) + half_us
+            done[hh] = t_e
+    return max(t_c, done[0], done[1])
+
+
+def predict_hybrid(p: Plan, model: LinkModel, algo: str = "direct", pp_virtual: int = 1,
+                   ep_overlap: bool = False) -> Dict[str, float]:
+    """hybrid_2d / 3d / 3d_moe / 4d from their plan (plan.plan_hybrid): the
+    schedule's makespan with the inner-group collectives on the compute stream
+    (csrc/src/strategy_pipeline.cpp micro_compute: a microbatch's TP
+    all-reduces and EP all-to-alls follow its compute in order, so they
+    lengthen it) and every pipeline send/recv taking one link's time
+    (rendezvous: both stages' link streams finish it together). The gradient
+    all-reduces that end the iteration (DP, EP non-expert, DualPipe mirror)
+    are added after the last backward, fully exposed: an upper bound when
+    they are bucketed into the backward. ep_overlap: --ep-overlap's two
+    half-microbatches, each all-to-all under the other half's compute
+    (_ep_overlap_op_us)."""
+    from . import schedule_sim as sim
+    S, mb = p.params["num_stages"], p.params["num_microbatches"]
+    sched = p.params.get("pp_schedule", "gpipe")
+    V = pp_virtual if sched == "interleaved" else 1
+    f, b = p.compute_per_unit_us["fwd_per_microbatch"], p.compute_per_unit_us["bwd_per_microbatch"]
+    msgs = {m.name: m for m in p.messages}
+    n_ops = mb * V  # forward (= backward) compute ops per rank per iteration
+    inner = 0.0     # inner-group collective time per compute op
+    for name in ("tp_allreduce", "ep_alltoall"):
+        m = msgs.get(name)
+        if m is not None:
+            inner += m.calls_per_iter / (2 * n_ops) * model.coll_us(m.op, m.wire_bytes, m.group_size, algo)
+    pipe = msgs.get("pipe_sendrecv")
+    link = model.coll_us("sendrecv", pipe.wire_bytes, 2) if pipe is not None and S > 1 else 0.0
+    fe, be = f + inner * V, b + inner * V  # build() splits f, b over the V chunks
+    a2a = msgs.get("ep_alltoall")
+    if ep_overlap:
+        if a2a is None or "tp_allreduce" in msgs or sched == "dualpipe":
+            raise ValueError("--ep-overlap applies to hybrid_3d_moe with gpipe / 1f1b / interleaved")
+        n = a2a.calls_per_iter // (2 * n_ops)
+        half = model.coll_us("alltoall", a2a.wire_bytes / 2, a2a.group_size, algo)
+        fe = _ep_overlap_op_us(f / V, n, half) * V
+        be = _ep_overlap_op_us(b / V, n, half) * V
+        inner = (fe - f) / V
+    if sched == "dualpipe":
+        streams = sim.build_dualpipe(S, mb, fe, be, link)
+    else:
+        streams = sim.build(S, mb, V, fe, be, sched, link)
+    span, stuck = sim.simulate(streams)
+    if stuck:
+        raise RuntimeError(f"{sched} schedule deadlocks in the model: {stuck[:4]}")
+    tail = 0.0
+    for name in ("pp_mirror_allreduce", "ep_nonexpert_allreduce", "dp_allreduce"):
+        m = msgs.get(name)
+        if m is not None and m.group_size > 1:
+            tail += m.calls_per_iter * model.coll_us(m.op, m.wire_bytes, m.group_size, algo)
+    floor = p.compute_per_unit_us["compute_floor_us"]
+    end = span + tail
+    return {"iter_ms": end / 1e3, "floor_ms": floor / 1e3, "exposed_ms": (end - floor) / 1e3,
+            "inner_comm_per_op_us": inner, "sendrecv_us": link, "tail_allreduce_us": tail}

@@ -82,6 +82,14 @@ def test_bench_hybrid_blocks_eight_ranks_cpu(tmp_path):
         assert h["pp_comm_time_ms"] is not None and h["dp_comm_time_ms"] is not None
     assert h3["params"] == [2, 4, 4] and h3["tp_comm_time_ms"] is not None and h3["busbw_GBps"]["tp_allreduce"] > 0
     assert h4["params"] == [2, 8, 4] and h4["ep_comm_time_ms"] is not None and h4["busbw_GBps"]["ep_alltoall"] > 0
+    # the same C4 config with the all-to-alls off the compute stream (--ep-overlap)
+    ov = h4["ep_overlap"]
+    assert "error" not in ov, ov
+    assert ov["ep_overlap"] is True and ov["floor_ms"] == h4["floor_ms"] and ov["ms_per_step"] >= 0.9 * ov["floor_ms"]
+    # the xGMI cost model's prediction next to every measured block
+    for h in (h3, h4, ov):
+        assert h["predicted_ms"] >= h["floor_ms"] and h["vs_predicted"] > 0
+    assert o["predicted_ms"] > 0
     # GPipe floor (mb + S - 1)(f_mb + b_mb): hybrid_3d f_mb = fwd / S / (mb T)
     assert h3["floor_ms"] == pytest.approx((4 + 1) * (2.0 + 4.0) / 2 / (4 * 4), rel=1e-3)
     assert h4["floor_ms"] == pytest.approx((8 + 1) * (2.0 + 4.0) / 2 / 8, rel=1e-3)

@@ -293,3 +293,40 @@ def test_dp_geometric_tail_shrinks_predicted_n8_step(root):
     geo = xm.predict_dp(st, 8, 8, lm, ratio=0.7)["iter_ms"]
     assert even == pytest.approx(7.504, abs=0.01)
     assert geo == pytest.approx(7.24, abs=0.01) and geo < even
+
+
+def test_hybrid_predictions_for_the_baseline_configs(root):
+    """plan hybrid_3d / hybrid_3d_moe --predict at N = 8 (the numbers the
+    driver's hybrid blocks report as predicted_ms): C3's TP all-reduces and
+    stage sends add ~22 ms to the 3.81 s GPipe floor; C4's 1,024 all-to-alls
+    on the compute stream add ~1.3 s, and --ep-overlap hides all but ~33 ms."""
+    c3 = P.predict("hybrid_3d", "llama3_70b_16_bfloat16", [2, 4, 4], 8, base=root)
+    assert c3["floor_ms"] == pytest.approx(3811.64, abs=0.1)
+    assert c3["iter_ms"] == pytest.approx(3833.3, abs=1.0)
+    c4 = P.predict("hybrid_3d_moe", "mixtral_8x7b_16_bfloat16", [2, 16, 4], 8, base=root)
+    c4o = P.predict("hybrid_3d_moe", "mixtral_8x7b_16_bfloat16", [2, 16, 4], 8, base=root, ep_overlap=True)
+    assert c4["floor_ms"] == pytest.approx(13557.7, abs=0.1) == c4o["floor_ms"]
+    assert c4["iter_ms"] == pytest.approx(14858.8, abs=2.0)
+    assert c4o["iter_ms"] == pytest.approx(13590.3, abs=2.0)
+    # a ring per collective (a switch fabric's algorithm) costs more than direct all-link collectives
+    ring = P.predict("hybrid_3d_moe", "mixtral_8x7b_16_bfloat16", [2, 16, 4], 8, base=root, algo="ring")
+    assert ring["iter_ms"] > c4["iter_ms"]
+
+
+def test_hybrid_prediction_with_free_links_is_the_floor(root):
+    """Links of infinite bandwidth and no latency: every schedule's prediction
+    is its compute floor (the simulator's critical path), for 1F1B,
+    interleaved and DualPipe as well as GPipe."""
+    for sched, V in (("gpipe", 1), ("1f1b", 1), ("interleaved", 2), ("dualpipe", 1)):
+        r = P.predict("hybrid_2d", "llama3_8b_16_bfloat16", [4, 8], 8, base=root, pp_schedule=sched, pp_virtual=V,
+                      link_gbps=1e12, alpha_us=0.0)
+        assert r["iter_ms"] == pytest.approx(r["floor_ms"], rel=1e-6), sched
+
+
+def test_ep_overlap_op_model():
+    from dlnetbench_amd.parallel.xgmi_model import _ep_overlap_op_us
+    assert _ep_overlap_op_us(100.0, 4, 0.0) == pytest.approx(100.0)
+    # all-to-all shorter than a half-slice: hidden except the last one
+    assert _ep_overlap_op_us(100.0, 4, 5.0) == pytest.approx(105.0)
+    # all-to-all longer than the other half's slice: the lane is the bound
+    assert _ep_overlap_op_us(100.0, 4, 50.0) == pytest.approx(12.5 + 8 * 50.0)
