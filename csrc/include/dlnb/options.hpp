@@ -77,6 +77,10 @@ struct Options {
   bool quiet = false;
   bool silent = false;  // print nothing (library use, e.g. bench.py)
   bool trace = false;   // roctx ranges around iterations and phases
+  // device timeline (dlnb/timeline.hpp): Chrome trace of every collective,
+  // P2P group and compute task of every rank, written by rank 0
+  std::string timeline_path;
+  int timeline_iters = 2;  // timed iterations kept in it (0 = all)
   int comm_cus = 32;    // CUs left free by the persistent compute for collectives
   // RCCL maxCTAs per communicator on a comm lane: -1 = comm_cus / lanes
   // (runner.cpp, collective_lanes), 0 = RCCL's default, N = N.

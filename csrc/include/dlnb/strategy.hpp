@@ -20,6 +20,7 @@
 #include "dlnb/json.hpp"
 #include "dlnb/options.hpp"
 #include "dlnb/timers.hpp"
+#include "dlnb/timeline.hpp"
 #include "dlnb/workload.hpp"
 
 namespace dlnb {
@@ -47,6 +48,9 @@ struct Context {
   // RCCL CTA cap for communicators whose collectives run on a comm lane
   // (a stream beside the compute); 0 = library default.
   int lane_ctas = 0;
+  // --timeline: the spans of this rank (declared last: released before the
+  // device whose stamp slots it holds)
+  std::unique_ptr<Timeline> timeline;
   int rank() const { return boot->info.rank; }
   int world() const { return boot->info.world_size; }
   HostGroup& hg() { return *boot->world; }

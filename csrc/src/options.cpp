@@ -108,6 +108,8 @@ std::string usage(StrategyKind kind, const std::string& prog) {
      << "  --quiet                only print the report section\n"
      << "  --silent               print nothing (the report is returned to the caller)\n"
      << "  --trace                emit roctx ranges (rocprofv3 --marker-trace)\n"
+     << "  --timeline PATH        device timeline of every rank (Chrome / Perfetto trace JSON, rank 0 writes it)\n"
+     << "  --timeline-iters N     timed iterations kept in the timeline (default 2, 0 = all)\n"
      << "  --comm-cus N           CUs the gemm compute leaves free for collectives (default 32)\n"
      << "  --rccl-max-ctas N      RCCL blocks per collective on each comm lane (default: comm-cus / lanes;\n"
      << "                         0 = RCCL's own choice)\n"
@@ -192,6 +194,11 @@ Options parse_options(StrategyKind kind, int argc, const char* const* argv) {
       o.time_scale = to_double(val("time-scale"), "time-scale");
     } else if (is("--json")) {
       o.json_path = val("json");
+    } else if (is("--timeline")) {
+      o.timeline_path = val("timeline");
+    } else if (is("--timeline-iters")) {
+      o.timeline_iters = std::stoi(val("timeline-iters"));
+      DLNB_REQUIRE(o.timeline_iters >= 0, "--timeline-iters must be >= 0");
     } else if (is("--stats-file")) {
       o.stats_file = val("stats-file");
     } else if (is("--store")) {

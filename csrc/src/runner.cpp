@@ -446,6 +446,13 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   shape.comm_cus = opt.comm_cus;
   ComputeMode mode = parse_compute_mode(opt.compute, ctx.dev->kind());
   ctx.compute = make_compute_engine(*ctx.dev, mode, shape, opt.time_scale);
+  if (!opt.timeline_path.empty()) {
+    // every communicator the strategy creates and every compute task it
+    // enqueues is traced (dlnb/timeline.hpp)
+    ctx.timeline = std::make_unique<Timeline>(*ctx.dev);
+    ctx.comms = make_tracing_factory(std::move(ctx.comms), ctx.timeline.get());
+    ctx.compute = make_tracing_compute(std::move(ctx.compute), ctx.timeline.get());
+  }
 
   if (opt.topology) print_topology(ctx);
 
@@ -492,6 +499,8 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       std::cerr << "[dlnb] warning: " << strat->streams().size() << " streams per rank > GPU_MAX_HW_QUEUES=" << nq
                 << "; streams will share hardware queues" << std::endl;
   }
+  Timeline* TL = ctx.timeline.get();
+  if (TL) TL->calibrate(*strat->streams()[0]);
   TimerSet& T = *strat->timers();
   const char* rkey = strat->runtime_key();
   T.ensure(rkey);
@@ -510,11 +519,13 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     std::vector<Stream*> others(ss.begin() + 1, ss.end());
     TraceRange tr("dlnb:graph_capture");
     T.begin_capture();
+    if (TL) TL->begin_capture();
     graph = ctx.dev->capture(*ss[0], others, [&] {
       ctx.compute->reset_clocks(*ss[0]);
       strat->enqueue_iteration();
     });
     T.end_capture();
+    if (TL) TL->end_capture();
     if (ri.rank == 0 && !opt.quiet)
       std::cout << "[dlnb] captured one iteration into a HIP graph of " << graph->nodes() << " nodes" << std::endl;
   }
@@ -536,6 +547,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     enqueue();
     strat->synchronize();
     warm.push_back(now_s() - t0);
+    if (TL) TL->collect(-1);
   }
   T.clear();
 
@@ -562,6 +574,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       TraceRange tr("dlnb:loop_iteration");
       enqueue();
       strat->synchronize();
+      if (TL) TL->collect(-1);
     }
     ctx.hg().barrier();
     ctx.hg().store().finish();
@@ -581,6 +594,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     enqueue();
     strat->synchronize();
     T.add(rkey, now_s() - t0);
+    if (TL) TL->collect(r);
     if (meter->available()) T.add("energy_consumed", meter->joules() - j0);
   }
   ctx.dev->synchronize();
@@ -606,6 +620,34 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     rank["compute_table_s"] = table_s;
   }
   auto all = ctx.hg().allgather(rank.dump());
+  Json timeline_info = nullptr;
+  if (TL) {
+    Json mine = TL->rank_json(ri.rank, opt.timeline_iters);
+    mine["device"] = ctx.dev->name() + " " + std::to_string(ctx.dev->index()) + " @ " + ri.hostname;
+    auto parts = ctx.hg().allgather(mine.dump());
+    timeline_info = Json::object();
+    timeline_info["path"] = opt.timeline_path;
+    timeline_info["iterations_kept"] = opt.timeline_iters;
+    long long nev = 0;
+    bool trunc = false;
+    std::vector<Json> docs;
+    for (const auto& p : parts) {
+      docs.push_back(Json::parse(p));
+      nev += static_cast<long long>(docs.back().at("events").size());
+      trunc = trunc || docs.back().at("truncated").as_bool();
+    }
+    timeline_info["events"] = nev;
+    timeline_info["truncated"] = trunc;
+    if (ri.rank == 0) {
+      Json meta = Json::object();
+      meta["strategy"] = strategy_name(opt.strategy);
+      meta["model"] = opt.model;
+      meta["backend"] = backend;
+      meta["graph"] = opt.graph;
+      meta["world_size"] = ri.world_size;
+      write_chrome_trace(opt.timeline_path, docs, meta);
+    }
+  }
 
   Json g = strat->global_json();
   Json ext = Json::object();
@@ -622,6 +664,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   ext["warmup_times"] = Json(warm);
   ext["timed_region_s"] = timed_region;
   ext["energy_source"] = meter->source();
+  if (TL) ext["timeline"] = timeline_info;
   {
     Json b = Json::object();
     b["lanes"] = lanes;

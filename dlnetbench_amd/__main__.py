@@ -6,7 +6,7 @@
                       exact check / bandwidth sweep of a comm backend (dlnb commtest)
     launch -n N <program ...>   generic N-rank launcher (utils/launch.py)
     sweep | plots | report | plan | schedule-sim | roofline | measure | gemm-bench | clock-check |
-    prof-summary | bench-report | download-models
+    prof-summary | bench-report | download-models | timeline
                       the tools, each with its own --help
 
 The reference spreads these over Makefile targets, SbatchMan jobs and loose
@@ -36,6 +36,7 @@ TOOLS = {
     "prof-summary": "dlnetbench_amd.tools.prof_summary",
     "bench-report": "dlnetbench_amd.tools.bench_report",
     "download-models": "dlnetbench_amd.tools.download_models",
+    "timeline": "dlnetbench_amd.tools.timeline",
 }
 
 

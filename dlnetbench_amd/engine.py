@@ -36,6 +36,7 @@ _FLAG = {
     "json": "--json", "store": "--store", "stats_file": "--stats-file", "comm_cus": "--comm-cus",
     "comm_lanes": "--comm-lanes", "pp_schedule": "--pp-schedule", "zero": "--zero", "cp_algo": "--cp-algo", "pp_virtual": "--pp-virtual",
     "ranks": "--ranks", "ep_imbalance": "--ep-imbalance", "rccl_max_ctas": "--rccl-max-ctas",
+    "timeline": "--timeline", "timeline_iters": "--timeline-iters",
 }
 _BOOL = {"in_place": "--in-place", "optimizer": "--optimizer", "loop": "--loop", "quiet": "--quiet",
          "silent": "--silent", "graph": "--graph", "trace": "--trace", "ep_overlap": "--ep-overlap",
