@@ -38,6 +38,11 @@ ride along as extra keys of the same JSON line:
   with its effective bus bandwidth as a ratio of the headline's (RCCL).
   Also a child process per rank, after ``comm_bound_xgmi``.
 
+* ``link_bench`` (N > 1): every collective's bus bandwidth at 16 MB and 128 MB
+  per rank on the job's GPUs with nothing else running, over RCCL, the xgmi
+  kernels (staged) and the xgmi zero-copy path (``dlnb commtest --bench``,
+  HIP-graph replayed): the links' side of the numbers above.
+
 At N = 1 a "collective" is a local device copy: bus bandwidth is reported
 as null (nccl-tests convention: nothing crosses a link).
 
@@ -194,6 +199,61 @@ def _exactness(a: argparse.Namespace, world: int, rank: int) -> Dict[str, Any]:
         d = json.load(f)
     os.remove(out)
     return d
+
+
+def _link_bench(a: argparse.Namespace, world: int, rank: int, backend: str, registered: bool) -> Dict[str, Any]:
+    """Collective bandwidth on the job's own GPUs, nothing else running
+    (`dlnb commtest --bench --graph`: 10 graph-replayed ops per size after 3
+    warm-ups, nccl-tests algbw / busbw, max time over ranks): what the links
+    give each collective of the backend, next to what the strategies got.
+    Returns {op: {elements: {"busbw_GBps", "time_us"}}} on rank 0."""
+    tag = ".lb" + backend + ("r" if registered else "")
+    _store_env(world, rank, tag)
+    cmd = [os.path.join(ROOT, "build", "bin", "dlnb"), "commtest", "--bench", "--backend", backend,
+           "--dtype", "bf16", "--sizes", a.link_sizes, "--iters", "10", "--warmup", "3"]
+    if backend != "cpu":
+        cmd.append("--graph")
+    if registered:
+        cmd.append("--registered")
+    if a.devices:
+        cmd += ["-d", a.devices]
+    env = dict(os.environ, DLNB_XGMI_TIMEOUT_S=os.environ.get("DLNB_XGMI_TIMEOUT_S", "20"),
+               DLNB_STORE_TIMEOUT=str(int(a.link_timeout)))
+    p = subprocess.run(cmd, env=env, timeout=a.link_timeout, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       text=True)
+    if p.returncode != 0:
+        raise RuntimeError(f"exit {p.returncode}: " + (p.stderr or "")[-300:])
+    if rank != 0:
+        return {}
+    out: Dict[str, Any] = {}
+    for ln in p.stdout.splitlines():
+        if not ln.startswith("{"):
+            continue
+        j = json.loads(ln)
+        if j.get("commtest") != "bench" or j["op"] == "copy":
+            continue
+        out.setdefault(j["op"], {})[str(int(j["count"]))] = {"busbw_GBps": round(j["busbw_GBps"], 2),
+                                                             "time_us": round(j["time_us"], 1)}
+    return out
+
+
+def _link_block(a: argparse.Namespace, world: int, rank: int, xgmi_ok: bool) -> Dict[str, Any]:
+    """RCCL, xgmi staged and xgmi zero-copy collective bandwidth at N > 1."""
+    res: Dict[str, Any] = {"dtype": "bf16", "elements_per_rank": [int(x) for x in a.link_sizes.split(",")],
+                           "hip_graph": a.backend != "cpu"}
+    checked = _exact_backends(a)  # the backends these ranks can run (ranks sharing a GPU: no RCCL)
+    runs = [("cpu", "cpu", False)] if checked == "cpu" else [("rccl", "rccl", False)] if "rccl" in checked else []
+    if checked != "cpu":
+        if xgmi_ok:
+            runs += [("xgmi", "xgmi", False), ("xgmi_registered", "xgmi", True)]
+        else:
+            res["xgmi"] = {"error": "skipped: the xgmi exactness check failed on these ranks"}
+    for key, backend, reg in runs:
+        try:
+            res[key] = _link_bench(a, world, rank, backend, reg)
+        except Exception as e:  # noqa: BLE001
+            res[key] = {"error": str(e)[:300]}
+    return res
 
 
 def _exact_block(a: argparse.Namespace, world: int, rank: int) -> Dict[str, Any]:
@@ -358,6 +418,10 @@ def main() -> int:
     ap.add_argument("--hybrid-timeout", type=float, default=150.0)
     ap.add_argument("--c4-ep-overlap", choices=["on", "off"], default="on",
                     help="also run C4 with --ep-overlap (the all-to-alls off the compute stream)")
+    ap.add_argument("--link-bench", choices=["auto", "on", "off"], default="auto",
+                    help="collective bandwidth of RCCL and the xgmi kernels on the job's GPUs (auto: N > 1 on GPU)")
+    ap.add_argument("--link-sizes", default="8388608,67108864", help="--link-bench elements per rank (bf16)")
+    ap.add_argument("--link-timeout", type=float, default=90.0)
     ap.add_argument("--json", default=None, help="also write the full headline report here (rank 0)")
     a = ap.parse_args()
     a.hybrid_backend = "rccl" if a.backend == "auto" else a.backend
@@ -503,6 +567,9 @@ def main() -> int:
             extra["hybrid_3d_moe"]["ep_overlap"] = _hybrid_block(
                 a, world, rank, ".c4o", "hybrid_3d_moe", a.c4_model, c4,
                 "GPipe (mb + S - 1)(f_mb + b_mb), BASELINE.md C4", ep_overlap=True)
+    # Collective bandwidth with nothing else running, RCCL and xgmi.
+    if a.link_bench == "on" or (a.link_bench == "auto" and world > 1 and on_gpu):
+        extra["link_bench"] = _link_block(a, world, rank, xgmi_exact_ok)
     # xgmi A/B last, in child processes (see the module docstring); skipped
     # when the exactness pass found the xgmi kernels wrong on these ranks.
     xgmi_on = on_gpu and (a.xgmi_ab == "on" or (a.xgmi_ab == "auto" and world > 1))

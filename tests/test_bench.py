@@ -33,7 +33,8 @@ def _json_lines(out: str):
 def test_bench_torchrun_cpu(n, tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", str(n), "--steps", "2", "--warmup", "1", "--backend", "cpu", "--compute", "sleep"] + TINY
+           "--gpus", str(n), "--steps", "2", "--warmup", "1", "--backend", "cpu", "--compute", "sleep",
+           "--link-bench", "on", "--link-sizes", "4096,65536"] + TINY
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=str(tmp_path),
                        env=dict(os.environ, OMP_NUM_THREADS="1"))
     assert p.returncode == 0, p.stderr[-3000:]
@@ -57,6 +58,11 @@ def test_bench_torchrun_cpu(n, tmp_path):
     d = o["exact_detail"]
     assert d["ok"] and d["world_size"] == n and d["failed"] == [] and d["sizes"] == [4097, 30000]
     assert d["rccl_nranks"] == -1 and o["rccl_nranks"] == {}  # no RCCL on the CPU backend
+    # the collective micro-benchmark on the job's ranks (RCCL / xgmi on GPUs; the shm backend here)
+    lb = o["link_bench"]
+    assert lb["elements_per_rank"] == [4096, 65536] and "error" not in lb["cpu"], lb
+    for op in ("all_reduce", "all_gather", "reduce_scatter", "all_to_all", "sendrecv"):
+        assert lb["cpu"][op]["65536"]["busbw_GBps"] > 0 and lb["cpu"][op]["4096"]["time_us"] > 0
 
 
 def test_bench_hybrid_blocks_eight_ranks_cpu(tmp_path):
@@ -159,7 +165,8 @@ def test_bench_torchrun_xgmi_two_ranks_one_gpu(tmp_path):
         pytest.skip("no GPU")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--backend", "xgmi", "--devices", "0,0"] + TINY
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--backend", "xgmi", "--devices", "0,0",
+           "--link-sizes", "1048576"] + TINY
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=str(tmp_path),
                        env=dict(os.environ, DLNB_XGMI_TIMEOUT_S="60"))
     assert p.returncode == 0, p.stderr[-3000:]
@@ -176,3 +183,8 @@ def test_bench_torchrun_xgmi_two_ranks_one_gpu(tmp_path):
     assert "error" not in h, h
     assert h["ms_per_step"] > 0 and h["effective_busbw_GBps"]["allgather"] > 0
     assert h["busbw_ratio_vs_headline"]["allgather"] > 0 and h["headline_backend"] == "XGMI"
+    lb = o["link_bench"]  # staged and zero-copy xgmi; no RCCL with 2 ranks on one GPU
+    assert "rccl" not in lb and lb["hip_graph"] is True
+    for k in ("xgmi", "xgmi_registered"):
+        assert "error" not in lb[k], lb
+        assert all(lb[k][op]["1048576"]["busbw_GBps"] > 0 for op in ("all_reduce", "all_gather", "sendrecv"))
