@@ -63,6 +63,14 @@ def _get(d: Optional[dict], *keys: str) -> Any:
     return d
 
 
+def _largest(by_size: Any) -> Any:
+    """busbw at the largest size of a link_bench op ({elements: {...}})."""
+    if not isinstance(by_size, dict) or not by_size:
+        return None
+    k = max(by_size, key=lambda x: int(x))
+    return by_size[k].get("busbw_GBps") if isinstance(by_size[k], dict) else None
+
+
 def rows(lines: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
     if not lines:
         return []
@@ -93,6 +101,10 @@ def rows(lines: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
             "c3_vs_floor": _get(d, "hybrid_3d", "vs_floor"),
             "c4_ms": _get(d, "hybrid_3d_moe", "ms_per_step"),
             "c4_vs_floor": _get(d, "hybrid_3d_moe", "vs_floor"),
+            "c4_overlap_ms": _get(d, "hybrid_3d_moe", "ep_overlap", "ms_per_step"),
+            "predicted_ms": d.get("predicted_ms"),
+            "link_ar_busbw_rccl": _largest(_get(d, "link_bench", "rccl", "all_reduce")),
+            "link_ar_busbw_xgmi": _largest(_get(d, "link_bench", "xgmi_registered", "all_reduce")),
         }
         out.append(r)
     return out
