@@ -187,7 +187,7 @@ XGMI_STRATS = [  # strategy, model, positional args, extra flags, ranks
     ("dp", "tiny_dense_8_bfloat16", ["4"], [], 8),
     ("fsdp", "tiny_dense_8_bfloat16", ["4", "2"], [], 4),
     ("fsdp", "tiny_dense_8_bfloat16", ["4", "8"], [], 8),
-    ("hybrid_2d", "tiny_dense_8_bfloat16", ["4", "4"], ["--pp-schedule", "1f1b"], 4),
+    ("hybrid_2d", "tiny_dense_8_bfloat16", ["2", "4"], ["--pp-schedule", "1f1b"], 4),  # DP 2 x PP 2
     ("hybrid_3d", "tiny_dense_8_bfloat16", ["2", "4", "2"], ["--pp-schedule", "1f1b"], 8),
     ("hybrid_3d_moe", "tiny_moe_8_bfloat16", ["2", "4", "2"], ["--pp-schedule", "1f1b", "--ep-overlap"], 4),
     ("dp", "tiny_dense_8_bfloat16", ["4"], ["--zero", "2"], 4),
