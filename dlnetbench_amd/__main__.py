@@ -6,7 +6,7 @@
                       exact check / bandwidth sweep of a comm backend (dlnb commtest)
     launch -n N <program ...>   generic N-rank launcher (utils/launch.py)
     sweep | plots | report | plan | schedule-sim | roofline | measure | gemm-bench | clock-check |
-    prof-summary | bench-report | download-models | timeline
+    prof-summary | bench-report | download-models | timeline | interference
                       the tools, each with its own --help
 
 The reference spreads these over Makefile targets, SbatchMan jobs and loose
@@ -37,6 +37,7 @@ TOOLS = {
     "bench-report": "dlnetbench_amd.tools.bench_report",
     "download-models": "dlnetbench_amd.tools.download_models",
     "timeline": "dlnetbench_amd.tools.timeline",
+    "interference": "dlnetbench_amd.tools.interference",
 }
 
 
