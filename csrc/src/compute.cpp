@@ -267,6 +267,24 @@ class GpuCompute : public ComputeEngine {
     auto s = dev_.create_stream(false);
     dev_.fill_random(A_.data(), static_cast<size_t>(Mmax) * K_, dtype_, 1, *s);
     dev_.fill_random(B_.data(), static_cast<size_t>(N_) * K_, dtype_, 2, *s);
+    // DLNB_GEMM_LEVELS="M:us,M:us,..." reuses an earlier calibration (the
+    // report's compute.gemm_levels) instead of measuring: a fixed-work run
+    // beside other jobs (tools/interference.py) must do the work it would do
+    // alone, not what a contended calibration says fits the table time.
+    const std::string given = env_or("DLNB_GEMM_LEVELS", "");
+    if (!given.empty()) {
+      for (const auto& item : split(given, ',')) {
+        const auto kv = split(trim(item), ':');
+        DLNB_REQUIRE(kv.size() == 2, "DLNB_GEMM_LEVELS: expected M:us entries, got '" << item << "'");
+        const int M = std::stoi(kv[0]);
+        const double us = std::stod(kv[1]);
+        DLNB_REQUIRE(M > 0 && M <= Mmax && M % 256 == 0 && us > 0, "DLNB_GEMM_LEVELS: bad entry '" << item << "'");
+        levels_.push_back(GemmLevel{M, us, 2.0 * M * static_cast<double>(N_) * K_});
+      }
+      std::sort(levels_.begin(), levels_.end(), [](const GemmLevel& a, const GemmLevel& b) { return a.M > b.M; });
+      s->synchronize();
+      return;
+    }
     auto e0 = dev_.create_event(true);
     auto e1 = dev_.create_event(true);
     // Run ~0.3 s first so the measurement sees the sustained (DVFS-settled)

@@ -98,7 +98,14 @@ def run(victim: str, victim_ranks: int, aggressor: str, aggressor_ranks: int, wa
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("PYTHONPATH", ROOT)
     vcmd, acmd = _cmd(victim), _cmd(aggressor)
-    alone = [_summary(_run_victim(vcmd, victim_ranks, timeout, env)) for _ in range(repeats)]
+    docs = [_run_victim(vcmd, victim_ranks, timeout, env) for _ in range(repeats)]
+    alone = [_summary(d) for d in docs]
+    # Fixed-work compute (gemm-work / flops) keeps its alone calibration: a
+    # calibration taken beside the aggressor would shrink the work to fit.
+    levels = docs[0]["global"]["dlnb"]["compute"].get("gemm_levels")
+    venv = dict(env)
+    if levels:
+        venv["DLNB_GEMM_LEVELS"] = ",".join(f"{int(lv['M'])}:{lv['us_per_launch']!r}" for lv in levels)
     log = tempfile.mktemp(prefix="dlnb_aggressor_", suffix=".log")
     agg = _start_aggressor(acmd, aggressor_ranks, timeout * repeats + warm_s + 60, env, log)
     try:
@@ -106,7 +113,7 @@ def run(victim: str, victim_ranks: int, aggressor: str, aggressor_ranks: int, wa
         if agg.poll() is not None:
             raise RuntimeError(f"aggressor exited {agg.returncode} before the victim started: "
                                + open(log).read()[-800:])
-        contended = [_summary(_run_victim(vcmd, victim_ranks, timeout, env)) for _ in range(repeats)]
+        contended = [_summary(_run_victim(vcmd, victim_ranks, timeout, venv)) for _ in range(repeats)]
         running = agg.poll() is None
     finally:
         code = _stop(agg)
@@ -126,7 +133,8 @@ def run(victim: str, victim_ranks: int, aggressor: str, aggressor_ranks: int, wa
     return {"victim": victim, "victim_ranks": victim_ranks, "aggressor": aggressor + " --loop",
             "aggressor_ranks": aggressor_ranks, "alone": a, "contended": c,
             "slowdown": round(c["median_ms"] / a["median_ms"], 4) if a["median_ms"] else None,
-            "comm": comm, "repeats": repeats}
+            "comm": comm, "repeats": repeats,
+            "fixed_work_levels": venv.get("DLNB_GEMM_LEVELS")}
 
 
 def main(argv=None) -> int:
