@@ -72,11 +72,10 @@ def _summary(doc: Dict[str, Any]) -> Dict[str, Any]:
             "backend": doc["global"].get("backend"), "world_size": doc["global"].get("world_size"), "comm": comm}
 
 
-def _start_aggressor(cmd: List[str], n: int, limit_s: float, env: Dict[str, str], log: str) -> subprocess.Popen:
-    f = open(log, "w")
+def _start_aggressor(cmd: List[str], n: int, limit_s: float, env: Dict[str, str], log) -> subprocess.Popen:
     # --loop: iterations until stopped; the launcher's --timeout is the hard stop
     return subprocess.Popen([sys.executable, "-m", "dlnetbench_amd.utils.launch", "-n", str(n), "--timeout",
-                             str(limit_s)] + cmd + ["--loop", "--quiet"], stdout=f, stderr=subprocess.STDOUT,
+                             str(limit_s)] + cmd + ["--loop", "--quiet"], stdout=log, stderr=subprocess.STDOUT,
                             env=env, cwd=ROOT)
 
 
@@ -106,20 +105,24 @@ def run(victim: str, victim_ranks: int, aggressor: str, aggressor_ranks: int, wa
     venv = dict(env)
     if levels:
         venv["DLNB_GEMM_LEVELS"] = ",".join(f"{int(lv['M'])}:{lv['us_per_launch']!r}" for lv in levels)
-    log = tempfile.mktemp(prefix="dlnb_aggressor_", suffix=".log")
+    log = tempfile.TemporaryFile(mode="w+", prefix="dlnb_aggressor_")
+
+    def log_tail() -> str:
+        log.flush()
+        log.seek(0)
+        return log.read()[-800:]
+
     agg = _start_aggressor(acmd, aggressor_ranks, timeout * repeats + warm_s + 60, env, log)
     try:
         time.sleep(warm_s)
         if agg.poll() is not None:
-            raise RuntimeError(f"aggressor exited {agg.returncode} before the victim started: "
-                               + open(log).read()[-800:])
+            raise RuntimeError(f"aggressor exited {agg.returncode} before the victim started: " + log_tail())
         contended = [_summary(_run_victim(vcmd, victim_ranks, timeout, venv)) for _ in range(repeats)]
         running = agg.poll() is None
     finally:
         code = _stop(agg)
-        tail = open(log).read()[-800:] if os.path.exists(log) else ""
-        if os.path.exists(log):
-            os.remove(log)
+        tail = log_tail()
+        log.close()
     if not running:
         raise RuntimeError(f"aggressor stopped while the victim ran (exit {code}): {tail}")
     a = min(alone, key=lambda s: s["median_ms"])
