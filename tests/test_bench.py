@@ -101,6 +101,31 @@ def test_bench_hybrid_blocks_eight_ranks_cpu(tmp_path):
     assert h4["floor_ms"] == pytest.approx((8 + 1) * (2.0 + 4.0) / 2 / 8, rel=1e-3)
 
 
+def test_bench_two_nodes_cpu(tmp_path):
+    """The multi-node launch (torchrun --nnodes 2, 2 ranks per "node", both on
+    127.0.0.1): LOCAL_WORLD_SIZE < WORLD_SIZE, so every phase rendezvouses on
+    MASTER_PORT + 1 + phase instead of a store file; one JSON line from
+    global rank 0, nothing from node 1."""
+    port = _free_port()
+    procs = []
+    for nr in (0, 1):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=2", f"--node-rank={nr}", "--nproc-per-node=2",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+               "--gpus", "4", "--steps", "2", "--warmup", "1", "--backend", "cpu", "--compute", "sleep"] + TINY
+        procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                                      cwd=str(tmp_path), env=dict(os.environ, OMP_NUM_THREADS="1")))
+    outs = [p.communicate(timeout=300) for p in procs]
+    for p, (_, err) in zip(procs, outs):
+        assert p.returncode == 0, err[-3000:]
+    assert _json_lines(outs[1][0]) == []
+    lines = _json_lines(outs[0][0])
+    assert len(lines) == 1, outs[0][0]
+    o = lines[0]
+    assert o["n_gpus"] == 4 and o["config"]["sharding_factor"] == 4 and o["config"]["global_batch"] == 32
+    assert o["exact"] == {"cpu": True, "cpu_eager": True} and "error" not in o["comm_bound"]
+    assert o["effective_busbw_GBps"]["allgather"] > 0
+
+
 def test_bench_single_rank_reports_no_bus_bandwidth(tmp_path):
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "0",
                         "--backend", "cpu", "--compute", "sleep"] + TINY,
