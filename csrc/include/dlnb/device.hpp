@@ -96,7 +96,8 @@ class Device {
   // Zeroed memory that other GPUs' kernels access directly through IPC
   // mappings (GPU: uncached, so a peer's stores are never shadowed by a stale
   // line in this device's L2 and this device's stores reach memory when
-  // they complete). Freed with raw_free. CPU: plain memory.
+  // they complete). Freed with raw_free. CPU: a memfd mapping another
+  // process of this host maps through /proc (cpu_peer_source).
   virtual void* raw_alloc_peer(size_t bytes) { return raw_alloc(bytes); }
   virtual void raw_free(void* p, size_t bytes) = 0;
   // Fill with deterministic pseudo-random values of type t in [-1, 1)
@@ -191,6 +192,11 @@ int gpu_device_count();  // 0 when no GPU / no HIP runtime
 // Text matrix of link type (XGMI / PCIE) and hop count between all visible
 // GPUs plus each GPU's PCI bus id (empty without GPUs).
 std::string describe_gpu_links();
+
+// CPU device peer allocations (Device::alloc_peer on the CPU device): the
+// "/proc/<pid>/fd/<fd>" path another process of this host opens to map the
+// allocation starting at p, or "" when p is not such an allocation.
+std::string cpu_peer_source(const void* p);
 
 // Seconds on a monotonic host clock.
 double now_s();

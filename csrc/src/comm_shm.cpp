@@ -8,6 +8,12 @@
 // segment per communicator: W staging slots + a result region for
 // collectives, and one single-slot mailbox per (src, dst) pair for P2P.
 // Synchronisation is a sense-reversing barrier on futexes in the segment.
+//
+// Zero-copy: buffers allocated with Device::alloc_peer (memfd mappings) and
+// registered with the communicator are mapped by every member, so a
+// collective on them reads and writes the members' buffers directly: an
+// all-reduce moves 2x its bytes per rank (read every member's chunk, write
+// the sum into every member's copy) instead of 4.5x through the staging slots.
 #include <fcntl.h>
 #include <linux/futex.h>
 #include <sched.h>
@@ -18,6 +24,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <deque>
 #include <cstring>
 #include <sstream>
 #include <thread>
@@ -201,7 +208,7 @@ class ShmComm : public Communicator {
  public:
   ShmComm(const std::string& name, const std::vector<int>& members, int my_world_rank, HostGroup& world,
           const std::string& job, size_t capacity, bool p2p)
-      : cap_(round_up(capacity ? capacity : 64, kAlign)), p2p_(p2p) {
+      : world_(&world), job_(job), cap_(round_up(capacity ? capacity : 64, kAlign)), p2p_(p2p) {
     name_ = name;
     members_ = members;
     size_ = static_cast<int>(members.size());
@@ -251,12 +258,73 @@ class ShmComm : public Communicator {
   }
 
   ~ShmComm() override {
+    for (auto& m : mapped_) munmap(m.first, m.second);
     if (base_ && base_ != MAP_FAILED) munmap(base_, total_);
   }
 
   std::string backend_name() const override { return "CPU-SHM"; }
 
+  bool wants_peer_buffers() const override { return size_ > 1; }
+
+  // Collective, paired by order across members (the xgmi backend's rule):
+  // every member maps every other member's k-th registered buffer.
+  void register_buffer(void* p, size_t bytes) override {
+    Reg r;
+    r.local = static_cast<char*>(p);
+    r.bytes = bytes;
+    r.peer.assign(static_cast<size_t>(size_), nullptr);
+    r.peer[static_cast<size_t>(rank_)] = r.local;
+    if (size_ > 1) {
+      const std::string src = cpu_peer_source(p);
+      DLNB_REQUIRE(!src.empty(), "shm backend: register_buffer needs a Device::alloc_peer allocation");
+      std::ostringstream key;
+      key << "shmreg/" << job_ << "/" << name_ << "/";
+      for (int m : members_) key << m << ",";
+      key << "reg" << regs_.size() << "/";
+      world_->store().set(key.str() + std::to_string(rank_), src + " " + std::to_string(bytes));
+      for (int q = 0; q < size_; ++q) {
+        if (q == rank_) continue;
+        std::istringstream in(world_->store().get(key.str() + std::to_string(q)));
+        std::string path;
+        size_t qb = 0;
+        in >> path >> qb;
+        DLNB_REQUIRE(qb == bytes, "shm: registration " << regs_.size() << " of " << name_ << ": rank " << q
+                                                        << " registered " << qb << " B, this rank " << bytes);
+        const int fd = ::open(path.c_str(), O_RDWR);
+        if (fd < 0) DLNB_THROW("shm: cannot open peer buffer " << path << ": " << std::strerror(errno));
+        void* a = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        ::close(fd);
+        if (a == MAP_FAILED) DLNB_THROW("shm: cannot map peer buffer " << path);
+        r.peer[static_cast<size_t>(q)] = static_cast<char*>(a);
+        mapped_.emplace_back(a, bytes);
+      }
+      // every member mapped every buffer before anyone may free one
+      barrier();
+    }
+    regs_.push_back(std::move(r));
+  }
+
   void all_reduce(const void* send, void* recv, size_t count, DType t, Stream& s) override {
+    const size_t bytes = count * dtype_size(t);
+    size_t so = 0, ro = 0;
+    const Reg* rs = find(send, bytes, so);
+    const Reg* rr = find(recv, bytes, ro);
+    if (rs && rr) {
+      enqueue(s, [=] {
+        const size_t es = dtype_size(t);
+        barrier();  // every member's send is ready, its previous use of recv done
+        size_t lo, n;
+        chunk(count, rank_, lo, n);
+        std::vector<const char*> srcs;
+        for (int q = 0; q < size_; ++q) srcs.push_back(rs->peer[static_cast<size_t>(q)] + so);
+        // this rank alone reads and writes chunk `rank_` of every member's buffers
+        par_reduce_sum(t, rr->local + ro + lo * es, srcs, lo, n);
+        for (int q = 0; q < size_; ++q)
+          if (q != rank_) par_copy(rr->peer[static_cast<size_t>(q)] + ro + lo * es, rr->local + ro + lo * es, n * es);
+        barrier();  // every chunk written everywhere; nobody reuses send while a peer reads it
+      });
+      return;
+    }
     enqueue(s, [=] {
       const size_t es = dtype_size(t), bytes = count * es;
       check(bytes);
@@ -272,6 +340,17 @@ class ShmComm : public Communicator {
   }
 
   void all_gather(const void* send, void* recv, size_t send_count, DType t, Stream& s) override {
+    size_t ro = 0;
+    if (const Reg* rr = find(recv, send_count * dtype_size(t) * size_, ro)) {
+      enqueue(s, [=] {
+        const size_t bytes = send_count * dtype_size(t);
+        barrier();
+        for (int q = 0; q < size_; ++q)
+          par_copy(rr->peer[static_cast<size_t>(q)] + ro + static_cast<size_t>(rank_) * bytes, send, bytes);
+        barrier();
+      });
+      return;
+    }
     enqueue(s, [=] {
       const size_t bytes = send_count * dtype_size(t);
       check(bytes);
@@ -283,6 +362,17 @@ class ShmComm : public Communicator {
   }
 
   void reduce_scatter(const void* send, void* recv, size_t recv_count, DType t, Stream& s) override {
+    size_t so = 0;
+    if (const Reg* rs = find(send, recv_count * dtype_size(t) * size_, so)) {
+      enqueue(s, [=] {
+        barrier();
+        std::vector<const char*> srcs;
+        for (int q = 0; q < size_; ++q) srcs.push_back(rs->peer[static_cast<size_t>(q)] + so);
+        par_reduce_sum(t, recv, srcs, recv_count * static_cast<size_t>(rank_), recv_count);
+        barrier();
+      });
+      return;
+    }
     enqueue(s, [=] {
       const size_t es = dtype_size(t), bytes = recv_count * es * size_;
       check(bytes);
@@ -294,6 +384,19 @@ class ShmComm : public Communicator {
   }
 
   void all_to_all(const void* send, void* recv, size_t count, DType t, Stream& s) override {
+    size_t so = 0;
+    const Reg* rs = send != recv ? find(send, count * dtype_size(t) * size_, so) : nullptr;
+    if (rs) {
+      enqueue(s, [=] {
+        const size_t blk = count * dtype_size(t);
+        barrier();
+        for (int q = 0; q < size_; ++q)
+          par_copy(static_cast<char*>(recv) + static_cast<size_t>(q) * blk,
+                   rs->peer[static_cast<size_t>(q)] + so + static_cast<size_t>(rank_) * blk, blk);
+        barrier();
+      });
+      return;
+    }
     enqueue(s, [=] {
       const size_t blk = count * dtype_size(t);
       check(blk * size_);
@@ -405,6 +508,26 @@ class ShmComm : public Communicator {
     wake(&m->taken);
   }
 
+  struct Reg {
+    char* local = nullptr;
+    size_t bytes = 0;
+    std::vector<char*> peer;  // by group rank (own entry = local)
+  };
+  // The registration holding [p, p + bytes) on this rank, with p's offset.
+  const Reg* find(const void* p, size_t bytes, size_t& off) const {
+    const char* c = static_cast<const char*>(p);
+    for (const auto& r : regs_)
+      if (c >= r.local && c + bytes <= r.local + r.bytes) {
+        off = static_cast<size_t>(c - r.local);
+        return &r;
+      }
+    return nullptr;
+  }
+
+  HostGroup* world_ = nullptr;
+  std::string job_;
+  std::deque<Reg> regs_;  // stable addresses: queued tasks hold Reg pointers
+  std::vector<std::pair<void*, size_t>> mapped_;
   size_t cap_;
   bool p2p_;
   char* base_ = nullptr;

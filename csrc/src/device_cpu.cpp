@@ -1,5 +1,8 @@
 #include <sys/mman.h>
 #include <time.h>
+#include <fcntl.h>
+#include <sys/syscall.h>
+#include <cerrno>
 #include <unistd.h>
 
 #include <atomic>
@@ -8,7 +11,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <map>
+#include <mutex>
 #include <set>
+#include <string>
 
 #include "dlnb/device.hpp"
 
@@ -191,6 +197,15 @@ void CpuStream::synchronize() {
 
 namespace {
 
+std::mutex& peer_mu() {
+  static std::mutex m;
+  return m;
+}
+std::map<const void*, int>& peer_fds() {
+  static std::map<const void*, int> m;
+  return m;
+}
+
 class CpuDevice : public Device {
  public:
   explicit CpuDevice(AbortFlag abort) : abort_(std::move(abort)), reg_(std::make_shared<CpuStreamRegistry>()) {}
@@ -211,7 +226,33 @@ class CpuDevice : public Device {
     if (p == MAP_FAILED) DLNB_THROW("host allocation of " << bytes << " bytes failed");
     return p;
   }
-  void raw_free(void* p, size_t bytes) override { munmap(p, bytes); }
+  // Peer memory: an anonymous memfd (no name to leak in /dev/shm if the
+  // process dies), mapped shared; peers open it through /proc/<pid>/fd.
+  void* raw_alloc_peer(size_t bytes) override {
+    const int fd = static_cast<int>(syscall(SYS_memfd_create, "dlnb_peer", 0u));
+    if (fd < 0) DLNB_THROW("memfd_create failed: " << std::strerror(errno));
+    if (ftruncate(fd, static_cast<off_t>(bytes)) != 0) {
+      ::close(fd);
+      DLNB_THROW("ftruncate of a " << bytes << "-byte peer buffer failed");
+    }
+    void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    if (p == MAP_FAILED) {
+      ::close(fd);
+      DLNB_THROW("host peer allocation of " << bytes << " bytes failed");
+    }
+    std::lock_guard<std::mutex> g(peer_mu());
+    peer_fds()[p] = fd;
+    return p;
+  }
+  void raw_free(void* p, size_t bytes) override {
+    munmap(p, bytes);
+    std::lock_guard<std::mutex> g(peer_mu());
+    auto it = peer_fds().find(p);
+    if (it != peer_fds().end()) {
+      ::close(it->second);
+      peer_fds().erase(it);
+    }
+  }
   void fill_random(void* p, size_t count, DType t, uint64_t seed, Stream& s) override {
     auto* cs = dynamic_cast<CpuStream*>(&s);
     cs->enqueue([p, count, t, seed] {
@@ -263,6 +304,13 @@ std::unique_ptr<Device> make_cpu_device(AbortFlag abort) { return std::unique_pt
 
 std::unique_ptr<GraphExec> Device::capture(Stream&, const std::vector<Stream*>&, const std::function<void()>&) {
   DLNB_THROW("--graph needs a GPU device (HIP graphs)");
+}
+
+std::string cpu_peer_source(const void* p) {
+  std::lock_guard<std::mutex> g(peer_mu());
+  auto it = peer_fds().find(p);
+  if (it == peer_fds().end()) return "";
+  return "/proc/" + std::to_string(static_cast<long>(getpid())) + "/fd/" + std::to_string(it->second);
 }
 
 }  // namespace dlnb

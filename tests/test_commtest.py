@@ -39,6 +39,15 @@ def test_cpu_backend_exact(w, dtype):
     assert out[0]["ok"] and out[0]["world_size"] == w and out[0]["backend"] == "CPU-SHM"
 
 
+@pytest.mark.parametrize("w,dtype", [(2, "bf16"), (3, "fp32"), (4, "fp8_e4m3")])
+def test_cpu_backend_registered_exact(w, dtype):
+    """--registered on the shm backend: memfd buffers every member maps, so the
+    collectives read and write the members' buffers directly (all-reduce out of
+    place and in place, all-gather, reduce-scatter, all-to-all), exactly."""
+    out = commtest(w, "--backend", "cpu", "--registered", "--dtype", dtype, "--sizes", "1,7,100,4097,70001")
+    assert out[0]["ok"] and out[0]["registered"] is True and out[0]["backend"] == "CPU-SHM"
+
+
 def test_cpu_backend_bench_lines():
     out = commtest(2, "--backend", "cpu", "--bench", "--sizes", "4096,65536", "--iters", "2", "--warmup", "1")
     ops = {(o["op"], o["count"]) for o in out}
