@@ -353,3 +353,29 @@ def test_prof_merge_busy_on_the_deadline_grid(tmp_path):
     c = prof_merge.merge(rep, [str(pm)])["global"]["dlnb"]["counters"]["classes"]["compute_gemm"]
     assert c["mfma_busy"] == pytest.approx(0.7 * 224 / 256) and c["mfma_busy_on_grid"] == pytest.approx(0.7)
     assert c["grid_cus"] == 224
+
+
+def test_slurm_environment_bootstrap(tmp_path, data_dir, root):
+    """Rank identity from Slurm's variables (SLURM_PROCID / SLURM_NTASKS /
+    SLURM_LOCALID, what srun in scripts/slurm/dlnb.sbatch provides) with the
+    store on DLNB_STORE_ADDR: 2 processes rendezvous and run DP on the CPU
+    backend."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    out = tmp_path / "r.json"
+    procs = []
+    for r in range(2):
+        env = {k: v for k, v in os.environ.items() if not k.startswith(("DLNB_", "RANK", "WORLD_SIZE", "LOCAL_"))}
+        env.update({"SLURM_PROCID": str(r), "SLURM_NTASKS": "2", "SLURM_LOCALID": str(r),
+                    "DLNB_STORE_ADDR": f"127.0.0.1:{port}", "SLURM_TOPOLOGY_ADDR": "root.sw0.node0"})
+        args = [os.path.join(root, "build", "bin", "dp"), "tiny_dense_8_bfloat16", "4", data_dir, "--backend", "cpu",
+                "--compute", "sleep", "-w", "1", "-r", "2", "--quiet"] + (["--json", str(out)] if r == 0 else [])
+        procs.append(subprocess.Popen(args, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    res = [p.communicate(timeout=120) for p in procs]
+    assert all(p.returncode == 0 for p in procs), res[0][1][-1500:] + res[1][1][-1500:]
+    d = json.loads(out.read_text())
+    assert d["global"]["world_size"] == 2 and sorted(r["rank"] for r in d["ranks"]) == [0, 1]
+    assert [r["local_rank"] for r in sorted(d["ranks"], key=lambda r: r["rank"])] == [0, 1]
+
