@@ -348,6 +348,13 @@ __device__ __forceinline__ void reduce_tail(char* out, const char* const* srcs, 
 // --------------------------------------------------------------- kernels
 
 __device__ __forceinline__ int peer_at(const Peers& P, int j) { return (P.rank + j) % P.nranks; }
+// The j-th (0-based) of the n - 1 other ranks this block serves when every
+// peer gets its own block of data: blocks start at different peers, so at
+// any moment a rank's blocks feed all of its xGMI links instead of every
+// block (and so the whole rank) streaming into the same peer.
+__device__ __forceinline__ int peer_rot(const Peers& P, int j) {
+  return peer_at(P, 1 + (j + static_cast<int>(blockIdx.x)) % (P.nranks - 1));
+}
 
 // for (r = 0; r < n; ++r) unrolled to kMaxRanks (see sum_vec)
 #define DLNB_FOR_RANKS(r, lo, n) _Pragma("unroll") for (int r = (lo); r < kMaxRanks; ++r) if (r < (n))
@@ -406,8 +413,8 @@ DLNB_XGMI_KERNEL a2a_kernel(Peers P, CollPiece c) {
   const size_t nv = c.bytes / 16;
   size_t lo, hi;
   blk_range(nv, lo, hi);
-  for (int j = 1; j < P.nranks; ++j) {
-    const int p = peer_at(P, j);
+  for (int j = 0; j + 1 < P.nranks; ++j) {
+    const int p = peer_rot(P, j);
     char* w = P.win[p] + rg + c.slot * P.rank;
     const char* s = c.send + static_cast<size_t>(p) * c.send_stride;
     copy_vec(V(w), V(s), lo, hi);
@@ -438,8 +445,8 @@ DLNB_XGMI_KERNEL rs_kernel(Peers P, CollPiece c) {
   const size_t nv = c.bytes / 16;
   size_t lo, hi;
   blk_range(nv, lo, hi);
-  for (int j = 1; j < P.nranks; ++j) {
-    const int p = peer_at(P, j);
+  for (int j = 0; j + 1 < P.nranks; ++j) {
+    const int p = peer_rot(P, j);
     char* w = P.win[p] + rg + c.slot * P.rank;
     const char* s = c.send + static_cast<size_t>(p) * c.send_stride;
     copy_vec(V(w), V(s), lo, hi);
@@ -489,8 +496,8 @@ DLNB_XGMI_KERNEL ar2_kernel(Peers P, CollPiece c) {
   blk_range(cv, lo, hi);
   auto chunk_hi = [&](int p, size_t h) { return min(h, nv > p * cv ? nv - p * cv : size_t(0)); };
   // 1. chunk p -> peer p's RS slot[rank]
-  for (int j = 1; j < P.nranks; ++j) {
-    const int p = peer_at(P, j);
+  for (int j = 0; j + 1 < P.nranks; ++j) {
+    const int p = peer_rot(P, j);
     copy_vec(V(P.win[p] + rg + c.slot * P.rank), V(c.send) + p * cv, lo, chunk_hi(p, hi));
   }
   exchange(P, 0, ep);
@@ -560,9 +567,10 @@ DLNB_XGMI_KERNEL a2a_direct_kernel(Peers P, DirectPiece c) {
   const size_t nv = c.bytes / 16;
   size_t lo, hi;
   blk_range(nv, lo, hi);
-  // block j of my send -> slot `rank` of rank j's receive buffer (own first, then staggered)
+  // block j of my send -> slot `rank` of rank j's receive buffer; blocks
+  // start at different ranks (own block included) so all links carry data
   for (int j = 0; j < P.nranks; ++j) {
-    const int r = peer_at(P, j);
+    const int r = peer_at(P, (j + static_cast<int>(blockIdx.x)) % P.nranks);
     const char* s = c.src[P.rank] + static_cast<size_t>(r) * c.bytes;
     copy_vec(V(c.dst[r]), V(s), lo, hi);
     copy_tail(c.dst[r], s, nv * 16, c.bytes);
