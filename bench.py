@@ -38,6 +38,11 @@ ride along as extra keys of the same JSON line:
   with its effective bus bandwidth as a ratio of the headline's (RCCL).
   Also a child process per rank, after ``comm_bound_xgmi``.
 
+* ``timeline`` (N > 1): the headline configuration for 2 more iterations
+  with ``--timeline`` (device-clock spans on every rank), summarised: the
+  largest exposed communication of any rank, the fraction of communication
+  that ran under compute, and each collective's mean duration and bus
+  bandwidth on the device clock while the compute ran beside it.
 * ``link_bench`` (N > 1): every collective's bus bandwidth at 16 MB and 128 MB
   per rank on the job's GPUs with nothing else running, over RCCL, the xgmi
   kernels (staged) and the xgmi zero-copy path (``dlnb commtest --bench``,
@@ -348,6 +353,57 @@ def _xgmi_ab(a: argparse.Namespace, world: int, rank: int, c5: dict) -> Dict[str
     return res
 
 
+def _timeline_block(a: argparse.Namespace, world: int, rank: int) -> Dict[str, Any]:
+    """The headline configuration again for 1 + 2 iterations with --timeline
+    (device-clock spans of every collective and compute task on every rank,
+    csrc/src/timeline.cpp), summarised: per rank how much communication ran
+    under compute and how much was exposed, and every collective's duration
+    and bus bandwidth on the device clock while the compute ran beside it."""
+    from dlnetbench_amd.tools import timeline as tlt
+    res: Dict[str, Any] = {"iterations": 2}
+    path = f"/tmp/dlnb_bench.trace_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}.json"
+    try:
+        _child_run(a, world, rank, ".tl", "fsdp", a.model, (a.units, world), a.timeline_timeout,
+                   backend=a.hybrid_backend, graph=a.graph and a.backend in ("auto", "rccl", "xgmi"),
+                   compute=a.compute, warmup=1, runs=2,
+                   schedule=a.schedule, wire_dtype="bf16", timeline=path, timeline_iters=2)
+        if rank != 0:
+            return res
+        ev = tlt.load(path)
+        os.remove(path)
+        bad = tlt.check(ev)
+        s = tlt.summarize(ev)
+        last = str(max(int(i) for r in s.values() for i in r))
+        per = {pid: its[last] for pid, its in s.items() if last in its}
+        res["ranks"] = len(per)
+        res["well_formed"] = not bad
+        res["span_ms_max"] = round(max(r["span_ms"] for r in per.values()), 3)
+        res["comm_exposed_ms_max"] = round(max(r["comm_exposed_ms"] for r in per.values()), 3)
+        busy = sum(r["comm_busy_ms"] for r in per.values())
+        res["comm_hidden_frac"] = round(sum(r["comm_hidden_ms"] for r in per.values()) / busy, 4) if busy else None
+        ops: Dict[str, Any] = {}
+        for e in ev:
+            if e["cat"] == "compute" or str(e["args"].get("iter")) != last:
+                continue
+            op = e["name"].split(" ")[0]
+            o = ops.setdefault(op, {"count": 0, "us": 0.0, "bytes": 0.0, "ranks": e["args"].get("ranks", 1)})
+            o["count"] += 1
+            o["us"] += e["dur"]
+            o["bytes"] += float(e["args"].get("bytes", 0.0))
+        from dlnetbench_amd.parallel.plan import busbw_factor
+        for op, o in ops.items():
+            n = int(o["ranks"])
+            kind = {"all_reduce": "allreduce", "all_gather": "allgather", "reduce_scatter": "reduce_scatter",
+                    "all_to_all": "alltoall"}.get(op, "sendrecv")
+            gbps = o["bytes"] / (o["us"] * 1e3) if o["us"] else None
+            ops[op] = {"count": o["count"], "mean_us": round(o["us"] / o["count"], 1),
+                       "busbw_GBps": round(gbps * busbw_factor(kind, n), 2) if gbps and n > 1 else None}
+        res["ops"] = ops
+    except Exception as e:  # noqa: BLE001
+        res = {"error": str(e)[:300]}
+    return res
+
+
 def _headline_xgmi(a: argparse.Namespace, world: int, rank: int, doc: dict) -> Dict[str, Any]:
     """The headline FSDP step itself over the xgmi kernels (zero-copy
     all-gather / reduce-scatter into registered buffers): its effective bus
@@ -418,6 +474,9 @@ def main() -> int:
     ap.add_argument("--hybrid-timeout", type=float, default=150.0)
     ap.add_argument("--c4-ep-overlap", choices=["on", "off"], default="on",
                     help="also run C4 with --ep-overlap (the all-to-alls off the compute stream)")
+    ap.add_argument("--timeline-block", choices=["auto", "on", "off"], default="auto",
+                    help="headline config with --timeline for 2 iterations, summarised (auto: N > 1 on GPU)")
+    ap.add_argument("--timeline-timeout", type=float, default=120.0)
     ap.add_argument("--link-bench", choices=["auto", "on", "off"], default="auto",
                     help="collective bandwidth of RCCL and the xgmi kernels on the job's GPUs (auto: N > 1 on GPU)")
     ap.add_argument("--link-sizes", default="8388608,67108864", help="--link-bench elements per rank (bf16)")
@@ -567,6 +626,9 @@ def main() -> int:
             extra["hybrid_3d_moe"]["ep_overlap"] = _hybrid_block(
                 a, world, rank, ".c4o", "hybrid_3d_moe", a.c4_model, c4,
                 "GPipe (mb + S - 1)(f_mb + b_mb), BASELINE.md C4", ep_overlap=True)
+    # Device timeline of the headline configuration (every rank's spans).
+    if a.timeline_block == "on" or (a.timeline_block == "auto" and world > 1 and on_gpu):
+        extra["timeline"] = _timeline_block(a, world, rank)
     # Collective bandwidth with nothing else running, RCCL and xgmi.
     if a.link_bench == "on" or (a.link_bench == "auto" and world > 1 and on_gpu):
         extra["link_bench"] = _link_block(a, world, rank, xgmi_exact_ok)

@@ -34,7 +34,7 @@ def test_bench_torchrun_cpu(n, tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", str(n), "--steps", "2", "--warmup", "1", "--backend", "cpu", "--compute", "sleep",
-           "--link-bench", "on", "--link-sizes", "4096,65536"] + TINY
+           "--link-bench", "on", "--link-sizes", "4096,65536", "--timeline-block", "on"] + TINY
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=str(tmp_path),
                        env=dict(os.environ, OMP_NUM_THREADS="1"))
     assert p.returncode == 0, p.stderr[-3000:]
@@ -63,6 +63,12 @@ def test_bench_torchrun_cpu(n, tmp_path):
     assert lb["elements_per_rank"] == [4096, 65536] and "error" not in lb["cpu"], lb
     for op in ("all_reduce", "all_gather", "reduce_scatter", "all_to_all", "sendrecv"):
         assert lb["cpu"][op]["65536"]["busbw_GBps"] > 0 and lb["cpu"][op]["4096"]["time_us"] > 0
+    # the headline config's device timeline, summarised (every rank, last iteration)
+    tl = o["timeline"]
+    assert "error" not in tl, tl
+    assert tl["ranks"] == n and tl["well_formed"] and 0 <= tl["comm_hidden_frac"] <= 1
+    assert tl["ops"]["all_gather"]["count"] == 7 * n and tl["ops"]["reduce_scatter"]["count"] == 4 * n
+    assert tl["ops"]["all_gather"]["busbw_GBps"] > 0 and tl["span_ms_max"] > 0
 
 
 def test_bench_hybrid_blocks_eight_ranks_cpu(tmp_path):
@@ -208,6 +214,9 @@ def test_bench_torchrun_xgmi_two_ranks_one_gpu(tmp_path):
     assert "error" not in h, h
     assert h["ms_per_step"] > 0 and h["effective_busbw_GBps"]["allgather"] > 0
     assert h["busbw_ratio_vs_headline"]["allgather"] > 0 and h["headline_backend"] == "XGMI"
+    tl = o["timeline"]  # the headline config's device timeline over the xgmi kernels, HIP graph
+    assert "error" not in tl and tl["ranks"] == 2 and tl["well_formed"], tl
+    assert tl["ops"]["all_gather"]["busbw_GBps"] > 0
     lb = o["link_bench"]  # staged and zero-copy xgmi; no RCCL with 2 ranks on one GPU
     assert "rccl" not in lb and lb["hip_graph"] is True
     for k in ("xgmi", "xgmi_registered"):
