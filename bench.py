@@ -38,6 +38,8 @@ ride along as extra keys of the same JSON line:
   with its effective bus bandwidth as a ratio of the headline's (RCCL).
   Also a child process per rank, after ``comm_bound_xgmi``.
 
+* ``model_fit`` (N > 1): the cost model's eta and alpha fitted to the
+  link_bench times, and every block's prediction redone with them.
 * ``timeline`` (N > 1): the headline configuration for 2 more iterations
   with ``--timeline`` (device-clock spans on every rank), summarised: the
   largest exposed communication of any rank, the fraction of communication
@@ -288,6 +290,38 @@ def _predicted_ms(a: argparse.Namespace, world: int, strategy: str, model: str, 
         return round(predict(strategy, model, list(params), world, base=a.base_path, **kw)["iter_ms"], 3)
     except Exception:  # noqa: BLE001
         return None
+
+
+def _model_fit(a: argparse.Namespace, world: int, extra: Dict[str, Any]) -> Optional[Dict[str, Any]]:
+    """The cost model refitted to this node: eta and alpha from the measured
+    link_bench times (xgmi_model.fit_link_model), then every block's
+    prediction again with them - what the links measured here say the
+    strategies should take."""
+    try:
+        from dlnetbench_amd.parallel.xgmi_model import fit_link_model
+        lb = extra["link_bench"]
+        key = next((k for k in ("rccl", "xgmi_registered", "xgmi", "cpu") if isinstance(lb.get(k), dict)
+                    and "error" not in lb[k] and lb[k]), None)
+        if key is None:
+            return None
+        f = fit_link_model(lb[key], world)
+        if not f.get("eta"):
+            return None
+        kw = {"eta": f["eta"], "alpha_us": f["alpha_us"]}
+        pred: Dict[str, Any] = {"headline": _predicted_ms(a, world, "fsdp", a.model, (a.units, world), **kw)}
+        if "comm_bound" in extra:
+            pred["comm_bound"] = _predicted_ms(a, world, "dp", a.c5_model, (a.c5_buckets,), wire=a.c5_wire, **kw)
+        for name, model, params, ov in (("hybrid_3d", a.c3_model, a.c3, False),
+                                        ("hybrid_3d_moe", a.c4_model, a.c4, False),
+                                        ("hybrid_3d_moe_ep_overlap", a.c4_model, a.c4, True)):
+            if name.split("_ep_")[0] in extra:
+                strat = "hybrid_3d" if name == "hybrid_3d" else "hybrid_3d_moe"
+                pred[name] = _predicted_ms(a, world, strat, model, tuple(int(x) for x in params.split(",")),
+                                           ep_overlap=ov, **kw)
+        return {"backend": key, "eta": f["eta"], "alpha_us": f["alpha_us"], "per_op": f["per_op"],
+                "predicted_ms": pred}
+    except Exception as e:  # noqa: BLE001
+        return {"error": str(e)[:300]}
 
 
 def _hybrid_block(a: argparse.Namespace, world: int, rank: int, tag: str, strategy: str, model: str,
@@ -695,6 +729,10 @@ def main() -> int:
     if "comm_bound" in extra and "error" not in extra["comm_bound"]:
         extra["comm_bound"]["predicted_ms"] = _predicted_ms(a, world, "dp", a.c5_model, (a.c5_buckets,),
                                                             wire=a.c5_wire)
+    if "link_bench" in extra:
+        fit = _model_fit(a, world, extra)
+        if fit:
+            out["model_fit"] = fit
     out.update(exact)
     out.update(extra)
     print(json.dumps(out), flush=True)

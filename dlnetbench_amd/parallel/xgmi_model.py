@@ -234,3 +234,50 @@ def predict_hybrid(p: Plan, model: LinkModel, algo: str = "direct", pp_virtual: 
     end = span + tail
     return {"iter_ms": end / 1e3, "floor_ms": floor / 1e3, "exposed_ms": (end - floor) / 1e3,
             "inner_comm_per_op_us": inner, "sendrecv_us": link, "tail_allreduce_us": tail}
+
+
+_FIT_OPS = {"all_reduce": "allreduce", "all_gather": "allgather", "reduce_scatter": "reduce_scatter",
+            "all_to_all": "alltoall", "sendrecv": "sendrecv"}
+
+
+def fit_link_model(lb: Dict[str, Dict[str, Dict[str, float]]], world: int, es: int = 2,
+                   link_gbps: float = 153.0) -> Dict[str, object]:
+    """eta and alpha of the direct-collective model from measured collective
+    times: bench.py's link_bench for one backend ({op: {elements per rank:
+    {"time_us", ...}}}, `dlnb commtest --bench` conventions). Every op's time
+    is linear in its bytes under the model, t = steps * alpha + k * bytes /
+    (B * eta) (k = 1/n for all-gather / reduce-scatter / all-to-all, 2/n for
+    all-reduce, 1 for send/recv; steps 1 or 2), so two sizes give one
+    (alpha, eta) per op; the medians over ops are the fit."""
+    import statistics
+    n = world
+    per_op = {}
+    for op, kind in _FIT_OPS.items():
+        pts = []
+        for count, v in (lb.get(op) or {}).items():
+            if not isinstance(v, dict) or not v.get("time_us"):
+                continue
+            c = float(count)
+            nbytes = c * es * (n if kind in ("allgather", "reduce_scatter", "alltoall") else 1)
+            pts.append((nbytes, float(v["time_us"])))
+        if len(pts) < 2 or n < 2:
+            continue
+        xs, ys = zip(*sorted(pts))
+        mx, my = sum(xs) / len(xs), sum(ys) / len(ys)
+        sxx = sum((x - mx) ** 2 for x in xs)
+        if sxx <= 0:
+            continue
+        slope = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sxx  # us per byte
+        icpt = my - slope * mx
+        if slope <= 0:
+            continue
+        k = 1.0 if kind == "sendrecv" else (2.0 / n if kind == "allreduce" else 1.0 / n)
+        steps = 2.0 if kind == "allreduce" else 1.0
+        eta = k / (slope * link_gbps * 1e3)
+        per_op[op] = {"eta": round(eta, 4), "alpha_us": round(max(0.0, icpt / steps), 2)}
+    if not per_op:
+        return {"eta": None, "alpha_us": None, "per_op": per_op}
+    return {"eta": round(statistics.median(v["eta"] for v in per_op.values()), 4),
+            "alpha_us": round(statistics.median(v["alpha_us"] for v in per_op.values()), 2),
+            "per_op": per_op}
+

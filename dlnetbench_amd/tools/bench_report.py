@@ -103,6 +103,8 @@ def rows(lines: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
             "c4_vs_floor": _get(d, "hybrid_3d_moe", "vs_floor"),
             "c4_overlap_ms": _get(d, "hybrid_3d_moe", "ep_overlap", "ms_per_step"),
             "predicted_ms": d.get("predicted_ms"),
+            "fit_eta": _get(d, "model_fit", "eta"),
+            "fit_predicted_ms": _get(d, "model_fit", "predicted_ms", "headline"),
             "tl_exposed_max_ms": _get(d, "timeline", "comm_exposed_ms_max"),
             "tl_hidden_frac": _get(d, "timeline", "comm_hidden_frac"),
             "link_ar_busbw_rccl": _largest(_get(d, "link_bench", "rccl", "all_reduce")),

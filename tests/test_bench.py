@@ -63,6 +63,10 @@ def test_bench_torchrun_cpu(n, tmp_path):
     assert lb["elements_per_rank"] == [4096, 65536] and "error" not in lb["cpu"], lb
     for op in ("all_reduce", "all_gather", "reduce_scatter", "all_to_all", "sendrecv"):
         assert lb["cpu"][op]["65536"]["busbw_GBps"] > 0 and lb["cpu"][op]["4096"]["time_us"] > 0
+    # the cost model refitted to the measured collective times, predictions redone with it
+    mf = o["model_fit"]
+    assert "error" not in mf and mf["backend"] == "cpu" and mf["eta"] > 0 and mf["alpha_us"] >= 0, mf
+    assert mf["predicted_ms"]["headline"] > 0 and mf["predicted_ms"]["comm_bound"] > 0
     # the headline config's device timeline, summarised (every rank, last iteration)
     tl = o["timeline"]
     assert "error" not in tl, tl

@@ -330,3 +330,21 @@ def test_ep_overlap_op_model():
     assert _ep_overlap_op_us(100.0, 4, 5.0) == pytest.approx(105.0)
     # all-to-all longer than the other half's slice: the lane is the bound
     assert _ep_overlap_op_us(100.0, 4, 50.0) == pytest.approx(12.5 + 8 * 50.0)
+
+
+def test_link_model_fit_round_trip():
+    """fit_link_model recovers eta and alpha from collective times the model
+    itself generated at two sizes (the link_bench layout bench.py reports)."""
+    from dlnetbench_amd.parallel import xgmi_model as xm
+    truth = xm.LinkModel(eta=0.55, alpha_us=25.0)
+    for world in (2, 4, 8):
+        lb = {}
+        for op, kind in xm._FIT_OPS.items():
+            for c in (8388608, 67108864):
+                nb = c * 2 * (world if kind in ("allgather", "reduce_scatter", "alltoall") else 1)
+                lb.setdefault(op, {})[str(c)] = {"time_us": truth.coll_us(kind, nb, world if kind != "sendrecv" else 2)}
+        f = xm.fit_link_model(lb, world)
+        assert f["eta"] == pytest.approx(0.55, rel=1e-3) and f["alpha_us"] == pytest.approx(25.0, abs=0.05)
+        assert set(f["per_op"]) == set(xm._FIT_OPS)
+    assert xm.fit_link_model({"all_reduce": {"8": {"time_us": 5.0}}}, 8)["eta"] is None  # one size: no fit
+
