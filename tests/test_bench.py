@@ -183,6 +183,8 @@ def test_bench_gpu_single_rank_secondaries(tmp_path):
     assert 0.8 < c5["gemm_work"]["compute_stretch"] < 1.5, c5
     assert 0.8 < o["compute_stretch"] < 1.5, o
     assert o["rccl_cta_budget"]["applies"] and o["rccl_cta_budget"]["max_ctas_per_lane"] == 32
+    # the bench binds /opt/rocm's HIP and RCCL (torch's bundled copies never load: DLNB_NO_TORCH)
+    assert o["runtime"]["librccl"].startswith("/opt/rocm") and o["runtime"]["libamdhip64"].startswith("/opt/rocm")
     # the comm-bound step again with RCCL's own CTA count (no maxCTAs cap)
     u = c5["rccl_default_ctas"]
     assert "error" not in u, u

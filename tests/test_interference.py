@@ -48,8 +48,8 @@ def test_interference_same_gpu():
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    r = interference.run(f"fsdp tiny_dense_8_bfloat16 4 1 {DATA} --backend rccl --compute gemm-work -w 1 -r 3", 1,
-                         f"dp tiny_dense_8_bfloat16 4 {DATA} --backend rccl --compute gemm", 1, warm_s=3.0,
+    r = interference.run(f"fsdp tiny_dense_8_bfloat16 4 1 {DATA} --backend rccl --compute gemm-work -w 1 -r 2", 1,
+                         f"dp tiny_dense_8_bfloat16 4 {DATA} --backend rccl --compute gemm", 1, warm_s=2.0,
                          timeout=120)
     assert r["alone"]["backend"] == "RCCL" and r["slowdown"] > 0.95, r
     assert r["fixed_work_levels"]  # the contended run reused the alone calibration (DLNB_GEMM_LEVELS)
