@@ -528,6 +528,11 @@ def main() -> int:
     # 3 minutes is hung - abort it and fall back (graph retry / error key)
     # instead of waiting out the runtime's 15-minute default.
     os.environ.setdefault("DLNB_TIMEOUT", "180")
+    # Rendezvous / host-barrier waits: ranks run the phases in lockstep (the
+    # worst legitimate skew is a communicator setup, seconds), so a rank that
+    # waits 5 minutes for a peer means the peer failed - stop there rather than
+    # after the store's 15-minute default.
+    os.environ.setdefault("DLNB_STORE_TIMEOUT", "300")
     # Everything below is native (HIP + RCCL from /opt/rocm); torch is not needed.
     os.environ.setdefault("DLNB_NO_TORCH", "1")
     # Multi-rank: prove the collectives exact on these ranks before timing them.
