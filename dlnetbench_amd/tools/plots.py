@@ -12,6 +12,7 @@ colour/marker maps, zoom insets, :15-209). Inputs here are sweep JSONL files
     python -m dlnetbench_amd.tools.plots pareto results.jsonl -o pareto.png
     python -m dlnetbench_amd.tools.plots knobs results.jsonl -o knobs.png [--metric barrier]
     python -m dlnetbench_amd.tools.plots knobs-pareto results.jsonl -o knobs_pareto.png
+    python -m dlnetbench_amd.tools.plots timeline trace.json -o timeline.png [--iter N]
 
 Collective-library knobs (the reference's PROTOCOL x ALGO and THREADS x
 CHANNELS axes, plot_dp.py:23-26) are read from each sweep point's
@@ -344,13 +345,59 @@ def plot_pareto(recs: List[dict], out: str) -> None:
     fig.savefig(out, dpi=150)
 
 
+def plot_timeline(trace: str, out: str, iteration=None) -> Dict[str, int]:
+    """Gantt chart of a --timeline trace (csrc/src/timeline.cpp): one row per
+    (rank, stream), compute spans in grey, collectives coloured by operation,
+    one iteration (the last one by default). Returns spans drawn per category."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    with open(trace) as f:
+        doc = json.load(f)
+    ev = [e for e in doc["traceEvents"] if e.get("ph") == "X"]
+    names = {(m["pid"], m["tid"]): m["args"]["name"] for m in doc["traceEvents"]
+             if m.get("ph") == "M" and m.get("name") == "thread_name"}
+    if iteration is None:
+        iteration = max((e["args"]["iter"] for e in ev), default=0)
+    ev = [e for e in ev if e["args"]["iter"] == iteration]
+    rows = sorted({(e["pid"], e["tid"]) for e in ev})
+    t0 = min((e["ts"] for e in ev), default=0.0)
+    ops = sorted({e["name"].split(" ")[0] for e in ev if e["cat"] != "compute"})
+    colors = create_color_map(ops)
+    fig, ax = plt.subplots(figsize=(12, 0.4 * len(rows) + 1.5))
+    drawn: Dict[str, int] = {}
+    for e in ev:
+        y = rows.index((e["pid"], e["tid"]))
+        op = e["name"].split(" ")[0]
+        c = "0.75" if e["cat"] == "compute" else colors[op]
+        ax.barh(y, e["dur"] / 1e3, left=(e["ts"] - t0) / 1e3, color=c, edgecolor="none", height=0.8)
+        drawn[e["cat"]] = drawn.get(e["cat"], 0) + 1
+    ax.set_yticks(range(len(rows)))
+    ax.set_yticklabels([f"r{p} {names.get((p, t), t)}" for p, t in rows], fontsize=7)
+    ax.invert_yaxis()
+    ax.set_xlabel("ms")
+    ax.set_title(f"{doc.get('otherData', {}).get('strategy', '')} iteration {iteration}")
+    import matplotlib.patches as mpatches
+    handles = [mpatches.Patch(color="0.75", label="compute")] + [mpatches.Patch(color=colors[o], label=o) for o in ops]
+    ax.legend(handles=handles, fontsize=7, loc="upper right")
+    fig.tight_layout()
+    fig.savefig(out, dpi=150)
+    plt.close(fig)
+    return drawn
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("kind", choices=["scaling", "barrier", "pareto", "knobs", "knobs-pareto"])
+    ap.add_argument("kind", choices=["scaling", "barrier", "pareto", "knobs", "knobs-pareto", "timeline"])
     ap.add_argument("inputs", nargs="+")
     ap.add_argument("-o", "--out", default="plot.png")
     ap.add_argument("--metric", choices=["runtime", "barrier"], default="runtime", help="knobs: y axis")
+    ap.add_argument("--iter", type=int, default=None, help="timeline: iteration (default: the last)")
     a = ap.parse_args(argv)
+    if a.kind == "timeline":
+        plot_timeline(a.inputs[0], a.out, a.iter)
+        print(a.out)
+        return 0
     recs = [r for p in a.inputs for r in load_records(p)]
     if a.kind == "knobs":
         plot_knobs(recs, a.out, a.metric)

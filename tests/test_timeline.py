@@ -47,6 +47,9 @@ def test_fsdp_timeline_two_processes(tmp_path):
     assert {e["args"]["iter"] for e in ev} == {1, 2}
     names = {m["args"]["name"] for m in doc["traceEvents"] if m["ph"] == "M" and m["name"] == "thread_name"}
     assert "compute" in names and any(n.startswith("comm: fsdp/") for n in names)
+    from dlnetbench_amd.tools import plots
+    drawn = plots.plot_timeline(str(out), str(tmp_path / "tl.png"))
+    assert drawn == {"comm": 2 * 11, "compute": 2 * 8} and (tmp_path / "tl.png").stat().st_size > 0
     g = json.loads(rep.read_text())["global"]["dlnb"]["timeline"]
     assert g["events"] == len(ev) and g["truncated"] is False and g["path"] == str(out)
     s = tlt.summarize(ev)
