@@ -203,14 +203,16 @@ def test_plan_cli(capsys, root):
     assert d["params"]["num_tensor_shards"] == 4
 
 
-@pytest.mark.parametrize("prog,args", [("fsdp", ["tiny_dense_8_bfloat16", "4", "2"]),
-                                       ("hybrid_3d_moe", ["tiny_moe_8_bfloat16", "2", "2", "1"]),
-                                       ("hybrid_3d", ["tiny_dense_8_bfloat16", "2", "2", "1"])])
-def test_asan_build_is_clean(prog, args, asan_bindir, data_dir):
-    """Host AddressSanitizer build (make asan, built on demand): no memory errors in the runtime."""
+@pytest.mark.parametrize("prog,args,extra", [("fsdp", ["tiny_dense_8_bfloat16", "4", "2"], ["--timeline", "{tmp}"]),
+                                             ("hybrid_3d_moe", ["tiny_moe_8_bfloat16", "2", "2", "1"], []),
+                                             ("hybrid_3d", ["tiny_dense_8_bfloat16", "2", "2", "1"], [])])
+def test_asan_build_is_clean(prog, args, extra, asan_bindir, data_dir, tmp_path):
+    """Host AddressSanitizer build (make asan, built on demand): no memory errors in the runtime (the fsdp
+    case: zero-copy shared-memory collectives on registered buffers, with the device timeline on)."""
     b = os.path.join(asan_bindir, prog)
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1")
-    code, outs = launch.launch(2, [b, *args, data_dir, "--quiet", "-w", "1", "-r", "2"], timeout=120,
+    extra = [x.replace("{tmp}", str(tmp_path / "tl.json")) for x in extra]
+    code, outs = launch.launch(2, [b, *args, data_dir, "--quiet", "-w", "1", "-r", "2", *extra], timeout=120,
                                capture=True, env=env)
     text = "".join(o or "" for o in outs)
     assert code == 0 and "AddressSanitizer" not in text, text[-3000:]
@@ -219,7 +221,8 @@ def test_asan_build_is_clean(prog, args, asan_bindir, data_dir):
 @pytest.mark.parametrize("prog,args,extra", [("fsdp", ["tiny_dense_8_bfloat16", "4", "4"], []),
                                              ("hybrid_2d", ["tiny_deep_8_bfloat16", "4", "8"],
                                               ["--pp-schedule", "interleaved"]),
-                                             ("hybrid_3d_moe", ["tiny_moe_8_bfloat16", "2", "4", "2"], ["--ep-overlap"])])
+                                             ("hybrid_3d_moe", ["tiny_moe_8_bfloat16", "2", "4", "2"],
+                                              ["--ep-overlap", "--timeline", "/dev/null"])])
 def test_tsan_loopback_threads_race_free(prog, args, extra, tsan_bindir, data_dir):
     """Host ThreadSanitizer build (make tsan, built on demand): 8 loopback rank threads on the CPU device,
     no data races."""
