@@ -229,7 +229,7 @@ XGMI_GRAPH_STRATS = [
     ("dp", "tiny_dense_8_bfloat16", ["4"], [], 2),
     ("fsdp", "tiny_dense_8_bfloat16", ["4", "4"], [], 4),
     ("hybrid_2d", "tiny_dense_8_bfloat16", ["2", "4"], ["--pp-schedule", "1f1b"], 2),
-    ("hybrid_3d_moe", "tiny_moe_8_bfloat16", ["2", "2", "2"], [], 4),
+    ("hybrid_3d_moe", "tiny_moe_8_bfloat16", ["1", "2", "2"], [], 2),  # captured EP all-to-alls
 ]
 
 
