@@ -4,8 +4,9 @@
     python -m dlnetbench_amd bench-report runs.jsonl --csv scaling.csv
 
 Every input holds bench.py JSON lines (a file with one line, a JSONL of
-several, or a JSON array of them); other lines are skipped, so a captured
-stdout works as is. Rows are sorted by ``n_gpus``. Columns: the headline
+several, a JSON array of them, or any JSON document that nests them, e.g. a
+driver's scaling record); other lines are skipped, so a captured stdout
+works as is. Rows are sorted by ``n_gpus``. Columns: the headline
 iteration and its weak-scaling efficiency against the smallest N
 (T_min / T_N; the headline keeps per-GPU work fixed), the headline's
 all-gather / reduce-scatter bus bandwidth, and the secondary blocks when
@@ -27,13 +28,36 @@ import sys
 from typing import Any, Dict, Iterable, List, Optional
 
 
+def _walk(obj: Any) -> Iterable[Dict[str, Any]]:
+    """Every dict inside a JSON document that looks like a bench.py line
+    (a driver's scaling record may nest the per-N lines at any depth)."""
+    if isinstance(obj, dict):
+        if "metric" in obj and "n_gpus" in obj and "value" in obj:
+            yield obj
+            return
+        for v in obj.values():
+            yield from _walk(v)
+    elif isinstance(obj, list):
+        for v in obj:
+            yield from _walk(v)
+    elif isinstance(obj, str) and '"metric"' in obj:
+        yield from _lines(obj)  # a captured stdout kept as a string
+
+
 def _lines(text: str) -> Iterable[Dict[str, Any]]:
     text = text.strip()
-    if text.startswith("["):
-        for d in json.loads(text):
-            if isinstance(d, dict):
-                yield d
-        return
+    if text.startswith("[") or (text.startswith("{") and "\n" not in text.rstrip()):
+        try:
+            yield from _walk(json.loads(text))
+            return
+        except json.JSONDecodeError:
+            pass
+    elif text.startswith("{"):
+        try:  # one pretty-printed document
+            yield from _walk(json.loads(text))
+            return
+        except json.JSONDecodeError:
+            pass
     for ln in text.splitlines():
         ln = ln.strip()
         if not ln.startswith("{"):
@@ -42,8 +66,7 @@ def _lines(text: str) -> Iterable[Dict[str, Any]]:
             d = json.loads(ln)
         except json.JSONDecodeError:
             continue
-        if isinstance(d, dict):
-            yield d
+        yield from _walk(d)
 
 
 def load(paths: List[str]) -> List[Dict[str, Any]]:

@@ -76,3 +76,14 @@ def test_exactness_and_hybrid_columns():
     assert r["rccl_nranks"] == 8 and r["c3_vs_floor"] == 1.02 and r["c4_ms"] == 15000.0
     r1 = bench_report.rows([json.loads(_line(1, 2816.0))])[0]
     assert r1["exact_rccl"] is None and r1["rccl_nranks"] is None and r1["c3_ms"] is None
+
+
+def test_nested_scaling_record(tmp_path):
+    """A driver-style record that nests the per-N lines (as dicts or inside a captured stdout string)."""
+    one = json.loads(_line(1, 2816.0))
+    eight = json.loads(_line(8, 2818.0))
+    doc = {"runs": [{"n": 1, "result": one}, {"n": 8, "stdout": "[bench] noise\n" + json.dumps(eight) + "\n"}]}
+    p = tmp_path / "scale.json"
+    p.write_text(json.dumps(doc, indent=1))
+    assert [d["n_gpus"] for d in bench_report.load([str(p)])] == [1, 8]
+
