@@ -75,7 +75,14 @@ def load(paths: List[str]) -> List[Dict[str, Any]]:
     for p in paths:
         with (sys.stdin if p == "-" else open(p)) as f:
             out += [d for d in _lines(f.read()) if "metric" in d and "n_gpus" in d and "value" in d]
-    return sorted(out, key=lambda d: d["n_gpus"])
+    # one run may appear twice in a record (the captured line and a parsed
+    # copy of part of it): keep the fullest copy of each
+    best: Dict[tuple, Dict[str, Any]] = {}
+    for d in out:
+        k = (d["n_gpus"], d["value"], d.get("steps"))
+        if k not in best or len(d) > len(best[k]):
+            best[k] = d
+    return sorted(best.values(), key=lambda d: d["n_gpus"])
 
 
 def _get(d: Optional[dict], *keys: str) -> Any:
