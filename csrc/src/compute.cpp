@@ -91,7 +91,11 @@ class GpuCompute : public ComputeEngine {
     const int kmul = dtype_ == DType::FP8_E4M3 ? 256 : 128;
     K_ = std::min(65536, std::max(512, (shape.ffn + kmul - 1) / kmul * kmul));
     N_ = std::min(32768, std::max(1024, (shape.hidden + 255) / 256 * 256));
-    if (mode_ != ComputeMode::Sleep && mode_ != ComputeMode::Spin) calibrate();
+    // GEMM operands for every GEMM mode; the launch-time calibration only for
+    // the fixed-work modes (a deadline task lasts its table time whatever a
+    // launch costs, so the gemm mode skips the ~0.6 s of measuring).
+    if (mode_ != ComputeMode::Sleep && mode_ != ComputeMode::Spin) alloc_operands();
+    if (mode_ == ComputeMode::GemmWork || mode_ == ComputeMode::Flops) calibrate();
     if (mode_ == ComputeMode::Gemm) {
       slots_ = dev_.alloc(kSlots * 64);
       // Leave `comm_cus` CUs to collectives: one 128-KiB-LDS block fits per
@@ -212,10 +216,12 @@ class GpuCompute : public ComputeEngine {
       j["deadline_slice_us"] = slice_us_;
       j["chained_tasks"] = chained_;  // enqueued so far (a captured graph counts its one iteration)
     }
-    if (!levels_.empty()) {
+    if (A_.data()) {
       j["gemm_dtype"] = dtype_name(dtype_);
       j["gemm_N"] = N_;
       j["gemm_K"] = K_;
+    }
+    if (!levels_.empty()) {
       Json lv = Json::array();
       for (const auto& l : levels_) {
         Json e = Json::object();
@@ -258,7 +264,7 @@ class GpuCompute : public ComputeEngine {
     return slots_.as<uint64_t>() + idx * 8;  // one 64-B line per stream
   }
 
-  void calibrate() {
+  void alloc_operands() {
     const int Mmax = kMmax;
     const size_t esz = dtype_size(dtype_);
     A_ = dev_.alloc(static_cast<size_t>(Mmax) * K_ * esz);
@@ -267,6 +273,12 @@ class GpuCompute : public ComputeEngine {
     auto s = dev_.create_stream(false);
     dev_.fill_random(A_.data(), static_cast<size_t>(Mmax) * K_, dtype_, 1, *s);
     dev_.fill_random(B_.data(), static_cast<size_t>(N_) * K_, dtype_, 2, *s);
+    s->synchronize();
+  }
+
+  void calibrate() {
+    const int Mmax = kMmax;
+    auto s = dev_.create_stream(false);
     // DLNB_GEMM_LEVELS="M:us,M:us,..." reuses an earlier calibration (the
     // report's compute.gemm_levels) instead of measuring: a fixed-work run
     // beside other jobs (tools/interference.py) must do the work it would do
