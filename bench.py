@@ -404,7 +404,6 @@ def _timeline_block(a: argparse.Namespace, world: int, rank: int) -> Dict[str, A
         if rank != 0:
             return res
         ev = tlt.load(path)
-        os.remove(path)
         bad = tlt.check(ev)
         s = tlt.summarize(ev)
         last = str(max(int(i) for r in s.values() for i in r))
@@ -435,6 +434,9 @@ def _timeline_block(a: argparse.Namespace, world: int, rank: int) -> Dict[str, A
         res["ops"] = ops
     except Exception as e:  # noqa: BLE001
         res = {"error": str(e)[:300]}
+    finally:
+        if rank == 0 and os.path.exists(path):
+            os.remove(path)
     return res
 
 
