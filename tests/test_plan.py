@@ -348,3 +348,13 @@ def test_link_model_fit_round_trip():
         assert set(f["per_op"]) == set(xm._FIT_OPS)
     assert xm.fit_link_model({"all_reduce": {"8": {"time_us": 5.0}}}, 8)["eta"] is None  # one size: no fit
 
+
+
+@pytest.mark.parametrize("sched", ["gpipe", "1f1b", "interleaved", "dualpipe"])
+def test_hybrid_predictions_every_schedule(root, sched):
+    """Every pipeline schedule of hybrid_2d and hybrid_4d simulates to completion with real link times
+    (no deadlock in the model) and lands at or above its compute floor."""
+    for strat, model, params in (("hybrid_2d", "llama3_8b_16_bfloat16", [4, 8]),
+                                 ("hybrid_4d", "mixtral_8x7b_16_bfloat16", [2, 16, 2, 2])):
+        r = P.predict(strat, model, params, 8, base=root, pp_schedule=sched, pp_virtual=2)
+        assert r["iter_ms"] >= r["floor_ms"] > 0 and r["sendrecv_us"] > 0
