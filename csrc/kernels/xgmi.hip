@@ -304,18 +304,38 @@ struct Elt<DType::FP8_E5M2> : Fp8<true> {};
 // a run-time count: the per-rank pointer arrays then stay in (scalar)
 // registers instead of going to scratch under the 64-register cap.
 
-// Sum of vector i over the first ns sources, unpacked into acc (fp32).
+// Sum of vector i over the first ns sources, unpacked into acc (fp32), in
+// source order. The loads of a group of G sources are issued before the first
+// is used: on a node 7 of 8 sources are a peer's memory across xGMI (round
+// trips of microseconds), and loading one source at a time (what the
+// compiler made of a load-add loop: a vmcnt(0) after every load) left each
+// thread with a single request in flight. G = 8 (all ranks) where the
+// unpacked vector is <= 8 floats, 4 for fp8 (16 floats; 8 loads would not
+// fit the 64-register budget beside two 16-float arrays).
 template <DType D>
 __device__ __forceinline__ void sum_vec(float* acc, const uint4* const* srcs, int ns, size_t i) {
   using E = Elt<D>;
+  constexpr int G = E::N <= 8 ? 8 : 4;
   float f[E::N];
-  E::unpack(srcs[0][i], acc);
 #pragma unroll
-  for (int s = 1; s < kMaxRanks; ++s) {
-    if (s < ns) {
-      E::unpack(srcs[s][i], f);
+  for (int g = 0; g < kMaxRanks; g += G) {
+    if (g < ns) {
+      uint4 v[G];
 #pragma unroll
-      for (int k = 0; k < E::N; ++k) acc[k] += f[k];
+      for (int u = 0; u < G; ++u)
+        if (g + u < ns) v[u] = srcs[g + u][i];
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        if (g + u < ns) {
+          if (g + u == 0) {
+            E::unpack(v[u], acc);
+          } else {
+            E::unpack(v[u], f);
+#pragma unroll
+            for (int k = 0; k < E::N; ++k) acc[k] += f[k];
+          }
+        }
+      }
     }
   }
 }
