@@ -546,6 +546,11 @@ def main() -> int:
         if rank == 0:
             print(f"[bench] exactness: {json.dumps(exact)}", file=sys.stderr)
     xgmi_exact_ok = not exact or bool(exact.get("exact", {}).get("xgmi", False))
+    # The xgmi blocks run with the release mode the pass proved exact on these
+    # ranks (the system-scope one when the default vmcnt hand-off failed).
+    rel = (exact.get("exact_detail") or {}).get("xgmi_release")
+    if xgmi_exact_ok and rel:
+        os.environ["DLNB_XGMI_RELEASE"] = rel
 
     from dlnetbench_amd import engine
     from dlnetbench_amd.utils.stats import load_stats
