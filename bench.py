@@ -277,6 +277,26 @@ def _exact_block(a: argparse.Namespace, world: int, rank: int) -> Dict[str, Any]
     return res
 
 
+class _Phases:
+    """Wall seconds of every bench phase on this rank (the line's
+    ``phase_seconds``: where the driver's run time went)."""
+
+    def __init__(self) -> None:
+        import time
+        self._t = time.monotonic
+        self.start = self._t()
+        self.s: Dict[str, float] = {}
+
+    def add(self, name: str, t0: float) -> None:
+        self.s[name] = round(self._t() - t0, 2)
+
+    def now(self) -> float:
+        return self._t()
+
+    def report(self) -> Dict[str, float]:
+        return dict(self.s, total=round(self._t() - self.start, 2))
+
+
 def _predicted_ms(a: argparse.Namespace, world: int, strategy: str, model: str, params: tuple,
                   **kw: Any) -> Optional[float]:
     """The xGMI cost model's iteration time for this run (parallel/plan.py
@@ -540,9 +560,12 @@ def main() -> int:
     # Multi-rank: prove the collectives exact on these ranks before timing them.
     # (every rank gets the same all-reduced verdict, so all ranks take the
     # same decisions below)
+    ph = _Phases()
     exact: Dict[str, Any] = {}
     if a.exact == "on" or (a.exact == "auto" and world > 1):
+        t0 = ph.now()
         exact = _exact_block(a, world, rank)
+        ph.add("exact", t0)
         if rank == 0:
             print(f"[bench] exactness: {json.dumps(exact)}", file=sys.stderr)
     xgmi_exact_ok = not exact or bool(exact.get("exact", {}).get("xgmi", False))
@@ -571,6 +594,7 @@ def main() -> int:
     extra: Dict[str, Any] = {}
     try:
         fsdp_kw = dict(schedule=a.schedule, wire_dtype="bf16")
+        t0 = ph.now()
         try:
             doc = run("", "fsdp", a.model, a.units, world, graph=use_graph, warmup=a.warmup, runs=a.steps,
                       compute=a.compute, json=a.json, **fsdp_kw)
@@ -583,7 +607,9 @@ def main() -> int:
             use_graph = False
             doc = run(".retry", "fsdp", a.model, a.units, world, graph=False, warmup=a.warmup, runs=a.steps,
                       compute=a.compute, json=a.json, **fsdp_kw)
+        ph.add("headline", t0)
         # Secondary measurements: failures are reported, never fatal to the headline.
+        t0 = ph.now()
         if a.c5_model != "none":
             c5: Dict[str, Any] = {}
             try:
@@ -646,7 +672,9 @@ def main() -> int:
                 except Exception as e:  # noqa: BLE001
                     c5["gemm_work"] = {"error": str(e)[:300]}
             extra["comm_bound"] = c5
+            ph.add("comm_bound", t0)
         if a.stretch_steps > 0 and on_gpu:
+            t0 = ph.now()
             try:
                 d = run(".work", "fsdp", a.model, a.units, world, graph=use_graph, warmup=1, runs=a.stretch_steps,
                         compute="gemm-work", **fsdp_kw)
@@ -654,6 +682,7 @@ def main() -> int:
                 extra["gemm_work_ms_per_step"] = round(d["global"]["dlnb"]["iteration"]["timed_ms_per_iter"], 3)
             except Exception as e:  # noqa: BLE001
                 extra["compute_stretch_error"] = str(e)[:300]
+            ph.add("compute_stretch", t0)
     finally:
         sys.stdout.flush()
         os.dup2(saved, 1)
@@ -662,30 +691,44 @@ def main() -> int:
     if a.hybrids == "on" or (a.hybrids == "auto" and world == 8 and on_gpu):
         c3 = tuple(int(x) for x in a.c3.split(","))
         c4 = tuple(int(x) for x in a.c4.split(","))
+        t0 = ph.now()
         extra["hybrid_3d"] = _hybrid_block(a, world, rank, ".c3", "hybrid_3d", a.c3_model, c3,
                                            "GPipe (mb + S - 1)(f_mb + b_mb), BASELINE.md C3")
+        ph.add("hybrid_3d", t0)
+        t0 = ph.now()
         extra["hybrid_3d_moe"] = _hybrid_block(a, world, rank, ".c4", "hybrid_3d_moe", a.c4_model, c4,
                                                "GPipe (mb + S - 1)(f_mb + b_mb), BASELINE.md C4")
+        ph.add("hybrid_3d_moe", t0)
         if a.c4_ep_overlap == "on":
+            t0 = ph.now()
             # the MI355X-side schedule for the same config: the 1,024
             # all-to-alls per iteration leave the compute stream
             extra["hybrid_3d_moe"]["ep_overlap"] = _hybrid_block(
                 a, world, rank, ".c4o", "hybrid_3d_moe", a.c4_model, c4,
                 "GPipe (mb + S - 1)(f_mb + b_mb), BASELINE.md C4", ep_overlap=True)
+            ph.add("hybrid_3d_moe_ep_overlap", t0)
     # Device timeline of the headline configuration (every rank's spans).
     if a.timeline_block == "on" or (a.timeline_block == "auto" and world > 1 and on_gpu):
+        t0 = ph.now()
         extra["timeline"] = _timeline_block(a, world, rank)
+        ph.add("timeline", t0)
     # Collective bandwidth with nothing else running, RCCL and xgmi.
     if a.link_bench == "on" or (a.link_bench == "auto" and world > 1 and on_gpu):
+        t0 = ph.now()
         extra["link_bench"] = _link_block(a, world, rank, xgmi_exact_ok)
+        ph.add("link_bench", t0)
     # xgmi A/B last, in child processes (see the module docstring); skipped
     # when the exactness pass found the xgmi kernels wrong on these ranks.
     xgmi_on = on_gpu and (a.xgmi_ab == "on" or (a.xgmi_ab == "auto" and world > 1))
     skip = {"error": "skipped: the xgmi exactness check failed on these ranks (see exact_detail)"}
     if a.c5_model != "none" and xgmi_on:
+        t0 = ph.now()
         extra["comm_bound_xgmi"] = _xgmi_ab(a, world, rank, extra.get("comm_bound", {})) if xgmi_exact_ok else skip
+        ph.add("comm_bound_xgmi", t0)
     if xgmi_on and a.xgmi_headline_steps > 0:
+        t0 = ph.now()
         extra["headline_xgmi"] = _headline_xgmi(a, world, rank, doc) if xgmi_exact_ok else skip
+        ph.add("headline_xgmi", t0)
     if rank != 0:
         return 0
     g = doc["global"]
@@ -747,6 +790,8 @@ def main() -> int:
             out["model_fit"] = fit
     out.update(exact)
     out.update(extra)
+    # rank 0's wall seconds per phase (the headline's includes setup, warm-up and the timed steps)
+    out["phase_seconds"] = ph.report()
     print(json.dumps(out), flush=True)
     return 0
 

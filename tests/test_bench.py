@@ -73,6 +73,10 @@ def test_bench_torchrun_cpu(n, tmp_path):
     assert tl["ranks"] == n and tl["well_formed"] and 0 <= tl["comm_hidden_frac"] <= 1
     assert tl["ops"]["all_gather"]["count"] == 7 * n and tl["ops"]["reduce_scatter"]["count"] == 4 * n
     assert tl["ops"]["all_gather"]["busbw_GBps"] > 0 and tl["span_ms_max"] > 0
+    # rank 0's wall seconds per phase, every phase that ran
+    ps = o["phase_seconds"]
+    assert set(ps) >= {"exact", "headline", "comm_bound", "timeline", "link_bench", "total"}, ps
+    assert ps["total"] >= sum(v for k, v in ps.items() if k != "total") - 0.1
 
 
 def test_bench_hybrid_blocks_eight_ranks_cpu(tmp_path):
@@ -109,6 +113,7 @@ def test_bench_hybrid_blocks_eight_ranks_cpu(tmp_path):
     # GPipe floor (mb + S - 1)(f_mb + b_mb): hybrid_3d f_mb = fwd / S / (mb T)
     assert h3["floor_ms"] == pytest.approx((4 + 1) * (2.0 + 4.0) / 2 / (4 * 4), rel=1e-3)
     assert h4["floor_ms"] == pytest.approx((8 + 1) * (2.0 + 4.0) / 2 / 8, rel=1e-3)
+    assert {"hybrid_3d", "hybrid_3d_moe", "hybrid_3d_moe_ep_overlap"} <= set(o["phase_seconds"])
 
 
 def test_bench_two_nodes_cpu(tmp_path):
