@@ -43,10 +43,12 @@ int num_cus(int device);
 bool gemm_shape_ok(int M, int N, int K, DType in_t);
 // variant:
 //   0 = the default: fp8 5 where it applies (K % 256 == 0), else 6 where it
-//       applies (>= 2 K-tiles), else 8;
+//       applies (>= 2 K-tiles), else 8; bf16 first the narrow-tile kernel
+//       when fewer 256 x 256 tiles than CUs leave some idle (gemm_tn_narrow);
 //   5 = one wave per SIMD, 128 x 128 of C per wave, MX MFMA with AGPR
 //       accumulators (gemm_4wave_fp8.hip; fp8, K % 256 == 0; the streaming
-//       persistent kernel when there are more tiles than CUs);
+//       persistent kernel when there are more tiles than CUs, 256 x 32 nf
+//       tiles when fewer square tiles than CUs leave some idle);
 //   6 = the 8-phase ping-pong schedule, 8 waves (2 per SIMD, 128 x 64 of C
 //       each; gemm_8phase.hip; bf16 balanced fragment reads when the K-tile
 //       count is even, fp8 one uniform K-tile body; >= 2 K-tiles);
@@ -57,6 +59,15 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
              void* stream, int variant = 0);
 bool gemm_8phase_shape_ok(int M, int N, int K, DType in_t);
 bool gemm_4wave_fp8_shape_ok(int M, int N, int K, DType in_t);
+// Tile width 32 nf (nf 4..6, or 8 = the square 256 x 256 tile of the other
+// kernels) a one-shot GEMM of an M x N output uses on `cus` CUs: narrower
+// tiles when the square ones leave CUs idle (gemm_4wave_fp8.hip, narrow kernel).
+int gemm_narrow_nf(int M, int N, int cus);
+// The narrow-tile one-shot GEMM (bf16 or fp8, K * elem_size % 256 == 0); false
+// (nothing launched) when gemm_narrow_nf picks the square tile or the shape
+// does not fit.
+bool gemm_tn_narrow(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                    DType in_t, void* stream);
 void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                        void* stream);
 void gemm_tn_4wave_fp8_deadline(const void* A, const void* B, void* C, int M, int N, int K, uint64_t ticks,

@@ -43,6 +43,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "dlnb/kernels.hpp"
 
@@ -128,6 +129,18 @@ __device__ __forceinline__ void mfma(f32x4& acc, const FragF& b, const FragF& a,
     asm("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
         : "+a"(acc)
         : "v"(bv), "v"(av), "v"(scale));
+}
+
+// bf16 inputs in the same fragment layout (narrow kernel): a lane's K chunks h
+// and h + 4 of a 128-byte K-tile row are bf16 K elements 8h..8h+7 and
+// 32+8h..32+8h+7, i.e. its operands of the K-tile's two 16x16x32 K-steps.
+template <bool ZERO>
+__device__ __forceinline__ void mfma_bf16(f32x4& acc, const FragF& b, const FragF& a) {
+  if constexpr (ZERO)
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(b.lo), "v"(a.lo));
+  else
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b.lo), "v"(a.lo));
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b.hi), "v"(a.hi));
 }
 
 // Deadline state (DL kernels, the compute stand-in): the clock is read at the
@@ -484,10 +497,272 @@ __global__ void __launch_bounds__(256, 1)
   wait_vm<0>();  // the clamped / next-tile staging still in flight
 }
 
+// ---------------------------------------------------------------------------
+// Narrow-N tiles (one-shot only): 256 x 32·NF of C per block, 128 x 16·NF per
+// wave (acc[8][NF] AGPRs), NF in 4..6 (at 7 hipcc moves the accumulators out
+// of the AGPRs and spills).
+//
+// A 256 x 256 tile grid quantises badly on skinny outputs: the ViT-H / GPT-2-L
+// FFN down projection (M = 8192 tokens, N = 1280, the C5 stand-in shape) is
+// 160 tiles for 256 CUs, so 96 CUs idle for the whole launch. 256 x 160 tiles
+// make it exactly 256 (the host picks NF by makespan, gemm_tn_4wave_fp8).
+// Same K-tile structure as ktile() above, with the MFMA stream of a K-tile
+// (8 rows x NF) and the per-K-tile work laid out by MFMA index m (H = 4 NF
+// MFMAs per half):
+//   first half   after every odd m: one 16-B part of B(t+1) (2 NF parts); after
+//                m = 4p + 3: B(t+2) piece p (NF pieces, 8 rows each: the B tile
+//                is 32 NF rows = 4 NF wave-instructions, instruction 4p + w
+//                from wave w); after m = 1 / 3: this K-tile's a[7]
+//   mid          vmcnt(NF) (A(t+1) landed; B(t+2) in flight) + lgkmcnt + barrier
+//   second half  A(t+1) parts of a[0..6] (14; a[i]'s at least two MFMAs after
+//                row i's last, a_part_slot) and the 8 A(t+2) pieces, spread
+// LDS per K-tile buffer: A0 A1 (the 128-row halves, as above) then the B rows
+// (32 NF x 128 B); the XOR swizzle phase of a B row is that of its row within
+// its 16-row fragment, so the lane offsets offl / offh are the square
+// kernel's.
+template <int NF>
+struct Narrow {
+  static constexpr int kB = 2 * kHalf;              // B rows' offset in a buffer
+  static constexpr int kBufN = 2 * kHalf + 32 * NF * kRB;  // bytes per K-tile buffer
+  static constexpr int kM = 8 * NF;                 // MFMAs per K-tile per wave
+  static constexpr int kH = 4 * NF;
+  // MFMA index after which part k (0..13) of a[k / 2] is read (-1: none)
+  static constexpr int a_part_slot(int k) {
+    int m = kH - 1;
+    for (int q = 0; q <= k; ++q) {
+      const int earliest = ((q >> 1) + 1) * NF + 1;  // two MFMAs after row q / 2's last
+      m = (m + 1 > earliest) ? m + 1 : earliest;
+    }
+    return m;
+  }
+  static_assert(NF >= 4 && NF <= 6, "narrow tile: NF 4..6");
+};
+
+template <int NF>
+__device__ __forceinline__ void stage_piece_n(const CtxF& c, int kt, int op, int p) {
+  const int tk = min(kt, c.last_kt);  // past the last K-tile: clamped copies, never read
+  char* buf = c.smem + (kt & 1) * Narrow<NF>::kBufN;
+  if (op == 0) {  // A: half p / 4, instruction (p % 4) * 4 + w
+    const int half = p >> 2, i = p & 3;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(c.ra, (lds_ptr_t)(buf + half * kHalf + (i * 4 + c.w) * 1024), 16,
+                                             c.voffA, tk * kRB + (half * 128 + i * 32) * c.lda, 0, 0);
+  } else {  // B: instruction 4p + w = rows 32p + 8w .. +7
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rb, (lds_ptr_t)(buf + Narrow<NF>::kB + (p * 4 + c.w) * 1024), 16,
+                                             c.voffB, tk * kRB + p * 32 * c.ldb, 0, 0);
+  }
+}
+
+template <int NF, bool BF16, int PAR, bool FIRST, bool READ7 = !FIRST>
+__device__ __forceinline__ void ktile_n(const CtxF& c, int t, int wr, int wc, int offl, int offh, FragF (&a)[8],
+                                        FragF (&b)[2][NF], f32x4 (&acc)[8][NF], int scale) {
+  using NW = Narrow<NF>;
+  const char* ca = c.smem + (t & 1) * NW::kBufN + wr * kHalf;
+  const char* nbuf = c.smem + ((t + 1) & 1) * NW::kBufN;
+  const char* na = nbuf + wr * kHalf;
+  const char* nb = nbuf + NW::kB + wc * NF * 2048;
+  // B(t+1) landed (A(t+1) may be in flight); lgkmcnt(14): the previous
+  // K-tile's B reads (older than its 14 A parts) are done before any wave
+  // restages their region
+  __builtin_amdgcn_s_waitcnt((8 & 15) | (7 << 4) | (14 << 8));
+  raw_barrier();
+#pragma unroll
+  for (int m = 0; m < NW::kM; ++m) {
+    const int i = m / NF, j = m % NF;
+    if (m == NW::kH) {
+      wait_vm<NF>();  // A(t+1) landed (B(t+2) in flight)
+      // this wave's a[7] reads (its oldest LDS reads of the K-tile) are done:
+      // at most the 2 NF - 1 B parts issued after them are still in flight
+      __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | ((2 * NF - 1 < 8 ? 2 * NF - 1 : 8) << 8) | (3 << 14));
+      raw_barrier();
+    }
+    if constexpr (BF16)
+      mfma_bf16<FIRST>(acc[i][j], b[PAR][j], a[i]);
+    else
+      mfma<FIRST>(acc[i][j], b[PAR][j], a[i], scale);
+    if (m < NW::kH) {
+      if (READ7 && m == 1) a[7].lo = read_part(ca, offl, offh, 7, 0);
+      if (READ7 && m == 3) a[7].hi = read_part(ca, offl, offh, 7, 1);
+      if (m & 1) {
+        const int k = m >> 1;  // B(t+1) part k: fragment k / 2, half k % 2
+        if (k & 1)
+          b[1 - PAR][k >> 1].hi = read_part(nb, offl, offh, k >> 1, 1);
+        else
+          b[1 - PAR][k >> 1].lo = read_part(nb, offl, offh, k >> 1, 0);
+      }
+      if ((m & 3) == 3) stage_piece_n<NF>(c, t + 2, 1, m >> 2);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 14; ++k)
+        if (NW::a_part_slot(k) == m) {
+          if (k & 1)
+            a[k >> 1].hi = read_part(na, offl, offh, k >> 1, 1);
+          else
+            a[k >> 1].lo = read_part(na, offl, offh, k >> 1, 0);
+        }
+      const int s = m - NW::kH;  // A(t+2) piece p after MFMA kH + floor(p kH / 8)
+#pragma unroll
+      for (int p = 0; p < 8; ++p)
+        if (s == (p * NW::kH) / 8) stage_piece_n<NF>(c, t + 2, 0, p);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int NF, bool BF16>
+__global__ void __launch_bounds__(256, 1)
+    gemm_4wave_narrow_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C,
+                                 int M, int N, int K, int lda, int ldb, int ldc, int group) {
+  using NW = Narrow<NF>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * NW::kBufN];
+  const int tid = threadIdx.x;
+  CtxF c;
+  const int lane = tid & 63;
+  c.w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = c.w >> 1, wc = c.w & 1;
+  const int r16 = lane & 15, h = lane >> 4;
+  c.smem = smem;
+  constexpr int esz = BF16 ? 2 : 1;
+  lda *= esz;  // bytes from here on
+  ldb *= esz;
+  c.lda = lda;
+  c.ldb = ldb;
+  {
+    const int r = c.w * 8 + (lane >> 3);
+    const int q = (lane & 7) ^ ((r >> 1) & 7);
+    c.voffA = r * lda + (q << 4);
+    c.voffB = r * ldb + (q << 4);
+  }
+  constexpr int TN = 32 * NF;
+  const int nt_m = M / kT, nt_n = N / TN, T = nt_m * nt_n;
+  int tm, tn;
+  tile_coords(xcd_remap(blockIdx.x, T), nt_m, nt_n, group, tm, tn);
+  c.ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(A) + static_cast<size_t>(tm) * kT * lda, 0, 0x7ffffff0,
+                                           0x00020000);
+  c.rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(B) + static_cast<size_t>(tn) * TN * ldb, 0, 0x7ffffff0,
+                                           0x00020000);
+  const int nk = K * esz / kRB;  // even, >= 2 (host-checked)
+  c.last_kt = nk - 1;
+  const int x = (r16 >> 1) & 7;
+  const int offl = r16 * kRB + ((h ^ x) << 4), offh = offl ^ 64;
+  int scale = 127;  // E8M0 1.0
+  asm volatile("" : "+v"(scale));
+
+  f32x4 acc[8][NF];
+  FragF a[8], b[2][NF];
+
+  // Prologue: B(0) A(0) B(1) A(1), then K-tile 0's fragments.
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+    for (int p = 0; p < NF; ++p) stage_piece_n<NF>(c, kt, 1, p);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) stage_piece_n<NF>(c, kt, 0, p);
+  }
+  wait_vm<NF + 8>();
+  raw_barrier();
+#pragma unroll
+  for (int f = 0; f < 8; ++f) {
+    a[f].lo = read_part(smem + wr * kHalf, offl, offh, f, 0);
+    a[f].hi = read_part(smem + wr * kHalf, offl, offh, f, 1);
+  }
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    b[0][f].lo = read_part(smem + NW::kB + wc * NF * 2048, offl, offh, f, 0);
+    b[0][f].hi = read_part(smem + NW::kB + wc * NF * 2048, offl, offh, f, 1);
+  }
+
+  ktile_n<NF, BF16, 0, true>(c, 0, wr, wc, offl, offh, a, b, acc, scale);
+  for (int t = 1; t < nk - 1; t += 2) {
+    ktile_n<NF, BF16, 1, false>(c, t, wr, wc, offl, offh, a, b, acc, scale);
+    ktile_n<NF, BF16, 0, false>(c, t + 1, wr, wc, offl, offh, a, b, acc, scale);
+  }
+  ktile_n<NF, BF16, 1, false>(c, nk - 1, wr, wc, offl, offh, a, b, acc, scale);
+  wait_vm<0>();  // the clamped staging copies
+
+  // MFMA D -> v_accvgpr_read wait states, tied to the last row (no read hoisted above)
+#pragma unroll
+  for (int j = 0; j < NF; ++j) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(acc[7][j]));
+  size_t lo = static_cast<size_t>(wr * 128 + r16) * ldc + wc * 16 * NF + 4 * h;
+  asm volatile("" : "+v"(lo));
+  __bf16* base = C + static_cast<size_t>(tm) * kT * ldc + static_cast<size_t>(tn) * TN + lo;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const f32x4 v = acc[i][j];
+      bf16x4 o;
+      o[0] = static_cast<__bf16>(v[0]);
+      o[1] = static_cast<__bf16>(v[1]);
+      o[2] = static_cast<__bf16>(v[2]);
+      o[3] = static_cast<__bf16>(v[3]);
+      *reinterpret_cast<bf16x4*>(base + static_cast<size_t>(i * 16) * ldc + j * 16) = o;
+    }
+}
+
 }  // namespace
 
 bool gemm_4wave_fp8_shape_ok(int M, int N, int K, DType in_t) {
   return in_t == DType::FP8_E4M3 && gemm_shape_ok(M, N, K, in_t) && K % 256 == 0 && K >= 256;
+}
+
+int gemm_narrow_nf(int M, int N, int cus) {
+  // Tile width 32 nf: the fewest rounds of tile work per CU, ceil(tiles / CUs)
+  // x nf (a tile's time ~ its width), ties to the wider tile. Only when the
+  // square tiles do not already fill the chip (more tiles: the streaming
+  // kernel). DLNB_GEMM_NARROW_NF=8 pins the square tile (A/B).
+  static const int forced = [] {
+    const char* v = std::getenv("DLNB_GEMM_NARROW_NF");
+    return v ? std::atoi(v) : 0;
+  }();
+  if (forced >= 4 && forced <= 8 && forced != 7) return (forced == 8 || N % (32 * forced) == 0) ? forced : 8;
+  const int sq = (M / kT) * (N / kT);
+  if (sq >= cus) return 8;
+  int best = 8;
+  long best_cost = static_cast<long>((sq + cus - 1) / cus) * 8;
+  for (int nf = 6; nf >= 4; --nf) {  // (nf = 7 spills its accumulators out of the AGPRs)
+    if (N % (32 * nf) != 0) continue;
+    const long t = static_cast<long>(M / kT) * (N / (32 * nf));
+    const long cost = (t + cus - 1) / cus * nf;
+    if (cost < best_cost) {
+      best = nf;
+      best_cost = cost;
+    }
+  }
+  return best;
+}
+
+bool gemm_tn_narrow(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                    DType in_t, void* stream) {
+  static const int cus = [] {
+    int dev = 0;
+    return hipGetDevice(&dev) == hipSuccess ? num_cus(dev) : 256;
+  }();
+  const size_t kbytes = static_cast<size_t>(K) * dtype_size(in_t);
+  if (!gemm_shape_ok(M, N, K, in_t) || kbytes % 256 != 0) return false;  // an even K-tile count
+  const int nf = gemm_narrow_nf(M, N, cus);
+  if (nf == 8) return false;
+  constexpr int group = 8;
+  const int nt = (M / kT) * (N / (32 * nf));
+  auto* a = static_cast<const char*>(A);
+  auto* b = static_cast<const char*>(B);
+  auto* cc = static_cast<__bf16*>(C);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const bool bf = in_t == DType::BF16;
+#define DLNB_NARROW(NF)                                                                                     \
+  if (bf)                                                                                                   \
+    hipLaunchKernelGGL((gemm_4wave_narrow_kernel<NF, true>), nt, 256, 0, st, a, b, cc, M, N, K, lda, ldb, ldc, \
+                       group);                                                                              \
+  else                                                                                                      \
+    hipLaunchKernelGGL((gemm_4wave_narrow_kernel<NF, false>), nt, 256, 0, st, a, b, cc, M, N, K, lda, ldb, ldc, group)
+  switch (nf) {
+    case 4: DLNB_NARROW(4); break;
+    case 5: DLNB_NARROW(5); break;
+    default: DLNB_NARROW(6); break;
+  }
+#undef DLNB_NARROW
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) DLNB_THROW("gemm narrow-tile launch failed: " << hipGetErrorString(e));
+  return true;
 }
 
 void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
@@ -510,6 +785,9 @@ void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int 
     if (e != hipSuccess) DLNB_THROW("gemm 4-wave fp8 stream launch failed: " << hipGetErrorString(e));
     return;
   }
+  // Fewer 256 x 256 tiles than CUs: a narrower tile may fill the chip (the
+  // ViT-H FFN down projection 8192 x 1280: 160 square tiles, 256 of 256 x 160).
+  if (gemm_tn_narrow(A, B, C, M, N, K, lda, ldb, ldc, DType::FP8_E4M3, stream)) return;
   hipLaunchKernelGGL(gemm_4wave_fp8_kernel<false>, tiles, 256, 0, static_cast<hipStream_t>(stream),
                      static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda,
                      ldb, ldc, group, nullptr, 0u, 0ull, 0ull, nullptr);

@@ -94,6 +94,8 @@ int dlnb_gemm_deadline_us(const void* A, const void* B, void* C, int M, int N, i
   });
 }
 
+int dlnb_gemm_narrow_nf(int M, int N, int cus) { return dlnb::kernels::gemm_narrow_nf(M, N, cus); }
+
 int dlnb_gemm_shape_ok(int M, int N, int K, int dtype) {
   return dlnb::kernels::gemm_shape_ok(M, N, K, static_cast<dlnb::DType>(dtype)) ? 1 : 0;
 }

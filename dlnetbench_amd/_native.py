@@ -57,6 +57,7 @@ def lib() -> ctypes.CDLL:
     L.dlnb_gemm_tn_waves.argtypes = [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]
     L.dlnb_gemm_deadline_us.argtypes = [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_dbl, c_int, c_vp, c_int, c_vp]
     L.dlnb_gemm_shape_ok.argtypes = [c_int, c_int, c_int, c_int]
+    L.dlnb_gemm_narrow_nf.argtypes = [c_int, c_int, c_int]
     L.dlnb_idle_wait_us.argtypes = [c_dbl, c_int, c_vp]
     L.dlnb_busy_spin_us.argtypes = [c_dbl, c_int, c_vp]
     L.dlnb_sgd_momentum_bf16.argtypes = [c_vp, c_vp, c_vp, c_size, c_float, c_float, c_vp]

@@ -26,8 +26,9 @@ def assert_close_bf16_out(c, ref):
     assert worst <= 0, f"max excess {worst}, max err {err.max().item()}, rms {ref.pow(2).mean().sqrt().item()}"
 
 
-# gemm_tn variants (kernels.hpp): 0 default, 5 4-wave MX (fp8), 6 8-phase, 8 8-wave
-@pytest.mark.parametrize("waves", [0, 8])
+# gemm_tn variants (kernels.hpp): 0 default (bf16: narrow tiles when square ones leave CUs idle), 5 4-wave MX
+# (fp8), 6 8-phase, 8 8-wave
+@pytest.mark.parametrize("waves", [0, 6, 8])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 512, 128), (512, 512, 64), (768, 256, 128),
                                    (512, 256, 1024), (768, 1280, 640), (2048, 1024, 4096), (256, 256, 192),
                                    (512, 768, 320)])
@@ -40,7 +41,7 @@ def test_gemm_bf16_matches_torch(M, N, K, waves):
     assert_close_bf16_out(c, a.float() @ b.float().t())
 
 
-@pytest.mark.parametrize("waves", [0, 8])
+@pytest.mark.parametrize("waves", [0, 6, 8])
 def test_gemm_bf16_identity_asymmetric(waves):
     # A = I picks rows of B: catches any row/column/quadrant swap in the C write.
     M = N = 256
@@ -65,12 +66,45 @@ def test_gemm_fp8_matches_torch(M, N, K, waves):
     assert_close_bf16_out(c, a.float() @ b.float().t())
 
 
+@pytest.mark.parametrize("M,N,K,nf", [(2048, 1280, 128, 4), (8192, 1280, 5120, 5), (7168, 1280, 640, 5),
+                                      (8192, 1536, 256, 6), (512, 768, 1024, 4)])
+def test_gemm_bf16_narrow_tiles(M, N, K, nf):
+    """bf16 through the narrow-tile kernel (two 16x16x32 MFMAs per 128-byte K-tile row on the MX kernel's
+    fragments), K down to the 2-K-tile minimum."""
+    from dlnetbench_amd import _native
+    assert _native.lib().dlnb_gemm_narrow_nf(M, N, torch.cuda.get_device_properties(0).multi_processor_count) == nf
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + nf)
+    a = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    b = torch.randn(N, K, device="cuda", generator=g).to(torch.bfloat16)
+    c = gemm.gemm_tn(a, b)
+    torch.cuda.synchronize()
+    assert_close_bf16_out(c, a.float() @ b.float().t())
+
+
 @pytest.mark.skipif(not hasattr(torch, "float8_e4m3fn"), reason="torch without float8")
-@pytest.mark.parametrize("M,N,K", [(4096, 4352, 512), (8192, 8192, 256), (2048, 8448, 1280)])
+@pytest.mark.parametrize("M,N,K,nf", [(2048, 1280, 256, 4), (8192, 1280, 5120, 5), (7168, 1280, 512, 5),
+                                      (8192, 1536, 256, 6), (8192, 1024, 1280, 4), (768, 512, 2048, 4)])
+def test_gemm_fp8_narrow_tiles(M, N, K, nf):
+    """Fewer 256 x 256 tiles than CUs: the MX fp8 kernel's 256 x 32 nf tiles (gemm_4wave_fp8.hip, narrow
+    kernel), including the ViT-H FFN down projection 8192 x 1280 x 5120 (the C5 stand-in shape) and the
+    2-K-tile minimum."""
+    from dlnetbench_amd import _native
+    assert _native.lib().dlnb_gemm_narrow_nf(M, N, torch.cuda.get_device_properties(0).multi_processor_count) == nf
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + nf)
+    a = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(torch.float8_e4m3fn)
+    b = (torch.randn(N, K, device="cuda", generator=g) * 0.5).to(torch.float8_e4m3fn)
+    c = gemm.gemm_tn(a, b)
+    torch.cuda.synchronize()
+    assert_close_bf16_out(c, a.float() @ b.float().t())
+
+
+@pytest.mark.skipif(not hasattr(torch, "float8_e4m3fn"), reason="torch without float8")
+@pytest.mark.parametrize("M,N,K", [(4096, 4352, 512), (8192, 8192, 256), (2048, 8448, 1280), (6144, 2048, 256)])
 def test_gemm_fp8_many_tiles(M, N, K):
     """More tiles than CUs: the one-wave-per-SIMD fp8 kernel runs as the streaming persistent kernel (a
     block's tiles as one K-tile stream, the next tile's first K-tiles staged during the current one's
-    last, K = 256 the 2-K-tile minimum); fewer tiles (test_gemm_fp8_matches_torch) a block per tile."""
+    last, K = 256 the 2-K-tile minimum); fewer tiles (test_gemm_fp8_matches_torch) a block per tile - square
+    tiles where no narrower one saves a round (6144 x 2048: 192 tiles), else test_gemm_fp8_narrow_tiles."""
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     a = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(torch.float8_e4m3fn)
     b = (torch.randn(N, K, device="cuda", generator=g) * 0.5).to(torch.float8_e4m3fn)
@@ -79,7 +113,7 @@ def test_gemm_fp8_many_tiles(M, N, K):
     assert_close_bf16_out(c, a.float() @ b.float().t())
 
 
-@pytest.mark.parametrize("dtype,waves", [("bf16", 0), ("bf16", 8), ("fp8", 0), ("fp8", 6), ("fp8", 8)])
+@pytest.mark.parametrize("dtype,waves", [("bf16", 0), ("bf16", 6), ("bf16", 8), ("fp8", 0), ("fp8", 6), ("fp8", 8)])
 def test_gemm_strided_operands(dtype, waves):
     """Row-strided A, B and C (views of wider matrices: leading dimensions > K, > N): the staging lane
     offsets and buffer resources use the leading dimensions, not K."""

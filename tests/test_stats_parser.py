@@ -104,3 +104,27 @@ def test_host_conversions_roundtrip():
     assert L.dlnb_fp8e4m3_to_float(L.dlnb_float_to_fp8e4m3(1000.0)) == 448.0
     assert L.dlnb_fp8e4m3_to_float(L.dlnb_float_to_fp8e4m3(-0.5)) == -0.5
     assert L.dlnb_fp8e4m3_to_float(0x7E) == 448.0
+
+
+@pytest.mark.parametrize("M,N,cus,nf", [
+    (8192, 1280, 256, 5),    # ViT-H / GPT-2-L FFN down (C5 stand-in): 160 square tiles -> 256 of 256 x 160
+    (8192, 1024, 256, 4),    # ViT-L: 128 -> 256 of 256 x 128
+    (8192, 1536, 256, 6),    # 192 -> 256 of 256 x 192
+    (4096, 4096, 256, 8),    # 256 square tiles already fill the chip
+    (8192, 4096, 256, 8),    # more tiles than CUs: the streaming square kernel
+    (6144, 2048, 256, 8),    # 192 tiles; 256 x 128 would need two rounds (384), no 160 / 192 fit: square
+    (8192, 1280, 224, 8),    # 224 CUs: 256 narrow tiles need 2 rounds of 5 > 1 round of 8
+    (512, 768, 256, 4),      # 6 square tiles: 12 of 256 x 128 beat 8 of 256 x 192
+])
+def test_fp8_narrow_tile_choice(M, N, cus, nf):
+    """The one-shot MX fp8 kernel's tile width (gemm_tn_4wave_fp8 -> gemm_4wave_fp8_narrow_nf): the fewest rounds
+    of tile work per CU. Host code only, runs without a GPU."""
+    assert _native.lib().dlnb_gemm_narrow_nf(M, N, cus) == nf
+
+
+def test_fp8_narrow_tile_choice_gpu_cases():
+    """The tile widths test_gpu_kernels.py::test_gemm_fp8_narrow_tiles expects on a 256-CU MI355X."""
+    L = _native.lib()
+    for M, N, nf in [(2048, 1280, 4), (8192, 1280, 5), (7168, 1280, 5), (8192, 1536, 6), (8192, 1024, 4),
+                     (768, 512, 4), (6144, 2048, 8)]:
+        assert L.dlnb_gemm_narrow_nf(M, N, 256) == nf, (M, N)
