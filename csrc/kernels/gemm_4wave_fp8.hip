@@ -499,7 +499,7 @@ __global__ void __launch_bounds__(256, 1)
 
 // ---------------------------------------------------------------------------
 // Narrow-N tiles (one-shot only): 256 x 32·NF of C per block, 128 x 16·NF per
-// wave (acc[8][NF] AGPRs), NF in 4..6 (at 7 hipcc moves the accumulators out
+// wave (acc[8][NF] AGPRs), NF in 3..6 (at 7 hipcc moves the accumulators out
 // of the AGPRs and spills).
 //
 // A 256 x 256 tile grid quantises badly on skinny outputs: the ViT-H / GPT-2-L
@@ -512,10 +512,12 @@ __global__ void __launch_bounds__(256, 1)
 //   first half   after every odd m: one 16-B part of B(t+1) (2 NF parts); after
 //                m = 4p + 3: B(t+2) piece p (NF pieces, 8 rows each: the B tile
 //                is 32 NF rows = 4 NF wave-instructions, instruction 4p + w
-//                from wave w); after m = 1 / 3: this K-tile's a[7]
+//                from wave w); after m = 1, 3 (, 5, 7): this K-tile's late
+//                row(s) a[7] (NF = 3: a[6], a[7]), read from its own buffer
 //   mid          vmcnt(NF) (A(t+1) landed; B(t+2) in flight) + lgkmcnt + barrier
-//   second half  A(t+1) parts of a[0..6] (14; a[i]'s at least two MFMAs after
-//                row i's last, a_part_slot) and the 8 A(t+2) pieces, spread
+//   second half  A(t+1) parts of the other rows (a[i]'s at least two MFMAs
+//                after row i's last, a_part_slot; at NF = 3 row 6 ends too late
+//                for that, hence two late rows) and the 8 A(t+2) pieces
 // LDS per K-tile buffer: A0 A1 (the 128-row halves, as above) then the B rows
 // (32 NF x 128 B); the XOR swizzle phase of a B row is that of its row within
 // its 16-row fragment, so the lane offsets offl / offh are the square
@@ -526,7 +528,9 @@ struct Narrow {
   static constexpr int kBufN = 2 * kHalf + 32 * NF * kRB;  // bytes per K-tile buffer
   static constexpr int kM = 8 * NF;                 // MFMAs per K-tile per wave
   static constexpr int kH = 4 * NF;
-  // MFMA index after which part k (0..13) of a[k / 2] is read (-1: none)
+  static constexpr int kLate = NF == 3 ? 2 : 1;  // rows read at the start of their own K-tile
+  static constexpr int kEarly = 2 * (8 - kLate);  // A parts read in the previous K-tile
+  // MFMA index after which part k (0..kEarly-1) of a[k / 2] is read
   static constexpr int a_part_slot(int k) {
     int m = kH - 1;
     for (int q = 0; q <= k; ++q) {
@@ -535,7 +539,8 @@ struct Narrow {
     }
     return m;
   }
-  static_assert(NF >= 4 && NF <= 6, "narrow tile: NF 4..6");
+  static_assert(NF >= 3 && NF <= 6, "narrow tile: NF 3..6");
+  static_assert(a_part_slot(kEarly - 1) < kM, "A(t+1) reads must fit the K-tile");
 };
 
 template <int NF>
@@ -560,19 +565,20 @@ __device__ __forceinline__ void ktile_n(const CtxF& c, int t, int wr, int wc, in
   const char* nbuf = c.smem + ((t + 1) & 1) * NW::kBufN;
   const char* na = nbuf + wr * kHalf;
   const char* nb = nbuf + NW::kB + wc * NF * 2048;
-  // B(t+1) landed (A(t+1) may be in flight); lgkmcnt(14): the previous
-  // K-tile's B reads (older than its 14 A parts) are done before any wave
+  // B(t+1) landed (A(t+1) may be in flight); lgkmcnt(kEarly): the previous
+  // K-tile's B reads (older than its kEarly A parts) are done before any wave
   // restages their region
-  __builtin_amdgcn_s_waitcnt((8 & 15) | (7 << 4) | (14 << 8));
+  __builtin_amdgcn_s_waitcnt((8 & 15) | (7 << 4) | (NW::kEarly << 8));
   raw_barrier();
 #pragma unroll
   for (int m = 0; m < NW::kM; ++m) {
     const int i = m / NF, j = m % NF;
     if (m == NW::kH) {
       wait_vm<NF>();  // A(t+1) landed (B(t+2) in flight)
-      // this wave's a[7] reads (its oldest LDS reads of the K-tile) are done:
-      // at most the 2 NF - 1 B parts issued after them are still in flight
-      __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | ((2 * NF - 1 < 8 ? 2 * NF - 1 : 8) << 8) | (3 << 14));
+      // this wave's late-row reads (the K-tile's first LDS reads) are done: at
+      // most the 2 NF - 2 kLate + 1 B parts issued after the last are in flight
+      constexpr int lg = 2 * NF - 2 * NW::kLate + 1 < 8 ? 2 * NF - 2 * NW::kLate + 1 : 8;
+      __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (lg << 8) | (3 << 14));
       raw_barrier();
     }
     if constexpr (BF16)
@@ -580,8 +586,13 @@ __device__ __forceinline__ void ktile_n(const CtxF& c, int t, int wr, int wc, in
     else
       mfma<FIRST>(acc[i][j], b[PAR][j], a[i], scale);
     if (m < NW::kH) {
-      if (READ7 && m == 1) a[7].lo = read_part(ca, offl, offh, 7, 0);
-      if (READ7 && m == 3) a[7].hi = read_part(ca, offl, offh, 7, 1);
+      if (READ7 && (m & 1) && (m >> 1) < 2 * NW::kLate) {  // late row 8 - kLate + r / 2, half r % 2
+        const int r = m >> 1, row = 8 - NW::kLate + (r >> 1);
+        if (r & 1)
+          a[row].hi = read_part(ca, offl, offh, row, 1);
+        else
+          a[row].lo = read_part(ca, offl, offh, row, 0);
+      }
       if (m & 1) {
         const int k = m >> 1;  // B(t+1) part k: fragment k / 2, half k % 2
         if (k & 1)
@@ -592,7 +603,7 @@ __device__ __forceinline__ void ktile_n(const CtxF& c, int t, int wr, int wc, in
       if ((m & 3) == 3) stage_piece_n<NF>(c, t + 2, 1, m >> 2);
     } else {
 #pragma unroll
-      for (int k = 0; k < 14; ++k)
+      for (int k = 0; k < NW::kEarly; ++k)
         if (NW::a_part_slot(k) == m) {
           if (k & 1)
             a[k >> 1].hi = read_part(na, offl, offh, k >> 1, 1);
@@ -714,12 +725,12 @@ int gemm_narrow_nf(int M, int N, int cus) {
     const char* v = std::getenv("DLNB_GEMM_NARROW_NF");
     return v ? std::atoi(v) : 0;
   }();
-  if (forced >= 4 && forced <= 8 && forced != 7) return (forced == 8 || N % (32 * forced) == 0) ? forced : 8;
+  if (forced >= 3 && forced <= 8 && forced != 7) return (forced == 8 || N % (32 * forced) == 0) ? forced : 8;
   const int sq = (M / kT) * (N / kT);
   if (sq >= cus) return 8;
   int best = 8;
   long best_cost = static_cast<long>((sq + cus - 1) / cus) * 8;
-  for (int nf = 6; nf >= 4; --nf) {  // (nf = 7 spills its accumulators out of the AGPRs)
+  for (int nf = 6; nf >= 3; --nf) {  // (nf = 7 spills its accumulators out of the AGPRs)
     if (N % (32 * nf) != 0) continue;
     const long t = static_cast<long>(M / kT) * (N / (32 * nf));
     const long cost = (t + cus - 1) / cus * nf;
@@ -755,6 +766,7 @@ bool gemm_tn_narrow(const void* A, const void* B, void* C, int M, int N, int K, 
   else                                                                                                      \
     hipLaunchKernelGGL((gemm_4wave_narrow_kernel<NF, false>), nt, 256, 0, st, a, b, cc, M, N, K, lda, ldb, ldc, group)
   switch (nf) {
+    case 3: DLNB_NARROW(3); break;
     case 4: DLNB_NARROW(4); break;
     case 5: DLNB_NARROW(5); break;
     default: DLNB_NARROW(6); break;

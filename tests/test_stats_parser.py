@@ -114,7 +114,8 @@ def test_host_conversions_roundtrip():
     (8192, 4096, 256, 8),    # more tiles than CUs: the streaming square kernel
     (6144, 2048, 256, 8),    # 192 tiles; 256 x 128 would need two rounds (384), no 160 / 192 fit: square
     (8192, 1280, 224, 8),    # 224 CUs: 256 narrow tiles need 2 rounds of 5 > 1 round of 8
-    (512, 768, 256, 4),      # 6 square tiles: 12 of 256 x 128 beat 8 of 256 x 192
+    (512, 768, 256, 3),      # 6 square tiles: 16 of 256 x 96 (3 units each) beat 12 of 256 x 128 (4)
+    (8192, 768, 256, 3),     # ViT-B: 96 -> 256 of 256 x 96
 ])
 def test_fp8_narrow_tile_choice(M, N, cus, nf):
     """The one-shot MX fp8 kernel's tile width (gemm_tn_4wave_fp8 -> gemm_4wave_fp8_narrow_nf): the fewest rounds
@@ -126,5 +127,5 @@ def test_fp8_narrow_tile_choice_gpu_cases():
     """The tile widths test_gpu_kernels.py::test_gemm_fp8_narrow_tiles expects on a 256-CU MI355X."""
     L = _native.lib()
     for M, N, nf in [(2048, 1280, 4), (8192, 1280, 5), (7168, 1280, 5), (8192, 1536, 6), (8192, 1024, 4),
-                     (768, 512, 4), (6144, 2048, 8)]:
+                     (768, 512, 4), (6144, 2048, 8), (8192, 768, 3), (512, 768, 3)]:
         assert L.dlnb_gemm_narrow_nf(M, N, 256) == nf, (M, N)
