@@ -46,6 +46,7 @@
 #include <cstdlib>
 
 #include "dlnb/kernels.hpp"
+#include "store_pair.hpp"
 
 namespace dlnb {
 namespace kernels {
@@ -263,21 +264,15 @@ __device__ __forceinline__ void store_tile(f32x4 (&acc)[8][8], __bf16* __restric
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
                : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[7][4]),
                  "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7]));
-  size_t lo = static_cast<size_t>(wr * 128 + r16) * ldc + wc * 128 + 4 * h;
+  size_t lo = static_cast<size_t>(wr * 128 + r16) * ldc + wc * 128;
   asm volatile("" : "+v"(lo));
   __bf16* base = C + static_cast<size_t>(tm) * kT * ldc + static_cast<size_t>(tn) * kT + lo;
+  const bool wide = epi::wide_ok(C, ldc);
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const f32x4 v = acc[i][j];
-      bf16x4 o;
-      o[0] = static_cast<__bf16>(v[0]);
-      o[1] = static_cast<__bf16>(v[1]);
-      o[2] = static_cast<__bf16>(v[2]);
-      o[3] = static_cast<__bf16>(v[3]);
-      *reinterpret_cast<bf16x4*>(base + static_cast<size_t>(i * 16) * ldc + j * 16) = o;
-    }
+    for (int j = 0; j < 8; j += 2)
+      epi::store_pair(base + static_cast<size_t>(i * 16) * ldc + j * 16, acc[i][j], acc[i][j + 1], h, wide);
 }
 
 // One 256 x 256 tile of C. Returns false if the deadline stopped it (no
@@ -693,21 +688,17 @@ __global__ void __launch_bounds__(256, 1)
   // MFMA D -> v_accvgpr_read wait states, tied to the last row (no read hoisted above)
 #pragma unroll
   for (int j = 0; j < NF; ++j) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(acc[7][j]));
-  size_t lo = static_cast<size_t>(wr * 128 + r16) * ldc + wc * 16 * NF + 4 * h;
+  size_t lo = static_cast<size_t>(wr * 128 + r16) * ldc + wc * 16 * NF;
   asm volatile("" : "+v"(lo));
   __bf16* base = C + static_cast<size_t>(tm) * kT * ldc + static_cast<size_t>(tn) * TN + lo;
+  const bool wide = epi::wide_ok(C, ldc);
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 8; ++i) {
 #pragma unroll
-    for (int j = 0; j < NF; ++j) {
-      const f32x4 v = acc[i][j];
-      bf16x4 o;
-      o[0] = static_cast<__bf16>(v[0]);
-      o[1] = static_cast<__bf16>(v[1]);
-      o[2] = static_cast<__bf16>(v[2]);
-      o[3] = static_cast<__bf16>(v[3]);
-      *reinterpret_cast<bf16x4*>(base + static_cast<size_t>(i * 16) * ldc + j * 16) = o;
-    }
+    for (int j = 0; j + 1 < NF; j += 2)
+      epi::store_pair(base + static_cast<size_t>(i * 16) * ldc + j * 16, acc[i][j], acc[i][j + 1], h, wide);
+    if constexpr (NF & 1) epi::store_one(base + static_cast<size_t>(i * 16) * ldc + (NF - 1) * 16, acc[i][NF - 1], h);
+  }
 }
 
 }  // namespace

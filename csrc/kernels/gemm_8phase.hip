@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include "dlnb/kernels.hpp"
+#include "store_pair.hpp"
 
 namespace dlnb {
 namespace kernels {
@@ -350,25 +351,19 @@ __device__ __forceinline__ bool tile(Ctx& c, const char* __restrict__ A, const c
     }
   }
 
-  // Epilogue: lane holds C[m = .. + r16][n = .. + 4h + 0..3] of each fragment.
+  // Epilogue: lane holds C[m = .. + r16][n = .. + 4h + 0..3] of each
+  // fragment; the j = 0, 1 fragments are adjacent (store_pair.hpp).
+  const bool wide = epi::wide_ok(C, ldc);
 #pragma unroll
   for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
     for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int m = tm * kT + qm * 128 + c.wr * 64 + i * 16 + c.r16;
-          const int n = tn * kT + qn * 128 + c.wc * 32 + j * 16 + 4 * c.h;
-          const f32x4 a = acc[qm][qn][i][j];
-          bf16x4 o;
-          o[0] = static_cast<__bf16>(a[0]);
-          o[1] = static_cast<__bf16>(a[1]);
-          o[2] = static_cast<__bf16>(a[2]);
-          o[3] = static_cast<__bf16>(a[3]);
-          *reinterpret_cast<bf16x4*>(C + static_cast<size_t>(m) * ldc + n) = o;
-        }
+      for (int i = 0; i < 4; ++i) {
+        const int m = tm * kT + qm * 128 + c.wr * 64 + i * 16 + c.r16;
+        const int n = tn * kT + qn * 128 + c.wc * 32;
+        epi::store_pair(C + static_cast<size_t>(m) * ldc + n, acc[qm][qn][i][0], acc[qm][qn][i][1], c.h, wide);
+      }
   return true;
 }
 
@@ -447,26 +442,21 @@ __device__ __forceinline__ void store_tile(const Ctx& c, __bf16* __restrict__ C,
   // This lane's element offset in the tile, made opaque so the compiler
   // cannot hoist the 32 store addresses out of the K-loop (they would stay
   // live across it and spill).
-  size_t lane = static_cast<size_t>(c.wr * 64 + c.r16) * ldc + c.wc * 32 + 4 * c.h;
+  size_t lane = static_cast<size_t>(c.wr * 64 + c.r16) * ldc + c.wc * 32;
   asm volatile("" : "+v"(lane));
   __bf16* base = C + static_cast<size_t>(tm) * kT * ldc + static_cast<size_t>(tn) * kT + lane;
+  const bool wide = epi::wide_ok(C, ldc);
 #pragma unroll
   for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
     for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const f32x4 a = acc[qm][qn][i][j];
-          bf16x4 o;
-          o[0] = static_cast<__bf16>(a[0]);
-          o[1] = static_cast<__bf16>(a[1]);
-          o[2] = static_cast<__bf16>(a[2]);
-          o[3] = static_cast<__bf16>(a[3]);
-          *reinterpret_cast<bf16x4*>(base + static_cast<size_t>(qm * 128 + i * 16) * ldc + qn * 128 + j * 16) = o;
-          acc[qm][qn][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
+      for (int i = 0; i < 4; ++i) {
+        epi::store_pair(base + static_cast<size_t>(qm * 128 + i * 16) * ldc + qn * 128, acc[qm][qn][i][0],
+                        acc[qm][qn][i][1], c.h, wide);
+        acc[qm][qn][i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc[qm][qn][i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
 }
 
 // Tile coordinates of linear tile index b (GROUP-ed M order, as tile()).
