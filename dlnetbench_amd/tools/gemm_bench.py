@@ -7,7 +7,8 @@ Interleaves the implementations round by round in one process
 (cdna_hip_programming.md §5.4 rule 24) on random [-1, 1) operands (rule 25)
 and prints TFLOP/s (median, best) as JSON lines, one key per variant
 (``v<n>_tflops_*``, n = the variant of ops.gemm.gemm_tn, csrc/include/dlnb/kernels.hpp:
-0 = the default, 5 = one wave per SIMD MX (fp8), 6 = 8-phase, 8 = 8 waves
+0 = the default - with 256 x 32nf narrow tiles where square ones leave CUs
+idle -, 5 = one wave per SIMD MX (fp8), 6 = 8-phase, 8 = 8 waves
 double-buffered) and ``torch_tflops_*``.
 """
 from __future__ import annotations
@@ -22,7 +23,10 @@ def main(argv=None) -> int:
     from dlnetbench_amd.ops import gemm
 
     ap = argparse.ArgumentParser()
-    ap.add_argument("--shapes", default="4096x4096x4096,8192x8192x8192,8192x14336x4096,8192x28672x8192,2048x5120x1280")
+    # square shapes, the headline stand-in (llama3-8B FFN down), and the skinny C5 stand-in (ViT-H FFN down,
+    # narrow tiles)
+    ap.add_argument("--shapes", default="4096x4096x4096,8192x8192x8192,8192x14336x4096,8192x4096x14336,"
+                                        "8192x1280x5120,2048x5120x1280")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=20)
