@@ -562,8 +562,9 @@ __device__ __forceinline__ void ktile_n(const CtxF& c, int t, int wr, int wc, in
   const char* nb = nbuf + NW::kB + wc * NF * 2048;
   // B(t+1) landed (A(t+1) may be in flight); lgkmcnt(kEarly): the previous
   // K-tile's B reads (older than its kEarly A parts) are done before any wave
-  // restages their region
-  __builtin_amdgcn_s_waitcnt((8 & 15) | (7 << 4) | (NW::kEarly << 8));
+  // restages their region (the first K-tile: every prologue read, whose B(0)
+  // reads are its youngest)
+  __builtin_amdgcn_s_waitcnt((8 & 15) | (7 << 4) | ((FIRST ? 0 : NW::kEarly) << 8));
   raw_barrier();
 #pragma unroll
   for (int m = 0; m < NW::kM; ++m) {
