@@ -178,6 +178,10 @@ __device__ __forceinline__ bool ktile(const CtxF& c, int t, int wr, int wc, int 
     wait_vm<(VM >= 0 ? VM : 8)>();
   else
     wait_vm<63>();
+  // lgkmcnt(14): this wave's B(t) reads (older than the previous K-tile's 14
+  // A parts) are done before any wave restages B(t+2) over them after the
+  // barrier; a tile's first K-tile waits for every read before it
+  __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | ((FIRST ? 0 : 14) << 8) | (3 << 14));
   raw_barrier();
   bool stop = false;
   uint64_t now = 0;
