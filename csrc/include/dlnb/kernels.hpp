@@ -61,7 +61,8 @@ bool gemm_8phase_shape_ok(int M, int N, int K, DType in_t);
 bool gemm_4wave_fp8_shape_ok(int M, int N, int K, DType in_t);
 // Tile width 32 nf (nf 3..6, or 8 = the square 256 x 256 tile of the other
 // kernels) a one-shot GEMM of an M x N output uses on `cus` CUs: narrower
-// tiles when the square ones leave CUs idle (gemm_4wave_fp8.hip, narrow kernel).
+// tiles when the square ones leave CUs idle - fewer tiles than CUs, or a last
+// round at least 10 % short (gemm_4wave_fp8.hip, narrow kernel).
 int gemm_narrow_nf(int M, int N, int cus);
 // The narrow-tile one-shot GEMM (bf16 or fp8, K * elem_size % 256 == 0); false
 // (nothing launched) when gemm_narrow_nf picks the square tile or the shape

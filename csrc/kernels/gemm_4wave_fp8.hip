@@ -714,18 +714,21 @@ bool gemm_4wave_fp8_shape_ok(int M, int N, int K, DType in_t) {
 
 int gemm_narrow_nf(int M, int N, int cus) {
   // Tile width 32 nf: the fewest rounds of tile work per CU, ceil(tiles / CUs)
-  // x nf (a tile's time ~ its width), ties to the wider tile. Only when the
-  // square tiles do not already fill the chip (more tiles: the streaming
-  // kernel). DLNB_GEMM_NARROW_NF=8 pins the square tile (A/B).
+  // x nf (a tile's time ~ its width), ties to the wider tile. Fewer square
+  // tiles than CUs: any saving (they idle CUs for the whole launch); more: a
+  // saving of at least 10 % (a partial last round - 640 square tiles are 2.5
+  // rounds, 1024 of 256 x 160 exactly 4 - against the square kernels' higher
+  // reuse and, fp8, the streaming kernel). DLNB_GEMM_NARROW_NF=8 pins the
+  // square tile (A/B), 3-6 forces a width where it divides N.
   static const int forced = [] {
     const char* v = std::getenv("DLNB_GEMM_NARROW_NF");
     return v ? std::atoi(v) : 0;
   }();
   if (forced >= 3 && forced <= 8 && forced != 7) return (forced == 8 || N % (32 * forced) == 0) ? forced : 8;
-  const int sq = (M / kT) * (N / kT);
-  if (sq >= cus) return 8;
+  const long sq = static_cast<long>(M / kT) * (N / kT);
+  const long sq_cost = (sq + cus - 1) / cus * 8;
   int best = 8;
-  long best_cost = static_cast<long>((sq + cus - 1) / cus) * 8;
+  long best_cost = sq_cost;
   for (int nf = 6; nf >= 3; --nf) {  // (nf = 7 spills its accumulators out of the AGPRs)
     if (N % (32 * nf) != 0) continue;
     const long t = static_cast<long>(M / kT) * (N / (32 * nf));
@@ -735,6 +738,7 @@ int gemm_narrow_nf(int M, int N, int cus) {
       best_cost = cost;
     }
   }
+  if (sq >= cus && best_cost * 10 > sq_cost * 9) return 8;
   return best;
 }
 
@@ -785,6 +789,10 @@ void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int 
     int dev = 0;
     return hipGetDevice(&dev) == hipSuccess ? num_cus(dev) : 256;
   }();
+  // A narrower tile when it saves rounds of tile work: fewer square tiles than
+  // CUs (the ViT-H FFN down projection 8192 x 1280: 160 square tiles, 256 of
+  // 256 x 160) or a partial last round (gemm_narrow_nf).
+  if (gemm_tn_narrow(A, B, C, M, N, K, lda, ldb, ldc, DType::FP8_E4M3, stream)) return;
   if (tiles > cus) {
     hipLaunchKernelGGL(gemm_4wave_fp8_stream_kernel<false>, cus, 256, 0, static_cast<hipStream_t>(stream),
                        static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K,
@@ -793,9 +801,6 @@ void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int 
     if (e != hipSuccess) DLNB_THROW("gemm 4-wave fp8 stream launch failed: " << hipGetErrorString(e));
     return;
   }
-  // Fewer 256 x 256 tiles than CUs: a narrower tile may fill the chip (the
-  // ViT-H FFN down projection 8192 x 1280: 160 square tiles, 256 of 256 x 160).
-  if (gemm_tn_narrow(A, B, C, M, N, K, lda, ldb, ldc, DType::FP8_E4M3, stream)) return;
   hipLaunchKernelGGL(gemm_4wave_fp8_kernel<false>, tiles, 256, 0, static_cast<hipStream_t>(stream),
                      static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda,
                      ldb, ldc, group, nullptr, 0u, 0ull, 0ull, nullptr);

@@ -543,7 +543,8 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
   const int tiles = (M / kTile) * (N / kTile);
   // 0: fp8 the one-wave-per-SIMD MX kernel where it applies (+5-7 % over the
   // 8-phase one), else the 8-phase kernel where it applies, else 8 waves
-  // bf16 with fewer square tiles than CUs: 256 x 32 nf tiles (fp8: inside variant 5)
+  // bf16 where 256 x 32 nf tiles save rounds of tile work (fewer square tiles
+  // than CUs, or a partial last round; fp8: inside variant 5)
   if (variant == 0 && in_t == DType::BF16 && gemm_tn_narrow(A, B, C, M, N, K, lda, ldb, ldc, in_t, stream)) return;
   if (variant == 0)
     variant = gemm_4wave_fp8_shape_ok(M, N, K, in_t) ? 5 : gemm_8phase_shape_ok(M, N, K, in_t) ? 6 : 8;
