@@ -42,6 +42,10 @@ struct ComputeShape {
   int ffn = 16384;    // FFN width (K)
   DType dtype = DType::BF16;
   int comm_cus = 32;  // CUs the persistent compute leaves to collectives
+  // Ranks sharing the device (loopback rank threads, several processes on one
+  // GPU): their deadline tasks are cut into 500-us slices by default so that
+  // the ranks' compute interleaves as it would on separate GPUs.
+  int ranks_on_device = 1;
 };
 
 class ComputeEngine {

@@ -48,6 +48,7 @@ struct Context {
   // RCCL CTA cap for communicators whose collectives run on a comm lane
   // (a stream beside the compute); 0 = library default.
   int lane_ctas = 0;
+  int ranks_on_device = 1;  // ranks of this job sharing this rank's device (loopback, -d 0,0)
   // --timeline: the spans of this rank (declared last: released before the
   // device whose stamp slots it holds)
   std::unique_ptr<Timeline> timeline;

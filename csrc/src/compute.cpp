@@ -110,7 +110,12 @@ class GpuCompute : public ComputeEngine {
       // 500-us slices every slice also abandons a partial 256 x 256 tile and
       // pays a prologue: 630 vs 679 TF/s per GHz on the headline
       // (profiles/slice_ab_r3.md), and a 4x larger graph.
-      slice_us_ = static_cast<double>(env_int("DLNB_GEMM_SLICE_US", 0));
+      // Ranks sharing one GPU (loopback, -d 0,0) keep 500-us slices: with one
+      // launch per task a rank's persistent grid holds the CUs for its whole
+      // task and the other ranks' compute (and so the collectives that wait
+      // for it) serialises behind it - 8 loopback ranks of the llama3_8b FSDP
+      // config ran 459 vs 317 ms per iteration (profiles/loopback_w8_r3.md).
+      slice_us_ = static_cast<double>(env_int("DLNB_GEMM_SLICE_US", shape.ranks_on_device > 1 ? 500 : 0));
     }
   }
 

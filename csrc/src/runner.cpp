@@ -261,6 +261,9 @@ std::string select_backend(Context& ctx, const std::string& requested, const std
                  "local rank " << ri.local_rank << " has no device (device list has " << list.size() << ")");
     int dev_index = list[static_cast<size_t>(ri.local_rank)];
     DLNB_REQUIRE(dev_index >= 0 && dev_index < ngpu, "device id " << dev_index << " out of range");
+    ctx.ranks_on_device = 0;
+    for (int r = 0; r < ri.local_size && r < static_cast<int>(list.size()); ++r)
+      ctx.ranks_on_device += list[static_cast<size_t>(r)] == dev_index;
     ctx.dev = make_gpu_device(dev_index);
     ctx.comms = backend == "rccl"    ? make_rccl_factory(ctx.hg(), *ctx.dev)
                 : backend == "xgmi" ? make_xgmi_factory(ctx.hg(), *ctx.dev)
@@ -283,6 +286,7 @@ std::string select_backend(Context& ctx, const std::string& requested, const std
         DLNB_REQUIRE(d == dev_index, "--backend loopback puts every rank on one device (-d " << devices << ")");
       DLNB_REQUIRE(dev_index >= 0 && dev_index < ngpu, "device id " << dev_index << " out of range");
       ctx.dev = make_gpu_device(dev_index);
+      ctx.ranks_on_device = ri.world_size;
     }
     ctx.comms = make_loopback_factory(ctx.hg(), *ctx.dev, ctx.boot->hub);
   } else {
@@ -444,6 +448,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   if (cdt == "auto") cdt = ctx.stats.dtype.find("8") != std::string::npos ? "fp8" : "bf16";
   shape.dtype = parse_dtype(cdt);
   shape.comm_cus = opt.comm_cus;
+  shape.ranks_on_device = std::max(1, ctx.ranks_on_device);
   ComputeMode mode = parse_compute_mode(opt.compute, ctx.dev->kind());
   ctx.compute = make_compute_engine(*ctx.dev, mode, shape, opt.time_scale);
   if (!opt.timeline_path.empty()) {

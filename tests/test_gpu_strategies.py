@@ -166,6 +166,9 @@ def test_fsdp_llama3_8b_loopback_8_ranks_one_gpu(root):
     assert g["allgather_msg_size_bytes"] == 250945664 * 2  # the gathered unit, as at N=1
     it = g["dlnb"]["iteration"]
     assert it["median_ms"] >= 0.9 * it["compute_floor_ms"]
+    # ranks sharing the GPU cut their deadline tasks into 500-us slices (compute.cpp), so the eight ranks'
+    # compute interleaves instead of queueing behind one rank's persistent grid
+    assert g["dlnb"]["compute"]["deadline_slice_us"] == 500
 
 
 def test_compute_stretch_fixed_work(data_dir):
