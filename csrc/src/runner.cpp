@@ -276,6 +276,7 @@ std::string select_backend(Context& ctx, const std::string& requested, const std
     if (backend == "loopback-cpu") {
       // CPU device only: no HIP call at all (GPU-less hosts and CPU tests)
       ctx.dev = make_cpu_device(loopback_cpu_abort_flag(*ctx.boot->hub));
+      ctx.ranks_on_device = ri.world_size;
     } else {
       // Every rank on the same GPU: the one given by -d (default 0).
       const int ngpu = gpu_device_count();
@@ -669,6 +670,9 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   ext["warmup_times"] = Json(warm);
   ext["timed_region_s"] = timed_region;
   ext["energy_source"] = meter->source();
+  // ranks of this job on this rank's device (> 1: loopback threads or -d 0,0;
+  // the deadline compute then runs in 500-us slices, compute.cpp)
+  ext["ranks_on_device"] = ctx.ranks_on_device;
   if (TL) ext["timeline"] = timeline_info;
   {
     Json b = Json::object();

@@ -79,6 +79,7 @@ def test_dp_loopback(w, data_dir):
     d = run(w, "dp", "tiny_dense_8_bfloat16", 5, data_dir, "-w", 1, "-r", 3)
     g = d["global"]
     assert DP_GLOBAL <= set(g) and g["world_size"] == w and g["backend"] == "LOOPBACK"
+    assert g["dlnb"]["ranks_on_device"] == w  # every rank thread on the one device
     assert len(d["ranks"]) == w
     for r in d["ranks"]:
         assert DP_RANK <= set(r) and len(r["runtimes"]) == 3
