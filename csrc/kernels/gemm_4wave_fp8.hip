@@ -37,9 +37,13 @@
 //     gemm_4wave_fp8_stream_kernel<false> (persistent, a block's tiles as one
 //     K-tile stream; the one-shot default with more tiles than CUs),
 //     gemm_4wave_fp8_kernel<true> (the persistent deadline compute stand-in)
-//     and gemm_4wave_fp8_stream_kernel<true> (its streaming variant, opt-in).
+//     and gemm_4wave_fp8_stream_kernel<true> (its streaming variant, opt-in);
+//     gemm_4wave_narrow_kernel<NF, BF16> (256 x 32 NF tiles, bf16 or fp8, for
+//     outputs whose square tiles would leave CUs idle; see "Narrow-N tiles").
+//   * Epilogues store two adjacent fragments per 16-byte store (store_pair.hpp).
 //
-// Variant 5 of dlnb::kernels::gemm_tn for fp8 (K a multiple of 256 bytes).
+// Variant 5 of dlnb::kernels::gemm_tn for fp8 (K a multiple of 256 bytes), and
+// the narrow-tile path of the default variant for bf16.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
