@@ -139,6 +139,7 @@ def rows(lines: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
             "tl_hidden_frac": _get(d, "timeline", "comm_hidden_frac"),
             "link_ar_busbw_rccl": _largest(_get(d, "link_bench", "rccl", "all_reduce")),
             "link_ar_busbw_xgmi": _largest(_get(d, "link_bench", "xgmi_registered", "all_reduce")),
+            "wall_s": _get(d, "phase_seconds", "total"),
         }
         out.append(r)
     return out

@@ -67,6 +67,7 @@ def test_exactness_and_hybrid_columns():
     d["hybrid_3d"] = {"ms_per_step": 3900.0, "vs_floor": 1.02}
     d["hybrid_3d_moe"] = {"ms_per_step": 15000.0, "vs_floor": 1.1, "ep_overlap": {"ms_per_step": 13600.0}}
     d["predicted_ms"] = 2815.9
+    d["phase_seconds"] = {"headline": 72.5, "total": 231.4}
     d["link_bench"] = {"rccl": {"all_reduce": {"8388608": {"busbw_GBps": 250.0}, "67108864": {"busbw_GBps": 310.0}}},
                        "xgmi_registered": {"error": "x"}}
     r = bench_report.rows([d])[0]
@@ -74,6 +75,7 @@ def test_exactness_and_hybrid_columns():
     assert r["link_ar_busbw_rccl"] == 310.0 and r["link_ar_busbw_xgmi"] is None
     assert r["c5_geometric_ms"] == 7.25 and r["exact_rccl"] is True and r["exact_xgmi"] is False
     assert r["rccl_nranks"] == 8 and r["c3_vs_floor"] == 1.02 and r["c4_ms"] == 15000.0
+    assert r["wall_s"] == 231.4
     r1 = bench_report.rows([json.loads(_line(1, 2816.0))])[0]
     assert r1["exact_rccl"] is None and r1["rccl_nranks"] is None and r1["c3_ms"] is None
 
