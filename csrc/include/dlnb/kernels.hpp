@@ -59,7 +59,7 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
              void* stream, int variant = 0);
 bool gemm_8phase_shape_ok(int M, int N, int K, DType in_t);
 bool gemm_4wave_fp8_shape_ok(int M, int N, int K, DType in_t);
-// Tile width 32 nf (nf 3..6, or 8 = the square 256 x 256 tile of the other
+// Tile width 32 nf (nf 3..7, or 8 = the square 256 x 256 tile of the other
 // kernels) a one-shot GEMM of an M x N output uses on `cus` CUs: narrower
 // tiles when the square ones leave CUs idle - fewer tiles than CUs, or a last
 // round at least 10 % short (gemm_4wave_fp8.hip, narrow kernel).

@@ -502,8 +502,7 @@ __global__ void __launch_bounds__(256, 1)
 
 // ---------------------------------------------------------------------------
 // Narrow-N tiles (one-shot only): 256 x 32·NF of C per block, 128 x 16·NF per
-// wave (acc[8][NF] AGPRs), NF in 3..6 (at 7 hipcc moves the accumulators out
-// of the AGPRs and spills).
+// wave (acc[8][NF] AGPRs), NF in 3..7.
 //
 // A 256 x 256 tile grid quantises badly on skinny outputs: the ViT-H / GPT-2-L
 // FFN down projection (M = 8192 tokens, N = 1280, the C5 stand-in shape) is
@@ -542,7 +541,7 @@ struct Narrow {
     }
     return m;
   }
-  static_assert(NF >= 3 && NF <= 6, "narrow tile: NF 3..6");
+  static_assert(NF >= 3 && NF <= 7, "narrow tile: NF 3..7");
   static_assert(a_part_slot(kEarly - 1) < kM, "A(t+1) reads must fit the K-tile");
 };
 
@@ -728,12 +727,12 @@ int gemm_narrow_nf(int M, int N, int cus) {
     const char* v = std::getenv("DLNB_GEMM_NARROW_NF");
     return v ? std::atoi(v) : 0;
   }();
-  if (forced >= 3 && forced <= 8 && forced != 7) return (forced == 8 || N % (32 * forced) == 0) ? forced : 8;
+  if (forced >= 3 && forced <= 8) return (forced == 8 || N % (32 * forced) == 0) ? forced : 8;
   const long sq = static_cast<long>(M / kT) * (N / kT);
   const long sq_cost = (sq + cus - 1) / cus * 8;
   int best = 8;
   long best_cost = sq_cost;
-  for (int nf = 6; nf >= 3; --nf) {  // (nf = 7 spills its accumulators out of the AGPRs)
+  for (int nf = 7; nf >= 3; --nf) {
     if (N % (32 * nf) != 0) continue;
     const long t = static_cast<long>(M / kT) * (N / (32 * nf));
     const long cost = (t + cus - 1) / cus * nf;
@@ -770,6 +769,7 @@ bool gemm_tn_narrow(const void* A, const void* B, void* C, int M, int N, int K, 
   else                                                                                                      \
     hipLaunchKernelGGL((gemm_4wave_narrow_kernel<NF, false>), nt, 256, 0, st, a, b, cc, M, N, K, lda, ldb, ldc, group)
   switch (nf) {
+    case 7: DLNB_NARROW(7); break;
     case 3: DLNB_NARROW(3); break;
     case 4: DLNB_NARROW(4); break;
     case 5: DLNB_NARROW(5); break;

@@ -68,7 +68,7 @@ def test_gemm_fp8_matches_torch(M, N, K, waves):
 
 @pytest.mark.parametrize("M,N,K,nf", [(2048, 1280, 128, 4), (8192, 1280, 5120, 5), (7168, 1280, 640, 5),
                                       (8192, 1536, 256, 6), (512, 768, 1024, 3), (8192, 768, 3072, 3),
-                                      (8192, 5120, 256, 5), (8192, 3072, 384, 6)])
+                                      (8192, 5120, 256, 5), (8192, 3072, 384, 6), (8192, 1792, 6400, 7)])
 def test_gemm_bf16_narrow_tiles(M, N, K, nf):
     """bf16 through the narrow-tile kernel (two 16x16x32 MFMAs per 128-byte K-tile row on the MX kernel's
     fragments), K down to the 2-K-tile minimum."""
@@ -86,7 +86,7 @@ def test_gemm_bf16_narrow_tiles(M, N, K, nf):
 @pytest.mark.parametrize("M,N,K,nf", [(2048, 1280, 256, 4), (8192, 1280, 5120, 5), (7168, 1280, 512, 5),
                                       (8192, 1536, 256, 6), (8192, 1024, 1280, 4), (768, 512, 2048, 4),
                                       (8192, 768, 3072, 3), (2048, 768, 256, 3), (8192, 5120, 512, 5),
-                                      (8192, 3072, 256, 6)])
+                                      (8192, 3072, 256, 6), (8192, 1792, 6400, 7), (2048, 1792, 256, 4)])
 def test_gemm_fp8_narrow_tiles(M, N, K, nf):
     """Fewer 256 x 256 tiles than CUs, or a partial last round (8192 x 5120: 640 square tiles): the MX fp8
     kernel's 256 x 32 nf tiles (gemm_4wave_fp8.hip, narrow kernel), including the ViT-H FFN down projection

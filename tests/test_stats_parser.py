@@ -116,6 +116,7 @@ def test_host_conversions_roundtrip():
     (8192, 1280, 224, 8),    # 224 CUs: 256 narrow tiles need 2 rounds of 5 > 1 round of 8
     (512, 768, 256, 3),      # 6 square tiles: 16 of 256 x 96 (3 units each) beat 12 of 256 x 128 (4)
     (8192, 768, 256, 3),     # ViT-B: 96 -> 256 of 256 x 96
+    (8192, 1792, 256, 7),    # GPT-2-XL hidden (1600, stand-in 1792): 224 -> 256 of 256 x 224
     (8192, 5120, 256, 5),    # 640 square tiles = 2.5 rounds (cost 24); 1024 of 256 x 160 = 4 rounds (20)
     (8192, 3072, 256, 6),    # 384 = 1.5 rounds (16); 512 of 256 x 192 = 2 rounds (12)
     (8192, 6144, 256, 8),    # 768 = 3 rounds (24); 1024 of 256 x 192 = 4 (24): no saving
