@@ -135,6 +135,84 @@ def _mean_of(doc: dict, key: str) -> Optional[float]:
     return round(sum(vals) / len(vals) * 1e3, 4) if vals else None
 
 
+def _run_bounded(cmd: list, env: dict, timeout: float, stdout: Any = subprocess.PIPE) -> subprocess.CompletedProcess:
+    """subprocess.run with the child killed at `timeout` and reported as an
+    error (never an exception that skips the rest of the bench)."""
+    try:
+        return subprocess.run(cmd, env=env, timeout=timeout, stdout=stdout, stderr=subprocess.PIPE, text=True)
+    except subprocess.TimeoutExpired as e:
+        err = e.stderr.decode(errors="replace") if isinstance(e.stderr, bytes) else (e.stderr or "")
+        raise RuntimeError(f"timeout after {timeout:.0f} s (wall budget): " + err[-200:]) from None
+
+
+class _Budget:
+    """The bench's wall-clock budget (the N > 1 run must print
+    its line within a bounded time, whatever hangs). Every phase after the
+    headline asks plan(name, want_s, need_s) for its child's time limit: the
+    smaller of what it wants and what is left (minus a reserve for the final
+    line); None = skip the phase (less than need_s left). All ranks must take
+    the same decisions (a rank that skips a phase its peers run leaves them
+    waiting at a rendezvous), so on one node rank 0 decides and publishes
+    each decision in a file the other ranks wait for; across nodes every rank
+    decides from its own clock (the phases are lockstep, so the clocks agree
+    to the rendezvous skew)."""
+
+    def __init__(self, total_s: float, reserve_s: float, world: int, rank: int) -> None:
+        import time
+        self._t = time.monotonic
+        self.start = self._t()
+        self.total, self.reserve, self.world, self.rank = total_s, reserve_s, world, rank
+        self.shared = world > 1 and int(os.environ.get("LOCAL_WORLD_SIZE", world)) == world
+        self.dir = f"/tmp/dlnb_bench_plan_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}"
+        self.plans: Dict[str, Any] = {}
+        self.seen_dir = False
+        if self.shared and rank == 0:
+            import atexit
+            import shutil
+            os.makedirs(self.dir, exist_ok=True)
+            atexit.register(lambda: shutil.rmtree(self.dir, ignore_errors=True))
+
+    def left(self) -> float:
+        return self.total - (self._t() - self.start) - self.reserve
+
+    def plan(self, name: str, want_s: float, need_s: float) -> Optional[float]:
+        import time
+        if not self.shared or self.rank == 0:
+            left = self.left()
+            t = round(min(want_s, left), 1)
+            dec = t if t >= need_s and t > 0 else None
+            if self.shared:
+                tmp = os.path.join(self.dir, name + ".tmp")
+                with open(tmp, "w") as f:
+                    json.dump({"timeout": dec}, f)
+                os.replace(tmp, os.path.join(self.dir, name + ".json"))
+        else:
+            path = os.path.join(self.dir, name + ".json")
+            deadline = self._t() + max(30.0, self.left() + self.reserve)
+            dec = None
+            while self._t() < deadline:
+                if os.path.exists(path):
+                    with open(path) as f:
+                        dec = json.load(f)["timeout"]
+                    break
+                if os.path.isdir(self.dir):
+                    self.seen_dir = True
+                elif self.seen_dir:
+                    break  # rank 0 has finished (and removed the plans): nothing more runs
+                time.sleep(0.02)
+        self.plans[name] = dec
+        return dec
+
+    def report(self) -> Dict[str, Any]:
+        return {"wall_budget_s": self.total, "reserve_s": self.reserve,
+                "timeouts_s": {k: v for k, v in self.plans.items() if v is not None},
+                "skipped": [k for k, v in self.plans.items() if v is None]}
+
+
+def _skipped(budget: _Budget) -> Dict[str, Any]:
+    return {"skipped": f"wall budget ({budget.total:.0f} s) left too little time for this block"}
+
+
 def _child_run(a: argparse.Namespace, world: int, rank: int, tag: str, strategy: str, model: str,
                params: tuple, timeout: float, backend: str = "xgmi", graph: bool = True,
                **kw: Any) -> Dict[str, Any]:
@@ -144,13 +222,13 @@ def _child_run(a: argparse.Namespace, world: int, rank: int, tag: str, strategy:
     _store_env(world, rank, tag)
     out = f"/tmp/dlnb_bench{tag}_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}.json"
     args = engine.build_args(strategy, model, *params, base_path=a.base_path, backend=backend,
-                             graph=graph or None, devices=a.devices, time_scale=a.time_scale, quiet=True,
+                             graph=graph or None, devices=a.devices, time_scale=a.time_scale, silent=True,
                              json=out if rank == 0 else None, **kw)
-    env = dict(os.environ, DLNB_XGMI_TIMEOUT_S=os.environ.get("DLNB_XGMI_TIMEOUT_S", "20"))
-    # bounded well below any driver limit, so a first-time cross-device
-    # failure costs a minute or two and the headline line still prints
-    p = subprocess.run([os.path.join(ROOT, "build", "bin", strategy), *args], env=env, timeout=timeout,
-                       stdout=sys.stderr, stderr=subprocess.PIPE, text=True)
+    env = dict(os.environ, DLNB_XGMI_TIMEOUT_S=os.environ.get("DLNB_XGMI_TIMEOUT_S", "20"),
+               DLNB_BLOCK=tag.lstrip("."), DLNB_STORE_TIMEOUT=str(max(10, int(timeout))))
+    # bounded by the wall budget (_Budget), so a first-time cross-device
+    # failure costs this block and the line still prints
+    p = _run_bounded([os.path.join(ROOT, "build", "bin", strategy), *args], env, timeout, stdout=sys.stderr)
     if p.returncode != 0:
         raise RuntimeError(f"exit {p.returncode}: " + (p.stderr or "")[-300:])
     if rank != 0:
@@ -181,7 +259,7 @@ def _exact_backends(a: argparse.Namespace) -> str:
     return "rccl,xgmi"
 
 
-def _exactness(a: argparse.Namespace, world: int, rank: int) -> Dict[str, Any]:
+def _exactness(a: argparse.Namespace, world: int, rank: int, timeout: float) -> Dict[str, Any]:
     """Before any timed phase of a multi-rank job: every collective (all-reduce
     in and out of place, all-gather, reduce-scatter, all-to-all, ring
     send/recv) of every backend the bench times, eager and graph-replayed
@@ -197,9 +275,8 @@ def _exactness(a: argparse.Namespace, world: int, rank: int) -> Dict[str, Any]:
     if a.devices:
         cmd += ["-d", a.devices]
     env = dict(os.environ, DLNB_XGMI_TIMEOUT_S=os.environ.get("DLNB_EXACT_XGMI_TIMEOUT_S", "10"),
-               DLNB_STORE_TIMEOUT=str(int(a.exact_timeout)))
-    p = subprocess.run(cmd, env=env, timeout=a.exact_timeout, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                       text=True)
+               DLNB_STORE_TIMEOUT=str(max(10, int(timeout))), DLNB_BLOCK="exact")
+    p = _run_bounded(cmd, env, timeout)
     if not os.path.exists(out):
         raise RuntimeError(f"exit {p.returncode}: " + (p.stderr or "")[-300:])
     with open(out) as f:
@@ -208,7 +285,8 @@ def _exactness(a: argparse.Namespace, world: int, rank: int) -> Dict[str, Any]:
     return d
 
 
-def _link_bench(a: argparse.Namespace, world: int, rank: int, backend: str, registered: bool) -> Dict[str, Any]:
+def _link_bench(a: argparse.Namespace, world: int, rank: int, backend: str, registered: bool,
+                timeout: float) -> Dict[str, Any]:
     """Collective bandwidth on the job's own GPUs, nothing else running
     (`dlnb commtest --bench --graph`: 10 graph-replayed ops per size after 3
     warm-ups, nccl-tests algbw / busbw, max time over ranks): what the links
@@ -225,9 +303,8 @@ def _link_bench(a: argparse.Namespace, world: int, rank: int, backend: str, regi
     if a.devices:
         cmd += ["-d", a.devices]
     env = dict(os.environ, DLNB_XGMI_TIMEOUT_S=os.environ.get("DLNB_XGMI_TIMEOUT_S", "20"),
-               DLNB_STORE_TIMEOUT=str(int(a.link_timeout)))
-    p = subprocess.run(cmd, env=env, timeout=a.link_timeout, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                       text=True)
+               DLNB_STORE_TIMEOUT=str(max(10, int(timeout))), DLNB_BLOCK="link_" + backend)
+    p = _run_bounded(cmd, env, timeout)
     if p.returncode != 0:
         raise RuntimeError(f"exit {p.returncode}: " + (p.stderr or "")[-300:])
     if rank != 0:
@@ -244,7 +321,8 @@ def _link_bench(a: argparse.Namespace, world: int, rank: int, backend: str, regi
     return out
 
 
-def _link_block(a: argparse.Namespace, world: int, rank: int, xgmi_ok: bool) -> Dict[str, Any]:
+def _link_block(a: argparse.Namespace, world: int, rank: int, xgmi_ok: bool, budget: "_Budget",
+                est: "_Estimator") -> Dict[str, Any]:
     """RCCL, xgmi staged and xgmi zero-copy collective bandwidth at N > 1."""
     res: Dict[str, Any] = {"dtype": "bf16", "elements_per_rank": [int(x) for x in a.link_sizes.split(",")],
                            "hip_graph": a.backend != "cpu"}
@@ -256,17 +334,21 @@ def _link_block(a: argparse.Namespace, world: int, rank: int, xgmi_ok: bool) -> 
         else:
             res["xgmi"] = {"error": "skipped: the xgmi exactness check failed on these ranks"}
     for key, backend, reg in runs:
+        t = budget.plan("link_bench_" + key, min(a.link_timeout, 2 * est.setup + 40), est.setup + 5)
+        if t is None:
+            res[key] = _skipped(budget)
+            continue
         try:
-            res[key] = _link_bench(a, world, rank, backend, reg)
+            res[key] = _link_bench(a, world, rank, backend, reg, t)
         except Exception as e:  # noqa: BLE001
             res[key] = {"error": str(e)[:300]}
     return res
 
 
-def _exact_block(a: argparse.Namespace, world: int, rank: int) -> Dict[str, Any]:
+def _exact_block(a: argparse.Namespace, world: int, rank: int, timeout: float) -> Dict[str, Any]:
     res: Dict[str, Any] = {}
     try:
-        d = _exactness(a, world, rank)
+        d = _exactness(a, world, rank, timeout)
         res = {"exact": d["exact"], "exact_detail": {
             "ok": d["ok"], "seconds": round(d["seconds"], 2), "sizes": d["sizes"], "xgmi_release": d["xgmi_release"],
             "rccl_nranks": d["rccl_nranks"], "world_size": d["world_size"],
@@ -295,6 +377,33 @@ class _Phases:
 
     def report(self) -> Dict[str, float]:
         return dict(self.s, total=round(self._t() - self.start, 2))
+
+
+class _Estimator:
+    """Expected wall seconds of a child run, for its time limit: setup (the
+    headline's own: process start, RCCL / xgmi communicators, buffers, graph
+    capture; scaled for the hybrids' larger working sets) + its iterations at
+    the xGMI cost model's iteration time (x --time-scale), or the headline's
+    measured one. A block's limit is 2x that + 20 s, capped by its flag and by
+    the wall budget (_Budget.plan)."""
+
+    def __init__(self, a: argparse.Namespace, world: int, headline_s: float, headline_iters: int,
+                 headline_ms: float) -> None:
+        self.a, self.world = a, world
+        self.head_ms = headline_ms
+        self.setup = max(5.0, 1.5 * (headline_s - headline_iters * headline_ms / 1e3))
+
+    def iter_s(self, strategy: str, model: str, params: tuple, **kw: Any) -> float:
+        a = self.a
+        try:
+            from dlnetbench_amd.parallel.plan import predict
+            ms = predict(strategy, model, list(params), self.world, base=a.base_path, **kw)["iter_ms"]
+        except Exception:  # noqa: BLE001
+            ms = self.head_ms
+        return ms * (a.time_scale if a.time_scale is not None else 1.0) / 1e3
+
+    def want(self, nominal_s: float, cap_s: float) -> float:
+        return min(cap_s, 2.0 * nominal_s + 20.0)
 
 
 def _predicted_ms(a: argparse.Namespace, world: int, strategy: str, model: str, params: tuple,
@@ -344,23 +453,37 @@ def _model_fit(a: argparse.Namespace, world: int, extra: Dict[str, Any]) -> Opti
         return {"error": str(e)[:300]}
 
 
+def _per_run_ms(d: dict) -> list:
+    """Every timed iteration's time (ms): the slowest rank's per run."""
+    return [round(x * 1e3, 3) for x in d["global"]["dlnb"]["iteration"].get("per_run_max_s", [])]
+
+
 def _hybrid_block(a: argparse.Namespace, world: int, rank: int, tag: str, strategy: str, model: str,
-                  params: tuple, floor_note: str, ep_overlap: bool = False) -> Dict[str, Any]:
+                  params: tuple, floor_note: str, budget: "_Budget", est: "_Estimator", runs: int,
+                  ep_overlap: bool = False) -> Dict[str, Any]:
     """One BASELINE hybrid config (C3 hybrid_3d / C4 hybrid_3d_moe) on the job's
-    GPUs over RCCL: 1 warm-up + 1 timed iteration in a child process, its
-    time against the GPipe compute floor and the xGMI model's prediction, and
-    its per-group communication. ep_overlap: the same config with
-    --ep-overlap (each half-microbatch's all-to-all under the other half's
-    compute instead of on the compute stream)."""
+    GPUs over RCCL: 1 warm-up + `runs` timed iterations in a child process
+    (every run's time in per_run_ms; the reference's hybrid_3d default is 3
+    runs, cpp/hybrid_parallel/hybrid_3d.cpp:62 - as many as the wall budget
+    affords), its time against the GPipe compute floor and the xGMI model's
+    prediction, and its per-group communication. ep_overlap: the same config
+    with --ep-overlap (each half-microbatch's all-to-all under the other
+    half's compute instead of on the compute stream)."""
     res: Dict[str, Any] = {"model": model, "strategy": strategy, "params": list(params), "backend": "RCCL"}
     if ep_overlap:
         res["ep_overlap"] = True
+    nominal = 2 * est.setup + 10 + (1 + runs) * est.iter_s(strategy, model, params, ep_overlap=ep_overlap)
+    t = budget.plan(tag.lstrip("."), est.want(nominal, a.hybrid_timeout), nominal)
+    if t is None:
+        res.update(_skipped(budget))
+        return res
     try:
-        d = _child_run(a, world, rank, tag, strategy, model, params, a.hybrid_timeout, backend=a.hybrid_backend,
-                       graph=False, compute=a.compute, warmup=1, runs=1, ep_overlap=ep_overlap or None)
+        d = _child_run(a, world, rank, tag, strategy, model, params, t, backend=a.hybrid_backend,
+                       graph=False, compute=a.compute, warmup=1, runs=runs, ep_overlap=ep_overlap or None)
         if rank != 0:
             return res
         g, it = d["global"], d["global"]["dlnb"]["iteration"]
+        res["per_run_ms"] = _per_run_ms(d)
         pred = _predicted_ms(a, world, strategy, model, params, ep_overlap=ep_overlap)
         res.update({"ms_per_step": round(it["timed_ms_per_iter"], 3), "median_ms": round(it["median_ms"], 3),
                     "floor_ms": round(it["compute_floor_ms"], 3), "floor_note": floor_note,
@@ -384,12 +507,16 @@ def _hybrid_block(a: argparse.Namespace, world: int, rank: int, tag: str, strate
     return res
 
 
-def _xgmi_ab(a: argparse.Namespace, world: int, rank: int, c5: dict) -> Dict[str, Any]:
+def _xgmi_ab(a: argparse.Namespace, world: int, rank: int, c5: dict, budget: "_Budget",
+             est: "_Estimator") -> Dict[str, Any]:
     """The comm-bound DP secondary over the xgmi backend (HIP graph)."""
     res: Dict[str, Any] = {"backend": "XGMI", "hip_graph": True}
+    nominal = est.setup + (5 + a.c5_steps) * est.iter_s("dp", a.c5_model, (a.c5_buckets,), wire=a.c5_wire)
+    t = budget.plan("comm_bound_xgmi", est.want(nominal, 90), nominal)
+    if t is None:
+        return _skipped(budget)
     try:
-        # ~10 s expected (55 iterations of ~7.5 ms + setup)
-        d = _xgmi_child(a, world, rank, ".xgmi", "dp", a.c5_model, (a.c5_buckets,), 90, warmup=5,
+        d = _xgmi_child(a, world, rank, ".xgmi", "dp", a.c5_model, (a.c5_buckets,), t, warmup=5,
                         runs=a.c5_steps, wire_dtype=a.c5_wire)
         if rank != 0:
             return res
@@ -407,7 +534,8 @@ def _xgmi_ab(a: argparse.Namespace, world: int, rank: int, c5: dict) -> Dict[str
     return res
 
 
-def _timeline_block(a: argparse.Namespace, world: int, rank: int) -> Dict[str, Any]:
+def _timeline_block(a: argparse.Namespace, world: int, rank: int, budget: "_Budget",
+                    est: "_Estimator") -> Dict[str, Any]:
     """The headline configuration again for 1 + 2 iterations with --timeline
     (device-clock spans of every collective and compute task on every rank,
     csrc/src/timeline.cpp), summarised: per rank how much communication ran
@@ -416,8 +544,12 @@ def _timeline_block(a: argparse.Namespace, world: int, rank: int) -> Dict[str, A
     from dlnetbench_amd.tools import timeline as tlt
     res: Dict[str, Any] = {"iterations": 2}
     path = f"/tmp/dlnb_bench.trace_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}.json"
+    nominal = est.setup + 3 * est.head_ms / 1e3
+    t = budget.plan("timeline", est.want(nominal, a.timeline_timeout), nominal)
+    if t is None:
+        return _skipped(budget)
     try:
-        _child_run(a, world, rank, ".tl", "fsdp", a.model, (a.units, world), a.timeline_timeout,
+        _child_run(a, world, rank, ".tl", "fsdp", a.model, (a.units, world), t,
                    backend=a.hybrid_backend, graph=a.graph and a.backend in ("auto", "rccl", "xgmi"),
                    compute=a.compute, warmup=1, runs=2,
                    schedule=a.schedule, wire_dtype="bf16", timeline=path, timeline_iters=2)
@@ -460,14 +592,18 @@ def _timeline_block(a: argparse.Namespace, world: int, rank: int) -> Dict[str, A
     return res
 
 
-def _headline_xgmi(a: argparse.Namespace, world: int, rank: int, doc: dict) -> Dict[str, Any]:
+def _headline_xgmi(a: argparse.Namespace, world: int, rank: int, doc: dict, budget: "_Budget",
+                   est: "_Estimator") -> Dict[str, Any]:
     """The headline FSDP step itself over the xgmi kernels (zero-copy
     all-gather / reduce-scatter into registered buffers): its effective bus
     bandwidth next to the headline's, under the same deadline compute."""
     res: Dict[str, Any] = {"backend": "XGMI", "hip_graph": True}
+    nominal = est.setup + (1 + a.xgmi_headline_steps) * est.head_ms / 1e3
+    t = budget.plan("headline_xgmi", est.want(nominal, 150), nominal)
+    if t is None:
+        return _skipped(budget)
     try:
-        # ~4 iterations of ~2.8 s + setup
-        d = _xgmi_child(a, world, rank, ".xgmih", "fsdp", a.model, (a.units, world), 150, warmup=1,
+        d = _xgmi_child(a, world, rank, ".xgmih", "fsdp", a.model, (a.units, world), t, warmup=1,
                         runs=a.xgmi_headline_steps, schedule=a.schedule, wire_dtype="bf16")
         if rank != 0:
             return res
@@ -482,6 +618,95 @@ def _headline_xgmi(a: argparse.Namespace, world: int, rank: int, doc: dict) -> D
     except Exception as e:  # noqa: BLE001
         res = {"error": str(e)[:300]}
     return res
+
+
+def _dp_block(a: argparse.Namespace, world: int, rank: int, budget: _Budget, est: _Estimator, tag: str,
+              graph: bool, compute: str, **kw: Any) -> Dict[str, Any]:
+    """The comm-bound ViT-H DP step (BASELINE C5) as a child run of every rank,
+    bounded by the budget; returns the child's report (rank 0) or raises."""
+    nominal = est.setup + (5 + a.c5_steps) * est.iter_s("dp", a.c5_model, (a.c5_buckets,), wire=a.c5_wire)
+    if compute in ("gemm-work", "flops"):
+        nominal += 5.0  # the fixed-work calibration
+    t = budget.plan(tag.lstrip("."), est.want(nominal, 90), nominal)
+    if t is None:
+        raise _Skip()
+    return _child_run(a, world, rank, tag, "dp", a.c5_model, (a.c5_buckets,), t, backend=a.backend, graph=graph,
+                      compute=compute, warmup=5, runs=a.c5_steps, wire_dtype=a.c5_wire, **kw)
+
+
+class _Skip(Exception):
+    pass
+
+
+def _c5_blocks(a: argparse.Namespace, world: int, rank: int, budget: _Budget, est: _Estimator, graph: bool,
+               on_gpu: bool) -> Dict[str, Any]:
+    """BASELINE C5 (ViT-H/32 fp8 DP, 8 buckets) and its variants: RCCL's own
+    CTA count, geometric buckets, fixed-work compute (compute_stretch)."""
+    c5: Dict[str, Any] = {}
+
+    def common(d: dict) -> Dict[str, Any]:
+        it = d["global"]["dlnb"]["iteration"]
+        return {"ms_per_step": round(it["timed_ms_per_iter"], 4), "median_ms": round(it["median_ms"], 4),
+                "exposed_comm_ms": _mean_of(d, "barrier_time"),
+                "allreduce_busbw_GBps": _busbw(d, "allreduce", world)}
+
+    try:
+        d = _dp_block(a, world, rank, budget, est, ".c5", graph, a.compute)
+        if rank == 0:
+            it = d["global"]["dlnb"]["iteration"]
+            c5.update({
+                "model": a.c5_model, "strategy": f"dp{world}", "num_buckets": a.c5_buckets,
+                "wire_dtype": a.c5_wire, "compute": a.compute,
+                "compute_dtype": d["global"]["dlnb"]["compute"].get("gemm_dtype", "auto"),
+                **common(d),
+                "floor_ms": round(it["compute_floor_ms"], 4),
+                "allreduce_bytes": d["global"]["msg_size_avg_bytes"] * a.c5_buckets,
+                "allreduce_algbw_GBps": _algbw(d, "allreduce"),
+                "transport": "link" if world > 1 else "local-copy",
+                "backend": d["global"]["backend"],
+            })
+        else:
+            c5["backend"] = "?"
+    except _Skip:
+        return _skipped(budget)
+    except Exception as e:  # noqa: BLE001
+        # the variants still run: whether a block runs must not depend on an
+        # outcome that can differ between ranks (only on rank 0's plan)
+        c5["error"] = str(e)[:300]
+    variants = []
+    if on_gpu and a.c5_ctas_ab and a.hybrid_backend == "rccl":
+        # the same step with RCCL's own CTA count (no maxCTAs cap from the
+        # comm-CU budget): one comm lane cannot deadlock against another, so
+        # this shows what the 32-CU budget costs the all-reduce over the links
+        variants.append(("rccl_default_ctas", ".c5c", a.compute, {"rccl_max_ctas": 0}))
+    if 0 < a.c5_bucket_ratio < 1:
+        # opt-in policy: shrink the exposed tail (the last bucket's all-reduce
+        # runs after the backward ends)
+        variants.append(("geometric_buckets", ".c5g", a.compute, {"dp_bucket_ratio": a.c5_bucket_ratio}))
+    if a.stretch_steps > 0 and on_gpu:
+        variants.append(("gemm_work", ".c5w", "gemm-work", {}))
+    for key, tag, compute, kw in variants:
+        try:
+            d = _dp_block(a, world, rank, budget, est, tag, graph, compute, **kw)
+            if rank == 0:
+                v = common(d)
+                if key == "rccl_default_ctas":
+                    v["allreduce_algbw_GBps"] = _algbw(d, "allreduce")
+                if key == "geometric_buckets":
+                    v = {"bucket_ratio": a.c5_bucket_ratio, **v}
+                if key == "gemm_work":
+                    v.pop("allreduce_busbw_GBps")
+                    v["compute_stretch"] = d["global"]["dlnb"].get("compute_stretch")
+                c5[key] = v
+        except _Skip:
+            c5[key] = _skipped(budget)
+        except Exception as e:  # noqa: BLE001
+            c5[key] = {"error": str(e)[:300]}
+    return c5
+
+
+def _backend_key(name: Optional[str]) -> str:
+    return {"RCCL": "rccl", "XGMI": "xgmi", "CPU-SHM": "cpu", "MIXED": "mixed"}.get(name or "", (name or "").lower())
 
 
 def main() -> int:
@@ -500,6 +725,11 @@ def main() -> int:
                     help="device list by local rank, e.g. 0,0 to put 2 ranks on one GPU (xgmi backend tests)")
     ap.add_argument("--base-path", default=ROOT, help="directory holding model_stats/ and models/")
     ap.add_argument("--time-scale", type=float, default=None, help="scale every compute duration (tests)")
+    ap.add_argument("--wall-budget-s", type=float, default=float(os.environ.get("DLNB_BENCH_WALL_S", "480")),
+                    help="wall seconds for the whole bench: every phase after the headline gets at most what is "
+                         "left and is skipped when too little is (env DLNB_BENCH_WALL_S)")
+    ap.add_argument("--budget-reserve-s", type=float, default=10.0,
+                    help="seconds of the wall budget kept for writing the line")
     ap.add_argument("--c5-model", default=C5_MODEL, help="comm-bound DP secondary ('none' skips it)")
     ap.add_argument("--c5-buckets", type=int, default=8)
     ap.add_argument("--c5-steps", type=int, default=50)
@@ -525,8 +755,10 @@ def main() -> int:
                     help="BASELINE C3 hybrid_3d / C4 hybrid_3d_moe blocks (auto: N == 8 on the GPU)")
     ap.add_argument("--c3-model", default=C3_MODEL)
     ap.add_argument("--c3", default=C3_PARAMS, help="hybrid_3d num_stages,num_microbatches,num_tensor_shards")
+    ap.add_argument("--c3-runs", type=int, default=2, help="timed iterations of the C3 block")
     ap.add_argument("--c4-model", default=C4_MODEL)
     ap.add_argument("--c4", default=C4_PARAMS, help="hybrid_3d_moe num_stages,num_microbatches,num_expert_shards")
+    ap.add_argument("--c4-runs", type=int, default=1, help="timed iterations of the C4 blocks")
     ap.add_argument("--hybrid-timeout", type=float, default=150.0)
     ap.add_argument("--c4-ep-overlap", choices=["on", "off"], default="on",
                     help="also run C4 with --ep-overlap (the all-to-alls off the compute stream)")
@@ -557,14 +789,17 @@ def main() -> int:
     os.environ.setdefault("DLNB_STORE_TIMEOUT", "300")
     # Everything below is native (HIP + RCCL from /opt/rocm); torch is not needed.
     os.environ.setdefault("DLNB_NO_TORCH", "1")
+    budget = _Budget(a.wall_budget_s, a.budget_reserve_s, world, rank)
+    ph = _Phases()
+    on_gpu = a.backend in ("auto", "rccl", "xgmi")
     # Multi-rank: prove the collectives exact on these ranks before timing them.
     # (every rank gets the same all-reduced verdict, so all ranks take the
     # same decisions below)
-    ph = _Phases()
     exact: Dict[str, Any] = {}
     if a.exact == "on" or (a.exact == "auto" and world > 1):
         t0 = ph.now()
-        exact = _exact_block(a, world, rank)
+        t = budget.plan("exact", a.exact_timeout, 5.0)
+        exact = _exact_block(a, world, rank, t) if t else {"exact": {}, "exact_detail": _skipped(budget)}
         ph.add("exact", t0)
         if rank == 0:
             print(f"[bench] exactness: {json.dumps(exact)}", file=sys.stderr)
@@ -578,7 +813,6 @@ def main() -> int:
     from dlnetbench_amd import engine
     from dlnetbench_amd.utils.stats import load_stats
     st = load_stats(os.path.join(a.base_path, "model_stats", a.model + ".txt"))
-    on_gpu = a.backend in ("auto", "rccl", "xgmi")
     use_graph = a.graph and on_gpu and a.schedule == "overlap"
 
     def run(phase: str, strategy: str, model: str, *params: int, graph: bool, **kw: Any) -> dict:
@@ -592,204 +826,184 @@ def main() -> int:
     saved = os.dup(1)
     os.dup2(2, 1)
     extra: Dict[str, Any] = {}
+    doc: Optional[dict] = None
+    headline_error: Optional[str] = None
     try:
         fsdp_kw = dict(schedule=a.schedule, wire_dtype="bf16")
         t0 = ph.now()
         try:
-            doc = run("", "fsdp", a.model, a.units, world, graph=use_graph, warmup=a.warmup, runs=a.steps,
-                      compute=a.compute, json=a.json, **fsdp_kw)
-        except RuntimeError as e:
-            if not use_graph:
-                raise
-            # Graph capture is symmetric across ranks, so every rank takes this
-            # path; the retry rendezvouses on a fresh store.
-            print(f"[bench] HIP graph run failed ({e}); retrying with per-iteration enqueue", file=sys.stderr)
-            use_graph = False
-            doc = run(".retry", "fsdp", a.model, a.units, world, graph=False, warmup=a.warmup, runs=a.steps,
-                      compute=a.compute, json=a.json, **fsdp_kw)
+            try:
+                doc = run("", "fsdp", a.model, a.units, world, graph=use_graph, warmup=a.warmup, runs=a.steps,
+                          compute=a.compute, json=a.json, **fsdp_kw)
+            except RuntimeError as e:
+                if not use_graph:
+                    raise
+                # Graph capture is symmetric across ranks, so every rank takes this
+                # path; the retry rendezvouses on a fresh store.
+                print(f"[bench] HIP graph run failed ({e}); retrying with per-iteration enqueue", file=sys.stderr)
+                use_graph = False
+                doc = run(".retry", "fsdp", a.model, a.units, world, graph=False, warmup=a.warmup, runs=a.steps,
+                          compute=a.compute, json=a.json, **fsdp_kw)
+        except Exception as e:  # noqa: BLE001
+            # still print a line (value null, the error): the driver reads
+            # what failed instead of nothing
+            headline_error = str(e)[:500]
         ph.add("headline", t0)
-        # Secondary measurements: failures are reported, never fatal to the headline.
-        t0 = ph.now()
-        if a.c5_model != "none":
-            c5: Dict[str, Any] = {}
-            try:
-                d = run(".c5", "dp", a.c5_model, a.c5_buckets, graph=use_graph, warmup=5, runs=a.c5_steps,
-                        compute=a.compute, wire_dtype=a.c5_wire)
-                it = d["global"]["dlnb"]["iteration"]
-                c5.update({
-                    "model": a.c5_model, "strategy": f"dp{world}", "num_buckets": a.c5_buckets,
-                    "wire_dtype": a.c5_wire, "compute": a.compute,
-                    "compute_dtype": d["global"]["dlnb"]["compute"].get("gemm_dtype", "auto"),
-                    "ms_per_step": round(it["timed_ms_per_iter"], 4), "median_ms": round(it["median_ms"], 4),
-                    "floor_ms": round(it["compute_floor_ms"], 4),
-                    "exposed_comm_ms": _mean_of(d, "barrier_time"),
-                    "allreduce_bytes": d["global"]["msg_size_avg_bytes"] * a.c5_buckets,
-                    "allreduce_busbw_GBps": _busbw(d, "allreduce", world),
-                    "allreduce_algbw_GBps": _algbw(d, "allreduce"),
-                    "transport": "link" if world > 1 else "local-copy",
-                    "backend": d["global"]["backend"],
-                })
-            except Exception as e:  # noqa: BLE001
-                c5["error"] = str(e)[:300]
-            if on_gpu and c5.get("backend") == "RCCL" and a.c5_ctas_ab:
-                # The same step with RCCL's own CTA count (no maxCTAs cap from the
-                # comm-CU budget): one comm lane cannot deadlock against another, so
-                # this shows what the 32-CU budget costs the all-reduce over the links.
-                try:
-                    d = run(".c5c", "dp", a.c5_model, a.c5_buckets, graph=use_graph, warmup=5, runs=a.c5_steps,
-                            compute=a.compute, wire_dtype=a.c5_wire, rccl_max_ctas=0)
-                    it = d["global"]["dlnb"]["iteration"]
-                    c5["rccl_default_ctas"] = {"ms_per_step": round(it["timed_ms_per_iter"], 4),
-                                               "median_ms": round(it["median_ms"], 4),
-                                               "exposed_comm_ms": _mean_of(d, "barrier_time"),
-                                               "allreduce_busbw_GBps": _busbw(d, "allreduce", world),
-                                               "allreduce_algbw_GBps": _algbw(d, "allreduce")}
-                except Exception as e:  # noqa: BLE001
-                    c5["rccl_default_ctas"] = {"error": str(e)[:300]}
-            if 0 < a.c5_bucket_ratio < 1 and "error" not in c5:
-                # opt-in policy: shrink the exposed tail (the last bucket's
-                # all-reduce runs after the backward ends)
-                try:
-                    d = run(".c5g", "dp", a.c5_model, a.c5_buckets, graph=use_graph, warmup=5, runs=a.c5_steps,
-                            compute=a.compute, wire_dtype=a.c5_wire, dp_bucket_ratio=a.c5_bucket_ratio)
-                    it = d["global"]["dlnb"]["iteration"]
-                    c5["geometric_buckets"] = {"bucket_ratio": a.c5_bucket_ratio,
-                                               "ms_per_step": round(it["timed_ms_per_iter"], 4),
-                                               "median_ms": round(it["median_ms"], 4),
-                                               "exposed_comm_ms": _mean_of(d, "barrier_time"),
-                                               "allreduce_busbw_GBps": _busbw(d, "allreduce", world)}
-                except Exception as e:  # noqa: BLE001
-                    c5["geometric_buckets"] = {"error": str(e)[:300]}
-            if a.stretch_steps > 0 and on_gpu:
-                try:
-                    d = run(".c5w", "dp", a.c5_model, a.c5_buckets, graph=use_graph, warmup=5, runs=a.c5_steps,
-                            compute="gemm-work", wire_dtype=a.c5_wire)
-                    it = d["global"]["dlnb"]["iteration"]
-                    c5["gemm_work"] = {"ms_per_step": round(it["timed_ms_per_iter"], 4),
-                                       "median_ms": round(it["median_ms"], 4),
-                                       "exposed_comm_ms": _mean_of(d, "barrier_time"),
-                                       "compute_stretch": d["global"]["dlnb"].get("compute_stretch")}
-                except Exception as e:  # noqa: BLE001
-                    c5["gemm_work"] = {"error": str(e)[:300]}
-            extra["comm_bound"] = c5
-            ph.add("comm_bound", t0)
-        if a.stretch_steps > 0 and on_gpu:
-            t0 = ph.now()
-            try:
-                d = run(".work", "fsdp", a.model, a.units, world, graph=use_graph, warmup=1, runs=a.stretch_steps,
-                        compute="gemm-work", **fsdp_kw)
-                extra["compute_stretch"] = d["global"]["dlnb"].get("compute_stretch")
-                extra["gemm_work_ms_per_step"] = round(d["global"]["dlnb"]["iteration"]["timed_ms_per_iter"], 3)
-            except Exception as e:  # noqa: BLE001
-                extra["compute_stretch_error"] = str(e)[:300]
-            ph.add("compute_stretch", t0)
     finally:
         sys.stdout.flush()
         os.dup2(saved, 1)
         os.close(saved)
-    # BASELINE C3 / C4 hybrids (8 GPUs), each a child process per rank.
-    if a.hybrids == "on" or (a.hybrids == "auto" and world == 8 and on_gpu):
-        c3 = tuple(int(x) for x in a.c3.split(","))
-        c4 = tuple(int(x) for x in a.c4.split(","))
-        t0 = ph.now()
-        extra["hybrid_3d"] = _hybrid_block(a, world, rank, ".c3", "hybrid_3d", a.c3_model, c3,
-                                           "GPipe (mb + S - 1)(f_mb + b_mb), BASELINE.md C3")
-        ph.add("hybrid_3d", t0)
-        t0 = ph.now()
-        extra["hybrid_3d_moe"] = _hybrid_block(a, world, rank, ".c4", "hybrid_3d_moe", a.c4_model, c4,
-                                               "GPipe (mb + S - 1)(f_mb + b_mb), BASELINE.md C4")
-        ph.add("hybrid_3d_moe", t0)
-        if a.c4_ep_overlap == "on":
+    head_ms = doc["global"]["dlnb"]["iteration"]["timed_ms_per_iter"] if doc else 3000.0
+    est = _Estimator(a, world, ph.s.get("headline", 30.0), a.warmup + a.steps, head_ms)
+    if doc is not None:
+        # Secondary measurements, in order of value, each a bounded child run
+        # of every rank: failures and overruns are reported, never fatal.
+        if a.c5_model != "none":
             t0 = ph.now()
-            # the MI355X-side schedule for the same config: the 1,024
-            # all-to-alls per iteration leave the compute stream
-            extra["hybrid_3d_moe"]["ep_overlap"] = _hybrid_block(
-                a, world, rank, ".c4o", "hybrid_3d_moe", a.c4_model, c4,
-                "GPipe (mb + S - 1)(f_mb + b_mb), BASELINE.md C4", ep_overlap=True)
-            ph.add("hybrid_3d_moe_ep_overlap", t0)
-    # Device timeline of the headline configuration (every rank's spans).
-    if a.timeline_block == "on" or (a.timeline_block == "auto" and world > 1 and on_gpu):
-        t0 = ph.now()
-        extra["timeline"] = _timeline_block(a, world, rank)
-        ph.add("timeline", t0)
-    # Collective bandwidth with nothing else running, RCCL and xgmi.
-    if a.link_bench == "on" or (a.link_bench == "auto" and world > 1 and on_gpu):
-        t0 = ph.now()
-        extra["link_bench"] = _link_block(a, world, rank, xgmi_exact_ok)
-        ph.add("link_bench", t0)
-    # xgmi A/B last, in child processes (see the module docstring); skipped
-    # when the exactness pass found the xgmi kernels wrong on these ranks.
-    xgmi_on = on_gpu and (a.xgmi_ab == "on" or (a.xgmi_ab == "auto" and world > 1))
-    skip = {"error": "skipped: the xgmi exactness check failed on these ranks (see exact_detail)"}
-    if a.c5_model != "none" and xgmi_on:
-        t0 = ph.now()
-        extra["comm_bound_xgmi"] = _xgmi_ab(a, world, rank, extra.get("comm_bound", {})) if xgmi_exact_ok else skip
-        ph.add("comm_bound_xgmi", t0)
-    if xgmi_on and a.xgmi_headline_steps > 0:
-        t0 = ph.now()
-        extra["headline_xgmi"] = _headline_xgmi(a, world, rank, doc) if xgmi_exact_ok else skip
-        ph.add("headline_xgmi", t0)
+            extra["comm_bound"] = _c5_blocks(a, world, rank, budget, est, use_graph, on_gpu)
+            ph.add("comm_bound", t0)
+        if a.stretch_steps > 0 and on_gpu:
+            t0 = ph.now()
+            nominal = est.setup + 5.0 + (1 + a.stretch_steps) * head_ms / 1e3
+            t = budget.plan("compute_stretch", est.want(nominal, 150), nominal)
+            if t is None:
+                extra["compute_stretch_error"] = _skipped(budget)["skipped"]
+            else:
+                try:
+                    d = _child_run(a, world, rank, ".work", "fsdp", a.model, (a.units, world), t, backend=a.backend,
+                                   graph=use_graph, compute="gemm-work", warmup=1, runs=a.stretch_steps, **fsdp_kw)
+                    if rank == 0:
+                        extra["compute_stretch"] = d["global"]["dlnb"].get("compute_stretch")
+                        extra["gemm_work_ms_per_step"] = round(d["global"]["dlnb"]["iteration"]["timed_ms_per_iter"],
+                                                               3)
+                except Exception as e:  # noqa: BLE001
+                    extra["compute_stretch_error"] = str(e)[:300]
+            ph.add("compute_stretch", t0)
+        # BASELINE C3 / C4 hybrids (8 GPUs), each a child process per rank.
+        if a.hybrids == "on" or (a.hybrids == "auto" and world == 8 and on_gpu):
+            c3 = tuple(int(x) for x in a.c3.split(","))
+            c4 = tuple(int(x) for x in a.c4.split(","))
+            note = "GPipe (mb + S - 1)(f_mb + b_mb), BASELINE.md "
+            t0 = ph.now()
+            extra["hybrid_3d"] = _hybrid_block(a, world, rank, ".c3", "hybrid_3d", a.c3_model, c3, note + "C3",
+                                               budget, est, a.c3_runs)
+            ph.add("hybrid_3d", t0)
+            t0 = ph.now()
+            extra["hybrid_3d_moe"] = _hybrid_block(a, world, rank, ".c4", "hybrid_3d_moe", a.c4_model, c4,
+                                                   note + "C4", budget, est, a.c4_runs)
+            ph.add("hybrid_3d_moe", t0)
+            if a.c4_ep_overlap == "on":
+                t0 = ph.now()
+                # the MI355X-side schedule for the same config: the 1,024
+                # all-to-alls per iteration leave the compute stream
+                extra["hybrid_3d_moe"]["ep_overlap"] = _hybrid_block(
+                    a, world, rank, ".c4o", "hybrid_3d_moe", a.c4_model, c4, note + "C4", budget, est, a.c4_runs,
+                    ep_overlap=True)
+                ph.add("hybrid_3d_moe_ep_overlap", t0)
+        # Collective bandwidth with nothing else running, RCCL and xgmi.
+        if a.link_bench == "on" or (a.link_bench == "auto" and world > 1 and on_gpu):
+            t0 = ph.now()
+            extra["link_bench"] = _link_block(a, world, rank, xgmi_exact_ok, budget, est)
+            ph.add("link_bench", t0)
+        # Device timeline of the headline configuration (every rank's spans).
+        if a.timeline_block == "on" or (a.timeline_block == "auto" and world > 1 and on_gpu):
+            t0 = ph.now()
+            extra["timeline"] = _timeline_block(a, world, rank, budget, est)
+            ph.add("timeline", t0)
+        # xgmi A/B last, in child processes (see the module docstring); skipped
+        # when the exactness pass found the xgmi kernels wrong on these ranks.
+        xgmi_on = on_gpu and (a.xgmi_ab == "on" or (a.xgmi_ab == "auto" and world > 1))
+        skip = {"error": "skipped: the xgmi exactness check failed on these ranks (see exact_detail)"}
+        if a.c5_model != "none" and xgmi_on:
+            t0 = ph.now()
+            extra["comm_bound_xgmi"] = (_xgmi_ab(a, world, rank, extra.get("comm_bound", {}), budget, est)
+                                        if xgmi_exact_ok else skip)
+            ph.add("comm_bound_xgmi", t0)
+        if xgmi_on and a.xgmi_headline_steps > 0:
+            t0 = ph.now()
+            extra["headline_xgmi"] = _headline_xgmi(a, world, rank, doc, budget, est) if xgmi_exact_ok else skip
+            ph.add("headline_xgmi", t0)
     if rank != 0:
         return 0
-    g = doc["global"]
-    it = g["dlnb"]["iteration"]
-    ms = it["timed_ms_per_iter"]
-    exposed = ms - it["compute_floor_ms"]
-    out = {
-        "metric": METRIC,
-        "value": round(ms, 3),
-        "unit": "ms",
-        "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": round(ms, 3),
-        "higher_is_better": False,
-        "scaling": "weak",
-        "vs_baseline": round(ms / BASELINE_MS, 4) if a.model == DEFAULT_MODEL and a.time_scale is None else None,
-        "dtype": "bf16",
-        "data": ("synthetic (random-init buffers; compute = MFMA GEMM stand-in bounded to the table durations)"
-                 if a.compute == "gemm" else f"synthetic (random-init buffers; compute mode {a.compute})"),
-        "config": {
-            "model": a.model,
-            "global_batch": int(g["local_batch_size"]) * world,
-            "seq_len": st.seq_len,
-            "parallelism": f"fsdp{world}",
-            "num_units": g["num_units"],
-            "sharding_factor": g["sharding_factor"],
-            "compute": a.compute,
-            "schedule": a.schedule,
-            "backend": g["backend"],
-            "hip_graph": bool(use_graph),
-        },
-        # null at N = 1: a 1-rank all-gather / reduce-scatter is a local copy
-        "effective_busbw_GBps": {k: _busbw(doc, k, world) for k in ("allgather", "reduce_scatter")},
-        "exposed_comm_ms": round(exposed, 3),
-        "median_ms": round(it["median_ms"], 3),
-        "baseline_ms": BASELINE_MS,
-        "baseline_note": "derived reference floor (BASELINE.md C2: fwd+bwd of llama3_8b_16_bfloat16); lower is better",
-        "rccl_cta_budget": g["dlnb"].get("rccl_cta_budget"),
-        # energy per step (J): hwmon / amd-smi power sampled every 5 ms on every GPU
-        # (the reference's energy_consumed, plots_pareto_energy.py); sum over GPUs and mean per GPU
-        "energy_J_per_step": _energy(doc),
-        "energy_source": g["dlnb"].get("energy_source"),
-        # ncclCommCount of every RCCL communicator of the headline run: proof
-        # that RCCL formed an N-rank group
-        "rccl_nranks": g["dlnb"].get("rccl_nranks"),
-        "runtime": g["dlnb"].get("runtime"),
-        # the xGMI cost model's iteration at this N (BASELINE.md "Link-model
-        # expectations"): the headline and the comm-bound block should land
-        # near these on an 8 x MI355X node (plus ~1-2 ms of fixed overhead)
-        "predicted_ms": _predicted_ms(a, world, "fsdp", a.model, (a.units, world)),
-    }
-    if "comm_bound" in extra and "error" not in extra["comm_bound"]:
-        extra["comm_bound"]["predicted_ms"] = _predicted_ms(a, world, "dp", a.c5_model, (a.c5_buckets,),
-                                                            wire=a.c5_wire)
+    out: Dict[str, Any] = {"metric": METRIC, "value": None, "unit": "ms", "n_gpus": world, "steps": a.steps,
+                           "warmup": a.warmup, "ms_per_step": None, "higher_is_better": False, "scaling": "weak",
+                           "vs_baseline": None, "dtype": "bf16"}
+    if doc is not None:
+        g = doc["global"]
+        it = g["dlnb"]["iteration"]
+        ms = it["timed_ms_per_iter"]
+        exposed = ms - it["compute_floor_ms"]
+        out.update({
+            "value": round(ms, 3),
+            "ms_per_step": round(ms, 3),
+            "vs_baseline": round(ms / BASELINE_MS, 4) if a.model == DEFAULT_MODEL and a.time_scale is None else None,
+            "data": ("synthetic (random-init buffers; compute = MFMA GEMM stand-in bounded to the table durations)"
+                     if a.compute == "gemm" else f"synthetic (random-init buffers; compute mode {a.compute})"),
+            "config": {
+                "model": a.model,
+                "global_batch": int(g["local_batch_size"]) * world,
+                "seq_len": st.seq_len,
+                "parallelism": f"fsdp{world}",
+                "num_units": g["num_units"],
+                "sharding_factor": g["sharding_factor"],
+                "compute": a.compute,
+                "schedule": a.schedule,
+                "backend": g["backend"],
+                "hip_graph": bool(use_graph),
+                "device_gates": g.get("device_gates"),
+            },
+            # null at N = 1: a 1-rank all-gather / reduce-scatter is a local copy
+            "effective_busbw_GBps": {k: _busbw(doc, k, world) for k in ("allgather", "reduce_scatter")},
+            "exposed_comm_ms": round(exposed, 3),
+            "median_ms": round(it["median_ms"], 3),
+            "per_run_ms": _per_run_ms(doc),
+            "baseline_ms": BASELINE_MS,
+            "baseline_note": "derived reference floor (BASELINE.md C2: fwd+bwd of llama3_8b_16_bfloat16); lower is better",
+            "rccl_cta_budget": g["dlnb"].get("rccl_cta_budget"),
+            # energy per step (J): hwmon / amd-smi power sampled every 5 ms on every GPU
+            # (the reference's energy_consumed, plots_pareto_energy.py); sum over GPUs and mean per GPU
+            "energy_J_per_step": _energy(doc),
+            "energy_source": g["dlnb"].get("energy_source"),
+            # ncclCommCount of every RCCL communicator of the headline run: proof
+            # that RCCL formed an N-rank group
+            "rccl_nranks": g["dlnb"].get("rccl_nranks"),
+            "runtime": g["dlnb"].get("runtime"),
+            # the xGMI cost model's iteration at this N (BASELINE.md "Link-model
+            # expectations"): the headline and the comm-bound block should land
+            # near these on an 8 x MI355X node (plus ~1-2 ms of fixed overhead)
+            "predicted_ms": _predicted_ms(a, world, "fsdp", a.model, (a.units, world)),
+        })
+    else:
+        out["error"] = "headline failed: " + (headline_error or "?")
+        out["data"] = "synthetic"
+        out["config"] = {"model": a.model, "parallelism": f"fsdp{world}", "compute": a.compute}
+    cb = extra.get("comm_bound")
+    if cb and "error" not in cb and "skipped" not in cb:
+        cb["predicted_ms"] = _predicted_ms(a, world, "dp", a.c5_model, (a.c5_buckets,), wire=a.c5_wire)
     if "link_bench" in extra:
         fit = _model_fit(a, world, extra)
         if fit:
             out["model_fit"] = fit
     out.update(exact)
+    # Every timed number is qualified by the exactness verdict of its backend
+    # (VERDICT r3 #4): "verified" per checked backend; a block timed on a
+    # backend whose collectives were not exact on these ranks keeps its
+    # numbers and carries "error".
+    if exact.get("exact"):
+        ver = {b: bool(exact["exact"].get(b)) for b in _exact_backends(a).split(",")}
+        out["verified"] = ver
+        for key, blk in [("headline", out), ("comm_bound", extra.get("comm_bound")),
+                         ("hybrid_3d", extra.get("hybrid_3d")), ("hybrid_3d_moe", extra.get("hybrid_3d_moe")),
+                         ("hybrid_3d_moe_ep_overlap", (extra.get("hybrid_3d_moe") or {}).get("ep_overlap"))]:
+            if not isinstance(blk, dict):
+                continue
+            b = _backend_key(blk.get("backend") if key != "headline" else (blk.get("config") or {}).get("backend"))
+            if b in ver and not ver[b] and "error" not in blk:
+                blk["error"] = f"{b} exactness failed (see exact_detail); timed anyway"
+    else:
+        out["verified"] = None  # no exactness pass (N = 1: collectives are local copies)
     out.update(extra)
+    out["budget"] = budget.report()
     # rank 0's wall seconds per phase (the headline's includes setup, warm-up and the timed steps)
     out["phase_seconds"] = ph.report()
     print(json.dumps(out), flush=True)

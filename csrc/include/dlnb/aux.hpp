@@ -12,10 +12,13 @@
 //     energy counter with DLNB_ENERGY=amdsmi;
 //   * Tracer emits roctx ranges (libroctx64, dlopen'd) around iterations
 //     and phases when --trace is given, visible with rocprofv3 --marker-trace;
-//   * FaultInjector (DLNB_INJECT_FAULT="rank=R,iter=I,mode=exit|hang|throw")
+//   * FaultInjector (DLNB_INJECT_FAULT="rank=R,iter=I,mode=exit|hang|throw[,block=TAG]";
+//     block: only in a run whose DLNB_BLOCK env is TAG)
 //     kills, hangs or fails one rank at one iteration to exercise the
 //     timeout / async-error detection and the launcher's teardown.
 #pragma once
+
+#include <functional>
 
 #include <atomic>
 #include <memory>
@@ -64,7 +67,8 @@ class FaultInjector {
   // Parses DLNB_INJECT_FAULT for this rank.
   explicit FaultInjector(int rank);
   // Called at the start of every iteration (warm-up and timed, counted from 0).
-  void at_iteration(long long iter);
+  // mode=task calls enqueue_failing_task (a stream task that throws).
+  void at_iteration(long long iter, const std::function<void()>& enqueue_failing_task = {});
   bool armed() const { return armed_; }
 
  private:

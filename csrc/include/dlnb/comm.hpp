@@ -121,6 +121,11 @@ AbortFlag loopback_cpu_abort_flag(LoopbackHub& hub);
 void loopback_drained(LoopbackHub& hub, bool wait, double timeout_s);
 std::unique_ptr<CommFactory> make_loopback_factory(HostGroup& world, Device& dev, std::shared_ptr<LoopbackHub> hub);
 
+// DLNB_COMM_FAULT set: wraps every communicator of `inner` in a fault
+// injector (comm_fault.cpp: swap parts of an op's output, or skip the op);
+// otherwise returns inner. Tests of the exactness checks only.
+std::unique_ptr<CommFactory> wrap_comm_faults(std::unique_ptr<CommFactory> inner, Device& dev, int world_rank);
+
 // Host-memory helpers of the CPU backends (multi-threaded for large sizes).
 // dst[i] = sum over srcs of src[i] (fp32 accumulation); dst may alias a src.
 void host_reduce_sum(DType t, void* dst, const std::vector<const char*>& srcs, size_t count);

@@ -53,6 +53,9 @@ bool starts_with(const std::string& s, const std::string& p);
 bool ends_with(const std::string& s, const std::string& p);
 std::string env_or(const char* name, const std::string& dflt);
 long long env_int(const char* name, long long dflt);
+// True in the CLI binaries (main_for), false when a host process (Python)
+// runs the library: only a CLI process may end itself on a fatal error.
+bool cli_process();
 
 // Host-side bf16 / fp8 <-> float conversions (CPU backend reductions, tests).
 float bf16_to_float(uint16_t v);

@@ -74,6 +74,29 @@ class ComputeEngine {
   // Other modes: run().
   virtual void run_chained(Stream& s, double us, double flops) { run(s, us, flops); }
   virtual uint64_t task_ticks(double us) const { (void)us; return 0; }
+  // Device-side dependency times (gemm mode; csrc/kernels/deadline_sync.hpp).
+  // A gate is a device word: signal(s, g) enqueues on s (a collective's
+  // stream, after the collective, before the event the compute stream waits
+  // on) a one-wave kernel that raises it with a fresh tag and the time.
+  // run_gated() enqueues a task whose first block reads its gates (at most
+  // 2, signalled before in host order; the caller also waits on their
+  // events, so they are already raised) and, with chain = true, starts at
+  // max(the stream's previous deadline, the gates' times): the queue hop and
+  // launch gap after a stream wait are absorbed, a late collective is not.
+  // *start gets the task's effective start (stall timers: the gap to the
+  // previous deadline is the exposed wait). gates_task(us): whether a task
+  // of us microseconds can use this (else run_stamped).
+  virtual bool gates_task(double us) const { (void)us; return false; }
+  virtual int make_gate() { DLNB_THROW("this compute mode has no device gates"); }
+  virtual void signal(Stream& s, int gate) { (void)s; (void)gate; DLNB_THROW("this compute mode has no device gates"); }
+  virtual void run_gated(Stream& s, double us, double flops, const std::vector<int>& gates, uint64_t* start,
+                         bool chain) {
+    (void)s; (void)us; (void)flops; (void)gates; (void)start; (void)chain;
+    DLNB_THROW("this compute mode has no device gates");
+  }
+  // A second host-mapped slot the next deadline task's kernel writes its
+  // start into (the --timeline decorator's span start).
+  virtual void set_next_start_slot(uint64_t* slot) { (void)slot; }
   // Graph mode: enqueue on s a reset of whatever per-task device state the
   // engine keys by epoch (a replayed graph repeats the captured epochs).
   virtual void reset_clocks(Stream& s) { (void)s; }

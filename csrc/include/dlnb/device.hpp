@@ -119,9 +119,12 @@ class Device {
   virtual size_t free_memory() const = 0;
   // Capture everything `enqueue` puts on `origin` and `others` into one graph:
   // the other streams are forked from origin before and joined back after,
-  // so the graph is launched on origin alone. GPU only.
+  // so the graph is launched on origin alone. `head` (optional) is enqueued
+  // on origin before the fork, so everything of every stream comes after it
+  // (the compute engine's slot / gate reset). GPU only.
   virtual std::unique_ptr<GraphExec> capture(Stream& origin, const std::vector<Stream*>& others,
-                                             const std::function<void()>& enqueue);
+                                             const std::function<void()>& enqueue,
+                                             const std::function<void()>& head = {});
 
   Buffer alloc(size_t bytes) { return Buffer(this, bytes); }
   Buffer alloc_peer(size_t bytes) { return Buffer(this, bytes, true); }

@@ -27,6 +27,20 @@ namespace kernels {
 
 void fill_random(void* p, size_t count, DType t, uint64_t seed, void* stream);
 
+// How a deadline task's start is decided (csrc/kernels/deadline_sync.hpp):
+// wait for up to two gates (device words a collective's stream raises with
+// gate_signal), continue the stream's previous task (chain), and write the
+// start to up to two host-mapped stamp slots.
+struct DlSync {
+  uint64_t* tstart[2] = {nullptr, nullptr};
+  const uint64_t* gate[2] = {nullptr, nullptr};
+  uint32_t tag[2] = {0, 0};
+  uint32_t chain = 0;
+};
+// One wave stores {tag:16 | s_memrealtime:48} into *gate (device memory,
+// agent scope) when the stream reaches this point. tag != 0.
+void gate_signal(uint64_t* gate, uint32_t tag, void* stream);
+
 // Deadline kernels; ticks of the 100 MHz s_memrealtime clock (see
 // wallclock_hz()).
 void idle_wait(uint64_t ticks, void* stream);
@@ -73,28 +87,29 @@ void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int 
                        void* stream);
 void gemm_tn_4wave_fp8_deadline(const void* A, const void* B, void* C, int M, int N, int K, uint64_t ticks,
                                 uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
-                                uint64_t* tstart);
+                                const DlSync& sync);
 void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, DType in_t,
                     void* stream);
 void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
                              uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
-                             uint64_t* tstart);
+                             const DlSync& sync);
 
 // Persistent deadline variant (the default stand-in compute): a grid of
 // `grid` blocks (<= one per CU: 128 KiB LDS each) walks the M x N tile space
 // of C = A.B^T round-robin and stops min(ticks, slice_end) (100 MHz
-// s_memrealtime) after t0. t0 is agreed through *slot: the first block of the
-// first launch of `epoch` (1..65535, different from the slot's previous task)
-// CASes {epoch:16 | t0:48} into it; every other block and every later launch
-// with the same epoch reads it. A task is one launch by default; with
-// DLNB_GEMM_SLICE_US it is issued as several launches (slices) with
+// s_memrealtime) after t0. t0 is agreed through *slot (a 64-byte line per
+// stream): the first block of the first launch of `epoch` (1..65535,
+// different from the slot's previous task) claims the task, waits for its
+// gates and decides t0 (sync: deadline_sync.hpp); every other block and every
+// later launch with the same epoch reads it. A task is one launch by default;
+// with DLNB_GEMM_SLICE_US it is issued as several launches (slices) with
 // increasing slice_end (compute.cpp; profiles/slice_ab_r3.md).
 // Leading dimensions are K, K and N.
-// tstart (optional, host-mapped): the block that claims the epoch stores the
-// task's start (s_memrealtime) there - stall timing without extra kernels.
+// sync.tstart (optional, host-mapped): the claiming block stores the task's
+// start (s_memrealtime) there - stall timing without extra kernels.
 void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
                       uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end = 0,
-                      uint64_t* tstart = nullptr);
+                      const DlSync& sync = DlSync());
 
 // Elementwise "optimizer" stand-in (SGD-momentum on bf16 shards, fp32 math):
 // p = p - lr * (m = beta*m + g). Used by the optional --optimizer step.

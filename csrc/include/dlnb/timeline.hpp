@@ -42,6 +42,9 @@ class Timeline {
   // A span of work on stream s: begin() before the work is enqueued, end()
   // after (same stream). Returns / takes -1 when the slots ran out.
   int begin(Stream& s);
+  // The same, but the span's start is written by the work itself (a deadline
+  // kernel's start, ComputeEngine::set_next_start_slot) into *slot.
+  int begin_external(uint64_t** slot);
   void end(int token, Stream& s, const char* cat, const std::string& name, Json args = Json::object());
   // Track name of a stream (the first name given wins).
   void label(Stream& s, const std::string& name);

@@ -1,0 +1,115 @@
+// Start-time agreement of the persistent deadline GEMMs (every deadline
+// kernel: kernels.hip, gemm_8phase.hip, gemm_4wave_fp8.hip).
+//
+// A deadline task's blocks must all stop `ticks` after ONE start time t0.
+// Thread 0 of every block calls agree_t0(); the slot is one 64-byte line per
+// compute stream (ComputeEngine, compute.cpp):
+//   word 0: {epoch:16 | t0:48}  the published start of the current task
+//   word 1: t0 + ticks (48 bit)  the deadline of the stream's last task
+//   word 2: epoch of the last task whose start was claimed
+//   word 3: 1 once a gate wait timed out (never expected)
+// The first block of a task (epoch = task number on the stream, never 0)
+// claims word 2 with a CAS and decides t0; every other block of the task and
+// every later launch of the same task (DLNB_GEMM_SLICE_US slices) waits for
+// word 0 to carry the epoch and reads t0 back.
+//
+// How the claiming block decides t0 (DlSync, dlnb/kernels.hpp):
+//   * gates: device words {tag:16 | time:48} that a one-wave kernel on a
+//     collective's stream raises when the collective is done
+//     (kernels::gate_signal). The block spins until each gate carries its
+//     tag and takes the latest time. The strategies also order the task
+//     after the collective with a stream wait, so the gates are raised by
+//     then: the gate dates the dependency, the graph edge orders it (a
+//     kernel spinning on a word raised by a node queued behind it on the
+//     same hardware queue would never finish);
+//   * chain: the task continues the stream's previous task, so it starts at
+//     max(previous deadline, the latest gate) - a late launch (queue hop,
+//     the previous grid's drain) is absorbed, a late collective is not (the
+//     start moves to the time its gate was raised, and that wait is what the
+//     strategy's timers report as exposed communication);
+//   * otherwise t0 = the time the gates opened (now, with no gates).
+// t0 (as a full 64-bit s_memrealtime value) goes to up to two host-mapped
+// stamp slots (the strategy's stall timer, the --timeline span).
+// Every access is a relaxed agent-scope atomic (coherent across the XCDs'
+// L2s): the stand-in GEMM reads its own operands, never a collective's
+// output, so the gates order time, not data.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "dlnb/kernels.hpp"
+
+namespace dlnb {
+namespace kernels {
+namespace dl {
+
+constexpr uint64_t kMask48 = (1ull << 48) - 1;
+constexpr uint64_t kGateTimeoutTicks = 60ull * 100000000ull;  // 60 s at 100 MHz
+
+// a at or after b on the 48-bit clock (wraps every 32 days at 100 MHz)
+__device__ __forceinline__ bool not_before(uint64_t a, uint64_t b) { return ((a - b) & kMask48) < (1ull << 47); }
+
+__device__ __forceinline__ uint64_t ld(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint64_t agree_t0(uint64_t* slot, uint32_t epoch, uint64_t ticks, const DlSync& s) {
+  uint64_t* claim = slot + 2;
+  uint64_t c = ld(claim);
+  bool won = false;
+  while (c != epoch) {
+    if (__hip_atomic_compare_exchange_strong(claim, &c, static_cast<uint64_t>(epoch), __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      won = true;
+      break;
+    }
+  }
+  if (!won) {
+    uint64_t cur;
+    while (((cur = ld(slot)) >> 48) != epoch)
+      __builtin_amdgcn_s_sleep(1);
+    return cur & kMask48;
+  }
+  uint64_t gate_t = 0;
+  bool gated = false;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    if (!s.gate[i]) continue;
+    uint64_t v;
+    const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+    while (((v = ld(s.gate[i])) >> 48) != s.tag[i]) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - w0 > kGateTimeoutTicks) {
+        // never raised (a bug): give up rather than hold the CUs forever,
+        // and leave the mark in word 3 of the slot for the host to find
+        __hip_atomic_store(slot + 3, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        v = __builtin_amdgcn_s_memrealtime() & kMask48;
+        break;
+      }
+    }
+    const uint64_t t = v & kMask48;
+    gate_t = gated && not_before(gate_t, t) ? gate_t : t;
+    gated = true;
+  }
+  const uint64_t raw = __builtin_amdgcn_s_memrealtime();
+  const uint64_t now = raw & kMask48;
+  uint64_t t0 = now;  // unchained: when the gates opened
+  const uint64_t prev = s.chain ? ld(slot + 1) & kMask48 : 0;
+  if (prev != 0) {  // 0: nothing to continue (the slot was reset)
+    t0 = gated && not_before(gate_t, prev) ? gate_t : prev;
+    if (!not_before(now, t0)) t0 = now;  // never in the future
+  }
+  __hip_atomic_store(slot + 1, (t0 + ticks) & kMask48, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(slot, (static_cast<uint64_t>(epoch) << 48) | t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t full = raw - ((now - t0) & kMask48);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    if (s.tstart[i]) __hip_atomic_store(s.tstart[i], full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return t0;
+}
+
+}  // namespace dl
+}  // namespace kernels
+}  // namespace dlnb

@@ -49,6 +49,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "deadline_sync.hpp"
 #include "dlnb/kernels.hpp"
 #include "store_pair.hpp"
 
@@ -346,25 +347,6 @@ __device__ __forceinline__ void tile_coords(int bid, int nt_m, int nt_n, int gro
   tn = (bid % per_group) / gsz;
 }
 
-// The deadline's t0, agreed per task epoch: the first block to arrive
-// publishes its start {epoch:16 | t0:48} in *slot (and stamps *tstart); every
-// other block of that epoch reads it back.
-__device__ __forceinline__ uint64_t agree_t0(uint64_t* slot, uint32_t epoch, uint64_t* tstart) {
-  constexpr uint64_t kMask48 = (1ull << 48) - 1;
-  const uint64_t raw = __builtin_amdgcn_s_memrealtime();
-  const uint64_t mine = (static_cast<uint64_t>(epoch) << 48) | (raw & kMask48);
-  uint64_t cur = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  while ((cur >> 48) != epoch) {
-    if (__hip_atomic_compare_exchange_strong(slot, &cur, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT)) {
-      cur = mine;
-      if (tstart) __hip_atomic_store(tstart, raw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      break;
-    }
-  }
-  return cur & kMask48;
-}
-
 // DL = false: one launch, grid = tiles. DL = true: persistent stand-in
 // compute with gemm_tn_deadline's contract (kernels.hip): grid <= resident
 // blocks walks the tiles round-robin and stops min(ticks, slice_end) after t0,
@@ -373,7 +355,7 @@ template <bool DL>
 __global__ void __launch_bounds__(256, 1)
     gemm_4wave_fp8_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
                           int K, int lda, int ldb, int ldc, int group, uint64_t* __restrict__ slot, uint32_t epoch,
-                          uint64_t ticks, uint64_t slice_end, uint64_t* __restrict__ tstart) {
+                          uint64_t ticks, uint64_t slice_end, DlSync sync) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + 16];  // ONE array: staging + deadline flags
   const int tid = threadIdx.x;
   CtxF c;
@@ -395,7 +377,7 @@ __global__ void __launch_bounds__(256, 1)
     tile_coords(xcd_remap(blockIdx.x, T), nt_m, nt_n, group, tm, tn);
     tile4<false>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d);
   } else {
-    if (tid == 0) d.t0 = agree_t0(slot, epoch, tstart);  // only thread 0 reads the clock
+    if (tid == 0) d.t0 = dl::agree_t0(slot, epoch, ticks, sync);  // only thread 0 reads the clock
     for (int round = 0;; ++round) {
       tile_coords(xcd_remap((blockIdx.x + round * gridDim.x) % T, T), nt_m, nt_n, group, tm, tn);
       if (!tile4<true>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d)) return;
@@ -422,7 +404,7 @@ template <bool DL>
 __global__ void __launch_bounds__(256, 1)
     gemm_4wave_fp8_stream_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C,
                                  int M, int N, int K, int lda, int ldb, int ldc, int group, uint64_t* __restrict__ slot,
-                                 uint32_t epoch, uint64_t ticks, uint64_t slice_end, uint64_t* __restrict__ tstart) {
+                                 uint32_t epoch, uint64_t ticks, uint64_t slice_end, DlSync sync) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + 16];  // ONE array: staging + deadline flags
   const int tid = threadIdx.x;
   CtxF c;
@@ -443,7 +425,7 @@ __global__ void __launch_bounds__(256, 1)
   const int G = gridDim.x;
   DeadlineF d{0, ticks, slice_end, (lds_flag_t*)(smem + 2 * kBuf), tid};
   if constexpr (DL) {
-    if (tid == 0) d.t0 = agree_t0(slot, epoch, tstart);  // only thread 0 reads the clock
+    if (tid == 0) d.t0 = dl::agree_t0(slot, epoch, ticks, sync);  // only thread 0 reads the clock
   }
   // one-shot: grid <= T (host), the stream ends after the block's last tile;
   // DL: tile indices wrap, the stream never ends before the deadline
@@ -800,28 +782,28 @@ void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int 
   if (tiles > cus) {
     hipLaunchKernelGGL(gemm_4wave_fp8_stream_kernel<false>, cus, 256, 0, static_cast<hipStream_t>(stream),
                        static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K,
-                       lda, ldb, ldc, group, nullptr, 0u, 0ull, 0ull, nullptr);
+                       lda, ldb, ldc, group, nullptr, 0u, 0ull, 0ull, DlSync());
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) DLNB_THROW("gemm 4-wave fp8 stream launch failed: " << hipGetErrorString(e));
     return;
   }
   hipLaunchKernelGGL(gemm_4wave_fp8_kernel<false>, tiles, 256, 0, static_cast<hipStream_t>(stream),
                      static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda,
-                     ldb, ldc, group, nullptr, 0u, 0ull, 0ull, nullptr);
+                     ldb, ldc, group, nullptr, 0u, 0ull, 0ull, DlSync());
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 4-wave fp8 launch failed: " << hipGetErrorString(e));
 }
 
 void gemm_tn_4wave_fp8_deadline(const void* A, const void* B, void* C, int M, int N, int K, uint64_t ticks,
                                 uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
-                                uint64_t* tstart) {
+                                const DlSync& sync) {
   DLNB_REQUIRE(gemm_4wave_fp8_shape_ok(M, N, K, DType::FP8_E4M3), "gemm 4-wave fp8 deadline: unsupported shape");
   // The per-tile kernel. (Its streaming twin ran +5 % MFMA per clock at a 5 %
   // lower, power-capped clock on the 224 CUs - the same 2620-2630 TF/s - so
   // it was not kept as a deadline kernel: profiles/gemm_deadline_stream_r2.md.)
   hipLaunchKernelGGL(gemm_4wave_fp8_kernel<true>, grid, 256, 0, static_cast<hipStream_t>(stream),
                      static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, K, K,
-                     N, 8, slot, epoch, ticks, slice_end, tstart);
+                     N, 8, slot, epoch, ticks, slice_end, sync);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 4-wave fp8 deadline launch failed: " << hipGetErrorString(e));
 }

@@ -24,6 +24,7 @@
 // Variant 3 of dlnb::kernels::gemm_tn (the library's one-shot GEMM).
 #include <hip/hip_runtime.h>
 
+#include "deadline_sync.hpp"
 #include "dlnb/kernels.hpp"
 #include "store_pair.hpp"
 
@@ -375,7 +376,7 @@ template <bool FP8, bool DL, bool BAL = false, bool UNI = false>
 __global__ void __launch_bounds__(512, 1)
     gemm_8phase_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
                        int K, int lda, int ldb, int ldc, uint64_t* __restrict__ slot, uint32_t epoch, uint64_t ticks,
-                       uint64_t slice_end, uint64_t* __restrict__ tstart, int group = 8) {
+                       uint64_t slice_end, DlSync sync, int group = 8) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + 16];  // ONE array: staging + deadline flags
   const int tid = threadIdx.x;
   Ctx c;
@@ -396,21 +397,7 @@ __global__ void __launch_bounds__(512, 1)
   if constexpr (!DL) {
     tile<FP8, false, BAL, UNI>(c, A, B, C, M, N, K, ldc, xcd_remap(blockIdx.x, T), d, group);
   } else {
-    constexpr uint64_t kMask48 = (1ull << 48) - 1;
-    if (tid == 0) {
-      const uint64_t raw = __builtin_amdgcn_s_memrealtime();
-      const uint64_t mine = (static_cast<uint64_t>(epoch) << 48) | (raw & kMask48);
-      uint64_t cur = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      while ((cur >> 48) != epoch) {
-        if (__hip_atomic_compare_exchange_strong(slot, &cur, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT)) {
-          cur = mine;
-          if (tstart) __hip_atomic_store(tstart, raw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-      }
-      d.t0 = cur & kMask48;  // only thread 0 reads the clock
-    }
+    if (tid == 0) d.t0 = dl::agree_t0(slot, epoch, ticks, sync);  // only thread 0 reads the clock
     for (int round = 0;; ++round)
       if (!tile<FP8, true, BAL, UNI>(c, A, B, C, M, N, K, ldc, xcd_remap((blockIdx.x + round * gridDim.x) % T, T), d))
         return;
@@ -549,7 +536,7 @@ template <bool FP8>
 __global__ void __launch_bounds__(512, 1)
     gemm_8phase_stream_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M,
                               int N, int K, int lda, int ldb, int ldc, uint64_t* __restrict__ slot, uint32_t epoch,
-                              uint64_t ticks, uint64_t slice_end, uint64_t* __restrict__ tstart) {
+                              uint64_t ticks, uint64_t slice_end, DlSync sync) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + 16];  // ONE array: staging + deadline flags
   const int tid = threadIdx.x;
   Ctx c;
@@ -566,23 +553,7 @@ __global__ void __launch_bounds__(512, 1)
   c.voffA = lane_offset(c.lda, c.w, c.lane);
   c.voffB = lane_offset(c.ldb, c.w, c.lane);
   Deadline d{0, ticks, slice_end, (lds_flag_t*)(smem + 2 * kBuf), tid};
-  {
-    constexpr uint64_t kMask48 = (1ull << 48) - 1;
-    if (tid == 0) {
-      const uint64_t raw = __builtin_amdgcn_s_memrealtime();
-      const uint64_t mine = (static_cast<uint64_t>(epoch) << 48) | (raw & kMask48);
-      uint64_t cur = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      while ((cur >> 48) != epoch) {
-        if (__hip_atomic_compare_exchange_strong(slot, &cur, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT)) {
-          cur = mine;
-          if (tstart) __hip_atomic_store(tstart, raw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-      }
-      d.t0 = cur & kMask48;
-    }
-  }
+  if (tid == 0) d.t0 = dl::agree_t0(slot, epoch, ticks, sync);
   StreamCtx sc;
   sc.A = A;
   sc.B = B;
@@ -667,14 +638,14 @@ void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, 
     // fp8: one uniform K-tile body with plain reads (the balanced fp8 build
     // spills under the buffer_load staging, profiles/gemm_bench_r2.md)
     hipLaunchKernelGGL((gemm_8phase_kernel<true, false, false, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb,
-                       ldc, nullptr, 0u, 0ull, 0ull, nullptr, group);
+                       ldc, nullptr, 0u, 0ull, 0ull, DlSync(), group);
   } else if (even) {
     // bf16: balanced fragment reads (unrolled by two K-tiles: even counts)
     hipLaunchKernelGGL((gemm_8phase_kernel<false, false, true>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc,
-                       nullptr, 0u, 0ull, 0ull, nullptr, group);
+                       nullptr, 0u, 0ull, 0ull, DlSync(), group);
   } else {
     hipLaunchKernelGGL((gemm_8phase_kernel<false, false>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc, nullptr,
-                       0u, 0ull, 0ull, nullptr);
+                       0u, 0ull, 0ull, DlSync());
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 8-phase launch failed: " << hipGetErrorString(e));
@@ -682,7 +653,7 @@ void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, 
 
 void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
                              uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
-                             uint64_t* tstart) {
+                             const DlSync& sync) {
   DLNB_REQUIRE(gemm_8phase_shape_ok(M, N, K, in_t), "gemm 8-phase deadline: unsupported shape");
   hipStream_t st = static_cast<hipStream_t>(stream);
   auto* a = static_cast<const char*>(A);
@@ -702,16 +673,16 @@ void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N
   const int nk = static_cast<int>(static_cast<size_t>(K) * dtype_size(in_t) / kRB);
   if (in_t == DType::BF16 && nk <= 16) {
     hipLaunchKernelGGL((gemm_8phase_stream_kernel<false>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
-                       ticks, slice_end, tstart);
+                       ticks, slice_end, sync);
   } else if (in_t == DType::BF16 && nk % 2 == 0) {
     hipLaunchKernelGGL((gemm_8phase_kernel<false, true, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot,
-                       epoch, ticks, slice_end, tstart);
+                       epoch, ticks, slice_end, sync);
   } else if (in_t == DType::BF16) {
     hipLaunchKernelGGL((gemm_8phase_kernel<false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
-                       ticks, slice_end, tstart);
+                       ticks, slice_end, sync);
   } else {
     hipLaunchKernelGGL((gemm_8phase_kernel<true, true, false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot,
-                       epoch, ticks, slice_end, tstart);
+                       epoch, ticks, slice_end, sync);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 8-phase deadline launch failed: " << hipGetErrorString(e));

@@ -4,6 +4,7 @@
 
 #include <cstdio>
 
+#include "deadline_sync.hpp"
 #include "dlnb/kernels.hpp"
 
 #define DLNB_HIP_CHECK(expr)                                                       \
@@ -108,6 +109,13 @@ __global__ void stamp_kernel(uint64_t* slot) {
   if (threadIdx.x == 0) {
     const uint64_t t = __builtin_amdgcn_s_memrealtime();
     __hip_atomic_store(slot, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__global__ void gate_signal_kernel(uint64_t* gate, uint32_t tag) {
+  if (threadIdx.x == 0) {
+    const uint64_t t = __builtin_amdgcn_s_memrealtime() & dl::kMask48;
+    __hip_atomic_store(gate, (static_cast<uint64_t>(tag) << 48) | t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -322,7 +330,7 @@ template <bool FP8, bool DEADLINE, int WN, bool SWP = false>
 __global__ void __launch_bounds__(128 * WN, WN == 4 ? 2 : 1)
     gemm_tn_256_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
                        int K, int lda, int ldb, int ldc, uint64_t* __restrict__ slot, uint32_t epoch,
-                       uint64_t ticks, uint64_t slice_end, uint64_t* __restrict__ tstart) {
+                       uint64_t ticks, uint64_t slice_end, DlSync sync) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kStageBytes + 16];
   volatile int* stop_flag = reinterpret_cast<volatile int*>(smem + 2 * kStageBytes);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -331,25 +339,10 @@ __global__ void __launch_bounds__(128 * WN, WN == 4 ? 2 : 1)
   constexpr int WTN = kTile / WN;      // wave tile width (N)
   const int wm = w / WN, wn = w % WN;
   const int nt_m = M / kTile, nt_n = N / kTile, T = nt_m * nt_n;
-  constexpr uint64_t kMask48 = (1ull << 48) - 1;
+  constexpr uint64_t kMask48 = dl::kMask48;
   uint64_t t0 = 0;
   if constexpr (DEADLINE) {
-    if (tid == 0) {
-      const uint64_t raw = __builtin_amdgcn_s_memrealtime();
-      const uint64_t now = raw & kMask48;
-      const uint64_t mine = (static_cast<uint64_t>(epoch) << 48) | now;
-      uint64_t cur = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      while ((cur >> 48) != epoch) {
-        if (__hip_atomic_compare_exchange_strong(slot, &cur, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT)) {
-          cur = mine;
-          // the task's start, for stamp-free stall timing (host-mapped)
-          if (tstart) __hip_atomic_store(tstart, raw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-      }
-      t0 = cur & kMask48;
-    }
+    if (tid == 0) t0 = dl::agree_t0(slot, epoch, ticks, sync);
   }
   for (int round = 0;; ++round) {
   const int b = xcd_remap(DEADLINE ? (blockIdx.x + round * gridDim.x) % T : blockIdx.x, T);
@@ -469,6 +462,12 @@ void idle_wait(uint64_t ticks, void* stream) {
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
+void gate_signal(uint64_t* gate, uint32_t tag, void* stream) {
+  DLNB_REQUIRE(gate != nullptr && tag > 0 && tag < 65536, "gate_signal: bad gate/tag");
+  hipLaunchKernelGGL(gate_signal_kernel, 1, 64, 0, S(stream), gate, tag);
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
 void stamp(uint64_t* slot, void* stream) {
   hipLaunchKernelGGL(stamp_kernel, 1, 64, 0, S(stream), slot);
   DLNB_HIP_CHECK(hipGetLastError());
@@ -502,10 +501,10 @@ namespace {
 template <bool FP8, bool DEADLINE, int WN, bool SWP = false>
 void launch_gemm(int grid, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                  uint64_t* slot, uint32_t epoch, uint64_t ticks, uint64_t slice_end, hipStream_t st,
-                 uint64_t* tstart = nullptr) {
+                 const DlSync& sync = DlSync()) {
   hipLaunchKernelGGL((gemm_tn_256_kernel<FP8, DEADLINE, WN, SWP>), grid, 128 * WN, 0, st, static_cast<const char*>(A),
                      static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda, ldb, ldc, slot, epoch, ticks,
-                     slice_end, tstart);
+                     slice_end, sync);
 }
 
 // The 8-wave double-buffered kernel (variant 8): bf16 with software-pipelined
@@ -514,14 +513,14 @@ void launch_gemm(int grid, const void* A, const void* B, void* C, int M, int N, 
 template <bool DEADLINE>
 void dispatch_gemm(DType in_t, int grid, const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
                    int ldc, uint64_t* slot, uint32_t epoch, uint64_t ticks, uint64_t slice_end, hipStream_t st,
-                   uint64_t* tstart = nullptr) {
+                   const DlSync& sync = DlSync()) {
   const bool fp8 = in_t == DType::FP8_E4M3;
   if (!DEADLINE && !fp8)
     launch_gemm<false, false, 4, true>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st);
   else if (fp8)
-    launch_gemm<true, DEADLINE, 4>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st, tstart);
+    launch_gemm<true, DEADLINE, 4>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st, sync);
   else
-    launch_gemm<false, DEADLINE, 4>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st, tstart);
+    launch_gemm<false, DEADLINE, 4>(grid, A, B, C, M, N, K, lda, ldb, ldc, slot, epoch, ticks, slice_end, st, sync);
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
@@ -560,21 +559,21 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
 }
 
 void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
-                      uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end, uint64_t* tstart) {
+                      uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end, const DlSync& sync) {
   if (slice_end == 0) slice_end = ticks;
   DLNB_REQUIRE(gemm_shape_ok(M, N, K, in_t), "gemm_tn_deadline: unsupported shape");
   DLNB_REQUIRE(slot != nullptr && grid > 0 && epoch > 0 && epoch < 65536, "gemm_tn_deadline: bad slot/grid/epoch");
   // fp8: the one-wave-per-SIMD MX kernel where it applies (2665 vs ~2180 TF/s sustained)
   if (gemm_4wave_fp8_shape_ok(M, N, K, in_t)) {
-    gemm_tn_4wave_fp8_deadline(A, B, C, M, N, K, ticks, slot, epoch, grid, stream, slice_end, tstart);
+    gemm_tn_4wave_fp8_deadline(A, B, C, M, N, K, ticks, slot, epoch, grid, stream, slice_end, sync);
     return;
   }
   if (gemm_8phase_shape_ok(M, N, K, in_t)) {
-    gemm_tn_8phase_deadline(A, B, C, M, N, K, in_t, ticks, slot, epoch, grid, stream, slice_end, tstart);
+    gemm_tn_8phase_deadline(A, B, C, M, N, K, in_t, ticks, slot, epoch, grid, stream, slice_end, sync);
     return;
   }
   // 8 waves (a single K-tile)
-  dispatch_gemm<true>(in_t, grid, A, B, C, M, N, K, K, K, N, slot, epoch, ticks, slice_end, S(stream), tstart);
+  dispatch_gemm<true>(in_t, grid, A, B, C, M, N, K, K, K, N, slot, epoch, ticks, slice_end, S(stream), sync);
 }
 
 void sgd_momentum_bf16(void* param, void* mom, const void* grad, size_t n, float lr, float beta, void* stream) {

@@ -230,14 +230,18 @@ FaultInjector::FaultInjector(int rank) {
   if (spec.empty()) return;
   int r = -1;
   long long it = 0;
-  std::string mode = "exit";
+  std::string mode = "exit", block;
   for (auto& kv : split(spec, ',')) {
     auto p = split(kv, '=');
     if (p.size() != 2) continue;
     if (p[0] == "rank") r = std::stoi(p[1]);
     if (p[0] == "iter") it = std::stoll(p[1]);
     if (p[0] == "mode") mode = p[1];
+    if (p[0] == "block") block = p[1];
   }
+  // block=TAG: only in the run whose DLNB_BLOCK is TAG (bench.py names each
+  // of its child runs, so one phase of the bench can be made to hang)
+  if (!block.empty() && env_or("DLNB_BLOCK", "") != block) return;
   if (r == rank) {
     armed_ = true;
     iter_ = it;
@@ -245,10 +249,14 @@ FaultInjector::FaultInjector(int rank) {
   }
 }
 
-void FaultInjector::at_iteration(long long iter) {
+void FaultInjector::at_iteration(long long iter, const std::function<void()>& enqueue_failing_task) {
   if (!armed_ || iter != iter_) return;
   std::fprintf(stderr, "[dlnb] DLNB_INJECT_FAULT: injecting '%s' at iteration %lld\n", mode_.c_str(), iter);
   std::fflush(stderr);
+  if (mode_ == "task" && enqueue_failing_task) {
+    enqueue_failing_task();
+    return;
+  }
   if (mode_ == "exit") std::_Exit(42);
   if (mode_ == "throw") DLNB_THROW("injected fault at iteration " << iter);
   if (mode_ == "hang")

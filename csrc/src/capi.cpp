@@ -94,6 +94,31 @@ int dlnb_gemm_deadline_us(const void* A, const void* B, void* C, int M, int N, i
   });
 }
 
+// The deadline GEMM with the full start protocol (csrc/kernels/deadline_sync.hpp):
+// explicit epoch, chain flag, up to two gates with their tags, a start stamp.
+int dlnb_gemm_deadline_ex(const void* A, const void* B, void* C, int M, int N, int K, int dtype, double us, int device,
+                          void* slot, int grid, void* stream, unsigned epoch, int chain, void* gate0, unsigned tag0,
+                          void* gate1, unsigned tag1, void* tstart) {
+  return guard([&] {
+    double hz = dlnb::kernels::wallclock_hz(device);
+    if (grid <= 0) grid = dlnb::kernels::num_cus(device);
+    dlnb::kernels::DlSync sync;
+    sync.chain = chain ? 1u : 0u;
+    sync.gate[0] = static_cast<const uint64_t*>(gate0);
+    sync.gate[1] = static_cast<const uint64_t*>(gate1);
+    sync.tag[0] = tag0;
+    sync.tag[1] = tag1;
+    sync.tstart[0] = static_cast<uint64_t*>(tstart);
+    dlnb::kernels::gemm_tn_deadline(A, B, C, M, N, K, static_cast<dlnb::DType>(dtype),
+                                    static_cast<unsigned long long>(us * 1e-6 * hz), static_cast<uint64_t*>(slot),
+                                    epoch, grid, stream, 0, sync);
+  });
+}
+
+int dlnb_gate_signal(void* gate, unsigned tag, void* stream) {
+  return guard([&] { dlnb::kernels::gate_signal(static_cast<uint64_t*>(gate), tag, stream); });
+}
+
 int dlnb_gemm_narrow_nf(int M, int N, int cus) { return dlnb::kernels::gemm_narrow_nf(M, N, cus); }
 
 int dlnb_gemm_shape_ok(int M, int N, int K, int dtype) {

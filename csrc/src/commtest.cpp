@@ -22,6 +22,7 @@
 //
 // Reference equivalent: none (DLNetBench relies on nccl-tests externally).
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -42,10 +43,61 @@ double now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// v(rank, i) in 1..8 * 1..4 (fp8: 1): sums over <= 8 ranks are exact integers.
-float val(int rank, size_t i, DType t) {
-  if (t == DType::FP8_E4M3 || t == DType::FP8_E5M2) return 1.0f;
+// Check patterns (the fp8 pass used 1.0 everywhere, so a block
+// from the wrong peer, offset or replay passed). Every value is exact in every
+// wire dtype, both fp8 formats included, and is a hash of its coordinates:
+//   data(r, i)  (all-gather, all-to-all, send/recv): one of 48 values
+//               k * 2^(e-2), k = 4..7, e = -3..8 (0.125 .. 448: exact with e5m2's
+//               2 mantissa bits, so in e4m3, fp16, bf16, fp32), hashed from
+//               (r, i): a block from another peer, another offset (any
+//               distance, the 8 / 16-element vector widths included) or the
+//               previous replay (its offset moves with the replay) differs in
+//               ~47 of 48 elements;
+//   red(r, i)   (all-reduce, reduce-scatter) fp8: one-hot - only rank
+//               owner(i) = hash(i) % W contributes, a table value, the others
+//               0: the sum is exact, and a dropped, doubled, misrouted or stale
+//               contribution changes it; other dtypes: 1..8 hashed from (r, i)
+//               on every rank (sums <= 64: exact integers).
+// Outputs are poisoned (all bits set: NaN in every float format) before every
+// operation and every graph replay, so an operation that writes nothing fails.
+uint64_t mix(uint64_t a, uint64_t b) {
+  uint64_t x = a * 0x9E3779B97F4A7C15ull ^ (b + 0x632BE59BD9B4E019ull);
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+float table_val(uint64_t h) {
+  const int k = 4 + static_cast<int>(h % 4);
+  const int e = -3 + static_cast<int>((h >> 2) % 12);
+  return std::ldexp(static_cast<float>(k), e - 2);
+}
+
+bool is_fp8(DType t) { return t == DType::FP8_E4M3 || t == DType::FP8_E5M2; }
+
+// DLNB_COMMTEST_LEGACY_PATTERN=1: the round-3 patterns ((rank % 8 + 1) * (i % 4 + 1),
+// fp8: 1.0 everywhere), kept so a test can show which faults they missed.
+bool legacy_pattern() {
+  static const bool on = env_int("DLNB_COMMTEST_LEGACY_PATTERN", 0) != 0;
+  return on;
+}
+float legacy_val(int rank, size_t i, DType t) {
+  if (is_fp8(t)) return 1.0f;
   return static_cast<float>((rank % 8 + 1) * static_cast<int>(i % 4 + 1));
+}
+
+float data_val(int rank, size_t i, DType t) {
+  if (legacy_pattern()) return legacy_val(rank, i, t);
+  return table_val(mix(static_cast<uint64_t>(rank) + 1, i));
+}
+
+float red_val(int rank, size_t i, DType t, int W) {
+  if (legacy_pattern()) return legacy_val(rank, i, t);
+  if (is_fp8(t)) {
+    const int owner = static_cast<int>(mix(0x5EEDull, i) % static_cast<uint64_t>(W));
+    return rank == owner ? table_val(mix(0xABCull, i)) : 0.0f;
+  }
+  return static_cast<float>(1 + mix(static_cast<uint64_t>(rank) + 101, i) % 8);
 }
 
 void encode(DType t, float f, void* p, size_t i) {
@@ -104,12 +156,20 @@ struct Tester {
     s.synchronize();
     return h;
   }
-  // host vector of n elements: element i = v(rank, off + i)
+  // host vector of n elements: element i = data(rank, off + i) or red(rank, off + i)
   std::vector<char> pattern(int rank, size_t off, size_t n) {
     std::vector<char> h(n * es);
-    for (size_t i = 0; i < n; ++i) encode(t, val(rank, off + i, t), h.data(), i);
+    for (size_t i = 0; i < n; ++i) encode(t, data_val(rank, off + i, t), h.data(), i);
     return h;
   }
+  std::vector<char> red_pattern(int rank, size_t off, size_t n) {
+    std::vector<char> h(n * es);
+    for (size_t i = 0; i < n; ++i) encode(t, red_val(rank, off + i, t, W), h.data(), i);
+    return h;
+  }
+  float val(int rank, size_t i) const { return data_val(rank, i, t); }
+  // all bits set: NaN in bf16, fp16, fp32 and both fp8 formats
+  void poison(void* b, size_t bytes) { upload(b, std::vector<char>(bytes, static_cast<char>(0xFF))); }
   void expect(const char* what, size_t n, const std::vector<char>& got, size_t i, float want) {
     float g = decode(t, got.data(), i);
     if (g != want) {
@@ -120,7 +180,7 @@ struct Tester {
   }
   float sum_over_ranks(size_t i) {
     float a = 0.f;
-    for (int r = 0; r < W; ++r) a += val(r, i, t);
+    for (int r = 0; r < W; ++r) a += red_val(r, i, t, W);
     return a;
   }
 
@@ -130,37 +190,42 @@ struct Tester {
     void* a = get(keep, n * W * es, 0);
     void* b = get(keep, n * W * es, 1);
     // all-reduce out of place
-    upload(a, pattern(me, 0, n));
+    upload(a, red_pattern(me, 0, n));
+    poison(b, n * es);
     comm.all_reduce(a, b, n, t, s);
     auto got = download(b, n * es);
     for (size_t i = 0; i < n; ++i) expect("all_reduce", n, got, i, sum_over_ranks(i));
-    // all-reduce in place
+    // all-reduce in place (fresh input: an out-of-place op must not have touched it, but check that apart)
+    upload(a, red_pattern(me, 0, n));
     comm.all_reduce(a, a, n, t, s);
     got = download(a, n * es);
     for (size_t i = 0; i < n; ++i) expect("all_reduce(in-place)", n, got, i, sum_over_ranks(i));
     // all-gather
     upload(a, pattern(me, 0, n));
+    poison(b, n * W * es);
     comm.all_gather(a, b, n, t, s);
     got = download(b, n * W * es);
     for (int r = 0; r < W; ++r)
-      for (size_t i = 0; i < n; ++i) expect("all_gather", n, got, r * n + i, val(r, i, t));
-    // reduce-scatter: send has W blocks of n, element j = v(me, j)
-    upload(a, pattern(me, 0, n * W));
+      for (size_t i = 0; i < n; ++i) expect("all_gather", n, got, r * n + i, val(r, i));
+    // reduce-scatter: send has W blocks of n, element j = red(me, j)
+    upload(a, red_pattern(me, 0, n * W));
+    poison(b, n * es);
     comm.reduce_scatter(a, b, n, t, s);
     got = download(b, n * es);
     for (size_t i = 0; i < n; ++i) expect("reduce_scatter", n, got, i, sum_over_ranks(me * n + i));
-    // all-to-all: block p of rank r's send = v(r, p*n + i) -> recv block p on me = v(p, me*n + i)
+    // all-to-all: block p of rank r's send = data(r, p*n + i) -> recv block p on me = data(p, me*n + i)
     upload(a, pattern(me, 0, n * W));
+    poison(b, n * W * es);
     comm.all_to_all(a, b, n, t, s);
     got = download(b, n * W * es);
     for (int p = 0; p < W; ++p)
-      for (size_t i = 0; i < n; ++i) expect("all_to_all", n, got, p * n + i, val(p, me * n + i, t));
+      for (size_t i = 0; i < n; ++i) expect("all_to_all", n, got, p * n + i, val(p, me * n + i));
     if (inplace_a2a) {
       upload(a, pattern(me, 0, n * W));
       comm.all_to_all(a, a, n, t, s);
       got = download(a, n * W * es);
       for (int p = 0; p < W; ++p)
-        for (size_t i = 0; i < n; ++i) expect("all_to_all(in-place)", n, got, p * n + i, val(p, me * n + i, t));
+        for (size_t i = 0; i < n; ++i) expect("all_to_all(in-place)", n, got, p * n + i, val(p, me * n + i));
     }
     s.synchronize();
     if (failures != before) std::fprintf(stderr, "[commtest] rank %d: n=%zu FAILED\n", me, n);
@@ -176,13 +241,14 @@ struct Tester {
     void *ar_in = get(keep, nb, 0), *ar_out = get(keep, nb, 1), *ar_ip = get(keep, nb, 2);
     void *ag_out = get(keep, nb, 3), *blk_in = get(keep, nb, 4), *rs_out = get(keep, nb, 5);
     void *a2a_out = get(keep, nb, 6), *p_in = get(keep, nb, 7), *p_out = get(keep, nb, 8);
+    void *a2a_in = get(keep, nb, 9), *ag_in = get(keep, nb, 10);
     const int next = (me + 1) % W, prev = (me + W - 1) % W;
     auto g = ctx.dev->capture(s, {}, [&] {
       comm.all_reduce(ar_in, ar_out, n, t, s);
       comm.all_reduce(ar_ip, ar_ip, n, t, s);
-      comm.all_gather(ar_in, ag_out, n, t, s);
+      comm.all_gather(ag_in, ag_out, n, t, s);
       comm.reduce_scatter(blk_in, rs_out, n, t, s);
-      comm.all_to_all(blk_in, a2a_out, n, t, s);
+      comm.all_to_all(a2a_in, a2a_out, n, t, s);
       if (W > 1) {
         link.group_start();
         link.send(p_in, n, t, next, s);
@@ -191,12 +257,15 @@ struct Tester {
       }
     });
     for (int rep = 0; rep < reps; ++rep) {
-      // rank r's inputs at replay rep: v(r, rep + i)
-      const size_t o = static_cast<size_t>(rep);
-      upload(ar_in, pattern(me, o, n));
-      upload(ar_ip, pattern(me, o, n));
-      upload(blk_in, pattern(me, o, n * W));
+      // rank r's inputs at replay rep: data / red(r, 7 * rep + i); every output poisoned
+      const size_t o = static_cast<size_t>(rep) * 7;
+      upload(ar_in, red_pattern(me, o, n));
+      upload(ar_ip, red_pattern(me, o, n));
+      upload(blk_in, red_pattern(me, o, n * W));
+      upload(a2a_in, pattern(me, o, n * W));
       upload(p_in, pattern(me, o, n));
+      upload(ag_in, pattern(me, o, n));
+      for (void* out : {ar_out, ag_out, rs_out, a2a_out, p_out}) poison(out, nb);
       g->launch(s);
       auto got = download(ar_out, n * es);
       for (size_t i = 0; i < n; ++i) expect("graph all_reduce", n, got, i, sum_over_ranks(o + i));
@@ -204,15 +273,15 @@ struct Tester {
       for (size_t i = 0; i < n; ++i) expect("graph all_reduce(in-place)", n, got, i, sum_over_ranks(o + i));
       got = download(ag_out, n * W * es);
       for (int r = 0; r < W; ++r)
-        for (size_t i = 0; i < n; ++i) expect("graph all_gather", n, got, r * n + i, val(r, o + i, t));
+        for (size_t i = 0; i < n; ++i) expect("graph all_gather", n, got, r * n + i, val(r, o + i));
       got = download(rs_out, n * es);
       for (size_t i = 0; i < n; ++i) expect("graph reduce_scatter", n, got, i, sum_over_ranks(o + me * n + i));
       got = download(a2a_out, n * W * es);
       for (int p = 0; p < W; ++p)
-        for (size_t i = 0; i < n; ++i) expect("graph all_to_all", n, got, p * n + i, val(p, o + me * n + i, t));
+        for (size_t i = 0; i < n; ++i) expect("graph all_to_all", n, got, p * n + i, val(p, o + me * n + i));
       if (W > 1) {
         got = download(p_out, n * es);
-        for (size_t i = 0; i < n; ++i) expect("graph send/recv", n, got, i, val(prev, o + i, t));
+        for (size_t i = 0; i < n; ++i) expect("graph send/recv", n, got, i, val(prev, o + i));
       }
     }
     s.synchronize();
@@ -226,23 +295,26 @@ struct Tester {
     void* b = get(keep, n * es, 1);
     const int next = (me + 1) % W, prev = (me + W - 1) % W;
     for (int rep = 0; rep < 3; ++rep) {  // several messages: exercises the double-buffered slots
-      upload(a, pattern(me, static_cast<size_t>(rep), n));
+      upload(a, pattern(me, static_cast<size_t>(rep) * 7, n));
+      poison(b, n * es);
       link.group_start();
       link.send(a, n, t, next, s);
       link.recv(b, n, t, prev, s);
       link.group_end();
       auto got = download(b, n * es);
-      for (size_t i = 0; i < n; ++i) expect("send/recv", n, got, i, val(prev, rep + i, t));
+      for (size_t i = 0; i < n; ++i) expect("send/recv", n, got, i, val(prev, static_cast<size_t>(rep) * 7 + i));
     }
   }
 };
 
 std::unique_ptr<CommFactory> factory_for(Context& ctx, const std::string& b) {
-  if (b == "rccl") return make_rccl_factory(ctx.hg(), *ctx.dev);
-  if (b == "xgmi") return make_xgmi_factory(ctx.hg(), *ctx.dev);
-  if (b == "mixed") return make_mixed_factory(ctx.hg(), *ctx.dev);
-  if (b == "cpu") return make_shm_factory(ctx.hg(), *ctx.dev);
-  DLNB_THROW("commtest --suite: unknown backend " << b << " (rccl, xgmi, mixed, cpu)");
+  std::unique_ptr<CommFactory> f;
+  if (b == "rccl") f = make_rccl_factory(ctx.hg(), *ctx.dev);
+  else if (b == "xgmi") f = make_xgmi_factory(ctx.hg(), *ctx.dev);
+  else if (b == "mixed") f = make_mixed_factory(ctx.hg(), *ctx.dev);
+  else if (b == "cpu") f = make_shm_factory(ctx.hg(), *ctx.dev);
+  else DLNB_THROW("commtest --suite: unknown backend " << b << " (rccl, xgmi, mixed, cpu)");
+  return wrap_comm_faults(std::move(f), *ctx.dev, ctx.rank());
 }
 
 // Modes a backend is checked in: eager enqueue and HIP-graph replay; xgmi
@@ -309,7 +381,7 @@ int run_suite(Context& ctx, const std::vector<std::string>& backends, const std:
         if (b == "rccl" && comm->library_nranks() >= 0) rccl_nranks = comm->library_nranks();
         std::vector<Buffer> pool;
         if (want_reg && comm->wants_peer_buffers()) {
-          for (int i = 0; i < 9; ++i) {
+          for (int i = 0; i < 11; ++i) {
             pool.push_back(ctx.dev->alloc_peer(std::max<size_t>(16, maxn * W * maxes)));
             comm->register_buffer(pool.back().data(), pool.back().bytes());
           }
@@ -507,7 +579,7 @@ int commtest_main(int argc, char** argv) {
   const bool reg = registered && comm->wants_peer_buffers();
   std::vector<Buffer> pool;
   if (reg && !bench) {
-    for (int i = 0; i < 9; ++i) {
+    for (int i = 0; i < 11; ++i) {
       pool.push_back(ctx.dev->alloc_peer(std::max<size_t>(16, maxn * W * es)));
       comm->register_buffer(pool.back().data(), pool.back().bytes());
     }

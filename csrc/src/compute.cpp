@@ -97,7 +97,11 @@ class GpuCompute : public ComputeEngine {
     if (mode_ != ComputeMode::Sleep && mode_ != ComputeMode::Spin) alloc_operands();
     if (mode_ == ComputeMode::GemmWork || mode_ == ComputeMode::Flops) calibrate();
     if (mode_ == ComputeMode::Gemm) {
-      slots_ = dev_.alloc(kSlots * 64);
+      // one 64-byte line per compute stream, then the gate words
+      slots_ = dev_.alloc(kSlots * 64 + kGates * 8);
+      auto zs = dev_.create_stream(false);
+      dev_.memset_async(slots_.data(), 0, kSlots * 64 + kGates * 8, *zs);
+      zs->synchronize();
       // Leave `comm_cus` CUs to collectives: one 128-KiB-LDS block fits per
       // CU, so a grid of CUs - comm_cus blocks never touches those CUs and
       // RCCL / copy kernels on the high-priority comm streams always find
@@ -120,7 +124,7 @@ class GpuCompute : public ComputeEngine {
   }
 
   void reset_clocks(Stream& s) override {
-    if (mode_ == ComputeMode::Gemm) dev_.memset_async(slots_.data(), 0, kSlots * 64, s);
+    if (mode_ == ComputeMode::Gemm) dev_.memset_async(slots_.data(), 0, kSlots * 64 + kGates * 8, s);
   }
 
   bool stamps_task_start() const override { return mode_ == ComputeMode::Gemm; }
@@ -128,30 +132,57 @@ class GpuCompute : public ComputeEngine {
   void run(Stream& s, double us, double flops) override { run_stamped(s, us, flops, nullptr); }
 
   void run_chained(Stream& s, double us, double flops) override {
-    if (mode_ == ComputeMode::Gemm && us * scale_ >= 20.0) {
-      uint64_t* slot = slot_for(s);
-      auto it = chain_end_.find(slot);
-      if (it != chain_end_.end() && it->second > 0) {
-        // Same epoch, so the same t0: this task's slices end at the previous
-        // task's deadline + its own duration on the clock the chain started.
-        const uint64_t base = it->second, total = base + ticks(us * scale_);
-        const uint64_t slice = slice_us_ > 0 ? std::max<uint64_t>(ticks(slice_us_), 1) : total;
-        for (uint64_t end = base + slice;; end += slice) {
-          kernels::gemm_tn_deadline(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, total, slot, epoch_[slot],
-                                    grid_, s.native(), std::min(end, total), nullptr);
-          if (end >= total) break;
-        }
-        it->second = total;
-        ++chained_;
-        return;
-      }
+    if (mode_ == ComputeMode::Gemm && us * scale_ >= 20.0 && chain_live_[slot_for(s)]) {
+      kernels::DlSync sync;
+      sync.tstart[1] = extra_start_;
+      extra_start_ = nullptr;
+      deadline_task(s, us * scale_, sync, true);
+      ++chained_;
+      return;
     }
     run(s, us, flops);
   }
 
+  bool gates_task(double us) const override { return mode_ == ComputeMode::Gemm && us * scale_ >= 20.0; }
+
+  int make_gate() override {
+    DLNB_REQUIRE(mode_ == ComputeMode::Gemm, "gates need the gemm (deadline) compute");
+    DLNB_REQUIRE(gate_tag_.size() < kGates, "too many compute gates");
+    gate_tag_.push_back(0);
+    return static_cast<int>(gate_tag_.size()) - 1;
+  }
+
+  void signal(Stream& s, int gate) override {
+    uint32_t& tag = gate_tag_.at(gate);
+    tag = tag % 65535 + 1;
+    kernels::gate_signal(gate_word(gate), tag, s.native());
+  }
+
+  void run_gated(Stream& s, double us, double flops, const std::vector<int>& gates, uint64_t* start,
+                 bool chain) override {
+    DLNB_REQUIRE(gates_task(us), "run_gated: the task cannot wait on gates (see gates_task)");
+    DLNB_REQUIRE(gates.size() <= 2, "run_gated: at most 2 gates per task");
+    (void)flops;
+    kernels::DlSync sync;
+    for (size_t i = 0; i < gates.size(); ++i) {
+      sync.gate[i] = gate_word(gates[i]);
+      sync.tag[i] = gate_tag_.at(gates[i]);
+      DLNB_REQUIRE(sync.tag[i] != 0, "run_gated: gate " << gates[i] << " was never signalled");
+    }
+    sync.tstart[0] = start;
+    sync.tstart[1] = extra_start_;
+    extra_start_ = nullptr;
+    const bool chained = chain && chain_live_[slot_for(s)];
+    deadline_task(s, us * scale_, sync, chained);
+    if (chained) ++chained_;
+    ++gated_;
+  }
+
+  void set_next_start_slot(uint64_t* slot) override { extra_start_ = slot; }
+
   void run_stamped(Stream& s, double us, double flops, uint64_t* start) override {
     double d = us * scale_;
-    if (mode_ == ComputeMode::Gemm) chain_end_[slot_for(s)] = 0;  // a chain restarts at every unchained task
+    if (mode_ == ComputeMode::Gemm) chain_live_[slot_for(s)] = false;  // a chain restarts at every unchained task
     if (mode_ == ComputeMode::Sleep) {
       if (d > 0) kernels::idle_wait(ticks(d), s.native());
       return;
@@ -164,22 +195,23 @@ class GpuCompute : public ComputeEngine {
       // Fixed duration, real MFMA work: persistent deadline GEMM (the stand-in
       // keeps the matrix cores and HBM busy for exactly the table's time, so
       // DVFS or contention changes how much work is done, not how long).
-      if (d <= 0) return;
+      if (d <= 0) {
+        if (extra_start_) dev_.stamp(s, extra_start_);
+        extra_start_ = nullptr;
+        return;
+      }
       if (d < 20.0) {
         if (start) dev_.stamp(s, start);
+        if (extra_start_) dev_.stamp(s, extra_start_);
+        extra_start_ = nullptr;
         kernels::busy_spin(ticks(d), cus_, s.native());
         return;
       }
-      uint32_t& ep = epoch_[slot_for(s)];
-      ep = ep % 65535 + 1;  // 1..65535, never 0 (a fresh slot reads as epoch 0)
-      const uint64_t total = ticks(d);
-      const uint64_t slice = slice_us_ > 0 ? std::max<uint64_t>(ticks(slice_us_), 1) : total;
-      for (uint64_t end = slice;; end += slice) {
-        kernels::gemm_tn_deadline(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, total, slot_for(s), ep,
-                                  grid_, s.native(), std::min(end, total), end == slice ? start : nullptr);
-        if (end >= total) break;
-      }
-      chain_end_[slot_for(s)] = total;
+      kernels::DlSync sync;
+      sync.tstart[0] = start;
+      sync.tstart[1] = extra_start_;
+      extra_start_ = nullptr;
+      deadline_task(s, d, sync, false);
       return;
     }
     // Fixed-work modes from here on: bracket the task with device stamps.
@@ -220,6 +252,7 @@ class GpuCompute : public ComputeEngine {
       j["comm_reserved_cus"] = cus_ - grid_;
       j["deadline_slice_us"] = slice_us_;
       j["chained_tasks"] = chained_;  // enqueued so far (a captured graph counts its one iteration)
+      j["gated_tasks"] = gated_;      // tasks that waited on device gates instead of stream events
     }
     if (A_.data()) {
       j["gemm_dtype"] = dtype_name(dtype_);
@@ -243,6 +276,27 @@ class GpuCompute : public ComputeEngine {
 
  private:
   uint64_t ticks(double us) const { return static_cast<uint64_t>(us * 1e-6 * hz_ + 0.5); }
+
+  // One deadline task of d us on s (every slice launch carries the same
+  // epoch; the kernels agree its start through the stream's slot line,
+  // csrc/kernels/deadline_sync.hpp). chain: start at the stream's previous
+  // deadline (or the latest gate) instead of when the first block arrives.
+  void deadline_task(Stream& s, double d, kernels::DlSync sync, bool chain) {
+    uint64_t* slot = slot_for(s);
+    uint32_t& ep = epoch_[slot];
+    ep = ep % 65535 + 1;  // 1..65535, never 0 (a fresh slot reads as epoch 0)
+    sync.chain = chain ? 1u : 0u;
+    const uint64_t total = ticks(d);
+    const uint64_t slice = slice_us_ > 0 ? std::max<uint64_t>(ticks(slice_us_), 1) : total;
+    for (uint64_t end = slice;; end += slice) {
+      kernels::gemm_tn_deadline(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, total, slot, ep, grid_,
+                                s.native(), std::min(end, total), end == slice ? sync : kernels::DlSync());
+      if (end >= total) break;
+    }
+    chain_live_[slot] = true;
+  }
+
+  uint64_t* gate_word(int gate) { return slots_.as<uint64_t>() + kSlots * 8 + gate; }
 
   // table_us: the task's uncontended duration (gemm-work: the table time;
   // flops: the calibrated time of its FLOPs at the largest GEMM level).
@@ -330,14 +384,18 @@ class GpuCompute : public ComputeEngine {
 
   static constexpr int kMmax = 8192;
   static constexpr size_t kSlots = 64;
+  static constexpr size_t kGates = 4096;
   Device& dev_;
   ComputeMode mode_;
   double scale_;
   Buffer slots_;
   std::map<Stream*, size_t> slot_of_;
   std::map<uint64_t*, uint32_t> epoch_;
-  std::map<uint64_t*, uint64_t> chain_end_;  // deadline (ticks after t0) of the stream's last task, 0: no chain
-  long chained_ = 0;                         // tasks that continued a chain (describe())
+  std::map<uint64_t*, bool> chain_live_;  // the stream's last task was a deadline task a chained one may continue
+  std::vector<uint32_t> gate_tag_;        // last tag signalled per gate (1..65535)
+  uint64_t* extra_start_ = nullptr;       // set_next_start_slot
+  long chained_ = 0;                      // tasks that continued a chain (describe())
+  long gated_ = 0;
   int grid_ = 256;
   double slice_us_ = 500;
   double hz_ = 1e8;

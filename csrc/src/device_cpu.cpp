@@ -149,11 +149,19 @@ void CpuStream::run() {
     try {
       if (!abort_ || !abort_->load()) fn();
     } catch (const std::exception& e) {
-      // A failed task would leave peers and other streams waiting forever:
-      // fail the whole rank loudly (the launcher tears the job down).
+      // A failed task would leave peers and other streams waiting forever.
+      // A CLI rank ends loudly (the launcher tears the job down); in a library
+      // host (Python) the device's abort switch drains every stream (later
+      // tasks are skipped, event waits return) and synchronize() throws the
+      // error to the caller, which can run another job afterwards.
       std::fprintf(stderr, "[dlnb] fatal error on CPU stream: %s\n", e.what());
       std::fflush(stderr);
-      std::_Exit(17);
+      if (cli_process()) std::_Exit(17);
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (error_.empty()) error_ = e.what();
+      }
+      if (abort_) abort_->store(true);
     }
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -300,9 +308,14 @@ class CpuDevice : public Device {
 
 }  // namespace
 
-std::unique_ptr<Device> make_cpu_device(AbortFlag abort) { return std::unique_ptr<Device>(new CpuDevice(std::move(abort))); }
+std::unique_ptr<Device> make_cpu_device(AbortFlag abort) {
+  // every CPU device has an abort switch: a failing stream task raises it
+  if (!abort) abort = std::make_shared<std::atomic<bool>>(false);
+  return std::unique_ptr<Device>(new CpuDevice(std::move(abort)));
+}
 
-std::unique_ptr<GraphExec> Device::capture(Stream&, const std::vector<Stream*>&, const std::function<void()>&) {
+std::unique_ptr<GraphExec> Device::capture(Stream&, const std::vector<Stream*>&, const std::function<void()>&,
+                                           const std::function<void()>&) {
   DLNB_THROW("--graph needs a GPU device (HIP graphs)");
 }
 

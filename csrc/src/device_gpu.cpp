@@ -159,7 +159,8 @@ class GpuDevice : public Device {
     return f;
   }
   std::unique_ptr<GraphExec> capture(Stream& origin, const std::vector<Stream*>& others,
-                                     const std::function<void()>& enqueue) override {
+                                     const std::function<void()>& enqueue,
+                                     const std::function<void()>& head) override {
     // Fork/join events exist before the capture starts (no creation inside).
     auto fork = create_event(false);
     std::vector<std::unique_ptr<Event>> joins;
@@ -167,6 +168,7 @@ class GpuDevice : public Device {
     hipStream_t o = static_cast<hipStream_t>(origin.native());
     DLNB_HIP_CHECK(hipStreamBeginCapture(o, hipStreamCaptureModeThreadLocal));
     try {
+      if (head) head();
       origin.record(*fork);
       for (Stream* s : others) s->wait(*fork);
       enqueue();

@@ -293,6 +293,7 @@ std::string select_backend(Context& ctx, const std::string& requested, const std
   } else {
     DLNB_THROW("unknown backend '" << backend << "' (auto, rccl, xgmi, mixed, cpu, loopback, loopback-cpu)");
   }
+  ctx.comms = wrap_comm_faults(std::move(ctx.comms), *ctx.dev, ri.rank);
   ctx.comms.reset(new RecordingFactory(std::move(ctx.comms), &ctx.comm_log));
   return backend;
 }
@@ -382,6 +383,8 @@ Json run_loopback(const Options& opt) {
 }
 
 }  // namespace
+
+bool cli_process() { return g_cli_process.load(); }
 
 Json run_benchmark(const Options& opt) {
   if (opt.backend == "loopback" || opt.backend == "loopback-cpu") return run_loopback(opt);
@@ -505,6 +508,12 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       std::cerr << "[dlnb] warning: " << strat->streams().size() << " streams per rank > GPU_MAX_HW_QUEUES=" << nq
                 << "; streams will share hardware queues" << std::endl;
   }
+  // DLNB_INJECT_FAULT mode=task: a task that throws on the first stream
+  // (CPU devices; library hosts must get the error back, not lose the process)
+  auto inject_task = [&] {
+    DLNB_REQUIRE(ctx.dev->kind() == DeviceKind::CPU, "DLNB_INJECT_FAULT mode=task needs a CPU device");
+    ctx.dev->host_task(*strat->streams()[0], [] { DLNB_THROW("injected fault in a stream task"); });
+  };
   Timeline* TL = ctx.timeline.get();
   if (TL) TL->calibrate(*strat->streams()[0]);
   TimerSet& T = *strat->timers();
@@ -526,10 +535,10 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     TraceRange tr("dlnb:graph_capture");
     T.begin_capture();
     if (TL) TL->begin_capture();
-    graph = ctx.dev->capture(*ss[0], others, [&] {
-      ctx.compute->reset_clocks(*ss[0]);
-      strat->enqueue_iteration();
-    });
+    // the engine's slot / gate reset heads the graph, before every stream's
+    // first node (a gate raised on a comm stream must not be wiped by it)
+    graph = ctx.dev->capture(
+        *ss[0], others, [&] { strat->enqueue_iteration(); }, [&] { ctx.compute->reset_clocks(*ss[0]); });
     T.end_capture();
     if (TL) TL->end_capture();
     if (ri.rank == 0 && !opt.quiet)
@@ -547,7 +556,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   // ---- warm-up
   std::vector<double> warm;
   for (int i = 0; i < opt.warmup; ++i) {
-    fault.at_iteration(iter_no++);
+    fault.at_iteration(iter_no++, inject_task);
     TraceRange tr("dlnb:warmup_iteration");
     double t0 = now_s();
     enqueue();
@@ -576,7 +585,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     // runs forever unless --max-loop-iters bounds it.
     T.set_enabled(false);
     for (long long it = 0; opt.max_loop_iters == 0 || it < opt.max_loop_iters; ++it) {
-      fault.at_iteration(iter_no++);
+      fault.at_iteration(iter_no++, inject_task);
       TraceRange tr("dlnb:loop_iteration");
       enqueue();
       strat->synchronize();
@@ -593,7 +602,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   ctx.dev->synchronize();
   const double T0 = now_s();
   for (int r = 0; r < runs; ++r) {
-    fault.at_iteration(iter_no++);
+    fault.at_iteration(iter_no++, inject_task);
     TraceRange tr("dlnb:iteration");
     const double j0 = meter->joules();
     double t0 = now_s();

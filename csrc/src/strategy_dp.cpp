@@ -75,8 +75,12 @@ class DataParallel : public Strategy {
     bwd_us_per_bucket_ = st.avg_backward_time_us / nb_;
     // backward compute of bucket i: the reference's bwd/nb, or under a
     // geometric policy the bucket's share of the parameters
-    for (uint64_t sz : sizes_)
-      bwd_us_.push_back(ratio_ >= 1.0 ? bwd_us_per_bucket_ : st.avg_backward_time_us * sz / static_cast<double>(P_));
+    // (time and FLOPs alike: --compute flops sizes a task by its FLOPs)
+    for (uint64_t sz : sizes_) {
+      const double share = ratio_ >= 1.0 ? 1.0 / nb_ : static_cast<double>(sz) / static_cast<double>(P_);
+      bwd_us_.push_back(ratio_ >= 1.0 ? bwd_us_per_bucket_ : st.avg_backward_time_us * share);
+      bwd_flops_.push_back(st.backward_flops * share);
+    }
     fwd_flops_ = st.forward_flops;
     bwd_flops_per_bucket_ = st.backward_flops / nb_;
 
@@ -164,7 +168,7 @@ class DataParallel : public Strategy {
     ce.run(*compute_, fwd_us_, fwd_flops_);
     for (int i = 0; i < nb_; ++i) {
       // only event records on compute_ since the forward: one stretch of compute
-      ce.run_chained(*compute_, bwd_us_[i], bwd_flops_per_bucket_);
+      ce.run_chained(*compute_, bwd_us_[i], bwd_flops_[i]);
       compute_->record(*ready_[i]);
       comm_stream_->wait(*ready_[i]);
       const uint64_t n = shard_[i] * W_;
@@ -207,7 +211,7 @@ class DataParallel : public Strategy {
     ce.run(*compute_, fwd_us_, fwd_flops_);
     for (int i = 0; i < nb_; ++i) {
       // only event records on compute_ since the forward: one stretch of compute
-      ce.run_chained(*compute_, bwd_us_[i], bwd_flops_per_bucket_);
+      ce.run_chained(*compute_, bwd_us_[i], bwd_flops_[i]);
       compute_->record(*ready_[i]);
       comm_stream_->wait(*ready_[i]);
       int t = timers_->begin(*comm_stream_);
@@ -263,6 +267,10 @@ class DataParallel : public Strategy {
     if (ratio_ < 1.0) {
       g["bucket_policy"] = "geometric";
       g["bucket_sizes"] = Json(sizes_);
+      // every bucket's backward compute: time (sleep/spin/gemm modes) and
+      // FLOPs (--compute flops) in the same share as its parameters
+      g["bwd_us_per_bucket"] = Json(bwd_us_);
+      g["bwd_flops_per_bucket"] = Json(bwd_flops_);
     } else {
       g["bucket_policy"] = "even";
     }
@@ -295,7 +303,8 @@ class DataParallel : public Strategy {
   uint64_t P_ = 0;
   size_t es_ = 2;
   std::vector<uint64_t> sizes_;
-  std::vector<double> bwd_us_;  // backward compute per bucket
+  std::vector<double> bwd_us_;     // backward compute per bucket
+  std::vector<double> bwd_flops_;  // and its FLOPs
   double ratio_ = 1.0;
   double fwd_us_ = 0, bwd_us_per_bucket_ = 0, fwd_flops_ = 0, bwd_flops_per_bucket_ = 0;
   bool in_place_ = false;

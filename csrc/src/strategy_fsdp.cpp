@@ -118,6 +118,27 @@ class Fsdp : public Strategy {
     mk(bwd_done_);
     mk(rs_done_);
     mk(ar_done_);
+    // Device gates (ComputeEngine::run_gated): every compute task continues
+    // the previous one's deadline unless a collective it depends on finished
+    // later - the gate words the collectives' stream raises carry that time -
+    // so the compute stays one unbroken stretch of exactly the table time,
+    // with a late collective's wait (and only that) added. Without it each of
+    // the 64 tasks of a llama3_8b iteration starts after the cross-queue hop
+    // of the replayed graph (~10 us) and overshoots by its launch ramp and
+    // drain (~13 us): ~1.2 ms per iteration (profiles/timeline_r3.md). The
+    // event waits stay: the gate only dates the dependency, the graph edge
+    // still orders it (a kernel spinning on a word raised by a node the graph
+    // executor queued behind it on the same hardware queue would never
+    // finish). DLNB_DEVICE_GATES=0: plain event waits + run_stamped (A/B).
+    ComputeEngine& ce = *ctx.compute;
+    gated_ = !reference_ && env_int("DLNB_DEVICE_GATES", 1) != 0 && ce.gates_task(fwd_us_) && ce.gates_task(bwd_us_);
+    if (gated_) {
+      for (int u = 0; u < U_; ++u) {
+        g_ag_f_.push_back(ce.make_gate());
+        g_ag_b_.push_back(ce.make_gate());
+        g_rs_.push_back(ce.make_gate());
+      }
+    }
     if (o.optimizer) {
       DLNB_REQUIRE(ctx.wire == DType::BF16, "--optimizer needs --wire-dtype bf16");
       for (int u = 0; u < U_; ++u) mom_.push_back(dev.alloc(shard_[u] * es_));
@@ -159,28 +180,47 @@ class Fsdp : public Strategy {
   }
   void compute_after(Event& dep, const char* timer, double us, double flops) { compute_after(&dep, timer, us, flops); }
 
+  // The gated form (after the event waits on the gates' collectives): start
+  // at max(previous task's deadline, the gates' times); the first task of
+  // the iteration is not chained and has no timer.
+  void compute_gated(std::vector<int> gates, const char* timer, double us, double flops) {
+    ComputeEngine& ce = *ctx_->compute;
+    uint64_t* st = timers_->slot();
+    ce.run_gated(*compute_, us, flops, gates, st, prev_start_ != nullptr);
+    if (timer && prev_start_) timers_->gap(prev_start_, prev_ticks_, st, timer);
+    prev_start_ = st;
+    prev_ticks_ = ce.task_ticks(us);
+  }
+
   void enqueue_iteration() override {
     Context& ctx = *ctx_;
     const DType t = ctx.wire;
     prev_start_ = nullptr;
 
-    auto gather = [&](int u, Event& done, bool first) {
+    ComputeEngine& ce = *ctx.compute;
+    auto gather = [&](int u, Event& done, bool first, int gate) {
       int tk = timers_->begin(*ag_stream_);
       ag_comm_->all_gather(params_[u].data(), gathered_[u & 1].data(), shard_[u], t, *ag_stream_);
       timers_->end(tk, *ag_stream_, first ? "allgather" : "allgather_time");
+      if (gated_) ce.signal(*ag_stream_, gate);  // before the record: the event implies the gate
       ag_stream_->record(done);
     };
 
     // ---- forward
-    gather(0, *ag_f_[0], true);
+    gather(0, *ag_f_[0], true, gated_ ? g_ag_f_[0] : -1);
     if (reference_) ag_stream_->synchronize();  // blocking Allgather (fsdp.cpp:86-91)
     for (int u = 0; u < U_; ++u) {
       if (u + 1 < U_) {
         // gathered[(u+1)&1] was last read by forward(u-1).
         if (u >= 1) ag_stream_->wait(*fwd_done_[u - 1]);
-        gather(u + 1, *ag_f_[u + 1], false);
+        gather(u + 1, *ag_f_[u + 1], false, gated_ ? g_ag_f_[u + 1] : -1);
       }
-      compute_after(*ag_f_[u], u == 0 ? nullptr : "allgather_wait_fwd", fwd_us_, fwd_flops_);
+      if (gated_) {
+        compute_->wait(*ag_f_[u]);
+        compute_gated({g_ag_f_[u]}, u == 0 ? nullptr : "allgather_wait_fwd", fwd_us_, fwd_flops_);
+      } else {
+        compute_after(*ag_f_[u], u == 0 ? nullptr : "allgather_wait_fwd", fwd_us_, fwd_flops_);
+      }
       compute_->record(*fwd_done_[u]);
     }
 
@@ -189,20 +229,34 @@ class Fsdp : public Strategy {
       if (u - 1 >= 0) {
         // gathered[(u-1)&1] was last read by backward(u+1), or by forward(U-2).
         ag_stream_->wait(u + 1 <= U_ - 1 ? *bwd_done_[u + 1] : *fwd_done_[u - 1]);
-        gather(u - 1, *ag_b_[u - 1], false);
+        gather(u - 1, *ag_b_[u - 1], false, gated_ ? g_ag_b_[u - 1] : -1);
       }
       // full_grad[u&1] was last read by the reduce-scatter of unit u+2.
-      if (u + 2 <= U_ - 1) compute_->wait(*rs_done_[u + 2]);
-      if (u < U_ - 1)
-        compute_after(*ag_b_[u], "allgather_wait_bwd", bwd_us_, bwd_flops_);
-      else
-        compute_after(nullptr, nullptr, bwd_us_, bwd_flops_);
+      if (gated_) {
+        std::vector<int> gates;
+        if (u < U_ - 1) {
+          compute_->wait(*ag_b_[u]);
+          gates.push_back(g_ag_b_[u]);
+        }
+        if (u + 2 <= U_ - 1) {
+          compute_->wait(*rs_done_[u + 2]);
+          gates.push_back(g_rs_[u + 2]);
+        }
+        compute_gated(gates, u < U_ - 1 ? "allgather_wait_bwd" : nullptr, bwd_us_, bwd_flops_);
+      } else {
+        if (u + 2 <= U_ - 1) compute_->wait(*rs_done_[u + 2]);
+        if (u < U_ - 1)
+          compute_after(*ag_b_[u], "allgather_wait_bwd", bwd_us_, bwd_flops_);
+        else
+          compute_after(nullptr, nullptr, bwd_us_, bwd_flops_);
+      }
       compute_->record(*bwd_done_[u]);
 
       rs_stream_->wait(*bwd_done_[u]);
       int tk = timers_->begin(*rs_stream_);
       rs_comm_->reduce_scatter(full_grad_[u & 1].data(), grads_[u].data(), shard_[u], t, *rs_stream_);
       timers_->end(tk, *rs_stream_, "reduce_scatter");
+      if (gated_) ce.signal(*rs_stream_, g_rs_[u]);
       rs_stream_->record(*rs_done_[u]);
       if (reference_) compute_->wait(*rs_done_[u]);  // blocking Reduce_Scatter_block (fsdp.cpp:124)
       if (R_ > 1) {
@@ -257,6 +311,7 @@ class Fsdp : public Strategy {
     g["device"] = ctx.dev->kind() == DeviceKind::CPU ? "CPU" : "GPU";
     g["backend"] = ag_comm_->backend_name();
     g["comm_lanes"] = ctx.opt.comm_lanes;
+    g["device_gates"] = gated_;
     g["fwd_time_per_unit_us"] = fwd_us_;
     g["bwd_time_per_unit_us"] = bwd_us_;
     g["allgather_msg_size_bytes"] = max_shard_ * F_ * es_;
@@ -282,6 +337,8 @@ class Fsdp : public Strategy {
   uint64_t P_ = 0, max_shard_ = 0;
   size_t es_ = 2;
   bool reference_ = false;
+  bool gated_ = false;                         // device gates instead of compute-stream event waits
+  std::vector<int> g_ag_f_, g_ag_b_, g_rs_;    // gate per forward / backward all-gather, reduce-scatter
   std::vector<uint64_t> shard_;
   double fwd_us_ = 0, bwd_us_ = 0, fwd_flops_ = 0, bwd_flops_ = 0;
   std::vector<std::unique_ptr<Communicator>> comms_;

@@ -44,6 +44,17 @@ int Timeline::begin(Stream& s) {
   return idx;
 }
 
+int Timeline::begin_external(uint64_t** slot) {
+  *slot = nullptr;
+  if (frozen_ || next_ + 3 > cap_) {
+    if (!frozen_) truncated_ = true;
+    return -1;
+  }
+  const int idx = static_cast<int>(next_++);
+  *slot = stamps_ + idx;
+  return idx;
+}
+
 void Timeline::end(int token, Stream& s, const char* cat, const std::string& name, Json args) {
   if (token < 0) return;
   const int idx = static_cast<int>(next_++);  // begin() reserved room for it
@@ -340,18 +351,39 @@ class TracingCompute : public ComputeEngine {
     traced(s, "compute (chained)", us, [&] { in_->run_chained(s, us, flops); });
   }
   uint64_t task_ticks(double us) const override { return in_->task_ticks(us); }
+  bool gates_task(double us) const override { return in_->gates_task(us); }
+  int make_gate() override { return in_->make_gate(); }
+  void signal(Stream& s, int gate) override { in_->signal(s, gate); }
+  void run_gated(Stream& s, double us, double flops, const std::vector<int>& gates, uint64_t* start,
+                 bool chain) override {
+    Json a = Json::object();
+    a["gates"] = static_cast<int>(gates.size());
+    traced(s, chain ? "compute (chained)" : "compute", us, [&] { in_->run_gated(s, us, flops, gates, start, chain); },
+           a);
+  }
+  void set_next_start_slot(uint64_t* slot) override { in_->set_next_start_slot(slot); }
   void reset_clocks(Stream& s) override { in_->reset_clocks(s); }
   void set_task_timers(TimerSet* t) override { in_->set_task_timers(t); }
   Json describe() const override { return in_->describe(); }
   ComputeMode mode() const override { return in_->mode(); }
 
  private:
+  // A deadline engine's kernels write their task's effective start (after
+  // its gates, at the chain's deadline) into the span's first slot, so a
+  // wait for a collective shows as exposed communication, not as compute,
+  // and an absorbed launch gap not as idle; other engines: a stamp kernel.
   template <class F>
-  void traced(Stream& s, const char* name, double us, F&& fn) {
+  void traced(Stream& s, const char* name, double us, F&& fn, Json a = Json::object()) {
     tl_->label(s, "compute");
-    const int tok = tl_->begin(s);
+    int tok;
+    if (in_->stamps_task_start()) {
+      uint64_t* first = nullptr;
+      tok = tl_->begin_external(&first);
+      in_->set_next_start_slot(first);
+    } else {
+      tok = tl_->begin(s);
+    }
     fn();
-    Json a = Json::object();
     a["table_us"] = us;
     tl_->end(tok, s, "compute", name, a);
   }

@@ -54,7 +54,8 @@ def gemm_tn(a, b, out=None, waves: int = 0):
 
 def gemm_deadline_us(a, b, c, us: float, stamp=None, grid: int = 0):
     """Persistent MFMA GEMM over C = A.B^T tiles that stops after `us` microseconds
-    (device clock). `stamp` is a CUDA int64 tensor with >= 1 element (scratch)."""
+    (device clock). `stamp` is a CUDA int64 tensor with >= 8 elements (the
+    64-byte slot line the blocks agree their start through)."""
     import torch
     dt = _native.DTYPES["bf16"] if a.dtype == torch.bfloat16 else _native.DTYPES["fp8_e4m3"]
     M, K = a.shape
@@ -64,6 +65,33 @@ def gemm_deadline_us(a, b, c, us: float, stamp=None, grid: int = 0):
     _native.check(_native.lib().dlnb_gemm_deadline_us(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, dt, us,
                                                       a.device.index or 0, stamp.data_ptr(), grid, _stream(a)))
     return c
+
+
+def gemm_deadline_ex(a, b, c, us: float, slot, epoch: int, chain: bool = False, gates=(), tstart=None,
+                     grid: int = 0):
+    """gemm_deadline_us with the whole start protocol (csrc/kernels/deadline_sync.hpp): `slot` an int64
+    CUDA tensor of 8 elements reused by consecutive tasks of one stream, `epoch` the task number on it
+    (1..65535, different from the previous task's), `chain` start at the slot's previous deadline,
+    `gates` up to two (int64 CUDA tensor, index, tag) words to wait for, `tstart` an (int64 tensor,
+    index) that receives the task's start (s_memrealtime ticks)."""
+    import torch
+    dt = _native.DTYPES["bf16"] if a.dtype == torch.bfloat16 else _native.DTYPES["fp8_e4m3"]
+    M, K = a.shape
+    N = b.shape[0]
+    if slot.numel() < 8 or slot.dtype != torch.int64:
+        raise ValueError("slot must be an int64 tensor of >= 8 elements")
+    g = [(t.data_ptr() + 8 * i, tag) for t, i, tag in gates] + [(None, 0)] * (2 - len(gates))
+    ts = tstart[0].data_ptr() + 8 * tstart[1] if tstart is not None else None
+    _native.check(_native.lib().dlnb_gemm_deadline_ex(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, dt, us,
+                                                      a.device.index or 0, slot.data_ptr(), grid, _stream(a), epoch,
+                                                      int(chain), g[0][0], g[0][1], g[1][0], g[1][1], ts))
+    return c
+
+
+def gate_signal_(gate, index: int, tag: int):
+    """Raise gate[index] = {tag:16 | s_memrealtime:48} when torch's current stream reaches this point."""
+    _native.check(_native.lib().dlnb_gate_signal(gate.data_ptr() + 8 * index, tag, _stream(gate)))
+    return gate
 
 
 def fill_random_(t, seed: int = 0):

@@ -116,6 +116,74 @@ def test_bench_hybrid_blocks_eight_ranks_cpu(tmp_path):
     assert {"hybrid_3d", "hybrid_3d_moe", "hybrid_3d_moe_ep_overlap"} <= set(o["phase_seconds"])
 
 
+def _torchrun(n, args, tmp_path, env=None, timeout=300):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(n)] + args
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=str(tmp_path),
+                       env=dict(os.environ, OMP_NUM_THREADS="1", **(env or {})))
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    return lines[0]
+
+
+def test_bench_wall_budget_survives_a_hung_block_two_ranks(tmp_path):
+    """VERDICT r3 #1: a block that hangs on one rank (DLNB_INJECT_FAULT block=c5: rank 1's comm-bound child
+    never finishes) costs at most what the wall budget leaves; the line still prints within the budget, the
+    hung block reports its timeout and the blocks that no longer fit are skipped, on every rank alike."""
+    budget = 40
+    o = _torchrun(2, ["--steps", "2", "--warmup", "1", "--backend", "cpu", "--compute", "sleep",
+                      "--wall-budget-s", str(budget)] + TINY, tmp_path,
+                  env={"DLNB_INJECT_FAULT": "rank=1,iter=0,mode=hang,block=c5"}, timeout=200)
+    assert o["value"] > 0 and o["verified"] == {"cpu": True}
+    assert o["phase_seconds"]["total"] <= budget
+    assert "timeout" in o["comm_bound"]["error"]
+    b = o["budget"]
+    assert b["wall_budget_s"] == budget and "c5" in b["timeouts_s"] and "c5g" in b["skipped"]
+    assert "skipped" in o["comm_bound"]["geometric_buckets"]
+
+
+def test_bench_wall_budget_hybrids_eight_ranks(tmp_path):
+    """The N = 8 path with the hybrid blocks and a hang injected into C3 on rank 5: C3 reports its timeout
+    (its limit: --hybrid-timeout), the C4 blocks after it still run (per_run_ms: --c4-runs entries), one
+    line within the budget."""
+    budget = 75
+    o = _torchrun(8, ["--steps", "1", "--warmup", "0", "--backend", "cpu", "--compute", "sleep",
+                      "--hybrids", "on", "--c3-model", "tiny_deep_8_bfloat16", "--c3", "2,4,4",
+                      "--c4-model", "tiny_moe_8_bfloat16", "--c4", "2,8,4", "--c4-runs", "2", "--exact", "off",
+                      "--c5-model", "none", "--wall-budget-s", str(budget), "--hybrid-timeout", "25"] + TINY[:6],
+                  tmp_path, env={"DLNB_INJECT_FAULT": "rank=5,iter=0,mode=hang,block=c3"}, timeout=300)
+    assert o["phase_seconds"]["total"] <= budget
+    assert "timeout" in o["hybrid_3d"]["error"], o["hybrid_3d"]
+    h4 = o["hybrid_3d_moe"]
+    assert "error" not in h4 and len(h4["per_run_ms"]) == 2 and h4["ms_per_step"] > 0, h4
+    ov = h4["ep_overlap"]
+    assert ("skipped" in ov) or len(ov["per_run_ms"]) == 2, ov
+
+
+def test_bench_c3_two_timed_runs_eight_ranks(tmp_path):
+    """C3 (hybrid_3d) is timed over 2 iterations by default: per_run_ms has both (VERDICT r3 #7)."""
+    o = _torchrun(8, ["--steps", "1", "--warmup", "0", "--backend", "cpu", "--compute", "sleep",
+                      "--hybrids", "on", "--c3-model", "tiny_deep_8_bfloat16", "--c3", "2,4,4",
+                      "--c4-model", "tiny_moe_8_bfloat16", "--c4", "2,8,4", "--c4-ep-overlap", "off",
+                      "--exact", "off", "--c5-model", "none"] + TINY[:6], tmp_path, timeout=300)
+    h3 = o["hybrid_3d"]
+    assert "error" not in h3 and len(h3["per_run_ms"]) == 2 and all(x > 0 for x in h3["per_run_ms"]), h3
+    assert len(o["hybrid_3d_moe"]["per_run_ms"]) == 1
+
+
+def test_bench_unverified_backend_flags_its_blocks(tmp_path):
+    """VERDICT r3 #4: with the shm backend's collectives corrupted (DLNB_COMM_FAULT swaps two peers'
+    all-gather blocks on rank 0), the exactness pass fails, the line says verified.cpu = false, and the
+    headline and the comm-bound block - timed anyway - carry the error."""
+    o = _torchrun(2, ["--steps", "2", "--warmup", "1", "--backend", "cpu", "--compute", "sleep"] + TINY, tmp_path,
+                  env={"DLNB_COMM_FAULT": "mode=swap,op=all_gather,rank=0"}, timeout=200)
+    assert o["verified"] == {"cpu": False} and o["exact"]["cpu"] is False
+    assert "exactness failed" in o["error"] and o["value"] > 0
+    assert "exactness failed" in o["comm_bound"]["error"] and o["comm_bound"]["ms_per_step"] > 0
+
+
 def test_bench_two_nodes_cpu(tmp_path):
     """The multi-node launch (torchrun --nnodes 2, 2 ranks per "node", both on
     127.0.0.1): LOCAL_WORLD_SIZE < WORLD_SIZE, so every phase rendezvouses on

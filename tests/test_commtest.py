@@ -48,6 +48,57 @@ def test_cpu_backend_registered_exact(w, dtype):
     assert out[0]["ok"] and out[0]["registered"] is True and out[0]["backend"] == "CPU-SHM"
 
 
+FAULTS = ["mode=swap,op=all_gather", "mode=swap,op=all_to_all,rank=1", "mode=swap,op=all_reduce,rank=1",
+          "mode=swap,op=reduce_scatter,rank=0", "mode=swap,op=recv,rank=1", "mode=skip,op=all_gather",
+          "mode=skip,op=reduce_scatter", "mode=skip,op=recv", "mode=skip,op=all_reduce,call=1"]
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp8_e4m3", "fp8_e5m2"])
+@pytest.mark.parametrize("fault", FAULTS)
+def test_exactness_check_catches_injected_faults(fault, dtype):
+    """Mutation check of the exactness pass: a peer / offset misroute (swap two
+    parts of an op's output) or an op that never ran (skip: its output keeps stale data) fails the check
+    in every dtype, fp8 included (DLNB_COMM_FAULT, csrc/src/comm_fault.cpp)."""
+    p = launch(2, [DLNB, "commtest", "--backend", "cpu", "--dtype", dtype, "--sizes", "64,4097"],
+               {"DLNB_COMM_FAULT": fault}, timeout=100)
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode != 0 and lines and not lines[0]["ok"] and lines[0]["failures"] > 0, p.stdout + p.stderr[-2000:]
+
+
+@pytest.mark.parametrize("fault", ["mode=swap,op=all_gather", "mode=swap,op=all_to_all,rank=1",
+                                   "mode=swap,op=recv,rank=1"])
+def test_legacy_fp8_pattern_missed_misroutes(fault):
+    """Why the patterns changed: with round 3's fp8 pattern (1.0 for every rank and element) the same
+    misroutes pass unnoticed; the hashed patterns above catch them."""
+    p = launch(2, [DLNB, "commtest", "--backend", "cpu", "--dtype", "fp8_e4m3", "--sizes", "64,4097"],
+               {"DLNB_COMM_FAULT": fault, "DLNB_COMMTEST_LEGACY_PATTERN": "1"}, timeout=100)
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and lines[0]["ok"], p.stdout + p.stderr[-2000:]
+
+
+def test_suite_reports_injected_fault_per_combination(tmp_path):
+    """--suite (bench.py's exactness pass) on the CPU backend: the faulty combination is reported failed
+    and the verdict is all-reduced (every rank writes the same report)."""
+    out = tmp_path / "suite.json"
+    p = launch(2, [DLNB, "commtest", "--suite", "--backends", "cpu", "--dtypes", "bf16,fp8_e4m3",
+                   "--sizes", "4097,30000", "--json", str(out)], {"DLNB_COMM_FAULT": "mode=swap,op=all_gather"},
+               timeout=100)
+    d = json.loads(out.read_text())
+    assert p.returncode != 0 and d["ok"] is False and d["exact"]["cpu"] is False
+    assert {(r["dtype"], r["ok"]) for r in d["results"]} == {("bf16", False), ("fp8_e4m3", False)}
+
+
+def test_suite_eight_ranks_time_cpu(tmp_path):
+    """The exactness pass at N = 8 with bench.py's sizes stays within its time budget (here the CPU
+    backend on this container: 8 processes, every op poisoned and checked)."""
+    out = tmp_path / "suite.json"
+    p = launch(8, [DLNB, "commtest", "--suite", "--backends", "cpu", "--dtypes", "bf16,fp8_e4m3",
+                   "--sizes", "4097,300000,2097157", "--json", str(out)], timeout=200)
+    d = json.loads(out.read_text())
+    assert p.returncode == 0 and d["ok"] and d["world_size"] == 8, p.stderr[-2000:]
+    assert d["seconds"] < 20, d["seconds"]
+
+
 def test_cpu_backend_bench_lines():
     out = commtest(2, "--backend", "cpu", "--bench", "--sizes", "4096,65536", "--iters", "2", "--warmup", "1")
     ops = {(o["op"], o["count"]) for o in out}
@@ -301,3 +352,17 @@ def test_rccl_exactness_suite_single_rank():
     s = commtest(1, "--suite", "--backends", "rccl", "--dtypes", "bf16,fp8_e4m3")[0]
     assert s["ok"] and s["exact"] == {"rccl": True, "rccl_eager": True, "rccl_graph": True}, s
     assert s["rccl_nranks"] == 1 and s["runtime"]["librccl"].startswith("/opt/rocm")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fault", ["mode=swap,op=all_gather", "mode=skip,op=all_to_all", "mode=swap,op=recv,rank=0"])
+@pytest.mark.parametrize("dtype", ["bf16", "fp8_e4m3"])
+def test_xgmi_graph_check_catches_injected_faults(fault, dtype):
+    """The mutation check in HIP-graph mode on the GPU (xgmi kernels, 2 ranks sharing the GPU): a
+    misroute captured into the graph, or an op missing from it (its output stays poisoned), fails the
+    replayed check in bf16 and in fp8."""
+    _need_gpu()
+    p = launch(2, [DLNB, "commtest", "--backend", "xgmi", "-d", "0,0", "--graph", "--dtype", dtype,
+                   "--sizes", "4097,300000"], dict(SMALL_WINDOWS, DLNB_COMM_FAULT=fault), timeout=100)
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode != 0 and lines and not lines[0]["ok"] and lines[0]["graph"], p.stdout + p.stderr[-2000:]

@@ -246,3 +246,83 @@ def test_deadline_gemm_numerics(M, N, K, grid, dtype):
     torch.cuda.synchronize()
     assert not torch.isnan(c.float()).any(), "some tile was never stored"
     assert_close_bf16_out(c, a.float() @ b.float().t())
+
+
+def _grid():
+    # leave 32 CUs free, as the runtime does: the gate / idle kernels of the other stream need room
+    return torch.cuda.get_device_properties(0).multi_processor_count - 32
+
+
+def _deadline_operands(dtype="bf16"):
+    a = torch.empty(8192, 4096, device="cuda", dtype=torch.bfloat16)
+    b = torch.empty(4096, 4096, device="cuda", dtype=torch.bfloat16)
+    gemm.fill_random_(a, 1)
+    gemm.fill_random_(b, 2)
+    c = torch.empty(8192, 4096, device="cuda", dtype=torch.bfloat16)
+    return a, b, c
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+def test_deadline_chain_continues_previous_deadline(dtype):
+    """Chained deadline tasks (deadline_sync.hpp): the second task of a stream starts exactly at the first
+    one's deadline (its start stamp = first start + ticks), so a launch gap between them is absorbed and the
+    pair lasts the sum of their durations; an unchained task starts when its first block arrives."""
+    a, b, c = _deadline_operands()
+    if dtype == "fp8":
+        if not hasattr(torch, "float8_e4m3fn"):
+            pytest.skip("torch without float8")
+        a, b = a.to(torch.float8_e4m3fn), b.to(torch.float8_e4m3fn)
+    slot = torch.zeros(8, dtype=torch.int64, device="cuda")
+    ts = torch.zeros(4, dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    hz = 100e6
+    for rep in range(3):
+        ep = 1 + 3 * rep
+        e0.record(s)
+        gemm.gemm_deadline_ex(a, b, c, 2000.0, slot, ep, chain=False, tstart=(ts, 0), grid=_grid())
+        gemm.idle_wait_us(300.0)  # a gap the chain must absorb
+        gemm.gemm_deadline_ex(a, b, c, 3000.0, slot, ep + 1, chain=True, tstart=(ts, 1), grid=_grid())
+        gemm.gemm_deadline_ex(a, b, c, 1000.0, slot, ep + 2, chain=True, tstart=(ts, 2), grid=_grid())
+        e1.record(s)
+        torch.cuda.synchronize()
+    t = ts.tolist()
+    assert abs(t[1] - t[0] - 2000e-6 * hz) <= 1, t
+    assert abs(t[2] - t[1] - 3000e-6 * hz) <= 1, t
+    ms = e0.elapsed_time(e1)
+    assert 6.0 <= ms <= 6.0 * 1.01 + 0.05, ms  # 2 + 3 + 1 ms: the 0.3 ms gap was absorbed
+
+
+def test_deadline_gate_waits_for_signal():
+    """A gated task (deadline_sync.hpp) starts when its gate is raised on another stream (here after a
+    4 ms idle wait there), not when its kernel launches, and a chained gated task whose gate opened after
+    the previous deadline starts at the gate's time: the wait is exposed, never absorbed."""
+    a, b, c = _deadline_operands()
+    slot = torch.zeros(8, dtype=torch.int64, device="cuda")
+    gates = torch.zeros(4, dtype=torch.int64, device="cuda")
+    ts = torch.zeros(4, dtype=torch.int64, device="cuda")
+    other = torch.cuda.Stream()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    mask = (1 << 48) - 1
+    e0.record(s)
+    other.wait_event(e0)
+    # task 1: gate 0 raised right away; task 2 (chained): gate 1 raised ~4 ms later than task 1's deadline
+    with torch.cuda.stream(other):
+        gemm.gate_signal_(gates, 0, 7)
+        gemm.idle_wait_us(1000.0 + 4000.0)
+        gemm.gate_signal_(gates, 1, 9)
+    gemm.gemm_deadline_ex(a, b, c, 1000.0, slot, 1, chain=False, gates=[(gates, 0, 7)], tstart=(ts, 0),
+                          grid=_grid())
+    gemm.gemm_deadline_ex(a, b, c, 1000.0, slot, 2, chain=True, gates=[(gates, 1, 9), (gates, 0, 7)],
+                          tstart=(ts, 1), grid=_grid())
+    e1.record(s)
+    torch.cuda.synchronize()
+    g = gates.tolist()
+    t = ts.tolist()
+    assert g[0] >> 48 == 7 and g[1] >> 48 == 9, g
+    gate1 = g[1] & mask
+    assert (t[1] & mask) == gate1, (t, g)  # started at the late gate, not at the previous deadline
+    assert t[1] - t[0] >= round(4000e-6 * 100e6), t
+    ms = e0.elapsed_time(e1)
+    assert 6.0 <= ms <= 6.0 * 1.02 + 0.1, ms
