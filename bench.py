@@ -725,7 +725,7 @@ def main() -> int:
                     help="device list by local rank, e.g. 0,0 to put 2 ranks on one GPU (xgmi backend tests)")
     ap.add_argument("--base-path", default=ROOT, help="directory holding model_stats/ and models/")
     ap.add_argument("--time-scale", type=float, default=None, help="scale every compute duration (tests)")
-    ap.add_argument("--wall-budget-s", type=float, default=float(os.environ.get("DLNB_BENCH_WALL_S", "480")),
+    ap.add_argument("--wall-budget-s", type=float, default=float(os.environ.get("DLNB_BENCH_WALL_S", "420")),
                     help="wall seconds for the whole bench: every phase after the headline gets at most what is "
                          "left and is skipped when too little is (env DLNB_BENCH_WALL_S)")
     ap.add_argument("--budget-reserve-s", type=float, default=10.0,

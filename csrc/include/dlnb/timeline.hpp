@@ -46,6 +46,11 @@ class Timeline {
   // kernel's start, ComputeEngine::set_next_start_slot) into *slot.
   int begin_external(uint64_t** slot);
   void end(int token, Stream& s, const char* cat, const std::string& name, Json args = Json::object());
+  // End a span `dur_ticks` device-clock ticks after its start, without a
+  // stamp: a deadline task's span is [start, deadline] (its grid's drain
+  // after the deadline belongs to the next chained task, which starts at it).
+  void end_after(int token, Stream& s, uint64_t dur_ticks, const char* cat, const std::string& name,
+                 Json args = Json::object());
   // Track name of a stream (the first name given wins).
   void label(Stream& s, const std::string& name);
   // Graph mode: the spans enqueued between these are the captured
@@ -72,7 +77,8 @@ class Timeline {
   uint64_t* stamps_ = nullptr;
   size_t cap_ = 0, next_ = 0, max_events_ = 0;
   struct Span {
-    int a, b, lane;
+    int a, b, lane;  // b < 0: the span lasts dur ticks from a
+    uint64_t dur;
     const char* cat;
     std::string name;
     Json args;

@@ -256,7 +256,7 @@ class Fsdp : public Strategy {
       int tk = timers_->begin(*rs_stream_);
       rs_comm_->reduce_scatter(full_grad_[u & 1].data(), grads_[u].data(), shard_[u], t, *rs_stream_);
       timers_->end(tk, *rs_stream_, "reduce_scatter");
-      if (gated_) ce.signal(*rs_stream_, g_rs_[u]);
+      if (gated_ && u >= 2) ce.signal(*rs_stream_, g_rs_[u]);  // RS(u) gates bwd(u - 2)
       rs_stream_->record(*rs_done_[u]);
       if (reference_) compute_->wait(*rs_done_[u]);  // blocking Reduce_Scatter_block (fsdp.cpp:124)
       if (R_ > 1) {

@@ -59,7 +59,14 @@ void Timeline::end(int token, Stream& s, const char* cat, const std::string& nam
   if (token < 0) return;
   const int idx = static_cast<int>(next_++);  // begin() reserved room for it
   dev_.stamp(s, stamps_ + idx);
-  spans_.push_back(Span{token, idx, lane_of(s), cat, name, std::move(args)});
+  spans_.push_back(Span{token, idx, lane_of(s), 0, cat, name, std::move(args)});
+}
+
+void Timeline::end_after(int token, Stream& s, uint64_t dur_ticks, const char* cat, const std::string& name,
+                         Json args) {
+  if (token < 0) return;
+  ++next_;  // keep begin()'s accounting (two slots per span)
+  spans_.push_back(Span{token, -1, lane_of(s), dur_ticks, cat, name, std::move(args)});
 }
 
 void Timeline::begin_capture() {
@@ -78,7 +85,7 @@ void Timeline::collect(int iter) {
         break;
       }
       const uint64_t a = __atomic_load_n(stamps_ + sp.a, __ATOMIC_ACQUIRE);
-      const uint64_t b = __atomic_load_n(stamps_ + sp.b, __ATOMIC_ACQUIRE);
+      const uint64_t b = sp.b < 0 ? a + sp.dur : __atomic_load_n(stamps_ + sp.b, __ATOMIC_ACQUIRE);
       events_.push_back(Event{iter, sp.lane, sp.cat, sp.name, sp.args, a, b >= a ? b : a});
     }
   }
@@ -385,7 +392,10 @@ class TracingCompute : public ComputeEngine {
     }
     fn();
     a["table_us"] = us;
-    tl_->end(tok, s, "compute", name, a);
+    if (in_->stamps_task_start())
+      tl_->end_after(tok, s, in_->task_ticks(us), "compute", name, a);
+    else
+      tl_->end(tok, s, "compute", name, a);
   }
   std::unique_ptr<ComputeEngine> in_;
   Timeline* tl_;

@@ -305,22 +305,24 @@ def test_deadline_gate_waits_for_signal():
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     mask = (1 << 48) - 1
-    e0.record(s)
-    other.wait_event(e0)
-    # task 1: gate 0 raised right away; task 2 (chained): gate 1 raised ~4 ms later than task 1's deadline
-    with torch.cuda.stream(other):
-        gemm.gate_signal_(gates, 0, 7)
-        gemm.idle_wait_us(1000.0 + 4000.0)
-        gemm.gate_signal_(gates, 1, 9)
-    gemm.gemm_deadline_ex(a, b, c, 1000.0, slot, 1, chain=False, gates=[(gates, 0, 7)], tstart=(ts, 0),
-                          grid=_grid())
-    gemm.gemm_deadline_ex(a, b, c, 1000.0, slot, 2, chain=True, gates=[(gates, 1, 9), (gates, 0, 7)],
-                          tstart=(ts, 1), grid=_grid())
-    e1.record(s)
-    torch.cuda.synchronize()
+    for rep in range(2):  # the first round also loads the kernels
+        t0, t1 = 7 + 10 * rep, 9 + 10 * rep
+        e0.record(s)
+        other.wait_event(e0)
+        # task 1: gate 0 raised right away; task 2 (chained): gate 1 raised ~4 ms after task 1's deadline
+        with torch.cuda.stream(other):
+            gemm.gate_signal_(gates, 0, t0)
+            gemm.idle_wait_us(1000.0 + 4000.0)
+            gemm.gate_signal_(gates, 1, t1)
+        gemm.gemm_deadline_ex(a, b, c, 1000.0, slot, 1 + 2 * rep, chain=False, gates=[(gates, 0, t0)],
+                              tstart=(ts, 0), grid=_grid())
+        gemm.gemm_deadline_ex(a, b, c, 1000.0, slot, 2 + 2 * rep, chain=True, gates=[(gates, 1, t1), (gates, 0, t0)],
+                              tstart=(ts, 1), grid=_grid())
+        e1.record(s)
+        torch.cuda.synchronize()
     g = gates.tolist()
     t = ts.tolist()
-    assert g[0] >> 48 == 7 and g[1] >> 48 == 9, g
+    assert g[0] >> 48 == 17 and g[1] >> 48 == 19, g
     gate1 = g[1] & mask
     assert (t[1] & mask) == gate1, (t, g)  # started at the late gate, not at the previous deadline
     assert t[1] - t[0] >= round(4000e-6 * 100e6), t
