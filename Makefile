@@ -18,7 +18,10 @@ CXXFLAGS = $(OPT) -std=c++17 -fPIC -Wall -Wno-unused-result -Icsrc/include --off
 LDLIBS   = -L$(ROCM)/lib -lrccl -lamdhip64 -lpthread -lrt -Wl,-rpath,$(ROCM)/lib
 
 LIB_SRCS := $(wildcard csrc/src/*.cpp) $(wildcard csrc/kernels/*.hip)
-LIB_OBJS := $(patsubst csrc/%,$(BUILD)/obj/%.o,$(LIB_SRCS))
+# host-only C++ (no device pass): the CPU backend's multiversioned SIMD loops
+HOST_SRCS := $(wildcard csrc/host/*.cpp)
+HOSTCXX  ?= $(ROCM)/llvm/bin/clang++
+LIB_OBJS := $(patsubst csrc/%,$(BUILD)/obj/%.o,$(LIB_SRCS)) $(patsubst csrc/%,$(BUILD)/obj/%.o,$(HOST_SRCS))
 APPS     := dp fsdp hybrid_2d hybrid_3d hybrid_3d_moe hybrid_cp hybrid_4d dlnb
 LOOPS    := dp_loop fsdp_loop hybrid_2d_loop hybrid_3d_loop hybrid_3d_moe_loop hybrid_cp_loop hybrid_4d_loop
 LIB      := $(BUILD)/libdlnb.so
@@ -28,6 +31,10 @@ PYLIB    := dlnetbench_amd/_lib/libdlnb.so
 all: lib apps
 
 lib: $(PYLIB)
+
+$(BUILD)/obj/host/%.o: csrc/host/%
+	@mkdir -p $(dir $@)
+	$(HOSTCXX) $(subst -Xarch_host,,$(OPT)) -std=c++17 -fPIC -Wall -Icsrc/include -MMD -MP -c $< -o $@
 
 $(BUILD)/obj/%.o: csrc/%
 	@mkdir -p $(dir $@)

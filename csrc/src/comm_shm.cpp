@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "dlnb/comm.hpp"
+#include "dlnb/host_simd.hpp"
 
 namespace dlnb {
 
@@ -80,21 +81,6 @@ void wait_on(std::atomic<uint32_t>* word, Pred pred, double timeout_s, const cha
 
 void wake(std::atomic<uint32_t>* word) { futex(word, FUTEX_WAKE, INT32_MAX); }
 
-inline float bf16f(uint16_t v) {
-  uint32_t u = static_cast<uint32_t>(v) << 16;
-  float f;
-  std::memcpy(&f, &u, 4);
-  return f;
-}
-
-inline uint16_t fbf16(float f) {
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<uint16_t>((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<uint16_t>(u >> 16);
-}
-
 // Sum n elements starting at element off of every source into dst, blockwise
 // through an fp32 accumulator (vectorisable inner loops).
 void reduce_sum(DType t, void* dst, const std::vector<const char*>& srcs, size_t off, size_t n) {
@@ -107,20 +93,20 @@ void reduce_sum(DType t, void* dst, const std::vector<const char*>& srcs, size_t
   float acc[BLK];
   for (size_t b = 0; b < n; b += BLK) {
     const size_t m = std::min(BLK, n - b);
-    for (size_t i = 0; i < m; ++i) acc[i] = 0.f;
-    for (const char* s : srcs) {
-      const size_t e0 = off + b;
+    const size_t e0 = off + b;
+    if (t == DType::BF16)  // the first source initialises the accumulator (one pass fewer)
+      simd::set_bf16(acc, reinterpret_cast<const uint16_t*>(srcs[0]) + e0, m);
+    else
+      for (size_t i = 0; i < m; ++i) acc[i] = 0.f;
+    for (size_t si = t == DType::BF16 ? 1 : 0; si < srcs.size(); ++si) {
+      const char* s = srcs[si];
       switch (t) {
-        case DType::BF16: {
-          const uint16_t* p = reinterpret_cast<const uint16_t*>(s) + e0;
-          for (size_t i = 0; i < m; ++i) acc[i] += bf16f(p[i]);
+        case DType::BF16:
+          simd::acc_bf16(acc, reinterpret_cast<const uint16_t*>(s) + e0, m);
           break;
-        }
-        case DType::FP32: {
-          const float* p = reinterpret_cast<const float*>(s) + e0;
-          for (size_t i = 0; i < m; ++i) acc[i] += p[i];
+        case DType::FP32:
+          simd::acc_f32(acc, reinterpret_cast<const float*>(s) + e0, m);
           break;
-        }
         case DType::FP16: {
           const uint16_t* p = reinterpret_cast<const uint16_t*>(s) + e0;
           for (size_t i = 0; i < m; ++i) acc[i] += fp16_to_float(p[i]);
@@ -141,7 +127,7 @@ void reduce_sum(DType t, void* dst, const std::vector<const char*>& srcs, size_t
     char* d = static_cast<char*>(dst) + b * es;
     switch (t) {
       case DType::BF16:
-        for (size_t i = 0; i < m; ++i) reinterpret_cast<uint16_t*>(d)[i] = fbf16(acc[i]);
+        simd::store_bf16(reinterpret_cast<uint16_t*>(d), acc, m);
         break;
       case DType::FP32: std::memcpy(d, acc, m * 4); break;
       case DType::FP16:
