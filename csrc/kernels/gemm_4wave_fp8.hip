@@ -704,11 +704,11 @@ int gemm_narrow_nf(int M, int N, int cus) {
   // saving of at least 10 % (a partial last round - 640 square tiles are 2.5
   // rounds, 1024 of 256 x 160 exactly 4 - against the square kernels' higher
   // reuse and, fp8, the streaming kernel). DLNB_GEMM_NARROW_NF=8 pins the
-  // square tile (A/B), 3-6 forces a width where it divides N.
-  static const int forced = [] {
-    const char* v = std::getenv("DLNB_GEMM_NARROW_NF");
-    return v ? std::atoi(v) : 0;
-  }();
+  // square tile (A/B), 3-7 forces a width where it divides N. Read on every
+  // call (a getenv per GEMM launch is negligible), so an A/B in one process
+  // can change it between launches.
+  const char* env = std::getenv("DLNB_GEMM_NARROW_NF");
+  const int forced = env ? std::atoi(env) : 0;
   if (forced >= 3 && forced <= 8) return (forced == 8 || N % (32 * forced) == 0) ? forced : 8;
   const long sq = static_cast<long>(M / kT) * (N / kT);
   const long sq_cost = (sq + cus - 1) / cus * 8;

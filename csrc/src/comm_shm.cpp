@@ -23,6 +23,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <atomic>
 #include <deque>
 #include <cstring>
@@ -202,6 +203,7 @@ class ShmComm : public Communicator {
     for (int i = 0; i < size_; ++i)
       if (members[i] == my_world_rank) rank_ = i;
     DLNB_REQUIRE(rank_ >= 0, "rank " << my_world_rank << " is not a member of group " << name);
+    my_world_rank_ = my_world_rank;
     timeout_ = static_cast<double>(env_int("DLNB_TIMEOUT", 900));
 
     std::ostringstream key;
@@ -254,6 +256,10 @@ class ShmComm : public Communicator {
 
   // Collective, paired by order across members (the xgmi backend's rule):
   // every member maps every other member's k-th registered buffer.
+  // If some member cannot map a peer's buffer (ranks in separate PID
+  // namespaces or containers, /proc mounted hidepid), every member keeps the
+  // registration slot but marks it unusable, so all of them take the staged
+  // path for it (this used to throw on the failing rank only).
   void register_buffer(void* p, size_t bytes) override {
     Reg r;
     r.local = static_cast<char*>(p);
@@ -268,6 +274,8 @@ class ShmComm : public Communicator {
       for (int m : members_) key << m << ",";
       key << "reg" << regs_.size() << "/";
       world_->store().set(key.str() + std::to_string(rank_), src + " " + std::to_string(bytes));
+      std::string why;
+      std::vector<std::pair<void*, size_t>> mine;
       for (int q = 0; q < size_; ++q) {
         if (q == rank_) continue;
         std::istringstream in(world_->store().get(key.str() + std::to_string(q)));
@@ -276,14 +284,35 @@ class ShmComm : public Communicator {
         in >> path >> qb;
         DLNB_REQUIRE(qb == bytes, "shm: registration " << regs_.size() << " of " << name_ << ": rank " << q
                                                         << " registered " << qb << " B, this rank " << bytes);
-        const int fd = ::open(path.c_str(), O_RDWR);
-        if (fd < 0) DLNB_THROW("shm: cannot open peer buffer " << path << ": " << std::strerror(errno));
+        if (!why.empty()) continue;
+        // DLNB_SHM_NO_PEER_MAP=R: rank R behaves as if /proc/<pid>/fd were hidden (tests)
+        const int fd = env_int("DLNB_SHM_NO_PEER_MAP", -1) == my_world_rank_ ? -1 : ::open(path.c_str(), O_RDWR);
+        if (fd < 0) {
+          why = "cannot open peer buffer " + path + ": " + std::strerror(errno);
+          continue;
+        }
         void* a = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
         ::close(fd);
-        if (a == MAP_FAILED) DLNB_THROW("shm: cannot map peer buffer " << path);
+        if (a == MAP_FAILED) {
+          why = "cannot map peer buffer " + path;
+          continue;
+        }
         r.peer[static_cast<size_t>(q)] = static_cast<char*>(a);
-        mapped_.emplace_back(a, bytes);
+        mine.emplace_back(a, bytes);
       }
+      // every member's verdict: the registration is usable only if all mapped
+      world_->store().set(key.str() + "ok/" + std::to_string(rank_), why.empty() ? "1" : "0");
+      bool all_ok = true;
+      for (int q = 0; q < size_; ++q) all_ok = all_ok && world_->store().get(key.str() + "ok/" + std::to_string(q)) == "1";
+      if (!all_ok) {
+        if (!why.empty() && !warned_)
+          std::fprintf(stderr, "[dlnb] shm backend: %s; %s uses the staged (copy) path\n", why.c_str(), name_.c_str());
+        warned_ = true;
+        for (auto& m : mine) munmap(m.first, m.second);
+        mine.clear();
+        r.usable = false;
+      }
+      for (auto& m : mine) mapped_.push_back(m);
       // every member mapped every buffer before anyone may free one
       barrier();
     }
@@ -498,12 +527,15 @@ class ShmComm : public Communicator {
     char* local = nullptr;
     size_t bytes = 0;
     std::vector<char*> peer;  // by group rank (own entry = local)
+    bool usable = true;       // every member mapped every peer's buffer
   };
+  bool warned_ = false;
+  int my_world_rank_ = 0;
   // The registration holding [p, p + bytes) on this rank, with p's offset.
   const Reg* find(const void* p, size_t bytes, size_t& off) const {
     const char* c = static_cast<const char*>(p);
     for (const auto& r : regs_)
-      if (c >= r.local && c + bytes <= r.local + r.bytes) {
+      if (r.usable && c >= r.local && c + bytes <= r.local + r.bytes) {
         off = static_cast<size_t>(c - r.local);
         return &r;
       }

@@ -91,6 +91,18 @@ class GpuCompute : public ComputeEngine {
     const int kmul = dtype_ == DType::FP8_E4M3 ? 256 : 128;
     K_ = std::min(65536, std::max(512, (shape.ffn + kmul - 1) / kmul * kmul));
     N_ = std::min(32768, std::max(1024, (shape.hidden + 255) / 256 * 256));
+    // The operands must fit beside the strategy's buffers: at most 1/8 of this
+    // rank's share of free memory (ranks sharing the GPU each allocate their
+    // own set). Large-FFN models (K = ffn up to 64 Ki) shrink K, keeping its
+    // multiple (ffn 53248 x hidden 16384 is ~2.6 GB per rank).
+    if (mode_ != ComputeMode::Sleep && mode_ != ComputeMode::Spin) {
+      const size_t esz = dtype_size(dtype_);
+      const double share = static_cast<double>(dev_.free_memory()) / std::max(1, shape.ranks_on_device) / 8.0;
+      auto bytes = [&](int k) {
+        return static_cast<double>(kMmax + N_) * k * esz + static_cast<double>(kMmax) * N_ * 2;
+      };
+      while (K_ > 512 && share > 0 && bytes(K_) > share) K_ = std::max(512, (K_ / 2 + kmul - 1) / kmul * kmul);
+    }
     // GEMM operands for every GEMM mode; the launch-time calibration only for
     // the fixed-work modes (a deadline task lasts its table time whatever a
     // launch costs, so the gemm mode skips the ~0.6 s of measuring).

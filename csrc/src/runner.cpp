@@ -323,9 +323,19 @@ struct LoopbackJob {
 // LocalStore (host barriers / gathers) and one LoopbackHub (collectives). A
 // failing rank aborts both (and the job's CPU abort switch), so the others
 // leave their waits instead of hanging; the first failure is rethrown.
+// Rank threads of loopback jobs still running. A job whose rank threads did
+// not drain after a failure detaches them (below); they keep GPU streams and
+// buffers until they finally leave their waits, so this process refuses new
+// loopback jobs until then (they would share the GPU with the
+// next job and may still run at interpreter exit).
+std::atomic<int> g_loopback_threads{0};
+
 Json run_loopback(const Options& opt) {
   const int n = opt.ranks;
   DLNB_REQUIRE(n >= 1, "--ranks must be >= 1");
+  const int live = g_loopback_threads.load();
+  DLNB_REQUIRE(live == 0, "a previous loopback job of this process still has " << live
+                              << " rank threads blocked (detached after its failure); run the next job in a new process");
   DLNB_REQUIRE(env_int("WORLD_SIZE", 1) == 1 && env_int("DLNB_WORLD_SIZE", 1) == 1,
                "--backend loopback runs all ranks inside one process: launch it once, not under a multi-rank launcher");
   auto job = std::make_shared<LoopbackJob>();
@@ -335,6 +345,7 @@ Json run_loopback(const Options& opt) {
   job->docs.resize(static_cast<size_t>(n));
   std::vector<std::thread> threads;
   for (int r = 0; r < n; ++r) {
+    g_loopback_threads.fetch_add(1);
     threads.emplace_back([job, r, n] {
       try {
         Json d = run_rank(job->opt, bootstrap_loopback(r, n, job->store, job->hub));
@@ -350,6 +361,7 @@ Json run_loopback(const Options& opt) {
         loopback_abort(*job->hub, msg);
         job->store->abort(msg);
       }
+      g_loopback_threads.fetch_sub(1);
       std::lock_guard<std::mutex> g(job->mu);
       ++job->done;
       job->done_cv.notify_all();
@@ -374,7 +386,9 @@ Json run_loopback(const Options& opt) {
     std::fflush(stderr);
     if (g_cli_process.load()) std::_Exit(2);
     for (auto& t : threads) t.detach();
-    throw Error(err + " (" + std::to_string(stuck) + " rank threads still blocked were detached)");
+    throw Error(err + " (" + std::to_string(stuck) +
+                " rank threads still blocked were detached; this process runs no further loopback job until they "
+                "exit)");
   }
   g.unlock();
   for (auto& t : threads) t.join();

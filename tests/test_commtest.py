@@ -99,6 +99,16 @@ def test_suite_eight_ranks_time_cpu(tmp_path):
     assert d["seconds"] < 20, d["seconds"]
 
 
+def test_cpu_registered_falls_back_when_a_peer_cannot_map():
+    """a rank that cannot open a peer's buffer (separate PID namespace, hidepid /proc) no longer
+    fails the run: every member marks that registration unusable and the ops take the staged path, exactly."""
+    p = launch(2, [DLNB, "commtest", "--backend", "cpu", "--registered", "--dtype", "bf16", "--sizes", "7,4097"],
+               {"DLNB_SHM_NO_PEER_MAP": "1"}, timeout=100)
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and lines[0]["ok"], p.stdout + p.stderr[-2000:]
+    assert "staged (copy) path" in p.stderr
+
+
 def test_cpu_backend_bench_lines():
     out = commtest(2, "--backend", "cpu", "--bench", "--sizes", "4096,65536", "--iters", "2", "--warmup", "1")
     ops = {(o["op"], o["count"]) for o in out}
