@@ -103,7 +103,7 @@ def check(events: List[dict]) -> List[str]:
     for key, iv in lanes.items():
         iv.sort()
         for (a0, a1, an), (b0, b1, bn) in zip(iv, iv[1:]):
-            if b0 < a1 - 1e-3:  # 1 ns of rounding
+            if b0 < a1 - 2e-3:  # the trace rounds to 1 ns (either end)
                 bad.append(f"rank {key[0]} stream {key[1]} iter {key[2]}: '{bn}' starts before '{an}' ends")
     want = set().union(*iters.values()) if iters else set()
     for pid, its in iters.items():
