@@ -162,7 +162,9 @@ class _Budget:
         self._t = time.monotonic
         self.start = self._t()
         self.total, self.reserve, self.world, self.rank = total_s, reserve_s, world, rank
-        self.shared = world > 1 and int(os.environ.get("LOCAL_WORLD_SIZE", world)) == world
+        # one node (torchrun's LOCAL_WORLD_SIZE == WORLD_SIZE): rank 0's plan files;
+        # otherwise (several nodes, or a launcher that does not say) own clocks
+        self.shared = world > 1 and int(os.environ.get("LOCAL_WORLD_SIZE", "0")) == world
         self.dir = f"/tmp/dlnb_bench_plan_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}"
         self.plans: Dict[str, Any] = {}
         self.seen_dir = False
@@ -564,6 +566,9 @@ def _timeline_block(a: argparse.Namespace, world: int, rank: int, budget: "_Budg
         res["well_formed"] = not bad
         res["span_ms_max"] = round(max(r["span_ms"] for r in per.values()), 3)
         res["comm_exposed_ms_max"] = round(max(r["comm_exposed_ms"] for r in per.values()), 3)
+        if all("host_ms" in r for r in per.values()):
+            # what the host's timing adds to the device span (launch + completion detection)
+            res["host_boundary_ms_max"] = round(max(r["host_ms"] - r["span_ms"] for r in per.values()), 3)
         busy = sum(r["comm_busy_ms"] for r in per.values())
         res["comm_hidden_frac"] = round(sum(r["comm_hidden_ms"] for r in per.values()) / busy, 4) if busy else None
         ops: Dict[str, Any] = {}

@@ -63,6 +63,11 @@ class Timeline {
   void collect(int iter);
   // Pairs the device clock with the host's steady clock (host-syncs s).
   void calibrate(Stream& s);
+  // The host's view of iteration `iter` (now_s() before the enqueue / graph
+  // launch and after the streams were synchronised: what the reference times)
+  // as a span on a "host" track: host span - device span = the iteration
+  // boundary (launch + completion detection).
+  void host_iteration(int iter, double t0_s, double t1_s);
   // This rank's events of the last `keep_iters` collected iterations
   // (0 = all): {"rank", "lanes", "events": [[iter, lane, cat, name, ts_us,
   // dur_us, args], ...], "calibration_error_us", "truncated"}; ts_us on the

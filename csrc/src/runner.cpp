@@ -622,8 +622,12 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     double t0 = now_s();
     enqueue();
     strat->synchronize();
-    T.add(rkey, now_s() - t0);
-    if (TL) TL->collect(r);
+    const double t1 = now_s();
+    T.add(rkey, t1 - t0);
+    if (TL) {
+      TL->collect(r);
+      TL->host_iteration(r, t0, t1);
+    }
     if (meter->available()) T.add("energy_consumed", meter->joules() - j0);
   }
   ctx.dev->synchronize();

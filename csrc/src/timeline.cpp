@@ -94,6 +94,25 @@ void Timeline::collect(int iter) {
   next_ = 0;
 }
 
+void Timeline::host_iteration(int iter, double t0_s, double t1_s) {
+  if (iter < 0 || events_.size() >= max_events_) return;
+  static const int kHostLaneKey = 0;
+  auto it = lanes_.find(&kHostLaneKey);
+  int lane;
+  if (it == lanes_.end()) {
+    lane = static_cast<int>(lane_names_.size());
+    lanes_[&kHostLaneKey] = lane;
+    lane_names_.push_back("host iteration");
+  } else {
+    lane = it->second;
+  }
+  auto tick = [&](double t_s) {
+    const double d = (t_s * 1e6 - host_cal_us_) * hz_ / 1e6;
+    return static_cast<uint64_t>(static_cast<double>(tick_cal_) + d);
+  };
+  events_.push_back(Event{iter, lane, "host", "iteration (host)", Json::object(), tick(t0_s), tick(t1_s)});
+}
+
 void Timeline::calibrate(Stream& s) {
   // The stamp lands between the two host reads; the best of a few tries
   // (shortest bracket) pairs the clocks.

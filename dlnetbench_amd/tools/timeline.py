@@ -65,6 +65,10 @@ def summarize(events: List[dict]) -> Dict[str, dict]:
         by[(e["pid"], e["args"]["iter"])].append(e)
     out: Dict[str, dict] = defaultdict(dict)
     for (pid, it), evs in sorted(by.items()):
+        host = [e for e in evs if e["cat"] == "host"]
+        evs = [e for e in evs if e["cat"] != "host"]
+        if not evs:
+            continue
         comp = _union([(e["ts"], e["ts"] + e["dur"]) for e in evs if e["cat"] == "compute"])
         comm = _union([(e["ts"], e["ts"] + e["dur"]) for e in evs if e["cat"] in ("comm", "p2p")])
         t0 = min(e["ts"] for e in evs)
@@ -87,6 +91,14 @@ def summarize(events: List[dict]) -> Dict[str, dict]:
             "compute_idle_ms": (t1 - t0 - _length(comp)) / 1e3,
             "ops": {k: dict(v) for k, v in sorted(ops.items())},
         }
+        if host:
+            # the iteration as the host timed it, and what it adds to the device span
+            # (graph launch / enqueue before the first op, completion detection after the last)
+            h = host[0]
+            r = out[str(pid)][str(it)]
+            r["host_ms"] = h["dur"] / 1e3
+            r["launch_ms"] = (t0 - h["ts"]) / 1e3
+            r["completion_ms"] = (h["ts"] + h["dur"] - t1) / 1e3
     return dict(out)
 
 
@@ -129,11 +141,14 @@ def main(argv=None) -> int:
     if a.json:
         print(json.dumps(s, indent=1))
         return 0
-    print(f"{'rank':>4} {'iter':>4} {'span ms':>10} {'compute':>10} {'comm':>10} {'hidden':>10} {'exposed':>10}")
+    print(f"{'rank':>4} {'iter':>4} {'span ms':>10} {'compute':>10} {'comm':>10} {'hidden':>10} {'exposed':>10}"
+          f" {'host ms':>10} {'launch':>8} {'complete':>8}")
     for pid, its in s.items():
         for it, r in its.items():
+            host = (f" {r['host_ms']:10.3f} {r['launch_ms']:8.3f} {r['completion_ms']:8.3f}" if "host_ms" in r
+                    else "")
             print(f"{pid:>4} {it:>4} {r['span_ms']:10.3f} {r['compute_busy_ms']:10.3f} {r['comm_busy_ms']:10.3f} "
-                  f"{r['comm_hidden_ms']:10.3f} {r['comm_exposed_ms']:10.3f}")
+                  f"{r['comm_hidden_ms']:10.3f} {r['comm_exposed_ms']:10.3f}{host}")
     return 0
 
 

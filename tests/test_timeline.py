@@ -49,7 +49,7 @@ def test_fsdp_timeline_two_processes(tmp_path):
     assert "compute" in names and any(n.startswith("comm: fsdp/") for n in names)
     from dlnetbench_amd.tools import plots
     drawn = plots.plot_timeline(str(out), str(tmp_path / "tl.png"))
-    assert drawn == {"comm": 2 * 11, "compute": 2 * 8} and (tmp_path / "tl.png").stat().st_size > 0
+    assert drawn == {"comm": 2 * 11, "compute": 2 * 8, "host": 2} and (tmp_path / "tl.png").stat().st_size > 0
     g = json.loads(rep.read_text())["global"]["dlnb"]["timeline"]
     assert g["events"] == len(ev) and g["truncated"] is False and g["path"] == str(out)
     s = tlt.summarize(ev)
@@ -57,6 +57,8 @@ def test_fsdp_timeline_two_processes(tmp_path):
         r = s[pid]["2"]
         assert r["comm_busy_ms"] > 0 and r["compute_busy_ms"] > 0
         assert r["comm_hidden_ms"] + r["comm_exposed_ms"] == pytest.approx(r["comm_busy_ms"])
+        # the host's view of the iteration (what the runner times) brackets the device spans
+        assert r["host_ms"] >= r["span_ms"] - 0.05 and r["launch_ms"] > -0.05 and r["completion_ms"] > -0.05
         assert r["ops"]["all_gather"]["count"] == 7 and r["ops"]["all_gather"]["bytes"] > 0
 
 
