@@ -783,15 +783,16 @@ def main() -> int:
     if world != a.gpus:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    # An iteration takes ~3 s: a collective that has not completed within
-    # 3 minutes is hung - abort it and fall back (graph retry / error key)
-    # instead of waiting out the runtime's 15-minute default.
-    os.environ.setdefault("DLNB_TIMEOUT", "180")
+    # An iteration takes ~3 s: a collective that has not completed within a
+    # minute is hung - abort it and fall back (graph retry / error key)
+    # instead of waiting out the runtime's 15-minute default. Both headline
+    # attempts hanging then cost 2 minutes of the wall budget, not 6.
+    os.environ.setdefault("DLNB_TIMEOUT", "60")
     # Rendezvous / host-barrier waits: ranks run the phases in lockstep (the
     # worst legitimate skew is a communicator setup, seconds), so a rank that
-    # waits 5 minutes for a peer means the peer failed - stop there rather than
+    # waits 2 minutes for a peer means the peer failed - stop there rather than
     # after the store's 15-minute default.
-    os.environ.setdefault("DLNB_STORE_TIMEOUT", "300")
+    os.environ.setdefault("DLNB_STORE_TIMEOUT", "120")
     # Everything below is native (HIP + RCCL from /opt/rocm); torch is not needed.
     os.environ.setdefault("DLNB_NO_TORCH", "1")
     budget = _Budget(a.wall_budget_s, a.budget_reserve_s, world, rank)
