@@ -60,7 +60,8 @@ bool gemm_shape_ok(int M, int N, int K, DType in_t);
 //       applies (>= 2 K-tiles), else 8; bf16 first the narrow-tile kernel
 //       when fewer 256 x 256 tiles than CUs leave some idle (gemm_tn_narrow);
 //   5 = one wave per SIMD, 128 x 128 of C per wave, MX MFMA with AGPR
-//       accumulators (gemm_4wave_fp8.hip; fp8, K % 256 == 0; the streaming
+//       accumulators (gemm_4wave_fp8.hip; fp8, K % 256 == 0, or bf16 with two
+//       16x16x32 MFMAs per 128-byte K-tile row, K % 128 == 0; the streaming
 //       persistent kernel when there are more tiles than CUs, 256 x 32 nf
 //       tiles when fewer square tiles than CUs leave some idle);
 //   6 = the 8-phase ping-pong schedule, 8 waves (2 per SIMD, 128 x 64 of C
@@ -85,6 +86,13 @@ bool gemm_tn_narrow(const void* A, const void* B, void* C, int M, int N, int K, 
                     DType in_t, void* stream);
 void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                        void* stream);
+// The same one-wave-per-SIMD square kernel for bf16 (K * 2 % 256 == 0).
+bool gemm_4wave_shape_ok(int M, int N, int K, DType in_t);
+void gemm_tn_4wave_bf16(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                        void* stream);
+void gemm_tn_4wave_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
+                            uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
+                            const DlSync& sync);
 void gemm_tn_4wave_fp8_deadline(const void* A, const void* B, void* C, int M, int N, int K, uint64_t ticks,
                                 uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
                                 const DlSync& sync);

@@ -30,7 +30,8 @@ class TimerSet {
   TimerSet(const TimerSet&) = delete;
   TimerSet& operator=(const TimerSet&) = delete;
   int begin(Stream& s);
-  void end(int token, Stream& s, const std::string& name);
+  // Returns the end stamp's slot (nullptr when disabled), e.g. for gap().
+  const uint64_t* end(int token, Stream& s, const std::string& name);
   // Time the stall of stream s waiting for event e (exposed latency).
   void stall(Stream& s, Event& e, const std::string& name);
   // Stamp-free variant for a wait between two compute tasks on one stream

@@ -33,11 +33,14 @@
 //     offset). Uniform loop: the last K-tiles stage / read clamped copies of
 //     the last one (never used) - or, in the streaming kernel, the next
 //     tile's first K-tiles.
-//   * Kernels: gemm_4wave_fp8_kernel<false> (a block per tile),
-//     gemm_4wave_fp8_stream_kernel<false> (persistent, a block's tiles as one
+//   * Kernels: gemm_4wave_fp8_kernel<BF, false> (a block per tile),
+//     gemm_4wave_fp8_stream_kernel<BF, false> (persistent, a block's tiles as one
 //     K-tile stream; the one-shot default with more tiles than CUs),
-//     gemm_4wave_fp8_kernel<true> (the persistent deadline compute stand-in)
-//     and gemm_4wave_fp8_stream_kernel<true> (its streaming variant, opt-in);
+//     gemm_4wave_fp8_kernel<BF, true> (the persistent deadline compute stand-in)
+//     and gemm_4wave_fp8_stream_kernel<BF, true> (its streaming variant, opt-in);
+//     BF = true: bf16 operands in the same byte layout, two 16x16x32 bf16
+//     MFMAs per 128-byte K-tile row where fp8 issues one MX MFMA (the same
+//     MFMA time per K-tile, the same LDS / staging work: round 4);
 //     gemm_4wave_narrow_kernel<NF, BF16> (256 x 32 NF tiles, bf16 or fp8, for
 //     outputs whose square tiles would leave CUs idle; see "Narrow-N tiles").
 //   * Epilogues store two adjacent fragments per 16-byte store (store_pair.hpp).
@@ -171,7 +174,7 @@ struct DeadlineF {
 // waits are 63 when after_store (the previous tile's 64 stores are younger
 // than the loads waited for and would not fit the counter), else 8 - a
 // uniform branch, not a second instantiation of the K-tile body.
-template <int PAR, bool FIRST, bool DL, bool READ7 = !FIRST, int VM = 8>
+template <bool BF, int PAR, bool FIRST, bool DL, bool READ7 = !FIRST, int VM = 8>
 __device__ __forceinline__ bool ktile(const CtxF& c, int t, int wr, int wc, int offl, int offh, FragF (&a)[8],
                                       FragF (&b)[2][8], f32x4 (&acc)[8][8], int scale, const DeadlineF& d,
                                       bool after_store = false) {
@@ -215,8 +218,13 @@ __device__ __forceinline__ bool ktile(const CtxF& c, int t, int wr, int wc, int 
       raw_barrier();
       if constexpr (DL) stop = __builtin_amdgcn_readfirstlane(d.flag[t & 1]) != 0;
     }
-    mfma<FIRST>(acc[i][j], b[PAR][j], a[i], scale);
-    mfma<FIRST>(acc[i][j + 1], b[PAR][j + 1], a[i], scale);
+    if constexpr (BF) {  // bf16: two 32-deep K-steps per 128-byte K-tile row, same time as one MX MFMA
+      mfma_bf16<FIRST>(acc[i][j], b[PAR][j], a[i]);
+      mfma_bf16<FIRST>(acc[i][j + 1], b[PAR][j + 1], a[i]);
+    } else {
+      mfma<FIRST>(acc[i][j], b[PAR][j], a[i], scale);
+      mfma<FIRST>(acc[i][j + 1], b[PAR][j + 1], a[i], scale);
+    }
     // a[7] of THIS K-tile: read here, not right after the MFMA that last read
     // the previous a[7] (its K-tile's A region is restaged only after the mid
     // barrier, which waits for this read)
@@ -286,7 +294,7 @@ __device__ __forceinline__ void store_tile(f32x4 (&acc)[8][8], __bf16* __restric
 
 // One 256 x 256 tile of C. Returns false if the deadline stopped it (no
 // store; every staged load has been waited for).
-template <bool DL>
+template <bool BF, bool DL>
 __device__ __forceinline__ bool tile4(CtxF& c, const char* __restrict__ A, const char* __restrict__ B,
                                       __bf16* __restrict__ C, int lda, int ldb, int ldc, int K, int tm, int tn,
                                       int lane, const DeadlineF& d) {
@@ -320,12 +328,12 @@ __device__ __forceinline__ bool tile4(CtxF& c, const char* __restrict__ A, const
   FragF a[8], b[2][8];
 
   prologue(c, wr, wc, offl, offh, a, b);
-  bool stop = ktile<0, true, DL>(c, 0, wr, wc, offl, offh, a, b, acc, scale, d);
+  bool stop = ktile<BF, 0, true, DL>(c, 0, wr, wc, offl, offh, a, b, acc, scale, d);
   for (int t = 1; t < nk - 1 && !stop; t += 2) {
-    stop = ktile<1, false, DL>(c, t, wr, wc, offl, offh, a, b, acc, scale, d);
-    if (!stop) stop = ktile<0, false, DL>(c, t + 1, wr, wc, offl, offh, a, b, acc, scale, d);
+    stop = ktile<BF, 1, false, DL>(c, t, wr, wc, offl, offh, a, b, acc, scale, d);
+    if (!stop) stop = ktile<BF, 0, false, DL>(c, t + 1, wr, wc, offl, offh, a, b, acc, scale, d);
   }
-  if (!stop) stop = ktile<1, false, DL>(c, nk - 1, wr, wc, offl, offh, a, b, acc, scale, d);
+  if (!stop) stop = ktile<BF, 1, false, DL>(c, nk - 1, wr, wc, offl, offh, a, b, acc, scale, d);
   wait_vm<0>();  // the clamped staging copies (or, stopped, everything in flight)
   // Every wave passes this barrier before the next tile's prologue restages
   // K-tile 1's buffer, whose last reads (the clamped K-tile nk) were this
@@ -351,7 +359,7 @@ __device__ __forceinline__ void tile_coords(int bid, int nt_m, int nt_n, int gro
 // compute with gemm_tn_deadline's contract (kernels.hip): grid <= resident
 // blocks walks the tiles round-robin and stops min(ticks, slice_end) after t0,
 // agreed per epoch through *slot.
-template <bool DL>
+template <bool BF, bool DL>
 __global__ void __launch_bounds__(256, 1)
     gemm_4wave_fp8_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
                           int K, int lda, int ldb, int ldc, int group, uint64_t* __restrict__ slot, uint32_t epoch,
@@ -375,12 +383,12 @@ __global__ void __launch_bounds__(256, 1)
   int tm, tn;
   if constexpr (!DL) {
     tile_coords(xcd_remap(blockIdx.x, T), nt_m, nt_n, group, tm, tn);
-    tile4<false>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d);
+    tile4<BF, false>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d);
   } else {
     if (tid == 0) d.t0 = dl::agree_t0(slot, epoch, ticks, sync);  // only thread 0 reads the clock
     for (int round = 0;; ++round) {
       tile_coords(xcd_remap((blockIdx.x + round * gridDim.x) % T, T), nt_m, nt_n, group, tm, tn);
-      if (!tile4<true>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d)) return;
+      if (!tile4<BF, true>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d)) return;
     }
   }
 }
@@ -400,7 +408,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const char* base, in
                                            0x7ffffff0, 0x00020000);
 }
 
-template <bool DL>
+template <bool BF, bool DL>
 __global__ void __launch_bounds__(256, 1)
     gemm_4wave_fp8_stream_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C,
                                  int M, int N, int K, int lda, int ldb, int ldc, int group, uint64_t* __restrict__ slot,
@@ -455,12 +463,12 @@ __global__ void __launch_bounds__(256, 1)
   bool first = true, stop = false;
   for (;;) {
     // (the first tile re-reads the a[7] its prologue read: same data)
-    stop = ktile<0, true, DL, true, -1>(c, 0, wr, wc, offl, offh, a, b, acc, scale, d, !first);
+    stop = ktile<BF, 0, true, DL, true, -1>(c, 0, wr, wc, offl, offh, a, b, acc, scale, d, !first);
     for (int t = 1; t < nk - 1 && !stop; t += 2) {
-      stop = ktile<1, false, DL>(c, t, wr, wc, offl, offh, a, b, acc, scale, d);
-      if (!stop) stop = ktile<0, false, DL>(c, t + 1, wr, wc, offl, offh, a, b, acc, scale, d);
+      stop = ktile<BF, 1, false, DL>(c, t, wr, wc, offl, offh, a, b, acc, scale, d);
+      if (!stop) stop = ktile<BF, 0, false, DL>(c, t + 1, wr, wc, offl, offh, a, b, acc, scale, d);
     }
-    if (!stop) stop = ktile<1, false, DL>(c, nk - 1, wr, wc, offl, offh, a, b, acc, scale, d);
+    if (!stop) stop = ktile<BF, 1, false, DL>(c, nk - 1, wr, wc, offl, offh, a, b, acc, scale, d);
     if (DL && stop) break;  // partial tile: the stand-in result is not needed
     store_tile(acc, C, ldc, tm, tn, wr, wc, r16, h);
     if (!c.has_next) break;
@@ -763,10 +771,14 @@ bool gemm_tn_narrow(const void* A, const void* B, void* C, int M, int N, int K, 
   return true;
 }
 
-void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
-                       void* stream) {
-  DLNB_REQUIRE(gemm_4wave_fp8_shape_ok(M, N, K, DType::FP8_E4M3),
-               "gemm 4-wave fp8: unsupported shape M=" << M << " N=" << N << " K=" << K);
+namespace {
+
+// The square one-wave-per-SIMD kernels for either dtype: strides and K go in
+// as bytes (the staging and K-tile arithmetic work in bytes; bf16 runs two
+// 32-deep MFMAs per 128-byte K-tile row where fp8 runs one 128-deep MX MFMA).
+template <bool BF>
+void launch_4wave(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, void* stream) {
+  constexpr int esz = BF ? 2 : 1;
   const int tiles = (M / kT) * (N / kT);
   constexpr int group = 8;  // M-tiles sharing B panels in L2 (4 / 8 / 16 / 32 measured: 8 best)
   // more tiles than CUs: the streaming persistent kernel, one block per CU
@@ -775,37 +787,73 @@ void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int 
     int dev = 0;
     return hipGetDevice(&dev) == hipSuccess ? num_cus(dev) : 256;
   }();
+  auto* a = static_cast<const char*>(A);
+  auto* b = static_cast<const char*>(B);
+  auto* c = static_cast<__bf16*>(C);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (tiles > cus)
+    hipLaunchKernelGGL((gemm_4wave_fp8_stream_kernel<BF, false>), cus, 256, 0, st, a, b, c, M, N, K * esz,
+                       lda * esz, ldb * esz, ldc, group, nullptr, 0u, 0ull, 0ull, DlSync());
+  else
+    hipLaunchKernelGGL((gemm_4wave_fp8_kernel<BF, false>), tiles, 256, 0, st, a, b, c, M, N, K * esz, lda * esz,
+                       ldb * esz, ldc, group, nullptr, 0u, 0ull, 0ull, DlSync());
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) DLNB_THROW("gemm 4-wave launch failed: " << hipGetErrorString(e));
+}
+
+}  // namespace
+
+bool gemm_4wave_shape_ok(int M, int N, int K, DType in_t) {
+  const size_t kb = static_cast<size_t>(K) * dtype_size(in_t);
+  return gemm_shape_ok(M, N, K, in_t) && kb % 256 == 0 && kb >= 256;
+}
+
+void gemm_tn_4wave_fp8(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                       void* stream) {
+  DLNB_REQUIRE(gemm_4wave_fp8_shape_ok(M, N, K, DType::FP8_E4M3),
+               "gemm 4-wave fp8: unsupported shape M=" << M << " N=" << N << " K=" << K);
   // A narrower tile when it saves rounds of tile work: fewer square tiles than
   // CUs (the ViT-H FFN down projection 8192 x 1280: 160 square tiles, 256 of
   // 256 x 160) or a partial last round (gemm_narrow_nf).
   if (gemm_tn_narrow(A, B, C, M, N, K, lda, ldb, ldc, DType::FP8_E4M3, stream)) return;
-  if (tiles > cus) {
-    hipLaunchKernelGGL(gemm_4wave_fp8_stream_kernel<false>, cus, 256, 0, static_cast<hipStream_t>(stream),
-                       static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K,
-                       lda, ldb, ldc, group, nullptr, 0u, 0ull, 0ull, DlSync());
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) DLNB_THROW("gemm 4-wave fp8 stream launch failed: " << hipGetErrorString(e));
-    return;
-  }
-  hipLaunchKernelGGL(gemm_4wave_fp8_kernel<false>, tiles, 256, 0, static_cast<hipStream_t>(stream),
-                     static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, lda,
-                     ldb, ldc, group, nullptr, 0u, 0ull, 0ull, DlSync());
+  launch_4wave<false>(A, B, C, M, N, K, lda, ldb, ldc, stream);
+}
+
+void gemm_tn_4wave_bf16(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                        void* stream) {
+  DLNB_REQUIRE(gemm_4wave_shape_ok(M, N, K, DType::BF16),
+               "gemm 4-wave bf16: unsupported shape M=" << M << " N=" << N << " K=" << K);
+  launch_4wave<true>(A, B, C, M, N, K, lda, ldb, ldc, stream);
+}
+
+void gemm_tn_4wave_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
+                            uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
+                            const DlSync& sync) {
+  DLNB_REQUIRE(gemm_4wave_shape_ok(M, N, K, in_t) && in_t != DType::FP16,
+               "gemm 4-wave deadline: unsupported shape");
+  // The per-tile kernel. (Its streaming twin ran +5 % MFMA per clock at a 5 %
+  // lower, power-capped clock on the 224 CUs - the same 2620-2630 TF/s - so
+  // it was not kept as a deadline kernel: profiles/gemm_deadline_stream_r2.md.)
+  const int esz = static_cast<int>(dtype_size(in_t));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  auto* a = static_cast<const char*>(A);
+  auto* b = static_cast<const char*>(B);
+  auto* c = static_cast<__bf16*>(C);
+  if (in_t == DType::BF16)
+    hipLaunchKernelGGL((gemm_4wave_fp8_kernel<true, true>), grid, 256, 0, st, a, b, c, M, N, K * esz, K * esz,
+                       K * esz, N, 8, slot, epoch, ticks, slice_end, sync);
+  else
+    hipLaunchKernelGGL((gemm_4wave_fp8_kernel<false, true>), grid, 256, 0, st, a, b, c, M, N, K, K, K, N, 8, slot,
+                       epoch, ticks, slice_end, sync);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) DLNB_THROW("gemm 4-wave fp8 launch failed: " << hipGetErrorString(e));
+  if (e != hipSuccess) DLNB_THROW("gemm 4-wave deadline launch failed: " << hipGetErrorString(e));
 }
 
 void gemm_tn_4wave_fp8_deadline(const void* A, const void* B, void* C, int M, int N, int K, uint64_t ticks,
                                 uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
                                 const DlSync& sync) {
   DLNB_REQUIRE(gemm_4wave_fp8_shape_ok(M, N, K, DType::FP8_E4M3), "gemm 4-wave fp8 deadline: unsupported shape");
-  // The per-tile kernel. (Its streaming twin ran +5 % MFMA per clock at a 5 %
-  // lower, power-capped clock on the 224 CUs - the same 2620-2630 TF/s - so
-  // it was not kept as a deadline kernel: profiles/gemm_deadline_stream_r2.md.)
-  hipLaunchKernelGGL(gemm_4wave_fp8_kernel<true>, grid, 256, 0, static_cast<hipStream_t>(stream),
-                     static_cast<const char*>(A), static_cast<const char*>(B), static_cast<__bf16*>(C), M, N, K, K, K,
-                     N, 8, slot, epoch, ticks, slice_end, sync);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) DLNB_THROW("gemm 4-wave fp8 deadline launch failed: " << hipGetErrorString(e));
+  gemm_tn_4wave_deadline(A, B, C, M, N, K, DType::FP8_E4M3, ticks, slot, epoch, grid, stream, slice_end, sync);
 }
 
 }  // namespace kernels

@@ -551,6 +551,10 @@ void gemm_tn(const void* A, const void* B, void* C, int M, int N, int K, int lda
     gemm_tn_4wave_fp8(A, B, C, M, N, K, lda, ldb, ldc, stream);
     return;
   }
+  if (variant == 5 && in_t == DType::BF16 && gemm_4wave_shape_ok(M, N, K, in_t)) {
+    gemm_tn_4wave_bf16(A, B, C, M, N, K, lda, ldb, ldc, stream);
+    return;
+  }
   if ((variant == 5 || variant == 6) && gemm_8phase_shape_ok(M, N, K, in_t)) {
     gemm_tn_8phase(A, B, C, M, N, K, lda, ldb, ldc, in_t, stream);
     return;
@@ -566,6 +570,13 @@ void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K
   // fp8: the one-wave-per-SIMD MX kernel where it applies (2665 vs ~2180 TF/s sustained)
   if (gemm_4wave_fp8_shape_ok(M, N, K, in_t)) {
     gemm_tn_4wave_fp8_deadline(A, B, C, M, N, K, ticks, slot, epoch, grid, stream, slice_end, sync);
+    return;
+  }
+  // bf16: DLNB_DEADLINE_BF16=4wave picks the one-wave-per-SIMD kernel (A/B;
+  // read at every launch so one process can compare both)
+  const bool bf16_4wave = in_t == DType::BF16 && env_or("DLNB_DEADLINE_BF16", "8phase") == "4wave";
+  if (in_t == DType::BF16 && bf16_4wave && gemm_4wave_shape_ok(M, N, K, in_t)) {
+    gemm_tn_4wave_deadline(A, B, C, M, N, K, in_t, ticks, slot, epoch, grid, stream, slice_end, sync);
     return;
   }
   if (gemm_8phase_shape_ok(M, N, K, in_t)) {

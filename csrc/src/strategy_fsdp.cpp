@@ -196,6 +196,7 @@ class Fsdp : public Strategy {
     Context& ctx = *ctx_;
     const DType t = ctx.wire;
     prev_start_ = nullptr;
+    tail_end_ = nullptr;
 
     ComputeEngine& ce = *ctx.compute;
     auto gather = [&](int u, Event& done, bool first, int gate) {
@@ -255,7 +256,7 @@ class Fsdp : public Strategy {
       rs_stream_->wait(*bwd_done_[u]);
       int tk = timers_->begin(*rs_stream_);
       rs_comm_->reduce_scatter(full_grad_[u & 1].data(), grads_[u].data(), shard_[u], t, *rs_stream_);
-      timers_->end(tk, *rs_stream_, "reduce_scatter");
+      tail_end_ = timers_->end(tk, *rs_stream_, "reduce_scatter");
       if (gated_ && u >= 2) ce.signal(*rs_stream_, g_rs_[u]);  // RS(u) gates bwd(u - 2)
       rs_stream_->record(*rs_done_[u]);
       if (reference_) compute_->wait(*rs_done_[u]);  // blocking Reduce_Scatter_block (fsdp.cpp:124)
@@ -263,13 +264,22 @@ class Fsdp : public Strategy {
         ar_stream_->wait(*rs_done_[u]);
         int ta = timers_->begin(*ar_stream_);
         ar_comm_->all_reduce(grads_[u].data(), grads_[u].data(), shard_[u], t, *ar_stream_);
-        timers_->end(ta, *ar_stream_, "allreduce_time");
+        tail_end_ = timers_->end(ta, *ar_stream_, "allreduce_time");
         ar_stream_->record(*ar_done_[u]);
       }
     }
     // ---- tail: exposed reduce-scatter / replica all-reduce
     Event& tail = R_ > 1 ? *ar_done_[0] : *rs_done_[0];
-    timers_->stall(*compute_, tail, "barrier");
+    if (gated_ && !ctx.opt.optimizer && tail_end_ && prev_start_) {
+      // nothing runs on the compute stream after the last backward: the
+      // exposed tail is the last collective's end stamp minus the last
+      // deadline, with no wait + stamp pair (a cross-queue hop and two
+      // kernels) at the end of the iteration; the iteration still ends when
+      // every stream has (graph join / synchronize)
+      timers_->gap(prev_start_, prev_ticks_, tail_end_, "barrier");
+    } else {
+      timers_->stall(*compute_, tail, "barrier");
+    }
     if (ctx.opt.optimizer) {
       if (R_ > 1)
         for (int u = 1; u < U_; ++u) compute_->wait(*ar_done_[u]);
@@ -351,6 +361,7 @@ class Fsdp : public Strategy {
   std::vector<std::unique_ptr<Event>> ag_f_, fwd_done_, ag_b_, bwd_done_, rs_done_, ar_done_;
   std::vector<CommStat> stats_;
   const uint64_t* prev_start_ = nullptr;  // start stamp of the previous compute task
+  const uint64_t* tail_end_ = nullptr;    // end stamp of the iteration's last collective
   uint64_t prev_ticks_ = 0;
 };
 

@@ -20,12 +20,13 @@ int TimerSet::begin(Stream& s) {
   return idx;
 }
 
-void TimerSet::end(int token, Stream& s, const std::string& name) {
-  if (!enabled_ || token < 0) return;
+const uint64_t* TimerSet::end(int token, Stream& s, const std::string& name) {
+  if (!enabled_ || token < 0) return nullptr;
   DLNB_REQUIRE(next_ < cap_, "too many timer stamps in one iteration");
   int idx = static_cast<int>(next_++);
   dev_.stamp(s, stamps_ + idx);
   pending_.push_back(Pending{token, idx, name});
+  return stamps_ + idx;
 }
 
 void TimerSet::stall(Stream& s, Event& e, const std::string& name) {

@@ -26,9 +26,9 @@ def assert_close_bf16_out(c, ref):
     assert worst <= 0, f"max excess {worst}, max err {err.max().item()}, rms {ref.pow(2).mean().sqrt().item()}"
 
 
-# gemm_tn variants (kernels.hpp): 0 default (bf16: narrow tiles when square ones leave CUs idle), 5 4-wave MX
-# (fp8), 6 8-phase, 8 8-wave
-@pytest.mark.parametrize("waves", [0, 6, 8])
+# gemm_tn variants (kernels.hpp): 0 default (bf16: narrow tiles when square ones leave CUs idle), 5 4-wave (MX fp8,
+# or bf16 two 16x16x32 MFMAs per K-tile row; K % 128 == 0, else it falls through to 6), 6 8-phase, 8 8-wave
+@pytest.mark.parametrize("waves", [0, 5, 6, 8])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (256, 512, 128), (512, 512, 64), (768, 256, 128),
                                    (512, 256, 1024), (768, 1280, 640), (2048, 1024, 4096), (256, 256, 192),
                                    (512, 768, 320)])
@@ -226,13 +226,17 @@ DEADLINE_CASES = [
 ]
 
 
+@pytest.mark.parametrize("bf16_kernel", ["8phase", "4wave"])
 @pytest.mark.parametrize("dtype,M,N,K,grid", DEADLINE_CASES)
-def test_deadline_gemm_numerics(M, N, K, grid, dtype):
+def test_deadline_gemm_numerics(M, N, K, grid, dtype, bf16_kernel, monkeypatch):
     """The persistent deadline GEMM (the bench's compute), every kernel the shapes select. With a deadline
     long enough for several passes every tile of C holds a complete product: each one equals A.B^T.
     Small grids make every block cross many tile boundaries (grid 0 = the default, CUs - 32)."""
     if dtype == "fp8" and not hasattr(torch, "float8_e4m3fn"):
         pytest.skip("torch without float8")
+    if bf16_kernel == "4wave" and (dtype != "bf16" or K % 128):
+        pytest.skip("the bf16 one-wave-per-SIMD deadline kernel: bf16, K % 128 == 0")
+    monkeypatch.setenv("DLNB_DEADLINE_BF16", bf16_kernel)
     g = torch.Generator(device="cuda").manual_seed(M * 3 + N + K)
     a = torch.randn(M, K, device="cuda", generator=g)
     b = torch.randn(N, K, device="cuda", generator=g)
