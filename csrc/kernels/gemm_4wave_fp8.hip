@@ -152,6 +152,15 @@ __device__ __forceinline__ void mfma_bf16(f32x4& acc, const FragF& b, const Frag
   asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b.hi), "v"(a.hi));
 }
 
+// One 32-deep K-step of a bf16 fragment pair (the lo or hi chunks).
+template <bool ZERO>
+__device__ __forceinline__ void mfma_bf16_step(f32x4& acc, const i32x4& b, const i32x4& a) {
+  if constexpr (ZERO)
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc) : "v"(b), "v"(a));
+  else
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
+
 // Deadline state (DL kernels, the compute stand-in): the clock is read at the
 // start of every K-tile and thread 0 writes the stop decision into an LDS flag
 // (typed LDS pointer: a generic one becomes a FLAT store that waits vmcnt(0))
@@ -218,9 +227,14 @@ __device__ __forceinline__ bool ktile(const CtxF& c, int t, int wr, int wc, int 
       raw_barrier();
       if constexpr (DL) stop = __builtin_amdgcn_readfirstlane(d.flag[t & 1]) != 0;
     }
-    if constexpr (BF) {  // bf16: two 32-deep K-steps per 128-byte K-tile row, same time as one MX MFMA
-      mfma_bf16<FIRST>(acc[i][j], b[PAR][j], a[i]);
-      mfma_bf16<FIRST>(acc[i][j + 1], b[PAR][j + 1], a[i]);
+    if constexpr (BF) {
+      // bf16: two 32-deep K-steps per 128-byte K-tile row (lo, hi chunks),
+      // together the time of one MX MFMA; the two accumulators alternate so
+      // no MFMA waits on the one just issued into the same accumulator
+      mfma_bf16_step<FIRST>(acc[i][j], b[PAR][j].lo, a[i].lo);
+      mfma_bf16_step<FIRST>(acc[i][j + 1], b[PAR][j + 1].lo, a[i].lo);
+      mfma_bf16_step<false>(acc[i][j], b[PAR][j].hi, a[i].hi);
+      mfma_bf16_step<false>(acc[i][j + 1], b[PAR][j + 1].hi, a[i].hi);
     } else {
       mfma<FIRST>(acc[i][j], b[PAR][j], a[i], scale);
       mfma<FIRST>(acc[i][j + 1], b[PAR][j + 1], a[i], scale);
