@@ -1006,6 +1006,10 @@ def main() -> int:
             b = _backend_key(blk.get("backend") if key != "headline" else (blk.get("config") or {}).get("backend"))
             if b in ver and not ver[b] and "error" not in blk:
                 blk["error"] = f"{b} exactness failed (see exact_detail); timed anyway"
+    elif exact:
+        # the pass ran but did not complete (timeout, crash, budget): nothing is verified
+        out["verified"] = {b: None for b in _exact_backends(a).split(",")}
+        out["verified_note"] = "exactness pass did not complete: " + json.dumps(exact.get("exact_detail"))[:200]
     else:
         out["verified"] = None  # no exactness pass (N = 1: collectives are local copies)
     out.update(extra)
