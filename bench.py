@@ -455,6 +455,19 @@ def _model_fit(a: argparse.Namespace, world: int, extra: Dict[str, Any]) -> Opti
         return {"error": str(e)[:300]}
 
 
+def _rank_ms(d: dict) -> Optional[Dict[str, Any]]:
+    """Mean iteration time of each rank (its own host timer, ms): min / max and the slowest rank."""
+    means = {}
+    for r in d.get("ranks", []):
+        v = r.get("runtime") or r.get("runtimes")
+        if v:
+            means[int(r.get("rank", len(means)))] = sum(v) / len(v) * 1e3
+    if not means:
+        return None
+    slow = max(means, key=means.get)
+    return {"min": round(min(means.values()), 3), "max": round(means[slow], 3), "slowest_rank": slow}
+
+
 def _per_run_ms(d: dict) -> list:
     """Every timed iteration's time (ms): the slowest rank's per run."""
     return [round(x * 1e3, 3) for x in d["global"]["dlnb"]["iteration"].get("per_run_max_s", [])]
@@ -963,6 +976,8 @@ def main() -> int:
             "exposed_comm_ms": round(exposed, 3),
             "median_ms": round(it["median_ms"], 3),
             "per_run_ms": _per_run_ms(doc),
+            # every rank's mean iteration (ms): at N > 1 the straggler and the spread behind the max
+            "rank_ms": _rank_ms(doc),
             "baseline_ms": BASELINE_MS,
             "baseline_note": "derived reference floor (BASELINE.md C2: fwd+bwd of llama3_8b_16_bfloat16); lower is better",
             "rccl_cta_budget": g["dlnb"].get("rccl_cta_budget"),

@@ -46,6 +46,7 @@ def test_bench_torchrun_cpu(n, tmp_path):
     assert o["config"]["global_batch"] == 8 * n
     assert o["higher_is_better"] is False and o["scaling"] == "weak"
     assert o["ms_per_step"] == o["value"] > 0
+    assert len(o["per_run_ms"]) == 2 and 0 < o["rank_ms"]["min"] <= o["rank_ms"]["max"] and o["rank_ms"]["slowest_rank"] in range(n)
     assert o["effective_busbw_GBps"]["allgather"] > 0 and o["effective_busbw_GBps"]["reduce_scatter"] > 0
     c5 = o["comm_bound"]
     assert "error" not in c5, c5
