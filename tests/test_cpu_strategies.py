@@ -527,6 +527,8 @@ def test_stream_task_failure_raises_in_process_and_next_run_works(data_dir):
     from dlnetbench_amd import engine
     from dlnetbench_amd._native import NativeError
     kw = dict(base_path=data_dir, backend="cpu", compute="sleep", warmup=1, runs=3, silent=True)
+    # the same job before the fault, in this process and under the same host load: the yardstick for "normal"
+    before = engine.run("fsdp", "tiny_dense_8_bfloat16", 4, 1, **kw)["global"]["dlnb"]["iteration"]
     os.environ["DLNB_INJECT_FAULT"] = "rank=0,iter=1,mode=task"
     try:
         with pytest.raises(NativeError, match="injected fault in a stream task"):
@@ -536,5 +538,7 @@ def test_stream_task_failure_raises_in_process_and_next_run_works(data_dir):
     t0 = time.time()
     d = engine.run("fsdp", "tiny_dense_8_bfloat16", 4, 1, **kw)
     it = d["global"]["dlnb"]["iteration"]
-    assert it["compute_floor_ms"] <= it["timed_ms_per_iter"] < it["compute_floor_ms"] * 3 + 10  # loaded CI host
+    assert it["compute_floor_ms"] <= it["timed_ms_per_iter"]
+    # no leftover of the failed job slows it: within 2x + 20 ms of the clean run (a loaded CI host, e.g. pytest -n)
+    assert it["timed_ms_per_iter"] < 2 * before["timed_ms_per_iter"] + 20
     assert time.time() - t0 < 20
