@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
 import statistics
 
 
@@ -31,6 +32,9 @@ def main(argv=None) -> int:
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--variants", default=None, help="comma list of gemm_tn variants (default: 0,8 bf16; 0,6 fp8)")
+    ap.add_argument("--ab", default=None, metavar="ENV=v1,v2",
+                    help="run every variant once per value of a kernel environment knob read at launch "
+                         "(e.g. DLNB_G4_OPT=0,3), interleaved; keys v<n>_<value>_tflops_*")
     a = ap.parse_args(argv)
     dt = torch.bfloat16 if a.dtype == "bf16" else torch.float8_e4m3fn
     for shp in a.shapes.split(","):
@@ -44,10 +48,20 @@ def main(argv=None) -> int:
 
         variants = [int(v) for v in (a.variants or ("0,8" if a.dtype == "bf16" else "0,6")).split(",")]
 
-        def mk(v):
-            return lambda: gemm.gemm_tn(A, B, C, waves=v)
+        def mk(v, env=None):
+            if env is None:
+                return lambda: gemm.gemm_tn(A, B, C, waves=v)
 
-        fns = [(f"v{v}", mk(v)) for v in variants]
+            def fn():
+                os.environ[env[0]] = env[1]  # putenv: the launch reads it
+                gemm.gemm_tn(A, B, C, waves=v)
+            return fn
+
+        if a.ab:
+            knob, vals = a.ab.split("=", 1)
+            fns = [(f"v{v}_{x}", mk(v, (knob, x))) for v in variants for x in vals.split(",")]
+        else:
+            fns = [(f"v{v}", mk(v)) for v in variants]
         if dt == torch.bfloat16:
             def ref():
                 torch.matmul(A, B.t(), out=C)

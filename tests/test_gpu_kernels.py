@@ -116,6 +116,31 @@ def test_gemm_fp8_many_tiles(M, N, K):
     assert_close_bf16_out(c, a.float() @ b.float().t())
 
 
+@pytest.mark.parametrize("opt", [0, 1, 2, 3])
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+@pytest.mark.parametrize("M,N,Kb", [(512, 512, 256), (512, 768, 512), (768, 512, 768), (1024, 512, 1024),
+                                    (512, 512, 5120), (8192, 8192, 512), (4096, 4352, 1280), (6144, 4096, 2048)])
+def test_gemm_4wave_schedule_options(M, N, Kb, dtype, opt, monkeypatch):
+    """The one-wave-per-SIMD square kernels under every schedule option (gemm_4wave_fp8.hip OPT, DLNB_G4_OPT:
+    the clamp-free main K-loop, bf16 row-ordered K-steps): K from the 2-K-tile minimum (no main-loop pair)
+    through 4 (the last pair only), 6, 8 and 40 K-tiles; fewer tiles than CUs (a block per tile) and more (the
+    streaming kernel, whose last K-tiles stage the next tile's). Kb = K in bytes."""
+    if dtype == "fp8" and not hasattr(torch, "float8_e4m3fn"):
+        pytest.skip("torch without float8")
+    monkeypatch.setenv("DLNB_G4_OPT", str(opt))
+    monkeypatch.setenv("DLNB_GEMM_NARROW_NF", "8")  # square tiles only: this test is about those kernels
+    K = Kb // 2 if dtype == "bf16" else Kb
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + opt)
+    a = torch.randn(M, K, device="cuda", generator=g) * 0.5
+    b = torch.randn(N, K, device="cuda", generator=g) * 0.5
+    dt = torch.bfloat16 if dtype == "bf16" else torch.float8_e4m3fn
+    a, b = a.to(dt), b.to(dt)
+    c = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+    gemm.gemm_tn(a, b, c, waves=5)
+    torch.cuda.synchronize()
+    assert_close_bf16_out(c, a.float() @ b.float().t())
+
+
 @pytest.mark.parametrize("cpad", [256, 4])
 @pytest.mark.parametrize("dtype,waves", [("bf16", 0), ("bf16", 6), ("bf16", 8), ("fp8", 0), ("fp8", 6), ("fp8", 8)])
 def test_gemm_strided_operands(dtype, waves, cpad):
@@ -226,17 +251,22 @@ DEADLINE_CASES = [
 ]
 
 
+@pytest.mark.parametrize("g4_opt", [0, 3])
 @pytest.mark.parametrize("bf16_kernel", ["8phase", "4wave"])
 @pytest.mark.parametrize("dtype,M,N,K,grid", DEADLINE_CASES)
-def test_deadline_gemm_numerics(M, N, K, grid, dtype, bf16_kernel, monkeypatch):
+def test_deadline_gemm_numerics(M, N, K, grid, dtype, bf16_kernel, g4_opt, monkeypatch):
     """The persistent deadline GEMM (the bench's compute), every kernel the shapes select. With a deadline
     long enough for several passes every tile of C holds a complete product: each one equals A.B^T.
-    Small grids make every block cross many tile boundaries (grid 0 = the default, CUs - 32)."""
+    Small grids make every block cross many tile boundaries (grid 0 = the default, CUs - 32). g4_opt: the
+    one-wave-per-SIMD kernel's schedule options (DLNB_G4_OPT)."""
     if dtype == "fp8" and not hasattr(torch, "float8_e4m3fn"):
         pytest.skip("torch without float8")
     if bf16_kernel == "4wave" and (dtype != "bf16" or K % 128):
         pytest.skip("the bf16 one-wave-per-SIMD deadline kernel: bf16, K % 128 == 0")
+    if g4_opt and not (bf16_kernel == "4wave" or (dtype == "fp8" and K % 256 == 0)):
+        pytest.skip("schedule options: the one-wave-per-SIMD kernels only")
     monkeypatch.setenv("DLNB_DEADLINE_BF16", bf16_kernel)
+    monkeypatch.setenv("DLNB_G4_OPT", str(g4_opt))
     g = torch.Generator(device="cuda").manual_seed(M * 3 + N + K)
     a = torch.randn(M, K, device="cuda", generator=g)
     b = torch.randn(N, K, device="cuda", generator=g)
