@@ -117,8 +117,10 @@ __device__ __forceinline__ void stage_piece(const CtxF& c, int kt, int op, int p
 // The same piece for a K-tile known to be in range (kt <= last_kt, buffer
 // parity PAR at compile time): no clamp, no next-tile select, a constant LDS
 // buffer - two scalar ops per piece (M0, soffset) instead of a dozen compares
-// and selects per K-tile (OPT_MAIN; profiles/gemm_instmix_r4.md: the fp8
-// kernel issued 38 % more SALU per MFMA than the vendor's).
+// and selects per K-tile (the main K-loop, ktiles_rest; round 4:
+// profiles/gemm_instmix_r4.md measured 38 % more SALU per MFMA than the
+// vendor's fp8 kernel, this cut the loop's 67 SALU per K-tile to 32 and gave
+// +2-3 % at long K, profiles/gemm_g4_main_r4.md).
 template <int PAR>
 __device__ __forceinline__ void stage_piece_main(const CtxF& c, int kt, int op, int p) {
   const int half = p >> 2, i = p & 3;
@@ -127,14 +129,6 @@ __device__ __forceinline__ void stage_piece_main(const CtxF& c, int kt, int op, 
   __builtin_amdgcn_raw_ptr_buffer_load_lds(op ? c.rb : c.ra, (lds_ptr_t)lds, 16, op ? c.voffB : c.voffA,
                                            kt * kRB + (half * 128 + i * 32) * ld, 0, 0);
 }
-
-// Schedule options of the square kernels (template OPT, host: DLNB_G4_OPT):
-//   OPT_MAIN    the K-loop body without the last K-tile pair stages with
-//               stage_piece_main; buffers addressed by the compile-time parity
-//   OPT_ROWS    bf16: a row's 16 MFMAs as its 8 lo K-steps, then its 8 hi ones
-//               (same-accumulator MFMAs 8 apart instead of 2: no s_nop between
-//               them)
-constexpr int OPT_MAIN = 1, OPT_ROWS = 2;
 
 // One 16-B half of fragment f (rows 16 f + r16 of a half-tile): part 0 = K
 // chunk h, part 1 = chunk h + 4 (lane offsets offl / offh).
@@ -205,8 +199,8 @@ struct DeadlineF {
 // waits are 63 when after_store (the previous tile's 64 stores are younger
 // than the loads waited for and would not fit the counter), else 8 - a
 // uniform branch, not a second instantiation of the K-tile body.
-// OPT: schedule options (OPT_ROWS); MAIN: t + 2 <= last_kt (stage_piece_main).
-template <bool BF, int PAR, bool FIRST, bool DL, bool READ7 = !FIRST, int VM = 8, int OPT = 0, bool MAIN = false>
+// MAIN: t + 2 <= last_kt (stage_piece_main, compile-time buffers).
+template <bool BF, int PAR, bool FIRST, bool DL, bool READ7 = !FIRST, int VM = 8, bool MAIN = false>
 __device__ __forceinline__ bool ktile(const CtxF& c, int t, int wr, int wc, int offl, int offh, FragF (&a)[8],
                                       FragF (&b)[2][8], f32x4 (&acc)[8][8], int scale, const DeadlineF& d,
                                       bool after_store = false) {
@@ -251,20 +245,12 @@ __device__ __forceinline__ bool ktile(const CtxF& c, int t, int wr, int wc, int 
       raw_barrier();
       if constexpr (DL) stop = __builtin_amdgcn_readfirstlane(d.flag[t & 1]) != 0;
     }
-    if constexpr (BF && (OPT & OPT_ROWS)) {
-      // row i over its 4 pairs: lo K-steps of columns 0-3, 4-7, then hi ones
-      const int q = g & 3, j0 = (q & 1) * 4;
-      if (q < 2) {
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) mfma_bf16_step<FIRST>(acc[i][j0 + jj], b[PAR][j0 + jj].lo, a[i].lo);
-      } else {
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) mfma_bf16_step<false>(acc[i][j0 + jj], b[PAR][j0 + jj].hi, a[i].hi);
-      }
-    } else if constexpr (BF) {
+    if constexpr (BF) {
       // bf16: two 32-deep K-steps per 128-byte K-tile row (lo, hi chunks),
       // together the time of one MX MFMA; the two accumulators alternate so
-      // no MFMA waits on the one just issued into the same accumulator
+      // no MFMA waits on the one just issued into the same accumulator (a
+      // row's 8 lo K-steps before its 8 hi ones, same-accumulator MFMAs 8
+      // apart with no s_nop between them, measured the same, round 4)
       mfma_bf16_step<FIRST>(acc[i][j], b[PAR][j].lo, a[i].lo);
       mfma_bf16_step<FIRST>(acc[i][j + 1], b[PAR][j + 1].lo, a[i].lo);
       mfma_bf16_step<false>(acc[i][j], b[PAR][j].hi, a[i].hi);
@@ -312,25 +298,23 @@ __device__ __forceinline__ bool ktile(const CtxF& c, int t, int wr, int wc, int 
   return stop;
 }
 
-// K-tiles 1 .. nk - 1 of a tile (nk even), after its K-tile 0. OPT_MAIN: the
-// pairs whose staging stays inside the tile (t + 3 <= nk - 1) run the
-// clamp-free body; the last pair and K-tile keep the general one.
-template <bool BF, bool DL, int OPT>
+// K-tiles 1 .. nk - 1 of a tile (nk even), after its K-tile 0: the pairs
+// whose staging stays inside the tile (t + 3 <= nk - 1) run the clamp-free
+// body; the last pair and K-tile keep the general one.
+template <bool BF, bool DL>
 __device__ __forceinline__ bool ktiles_rest(const CtxF& c, int nk, int wr, int wc, int offl, int offh, FragF (&a)[8],
                                             FragF (&b)[2][8], f32x4 (&acc)[8][8], int scale, const DeadlineF& d,
                                             bool stop) {
   int t = 1;
-  if constexpr ((OPT & OPT_MAIN) != 0) {
-    for (; t < nk - 3 && !stop; t += 2) {
-      stop = ktile<BF, 1, false, DL, true, 8, OPT, true>(c, t, wr, wc, offl, offh, a, b, acc, scale, d);
-      if (!stop) stop = ktile<BF, 0, false, DL, true, 8, OPT, true>(c, t + 1, wr, wc, offl, offh, a, b, acc, scale, d);
-    }
+  for (; t < nk - 3 && !stop; t += 2) {
+    stop = ktile<BF, 1, false, DL, true, 8, true>(c, t, wr, wc, offl, offh, a, b, acc, scale, d);
+    if (!stop) stop = ktile<BF, 0, false, DL, true, 8, true>(c, t + 1, wr, wc, offl, offh, a, b, acc, scale, d);
   }
   for (; t < nk - 1 && !stop; t += 2) {
-    stop = ktile<BF, 1, false, DL, true, 8, OPT>(c, t, wr, wc, offl, offh, a, b, acc, scale, d);
-    if (!stop) stop = ktile<BF, 0, false, DL, true, 8, OPT>(c, t + 1, wr, wc, offl, offh, a, b, acc, scale, d);
+    stop = ktile<BF, 1, false, DL>(c, t, wr, wc, offl, offh, a, b, acc, scale, d);
+    if (!stop) stop = ktile<BF, 0, false, DL>(c, t + 1, wr, wc, offl, offh, a, b, acc, scale, d);
   }
-  if (!stop) stop = ktile<BF, 1, false, DL, true, 8, OPT>(c, nk - 1, wr, wc, offl, offh, a, b, acc, scale, d);
+  if (!stop) stop = ktile<BF, 1, false, DL>(c, nk - 1, wr, wc, offl, offh, a, b, acc, scale, d);
   return stop;
 }
 
@@ -374,7 +358,7 @@ __device__ __forceinline__ void store_tile(f32x4 (&acc)[8][8], __bf16* __restric
 
 // One 256 x 256 tile of C. Returns false if the deadline stopped it (no
 // store; every staged load has been waited for).
-template <bool BF, bool DL, int OPT>
+template <bool BF, bool DL>
 __device__ __forceinline__ bool tile4(CtxF& c, const char* __restrict__ A, const char* __restrict__ B,
                                       __bf16* __restrict__ C, int lda, int ldb, int ldc, int K, int tm, int tn,
                                       int lane, const DeadlineF& d) {
@@ -408,8 +392,8 @@ __device__ __forceinline__ bool tile4(CtxF& c, const char* __restrict__ A, const
   FragF a[8], b[2][8];
 
   prologue(c, wr, wc, offl, offh, a, b);
-  bool stop = ktile<BF, 0, true, DL, false, 8, OPT>(c, 0, wr, wc, offl, offh, a, b, acc, scale, d);
-  stop = ktiles_rest<BF, DL, OPT>(c, nk, wr, wc, offl, offh, a, b, acc, scale, d, stop);
+  bool stop = ktile<BF, 0, true, DL>(c, 0, wr, wc, offl, offh, a, b, acc, scale, d);
+  stop = ktiles_rest<BF, DL>(c, nk, wr, wc, offl, offh, a, b, acc, scale, d, stop);
   wait_vm<0>();  // the clamped staging copies (or, stopped, everything in flight)
   // Every wave passes this barrier before the next tile's prologue restages
   // K-tile 1's buffer, whose last reads (the clamped K-tile nk) were this
@@ -435,7 +419,7 @@ __device__ __forceinline__ void tile_coords(int bid, int nt_m, int nt_n, int gro
 // compute with gemm_tn_deadline's contract (kernels.hip): grid <= resident
 // blocks walks the tiles round-robin and stops min(ticks, slice_end) after t0,
 // agreed per epoch through *slot.
-template <bool BF, bool DL, int OPT = 0>
+template <bool BF, bool DL>
 __global__ void __launch_bounds__(256, 1)
     gemm_4wave_fp8_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
                           int K, int lda, int ldb, int ldc, int group, uint64_t* __restrict__ slot, uint32_t epoch,
@@ -459,12 +443,12 @@ __global__ void __launch_bounds__(256, 1)
   int tm, tn;
   if constexpr (!DL) {
     tile_coords(xcd_remap(blockIdx.x, T), nt_m, nt_n, group, tm, tn);
-    tile4<BF, false, OPT>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d);
+    tile4<BF, false>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d);
   } else {
     if (tid == 0) d.t0 = dl::agree_t0(slot, epoch, ticks, sync);  // only thread 0 reads the clock
     for (int round = 0;; ++round) {
       tile_coords(xcd_remap((blockIdx.x + round * gridDim.x) % T, T), nt_m, nt_n, group, tm, tn);
-      if (!tile4<BF, true, OPT>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d)) return;
+      if (!tile4<BF, true>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d)) return;
     }
   }
 }
@@ -484,7 +468,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const char* base, in
                                            0x7ffffff0, 0x00020000);
 }
 
-template <bool BF, bool DL, int OPT = 0>
+template <bool BF, bool DL>
 __global__ void __launch_bounds__(256, 1)
     gemm_4wave_fp8_stream_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C,
                                  int M, int N, int K, int lda, int ldb, int ldc, int group, uint64_t* __restrict__ slot,
@@ -539,8 +523,8 @@ __global__ void __launch_bounds__(256, 1)
   bool first = true, stop = false;
   for (;;) {
     // (the first tile re-reads the a[7] its prologue read: same data)
-    stop = ktile<BF, 0, true, DL, true, -1, OPT>(c, 0, wr, wc, offl, offh, a, b, acc, scale, d, !first);
-    stop = ktiles_rest<BF, DL, OPT>(c, nk, wr, wc, offl, offh, a, b, acc, scale, d, stop);
+    stop = ktile<BF, 0, true, DL, true, -1>(c, 0, wr, wc, offl, offh, a, b, acc, scale, d, !first);
+    stop = ktiles_rest<BF, DL>(c, nk, wr, wc, offl, offh, a, b, acc, scale, d, stop);
     if (DL && stop) break;  // partial tile: the stand-in result is not needed
     store_tile(acc, C, ldc, tm, tn, wr, wc, r16, h);
     if (!c.has_next) break;
@@ -848,14 +832,6 @@ namespace {
 // The square one-wave-per-SIMD kernels for either dtype: strides and K go in
 // as bytes (the staging and K-tile arithmetic work in bytes; bf16 runs two
 // 32-deep MFMAs per 128-byte K-tile row where fp8 runs one 128-deep MX MFMA).
-// Schedule options (OPT_MAIN | OPT_ROWS) of the square kernels: DLNB_G4_OPT,
-// read on every launch (A/B in one process).
-int g4_opt() {
-  const char* env = std::getenv("DLNB_G4_OPT");
-  const int v = env ? std::atoi(env) : 0;
-  return v >= 0 && v <= 3 ? v : 0;
-}
-
 template <bool BF>
 void launch_4wave(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, void* stream) {
   constexpr int esz = BF ? 2 : 1;
@@ -871,20 +847,12 @@ void launch_4wave(const void* A, const void* B, void* C, int M, int N, int K, in
   auto* b = static_cast<const char*>(B);
   auto* c = static_cast<__bf16*>(C);
   hipStream_t st = static_cast<hipStream_t>(stream);
-#define DLNB_G4_LAUNCH(OPT)                                                                                      \
-  if (tiles > cus)                                                                                             \
-    hipLaunchKernelGGL((gemm_4wave_fp8_stream_kernel<BF, false, OPT>), cus, 256, 0, st, a, b, c, M, N, K * esz, \
-                       lda * esz, ldb * esz, ldc, group, nullptr, 0u, 0ull, 0ull, DlSync());                  \
-  else                                                                                                         \
-    hipLaunchKernelGGL((gemm_4wave_fp8_kernel<BF, false, OPT>), tiles, 256, 0, st, a, b, c, M, N, K * esz,      \
-                       lda * esz, ldb * esz, ldc, group, nullptr, 0u, 0ull, 0ull, DlSync())
-  switch (g4_opt()) {
-    case 1: DLNB_G4_LAUNCH(1); break;
-    case 2: DLNB_G4_LAUNCH(2); break;
-    case 3: DLNB_G4_LAUNCH(3); break;
-    default: DLNB_G4_LAUNCH(0); break;
-  }
-#undef DLNB_G4_LAUNCH
+  if (tiles > cus)
+    hipLaunchKernelGGL((gemm_4wave_fp8_stream_kernel<BF, false>), cus, 256, 0, st, a, b, c, M, N, K * esz,
+                       lda * esz, ldb * esz, ldc, group, nullptr, 0u, 0ull, 0ull, DlSync());
+  else
+    hipLaunchKernelGGL((gemm_4wave_fp8_kernel<BF, false>), tiles, 256, 0, st, a, b, c, M, N, K * esz, lda * esz,
+                       ldb * esz, ldc, group, nullptr, 0u, 0ull, 0ull, DlSync());
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 4-wave launch failed: " << hipGetErrorString(e));
 }
@@ -927,22 +895,12 @@ void gemm_tn_4wave_deadline(const void* A, const void* B, void* C, int M, int N,
   auto* a = static_cast<const char*>(A);
   auto* b = static_cast<const char*>(B);
   auto* c = static_cast<__bf16*>(C);
-  const bool opt = g4_opt() == 3;
-  if (in_t == DType::BF16) {
-    if (opt)
-      hipLaunchKernelGGL((gemm_4wave_fp8_kernel<true, true, 3>), grid, 256, 0, st, a, b, c, M, N, K * esz, K * esz,
-                         K * esz, N, 8, slot, epoch, ticks, slice_end, sync);
-    else
-      hipLaunchKernelGGL((gemm_4wave_fp8_kernel<true, true>), grid, 256, 0, st, a, b, c, M, N, K * esz, K * esz,
-                         K * esz, N, 8, slot, epoch, ticks, slice_end, sync);
-  } else {
-    if (opt)
-      hipLaunchKernelGGL((gemm_4wave_fp8_kernel<false, true, 3>), grid, 256, 0, st, a, b, c, M, N, K, K, K, N, 8,
-                         slot, epoch, ticks, slice_end, sync);
-    else
-      hipLaunchKernelGGL((gemm_4wave_fp8_kernel<false, true>), grid, 256, 0, st, a, b, c, M, N, K, K, K, N, 8, slot,
-                         epoch, ticks, slice_end, sync);
-  }
+  if (in_t == DType::BF16)
+    hipLaunchKernelGGL((gemm_4wave_fp8_kernel<true, true>), grid, 256, 0, st, a, b, c, M, N, K * esz, K * esz,
+                       K * esz, N, 8, slot, epoch, ticks, slice_end, sync);
+  else
+    hipLaunchKernelGGL((gemm_4wave_fp8_kernel<false, true>), grid, 256, 0, st, a, b, c, M, N, K, K, K, N, 8, slot,
+                       epoch, ticks, slice_end, sync);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 4-wave deadline launch failed: " << hipGetErrorString(e));
 }

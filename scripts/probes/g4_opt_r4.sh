@@ -2,7 +2,8 @@
 # Round 4: schedule options of the one-wave-per-SIMD square GEMMs (gemm_4wave_fp8.hip OPT / DLNB_G4_OPT):
 # OPT_MAIN (clamp-free main K-loop staging, compile-time buffer parity: fewer SALU per MFMA) and OPT_ROWS
 # (bf16: a row's lo K-steps then its hi ones, no s_nop between same-accumulator MFMAs). Numerics first,
-# then one-shot TF/s interleaved against torch, fp8 and bf16.
+# then one-shot TF/s interleaved against torch, fp8 and bf16. (After this A/B the main loop became
+# unconditional and the row order was dropped; DLNB_G4_OPT no longer exists: profiles/gemm_g4_main_r4.md.)
 set -u
 O=gpurun_out/g4opt
 mkdir -p $O
