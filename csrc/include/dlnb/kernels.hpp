@@ -35,7 +35,7 @@ struct DlSync {
   uint64_t* tstart[2] = {nullptr, nullptr};
   const uint64_t* gate[2] = {nullptr, nullptr};
   uint32_t tag[2] = {0, 0};
-  uint32_t chain = 0;
+  uint32_t chain = 0;  // != 0: continue the stream's previous task, absorbing at most this many ticks of lateness
 };
 // One wave stores {tag:16 | s_memrealtime:48} into *gate (device memory,
 // agent scope) when the stream reaches this point. tag != 0.

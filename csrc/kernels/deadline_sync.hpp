@@ -22,11 +22,16 @@
 //     then: the gate dates the dependency, the graph edge orders it (a
 //     kernel spinning on a word raised by a node queued behind it on the
 //     same hardware queue would never finish);
-//   * chain: the task continues the stream's previous task, so it starts at
-//     max(previous deadline, the latest gate) - a late launch (queue hop,
-//     the previous grid's drain) is absorbed, a late collective is not (the
-//     start moves to the time its gate was raised, and that wait is what the
-//     strategy's timers report as exposed communication);
+//   * chain (!= 0: the most ticks of lateness to absorb): the task continues
+//     the stream's previous task, so it starts at max(previous deadline, the
+//     latest gate) - a late launch (queue hop, the previous grid's drain) is
+//     absorbed, a late collective is not (the start moves to the time its
+//     gate was raised, and that wait is what the strategy's timers report as
+//     exposed communication). A first block later than that start by more
+//     than `chain` ticks starts the task `chain` ticks before it arrived: a
+//     longer delay is not a launch hop (a replayed graph can queue a node
+//     behind another stream's collective on one hardware queue) and stays in
+//     the iteration time instead of being taken out of the compute;
 //   * otherwise t0 = the time the gates opened (now, with no gates).
 // t0 (as a full 64-bit s_memrealtime value) goes to up to two host-mapped
 // stamp slots (the strategy's stall timer, the --timeline span).
@@ -99,7 +104,10 @@ __device__ __forceinline__ uint64_t agree_t0(uint64_t* slot, uint32_t epoch, uin
   const uint64_t prev = s.chain ? ld(slot + 1) & kMask48 : 0;
   if (prev != 0) {  // 0: nothing to continue (the slot was reset)
     t0 = gated && not_before(gate_t, prev) ? gate_t : prev;
-    if (!not_before(now, t0)) t0 = now;  // never in the future
+    if (!not_before(now, t0))
+      t0 = now;  // never in the future
+    else if (((now - t0) & kMask48) > s.chain)
+      t0 = (now - s.chain) & kMask48;  // absorb at most `chain` ticks of lateness
   }
   __hip_atomic_store(slot + 1, (t0 + ticks) & kMask48, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(slot, (static_cast<uint64_t>(epoch) << 48) | t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

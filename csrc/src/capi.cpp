@@ -95,15 +95,16 @@ int dlnb_gemm_deadline_us(const void* A, const void* B, void* C, int M, int N, i
 }
 
 // The deadline GEMM with the full start protocol (csrc/kernels/deadline_sync.hpp):
-// explicit epoch, chain flag, up to two gates with their tags, a start stamp.
+// explicit epoch, chain (> 0: continue the slot's previous deadline absorbing at
+// most chain_us of lateness), up to two gates with their tags, a start stamp.
 int dlnb_gemm_deadline_ex(const void* A, const void* B, void* C, int M, int N, int K, int dtype, double us, int device,
-                          void* slot, int grid, void* stream, unsigned epoch, int chain, void* gate0, unsigned tag0,
+                          void* slot, int grid, void* stream, unsigned epoch, double chain_us, void* gate0, unsigned tag0,
                           void* gate1, unsigned tag1, void* tstart) {
   return guard([&] {
     double hz = dlnb::kernels::wallclock_hz(device);
     if (grid <= 0) grid = dlnb::kernels::num_cus(device);
     dlnb::kernels::DlSync sync;
-    sync.chain = chain ? 1u : 0u;
+    sync.chain = chain_us > 0 ? static_cast<uint32_t>(std::max(1.0, chain_us * 1e-6 * hz + 0.5)) : 0u;
     sync.gate[0] = static_cast<const uint64_t*>(gate0);
     sync.gate[1] = static_cast<const uint64_t*>(gate1);
     sync.tag[0] = tag0;

@@ -78,6 +78,7 @@ class GpuCompute : public ComputeEngine {
   GpuCompute(Device& dev, ComputeMode mode, const ComputeShape& shape, double scale)
       : dev_(dev), mode_(mode), scale_(scale) {
     hz_ = kernels::wallclock_hz(dev.index());
+    absorb_ticks_ = static_cast<uint32_t>(std::max<uint64_t>(ticks(static_cast<double>(env_int("DLNB_CHAIN_ABSORB_US", 30))), 1));
     cus_ = kernels::num_cus(dev.index());
     dtype_ = shape.dtype == DType::FP8_E4M3 ? DType::FP8_E4M3 : DType::BF16;
     // The stand-in is the layer's FFN down projection, C[tokens, hidden] =
@@ -264,6 +265,7 @@ class GpuCompute : public ComputeEngine {
       j["comm_reserved_cus"] = cus_ - grid_;
       j["deadline_slice_us"] = slice_us_;
       j["chained_tasks"] = chained_;  // enqueued so far (a captured graph counts its one iteration)
+      j["chain_absorb_us"] = absorb_ticks_ / hz_ * 1e6;  // most lateness a chained / gated task absorbs
       j["gated_tasks"] = gated_;      // tasks that waited on device gates instead of stream events
     }
     if (A_.data()) {
@@ -297,7 +299,7 @@ class GpuCompute : public ComputeEngine {
     uint64_t* slot = slot_for(s);
     uint32_t& ep = epoch_[slot];
     ep = ep % 65535 + 1;  // 1..65535, never 0 (a fresh slot reads as epoch 0)
-    sync.chain = chain ? 1u : 0u;
+    sync.chain = chain ? absorb_ticks_ : 0u;
     const uint64_t total = ticks(d);
     const uint64_t slice = slice_us_ > 0 ? std::max<uint64_t>(ticks(slice_us_), 1) : total;
     for (uint64_t end = slice;; end += slice) {
@@ -406,6 +408,11 @@ class GpuCompute : public ComputeEngine {
   std::map<uint64_t*, bool> chain_live_;  // the stream's last task was a deadline task a chained one may continue
   std::vector<uint32_t> gate_tag_;        // last tag signalled per gate (1..65535)
   uint64_t* extra_start_ = nullptr;       // set_next_start_slot
+  // Lateness a chained task absorbs (deadline_sync.hpp): the replayed graph's
+  // queue hop (8-11 us) + the previous grid's drain (~13 us) measured in
+  // round 3; anything later is a wait and stays in the iteration time.
+  // DLNB_CHAIN_ABSORB_US overrides.
+  uint32_t absorb_ticks_ = 1;
   long chained_ = 0;                      // tasks that continued a chain (describe())
   long gated_ = 0;
   int grid_ = 256;

@@ -67,11 +67,12 @@ def gemm_deadline_us(a, b, c, us: float, stamp=None, grid: int = 0):
     return c
 
 
-def gemm_deadline_ex(a, b, c, us: float, slot, epoch: int, chain: bool = False, gates=(), tstart=None,
+def gemm_deadline_ex(a, b, c, us: float, slot, epoch: int, chain=False, gates=(), tstart=None,
                      grid: int = 0):
     """gemm_deadline_us with the whole start protocol (csrc/kernels/deadline_sync.hpp): `slot` an int64
     CUDA tensor of 8 elements reused by consecutive tasks of one stream, `epoch` the task number on it
-    (1..65535, different from the previous task's), `chain` start at the slot's previous deadline,
+    (1..65535, different from the previous task's), `chain` start at the slot's previous deadline
+    absorbing at most `chain` us of lateness (True: the runtime's 30 us, DLNB_CHAIN_ABSORB_US),
     `gates` up to two (int64 CUDA tensor, index, tag) words to wait for, `tstart` an (int64 tensor,
     index) that receives the task's start (s_memrealtime ticks)."""
     import torch
@@ -84,7 +85,8 @@ def gemm_deadline_ex(a, b, c, us: float, slot, epoch: int, chain: bool = False, 
     ts = tstart[0].data_ptr() + 8 * tstart[1] if tstart is not None else None
     _native.check(_native.lib().dlnb_gemm_deadline_ex(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, dt, us,
                                                       a.device.index or 0, slot.data_ptr(), grid, _stream(a), epoch,
-                                                      int(chain), g[0][0], g[0][1], g[1][0], g[1][1], ts))
+                                                      30.0 if chain is True else float(chain or 0), g[0][0],
+                                                      g[0][1], g[1][0], g[1][1], ts))
     return c
 
 
