@@ -108,6 +108,12 @@ class Device {
   // Enqueue a host callback (CPU: task on the worker; GPU: hipLaunchHostFunc).
   virtual void host_task(Stream& s, std::function<void()> fn) = 0;
   virtual void synchronize() = 0;
+  // After a failed iteration, before the strategy (its events, buffers and
+  // communicators) is destroyed: stop every stream's queued work and wait for
+  // the streams to go idle. CPU devices raise their abort switch (queued
+  // tasks are skipped, event waits return) and drain; GPU devices: nothing
+  // (the communicators were aborted, the runtime owns the queues).
+  virtual void abort_and_drain() {}
   // Timestamps taken when a stream reaches a point (device clock on GPU: a
   // one-wave kernel stores s_memrealtime into host-mapped memory; host clock
   // on CPU). Unlike timing events they are exact across cross-stream waits.
@@ -170,6 +176,7 @@ class CpuStream : public Stream {
   void wait(Event& e) override;
   void synchronize() override;
   bool query() override;
+  void drain();  // wait until idle; a task's error stays for synchronize()
   void* native() override { return nullptr; }
   void enqueue(std::function<void()> fn);
 

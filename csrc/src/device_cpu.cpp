@@ -186,6 +186,11 @@ void CpuStream::wait(Event& e) {
   enqueue([ce, gen] { ce->wait_for(gen); });
 }
 
+void CpuStream::drain() {
+  std::unique_lock<std::mutex> g(mu_);
+  cv_.wait(g, [&] { return inflight_ == 0; });
+}
+
 bool CpuStream::query() {
   std::lock_guard<std::mutex> g(mu_);
   return inflight_ == 0;
@@ -291,6 +296,11 @@ class CpuDevice : public Device {
   void synchronize() override {
     std::lock_guard<std::mutex> g(reg_->mu);
     for (CpuStream* s : reg_->live) s->synchronize();
+  }
+  void abort_and_drain() override {
+    abort_->store(true);
+    std::lock_guard<std::mutex> g(reg_->mu);
+    for (CpuStream* s : reg_->live) s->drain();
   }
   uint64_t* alloc_stamps(size_t n) override { return static_cast<uint64_t*>(std::calloc(n, sizeof(uint64_t))); }
   void free_stamps(uint64_t* p, size_t) override { std::free(p); }

@@ -420,6 +420,11 @@ Json run_rank(const Options& opt, std::unique_ptr<Bootstrap> boot) {
   try {
     return run_rank_impl(opt, ctx, strat);
   } catch (const std::exception& e) {
+    // The strategy is destroyed before the device (ctx outlives strat): its
+    // events, buffers and communicators must not go while a stream task still
+    // uses them (a CPU stream waiting on a freed event never returned - seen
+    // after a peer died mid-iteration, library host).
+    if (ctx.dev && !ctx.boot->hub) ctx.dev->abort_and_drain();
     if (ctx.boot->hub) {
       const std::string msg = "rank " + std::to_string(ctx.boot->info.rank) + ": " + e.what();
       loopback_abort(*ctx.boot->hub, msg);

@@ -145,6 +145,22 @@ def test_bench_wall_budget_survives_a_hung_block_two_ranks(tmp_path):
     assert "skipped" in o["comm_bound"]["geometric_buckets"]
 
 
+def test_bench_headline_fallback_two_ranks(tmp_path):
+    """A headline that fails on its backend at N > 1 (rank 1 throws in its first iteration; rank 0's collective
+    times out) is timed again on the fallback backend as a bounded child run of every rank: the line carries a
+    value, the fallback's backend and the primary failure, and the blocks after it run (on GPU the fallback is
+    the xgmi kernels when the exactness pass proved them exact; here --fallback-backend cpu)."""
+    o = _torchrun(2, ["--steps", "2", "--warmup", "1", "--backend", "cpu", "--compute", "sleep",
+                      "--fallback-backend", "cpu", "--wall-budget-s", "120"] + TINY, tmp_path,
+                  env={"DLNB_INJECT_FAULT": "rank=1,iter=0,mode=throw,block=headline", "DLNB_TIMEOUT": "10"},
+                  timeout=300)
+    assert o["value"] > 0 and "error" not in o, o.get("error")
+    fb = o["headline_fallback"]
+    assert fb["backend"] == "cpu" and fb["primary_error"] and "error" not in fb, fb
+    assert o["config"]["backend"] == "CPU-SHM" and o["comm_bound"]["ms_per_step"] > 0
+    assert "headline_fallback" in o["phase_seconds"] and "headline_fallback" in o["budget"]["timeouts_s"]
+
+
 def test_bench_wall_budget_hybrids_eight_ranks(tmp_path):
     """The N = 8 path with the hybrid blocks and a hang injected into C3 on rank 5: C3 reports its timeout
     (its limit: --hybrid-timeout), the C4 blocks after it still run (per_run_ms: --c4-runs entries), one
