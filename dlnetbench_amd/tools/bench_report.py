@@ -104,14 +104,14 @@ def _largest(by_size: Any) -> Any:
 def rows(lines: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
     if not lines:
         return []
-    t0 = lines[0]["ms_per_step"]
+    t0 = next((d["ms_per_step"] for d in lines if d.get("ms_per_step")), None)
     out = []
     for d in lines:
         ms = d["ms_per_step"]
         r = {
             "n_gpus": d["n_gpus"],
             "ms_per_step": ms,
-            "efficiency": round(t0 / ms, 4) if ms else None,
+            "efficiency": round(t0 / ms, 4) if ms and t0 else None,
             "exposed_comm_ms": d.get("exposed_comm_ms"),
             "ag_busbw_GBps": _get(d, "effective_busbw_GBps", "allgather"),
             "rs_busbw_GBps": _get(d, "effective_busbw_GBps", "reduce_scatter"),
@@ -140,6 +140,9 @@ def rows(lines: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
             "link_ar_busbw_rccl": _largest(_get(d, "link_bench", "rccl", "all_reduce")),
             "link_ar_busbw_xgmi": _largest(_get(d, "link_bench", "xgmi_registered", "all_reduce")),
             "wall_s": _get(d, "phase_seconds", "total"),
+            # the backend the headline was timed on (the xgmi fallback when RCCL failed: headline_fallback)
+            "backend": _get(d, "config", "backend"),
+            "fallback": bool(d.get("headline_fallback")),
         }
         out.append(r)
     return out

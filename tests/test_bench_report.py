@@ -52,6 +52,21 @@ def test_cli_json_array_and_csv(tmp_path, capsys):
     assert rows[0].startswith("n_gpus,ms_per_step,efficiency") and len(rows) == 3
 
 
+def test_failed_and_fallback_lines(tmp_path):
+    """A line whose headline failed (value null) gets no efficiency and does not become the N = 1 reference;
+    a line timed on the fallback backend says so."""
+    fail = {"metric": "m", "value": None, "unit": "ms", "n_gpus": 2, "ms_per_step": None, "error": "headline failed"}
+    fb = json.loads(_line(8, 2820.0))
+    fb["config"] = {"backend": "XGMI"}
+    fb["headline_fallback"] = {"backend": "xgmi", "primary_backend": "auto", "primary_error": "rccl init"}
+    p = tmp_path / "r.txt"
+    p.write_text("\n".join([json.dumps(fail), _line(1, 2816.0), json.dumps(fb)]))
+    rs = bench_report.rows(bench_report.load([str(p)]))
+    assert [r["n_gpus"] for r in rs] == [1, 2, 8]
+    assert rs[1]["efficiency"] is None and rs[2]["efficiency"] == round(2816.0 / 2820.0, 4)
+    assert rs[2]["backend"] == "XGMI" and rs[2]["fallback"] and not rs[0]["fallback"]
+
+
 def test_no_lines_is_an_error(tmp_path):
     p = tmp_path / "empty.txt"
     p.write_text("nothing here\n")
