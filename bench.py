@@ -666,7 +666,8 @@ def _c5_blocks(a: argparse.Namespace, world: int, rank: int, budget: _Budget, es
         it = d["global"]["dlnb"]["iteration"]
         return {"ms_per_step": round(it["timed_ms_per_iter"], 4), "median_ms": round(it["median_ms"], 4),
                 "exposed_comm_ms": _mean_of(d, "barrier_time"),
-                "allreduce_busbw_GBps": _busbw(d, "allreduce", world)}
+                "allreduce_busbw_GBps": _busbw(d, "allreduce", world),
+                "chain_capped": d["global"]["dlnb"].get("chain_capped")}
 
     try:
         d = _dp_block(a, world, rank, budget, est, ".c5", graph, a.compute)
@@ -1030,6 +1031,9 @@ def main() -> int:
             # null at N = 1: a 1-rank all-gather / reduce-scatter is a local copy
             "effective_busbw_GBps": {k: _busbw(doc, k, world) for k in ("allgather", "reduce_scatter")},
             "exposed_comm_ms": round(exposed, 3),
+            # compute tasks per iteration that waited longer than a launch hop (the chained
+            # deadline's 30-us absorb cap) and that wait in ms - kept in the time, not hidden
+            "chain_capped": g["dlnb"].get("chain_capped"),
             "median_ms": round(it["median_ms"], 3),
             "per_run_ms": _per_run_ms(doc),
             # every rank's mean iteration (ms): at N > 1 the straggler and the spread behind the max

@@ -100,6 +100,12 @@ class ComputeEngine {
   // Graph mode: enqueue on s a reset of whatever per-task device state the
   // engine keys by epoch (a replayed graph repeats the captured epochs).
   virtual void reset_clocks(Stream& s) { (void)s; }
+  // Chained / gated deadline tasks whose first block came later than the
+  // absorb cap after their chained start (a wait, not a launch hop: e.g. a
+  // replayed graph queueing the task behind another stream's collective):
+  // zero the counters (stream-ordered on s) / read them (host, after a sync).
+  virtual void reset_capped(Stream& s) { (void)s; }
+  virtual bool capped(uint64_t& tasks, double& seconds) { (void)tasks; (void)seconds; return false; }
   // Fixed-work modes (gemm-work, flops): time every compute task on the
   // device into t ("compute_task_time") next to its table duration
   // ("compute_task_table"), so the runner can report how much collectives

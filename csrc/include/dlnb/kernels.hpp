@@ -36,6 +36,9 @@ struct DlSync {
   const uint64_t* gate[2] = {nullptr, nullptr};
   uint32_t tag[2] = {0, 0};
   uint32_t chain = 0;  // != 0: continue the stream's previous task, absorbing at most this many ticks of lateness
+  // {tasks, ticks}: chained tasks that arrived later than `chain` ticks after
+  // their start, and the lateness beyond it (device memory; nullptr: none)
+  uint64_t* capped = nullptr;
 };
 // One wave stores {tag:16 | s_memrealtime:48} into *gate (device memory,
 // agent scope) when the stream reaches this point. tag != 0.

@@ -104,10 +104,16 @@ __device__ __forceinline__ uint64_t agree_t0(uint64_t* slot, uint32_t epoch, uin
   const uint64_t prev = s.chain ? ld(slot + 1) & kMask48 : 0;
   if (prev != 0) {  // 0: nothing to continue (the slot was reset)
     t0 = gated && not_before(gate_t, prev) ? gate_t : prev;
-    if (!not_before(now, t0))
+    if (!not_before(now, t0)) {
       t0 = now;  // never in the future
-    else if (((now - t0) & kMask48) > s.chain)
+    } else if (((now - t0) & kMask48) > s.chain) {
+      const uint64_t excess = ((now - t0) & kMask48) - s.chain;
       t0 = (now - s.chain) & kMask48;  // absorb at most `chain` ticks of lateness
+      if (s.capped) {  // counted for the report: a wait the chain did not hide
+        __hip_atomic_fetch_add(s.capped, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(s.capped + 1, excess, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
   __hip_atomic_store(slot + 1, (t0 + ticks) & kMask48, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(slot, (static_cast<uint64_t>(epoch) << 48) | t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

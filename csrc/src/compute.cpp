@@ -112,6 +112,7 @@ class GpuCompute : public ComputeEngine {
     if (mode_ == ComputeMode::Gemm) {
       // one 64-byte line per compute stream, then the gate words
       slots_ = dev_.alloc(kSlots * 64 + kGates * 8);
+      capped_ = dev_.alloc(2 * sizeof(uint64_t));
       auto zs = dev_.create_stream(false);
       dev_.memset_async(slots_.data(), 0, kSlots * 64 + kGates * 8, *zs);
       zs->synchronize();
@@ -138,6 +139,19 @@ class GpuCompute : public ComputeEngine {
 
   void reset_clocks(Stream& s) override {
     if (mode_ == ComputeMode::Gemm) dev_.memset_async(slots_.data(), 0, kSlots * 64 + kGates * 8, s);
+  }
+  void reset_capped(Stream& s) override {
+    if (capped_.data()) dev_.memset_async(capped_.data(), 0, 2 * sizeof(uint64_t), s);
+  }
+  bool capped(uint64_t& tasks, double& seconds) override {
+    if (!capped_.data()) return false;
+    uint64_t v[2] = {0, 0};
+    auto st = dev_.create_stream(false);
+    dev_.copy_async(v, capped_.data(), sizeof(v), *st);
+    st->synchronize();
+    tasks = v[0];
+    seconds = static_cast<double>(v[1]) / hz_;
+    return true;
   }
 
   bool stamps_task_start() const override { return mode_ == ComputeMode::Gemm; }
@@ -300,6 +314,7 @@ class GpuCompute : public ComputeEngine {
     uint32_t& ep = epoch_[slot];
     ep = ep % 65535 + 1;  // 1..65535, never 0 (a fresh slot reads as epoch 0)
     sync.chain = chain ? absorb_ticks_ : 0u;
+    sync.capped = chain ? capped_.as<uint64_t>() : nullptr;
     const uint64_t total = ticks(d);
     const uint64_t slice = slice_us_ > 0 ? std::max<uint64_t>(ticks(slice_us_), 1) : total;
     for (uint64_t end = slice;; end += slice) {
@@ -403,6 +418,7 @@ class GpuCompute : public ComputeEngine {
   ComputeMode mode_;
   double scale_;
   Buffer slots_;
+  Buffer capped_;  // {tasks, ticks} beyond the absorb cap (DlSync::capped)
   std::map<Stream*, size_t> slot_of_;
   std::map<uint64_t*, uint32_t> epoch_;
   std::map<uint64_t*, bool> chain_live_;  // the stream's last task was a deadline task a chained one may continue

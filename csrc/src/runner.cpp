@@ -618,6 +618,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   }
 
   ctx.hg().barrier();
+  ctx.compute->reset_capped(*strat->streams()[0]);  // count the timed iterations only
   ctx.dev->synchronize();
   const double T0 = now_s();
   for (int r = 0; r < runs; ++r) {
@@ -642,6 +643,17 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   // ---- report
   Json rank = strat->rank_json();
   rank["energy_consumed"] = T.values_json("energy_consumed");
+  {
+    // chained deadline tasks that waited longer than the absorb cap (deadline_sync.hpp)
+    uint64_t ct = 0;
+    double cs = 0;
+    if (runs > 0 && ctx.compute->capped(ct, cs)) {
+      Json c = Json::object();
+      c["tasks_per_iter"] = static_cast<double>(ct) / runs;
+      c["ms_per_iter"] = cs / runs * 1e3;
+      rank["chain_capped"] = c;
+    }
+  }
   rank["hostname"] = ri.hostname;
   rank["rank"] = ri.rank;
   rank["local_rank"] = ri.local_rank;
@@ -766,6 +778,20 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     for (const auto& rj : ranks)
       if (rj.contains("compute_stretch")) worst = std::max(worst, rj.at("compute_stretch").as_double());
     if (worst > 0) ext["compute_stretch"] = worst;  // max over ranks
+    // Compute tasks that waited beyond the chain's absorb cap per iteration
+    // (the wait stays in the iteration time; max over ranks)
+    double ctasks = -1, cms = 0;
+    for (const auto& rj : ranks)
+      if (rj.contains("chain_capped")) {
+        ctasks = std::max(ctasks, rj.at("chain_capped").at("tasks_per_iter").as_double());
+        cms = std::max(cms, rj.at("chain_capped").at("ms_per_iter").as_double());
+      }
+    if (ctasks >= 0) {
+      Json c = Json::object();
+      c["tasks_per_iter_max"] = ctasks;
+      c["ms_per_iter_max"] = cms;
+      ext["chain_capped"] = c;
+    }
   }
   g["dlnb"] = ext;
 

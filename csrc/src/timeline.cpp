@@ -389,6 +389,8 @@ class TracingCompute : public ComputeEngine {
   }
   void set_next_start_slot(uint64_t* slot) override { in_->set_next_start_slot(slot); }
   void reset_clocks(Stream& s) override { in_->reset_clocks(s); }
+  void reset_capped(Stream& s) override { in_->reset_capped(s); }
+  bool capped(uint64_t& tasks, double& seconds) override { return in_->capped(tasks, seconds); }
   void set_task_timers(TimerSet* t) override { in_->set_task_timers(t); }
   Json describe() const override { return in_->describe(); }
   ComputeMode mode() const override { return in_->mode(); }
