@@ -795,6 +795,7 @@ def main() -> int:
     ap.add_argument("--json", default=None, help="also write the full headline report here (rank 0)")
     a = ap.parse_args()
     a.hybrid_backend = "rccl" if a.backend == "auto" else a.backend
+    checked_backends = _exact_backends(a)  # before a fallback changes a.backend
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -998,9 +999,6 @@ def main() -> int:
             ph.add("headline_xgmi", t0)
     if rank != 0:
         return 0
-    if fallback is not None and doc is not None:
-        # the value below is the fallback backend's
-        headline_error = None
     out: Dict[str, Any] = {"metric": METRIC, "value": None, "unit": "ms", "n_gpus": world, "steps": a.steps,
                            "warmup": a.warmup, "ms_per_step": None, "higher_is_better": False, "scaling": "weak",
                            "vs_baseline": None, "dtype": "bf16"}
@@ -1073,7 +1071,7 @@ def main() -> int:
     # backend whose collectives were not exact on these ranks keeps its
     # numbers and carries "error".
     if exact.get("exact"):
-        ver = {b: bool(exact["exact"].get(b)) for b in _exact_backends(a).split(",")}
+        ver = {b: bool(exact["exact"].get(b)) for b in checked_backends.split(",")}
         out["verified"] = ver
         for key, blk in [("headline", out), ("comm_bound", extra.get("comm_bound")),
                          ("hybrid_3d", extra.get("hybrid_3d")), ("hybrid_3d_moe", extra.get("hybrid_3d_moe")),
@@ -1085,7 +1083,7 @@ def main() -> int:
                 blk["error"] = f"{b} exactness failed (see exact_detail); timed anyway"
     elif exact:
         # the pass ran but did not complete (timeout, crash, budget): nothing is verified
-        out["verified"] = {b: None for b in _exact_backends(a).split(",")}
+        out["verified"] = {b: None for b in checked_backends.split(",")}
         out["verified_note"] = "exactness pass did not complete: " + json.dumps(exact.get("exact_detail"))[:200]
     else:
         out["verified"] = None  # no exactness pass (N = 1: collectives are local copies)
