@@ -89,6 +89,15 @@ class ComputeEngine {
   virtual bool gates_task(double us) const { (void)us; return false; }
   virtual int make_gate() { DLNB_THROW("this compute mode has no device gates"); }
   virtual void signal(Stream& s, int gate) { (void)s; (void)gate; DLNB_THROW("this compute mode has no device gates"); }
+  // The other direction: stream s (a comm lane) waits on the device until the
+  // gate carries the tag of its latest signal(), instead of a cross-stream
+  // event (no graph edge from the signalling stream; timeout_us bounds it,
+  // counted by gate_timeouts()).
+  virtual void wait_gate(Stream& s, int gate, double timeout_us) {
+    (void)s; (void)gate; (void)timeout_us;
+    DLNB_THROW("this compute mode has no device gates");
+  }
+  virtual uint64_t gate_timeouts() { return 0; }
   virtual void run_gated(Stream& s, double us, double flops, const std::vector<int>& gates, uint64_t* start,
                          bool chain) {
     (void)s; (void)us; (void)flops; (void)gates; (void)start; (void)chain;

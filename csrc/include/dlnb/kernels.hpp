@@ -43,6 +43,11 @@ struct DlSync {
 // One wave stores {tag:16 | s_memrealtime:48} into *gate (device memory,
 // agent scope) when the stream reaches this point. tag != 0.
 void gate_signal(uint64_t* gate, uint32_t tag, void* stream);
+// One wave waits until *gate carries tag (raised by gate_signal on another
+// stream), at most timeout ticks; a timeout adds 1 to *timeouts and lets the
+// stream go on (a wait that can never be satisfied - e.g. the raising kernel
+// queued behind this one on the same hardware queue - must not hang the GPU).
+void gate_wait(const uint64_t* gate, uint32_t tag, uint64_t timeout_ticks, uint64_t* timeouts, void* stream);
 
 // Deadline kernels; ticks of the 100 MHz s_memrealtime clock (see
 // wallclock_hz()).

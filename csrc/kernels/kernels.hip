@@ -119,6 +119,19 @@ __global__ void gate_signal_kernel(uint64_t* gate, uint32_t tag) {
   }
 }
 
+__global__ void gate_wait_kernel(const uint64_t* gate, uint32_t tag, uint64_t timeout_ticks, uint64_t* timeouts) {
+  if (threadIdx.x == 0) {
+    const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+    while ((__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 48) != tag) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - w0 > timeout_ticks) {
+        __hip_atomic_fetch_add(timeouts, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) busy_spin_kernel(uint64_t ticks, float* sink) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   float x = static_cast<float>(threadIdx.x) * 1e-3f, y = 0.999f;
@@ -465,6 +478,12 @@ void idle_wait(uint64_t ticks, void* stream) {
 void gate_signal(uint64_t* gate, uint32_t tag, void* stream) {
   DLNB_REQUIRE(gate != nullptr && tag > 0 && tag < 65536, "gate_signal: bad gate/tag");
   hipLaunchKernelGGL(gate_signal_kernel, 1, 64, 0, S(stream), gate, tag);
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
+void gate_wait(const uint64_t* gate, uint32_t tag, uint64_t timeout_ticks, uint64_t* timeouts, void* stream) {
+  DLNB_REQUIRE(gate != nullptr && timeouts != nullptr && tag > 0 && tag < 65536, "gate_wait: bad gate/tag");
+  hipLaunchKernelGGL(gate_wait_kernel, 1, 64, 0, S(stream), gate, tag, timeout_ticks, timeouts);
   DLNB_HIP_CHECK(hipGetLastError());
 }
 

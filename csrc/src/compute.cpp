@@ -112,9 +112,10 @@ class GpuCompute : public ComputeEngine {
     if (mode_ == ComputeMode::Gemm) {
       // one 64-byte line per compute stream, then the gate words
       slots_ = dev_.alloc(kSlots * 64 + kGates * 8);
-      capped_ = dev_.alloc(2 * sizeof(uint64_t));
+      capped_ = dev_.alloc(3 * sizeof(uint64_t));  // {capped tasks, capped ticks, gate-wait timeouts}
       auto zs = dev_.create_stream(false);
       dev_.memset_async(slots_.data(), 0, kSlots * 64 + kGates * 8, *zs);
+      dev_.memset_async(capped_.data(), 0, 3 * sizeof(uint64_t), *zs);
       zs->synchronize();
       // Leave `comm_cus` CUs to collectives: one 128-KiB-LDS block fits per
       // CU, so a grid of CUs - comm_cus blocks never touches those CUs and
@@ -183,6 +184,19 @@ class GpuCompute : public ComputeEngine {
     uint32_t& tag = gate_tag_.at(gate);
     tag = tag % 65535 + 1;
     kernels::gate_signal(gate_word(gate), tag, s.native());
+  }
+  void wait_gate(Stream& s, int gate, double timeout_us) override {
+    const uint32_t tag = gate_tag_.at(gate);
+    DLNB_REQUIRE(tag != 0, "wait_gate: gate " << gate << " was never signalled");
+    kernels::gate_wait(gate_word(gate), tag, ticks(timeout_us), capped_.as<uint64_t>() + 2, s.native());
+  }
+  uint64_t gate_timeouts() override {
+    if (!capped_.data()) return 0;
+    uint64_t v[3] = {0, 0, 0};
+    auto st = dev_.create_stream(false);
+    dev_.copy_async(v, capped_.data(), sizeof(v), *st);
+    st->synchronize();
+    return v[2];
   }
 
   void run_gated(Stream& s, double us, double flops, const std::vector<int>& gates, uint64_t* start,

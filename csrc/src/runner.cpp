@@ -651,6 +651,9 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       Json c = Json::object();
       c["tasks_per_iter"] = static_cast<double>(ct) / runs;
       c["ms_per_iter"] = cs / runs * 1e3;
+      // device gate waits (a comm lane waiting on a compute gate) that gave up
+      // at their bound: never expected - the wait's signal was queued behind it
+      c["gate_wait_timeouts"] = static_cast<double>(ctx.compute->gate_timeouts());
       rank["chain_capped"] = c;
     }
   }
@@ -780,16 +783,18 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     if (worst > 0) ext["compute_stretch"] = worst;  // max over ranks
     // Compute tasks that waited beyond the chain's absorb cap per iteration
     // (the wait stays in the iteration time; max over ranks)
-    double ctasks = -1, cms = 0;
+    double ctasks = -1, cms = 0, gto = 0;
     for (const auto& rj : ranks)
       if (rj.contains("chain_capped")) {
         ctasks = std::max(ctasks, rj.at("chain_capped").at("tasks_per_iter").as_double());
         cms = std::max(cms, rj.at("chain_capped").at("ms_per_iter").as_double());
+        gto = std::max(gto, rj.at("chain_capped").at("gate_wait_timeouts").as_double());
       }
     if (ctasks >= 0) {
       Json c = Json::object();
       c["tasks_per_iter_max"] = ctasks;
       c["ms_per_iter_max"] = cms;
+      c["gate_wait_timeouts_max"] = gto;
       ext["chain_capped"] = c;
     }
   }

@@ -95,6 +95,21 @@ class DataParallel : public Strategy {
     comm_ = ctx.comms->create("dp/world", all, (zero_ ? shard_[0] * W_ : sizes_[0]) * es_, false, ctx.lane_ctas);
     compute_ = dev.create_stream(false);
     comm_stream_ = dev.create_stream(true);
+    // Comm gates (GPU deadline compute, plain DP): each backward bucket's
+    // compute raises a device gate word on the compute stream and the comm
+    // lane waits for it on the device before the bucket's all-reduce, instead
+    // of a cross-stream event. The replayed graph then has no edge from the
+    // compute chain into the comm chain until the end of the iteration, so the
+    // executor keeps each chain on one hardware queue: with event edges it
+    // rotated the backward GEMMs over its queues and queued one behind an
+    // all-reduce every 4 buckets (profiles/absorb_r4.md: the 5th of 8 waited
+    // for the 4th bucket's all-reduce). DLNB_DP_COMM_GATES=1 turns them on
+    // (opt-in until measured on hardware; default: event waits).
+    ComputeEngine& ce0 = *ctx.compute;
+    comm_gates_ = !zero_ && o.schedule != "reference" && env_int("DLNB_DP_COMM_GATES", 0) != 0 &&
+                  ce0.gates_task(fwd_us_);
+    if (comm_gates_)
+      for (int i = 0; i < nb_; ++i) g_ready_.push_back(ce0.make_gate());
     // Out-of-place like the reference unless asked (or forced by memory).
     size_t need = static_cast<size_t>(P_) * es_ * 2;
     in_place_ = o.in_place || (dev.kind() == DeviceKind::GPU && need > dev.free_memory() * 0.85);
@@ -210,10 +225,16 @@ class DataParallel : public Strategy {
     ComputeEngine& ce = *ctx.compute;
     ce.run(*compute_, fwd_us_, fwd_flops_);
     for (int i = 0; i < nb_; ++i) {
-      // only event records on compute_ since the forward: one stretch of compute
+      // only event records (or gate signals) on compute_ since the forward: one stretch of compute
       ce.run_chained(*compute_, bwd_us_[i], bwd_flops_[i]);
-      compute_->record(*ready_[i]);
-      comm_stream_->wait(*ready_[i]);
+      if (comm_gates_) {
+        ce.signal(*compute_, g_ready_[i]);
+        // bounded: 4x the bucket's compute + 1 s (never expected to expire)
+        ce.wait_gate(*comm_stream_, g_ready_[i], bwd_us_[i] * ctx.opt.time_scale * 4 + 1e6);
+      } else {
+        compute_->record(*ready_[i]);
+        comm_stream_->wait(*ready_[i]);
+      }
       int t = timers_->begin(*comm_stream_);
       void* out = in_place_ ? grads_[i].data() : sums_[i].data();
       comm_->all_reduce(grads_[i].data(), out, sizes_[i], ctx.wire, *comm_stream_);
@@ -251,6 +272,7 @@ class DataParallel : public Strategy {
     for (uint64_t s : sizes_) sd += (s - avg) * (s - avg);
     sd = std::sqrt(sd / nb_);
     Json g = Json::object();
+    g["comm_gates"] = comm_gates_;
     g["model_name"] = ctx.opt.model;
     g["num_buckets"] = nb_;
     g["local_batch_size"] = ctx.stats.batch_size;
@@ -304,6 +326,8 @@ class DataParallel : public Strategy {
   size_t es_ = 2;
   std::vector<uint64_t> sizes_;
   std::vector<double> bwd_us_;     // backward compute per bucket
+  bool comm_gates_ = false;  // backward buckets signal the comm lane through device gates
+  std::vector<int> g_ready_;
   std::vector<double> bwd_flops_;  // and its FLOPs
   double ratio_ = 1.0;
   double fwd_us_ = 0, bwd_us_per_bucket_ = 0, fwd_flops_ = 0, bwd_flops_per_bucket_ = 0;

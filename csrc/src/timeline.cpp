@@ -380,6 +380,8 @@ class TracingCompute : public ComputeEngine {
   bool gates_task(double us) const override { return in_->gates_task(us); }
   int make_gate() override { return in_->make_gate(); }
   void signal(Stream& s, int gate) override { in_->signal(s, gate); }
+  void wait_gate(Stream& s, int gate, double timeout_us) override { in_->wait_gate(s, gate, timeout_us); }
+  uint64_t gate_timeouts() override { return in_->gate_timeouts(); }
   void run_gated(Stream& s, double us, double flops, const std::vector<int>& gates, uint64_t* start,
                  bool chain) override {
     Json a = Json::object();

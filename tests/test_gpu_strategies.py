@@ -220,6 +220,21 @@ def test_dp_backward_buckets_chain_deadline(root):
     cc = d["chain_capped"]
     assert 0 <= cc["tasks_per_iter_max"] <= 8 and 0 <= cc["ms_per_iter_max"] < 0.3, cc
     assert d["compute"]["chain_absorb_us"] == pytest.approx(30.0, abs=0.02)
+    assert cc["gate_wait_timeouts_max"] == 0, cc
+
+
+@pytest.mark.parametrize("graph", [True, False])
+def test_dp_comm_gates_exact_and_bounded(graph, data_dir):
+    """DP with comm gates (each bucket's all-reduce waits on the device for its backward's gate), graph-replayed
+    and eager, several iterations: every gate wait is satisfied (none times out) and the step is the compute
+    floor plus at most the last bucket's exposed all-reduce and the iteration boundary."""
+    doc = engine.run_native("dp", "tiny_dense_8_bfloat16", 4, base_path=data_dir, warmup=2, runs=6, compute="gemm",
+                            backend="rccl", graph=graph, quiet=True, env={"DLNB_DP_COMM_GATES": "1"})
+    d = doc["global"]["dlnb"]
+    assert doc["global"]["comm_gates"] is True
+    assert d["chain_capped"]["gate_wait_timeouts_max"] == 0, d["chain_capped"]
+    it = d["iteration"]
+    assert it["compute_floor_ms"] <= it["median_ms"] < it["compute_floor_ms"] + 1.0, it
 
 
 def test_runs_bind_the_bench_runtime(data_dir, root):
