@@ -836,7 +836,11 @@ template <bool BF>
 void launch_4wave(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, void* stream) {
   constexpr int esz = BF ? 2 : 1;
   const int tiles = (M / kT) * (N / kT);
-  constexpr int group = 8;  // M-tiles sharing B panels in L2 (4 / 8 / 16 / 32 measured: 8 best)
+  // M-tiles sharing B panels in L2. fp8: 4 (round 4, profiles/gemm_group_r4.md: 3 / 4 / 6 / 8 interleaved -
+  // 4 at or above 8 on every shape, +9 % at short K, where 8 re-read 15-37 % more operand panels from HBM than
+  // the vendor); bf16 on this kernel keeps 8. DLNB_GEMM_GROUP overrides (A/B, read per launch).
+  const char* genv = std::getenv("DLNB_GEMM_GROUP");
+  const int group = genv && std::atoi(genv) > 0 ? std::atoi(genv) : (BF ? 8 : 4);
   // more tiles than CUs: the streaming persistent kernel, one block per CU
   // (+1-5 %, profiles/gemm_bench_r2.md); else a block per tile
   static const int cus = [] {

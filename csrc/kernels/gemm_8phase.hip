@@ -24,6 +24,8 @@
 // Variant 3 of dlnb::kernels::gemm_tn (the library's one-shot GEMM).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "deadline_sync.hpp"
 #include "dlnb/kernels.hpp"
 #include "store_pair.hpp"
@@ -628,7 +630,9 @@ void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, 
                     void* stream) {
   DLNB_REQUIRE(gemm_8phase_shape_ok(M, N, K, in_t), "gemm 8-phase: unsupported shape M=" << M << " N=" << N << " K=" << K);
   const int tiles = (M / kT) * (N / kT);
-  constexpr int group = 8;  // M-tiles per L2 group of the tile order
+  // M-tiles per L2 group of the tile order; DLNB_GEMM_GROUP overrides (A/B, read per launch)
+  const char* genv = std::getenv("DLNB_GEMM_GROUP");
+  const int group = genv && std::atoi(genv) > 0 ? std::atoi(genv) : 8;
   hipStream_t st = static_cast<hipStream_t>(stream);
   auto* a = static_cast<const char*>(A);
   auto* b = static_cast<const char*>(B);
@@ -645,7 +649,7 @@ void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, 
                        nullptr, 0u, 0ull, 0ull, DlSync(), group);
   } else {
     hipLaunchKernelGGL((gemm_8phase_kernel<false, false>), tiles, 512, 0, st, a, b, cc, M, N, K, lda, ldb, ldc, nullptr,
-                       0u, 0ull, 0ull, DlSync());
+                       0u, 0ull, 0ull, DlSync(), group);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 8-phase launch failed: " << hipGetErrorString(e));
