@@ -86,6 +86,9 @@ bool gemm_4wave_fp8_shape_ok(int M, int N, int K, DType in_t);
 // kernels) a one-shot GEMM of an M x N output uses on `cus` CUs: narrower
 // tiles when the square ones leave CUs idle - fewer tiles than CUs, or a last
 // round at least 10 % short (gemm_4wave_fp8.hip, narrow kernel).
+// M-tiles per group of the one-shot GEMMs' tile order (groups walk the N-tiles
+// together and share B panels in L2): 4, or DLNB_GEMM_GROUP (read per call).
+int gemm_group();
 int gemm_narrow_nf(int M, int N, int cus);
 // The narrow-tile one-shot GEMM (bf16 or fp8, K * elem_size % 256 == 0); false
 // (nothing launched) when gemm_narrow_nf picks the square tile or the shape

@@ -761,6 +761,12 @@ bool gemm_4wave_fp8_shape_ok(int M, int N, int K, DType in_t) {
   return in_t == DType::FP8_E4M3 && gemm_shape_ok(M, N, K, in_t) && K % 256 == 0 && K >= 256;
 }
 
+int gemm_group() {
+  const char* env = std::getenv("DLNB_GEMM_GROUP");
+  const int g = env ? std::atoi(env) : 0;
+  return g > 0 ? g : 4;
+}
+
 int gemm_narrow_nf(int M, int N, int cus) {
   // Tile width 32 nf: the fewest rounds of tile work per CU, ceil(tiles / CUs)
   // x nf (a tile's time ~ its width), ties to the wider tile. Fewer square
@@ -801,7 +807,7 @@ bool gemm_tn_narrow(const void* A, const void* B, void* C, int M, int N, int K, 
   if (!gemm_shape_ok(M, N, K, in_t) || kbytes % 256 != 0) return false;  // an even K-tile count
   const int nf = gemm_narrow_nf(M, N, cus);
   if (nf == 8) return false;
-  constexpr int group = 8;
+  const int group = gemm_group();
   const int nt = (M / kT) * (N / (32 * nf));
   auto* a = static_cast<const char*>(A);
   auto* b = static_cast<const char*>(B);
@@ -836,11 +842,10 @@ template <bool BF>
 void launch_4wave(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, void* stream) {
   constexpr int esz = BF ? 2 : 1;
   const int tiles = (M / kT) * (N / kT);
-  // M-tiles sharing B panels in L2. fp8: 4 (round 4, profiles/gemm_group_r4.md: 3 / 4 / 6 / 8 interleaved -
-  // 4 at or above 8 on every shape, +9 % at short K, where 8 re-read 15-37 % more operand panels from HBM than
-  // the vendor); bf16 on this kernel keeps 8. DLNB_GEMM_GROUP overrides (A/B, read per launch).
-  const char* genv = std::getenv("DLNB_GEMM_GROUP");
-  const int group = genv && std::atoi(genv) > 0 ? std::atoi(genv) : (BF ? 8 : 4);
+  // M-tiles sharing B panels in L2: 4 (round 4, profiles/gemm_group_r4.md: 3 / 4 / 6 / 8 interleaved - 4 at or
+  // above 8 on every fp8 shape, +9 % at short K, where 8 re-read 15-37 % more operand panels from HBM than the
+  // vendor). DLNB_GEMM_GROUP overrides (A/B, read per launch).
+  const int group = gemm_group();
   // more tiles than CUs: the streaming persistent kernel, one block per CU
   // (+1-5 %, profiles/gemm_bench_r2.md); else a block per tile
   static const int cus = [] {

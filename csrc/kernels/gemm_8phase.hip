@@ -630,9 +630,7 @@ void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, 
                     void* stream) {
   DLNB_REQUIRE(gemm_8phase_shape_ok(M, N, K, in_t), "gemm 8-phase: unsupported shape M=" << M << " N=" << N << " K=" << K);
   const int tiles = (M / kT) * (N / kT);
-  // M-tiles per L2 group of the tile order; DLNB_GEMM_GROUP overrides (A/B, read per launch)
-  const char* genv = std::getenv("DLNB_GEMM_GROUP");
-  const int group = genv && std::atoi(genv) > 0 ? std::atoi(genv) : 8;
+  const int group = gemm_group();  // M-tiles per L2 group of the tile order (4; DLNB_GEMM_GROUP)
   hipStream_t st = static_cast<hipStream_t>(stream);
   auto* a = static_cast<const char*>(A);
   auto* b = static_cast<const char*>(B);
