@@ -653,6 +653,13 @@ void gemm_tn_8phase(const void* A, const void* B, void* C, int M, int N, int K, 
   if (e != hipSuccess) DLNB_THROW("gemm 8-phase launch failed: " << hipGetErrorString(e));
 }
 
+// Tile-order group of the per-tile deadline kernels (8; DLNB_DEADLINE_GROUP, A/B knob read per launch).
+static int deadline_group() {
+  const char* env = std::getenv("DLNB_DEADLINE_GROUP");
+  const int g = env ? std::atoi(env) : 0;
+  return g > 0 ? g : 8;
+}
+
 void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
                              uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end,
                              const DlSync& sync) {
@@ -678,13 +685,13 @@ void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N
                        ticks, slice_end, sync);
   } else if (in_t == DType::BF16 && nk % 2 == 0) {
     hipLaunchKernelGGL((gemm_8phase_kernel<false, true, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot,
-                       epoch, ticks, slice_end, sync);
+                       epoch, ticks, slice_end, sync, deadline_group());
   } else if (in_t == DType::BF16) {
     hipLaunchKernelGGL((gemm_8phase_kernel<false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
-                       ticks, slice_end, sync);
+                       ticks, slice_end, sync, deadline_group());
   } else {
     hipLaunchKernelGGL((gemm_8phase_kernel<true, true, false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot,
-                       epoch, ticks, slice_end, sync);
+                       epoch, ticks, slice_end, sync, deadline_group());
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 8-phase deadline launch failed: " << hipGetErrorString(e));
