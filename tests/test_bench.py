@@ -318,3 +318,30 @@ def test_bench_torchrun_xgmi_two_ranks_one_gpu(tmp_path):
     for k in ("xgmi", "xgmi_registered"):
         assert "error" not in lb[k], lb
         assert all(lb[k][op]["1048576"]["busbw_GBps"] > 0 for op in ("all_reduce", "all_gather", "sendrecv"))
+
+
+@pytest.mark.gpu
+def test_bench_headline_fallback_two_ranks_one_gpu(tmp_path):
+    """The driver's N > 1 launch with the default backend on a job where RCCL cannot form its communicator
+    (2 ranks sharing GPU 0 - what a first cross-device RCCL failure looks like to bench.py): the exactness pass
+    proves only the xgmi kernels, so the headline runs as a bounded child on RCCL, fails, and is timed on xgmi;
+    the line has a value, names the fallback and keeps the RCCL error (profiles/fallback_r4.md)."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--devices", "0,0", "--link-sizes", "1048576",
+           "--wall-budget-s", "240"] + TINY
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=str(tmp_path),
+                       env=dict(os.environ, DLNB_XGMI_TIMEOUT_S="60"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    o = lines[0]
+    assert o["value"] > 0 and "error" not in o, o.get("error")
+    fb = o["headline_fallback"]
+    assert fb["backend"] == "xgmi" and "ncclCommInitRank" in fb["primary_error"] and "error" not in fb, fb
+    assert o["config"]["backend"] == "XGMI" and o["verified"] == {"xgmi": True}
+    assert o["comm_bound"]["ms_per_step"] > 0 and o["comm_bound"]["backend"] == "XGMI"
+    assert o["phase_seconds"]["total"] <= 240
