@@ -120,6 +120,12 @@ class Device {
   virtual uint64_t* alloc_stamps(size_t n) = 0;  // zeroed, host-readable
   virtual void free_stamps(uint64_t* p, size_t n) = 0;
   virtual void stamp(Stream& s, uint64_t* slot) = 0;
+  // Handshake words (alloc_stamps memory) between the host and a stream:
+  // host_signal stores value when the stream reaches it; host_wait holds the
+  // stream until the host (or a signal) stored a value >= `value`, at most
+  // timeout_s (then it adds 1 to *timeouts and lets the stream go). GPU only.
+  virtual void host_signal(Stream& s, uint64_t* word, uint64_t value);
+  virtual void host_wait(Stream& s, const uint64_t* word, uint64_t value, double timeout_s, uint64_t* timeouts);
   virtual double stamp_hz() const = 0;
   virtual size_t total_memory() const = 0;
   virtual size_t free_memory() const = 0;

@@ -53,10 +53,22 @@ void gate_wait(const uint64_t* gate, uint32_t tag, uint64_t timeout_ticks, uint6
 // wallclock_hz()).
 void idle_wait(uint64_t ticks, void* stream);
 void busy_spin(uint64_t ticks, int blocks, void* stream);
+// The deadline clock's rate in Hz: measured against the host's steady clock
+// once per process (clock_cal_begin starts the window - the GPU device does
+// at creation - and the first wallclock_hz call ends it, sleeping until
+// DLNB_CLOCK_CAL_MS (500) have passed; 0 = the attribute's nominal rate).
 double wallclock_hz(int device);
+double wallclock_hz_nominal(int device);
+void clock_cal_begin(int device);
 // One wave stores s_memrealtime into *slot (host-mapped memory) when the
 // stream reaches this point.
 void stamp(uint64_t* slot, void* stream);
+// Host <-> stream handshake words in host-coherent memory (system scope):
+// host_signal stores `value`; host_wait holds the stream until *word >= value
+// (one wave spinning with s_sleep; after timeout_ticks it gives up and adds
+// one to *timeouts, so the stream always drains).
+void host_signal(uint64_t* word, uint64_t value, void* stream);
+void host_wait(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uint64_t* timeouts, void* stream);
 int num_cus(int device);
 
 // GEMM: requires M % 256 == 0, N % 256 == 0, K*elem_size % 128 == 0, leading

@@ -138,6 +138,23 @@ int main_for(StrategyKind kind, int argc, char** argv);
 // errors so a dead peer aborts the job instead of hanging it.
 void sync_streams(const std::vector<Stream*>& streams, const std::vector<Communicator*>& comms, Device& dev);
 
+// While alive on this thread: sync_streams() waits for *flag >= value (a
+// host-coherent word a kernel enqueued after the replayed graph stores)
+// instead of querying the streams - the graph joins every stream it forked
+// back onto its launch stream before that kernel runs, so the word proves the
+// whole iteration complete (runner's pre-armed graph loop).
+class CompletionFlag {
+ public:
+  CompletionFlag(const uint64_t* flag, uint64_t value);
+  ~CompletionFlag();
+  CompletionFlag(const CompletionFlag&) = delete;
+  CompletionFlag& operator=(const CompletionFlag&) = delete;
+
+ private:
+  const uint64_t* prev_;
+  uint64_t prev_value_;
+};
+
 // Helper shared by the drivers: a stats summary for bus-bandwidth reporting.
 struct CommStat {
   std::string name;

@@ -68,6 +68,11 @@ class Timeline {
   // as a span on a "host" track: host span - device span = the iteration
   // boundary (launch + completion detection).
   void host_iteration(int iter, double t0_s, double t1_s);
+  // Graph mode: a stamp on the launch stream right before (which = 0) and
+  // right after (1) the graph launch, outside the graph, so host_iteration()
+  // can split the boundary into submission, the graph's start, its join back
+  // onto the launch stream and the host's completion detection.
+  void edge(Stream& s, int which);
   // This rank's events of the last `keep_iters` collected iterations
   // (0 = all): {"rank", "lanes", "events": [[iter, lane, cat, name, ts_us,
   // dur_us, args], ...], "calibration_error_us", "truncated"}; ts_us on the
@@ -99,7 +104,7 @@ class Timeline {
   std::vector<Event> events_;
   std::map<const void*, int> lanes_;
   std::vector<std::string> lane_names_;
-  bool frozen_ = false, truncated_ = false;
+  bool frozen_ = false, truncated_ = false, edges_ = false;
   double hz_ = 1e9;
   double host_cal_us_ = 0.0, cal_err_us_ = 0.0;
   uint64_t tick_cal_ = 0;

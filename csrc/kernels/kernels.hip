@@ -3,6 +3,11 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include "dlnb/common.hpp"
+#include <thread>
+#include <mutex>
+#include <cmath>
+#include <chrono>
 
 #include "deadline_sync.hpp"
 #include "dlnb/kernels.hpp"
@@ -126,6 +131,23 @@ __global__ void gate_wait_kernel(const uint64_t* gate, uint32_t tag, uint64_t ti
       __builtin_amdgcn_s_sleep(2);
       if (__builtin_amdgcn_s_memrealtime() - w0 > timeout_ticks) {
         __hip_atomic_fetch_add(timeouts, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+}
+
+__global__ void host_signal_kernel(uint64_t* word, uint64_t value) {
+  if (threadIdx.x == 0) __hip_atomic_store(word, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void host_wait_kernel(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uint64_t* timeouts) {
+  if (threadIdx.x == 0) {
+    const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < value) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - w0 > timeout_ticks) {
+        __hip_atomic_fetch_add(timeouts, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
     }
@@ -487,6 +509,18 @@ void gate_wait(const uint64_t* gate, uint32_t tag, uint64_t timeout_ticks, uint6
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
+void host_signal(uint64_t* word, uint64_t value, void* stream) {
+  DLNB_REQUIRE(word != nullptr, "host_signal: null word");
+  hipLaunchKernelGGL(host_signal_kernel, 1, 64, 0, S(stream), word, value);
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
+void host_wait(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uint64_t* timeouts, void* stream) {
+  DLNB_REQUIRE(word != nullptr && timeouts != nullptr, "host_wait: null word");
+  hipLaunchKernelGGL(host_wait_kernel, 1, 64, 0, S(stream), word, value, timeout_ticks, timeouts);
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
 void stamp(uint64_t* slot, void* stream) {
   hipLaunchKernelGGL(stamp_kernel, 1, 64, 0, S(stream), slot);
   DLNB_HIP_CHECK(hipGetLastError());
@@ -497,10 +531,100 @@ void busy_spin(uint64_t ticks, int blocks, void* stream) {
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
-double wallclock_hz(int device) {
+double wallclock_hz_nominal(int device) {
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) khz = 100000;
   return static_cast<double>(khz) * 1e3;
+}
+
+namespace {
+// The s_memrealtime clock's rate against the host's steady clock, measured
+// once per process and device: a reading pairs one stamp with the midpoint of
+// the tightest of 16 host brackets (launch + stream synchronize, ~5.5 us
+// half-width); two readings >= DLNB_CLOCK_CAL_MS (500) apart. The MI355X's
+// 100 MHz reference ran 7.6 ppm slow on the box measured (-7.63..-7.70 ppm at
+// 0.5..15.5 s windows, profiles/host_boundary_r4.md): a deadline task timed
+// in nominal ticks then lasted 21 us longer than the table time per headline
+// iteration; with the measured rate the tasks last the table time in host
+// (wall-clock) time, whichever way the box's crystal is off.
+struct ClockCal {
+  std::mutex mu;
+  bool begun = false, done = false;
+  double hz = 0.0, host_us = 0.0;
+  uint64_t tick = 0;
+};
+ClockCal& clock_cal(int device) {
+  static ClockCal c[64];
+  return c[device & 63];
+}
+double steady_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+void read_clock(int device, double* host_us, uint64_t* tick) {
+  int prev = 0;
+  DLNB_HIP_CHECK(hipGetDevice(&prev));
+  DLNB_HIP_CHECK(hipSetDevice(device));
+  hipStream_t s{};
+  DLNB_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  void* p = nullptr;
+  DLNB_HIP_CHECK(hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  uint64_t* slot = static_cast<uint64_t*>(p);
+  double best = 1e30;
+  for (int i = 0; i < 16; ++i) {
+    const double h0 = steady_us();
+    hipLaunchKernelGGL(stamp_kernel, 1, 64, 0, s, slot);
+    DLNB_HIP_CHECK(hipStreamSynchronize(s));
+    const double h1 = steady_us();
+    if (h1 - h0 < best) {
+      best = h1 - h0;
+      *host_us = 0.5 * (h0 + h1);
+      *tick = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
+    }
+  }
+  DLNB_HIP_CHECK(hipHostFree(p));
+  DLNB_HIP_CHECK(hipStreamDestroy(s));
+  DLNB_HIP_CHECK(hipSetDevice(prev));
+}
+void clock_cal_begin_locked(int device, ClockCal& c) {
+  c.begun = true;
+  if (env_int("DLNB_CLOCK_CAL_MS", 500) <= 0) {
+    c.hz = wallclock_hz_nominal(device);
+    c.done = true;
+    return;
+  }
+  read_clock(device, &c.host_us, &c.tick);
+}
+}  // namespace
+
+void clock_cal_begin(int device) {
+  ClockCal& c = clock_cal(device);
+  std::lock_guard<std::mutex> g(c.mu);
+  if (!c.begun) clock_cal_begin_locked(device, c);
+}
+
+double wallclock_hz(int device) {
+  ClockCal& c = clock_cal(device);
+  std::lock_guard<std::mutex> g(c.mu);
+  if (c.done) return c.hz;
+  if (!c.begun) clock_cal_begin_locked(device, c);
+  if (c.done) return c.hz;
+  const double window_us = static_cast<double>(env_int("DLNB_CLOCK_CAL_MS", 500)) * 1e3;
+  const double waited = steady_us() - c.host_us;
+  if (waited < window_us) std::this_thread::sleep_for(std::chrono::duration<double, std::micro>(window_us - waited));
+  double h = 0.0;
+  uint64_t t = 0;
+  read_clock(device, &h, &t);
+  const double nominal = wallclock_hz_nominal(device);
+  const double hz = static_cast<double>(t - c.tick) / ((h - c.host_us) * 1e-6);
+  if (t > c.tick && h > c.host_us && std::fabs(hz / nominal - 1.0) < 200e-6) {
+    c.hz = hz;
+  } else {  // a preempted reading, or not the clock we think: keep the attribute's rate
+    std::fprintf(stderr, "[dlnb] warning: device %d clock measured at %.1f Hz vs %.0f nominal; using nominal\n", device,
+                 hz, nominal);
+    c.hz = nominal;
+  }
+  c.done = true;
+  return c.hz;
 }
 
 int num_cus(int device) {

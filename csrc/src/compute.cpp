@@ -77,8 +77,10 @@ class GpuCompute : public ComputeEngine {
  public:
   GpuCompute(Device& dev, ComputeMode mode, const ComputeShape& shape, double scale)
       : dev_(dev), mode_(mode), scale_(scale) {
-    hz_ = kernels::wallclock_hz(dev.index());
-    absorb_ticks_ = static_cast<uint32_t>(std::max<uint64_t>(ticks(static_cast<double>(env_int("DLNB_CHAIN_ABSORB_US", 30))), 1));
+    // (the rate itself is taken at the first task, kernels::wallclock_hz; the
+    // absorb cap needs no ppm)
+    absorb_ticks_ = static_cast<uint32_t>(std::max<double>(
+        static_cast<double>(env_int("DLNB_CHAIN_ABSORB_US", 30)) * 1e-6 * kernels::wallclock_hz_nominal(dev.index()), 1.0));
     cus_ = kernels::num_cus(dev.index());
     dtype_ = shape.dtype == DType::FP8_E4M3 ? DType::FP8_E4M3 : DType::BF16;
     // The stand-in is the layer's FFN down projection, C[tokens, hidden] =
@@ -151,7 +153,7 @@ class GpuCompute : public ComputeEngine {
     dev_.copy_async(v, capped_.data(), sizeof(v), *st);
     st->synchronize();
     tasks = v[0];
-    seconds = static_cast<double>(v[1]) / hz_;
+    seconds = static_cast<double>(v[1]) / hz();
     return true;
   }
 
@@ -286,14 +288,15 @@ class GpuCompute : public ComputeEngine {
     Json j = Json::object();
     j["mode"] = compute_mode_name(mode_);
     j["time_scale"] = scale_;
-    j["wallclock_hz"] = hz_;
+    j["wallclock_hz"] = hz();
+    j["wallclock_hz_nominal"] = kernels::wallclock_hz_nominal(dev_.index());
     j["num_cus"] = cus_;
     if (mode_ == ComputeMode::Gemm) {
       j["deadline_grid"] = grid_;
       j["comm_reserved_cus"] = cus_ - grid_;
       j["deadline_slice_us"] = slice_us_;
       j["chained_tasks"] = chained_;  // enqueued so far (a captured graph counts its one iteration)
-      j["chain_absorb_us"] = absorb_ticks_ / hz_ * 1e6;  // most lateness a chained / gated task absorbs
+      j["chain_absorb_us"] = absorb_ticks_ / hz() * 1e6;  // most lateness a chained / gated task absorbs
       j["gated_tasks"] = gated_;      // tasks that waited on device gates instead of stream events
     }
     if (A_.data()) {
@@ -317,7 +320,11 @@ class GpuCompute : public ComputeEngine {
   ComputeMode mode() const override { return mode_; }
 
  private:
-  uint64_t ticks(double us) const { return static_cast<uint64_t>(us * 1e-6 * hz_ + 0.5); }
+  uint64_t ticks(double us) const { return static_cast<uint64_t>(us * 1e-6 * hz() + 0.5); }
+  double hz() const {
+    if (hz_ <= 0.0) hz_ = kernels::wallclock_hz(dev_.index());
+    return hz_;
+  }
 
   // One deadline task of d us on s (every slice launch carries the same
   // epoch; the kernels agree its start through the stream's slot line,
@@ -447,7 +454,7 @@ class GpuCompute : public ComputeEngine {
   long gated_ = 0;
   int grid_ = 256;
   double slice_us_ = 500;
-  double hz_ = 1e8;
+  mutable double hz_ = 0.0;  // hz()
   int cus_ = 256;
   DType dtype_ = DType::BF16;
   int K_ = 4096, N_ = 16384;

@@ -329,6 +329,11 @@ std::unique_ptr<GraphExec> Device::capture(Stream&, const std::vector<Stream*>&,
   DLNB_THROW("--graph needs a GPU device (HIP graphs)");
 }
 
+void Device::host_signal(Stream&, uint64_t*, uint64_t) { DLNB_THROW("host_signal needs a GPU device"); }
+void Device::host_wait(Stream&, const uint64_t*, uint64_t, double, uint64_t*) {
+  DLNB_THROW("host_wait needs a GPU device");
+}
+
 std::string cpu_peer_source(const void* p) {
   std::lock_guard<std::mutex> g(peer_mu());
   auto it = peer_fds().find(p);

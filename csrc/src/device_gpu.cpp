@@ -90,7 +90,7 @@ class GpuDevice : public Device {
     name_ = prop.name;
     arch_ = prop.gcnArchName;
     total_ = prop.totalGlobalMem;
-    hz_ = kernels::wallclock_hz(idx_);
+    kernels::clock_cal_begin(idx_);  // the rate is taken at its first use (stamp_hz), after setup
   }
   DeviceKind kind() const override { return DeviceKind::GPU; }
   std::string name() const override { return name_ + " (" + arch_ + ")"; }
@@ -151,7 +151,11 @@ class GpuDevice : public Device {
   }
   void free_stamps(uint64_t* p, size_t) override { (void)hipHostFree(p); }
   void stamp(Stream& s, uint64_t* slot) override { kernels::stamp(slot, s.native()); }
-  double stamp_hz() const override { return hz_; }
+  void host_signal(Stream& s, uint64_t* word, uint64_t value) override { kernels::host_signal(word, value, s.native()); }
+  void host_wait(Stream& s, const uint64_t* word, uint64_t value, double timeout_s, uint64_t* timeouts) override {
+    kernels::host_wait(word, value, static_cast<uint64_t>(timeout_s * stamp_hz()), timeouts, s.native());
+  }
+  double stamp_hz() const override { return kernels::wallclock_hz(idx_); }
   size_t total_memory() const override { return total_; }
   size_t free_memory() const override {
     size_t f = 0, t = 0;

@@ -267,7 +267,7 @@ void Json::dump_to(std::string& out, int indent, int depth) const {
         out += "null";
       } else {
         char buf[64];
-        std::snprintf(buf, sizeof(buf), "%.9g", n_);
+        std::snprintf(buf, sizeof(buf), "%.12g", n_);  // 1e-5 us at a 10-s timeline offset
         out += buf;
       }
       break;

@@ -9,6 +9,7 @@
 // divides a world-sum by the warm-up count, cpp/utils.hpp:127-128) and takes
 // the max over ranks; loop mode is a run-time flag (or a *_loop argv[0]).
 #include <algorithm>
+#include <exception>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -33,6 +34,20 @@ extern char** environ;
 
 namespace dlnb {
 
+namespace {
+thread_local const uint64_t* t_done_flag = nullptr;
+thread_local uint64_t t_done_value = 0;
+}  // namespace
+
+CompletionFlag::CompletionFlag(const uint64_t* flag, uint64_t value) : prev_(t_done_flag), prev_value_(t_done_value) {
+  t_done_flag = flag;
+  t_done_value = value;
+}
+CompletionFlag::~CompletionFlag() {
+  t_done_flag = prev_;
+  t_done_value = prev_value_;
+}
+
 void sync_streams(const std::vector<Stream*>& streams, const std::vector<Communicator*>& comms, Device& dev) {
   (void)dev;
   // Poll period: with the default 50-us timer slack a 20-us sleep woke ~70 us
@@ -47,8 +62,11 @@ void sync_streams(const std::vector<Stream*>& streams, const std::vector<Communi
   const double timeout = static_cast<double>(env_int("DLNB_TIMEOUT", 900));
   const double t0 = now_s();
   int polls = 0;
+  const uint64_t* flag = t_done_flag;
+  const uint64_t want = t_done_value;
+  auto done = [&](Stream* s) { return flag ? __atomic_load_n(flag, __ATOMIC_ACQUIRE) >= want : s->query(); };
   for (Stream* s : streams) {
-    while (!s->query()) {
+    while (!done(s)) {
       if (++polls % 64 == 0) {
         for (Communicator* c : comms) {
           if (!c) continue;
@@ -533,6 +551,9 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     DLNB_REQUIRE(ctx.dev->kind() == DeviceKind::CPU, "DLNB_INJECT_FAULT mode=task needs a CPU device");
     ctx.dev->host_task(*strat->streams()[0], [] { DLNB_THROW("injected fault in a stream task"); });
   };
+  // the deadline clock's measured rate (kernels::wallclock_hz): taken here,
+  // after setup gave its window time, and never inside a graph capture
+  if (ctx.dev->kind() == DeviceKind::GPU) (void)ctx.dev->stamp_hz();
   Timeline* TL = ctx.timeline.get();
   if (TL) TL->calibrate(*strat->streams()[0]);
   TimerSet& T = *strat->timers();
@@ -617,17 +638,65 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     return doc;
   }
 
+  // DLNB_TIMELINE_EDGES=1 (with --timeline --graph): a stamp kernel on the
+  // launch stream before and after each timed graph launch (Timeline::edge;
+  // two more kernels per iteration, so off by default)
+  const bool tl_edges = env_int("DLNB_TIMELINE_EDGES", 0) != 0;
+  // Graph replays on a GPU (DLNB_PREARM=1, the default): the host runs one
+  // launch ahead. Iteration r+1's graph is enqueued while r runs, behind a
+  // one-wave kernel that holds the launch stream until the host stores r+2 in
+  // a host-coherent "go" word; a kernel after each graph stores r+1 in a
+  // "done" word the host polls (CompletionFlag). Each iteration is still
+  // timed alone, from the go store to the host seeing its done word, but its
+  // start no longer waits for hipGraphLaunch's submission after an idle
+  // device (~70 us) and its end not for hipStreamQuery (~20 us)
+  // (profiles/host_boundary_r4.md). Iteration 0 is armed before the timed
+  // region starts (as the last warm-up iteration would in a longer loop); all
+  // of its device work runs inside it, as does the loop's closing device
+  // synchronize. DLNB_PREARM=0: launch, then poll the streams (A/B).
+  uint64_t* hs = nullptr;  // [0] go, [1] done, [2] go-wait timeouts
+  if (graph && ctx.dev->kind() == DeviceKind::GPU && env_int("DLNB_PREARM", 1) != 0) hs = ctx.dev->alloc_stamps(3);
+  struct Handshake {
+    Device& d;
+    uint64_t*& p;
+    ~Handshake() {
+      if (!p) return;
+      if (std::uncaught_exceptions() == 0) {
+        d.free_stamps(p, 3);
+      } else {  // release any armed graph (not freed: hipHostFree waits for the device, which may be hung)
+        __atomic_store_n(p, ~0ull, __ATOMIC_RELEASE);
+      }
+    }
+  } handshake{*ctx.dev, hs};
+  const double go_timeout_s = 30.0;
+  auto arm = [&](int r) {
+    ctx.dev->host_wait(*origin, hs, static_cast<uint64_t>(r) + 1, go_timeout_s, hs + 2);
+    if (TL && tl_edges) TL->edge(*origin, 0);
+    graph->launch(*origin);
+    if (TL && tl_edges) TL->edge(*origin, 1);
+    ctx.dev->host_signal(*origin, hs + 1, static_cast<uint64_t>(r) + 1);
+  };
   ctx.hg().barrier();
   ctx.compute->reset_capped(*strat->streams()[0]);  // count the timed iterations only
   ctx.dev->synchronize();
+  if (hs && runs > 0) arm(0);  // submitted, held until the first go
   const double T0 = now_s();
   for (int r = 0; r < runs; ++r) {
     fault.at_iteration(iter_no++, inject_task);
     TraceRange tr("dlnb:iteration");
     const double j0 = meter->joules();
     double t0 = now_s();
-    enqueue();
-    strat->synchronize();
+    if (hs) {
+      __atomic_store_n(hs, static_cast<uint64_t>(r) + 1, __ATOMIC_RELEASE);  // go
+      if (r + 1 < runs) arm(r + 1);
+      CompletionFlag cf(hs + 1, static_cast<uint64_t>(r) + 1);
+      strat->synchronize();
+    } else {
+      if (TL && graph && tl_edges) TL->edge(*origin, 0);
+      enqueue();
+      if (TL && graph && tl_edges) TL->edge(*origin, 1);
+      strat->synchronize();
+    }
     const double t1 = now_s();
     T.add(rkey, t1 - t0);
     if (TL) {
@@ -642,6 +711,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
 
   // ---- report
   Json rank = strat->rank_json();
+  if (hs) rank["prearm_go_timeouts"] = static_cast<double>(__atomic_load_n(hs + 2, __ATOMIC_ACQUIRE));
   rank["energy_consumed"] = T.values_json("energy_consumed");
   {
     // chained deadline tasks that waited longer than the absorb cap (deadline_sync.hpp)

@@ -12,7 +12,6 @@ namespace dlnb {
 
 Timeline::Timeline(Device& dev, size_t cap, size_t max_events) : dev_(dev), cap_(cap), max_events_(max_events) {
   stamps_ = dev_.alloc_stamps(cap_);
-  hz_ = dev_.stamp_hz();
 }
 
 Timeline::~Timeline() {
@@ -35,7 +34,7 @@ void Timeline::label(Stream& s, const std::string& name) {
 }
 
 int Timeline::begin(Stream& s) {
-  if (frozen_ || next_ + 3 > cap_) {  // 2 for the span; the last slot is calibrate()'s
+  if (frozen_ || next_ + 5 > cap_) {  // 2 for the span; the last 3 slots are calibrate()'s and edge()'s
     if (!frozen_) truncated_ = true;
     return -1;
   }
@@ -46,7 +45,7 @@ int Timeline::begin(Stream& s) {
 
 int Timeline::begin_external(uint64_t** slot) {
   *slot = nullptr;
-  if (frozen_ || next_ + 3 > cap_) {
+  if (frozen_ || next_ + 5 > cap_) {
     if (!frozen_) truncated_ = true;
     return -1;
   }
@@ -111,9 +110,30 @@ void Timeline::host_iteration(int iter, double t0_s, double t1_s) {
     return static_cast<uint64_t>(static_cast<double>(tick_cal_) + d);
   };
   events_.push_back(Event{iter, lane, "host", "iteration (host)", Json::object(), tick(t0_s), tick(t1_s)});
+  if (edges_) {
+    static const int kEdgeLaneKey = 0;
+    auto ie = lanes_.find(&kEdgeLaneKey);
+    if (ie == lanes_.end()) {
+      lane = static_cast<int>(lane_names_.size());
+      lanes_[&kEdgeLaneKey] = lane;
+      lane_names_.push_back("graph launch edges");
+    } else {
+      lane = ie->second;
+    }
+    const uint64_t e0 = __atomic_load_n(stamps_ + cap_ - 2, __ATOMIC_ACQUIRE);
+    const uint64_t e1 = __atomic_load_n(stamps_ + cap_ - 3, __ATOMIC_ACQUIRE);
+    events_.push_back(Event{iter, lane, "edge", "before graph launch", Json::object(), e0, e0});
+    events_.push_back(Event{iter, lane, "edge", "after graph launch", Json::object(), e1, e1});
+  }
+}
+
+void Timeline::edge(Stream& s, int which) {
+  dev_.stamp(s, stamps_ + cap_ - 2 - (which ? 1 : 0));
+  edges_ = true;
 }
 
 void Timeline::calibrate(Stream& s) {
+  hz_ = dev_.stamp_hz();  // here, not at construction: the rate's measuring window ends at its first use
   // The stamp lands between the two host reads; the best of a few tries
   // (shortest bracket) pairs the clocks.
   double best = std::numeric_limits<double>::max();
@@ -142,7 +162,7 @@ Json Timeline::rank_json(int rank, int keep_iters) const {
     return host_cal_us_ + (static_cast<double>(t) - static_cast<double>(tick_cal_)) / hz_ * 1e6;
   };
   // Times go out relative to an integer origin (ns on the host clock): the
-  // JSON writer keeps 9 significant digits, ~100 us of an absolute clock.
+  // JSON writer keeps 12 significant digits, ~0.1 us of an absolute clock.
   long long origin_ns = 0;
   for (const auto& e : events_)
     if (e.iter >= first) {

@@ -1,9 +1,14 @@
 """Accuracy of the device-clock deadline kernels (idle wait, busy spin, MFMA GEMM).
 
     python -m dlnetbench_amd.tools.clock_check [--us 29320]
+    python -m dlnetbench_amd.tools.clock_check --long-ms 2000 [--reps 5]
 
 For each kernel: launch it back to back, time with HIP events and with the
 host clock, print the relative error against the requested duration as JSON.
+--long-ms: one idle wait of that length per rep, each bracketed by host
+synchronizes, so a rate error of the deadline clock (kernels::wallclock_hz)
+shows as ppm of host time (10 ppm = 20 us at 2 s; the launch + sync overhead,
+~10-20 us, is the offset measured with a 1 ms wait).
 """
 from __future__ import annotations
 
@@ -11,6 +16,29 @@ import argparse
 import json
 import statistics
 import time
+
+
+def _long(a) -> int:
+    import torch
+    from dlnetbench_amd import _native
+    from dlnetbench_amd.ops import gemm
+
+    def host_ms(us):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        gemm.idle_wait_us(us)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e3
+
+    hz = _native.lib().dlnb_wallclock_hz(0)
+    host_ms(1000.0)
+    offset = statistics.median(host_ms(1000.0) - 1.0 for _ in range(5))  # launch + sync around a 1 ms wait
+    errs = [host_ms(a.long_ms * 1e3) - offset - a.long_ms for _ in range(a.reps)]
+    med = statistics.median(errs)
+    print(json.dumps({"wallclock_hz": hz, "long_ms": a.long_ms, "offset_ms": round(offset, 4),
+                      "err_us": [round(e * 1e3, 1) for e in errs], "err_us_median": round(med * 1e3, 1),
+                      "err_ppm_median": round(med / a.long_ms * 1e6, 2)}), flush=True)
+    return 0
 
 
 def main(argv=None) -> int:
@@ -21,7 +49,10 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--us", type=float, default=29320.0)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--long-ms", type=float, default=0.0)
     a = ap.parse_args(argv)
+    if a.long_ms > 0:
+        return _long(a)
     A = torch.empty(8192, 4096, device="cuda", dtype=torch.bfloat16)
     B = torch.empty(14336, 4096, device="cuda", dtype=torch.bfloat16)
     C = torch.empty(8192, 14336, device="cuda", dtype=torch.bfloat16)

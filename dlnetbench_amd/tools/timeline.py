@@ -66,7 +66,8 @@ def summarize(events: List[dict]) -> Dict[str, dict]:
     out: Dict[str, dict] = defaultdict(dict)
     for (pid, it), evs in sorted(by.items()):
         host = [e for e in evs if e["cat"] == "host"]
-        evs = [e for e in evs if e["cat"] != "host"]
+        edges = {e["name"]: e["ts"] for e in evs if e["cat"] == "edge"}
+        evs = [e for e in evs if e["cat"] not in ("host", "edge")]
         if not evs:
             continue
         comp = _union([(e["ts"], e["ts"] + e["dur"]) for e in evs if e["cat"] == "compute"])
@@ -99,6 +100,11 @@ def summarize(events: List[dict]) -> Dict[str, dict]:
             r["host_ms"] = h["dur"] / 1e3
             r["launch_ms"] = (t0 - h["ts"]) / 1e3
             r["completion_ms"] = (h["ts"] + h["dur"] - t1) / 1e3
+            if len(edges) == 2:
+                # DLNB_TIMELINE_EDGES=1: stamps on the launch stream around the graph launch
+                e0, e1 = edges["before graph launch"], edges["after graph launch"]
+                r["edges"] = {"submit_ms": (e0 - h["ts"]) / 1e3, "graph_start_ms": (t0 - e0) / 1e3,
+                              "graph_join_ms": (e1 - t1) / 1e3, "detect_ms": (h["ts"] + h["dur"] - e1) / 1e3}
     return dict(out)
 
 
@@ -147,6 +153,8 @@ def main(argv=None) -> int:
         for it, r in its.items():
             host = (f" {r['host_ms']:10.3f} {r['launch_ms']:8.3f} {r['completion_ms']:8.3f}" if "host_ms" in r
                     else "")
+            if "edges" in r:
+                host += " " + " ".join(f"{k[:-3]}={v:.3f}" for k, v in r["edges"].items())
             print(f"{pid:>4} {it:>4} {r['span_ms']:10.3f} {r['compute_busy_ms']:10.3f} {r['comm_busy_ms']:10.3f} "
                   f"{r['comm_hidden_ms']:10.3f} {r['comm_exposed_ms']:10.3f}{host}")
     return 0

@@ -89,6 +89,26 @@ def test_strategy_hip_graph_replay(strategy, model, params, data_dir):
     # per-run timer vectors keep their length under replay
     key = "runtime" if strategy == "fsdp" else "runtimes"
     assert len(r[key]) == 3
+    assert r["prearm_go_timeouts"] == 0  # every armed replay was started by the host's go, none by the timeout
+
+
+@pytest.mark.parametrize("prearm", ["1", "0"])
+def test_graph_loop_prearm_and_clock_rate(prearm, data_dir):
+    """The timed graph loop with the next replay armed behind a host go word (DLNB_PREARM=1, the default) and
+    without (launch + stream polling): same iteration count, each iteration timed alone, no go-wait timeout; the
+    deadline clock's rate is the one measured against the host clock (within 200 ppm of the nominal 100 MHz,
+    not exactly it), and the compute tasks still last the table time on it (profiles/host_boundary_r4.md)."""
+    doc = engine.run_native("fsdp", "tiny_dense_8_bfloat16", 4, 1, base_path=data_dir, warmup=1, runs=5,
+                            compute="gemm", backend="rccl", quiet=True, graph=True, env={"DLNB_PREARM": prearm})
+    g = doc["global"]["dlnb"]
+    r = doc["ranks"][0]
+    assert len(r["runtime"]) == 5
+    assert ("prearm_go_timeouts" in r) == (prearm == "1") and r.get("prearm_go_timeouts", 0) == 0
+    it = g["iteration"]
+    assert it["compute_floor_ms"] * 0.999 <= it["median_ms"] < it["compute_floor_ms"] * 1.1 + 1.0
+    c = g["compute"]
+    assert c["wallclock_hz_nominal"] == 1e8 and c["wallclock_hz"] != 1e8
+    assert abs(c["wallclock_hz"] / c["wallclock_hz_nominal"] - 1) < 200e-6
 
 
 @pytest.mark.parametrize("zero", [1, 2])

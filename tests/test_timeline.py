@@ -118,3 +118,21 @@ def test_timeline_graph_replay_on_gpu(tmp_path):
     # replays differ: the second kept iteration starts after the first ends
     t1 = max(e["ts"] + e["dur"] for e in ev if e["args"]["iter"] == 1)
     assert min(e["ts"] for e in ev if e["args"]["iter"] == 2) >= t1
+
+
+def test_summarize_graph_launch_edges():
+    """DLNB_TIMELINE_EDGES=1 (GPU graph replays): the two stamps on the launch stream around the graph split the
+    host boundary into submission, graph start, join and completion detection; they are not device work."""
+    def x(cat, name, ts, dur, tid=0):
+        return {"ph": "X", "pid": 0, "tid": tid, "cat": cat, "name": name, "ts": ts, "dur": dur, "args": {"iter": 1}}
+    ev = [x("host", "iteration (host)", 0.0, 1100.0, 9),
+          x("edge", "before graph launch", 10.0, 0.0, 8), x("edge", "after graph launch", 1060.0, 0.0, 8),
+          x("comm", "all_gather fsdp/unit/0", 30.0, 100.0, 1), x("compute", "compute", 130.0, 900.0, 2),
+          x("comm", "reduce_scatter fsdp/unit/0", 1030.0, 25.0, 1)]
+    assert tlt.check(ev) == []
+    r = tlt.summarize(ev)["0"]["1"]
+    assert r["span_ms"] == pytest.approx(1.025) and r["comm_exposed_ms"] == pytest.approx(0.125)
+    assert r["launch_ms"] == pytest.approx(0.030) and r["completion_ms"] == pytest.approx(0.045)
+    e = r["edges"]
+    assert e["submit_ms"] == pytest.approx(0.010) and e["graph_start_ms"] == pytest.approx(0.020)
+    assert e["graph_join_ms"] == pytest.approx(0.005) and e["detect_ms"] == pytest.approx(0.040)
