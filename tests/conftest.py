@@ -35,8 +35,14 @@ def _sanitizer_build(kind: str) -> str:
     """`make asan` / `make tsan` into build-<kind>/ (incremental: the first
     session compiles the tree once, later ones only what changed) and return
     its bin directory. A failing build fails the tests that need it."""
+    import fcntl
     import subprocess
-    p = subprocess.run(["make", "-C", ROOT, f"-j{min(16, os.cpu_count() or 4)}", kind], capture_output=True, text=True)
+    # one make per tree at a time: pytest-xdist workers each build the session fixture, and two makes
+    # relinking build-<kind>/libdlnb.so under each other fail the link of the binaries
+    with open(os.path.join(ROOT, f".build-{kind}.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        p = subprocess.run(["make", "-C", ROOT, f"-j{min(16, os.cpu_count() or 4)}", kind], capture_output=True,
+                           text=True)
     assert p.returncode == 0, f"make {kind} failed:\n" + p.stdout[-2000:] + p.stderr[-3000:]
     return os.path.join(ROOT, f"build-{kind}", "bin")
 
