@@ -72,7 +72,10 @@ class ComputeEngine {
   // of a stream on different hardware queues: ~10 us per hop, measured in
   // profiles/graph_queues_r2.md). The compute still lasts the table's total.
   // Other modes: run().
-  virtual void run_chained(Stream& s, double us, double flops) { run(s, us, flops); }
+  // start (optional): as run_stamped's.
+  virtual void run_chained(Stream& s, double us, double flops, uint64_t* start = nullptr) {
+    run_stamped(s, us, flops, start);
+  }
   virtual uint64_t task_ticks(double us) const { (void)us; return 0; }
   // Device-side dependency times (gemm mode; csrc/kernels/deadline_sync.hpp).
   // A gate is a device word: signal(s, g) enqueues on s (a collective's
@@ -92,12 +95,11 @@ class ComputeEngine {
   // The other direction: stream s (a comm lane) waits on the device until the
   // gate carries the tag of its latest signal(), instead of a cross-stream
   // event (no graph edge from the signalling stream; timeout_us bounds it,
-  // counted by gate_timeouts()).
+  // counted in chain_counters()).
   virtual void wait_gate(Stream& s, int gate, double timeout_us) {
     (void)s; (void)gate; (void)timeout_us;
     DLNB_THROW("this compute mode has no device gates");
   }
-  virtual uint64_t gate_timeouts() { return 0; }
   virtual void run_gated(Stream& s, double us, double flops, const std::vector<int>& gates, uint64_t* start,
                          bool chain) {
     (void)s; (void)us; (void)flops; (void)gates; (void)start; (void)chain;
@@ -107,14 +109,29 @@ class ComputeEngine {
   // start into (the --timeline decorator's span start).
   virtual void set_next_start_slot(uint64_t* slot) { (void)slot; }
   // Graph mode: enqueue on s a reset of whatever per-task device state the
-  // engine keys by epoch (a replayed graph repeats the captured epochs).
+  // engine keys by epoch (a replayed graph repeats the captured epochs):
+  // reset_clocks every stream's (one graph, at its head), reset_slot only
+  // the state of tasks that ran on s (lane graphs: at the tail of s's graph,
+  // the lane's own tasks being done by then).
   virtual void reset_clocks(Stream& s) { (void)s; }
-  // Chained / gated deadline tasks whose first block came later than the
-  // absorb cap after their chained start (a wait, not a launch hop: e.g. a
-  // replayed graph queueing the task behind another stream's collective):
-  // zero the counters (stream-ordered on s) / read them (host, after a sync).
+  virtual void reset_slot(Stream& s) { (void)s; }
+  // Counters of the chained / gated deadline tasks (kernels::DlCounter):
+  //   capped: tasks whose first block came later than the absorb cap after
+  //     their chained start (a wait, not a launch hop: e.g. a replayed graph
+  //     queueing the task behind another stream's collective) and that
+  //     lateness beyond the cap, which stays in the iteration time;
+  //   absorbed: the lateness (<= the cap per task) chained tasks took out of
+  //     their own compute - launch hops and drains the iteration does not see;
+  //   timeouts: gate waits that gave up (comm lanes' gate_wait, deadline
+  //     tasks' gates; never expected, counted since the engine was made).
+  // reset_capped zeroes the capped / absorbed counts (stream-ordered on s);
+  // chain_counters reads them (host, after a sync).
+  struct ChainCounters {
+    double capped_tasks = 0, capped_s = 0, absorbed_tasks = 0, absorbed_s = 0;
+    double wait_timeouts = 0, gate_timeouts = 0;
+  };
   virtual void reset_capped(Stream& s) { (void)s; }
-  virtual bool capped(uint64_t& tasks, double& seconds) { (void)tasks; (void)seconds; return false; }
+  virtual bool chain_counters(ChainCounters& c) { (void)c; return false; }
   // Fixed-work modes (gemm-work, flops): time every compute task on the
   // device into t ("compute_task_time") next to its table duration
   // ("compute_task_table"), so the runner can report how much collectives

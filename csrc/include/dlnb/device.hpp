@@ -50,6 +50,10 @@ class GraphExec {
   virtual ~GraphExec() = default;
   virtual void launch(Stream& s) = 0;
   virtual size_t nodes() const = 0;
+  virtual size_t edges() const { return 0; }
+  // a chain: every node but the first depends on exactly the one before it,
+  // so the executor runs the whole graph on the launch stream's queue
+  bool linear() const { return nodes() == 0 || edges() + 1 == nodes(); }
 };
 
 // Owning buffer (device memory on GPU, page-aligned host memory on CPU).
@@ -124,8 +128,40 @@ class Device {
   // host_signal stores value when the stream reaches it; host_wait holds the
   // stream until the host (or a signal) stored a value >= `value`, at most
   // timeout_s (then it adds 1 to *timeouts and lets the stream go). GPU only.
+  // host_wait also stores iter_value into the device's iteration word once
+  // released (iter_value 0: leaves it).
   virtual void host_signal(Stream& s, uint64_t* word, uint64_t value);
-  virtual void host_wait(Stream& s, const uint64_t* word, uint64_t value, double timeout_s, uint64_t* timeouts);
+  virtual void host_wait(Stream& s, const uint64_t* word, uint64_t value, double timeout_s, uint64_t* timeouts,
+                         uint64_t iter_value = 0);
+  // ---- device gates (GPU): ordering between streams through device words
+  // (kernels::gate_signal / gate_wait) instead of graph edges.
+  // A gate is two 16-byte-aligned words {seq, time}; seq carries the
+  // iteration word (iter_word) so a replayed graph's gates never satisfy the
+  // next replay's waits. alloc_gate: a zeroed gate (freed with the device).
+  virtual uint64_t* alloc_gate();
+  virtual uint64_t* iter_word() { return nullptr; }
+  // Enqueue on s a store of `it` into the iteration word (a lane's head).
+  virtual void set_iteration(Stream& s, uint64_t it);
+  // Gate events: while on, recording a dependency-only event (create_event
+  // (false)) raises its gate on the recording stream and waiting on it
+  // enqueues a one-wave gate_wait on the waiting stream (the mode is read at
+  // enqueue time). The runner turns it on for lane graphs: every stream is
+  // captured into its own linear graph, with no cross-stream edge for the
+  // graph executor to act on (it spreads a forked graph over its hardware
+  // queues and can queue a compute node behind a collective,
+  // profiles/absorb_r4.md). Waits are bounded (DLNB_GATE_TIMEOUT_S, 60) and
+  // counted (gate_event_timeouts).
+  virtual void set_gate_events(bool on) { DLNB_REQUIRE(!on, "gate events need a GPU device"); }
+  virtual bool gate_events() const { return false; }
+  virtual uint64_t gate_event_timeouts() { return 0; }
+  // Whether each stream of `ss` runs while another of them is blocked: every
+  // ordered pair is probed (a one-wave wait on one for a store enqueued later
+  // on the other, bounded by timeout_s). Two streams on one hardware queue
+  // would deadlock gate waits between them. detail: the failing pairs.
+  virtual bool queues_independent(const std::vector<Stream*>& ss, double timeout_s, std::string* detail) {
+    (void)ss; (void)timeout_s; (void)detail;
+    return true;
+  }
   virtual double stamp_hz() const = 0;
   virtual size_t total_memory() const = 0;
   virtual size_t free_memory() const = 0;
@@ -137,6 +173,13 @@ class Device {
   virtual std::unique_ptr<GraphExec> capture(Stream& origin, const std::vector<Stream*>& others,
                                              const std::function<void()>& enqueue,
                                              const std::function<void()>& head = {});
+  // Lane capture: every stream of `lanes` is captured into its own graph at
+  // the same time (no fork / join: the strategy's cross-stream dependencies
+  // must be gate events). tail(i) runs after enqueue, still capturing, to add
+  // lane i's last nodes. Graph i is launched on lanes[i]. GPU only.
+  virtual std::vector<std::unique_ptr<GraphExec>> capture_lanes(const std::vector<Stream*>& lanes,
+                                                                const std::function<void()>& enqueue,
+                                                                const std::function<void(size_t)>& tail = {});
 
   Buffer alloc(size_t bytes) { return Buffer(this, bytes); }
   Buffer alloc_peer(size_t bytes) { return Buffer(this, bytes, true); }

@@ -31,28 +31,56 @@ void fill_random(void* p, size_t count, DType t, uint64_t seed, void* stream);
 // wait for up to two gates (device words a collective's stream raises with
 // gate_signal), continue the stream's previous task (chain), and write the
 // start to up to two host-mapped stamp slots.
+// Counters a deadline task adds to (DlSync::counters, device memory), also
+// read by the host (ComputeEngine::chain_counters):
+enum DlCounter : int {
+  kCappedTasks = 0,    // chained tasks whose first block came later than the absorb cap
+  kCappedTicks = 1,    // and the lateness beyond the cap
+  kWaitTimeouts = 2,   // gate_wait kernels (a comm lane waiting on a compute gate) that gave up
+  kGateTimeouts = 3,   // deadline tasks whose gate wait gave up (agree_t0)
+  kAbsorbedTicks = 4,  // lateness chained tasks took out of their own compute (<= the cap each)
+  kAbsorbedTasks = 5,  // chained tasks that absorbed any
+  kNumCounters = 8
+};
 struct DlSync {
   uint64_t* tstart[2] = {nullptr, nullptr};
   const uint64_t* gate[2] = {nullptr, nullptr};
   uint32_t tag[2] = {0, 0};
   uint32_t chain = 0;  // != 0: continue the stream's previous task, absorbing at most this many ticks of lateness
-  // {tasks, ticks}: chained tasks that arrived later than `chain` ticks after
-  // their start, and the lateness beyond it (device memory; nullptr: none)
-  uint64_t* capped = nullptr;
+  uint64_t* counters = nullptr;      // DlCounter words (nullptr: none)
+  const uint64_t* iter = nullptr;    // iteration word the gates' sequence numbers carry (nullptr: 0)
+  uint64_t gate_timeout = 0;         // ticks a gate wait may last (0: 60 s)
 };
-// One wave stores {tag:16 | s_memrealtime:48} into *gate (device memory,
-// agent scope) when the stream reaches this point. tag != 0.
-void gate_signal(uint64_t* gate, uint32_t tag, void* stream);
-// One wave waits until *gate carries tag (raised by gate_signal on another
-// stream), at most timeout ticks; a timeout adds 1 to *timeouts and lets the
-// stream go on (a wait that can never be satisfied - e.g. the raising kernel
-// queued behind this one on the same hardware queue - must not hang the GPU).
-void gate_wait(const uint64_t* gate, uint32_t tag, uint64_t timeout_ticks, uint64_t* timeouts, void* stream);
+// Device gates: two words {seq, time} in device memory (16-byte aligned).
+// seq = iteration << 32 | tag, the iteration read from *iter (the device's
+// iteration word, Device::iter_word; nullptr = 0) when the kernel runs: a
+// replayed graph repeats its captured tags, and the iteration word (set at
+// the head of every replay on every lane) keeps one replay's gates from
+// satisfying the next replay's waits, with no reset between them.
+// gate_signal: one wave stores the time (s_memrealtime), then seq (release)
+// when the stream reaches this point. tag != 0.
+void gate_signal(uint64_t* gate, const uint64_t* iter, uint32_t tag, void* stream);
+// One wave waits until the gate carries this iteration's seq for tag (raised
+// by gate_signal on another stream), at most timeout ticks; a timeout adds 1
+// to *timeouts and lets the stream go on (a wait that can never be satisfied
+// - e.g. the raising kernel queued behind this one on the same hardware queue
+// - must not hang the GPU).
+void gate_wait(const uint64_t* gate, const uint64_t* iter, uint32_t tag, uint64_t timeout_ticks, uint64_t* timeouts,
+               void* stream);
+// One wave stores value into *word (device memory, agent scope): the
+// iteration word at the head of a lane.
+void set_word(uint64_t* word, uint64_t value, void* stream);
+// A probe: does stream a run while a kernel enqueued later on stream b has not?
+// (a waits on a word b stores, at most timeout ticks). Returns false when a
+// timed out, i.e. both streams feed one hardware queue. Synchronises both.
+bool queues_independent(void* a, void* b, uint64_t timeout_ticks);
 
 // Deadline kernels; ticks of the 100 MHz s_memrealtime clock (see
 // wallclock_hz()).
-void idle_wait(uint64_t ticks, void* stream);
-void busy_spin(uint64_t ticks, int blocks, void* stream);
+// start, start2 (optional, host-mapped): the kernel stores its own start time
+// there (s_memrealtime), so stall timers work from the task itself (gap()).
+void idle_wait(uint64_t ticks, void* stream, uint64_t* start = nullptr, uint64_t* start2 = nullptr);
+void busy_spin(uint64_t ticks, int blocks, void* stream, uint64_t* start = nullptr, uint64_t* start2 = nullptr);
 // The deadline clock's rate in Hz: measured against the host's steady clock
 // once per process (clock_cal_begin starts the window - the GPU device does
 // at creation - and the first wallclock_hz call ends it, sleeping until
@@ -67,8 +95,11 @@ void stamp(uint64_t* slot, void* stream);
 // host_signal stores `value`; host_wait holds the stream until *word >= value
 // (one wave spinning with s_sleep; after timeout_ticks it gives up and adds
 // one to *timeouts, so the stream always drains).
+// host_wait also stores iter_value into *iter_out (device memory; optional)
+// once released: the pre-armed loop's lane head sets the iteration word.
 void host_signal(uint64_t* word, uint64_t value, void* stream);
-void host_wait(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uint64_t* timeouts, void* stream);
+void host_wait(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uint64_t* timeouts, void* stream,
+               uint64_t* iter_out = nullptr, uint64_t iter_value = 0);
 int num_cus(int device);
 
 // GEMM: requires M % 256 == 0, N % 256 == 0, K*elem_size % 128 == 0, leading

@@ -138,20 +138,22 @@ int main_for(StrategyKind kind, int argc, char** argv);
 // errors so a dead peer aborts the job instead of hanging it.
 void sync_streams(const std::vector<Stream*>& streams, const std::vector<Communicator*>& comms, Device& dev);
 
-// While alive on this thread: sync_streams() waits for *flag >= value (a
-// host-coherent word a kernel enqueued after the replayed graph stores)
-// instead of querying the streams - the graph joins every stream it forked
-// back onto its launch stream before that kernel runs, so the word proves the
-// whole iteration complete (runner's pre-armed graph loop).
+// While alive on this thread: sync_streams() waits for flags[i] >= value for
+// every i < n (host-coherent words a kernel enqueued after each replayed
+// graph stores) instead of querying the streams - a single graph joins every
+// stream it forked back onto its launch stream before that kernel runs, and
+// lane graphs have one word per lane, so the words prove the whole iteration
+// complete (runner's pre-armed graph loop).
 class CompletionFlag {
  public:
-  CompletionFlag(const uint64_t* flag, uint64_t value);
+  CompletionFlag(const uint64_t* flags, size_t n, uint64_t value);
   ~CompletionFlag();
   CompletionFlag(const CompletionFlag&) = delete;
   CompletionFlag& operator=(const CompletionFlag&) = delete;
 
  private:
   const uint64_t* prev_;
+  size_t prev_n_;
   uint64_t prev_value_;
 };
 

@@ -7,21 +7,19 @@
 //   word 0: {epoch:16 | t0:48}  the published start of the current task
 //   word 1: t0 + ticks (48 bit)  the deadline of the stream's last task
 //   word 2: epoch of the last task whose start was claimed
-//   word 3: 1 once a gate wait timed out (never expected)
 // The first block of a task (epoch = task number on the stream, never 0)
 // claims word 2 with a CAS and decides t0; every other block of the task and
 // every later launch of the same task (DLNB_GEMM_SLICE_US slices) waits for
 // word 0 to carry the epoch and reads t0 back.
 //
 // How the claiming block decides t0 (DlSync, dlnb/kernels.hpp):
-//   * gates: device words {tag:16 | time:48} that a one-wave kernel on a
+//   * gates: two-word device gates {seq, time} that a one-wave kernel on a
 //     collective's stream raises when the collective is done
-//     (kernels::gate_signal). The block spins until each gate carries its
-//     tag and takes the latest time. The strategies also order the task
-//     after the collective with a stream wait, so the gates are raised by
-//     then: the gate dates the dependency, the graph edge orders it (a
-//     kernel spinning on a word raised by a node queued behind it on the
-//     same hardware queue would never finish);
+//     (kernels::gate_signal; seq = the device's iteration word << 32 | tag).
+//     The block spins until each gate carries this iteration's seq and takes
+//     the latest time. With per-lane graphs (the runner's lane mode) the gate
+//     is the only ordering between the collective and the task: the task's
+//     own kernel holds the stream until the collective is done;
 //   * chain (!= 0: the most ticks of lateness to absorb): the task continues
 //     the stream's previous task, so it starts at max(previous deadline, the
 //     latest gate) - a late launch (queue hop, the previous grid's drain) is
@@ -31,13 +29,17 @@
 //     than `chain` ticks starts the task `chain` ticks before it arrived: a
 //     longer delay is not a launch hop (a replayed graph can queue a node
 //     behind another stream's collective on one hardware queue) and stays in
-//     the iteration time instead of being taken out of the compute;
+//     the iteration time instead of being taken out of the compute. Both the
+//     absorbed part and the part beyond the cap are counted (DlCounter);
 //   * otherwise t0 = the time the gates opened (now, with no gates).
+// A gate never raised within gate_timeout (a bug, or a peer that died) ends
+// the wait: the task starts then and kGateTimeouts counts it, so the report
+// shows it (chain_capped.compute_gate_timeouts) and the CUs are released.
 // t0 (as a full 64-bit s_memrealtime value) goes to up to two host-mapped
 // stamp slots (the strategy's stall timer, the --timeline span).
 // Every access is a relaxed agent-scope atomic (coherent across the XCDs'
-// L2s): the stand-in GEMM reads its own operands, never a collective's
-// output, so the gates order time, not data.
+// L2s) except the gates' acquire loads: the stand-in GEMM reads its own
+// operands, never a collective's output, so the gates order time, not data.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -60,6 +62,16 @@ __device__ __forceinline__ uint64_t ld(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+__device__ __forceinline__ void count(uint64_t* counters, int i, uint64_t v) {
+  if (counters) __hip_atomic_fetch_add(counters + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A gate's expected sequence word this iteration (kernels::gate_signal).
+__device__ __forceinline__ uint64_t gate_seq(const uint64_t* iter, uint32_t tag) {
+  const uint64_t it = iter ? ld(iter) : 0ull;
+  return (it << 32) | tag;
+}
+
 __device__ __forceinline__ uint64_t agree_t0(uint64_t* slot, uint32_t epoch, uint64_t ticks, const DlSync& s) {
   uint64_t* claim = slot + 2;
   uint64_t c = ld(claim);
@@ -79,22 +91,26 @@ __device__ __forceinline__ uint64_t agree_t0(uint64_t* slot, uint32_t epoch, uin
   }
   uint64_t gate_t = 0;
   bool gated = false;
+  const uint64_t gate_timeout = s.gate_timeout ? s.gate_timeout : kGateTimeoutTicks;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     if (!s.gate[i]) continue;
-    uint64_t v;
+    const uint64_t want = gate_seq(s.iter, s.tag[i]);
+    uint64_t t;
     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-    while (((v = ld(s.gate[i])) >> 48) != s.tag[i]) {
+    for (;;) {
+      if (__hip_atomic_load(s.gate[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == want) {
+        t = ld(s.gate[i] + 1) & kMask48;
+        break;
+      }
       __builtin_amdgcn_s_sleep(2);
-      if (__builtin_amdgcn_s_memrealtime() - w0 > kGateTimeoutTicks) {
-        // never raised (a bug): give up rather than hold the CUs forever,
-        // and leave the mark in word 3 of the slot for the host to find
-        __hip_atomic_store(slot + 3, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        v = __builtin_amdgcn_s_memrealtime() & kMask48;
+      if (__builtin_amdgcn_s_memrealtime() - w0 > gate_timeout) {
+        // never raised: give up rather than hold the CUs forever, and count it
+        count(s.counters, kGateTimeouts, 1ull);
+        t = __builtin_amdgcn_s_memrealtime() & kMask48;
         break;
       }
     }
-    const uint64_t t = v & kMask48;
     gate_t = gated && not_before(gate_t, t) ? gate_t : t;
     gated = true;
   }
@@ -106,12 +122,16 @@ __device__ __forceinline__ uint64_t agree_t0(uint64_t* slot, uint32_t epoch, uin
     t0 = gated && not_before(gate_t, prev) ? gate_t : prev;
     if (!not_before(now, t0)) {
       t0 = now;  // never in the future
-    } else if (((now - t0) & kMask48) > s.chain) {
-      const uint64_t excess = ((now - t0) & kMask48) - s.chain;
-      t0 = (now - s.chain) & kMask48;  // absorb at most `chain` ticks of lateness
-      if (s.capped) {  // counted for the report: a wait the chain did not hide
-        __hip_atomic_fetch_add(s.capped, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(s.capped + 1, excess, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const uint64_t late = (now - t0) & kMask48;
+      if (late > s.chain) {
+        t0 = (now - s.chain) & kMask48;  // absorb at most `chain` ticks of lateness
+        count(s.counters, kCappedTasks, 1ull);  // a wait the chain did not hide
+        count(s.counters, kCappedTicks, late - s.chain);
+      }
+      if (late > 0) {
+        count(s.counters, kAbsorbedTasks, 1ull);
+        count(s.counters, kAbsorbedTicks, late > s.chain ? s.chain : late);
       }
     }
   }

@@ -105,8 +105,10 @@ __global__ void fill_kernel(Tstore* __restrict__ p, size_t n8, size_t n, uint64_
 
 // ------------------------------------------------------------- deadlines
 
-__global__ void idle_wait_kernel(uint64_t ticks) {
+__global__ void idle_wait_kernel(uint64_t ticks, uint64_t* start, uint64_t* start2) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  if (start) __hip_atomic_store(start, t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (start2) __hip_atomic_store(start2, t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
 
@@ -117,20 +119,41 @@ __global__ void stamp_kernel(uint64_t* slot) {
   }
 }
 
-__global__ void gate_signal_kernel(uint64_t* gate, uint32_t tag) {
+__global__ void gate_signal_kernel(uint64_t* gate, const uint64_t* iter, uint32_t tag) {
   if (threadIdx.x == 0) {
-    const uint64_t t = __builtin_amdgcn_s_memrealtime() & dl::kMask48;
-    __hip_atomic_store(gate, (static_cast<uint64_t>(tag) << 48) | t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t seq = dl::gate_seq(iter, tag);
+    __hip_atomic_store(gate + 1, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(gate, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
-__global__ void gate_wait_kernel(const uint64_t* gate, uint32_t tag, uint64_t timeout_ticks, uint64_t* timeouts) {
+__global__ void gate_wait_kernel(const uint64_t* gate, const uint64_t* iter, uint32_t tag, uint64_t timeout_ticks,
+                                 uint64_t* timeouts) {
   if (threadIdx.x == 0) {
+    const uint64_t want = dl::gate_seq(iter, tag);
     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-    while ((__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 48) != tag) {
+    while (__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != want) {
       __builtin_amdgcn_s_sleep(2);
       if (__builtin_amdgcn_s_memrealtime() - w0 > timeout_ticks) {
         __hip_atomic_fetch_add(timeouts, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+}
+
+__global__ void set_word_kernel(uint64_t* word, uint64_t value) {
+  if (threadIdx.x == 0) __hip_atomic_store(word, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// queue probe: a waits for b's store (system scope: the word is host memory)
+__global__ void probe_wait_kernel(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uint64_t* timed_out) {
+  if (threadIdx.x == 0) {
+    const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != value) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - w0 > timeout_ticks) {
+        __hip_atomic_store(timed_out, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
     }
@@ -141,7 +164,8 @@ __global__ void host_signal_kernel(uint64_t* word, uint64_t value) {
   if (threadIdx.x == 0) __hip_atomic_store(word, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ void host_wait_kernel(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uint64_t* timeouts) {
+__global__ void host_wait_kernel(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uint64_t* timeouts,
+                                 uint64_t* iter_out, uint64_t iter_value) {
   if (threadIdx.x == 0) {
     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < value) {
@@ -151,11 +175,17 @@ __global__ void host_wait_kernel(const uint64_t* word, uint64_t value, uint64_t 
         break;
       }
     }
+    if (iter_out) __hip_atomic_store(iter_out, iter_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
-__global__ void __launch_bounds__(256) busy_spin_kernel(uint64_t ticks, float* sink) {
+__global__ void __launch_bounds__(256) busy_spin_kernel(uint64_t ticks, float* sink, uint64_t* start,
+                                                        uint64_t* start2) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (start) __hip_atomic_store(start, t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (start2) __hip_atomic_store(start2, t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   float x = static_cast<float>(threadIdx.x) * 1e-3f, y = 0.999f;
   for (;;) {
 #pragma unroll
@@ -492,21 +522,47 @@ void fill_random(void* p, size_t count, DType t, uint64_t seed, void* stream) {
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
-void idle_wait(uint64_t ticks, void* stream) {
-  hipLaunchKernelGGL(idle_wait_kernel, 1, 64, 0, S(stream), ticks);
+void idle_wait(uint64_t ticks, void* stream, uint64_t* start, uint64_t* start2) {
+  hipLaunchKernelGGL(idle_wait_kernel, 1, 64, 0, S(stream), ticks, start, start2);
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
-void gate_signal(uint64_t* gate, uint32_t tag, void* stream) {
-  DLNB_REQUIRE(gate != nullptr && tag > 0 && tag < 65536, "gate_signal: bad gate/tag");
-  hipLaunchKernelGGL(gate_signal_kernel, 1, 64, 0, S(stream), gate, tag);
+void gate_signal(uint64_t* gate, const uint64_t* iter, uint32_t tag, void* stream) {
+  DLNB_REQUIRE(gate != nullptr && tag > 0 && reinterpret_cast<uintptr_t>(gate) % 16 == 0, "gate_signal: bad gate/tag");
+  hipLaunchKernelGGL(gate_signal_kernel, 1, 64, 0, S(stream), gate, iter, tag);
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
-void gate_wait(const uint64_t* gate, uint32_t tag, uint64_t timeout_ticks, uint64_t* timeouts, void* stream) {
-  DLNB_REQUIRE(gate != nullptr && timeouts != nullptr && tag > 0 && tag < 65536, "gate_wait: bad gate/tag");
-  hipLaunchKernelGGL(gate_wait_kernel, 1, 64, 0, S(stream), gate, tag, timeout_ticks, timeouts);
+void gate_wait(const uint64_t* gate, const uint64_t* iter, uint32_t tag, uint64_t timeout_ticks, uint64_t* timeouts,
+               void* stream) {
+  DLNB_REQUIRE(gate != nullptr && timeouts != nullptr && tag > 0 && reinterpret_cast<uintptr_t>(gate) % 16 == 0,
+               "gate_wait: bad gate/tag");
+  hipLaunchKernelGGL(gate_wait_kernel, 1, 64, 0, S(stream), gate, iter, tag, timeout_ticks, timeouts);
   DLNB_HIP_CHECK(hipGetLastError());
+}
+
+void set_word(uint64_t* word, uint64_t value, void* stream) {
+  DLNB_REQUIRE(word != nullptr, "set_word: null word");
+  hipLaunchKernelGGL(set_word_kernel, 1, 64, 0, S(stream), word, value);
+  DLNB_HIP_CHECK(hipGetLastError());
+}
+
+bool queues_independent(void* a, void* b, uint64_t timeout_ticks) {
+  void* p = nullptr;
+  DLNB_HIP_CHECK(hipHostMalloc(&p, 2 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
+  uint64_t* w = static_cast<uint64_t*>(p);
+  w[0] = 0;
+  w[1] = 0;
+  hipLaunchKernelGGL(probe_wait_kernel, 1, 64, 0, S(a), w, 1ull, timeout_ticks, w + 1);
+  hipLaunchKernelGGL(host_signal_kernel, 1, 64, 0, S(b), w, 1ull);
+  hipError_t e = hipGetLastError();
+  const hipError_t ea = hipStreamSynchronize(S(a)), eb = hipStreamSynchronize(S(b));
+  const bool ok = __atomic_load_n(w + 1, __ATOMIC_ACQUIRE) == 0;
+  (void)hipHostFree(p);
+  DLNB_HIP_CHECK(e);
+  DLNB_HIP_CHECK(ea);
+  DLNB_HIP_CHECK(eb);
+  return ok;
 }
 
 void host_signal(uint64_t* word, uint64_t value, void* stream) {
@@ -515,9 +571,10 @@ void host_signal(uint64_t* word, uint64_t value, void* stream) {
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
-void host_wait(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uint64_t* timeouts, void* stream) {
+void host_wait(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uint64_t* timeouts, void* stream,
+               uint64_t* iter_out, uint64_t iter_value) {
   DLNB_REQUIRE(word != nullptr && timeouts != nullptr, "host_wait: null word");
-  hipLaunchKernelGGL(host_wait_kernel, 1, 64, 0, S(stream), word, value, timeout_ticks, timeouts);
+  hipLaunchKernelGGL(host_wait_kernel, 1, 64, 0, S(stream), word, value, timeout_ticks, timeouts, iter_out, iter_value);
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
@@ -526,8 +583,8 @@ void stamp(uint64_t* slot, void* stream) {
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
-void busy_spin(uint64_t ticks, int blocks, void* stream) {
-  hipLaunchKernelGGL(busy_spin_kernel, blocks, 256, 0, S(stream), ticks, static_cast<float*>(nullptr));
+void busy_spin(uint64_t ticks, int blocks, void* stream, uint64_t* start, uint64_t* start2) {
+  hipLaunchKernelGGL(busy_spin_kernel, blocks, 256, 0, S(stream), ticks, static_cast<float*>(nullptr), start, start2);
   DLNB_HIP_CHECK(hipGetLastError());
 }
 

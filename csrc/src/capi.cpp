@@ -96,10 +96,11 @@ int dlnb_gemm_deadline_us(const void* A, const void* B, void* C, int M, int N, i
 
 // The deadline GEMM with the full start protocol (csrc/kernels/deadline_sync.hpp):
 // explicit epoch, chain (> 0: continue the slot's previous deadline absorbing at
-// most chain_us of lateness), up to two gates with their tags, a start stamp.
+// most chain_us of lateness), up to two gates (iteration 0) with their tags, a
+// start stamp, the DlCounter words (optional, kernels::kNumCounters int64).
 int dlnb_gemm_deadline_ex(const void* A, const void* B, void* C, int M, int N, int K, int dtype, double us, int device,
                           void* slot, int grid, void* stream, unsigned epoch, double chain_us, void* gate0, unsigned tag0,
-                          void* gate1, unsigned tag1, void* tstart) {
+                          void* gate1, unsigned tag1, void* tstart, void* counters) {
   return guard([&] {
     double hz = dlnb::kernels::wallclock_hz(device);
     if (grid <= 0) grid = dlnb::kernels::num_cus(device);
@@ -110,14 +111,16 @@ int dlnb_gemm_deadline_ex(const void* A, const void* B, void* C, int M, int N, i
     sync.tag[0] = tag0;
     sync.tag[1] = tag1;
     sync.tstart[0] = static_cast<uint64_t*>(tstart);
+    sync.counters = static_cast<uint64_t*>(counters);
     dlnb::kernels::gemm_tn_deadline(A, B, C, M, N, K, static_cast<dlnb::DType>(dtype),
                                     static_cast<unsigned long long>(us * 1e-6 * hz), static_cast<uint64_t*>(slot),
                                     epoch, grid, stream, 0, sync);
   });
 }
 
+// Raise a two-word gate {seq = tag (iteration 0), time} when the stream gets here.
 int dlnb_gate_signal(void* gate, unsigned tag, void* stream) {
-  return guard([&] { dlnb::kernels::gate_signal(static_cast<uint64_t*>(gate), tag, stream); });
+  return guard([&] { dlnb::kernels::gate_signal(static_cast<uint64_t*>(gate), nullptr, tag, stream); });
 }
 
 int dlnb_gemm_narrow_nf(int M, int N, int cus) { return dlnb::kernels::gemm_narrow_nf(M, N, cus); }

@@ -82,6 +82,8 @@ class GpuCompute : public ComputeEngine {
     absorb_ticks_ = static_cast<uint32_t>(std::max<double>(
         static_cast<double>(env_int("DLNB_CHAIN_ABSORB_US", 30)) * 1e-6 * kernels::wallclock_hz_nominal(dev.index()), 1.0));
     cus_ = kernels::num_cus(dev.index());
+    gate_timeout_ticks_ = static_cast<uint64_t>(static_cast<double>(env_int("DLNB_GATE_TIMEOUT_S", 60)) *
+                                                kernels::wallclock_hz_nominal(dev.index()));
     dtype_ = shape.dtype == DType::FP8_E4M3 ? DType::FP8_E4M3 : DType::BF16;
     // The stand-in is the layer's FFN down projection, C[tokens, hidden] =
     // A[tokens, ffn] . W[hidden, ffn]^T: its long K (the FFN width) keeps
@@ -112,12 +114,12 @@ class GpuCompute : public ComputeEngine {
     if (mode_ != ComputeMode::Sleep && mode_ != ComputeMode::Spin) alloc_operands();
     if (mode_ == ComputeMode::GemmWork || mode_ == ComputeMode::Flops) calibrate();
     if (mode_ == ComputeMode::Gemm) {
-      // one 64-byte line per compute stream, then the gate words
-      slots_ = dev_.alloc(kSlots * 64 + kGates * 8);
-      capped_ = dev_.alloc(3 * sizeof(uint64_t));  // {capped tasks, capped ticks, gate-wait timeouts}
+      // one 64-byte line per compute stream; the counters (DlCounter)
+      slots_ = dev_.alloc(kSlots * 64);
+      counters_ = dev_.alloc(kernels::kNumCounters * sizeof(uint64_t));
       auto zs = dev_.create_stream(false);
-      dev_.memset_async(slots_.data(), 0, kSlots * 64 + kGates * 8, *zs);
-      dev_.memset_async(capped_.data(), 0, 3 * sizeof(uint64_t), *zs);
+      dev_.memset_async(slots_.data(), 0, kSlots * 64, *zs);
+      dev_.memset_async(counters_.data(), 0, kernels::kNumCounters * sizeof(uint64_t), *zs);
       zs->synchronize();
       // Leave `comm_cus` CUs to collectives: one 128-KiB-LDS block fits per
       // CU, so a grid of CUs - comm_cus blocks never touches those CUs and
@@ -141,64 +143,73 @@ class GpuCompute : public ComputeEngine {
   }
 
   void reset_clocks(Stream& s) override {
-    if (mode_ == ComputeMode::Gemm) dev_.memset_async(slots_.data(), 0, kSlots * 64 + kGates * 8, s);
+    if (mode_ == ComputeMode::Gemm) dev_.memset_async(slots_.data(), 0, kSlots * 64, s);
+  }
+  void reset_slot(Stream& s) override {
+    if (mode_ != ComputeMode::Gemm) return;
+    auto it = slot_of_.find(&s);
+    if (it != slot_of_.end()) dev_.memset_async(slots_.as<uint64_t>() + it->second * 8, 0, 64, s);
   }
   void reset_capped(Stream& s) override {
-    if (capped_.data()) dev_.memset_async(capped_.data(), 0, 2 * sizeof(uint64_t), s);
+    // the capped / absorbed counts (the timeouts stay: counted since start)
+    if (!counters_.data()) return;
+    uint64_t* c = counters_.as<uint64_t>();
+    dev_.memset_async(c + kernels::kCappedTasks, 0, 2 * sizeof(uint64_t), s);
+    dev_.memset_async(c + kernels::kAbsorbedTicks, 0, 2 * sizeof(uint64_t), s);
   }
-  bool capped(uint64_t& tasks, double& seconds) override {
-    if (!capped_.data()) return false;
-    uint64_t v[2] = {0, 0};
+  bool chain_counters(ChainCounters& out) override {
+    if (!counters_.data()) return false;
+    uint64_t v[kernels::kNumCounters] = {};
     auto st = dev_.create_stream(false);
-    dev_.copy_async(v, capped_.data(), sizeof(v), *st);
+    dev_.copy_async(v, counters_.data(), sizeof(v), *st);
     st->synchronize();
-    tasks = v[0];
-    seconds = static_cast<double>(v[1]) / hz();
+    out.capped_tasks = static_cast<double>(v[kernels::kCappedTasks]);
+    out.capped_s = static_cast<double>(v[kernels::kCappedTicks]) / hz();
+    out.absorbed_tasks = static_cast<double>(v[kernels::kAbsorbedTasks]);
+    out.absorbed_s = static_cast<double>(v[kernels::kAbsorbedTicks]) / hz();
+    out.wait_timeouts = static_cast<double>(v[kernels::kWaitTimeouts]);
+    out.gate_timeouts = static_cast<double>(v[kernels::kGateTimeouts]);
     return true;
   }
 
-  bool stamps_task_start() const override { return mode_ == ComputeMode::Gemm; }
+  bool stamps_task_start() const override {
+    return mode_ == ComputeMode::Gemm || mode_ == ComputeMode::Sleep || mode_ == ComputeMode::Spin;
+  }
   uint64_t task_ticks(double us) const override { return ticks(us * scale_); }
   void run(Stream& s, double us, double flops) override { run_stamped(s, us, flops, nullptr); }
 
-  void run_chained(Stream& s, double us, double flops) override {
+  void run_chained(Stream& s, double us, double flops, uint64_t* start) override {
     if (mode_ == ComputeMode::Gemm && us * scale_ >= 20.0 && chain_live_[slot_for(s)]) {
       kernels::DlSync sync;
+      sync.tstart[0] = start;
       sync.tstart[1] = extra_start_;
       extra_start_ = nullptr;
       deadline_task(s, us * scale_, sync, true);
       ++chained_;
       return;
     }
-    run(s, us, flops);
+    run_stamped(s, us, flops, start);
   }
 
   bool gates_task(double us) const override { return mode_ == ComputeMode::Gemm && us * scale_ >= 20.0; }
 
   int make_gate() override {
     DLNB_REQUIRE(mode_ == ComputeMode::Gemm, "gates need the gemm (deadline) compute");
-    DLNB_REQUIRE(gate_tag_.size() < kGates, "too many compute gates");
+    gates_.push_back(dev_.alloc_gate());
     gate_tag_.push_back(0);
-    return static_cast<int>(gate_tag_.size()) - 1;
+    return static_cast<int>(gates_.size()) - 1;
   }
 
   void signal(Stream& s, int gate) override {
     uint32_t& tag = gate_tag_.at(gate);
-    tag = tag % 65535 + 1;
-    kernels::gate_signal(gate_word(gate), tag, s.native());
+    tag = tag == 0xffffffffu ? 1u : tag + 1;
+    kernels::gate_signal(gates_.at(gate), dev_.iter_word(), tag, s.native());
   }
   void wait_gate(Stream& s, int gate, double timeout_us) override {
     const uint32_t tag = gate_tag_.at(gate);
     DLNB_REQUIRE(tag != 0, "wait_gate: gate " << gate << " was never signalled");
-    kernels::gate_wait(gate_word(gate), tag, ticks(timeout_us), capped_.as<uint64_t>() + 2, s.native());
-  }
-  uint64_t gate_timeouts() override {
-    if (!capped_.data()) return 0;
-    uint64_t v[3] = {0, 0, 0};
-    auto st = dev_.create_stream(false);
-    dev_.copy_async(v, capped_.data(), sizeof(v), *st);
-    st->synchronize();
-    return v[2];
+    kernels::gate_wait(gates_.at(gate), dev_.iter_word(), tag, ticks(timeout_us),
+                       counters_.as<uint64_t>() + kernels::kWaitTimeouts, s.native());
   }
 
   void run_gated(Stream& s, double us, double flops, const std::vector<int>& gates, uint64_t* start,
@@ -208,7 +219,7 @@ class GpuCompute : public ComputeEngine {
     (void)flops;
     kernels::DlSync sync;
     for (size_t i = 0; i < gates.size(); ++i) {
-      sync.gate[i] = gate_word(gates[i]);
+      sync.gate[i] = gates_.at(gates[i]);
       sync.tag[i] = gate_tag_.at(gates[i]);
       DLNB_REQUIRE(sync.tag[i] != 0, "run_gated: gate " << gates[i] << " was never signalled");
     }
@@ -226,12 +237,18 @@ class GpuCompute : public ComputeEngine {
   void run_stamped(Stream& s, double us, double flops, uint64_t* start) override {
     double d = us * scale_;
     if (mode_ == ComputeMode::Gemm) chain_live_[slot_for(s)] = false;  // a chain restarts at every unchained task
-    if (mode_ == ComputeMode::Sleep) {
-      if (d > 0) kernels::idle_wait(ticks(d), s.native());
-      return;
-    }
-    if (mode_ == ComputeMode::Spin) {
-      if (d > 0) kernels::busy_spin(ticks(d), cus_, s.native());
+    if (mode_ == ComputeMode::Sleep || mode_ == ComputeMode::Spin) {
+      // the kernel stamps its own start (stall timers: gap() from it)
+      uint64_t* extra = extra_start_;
+      extra_start_ = nullptr;
+      if (d <= 0) {
+        if (start) dev_.stamp(s, start);
+        if (extra) dev_.stamp(s, extra);
+      } else if (mode_ == ComputeMode::Sleep) {
+        kernels::idle_wait(ticks(d), s.native(), start, extra);
+      } else {
+        kernels::busy_spin(ticks(d), cus_, s.native(), start, extra);
+      }
       return;
     }
     if (mode_ == ComputeMode::Gemm) {
@@ -239,15 +256,14 @@ class GpuCompute : public ComputeEngine {
       // keeps the matrix cores and HBM busy for exactly the table's time, so
       // DVFS or contention changes how much work is done, not how long).
       if (d <= 0) {
+        if (start) dev_.stamp(s, start);
         if (extra_start_) dev_.stamp(s, extra_start_);
         extra_start_ = nullptr;
         return;
       }
       if (d < 20.0) {
-        if (start) dev_.stamp(s, start);
-        if (extra_start_) dev_.stamp(s, extra_start_);
+        kernels::busy_spin(ticks(d), cus_, s.native(), start, extra_start_);
         extra_start_ = nullptr;
-        kernels::busy_spin(ticks(d), cus_, s.native());
         return;
       }
       kernels::DlSync sync;
@@ -335,7 +351,9 @@ class GpuCompute : public ComputeEngine {
     uint32_t& ep = epoch_[slot];
     ep = ep % 65535 + 1;  // 1..65535, never 0 (a fresh slot reads as epoch 0)
     sync.chain = chain ? absorb_ticks_ : 0u;
-    sync.capped = chain ? capped_.as<uint64_t>() : nullptr;
+    sync.counters = counters_.as<uint64_t>();
+    sync.iter = dev_.iter_word();
+    sync.gate_timeout = gate_timeout_ticks_;
     const uint64_t total = ticks(d);
     const uint64_t slice = slice_us_ > 0 ? std::max<uint64_t>(ticks(slice_us_), 1) : total;
     for (uint64_t end = slice;; end += slice) {
@@ -345,8 +363,6 @@ class GpuCompute : public ComputeEngine {
     }
     chain_live_[slot] = true;
   }
-
-  uint64_t* gate_word(int gate) { return slots_.as<uint64_t>() + kSlots * 8 + gate; }
 
   // table_us: the task's uncontended duration (gemm-work: the table time;
   // flops: the calibrated time of its FLOPs at the largest GEMM level).
@@ -434,22 +450,23 @@ class GpuCompute : public ComputeEngine {
 
   static constexpr int kMmax = 8192;
   static constexpr size_t kSlots = 64;
-  static constexpr size_t kGates = 4096;
   Device& dev_;
   ComputeMode mode_;
   double scale_;
   Buffer slots_;
-  Buffer capped_;  // {tasks, ticks} beyond the absorb cap (DlSync::capped)
+  Buffer counters_;  // kernels::DlCounter words (DlSync::counters)
+  std::vector<uint64_t*> gates_;          // device gates (Device::alloc_gate)
   std::map<Stream*, size_t> slot_of_;
   std::map<uint64_t*, uint32_t> epoch_;
   std::map<uint64_t*, bool> chain_live_;  // the stream's last task was a deadline task a chained one may continue
-  std::vector<uint32_t> gate_tag_;        // last tag signalled per gate (1..65535)
+  std::vector<uint32_t> gate_tag_;        // last tag signalled per gate (never 0 once signalled)
   uint64_t* extra_start_ = nullptr;       // set_next_start_slot
   // Lateness a chained task absorbs (deadline_sync.hpp): the replayed graph's
   // queue hop (8-11 us) + the previous grid's drain (~13 us) measured in
   // round 3; anything later is a wait and stays in the iteration time.
   // DLNB_CHAIN_ABSORB_US overrides.
   uint32_t absorb_ticks_ = 1;
+  uint64_t gate_timeout_ticks_ = 0;  // a deadline task's gate wait bound (DLNB_GATE_TIMEOUT_S)
   long chained_ = 0;                      // tasks that continued a chain (describe())
   long gated_ = 0;
   int grid_ = 256;

@@ -329,10 +329,17 @@ std::unique_ptr<GraphExec> Device::capture(Stream&, const std::vector<Stream*>&,
   DLNB_THROW("--graph needs a GPU device (HIP graphs)");
 }
 
+std::vector<std::unique_ptr<GraphExec>> Device::capture_lanes(const std::vector<Stream*>&, const std::function<void()>&,
+                                                               const std::function<void(size_t)>&) {
+  DLNB_THROW("lane graphs need a GPU device (HIP graphs)");
+}
+
 void Device::host_signal(Stream&, uint64_t*, uint64_t) { DLNB_THROW("host_signal needs a GPU device"); }
-void Device::host_wait(Stream&, const uint64_t*, uint64_t, double, uint64_t*) {
+void Device::host_wait(Stream&, const uint64_t*, uint64_t, double, uint64_t*, uint64_t) {
   DLNB_THROW("host_wait needs a GPU device");
 }
+uint64_t* Device::alloc_gate() { DLNB_THROW("device gates need a GPU device"); }
+void Device::set_iteration(Stream&, uint64_t) {}
 
 std::string cpu_peer_source(const void* p) {
   std::lock_guard<std::mutex> g(peer_mu());

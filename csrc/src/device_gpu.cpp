@@ -18,9 +18,11 @@ namespace dlnb {
 
 namespace {
 
+class GpuDevice;
+
 class GpuEvent : public Event {
  public:
-  explicit GpuEvent(bool timing) {
+  GpuEvent(bool timing, GpuDevice* dev) : dev(timing ? nullptr : dev) {
     // Dependency-only events: no timestamp and, on HIP >= 7.2, no
     // system-scope fence (an L2 writeback after every GEMM otherwise; the
     // ordering we need is device-local). Timing events keep the defaults.
@@ -38,6 +40,13 @@ class GpuEvent : public Event {
   }
   ~GpuEvent() override { (void)hipEventDestroy(ev); }
   hipEvent_t ev{};
+  // gate events (Device::set_gate_events): the device (nullptr for timing
+  // events, which never become gates), the gate (allocated at the first gate
+  // record) and the tag of the latest record (0: never recorded as a gate)
+  GpuDevice* dev = nullptr;
+  uint64_t* gate = nullptr;
+  uint32_t tag = 0;
+  hipStream_t on = nullptr;  // stream of the latest gate record
 };
 
 class GpuStream : public Stream {
@@ -50,8 +59,8 @@ class GpuStream : public Stream {
     DLNB_HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high_priority ? hi : lo));
   }
   ~GpuStream() override { (void)hipStreamDestroy(s); }
-  void record(Event& e) override { DLNB_HIP_CHECK(hipEventRecord(static_cast<GpuEvent&>(e).ev, s)); }
-  void wait(Event& e) override { DLNB_HIP_CHECK(hipStreamWaitEvent(s, static_cast<GpuEvent&>(e).ev, 0)); }
+  void record(Event& e) override;
+  void wait(Event& e) override;
   void synchronize() override { DLNB_HIP_CHECK(hipStreamSynchronize(s)); }
   bool query() override {
     hipError_t e = hipStreamQuery(s);
@@ -65,15 +74,28 @@ class GpuStream : public Stream {
 
 class GpuGraphExec : public GraphExec {
  public:
-  GpuGraphExec(hipGraphExec_t e, size_t n) : exec_(e), n_(n) {}
+  GpuGraphExec(hipGraphExec_t e, size_t n, size_t edges) : exec_(e), n_(n), edges_(edges) {}
   ~GpuGraphExec() override { (void)hipGraphExecDestroy(exec_); }
   void launch(Stream& s) override { DLNB_HIP_CHECK(hipGraphLaunch(exec_, static_cast<hipStream_t>(s.native()))); }
   size_t nodes() const override { return n_; }
+  size_t edges() const override { return edges_; }
 
  private:
   hipGraphExec_t exec_;
-  size_t n_;
+  size_t n_, edges_;
 };
+
+// Instantiate a captured graph (destroying it); node and edge counts kept.
+std::unique_ptr<GraphExec> instantiate(hipGraph_t g) {
+  size_t n = 0, ne = 0;
+  (void)hipGraphGetNodes(g, nullptr, &n);
+  (void)hipGraphGetEdges(g, nullptr, nullptr, &ne);
+  hipGraphExec_t e = nullptr;
+  hipError_t err = hipGraphInstantiate(&e, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (err != hipSuccess) DLNB_THROW("hipGraphInstantiate failed: " << hipGetErrorString(err));
+  return std::unique_ptr<GraphExec>(new GpuGraphExec(e, n, ne));
+}
 
 void host_trampoline(void* p) {
   auto* fn = static_cast<std::function<void()>*>(p);
@@ -92,13 +114,18 @@ class GpuDevice : public Device {
     total_ = prop.totalGlobalMem;
     kernels::clock_cal_begin(idx_);  // the rate is taken at its first use (stamp_hz), after setup
   }
+  ~GpuDevice() override {
+    if (pool_) (void)hipFree(pool_);
+  }
   DeviceKind kind() const override { return DeviceKind::GPU; }
   std::string name() const override { return name_ + " (" + arch_ + ")"; }
   int index() const override { return idx_; }
   std::unique_ptr<Stream> create_stream(bool high_priority) override {
     return std::unique_ptr<Stream>(new GpuStream(idx_, high_priority));
   }
-  std::unique_ptr<Event> create_event(bool timing) override { return std::unique_ptr<Event>(new GpuEvent(timing)); }
+  std::unique_ptr<Event> create_event(bool timing) override {
+    return std::unique_ptr<Event>(new GpuEvent(timing, this));
+  }
   double elapsed_ms(Event& a, Event& b) override {
     float ms = 0;
     DLNB_HIP_CHECK(hipEventSynchronize(static_cast<GpuEvent&>(b).ev));
@@ -152,8 +179,63 @@ class GpuDevice : public Device {
   void free_stamps(uint64_t* p, size_t) override { (void)hipHostFree(p); }
   void stamp(Stream& s, uint64_t* slot) override { kernels::stamp(slot, s.native()); }
   void host_signal(Stream& s, uint64_t* word, uint64_t value) override { kernels::host_signal(word, value, s.native()); }
-  void host_wait(Stream& s, const uint64_t* word, uint64_t value, double timeout_s, uint64_t* timeouts) override {
-    kernels::host_wait(word, value, static_cast<uint64_t>(timeout_s * stamp_hz()), timeouts, s.native());
+  void host_wait(Stream& s, const uint64_t* word, uint64_t value, double timeout_s, uint64_t* timeouts,
+                 uint64_t iter_value) override {
+    kernels::host_wait(word, value, static_cast<uint64_t>(timeout_s * stamp_hz()), timeouts, s.native(),
+                       iter_value ? iter_word() : nullptr, iter_value);
+  }
+
+  // ---- gates: one zeroed device block, carved without HIP calls (gates are
+  // taken during graph capture); [0] the iteration word, [1] gate-event wait
+  // timeouts, gates from byte 64 on, 16 bytes each.
+  uint64_t* alloc_gate() override {
+    ensure_pool();
+    DLNB_REQUIRE(next_gate_ < kPoolGates, "device gate pool exhausted (" << kPoolGates << " gates)");
+    return pool_ + 8 + 2 * next_gate_++;
+  }
+  uint64_t* iter_word() override {
+    ensure_pool();
+    return pool_;
+  }
+  void set_iteration(Stream& s, uint64_t it) override { kernels::set_word(iter_word(), it, s.native()); }
+  void set_gate_events(bool on) override {
+    if (on) ensure_pool();
+    gate_events_ = on;
+  }
+  bool gate_events() const override { return gate_events_; }
+  uint64_t gate_event_timeouts() override {
+    if (!pool_) return 0;
+    uint64_t v = 0;
+    DLNB_HIP_CHECK(hipMemcpy(&v, pool_ + 1, sizeof(v), hipMemcpyDeviceToHost));
+    return v;
+  }
+  uint64_t gate_timeout_ticks() {
+    static const double s = static_cast<double>(env_int("DLNB_GATE_TIMEOUT_S", 60));
+    return static_cast<uint64_t>(s * stamp_hz());
+  }
+  void gate_record(GpuEvent& e, hipStream_t s) {
+    if (!e.gate) e.gate = alloc_gate();
+    e.tag = e.tag == 0xffffffffu ? 1u : e.tag + 1;
+    e.on = s;
+    kernels::gate_signal(e.gate, iter_word(), e.tag, s);
+  }
+  void gate_wait(GpuEvent& e, hipStream_t s) {
+    if (e.tag == 0) return;  // never recorded: nothing to wait for (as a HIP event)
+    if (e.on == s) return;   // recorded on this stream: already ordered
+    kernels::gate_wait(e.gate, iter_word(), e.tag, gate_timeout_ticks(), pool_ + 1, s);
+  }
+  bool queues_independent(const std::vector<Stream*>& ss, double timeout_s, std::string* detail) override {
+    const uint64_t t = static_cast<uint64_t>(timeout_s * stamp_hz());
+    bool ok = true;
+    for (size_t a = 0; a < ss.size(); ++a)
+      for (size_t b = 0; b < ss.size(); ++b) {
+        if (a == b) continue;
+        if (!kernels::queues_independent(ss[a]->native(), ss[b]->native(), t)) {
+          ok = false;
+          if (detail) *detail += (detail->empty() ? "" : ", ") + std::to_string(a) + " waits behind " + std::to_string(b);
+        }
+      }
+    return ok;
   }
   double stamp_hz() const override { return kernels::wallclock_hz(idx_); }
   size_t total_memory() const override { return total_; }
@@ -188,23 +270,84 @@ class GpuDevice : public Device {
     }
     hipGraph_t g = nullptr;
     DLNB_HIP_CHECK(hipStreamEndCapture(o, &g));
-    size_t n = 0;
-    (void)hipGraphGetNodes(g, nullptr, &n);
-    hipGraphExec_t e = nullptr;
-    hipError_t err = hipGraphInstantiate(&e, g, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(g);
-    if (err != hipSuccess) DLNB_THROW("hipGraphInstantiate failed: " << hipGetErrorString(err));
-    return std::unique_ptr<GraphExec>(new GpuGraphExec(e, n));
+    return instantiate(g);
+  }
+
+  std::vector<std::unique_ptr<GraphExec>> capture_lanes(const std::vector<Stream*>& lanes,
+                                                        const std::function<void()>& enqueue,
+                                                        const std::function<void(size_t)>& tail) override {
+    size_t begun = 0;
+    auto end_all = [&] {  // after a failure: end every capture begun, drop the graphs
+      for (size_t i = 0; i < begun; ++i) {
+        hipGraph_t g = nullptr;
+        (void)hipStreamEndCapture(static_cast<hipStream_t>(lanes[i]->native()), &g);
+        if (g) (void)hipGraphDestroy(g);
+      }
+    };
+    try {
+      for (; begun < lanes.size(); ++begun)
+        DLNB_HIP_CHECK(hipStreamBeginCapture(static_cast<hipStream_t>(lanes[begun]->native()),
+                                             hipStreamCaptureModeThreadLocal));
+      enqueue();
+      if (tail)
+        for (size_t i = 0; i < lanes.size(); ++i) tail(i);
+    } catch (...) {
+      end_all();
+      throw;
+    }
+    std::vector<hipGraph_t> gs(lanes.size(), nullptr);
+    hipError_t first = hipSuccess;
+    for (size_t i = 0; i < lanes.size(); ++i) {
+      hipError_t e = hipStreamEndCapture(static_cast<hipStream_t>(lanes[i]->native()), &gs[i]);
+      if (e != hipSuccess && first == hipSuccess) first = e;
+    }
+    if (first != hipSuccess) {
+      for (hipGraph_t g : gs)
+        if (g) (void)hipGraphDestroy(g);
+      DLNB_THROW("lane capture failed: " << hipGetErrorString(first)
+                                         << " (a cross-stream dependency that is not a gate event?)");
+    }
+    std::vector<std::unique_ptr<GraphExec>> out;
+    for (hipGraph_t g : gs) out.push_back(instantiate(g));
+    return out;
   }
 
  private:
+  static constexpr size_t kPoolGates = 65536;
+  void ensure_pool() {
+    if (pool_) return;
+    const size_t bytes = 64 + kPoolGates * 16;
+    DLNB_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&pool_), bytes));
+    DLNB_HIP_CHECK(hipMemset(pool_, 0, bytes));
+    DLNB_HIP_CHECK(hipStreamSynchronize(nullptr));
+  }
+  uint64_t* pool_ = nullptr;
+  size_t next_gate_ = 0;
+  bool gate_events_ = false;
   int idx_;
   std::string name_, arch_;
   size_t total_ = 0;
-  double hz_ = 1e8;
 };
 
 }  // namespace
+
+void GpuStream::record(Event& e) {
+  auto& g = static_cast<GpuEvent&>(e);
+  if (g.dev && g.dev->gate_events()) {
+    g.dev->gate_record(g, s);
+    return;
+  }
+  DLNB_HIP_CHECK(hipEventRecord(g.ev, s));
+}
+
+void GpuStream::wait(Event& e) {
+  auto& g = static_cast<GpuEvent&>(e);
+  if (g.dev && g.dev->gate_events()) {
+    g.dev->gate_wait(g, s);
+    return;
+  }
+  DLNB_HIP_CHECK(hipStreamWaitEvent(s, g.ev, 0));
+}
 
 std::unique_ptr<Device> make_gpu_device(int local_index) { return std::unique_ptr<Device>(new GpuDevice(local_index)); }
 

@@ -36,15 +36,19 @@ namespace dlnb {
 
 namespace {
 thread_local const uint64_t* t_done_flag = nullptr;
+thread_local size_t t_done_n = 0;
 thread_local uint64_t t_done_value = 0;
 }  // namespace
 
-CompletionFlag::CompletionFlag(const uint64_t* flag, uint64_t value) : prev_(t_done_flag), prev_value_(t_done_value) {
-  t_done_flag = flag;
+CompletionFlag::CompletionFlag(const uint64_t* flags, size_t n, uint64_t value)
+    : prev_(t_done_flag), prev_n_(t_done_n), prev_value_(t_done_value) {
+  t_done_flag = flags;
+  t_done_n = n;
   t_done_value = value;
 }
 CompletionFlag::~CompletionFlag() {
   t_done_flag = prev_;
+  t_done_n = prev_n_;
   t_done_value = prev_value_;
 }
 
@@ -63,8 +67,14 @@ void sync_streams(const std::vector<Stream*>& streams, const std::vector<Communi
   const double t0 = now_s();
   int polls = 0;
   const uint64_t* flag = t_done_flag;
+  const size_t nflags = t_done_n;
   const uint64_t want = t_done_value;
-  auto done = [&](Stream* s) { return flag ? __atomic_load_n(flag, __ATOMIC_ACQUIRE) >= want : s->query(); };
+  auto done = [&](Stream* s) {
+    if (!flag) return s->query();
+    for (size_t i = 0; i < nflags; ++i)
+      if (__atomic_load_n(flag + i, __ATOMIC_ACQUIRE) < want) return false;
+    return true;
+  };
   for (Stream* s : streams) {
     while (!done(s)) {
       if (++polls % 64 == 0) {
@@ -561,8 +571,22 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   T.ensure(rkey);
   ctx.compute->set_task_timers(&T);
 
-  // ---- HIP graph: capture one iteration, replay it every iteration
+  // ---- HIP graph: capture one iteration, replay it every iteration.
+  // Lane graphs (the default): every stream of the strategy is captured into
+  // its own linear graph, launched on that stream, and the streams' ordering
+  // is carried by device gates (Device::set_gate_events: an event record
+  // raises a gate, a wait spins on it) instead of graph edges. The graph
+  // executor then has no fork to spread over its hardware queues: compute
+  // stays on the compute stream's queue and every collective on its lane's,
+  // so no compute task queues behind a collective (profiles/absorb_r4.md), and
+  // every stamp pair on one stream times exactly that stream's work. It needs
+  // every stream on a hardware queue of its own (a gate wait would otherwise
+  // hold the queue its signal sits behind): probed first, and a single graph
+  // with event edges when they share one (lane_graphs.reason says why).
   std::unique_ptr<GraphExec> graph;
+  std::vector<std::unique_ptr<GraphExec>> lane_graphs;
+  Json lane_info = Json::object();
+  std::vector<Stream*> lanes_ss;  // streams the replay is launched on (lane graphs: each; else the compute stream)
   if (opt.graph) {
     DLNB_REQUIRE(ctx.dev->kind() == DeviceKind::GPU, "--graph needs a GPU");
     // xgmi kernels take their epochs from device-side counters, so a replayed
@@ -572,24 +596,90 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     DLNB_REQUIRE(strat->capturable(), "--graph cannot capture --schedule reference (it blocks the host)");
     std::vector<Stream*> ss = strat->streams();
     std::vector<Stream*> others(ss.begin() + 1, ss.end());
+    std::string why;
+    bool lanes = false;
+    if (env_int("DLNB_LANE_GRAPHS", 1) == 0) {
+      why = "DLNB_LANE_GRAPHS=0";
+    } else if (ss.size() < 2) {
+      why = "one stream";
+    } else {
+      std::string detail;
+      lanes = ctx.dev->queues_independent(ss, 0.05, &detail);
+      if (!lanes) why = "streams share a hardware queue (" + detail + ")";
+      // every rank takes the same decision (a gate-joined rank and an
+      // edge-joined one issue the same collectives, but keep the reports alike)
+      lanes = ctx.hg().allreduce_max(lanes ? 0.0 : 1.0) < 0.5;
+      if (!lanes && why.empty()) why = "another rank's streams share a hardware queue";
+    }
     TraceRange tr("dlnb:graph_capture");
     T.begin_capture();
     if (TL) TL->begin_capture();
-    // the engine's slot / gate reset heads the graph, before every stream's
-    // first node (a gate raised on a comm stream must not be wiped by it)
-    graph = ctx.dev->capture(
-        *ss[0], others, [&] { strat->enqueue_iteration(); }, [&] { ctx.compute->reset_clocks(*ss[0]); });
+    if (lanes) {
+      ctx.dev->set_gate_events(true);
+      // each lane ends by clearing its own deadline slot for the next replay
+      lane_graphs = ctx.dev->capture_lanes(
+          ss, [&] { strat->enqueue_iteration(); }, [&](size_t i) { ctx.compute->reset_slot(*ss[i]); });
+      lanes_ss = ss;
+      // the first replay starts from cleared slots too
+      ctx.compute->reset_clocks(*ss[0]);
+      ss[0]->synchronize();
+    } else {
+      // the engine's slot reset heads the graph, before every stream's first node
+      graph = ctx.dev->capture(
+          *ss[0], others, [&] { strat->enqueue_iteration(); }, [&] { ctx.compute->reset_clocks(*ss[0]); });
+      lanes_ss = {ss[0]};
+    }
     T.end_capture();
     if (TL) TL->end_capture();
-    if (ri.rank == 0 && !opt.quiet)
-      std::cout << "[dlnb] captured one iteration into a HIP graph of " << graph->nodes() << " nodes" << std::endl;
-  }
-  Stream* origin = graph ? strat->streams()[0] : nullptr;
-  auto enqueue = [&] {
-    if (graph)
-      graph->launch(*origin);
+    lane_info["enabled"] = lanes;
+    if (!lanes) lane_info["reason"] = why;
+    Json per = Json::array();
+    size_t total = 0;
+    bool all_linear = true;
+    auto describe = [&](const GraphExec& g) {
+      Json e = Json::object();
+      e["nodes"] = static_cast<double>(g.nodes());
+      e["edges"] = static_cast<double>(g.edges());
+      e["linear"] = g.linear();
+      total += g.nodes();
+      all_linear = all_linear && g.linear();
+      per.push_back(e);
+    };
+    if (lanes)
+      for (auto& g : lane_graphs) describe(*g);
     else
+      describe(*graph);
+    lane_info["graphs"] = per;
+    lane_info["linear"] = all_linear;
+    if (ri.rank == 0 && !opt.quiet) {
+      if (lanes)
+        std::cout << "[dlnb] captured one iteration into " << lane_graphs.size() << " lane graphs of " << total
+                  << " nodes (" << (all_linear ? "all linear" : "NOT all linear") << ")" << std::endl;
+      else
+        std::cout << "[dlnb] captured one iteration into a HIP graph of " << total << " nodes"
+                  << (why.empty() ? "" : " (no lane graphs: " + why + ")") << std::endl;
+    }
+  }
+  const bool replay = graph || !lane_graphs.empty();
+  Stream* origin = replay ? strat->streams()[0] : nullptr;
+  // Device iteration word (gates' sequence numbers): one value per replay,
+  // stored at the head of every lane before its graph runs.
+  uint64_t dev_iter = 0;
+  auto launch_graphs = [&] {
+    if (lane_graphs.empty()) {
+      graph->launch(*origin);
+      return;
+    }
+    for (size_t i = 0; i < lane_graphs.size(); ++i) lane_graphs[i]->launch(*lanes_ss[i]);
+  };
+  auto enqueue = [&] {
+    if (replay) {
+      const uint64_t it = ++dev_iter;
+      for (Stream* l : lanes_ss) ctx.dev->set_iteration(*l, it);
+      launch_graphs();
+    } else {
       strat->enqueue_iteration();
+    }
   };
   ctx.hg().barrier();
 
@@ -654,27 +744,39 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   // region starts (as the last warm-up iteration would in a longer loop); all
   // of its device work runs inside it, as does the loop's closing device
   // synchronize. DLNB_PREARM=0: launch, then poll the streams (A/B).
-  uint64_t* hs = nullptr;  // [0] go, [1] done, [2] go-wait timeouts
-  if (graph && ctx.dev->kind() == DeviceKind::GPU && env_int("DLNB_PREARM", 1) != 0) hs = ctx.dev->alloc_stamps(3);
+  // Lane graphs: every lane has its own go wait and done word; the host
+  // waits for all of them (the iteration ends when every stream has).
+  const size_t nlanes = lanes_ss.size();
+  const size_t nhs = 2 + nlanes;
+  uint64_t* hs = nullptr;  // [0] go, [1] go-wait timeouts, [2 + i] lane i done
+  if (replay && ctx.dev->kind() == DeviceKind::GPU && env_int("DLNB_PREARM", 1) != 0) hs = ctx.dev->alloc_stamps(nhs);
   struct Handshake {
     Device& d;
     uint64_t*& p;
+    size_t n;
     ~Handshake() {
       if (!p) return;
       if (std::uncaught_exceptions() == 0) {
-        d.free_stamps(p, 3);
+        d.free_stamps(p, n);
       } else {  // release any armed graph (not freed: hipHostFree waits for the device, which may be hung)
         __atomic_store_n(p, ~0ull, __ATOMIC_RELEASE);
       }
     }
-  } handshake{*ctx.dev, hs};
+  } handshake{*ctx.dev, hs, nhs};
   const double go_timeout_s = 30.0;
   auto arm = [&](int r) {
-    ctx.dev->host_wait(*origin, hs, static_cast<uint64_t>(r) + 1, go_timeout_s, hs + 2);
-    if (TL && tl_edges) TL->edge(*origin, 0);
-    graph->launch(*origin);
-    if (TL && tl_edges) TL->edge(*origin, 1);
-    ctx.dev->host_signal(*origin, hs + 1, static_cast<uint64_t>(r) + 1);
+    const uint64_t it = ++dev_iter;
+    for (size_t i = 0; i < nlanes; ++i) {
+      Stream& l = *lanes_ss[i];
+      ctx.dev->host_wait(l, hs, static_cast<uint64_t>(r) + 1, go_timeout_s, hs + 1, it);
+      if (TL && tl_edges && i == 0) TL->edge(l, 0);
+      if (lane_graphs.empty())
+        graph->launch(l);
+      else
+        lane_graphs[i]->launch(l);
+      if (TL && tl_edges && i == 0) TL->edge(l, 1);
+      ctx.dev->host_signal(l, hs + 2 + i, static_cast<uint64_t>(r) + 1);
+    }
   };
   ctx.hg().barrier();
   ctx.compute->reset_capped(*strat->streams()[0]);  // count the timed iterations only
@@ -689,12 +791,12 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     if (hs) {
       __atomic_store_n(hs, static_cast<uint64_t>(r) + 1, __ATOMIC_RELEASE);  // go
       if (r + 1 < runs) arm(r + 1);
-      CompletionFlag cf(hs + 1, static_cast<uint64_t>(r) + 1);
+      CompletionFlag cf(hs + 2, nlanes, static_cast<uint64_t>(r) + 1);
       strat->synchronize();
     } else {
-      if (TL && graph && tl_edges) TL->edge(*origin, 0);
+      if (TL && replay && tl_edges) TL->edge(*origin, 0);
       enqueue();
-      if (TL && graph && tl_edges) TL->edge(*origin, 1);
+      if (TL && replay && tl_edges) TL->edge(*origin, 1);
       strat->synchronize();
     }
     const double t1 = now_s();
@@ -711,19 +813,22 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
 
   // ---- report
   Json rank = strat->rank_json();
-  if (hs) rank["prearm_go_timeouts"] = static_cast<double>(__atomic_load_n(hs + 2, __ATOMIC_ACQUIRE));
+  if (hs) rank["prearm_go_timeouts"] = static_cast<double>(__atomic_load_n(hs + 1, __ATOMIC_ACQUIRE));
   rank["energy_consumed"] = T.values_json("energy_consumed");
   {
-    // chained deadline tasks that waited longer than the absorb cap (deadline_sync.hpp)
-    uint64_t ct = 0;
-    double cs = 0;
-    if (runs > 0 && ctx.compute->capped(ct, cs)) {
+    // chained deadline tasks: lateness absorbed (<= the cap each) and beyond
+    // the cap (deadline_sync.hpp), gate waits that timed out
+    ComputeEngine::ChainCounters cc;
+    if (runs > 0 && ctx.compute->chain_counters(cc)) {
       Json c = Json::object();
-      c["tasks_per_iter"] = static_cast<double>(ct) / runs;
-      c["ms_per_iter"] = cs / runs * 1e3;
-      // device gate waits (a comm lane waiting on a compute gate) that gave up
-      // at their bound: never expected - the wait's signal was queued behind it
-      c["gate_wait_timeouts"] = static_cast<double>(ctx.compute->gate_timeouts());
+      c["tasks_per_iter"] = cc.capped_tasks / runs;
+      c["ms_per_iter"] = cc.capped_s / runs * 1e3;
+      c["absorbed_tasks_per_iter"] = cc.absorbed_tasks / runs;
+      c["absorbed_ms_per_iter"] = cc.absorbed_s / runs * 1e3;
+      // device gate waits that gave up at their bound (never expected): a comm
+      // lane's gate_wait, a deadline task's gate, a gate event's wait
+      c["gate_wait_timeouts"] = cc.wait_timeouts + static_cast<double>(ctx.dev->gate_event_timeouts());
+      c["compute_gate_timeouts"] = cc.gate_timeouts;
       rank["chain_capped"] = c;
     }
   }
@@ -776,7 +881,15 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   Json ext = Json::object();
   ext["strategy"] = strategy_name(opt.strategy);
   ext["schedule"] = opt.schedule;
-  ext["graph"] = graph ? static_cast<double>(graph->nodes()) : 0.0;
+  {
+    size_t nodes = graph ? graph->nodes() : 0;
+    for (const auto& g : lane_graphs) nodes += g->nodes();
+    ext["graph"] = static_cast<double>(nodes);
+  }
+  if (opt.graph) ext["lane_graphs"] = lane_info;
+  // pre-armed replay loop (each iteration's launch submitted during the one
+  // before, released by a host store; DLNB_PREARM=0 launches in the loop)
+  ext["prearm"] = hs != nullptr;
   ext["wire_dtype"] = dtype_name(ctx.wire);
   ext["compute"] = ctx.compute->describe();
   ext["stats_file"] = stats_path;
@@ -853,18 +966,27 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     if (worst > 0) ext["compute_stretch"] = worst;  // max over ranks
     // Compute tasks that waited beyond the chain's absorb cap per iteration
     // (the wait stays in the iteration time; max over ranks)
-    double ctasks = -1, cms = 0, gto = 0;
+    double ctasks = -1, cms = 0, gto = 0, cgto = 0, ams = 0, atasks = 0;
     for (const auto& rj : ranks)
       if (rj.contains("chain_capped")) {
-        ctasks = std::max(ctasks, rj.at("chain_capped").at("tasks_per_iter").as_double());
-        cms = std::max(cms, rj.at("chain_capped").at("ms_per_iter").as_double());
-        gto = std::max(gto, rj.at("chain_capped").at("gate_wait_timeouts").as_double());
+        const Json& c = rj.at("chain_capped");
+        ctasks = std::max(ctasks, c.at("tasks_per_iter").as_double());
+        cms = std::max(cms, c.at("ms_per_iter").as_double());
+        gto = std::max(gto, c.at("gate_wait_timeouts").as_double());
+        cgto = std::max(cgto, c.at("compute_gate_timeouts").as_double());
+        ams = std::max(ams, c.at("absorbed_ms_per_iter").as_double());
+        atasks = std::max(atasks, c.at("absorbed_tasks_per_iter").as_double());
       }
     if (ctasks >= 0) {
       Json c = Json::object();
       c["tasks_per_iter_max"] = ctasks;
       c["ms_per_iter_max"] = cms;
       c["gate_wait_timeouts_max"] = gto;
+      c["compute_gate_timeouts_max"] = cgto;
+      // lateness the chained tasks took out of their own compute (launch
+      // hops, drains): invisible in the iteration time, shown here
+      c["absorbed_ms_per_iter_max"] = ams;
+      c["absorbed_tasks_per_iter_max"] = atasks;
       ext["chain_capped"] = c;
     }
   }

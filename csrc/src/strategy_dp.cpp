@@ -223,14 +223,28 @@ class DataParallel : public Strategy {
     }
     Context& ctx = *ctx_;
     ComputeEngine& ce = *ctx.compute;
+    // Exposed communication (barrier_time, the reference's timer around the
+    // final WaitAll, dp.cpp:102-104) from stamps no executor can reorder: the
+    // last backward task's own start stamp + its duration (its deadline) to
+    // the end stamp of the last all-reduce on the comm stream, when the
+    // engine's kernels stamp their start (deadline / sleep / spin compute).
+    // A stamp-wait-stamp on the compute stream (stall) otherwise.
+    const bool stamped = ce.stamps_task_start();
+    const uint64_t* last_start = nullptr;
+    const uint64_t* tail_end = nullptr;
     ce.run(*compute_, fwd_us_, fwd_flops_);
     for (int i = 0; i < nb_; ++i) {
       // only event records (or gate signals) on compute_ since the forward: one stretch of compute
-      ce.run_chained(*compute_, bwd_us_[i], bwd_flops_[i]);
+      uint64_t* st = stamped && i == nb_ - 1 ? timers_->slot() : nullptr;
+      ce.run_chained(*compute_, bwd_us_[i], bwd_flops_[i], st);
+      if (st) last_start = st;
       if (comm_gates_) {
         ce.signal(*compute_, g_ready_[i]);
-        // bounded: 4x the bucket's compute + 1 s (never expected to expire)
-        ce.wait_gate(*comm_stream_, g_ready_[i], bwd_us_[i] * ctx.opt.time_scale * 4 + 1e6);
+        // bounded by 4x the compute queued ahead of the signal (the forward and
+        // buckets 0..i) + 1 s: never expected to expire
+        double ahead = fwd_us_;
+        for (int j = 0; j <= i; ++j) ahead += bwd_us_[j];
+        ce.wait_gate(*comm_stream_, g_ready_[i], ahead * ctx.opt.time_scale * 4 + 1e6);
       } else {
         compute_->record(*ready_[i]);
         comm_stream_->wait(*ready_[i]);
@@ -238,10 +252,17 @@ class DataParallel : public Strategy {
       int t = timers_->begin(*comm_stream_);
       void* out = in_place_ ? grads_[i].data() : sums_[i].data();
       comm_->all_reduce(grads_[i].data(), out, sizes_[i], ctx.wire, *comm_stream_);
-      timers_->end(t, *comm_stream_, "allreduce_time");
+      const uint64_t* e = timers_->end(t, *comm_stream_, "allreduce_time");
+      if (e) tail_end = e;
     }
-    comm_stream_->record(*done_);
-    timers_->stall(*compute_, *done_, "barrier_time");
+    if (last_start && tail_end && !ctx.opt.optimizer) {
+      // nothing follows on the compute stream: the iteration ends when both
+      // streams have (graph join, lane done words, synchronize)
+      timers_->gap(last_start, ce.task_ticks(bwd_us_[nb_ - 1]), tail_end, "barrier_time");
+    } else {
+      comm_stream_->record(*done_);
+      timers_->stall(*compute_, *done_, "barrier_time");
+    }
     if (ctx.opt.optimizer) {
       // Optimizer over the full (replicated) gradient, bucket by bucket.
       size_t off = 0;

@@ -199,12 +199,17 @@ class Fsdp : public Strategy {
     tail_end_ = nullptr;
 
     ComputeEngine& ce = *ctx.compute;
+    // Lane graphs (the runner's gate events): a gated task's own gates are
+    // its only ordering after the collectives - the compute stream's event
+    // waits (and the records nobody else waits for) would add a gate kernel
+    // each, on the compute or the comm lane.
+    const bool lane = gated_ && ctx.dev->gate_events();
     auto gather = [&](int u, Event& done, bool first, int gate) {
       int tk = timers_->begin(*ag_stream_);
       ag_comm_->all_gather(params_[u].data(), gathered_[u & 1].data(), shard_[u], t, *ag_stream_);
       timers_->end(tk, *ag_stream_, first ? "allgather" : "allgather_time");
       if (gated_) ce.signal(*ag_stream_, gate);  // before the record: the event implies the gate
-      ag_stream_->record(done);
+      if (!lane) ag_stream_->record(done);
     };
 
     // ---- forward
@@ -217,7 +222,7 @@ class Fsdp : public Strategy {
         gather(u + 1, *ag_f_[u + 1], false, gated_ ? g_ag_f_[u + 1] : -1);
       }
       if (gated_) {
-        compute_->wait(*ag_f_[u]);
+        if (!lane) compute_->wait(*ag_f_[u]);
         compute_gated({g_ag_f_[u]}, u == 0 ? nullptr : "allgather_wait_fwd", fwd_us_, fwd_flops_);
       } else {
         compute_after(*ag_f_[u], u == 0 ? nullptr : "allgather_wait_fwd", fwd_us_, fwd_flops_);
@@ -236,11 +241,11 @@ class Fsdp : public Strategy {
       if (gated_) {
         std::vector<int> gates;
         if (u < U_ - 1) {
-          compute_->wait(*ag_b_[u]);
+          if (!lane) compute_->wait(*ag_b_[u]);
           gates.push_back(g_ag_b_[u]);
         }
         if (u + 2 <= U_ - 1) {
-          compute_->wait(*rs_done_[u + 2]);
+          if (!lane) compute_->wait(*rs_done_[u + 2]);
           gates.push_back(g_rs_[u + 2]);
         }
         compute_gated(gates, u < U_ - 1 ? "allgather_wait_bwd" : nullptr, bwd_us_, bwd_flops_);
@@ -258,7 +263,9 @@ class Fsdp : public Strategy {
       rs_comm_->reduce_scatter(full_grad_[u & 1].data(), grads_[u].data(), shard_[u], t, *rs_stream_);
       tail_end_ = timers_->end(tk, *rs_stream_, "reduce_scatter");
       if (gated_ && u >= 2) ce.signal(*rs_stream_, g_rs_[u]);  // RS(u) gates bwd(u - 2)
-      rs_stream_->record(*rs_done_[u]);
+      // (lane graphs: waited for only by the replica all-reduce, the tail's
+      // stall and the optimizer)
+      if (!lane || R_ > 1 || u == 0) rs_stream_->record(*rs_done_[u]);
       if (reference_) compute_->wait(*rs_done_[u]);  // blocking Reduce_Scatter_block (fsdp.cpp:124)
       if (R_ > 1) {
         ar_stream_->wait(*rs_done_[u]);

@@ -393,15 +393,14 @@ class TracingCompute : public ComputeEngine {
     traced(s, "compute", us, [&] { in_->run_stamped(s, us, flops, start); });
   }
   bool stamps_task_start() const override { return in_->stamps_task_start(); }
-  void run_chained(Stream& s, double us, double flops) override {
-    traced(s, "compute (chained)", us, [&] { in_->run_chained(s, us, flops); });
+  void run_chained(Stream& s, double us, double flops, uint64_t* start) override {
+    traced(s, "compute (chained)", us, [&] { in_->run_chained(s, us, flops, start); });
   }
   uint64_t task_ticks(double us) const override { return in_->task_ticks(us); }
   bool gates_task(double us) const override { return in_->gates_task(us); }
   int make_gate() override { return in_->make_gate(); }
   void signal(Stream& s, int gate) override { in_->signal(s, gate); }
   void wait_gate(Stream& s, int gate, double timeout_us) override { in_->wait_gate(s, gate, timeout_us); }
-  uint64_t gate_timeouts() override { return in_->gate_timeouts(); }
   void run_gated(Stream& s, double us, double flops, const std::vector<int>& gates, uint64_t* start,
                  bool chain) override {
     Json a = Json::object();
@@ -411,8 +410,9 @@ class TracingCompute : public ComputeEngine {
   }
   void set_next_start_slot(uint64_t* slot) override { in_->set_next_start_slot(slot); }
   void reset_clocks(Stream& s) override { in_->reset_clocks(s); }
+  void reset_slot(Stream& s) override { in_->reset_slot(s); }
   void reset_capped(Stream& s) override { in_->reset_capped(s); }
-  bool capped(uint64_t& tasks, double& seconds) override { return in_->capped(tasks, seconds); }
+  bool chain_counters(ChainCounters& c) override { return in_->chain_counters(c); }
   void set_task_timers(TimerSet* t) override { in_->set_task_timers(t); }
   Json describe() const override { return in_->describe(); }
   ComputeMode mode() const override { return in_->mode(); }

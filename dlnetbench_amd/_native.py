@@ -57,7 +57,7 @@ def lib() -> ctypes.CDLL:
     L.dlnb_gemm_tn_waves.argtypes = [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_vp]
     L.dlnb_gemm_deadline_us.argtypes = [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_dbl, c_int, c_vp, c_int, c_vp]
     L.dlnb_gemm_deadline_ex.argtypes = [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_dbl, c_int, c_vp, c_int, c_vp,
-                                        ctypes.c_uint, c_dbl, c_vp, ctypes.c_uint, c_vp, ctypes.c_uint, c_vp]
+                                        ctypes.c_uint, c_dbl, c_vp, ctypes.c_uint, c_vp, ctypes.c_uint, c_vp, c_vp]
     L.dlnb_gate_signal.argtypes = [c_vp, ctypes.c_uint, c_vp]
     L.dlnb_gemm_shape_ok.argtypes = [c_int, c_int, c_int, c_int]
     L.dlnb_gemm_narrow_nf.argtypes = [c_int, c_int, c_int]

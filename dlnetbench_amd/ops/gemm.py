@@ -62,37 +62,49 @@ def gemm_deadline_us(a, b, c, us: float, stamp=None, grid: int = 0):
     N = b.shape[0]
     if stamp is None:
         stamp = torch.zeros(8, dtype=torch.int64, device=a.device)
+    if stamp.numel() < 8 or stamp.dtype != torch.int64:
+        # the kernels use words 0-2 of the 64-byte slot line (deadline_sync.hpp)
+        raise ValueError("stamp must be an int64 tensor of >= 8 elements")
     _native.check(_native.lib().dlnb_gemm_deadline_us(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, dt, us,
                                                       a.device.index or 0, stamp.data_ptr(), grid, _stream(a)))
     return c
 
 
 def gemm_deadline_ex(a, b, c, us: float, slot, epoch: int, chain=False, gates=(), tstart=None,
-                     grid: int = 0):
+                     grid: int = 0, counters=None):
     """gemm_deadline_us with the whole start protocol (csrc/kernels/deadline_sync.hpp): `slot` an int64
     CUDA tensor of 8 elements reused by consecutive tasks of one stream, `epoch` the task number on it
     (1..65535, different from the previous task's), `chain` start at the slot's previous deadline
     absorbing at most `chain` us of lateness (True: the runtime's 30 us, DLNB_CHAIN_ABSORB_US),
-    `gates` up to two (int64 CUDA tensor, index, tag) words to wait for, `tstart` an (int64 tensor,
-    index) that receives the task's start (s_memrealtime ticks)."""
+    `gates` up to two (int64 CUDA tensor, gate index, tag) to wait for - gate i is the two words
+    [2i, 2i+1] = {seq, time} (gate_signal_), `tstart` an (int64 tensor, index) that receives the
+    task's start (s_memrealtime ticks), `counters` an int64 CUDA tensor of >= 8 elements the task adds
+    its kernels::DlCounter counts to (capped / absorbed lateness, gate timeouts)."""
     import torch
     dt = _native.DTYPES["bf16"] if a.dtype == torch.bfloat16 else _native.DTYPES["fp8_e4m3"]
     M, K = a.shape
     N = b.shape[0]
     if slot.numel() < 8 or slot.dtype != torch.int64:
         raise ValueError("slot must be an int64 tensor of >= 8 elements")
-    g = [(t.data_ptr() + 8 * i, tag) for t, i, tag in gates] + [(None, 0)] * (2 - len(gates))
+    g = [(t.data_ptr() + 16 * i, tag) for t, i, tag in gates] + [(None, 0)] * (2 - len(gates))
     ts = tstart[0].data_ptr() + 8 * tstart[1] if tstart is not None else None
+    if counters is not None and (counters.numel() < 8 or counters.dtype != torch.int64):
+        raise ValueError("counters must be an int64 tensor of >= 8 elements")
+    cp = counters.data_ptr() if counters is not None else None
     _native.check(_native.lib().dlnb_gemm_deadline_ex(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, dt, us,
                                                       a.device.index or 0, slot.data_ptr(), grid, _stream(a), epoch,
                                                       30.0 if chain is True else float(chain or 0), g[0][0],
-                                                      g[0][1], g[1][0], g[1][1], ts))
+                                                      g[0][1], g[1][0], g[1][1], ts, cp))
     return c
 
 
 def gate_signal_(gate, index: int, tag: int):
-    """Raise gate[index] = {tag:16 | s_memrealtime:48} when torch's current stream reaches this point."""
-    _native.check(_native.lib().dlnb_gate_signal(gate.data_ptr() + 8 * index, tag, _stream(gate)))
+    """Raise gate `index` of an int64 CUDA tensor (words [2 index, 2 index + 1] = {seq = tag, time =
+    s_memrealtime}) when torch's current stream reaches this point."""
+    import torch
+    if gate.numel() < 2 * index + 2 or gate.dtype != torch.int64:
+        raise ValueError("gate must be an int64 tensor with two words per gate")
+    _native.check(_native.lib().dlnb_gate_signal(gate.data_ptr() + 16 * index, tag, _stream(gate)))
     return gate
 
 

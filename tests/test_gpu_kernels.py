@@ -352,10 +352,10 @@ def test_deadline_gate_waits_for_signal():
                               tstart=(ts, 1), grid=_grid())
         e1.record(s)
         torch.cuda.synchronize()
-    g = gates.tolist()
+    g = gates.tolist()  # gate i = words [2i, 2i+1] = {seq, time}; seq = tag at iteration 0
     t = ts.tolist()
-    assert g[0] >> 48 == 17 and g[1] >> 48 == 19, g
-    gate1 = g[1] & mask
+    assert g[0] == 17 and g[2] == 19, g
+    gate1 = g[3] & mask
     assert (t[1] & mask) == gate1, (t, g)  # started at the late gate, not at the previous deadline
     from dlnetbench_amd import _native
     assert t[1] - t[0] >= round(4000e-6 * _native.lib().dlnb_wallclock_hz(0)) - 1, t
