@@ -663,11 +663,18 @@ def _c5_blocks(a: argparse.Namespace, world: int, rank: int, budget: _Budget, es
     c5: Dict[str, Any] = {}
 
     def common(d: dict) -> Dict[str, Any]:
-        it = d["global"]["dlnb"]["iteration"]
+        dl = d["global"]["dlnb"]
+        it = dl["iteration"]
+        cc = dl.get("chain_capped") or {}
         return {"ms_per_step": round(it["timed_ms_per_iter"], 4), "median_ms": round(it["median_ms"], 4),
+                # the device-timed exposed all-reduce tail (barrier_time: last all-reduce's end stamp minus
+                # the last backward's deadline) next to what the host sees over the floor
                 "exposed_comm_ms": _mean_of(d, "barrier_time"),
+                "step_minus_floor_ms": round(it["median_ms"] - it["compute_floor_ms"], 4),
                 "allreduce_busbw_GBps": _busbw(d, "allreduce", world),
-                "chain_capped": d["global"]["dlnb"].get("chain_capped")}
+                "chain_capped": cc or None,
+                "chain_absorbed_ms_per_iter": cc.get("absorbed_ms_per_iter_max"),
+                "lane_graphs": (dl.get("lane_graphs") or {}).get("enabled")}
 
     try:
         d = _dp_block(a, world, rank, budget, est, ".c5", graph, a.compute)
@@ -777,7 +784,7 @@ def main() -> int:
     ap.add_argument("--c3-runs", type=int, default=2, help="timed iterations of the C3 block")
     ap.add_argument("--c4-model", default=C4_MODEL)
     ap.add_argument("--c4", default=C4_PARAMS, help="hybrid_3d_moe num_stages,num_microbatches,num_expert_shards")
-    ap.add_argument("--c4-runs", type=int, default=1, help="timed iterations of the C4 blocks")
+    ap.add_argument("--c4-runs", type=int, default=2, help="timed iterations of the C4 blocks")
     ap.add_argument("--hybrid-timeout", type=float, default=150.0)
     ap.add_argument("--c4-ep-overlap", choices=["on", "off"], default="on",
                     help="also run C4 with --ep-overlap (the all-to-alls off the compute stream)")
@@ -936,23 +943,23 @@ def main() -> int:
             t0 = ph.now()
             extra["comm_bound"] = _c5_blocks(a, world, rank, budget, est, use_graph, on_gpu)
             ph.add("comm_bound", t0)
-        if a.stretch_steps > 0 and on_gpu:
+        # The cross-GPU link evidence right after C5, before the hybrids (VERDICT
+        # r4 #4: a slow first cross-device hybrid must not skip it): collective
+        # bandwidth with nothing else running, RCCL and xgmi, then the
+        # comm-bound step over the xgmi kernels.
+        if a.link_bench == "on" or (a.link_bench == "auto" and world > 1 and on_gpu):
             t0 = ph.now()
-            nominal = est.setup + 5.0 + (1 + a.stretch_steps) * head_ms / 1e3
-            t = budget.plan("compute_stretch", est.want(nominal, 150), nominal)
-            if t is None:
-                extra["compute_stretch_error"] = _skipped(budget)["skipped"]
-            else:
-                try:
-                    d = _child_run(a, world, rank, ".work", "fsdp", a.model, (a.units, world), t, backend=a.backend,
-                                   graph=use_graph, compute="gemm-work", warmup=1, runs=a.stretch_steps, **fsdp_kw)
-                    if rank == 0:
-                        extra["compute_stretch"] = d["global"]["dlnb"].get("compute_stretch")
-                        extra["gemm_work_ms_per_step"] = round(d["global"]["dlnb"]["iteration"]["timed_ms_per_iter"],
-                                                               3)
-                except Exception as e:  # noqa: BLE001
-                    extra["compute_stretch_error"] = str(e)[:300]
-            ph.add("compute_stretch", t0)
+            extra["link_bench"] = _link_block(a, world, rank, xgmi_exact_ok, budget, est)
+            ph.add("link_bench", t0)
+        # xgmi A/B in child processes (see the module docstring); skipped when
+        # the exactness pass found the xgmi kernels wrong on these ranks.
+        xgmi_on = on_gpu and (a.xgmi_ab == "on" or (a.xgmi_ab == "auto" and world > 1))
+        skip = {"error": "skipped: the xgmi exactness check failed on these ranks (see exact_detail)"}
+        if a.c5_model != "none" and xgmi_on:
+            t0 = ph.now()
+            extra["comm_bound_xgmi"] = (_xgmi_ab(a, world, rank, extra.get("comm_bound", {}), budget, est)
+                                        if xgmi_exact_ok else skip)
+            ph.add("comm_bound_xgmi", t0)
         # BASELINE C3 / C4 hybrids (8 GPUs), each a child process per rank.
         if a.hybrids == "on" or (a.hybrids == "auto" and world == 8 and on_gpu):
             c3 = tuple(int(x) for x in a.c3.split(","))
@@ -974,25 +981,29 @@ def main() -> int:
                     a, world, rank, ".c4o", "hybrid_3d_moe", a.c4_model, c4, note + "C4", budget, est, a.c4_runs,
                     ep_overlap=True)
                 ph.add("hybrid_3d_moe_ep_overlap", t0)
-        # Collective bandwidth with nothing else running, RCCL and xgmi.
-        if a.link_bench == "on" or (a.link_bench == "auto" and world > 1 and on_gpu):
+        if a.stretch_steps > 0 and on_gpu:
             t0 = ph.now()
-            extra["link_bench"] = _link_block(a, world, rank, xgmi_exact_ok, budget, est)
-            ph.add("link_bench", t0)
+            nominal = est.setup + 5.0 + (1 + a.stretch_steps) * head_ms / 1e3
+            t = budget.plan("compute_stretch", est.want(nominal, 150), nominal)
+            if t is None:
+                extra["compute_stretch_error"] = _skipped(budget)["skipped"]
+            else:
+                try:
+                    d = _child_run(a, world, rank, ".work", "fsdp", a.model, (a.units, world), t, backend=a.backend,
+                                   graph=use_graph, compute="gemm-work", warmup=1, runs=a.stretch_steps, **fsdp_kw)
+                    if rank == 0:
+                        extra["compute_stretch"] = d["global"]["dlnb"].get("compute_stretch")
+                        extra["gemm_work_ms_per_step"] = round(d["global"]["dlnb"]["iteration"]["timed_ms_per_iter"],
+                                                               3)
+                except Exception as e:  # noqa: BLE001
+                    extra["compute_stretch_error"] = str(e)[:300]
+            ph.add("compute_stretch", t0)
         # Device timeline of the headline configuration (every rank's spans).
         if a.timeline_block == "on" or (a.timeline_block == "auto" and world > 1 and on_gpu):
             t0 = ph.now()
             extra["timeline"] = _timeline_block(a, world, rank, budget, est)
             ph.add("timeline", t0)
-        # xgmi A/B last, in child processes (see the module docstring); skipped
-        # when the exactness pass found the xgmi kernels wrong on these ranks.
-        xgmi_on = on_gpu and (a.xgmi_ab == "on" or (a.xgmi_ab == "auto" and world > 1))
-        skip = {"error": "skipped: the xgmi exactness check failed on these ranks (see exact_detail)"}
-        if a.c5_model != "none" and xgmi_on:
-            t0 = ph.now()
-            extra["comm_bound_xgmi"] = (_xgmi_ab(a, world, rank, extra.get("comm_bound", {}), budget, est)
-                                        if xgmi_exact_ok else skip)
-            ph.add("comm_bound_xgmi", t0)
+        # the headline over the xgmi kernels last
         if xgmi_on and a.xgmi_headline_steps > 0 and not (fallback and fallback["backend"] == "xgmi"):
             t0 = ph.now()
             extra["headline_xgmi"] = _headline_xgmi(a, world, rank, doc, budget, est) if xgmi_exact_ok else skip
@@ -1032,6 +1043,13 @@ def main() -> int:
             # compute tasks per iteration that waited longer than a launch hop (the chained
             # deadline's 30-us absorb cap) and that wait in ms - kept in the time, not hidden
             "chain_capped": g["dlnb"].get("chain_capped"),
+            # launch hops / drains the chained deadline tasks took out of their own compute
+            # (<= 30 us each): not in the iteration time, reported so nothing is hidden
+            "chain_absorbed_ms_per_iter": (g["dlnb"].get("chain_capped") or {}).get("absorbed_ms_per_iter_max"),
+            # one linear HIP graph per stream joined by device gates (or why not), and whether each
+            # iteration's launch was pre-armed during the previous one
+            "lane_graphs": g["dlnb"].get("lane_graphs"),
+            "prearm": g["dlnb"].get("prearm"),
             "median_ms": round(it["median_ms"], 3),
             "per_run_ms": _per_run_ms(doc),
             # every rank's mean iteration (ms): at N > 1 the straggler and the spread behind the max

@@ -107,6 +107,8 @@ def test_bench_hybrid_blocks_eight_ranks_cpu(tmp_path):
     ov = h4["ep_overlap"]
     assert "error" not in ov, ov
     assert ov["ep_overlap"] is True and ov["floor_ms"] == h4["floor_ms"] and ov["ms_per_step"] >= 0.9 * ov["floor_ms"]
+    # C4 is timed over 2 iterations by default, both blocks, within the default budget
+    assert len(h4["per_run_ms"]) == 2 and len(ov["per_run_ms"]) == 2, (h4, ov)
     # the xGMI cost model's prediction next to every measured block
     for h in (h3, h4, ov):
         assert h["predicted_ms"] >= h["floor_ms"] and h["vs_predicted"] > 0
@@ -187,7 +189,27 @@ def test_bench_c3_two_timed_runs_eight_ranks(tmp_path):
                       "--exact", "off", "--c5-model", "none"] + TINY[:6], tmp_path, timeout=300)
     h3 = o["hybrid_3d"]
     assert "error" not in h3 and len(h3["per_run_ms"]) == 2 and all(x > 0 for x in h3["per_run_ms"]), h3
-    assert len(o["hybrid_3d_moe"]["per_run_ms"]) == 1
+    assert len(o["hybrid_3d_moe"]["per_run_ms"]) == 2
+
+
+def test_bench_links_before_hybrids_eight_ranks(tmp_path):
+    """the link evidence (link_bench, then comm_bound_xgmi on GPUs) runs right after C5 and
+    before the hybrids, so a C3 that hangs (rank 5, its limit --hybrid-timeout) and a budget too small for
+    C4 after it leave link_bench measured and C4 reported skipped."""
+    budget = 60
+    o = _torchrun(8, ["--steps", "1", "--warmup", "0", "--backend", "cpu", "--compute", "sleep",
+                      "--hybrids", "on", "--c3-model", "tiny_deep_8_bfloat16", "--c3", "2,4,4",
+                      "--c4-model", "tiny_moe_8_bfloat16", "--c4", "2,8,4", "--exact", "off",
+                      "--c5-model", "none", "--link-bench", "on", "--link-sizes", "4096",
+                      "--wall-budget-s", str(budget), "--hybrid-timeout", "30"] + TINY[:6],
+                  tmp_path, env={"DLNB_INJECT_FAULT": "rank=5,iter=0,mode=hang,block=c3"}, timeout=300)
+    assert o["phase_seconds"]["total"] <= budget
+    lb = o["link_bench"]
+    assert "error" not in lb["cpu"] and "skipped" not in lb, lb
+    order = list(o["phase_seconds"])
+    assert order.index("link_bench") < order.index("hybrid_3d"), order
+    assert "timeout" in o["hybrid_3d"]["error"], o["hybrid_3d"]
+    assert "skipped" in o["hybrid_3d_moe"], o["hybrid_3d_moe"]
 
 
 def test_bench_unverified_backend_flags_its_blocks(tmp_path):
