@@ -87,6 +87,9 @@ void busy_spin(uint64_t ticks, int blocks, void* stream, uint64_t* start = nullp
 // DLNB_CLOCK_CAL_MS (500) have passed; 0 = the attribute's nominal rate).
 double wallclock_hz(int device);
 double wallclock_hz_nominal(int device);
+// The measured rate's uncertainty (ppm: the two readings' standard errors
+// over the window); < 0 when the nominal rate is used.
+double wallclock_uncertainty_ppm(int device);
 void clock_cal_begin(int device);
 // One wave stores s_memrealtime into *slot (host-mapped memory) when the
 // stream reaches this point.

@@ -7,6 +7,7 @@
 #include <thread>
 #include <mutex>
 #include <cmath>
+#include <vector>
 #include <chrono>
 
 #include "deadline_sync.hpp"
@@ -594,20 +595,43 @@ double wallclock_hz_nominal(int device) {
   return static_cast<double>(khz) * 1e3;
 }
 
+// One wave streams the device clock into host-coherent memory: slot[0] =
+// s_memrealtime, rewritten every few hundred ns for `ticks`, then slot[1] = 1.
+__global__ void clock_stream_kernel(uint64_t* slot, uint64_t ticks) {
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t t = t0;
+    while (t - t0 < ticks) {
+      __hip_atomic_store(slot, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __builtin_amdgcn_s_sleep(4);
+      t = __builtin_amdgcn_s_memrealtime();
+    }
+    __hip_atomic_store(slot + 1, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 namespace {
 // The s_memrealtime clock's rate against the host's steady clock, measured
-// once per process and device: a reading pairs one stamp with the midpoint of
-// the tightest of 16 host brackets (launch + stream synchronize, ~5.5 us
-// half-width); two readings >= DLNB_CLOCK_CAL_MS (500) apart. The MI355X's
-// 100 MHz reference ran 7.6 ppm slow on the box measured (-7.63..-7.70 ppm at
-// 0.5..15.5 s windows, profiles/host_boundary_r4.md): a deadline task timed
-// in nominal ticks then lasted 21 us longer than the table time per headline
-// iteration; with the measured rate the tasks last the table time in host
-// (wall-clock) time, whichever way the box's crystal is off.
+// once per process and device from two readings >= DLNB_CLOCK_CAL_MS (500)
+// apart. A reading (read_clock) streams the device clock into host memory for
+// 10 ms (clock_stream_kernel) while the host samples it with its own clock
+// around every load - thousands of (host, device) pairs - and fits the device
+// clock to the host clock over them: the fit's value at the samples' mean
+// host time is the reading, its standard error (the pairs' scatter / sqrt n,
+// tens of ns) the reading's uncertainty. The latency from a device store to
+// the host seeing it is the same at both readings and drops out of the rate.
+// Round 4 paired one stamp with the tightest of 16 launch + synchronize
+// brackets (~5.5 us half-width): up to +-20 ppm over 500 ms, the
+// size of the headline deltas; this is ~0.1 ppm (wallclock_uncertainty_ppm).
+// The MI355X's 100 MHz reference ran 7.6 ppm slow on the box measured
+// (profiles/host_boundary_r4.md): a deadline task timed in nominal ticks then
+// lasted 21 us longer than the table time per headline iteration; with the
+// measured rate the tasks last the table time in host (wall-clock) time.
 struct ClockCal {
   std::mutex mu;
   bool begun = false, done = false;
-  double hz = 0.0, host_us = 0.0;
+  double hz = 0.0, host_us = 0.0, err_us = 0.0;
+  double uncertainty_ppm = -1.0;  // < 0: nominal rate (not measured)
   uint64_t tick = 0;
 };
 ClockCal& clock_cal(int device) {
@@ -617,7 +641,8 @@ ClockCal& clock_cal(int device) {
 double steady_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-void read_clock(int device, double* host_us, uint64_t* tick) {
+// Returns false when the stream never showed up (then nothing is read).
+bool read_clock(int device, double* host_us, uint64_t* tick, double* err_us) {
   int prev = 0;
   DLNB_HIP_CHECK(hipGetDevice(&prev));
   DLNB_HIP_CHECK(hipSetDevice(device));
@@ -626,30 +651,66 @@ void read_clock(int device, double* host_us, uint64_t* tick) {
   void* p = nullptr;
   DLNB_HIP_CHECK(hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent));
   uint64_t* slot = static_cast<uint64_t*>(p);
-  double best = 1e30;
-  for (int i = 0; i < 16; ++i) {
+  slot[0] = 0;
+  slot[1] = 0;
+  const double nominal = wallclock_hz_nominal(device);
+  hipLaunchKernelGGL(clock_stream_kernel, 1, 64, 0, s, slot, static_cast<uint64_t>(0.010 * nominal));
+  const hipError_t le = hipGetLastError();
+  std::vector<double> hs;
+  std::vector<uint64_t> ts;
+  hs.reserve(1 << 16);
+  ts.reserve(1 << 16);
+  const double start = steady_us();
+  uint64_t last = 0;
+  while (__atomic_load_n(slot + 1, __ATOMIC_ACQUIRE) == 0 && steady_us() - start < 2e6) {
     const double h0 = steady_us();
-    hipLaunchKernelGGL(stamp_kernel, 1, 64, 0, s, slot);
-    DLNB_HIP_CHECK(hipStreamSynchronize(s));
+    const uint64_t v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
     const double h1 = steady_us();
-    if (h1 - h0 < best) {
-      best = h1 - h0;
-      *host_us = 0.5 * (h0 + h1);
-      *tick = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
+    if (v != last && v != 0 && hs.size() < (1u << 16)) {
+      hs.push_back(0.5 * (h0 + h1));
+      ts.push_back(v);
+      last = v;
     }
   }
-  DLNB_HIP_CHECK(hipHostFree(p));
-  DLNB_HIP_CHECK(hipStreamDestroy(s));
+  const hipError_t se = hipStreamSynchronize(s);
+  (void)hipHostFree(p);
+  (void)hipStreamDestroy(s);
   DLNB_HIP_CHECK(hipSetDevice(prev));
+  DLNB_HIP_CHECK(le);
+  DLNB_HIP_CHECK(se);
+  if (hs.size() < 16) return false;
+  // least squares tick = a + b (h - hm), in ticks relative to the first
+  const size_t n = hs.size();
+  double hm = 0, tm = 0;
+  for (size_t i = 0; i < n; ++i) {
+    hm += hs[i];
+    tm += static_cast<double>(ts[i] - ts[0]);
+  }
+  hm /= n;
+  tm /= n;
+  double sxx = 0, sxy = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const double x = hs[i] - hm, y = static_cast<double>(ts[i] - ts[0]) - tm;
+    sxx += x * x;
+    sxy += x * y;
+  }
+  const double b = sxy / sxx;  // ticks per us
+  double ss = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const double r = static_cast<double>(ts[i] - ts[0]) - tm - b * (hs[i] - hm);
+    ss += r * r;
+  }
+  *host_us = hm;
+  *tick = ts[0] + static_cast<uint64_t>(std::llround(tm));
+  *err_us = std::sqrt(ss / static_cast<double>(n - 2)) / b / std::sqrt(static_cast<double>(n));
+  return true;
 }
 void clock_cal_begin_locked(int device, ClockCal& c) {
   c.begun = true;
-  if (env_int("DLNB_CLOCK_CAL_MS", 500) <= 0) {
+  if (env_int("DLNB_CLOCK_CAL_MS", 500) <= 0 || !read_clock(device, &c.host_us, &c.tick, &c.err_us)) {
     c.hz = wallclock_hz_nominal(device);
     c.done = true;
-    return;
   }
-  read_clock(device, &c.host_us, &c.tick);
 }
 }  // namespace
 
@@ -668,20 +729,31 @@ double wallclock_hz(int device) {
   const double window_us = static_cast<double>(env_int("DLNB_CLOCK_CAL_MS", 500)) * 1e3;
   const double waited = steady_us() - c.host_us;
   if (waited < window_us) std::this_thread::sleep_for(std::chrono::duration<double, std::micro>(window_us - waited));
-  double h = 0.0;
+  double h = 0.0, err = 0.0;
   uint64_t t = 0;
-  read_clock(device, &h, &t);
+  const bool ok = read_clock(device, &h, &t, &err);
   const double nominal = wallclock_hz_nominal(device);
-  const double hz = static_cast<double>(t - c.tick) / ((h - c.host_us) * 1e-6);
-  if (t > c.tick && h > c.host_us && std::fabs(hz / nominal - 1.0) < 200e-6) {
+  const double hz = ok ? static_cast<double>(t - c.tick) / ((h - c.host_us) * 1e-6) : 0.0;
+  const double unc = ok ? (c.err_us + err) / (h - c.host_us) * 1e6 : 1e9;
+  // the rate only with a sane value and an uncertainty well under the ppm
+  // the deadline compute cares about (a preempted host, a wrong clock)
+  if (ok && t > c.tick && h > c.host_us && std::fabs(hz / nominal - 1.0) < 200e-6 && unc < 2.0) {
     c.hz = hz;
-  } else {  // a preempted reading, or not the clock we think: keep the attribute's rate
-    std::fprintf(stderr, "[dlnb] warning: device %d clock measured at %.1f Hz vs %.0f nominal; using nominal\n", device,
-                 hz, nominal);
+    c.uncertainty_ppm = unc;
+  } else {
+    std::fprintf(stderr,
+                 "[dlnb] warning: device %d clock measured at %.1f Hz (+-%.2f ppm) vs %.0f nominal; using nominal\n",
+                 device, hz, unc, nominal);
     c.hz = nominal;
   }
   c.done = true;
   return c.hz;
+}
+
+double wallclock_uncertainty_ppm(int device) {
+  ClockCal& c = clock_cal(device);
+  std::lock_guard<std::mutex> g(c.mu);
+  return c.done ? c.uncertainty_ppm : -1.0;
 }
 
 int num_cus(int device) {

@@ -306,6 +306,7 @@ class GpuCompute : public ComputeEngine {
     j["time_scale"] = scale_;
     j["wallclock_hz"] = hz();
     j["wallclock_hz_nominal"] = kernels::wallclock_hz_nominal(dev_.index());
+    j["wallclock_uncertainty_ppm"] = kernels::wallclock_uncertainty_ppm(dev_.index());
     j["num_cus"] = cus_;
     if (mode_ == ComputeMode::Gemm) {
       j["deadline_grid"] = grid_;

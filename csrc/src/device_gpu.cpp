@@ -47,6 +47,7 @@ class GpuEvent : public Event {
   uint64_t* gate = nullptr;
   uint32_t tag = 0;
   hipStream_t on = nullptr;  // stream of the latest gate record
+  uint64_t gen = 0;          // the device's capture generation at that record
 };
 
 class GpuStream : public Stream {
@@ -217,11 +218,17 @@ class GpuDevice : public Device {
     if (!e.gate) e.gate = alloc_gate();
     e.tag = e.tag == 0xffffffffu ? 1u : e.tag + 1;
     e.on = s;
+    e.gen = gen_;
     kernels::gate_signal(e.gate, iter_word(), e.tag, s);
   }
   void gate_wait(GpuEvent& e, hipStream_t s) {
     if (e.tag == 0) return;  // never recorded: nothing to wait for (as a HIP event)
     if (e.on == s) return;   // recorded on this stream: already ordered
+    // recorded before this capture began (a previous iteration's record): in a
+    // replay its gate carries the previous iteration's sequence number and
+    // would never match - as a HIP event outside the capture, nothing to wait
+    // for inside the graph
+    if (e.gen != gen_) return;
     kernels::gate_wait(e.gate, iter_word(), e.tag, gate_timeout_ticks(), pool_ + 1, s);
   }
   bool queues_independent(const std::vector<Stream*>& ss, double timeout_s, std::string* detail) override {
@@ -276,6 +283,7 @@ class GpuDevice : public Device {
   std::vector<std::unique_ptr<GraphExec>> capture_lanes(const std::vector<Stream*>& lanes,
                                                         const std::function<void()>& enqueue,
                                                         const std::function<void(size_t)>& tail) override {
+    ++gen_;  // gate records from before this capture are not waited for in it
     size_t begun = 0;
     auto end_all = [&] {  // after a failure: end every capture begun, drop the graphs
       for (size_t i = 0; i < begun; ++i) {
@@ -323,6 +331,7 @@ class GpuDevice : public Device {
   }
   uint64_t* pool_ = nullptr;
   size_t next_gate_ = 0;
+  uint64_t gen_ = 0;  // capture generation (capture_lanes)
   bool gate_events_ = false;
   int idx_;
   std::string name_, arch_;

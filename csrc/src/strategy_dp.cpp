@@ -232,7 +232,8 @@ class DataParallel : public Strategy {
     const bool stamped = ce.stamps_task_start();
     const uint64_t* last_start = nullptr;
     const uint64_t* tail_end = nullptr;
-    ce.run(*compute_, fwd_us_, fwd_flops_);
+    uint64_t* fwd_start = stamped ? timers_->slot() : nullptr;
+    ce.run_stamped(*compute_, fwd_us_, fwd_flops_, fwd_start);
     for (int i = 0; i < nb_; ++i) {
       // only event records (or gate signals) on compute_ since the forward: one stretch of compute
       uint64_t* st = stamped && i == nb_ - 1 ? timers_->slot() : nullptr;
@@ -259,6 +260,8 @@ class DataParallel : public Strategy {
       // nothing follows on the compute stream: the iteration ends when both
       // streams have (graph join, lane done words, synchronize)
       timers_->gap(last_start, ce.task_ticks(bwd_us_[nb_ - 1]), tail_end, "barrier_time");
+      // the iteration on the device clock: forward start to the last all-reduce's end
+      timers_->gap(fwd_start, 0, tail_end, "device_span_time");
     } else {
       comm_stream_->record(*done_);
       timers_->stall(*compute_, *done_, "barrier_time");
@@ -330,6 +333,7 @@ class DataParallel : public Strategy {
     r["runtimes"] = timers_->values_json("runtimes");
     r["barrier_time"] = timers_->values_json("barrier_time");
     r["allreduce_time"] = timers_->values_json("allreduce_time");
+    if (!timers_->get("device_span_time").empty()) r["device_span_time"] = timers_->values_json("device_span_time");
     if (zero_) {
       r["reduce_scatter_time"] = timers_->values_json("reduce_scatter_time");
       r["param_allgather_time"] = timers_->values_json("param_allgather_time");

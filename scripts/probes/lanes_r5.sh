@@ -37,4 +37,10 @@ timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o c5
   build/bin/dp vit_h_32_float8 8 . --backend rccl --compute gemm --graph -w 2 -r 4 --quiet --silent \
   > $O/trace.log 2>&1 || { echo "trace rc=$?" >> $O/steps.log; exit 1; }
 ok trace
+# the slow replay every 16 timed iterations - HIP API + kernel trace of a 40-replay headline
+step trace16
+timeout -k 10 240 rocprofv3 --hip-trace --kernel-trace --output-format csv -d $O/trace16 -o head -- \
+  build/bin/fsdp llama3_8b_16_bfloat16 32 1 . --backend rccl --compute gemm --graph -w 1 -r 40 --time-scale 0.05 \
+  --quiet --silent --json $O/trace16.json > $O/trace16.log 2>&1 || { echo "trace16 rc=$?" >> $O/steps.log; exit 1; }
+ok trace16
 echo done >> $O/steps.log

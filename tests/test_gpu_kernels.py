@@ -325,6 +325,39 @@ def test_deadline_chain_continues_previous_deadline(dtype):
     assert 6.27 <= ms <= 6.3 * 1.01 + 0.08, ms  # 2 + 3 + 1 ms + the unabsorbed part of the wait
 
 
+def test_deadline_chain_counts_absorbed_lateness():
+    """the lateness a chained task takes out of its own compute is counted, not only what
+    exceeds the cap. Two chained deadline tasks back to back absorb the previous grid's drain and the launch
+    hop; with a 10-us idle kernel between them ~10 us more (+ its launch); the second task still starts at the
+    first's deadline and nothing is capped."""
+    a, b, c = _deadline_operands()
+    slot = torch.zeros(8, dtype=torch.int64, device="cuda")
+    ts = torch.zeros(4, dtype=torch.int64, device="cuda")
+    counters = torch.zeros(8, dtype=torch.int64, device="cuda")
+    from dlnetbench_amd import _native
+    hz = _native.lib().dlnb_wallclock_hz(0)
+    absorbed = {}
+    ep = 0
+    for idle in (0.0, 10.0, 0.0, 10.0):  # each twice: the first round also loads the kernels
+        counters.zero_()
+        gemm.gemm_deadline_ex(a, b, c, 1000.0, slot, ep + 1, chain=False, tstart=(ts, 0), grid=_grid(),
+                              counters=counters)
+        if idle:
+            gemm.idle_wait_us(idle)
+        gemm.gemm_deadline_ex(a, b, c, 1000.0, slot, ep + 2, chain=True, tstart=(ts, 1), grid=_grid(),
+                              counters=counters)
+        torch.cuda.synchronize()
+        ep += 2
+        v = counters.tolist()
+        t = ts.tolist()
+        assert v[0] == 0 and v[1] == 0, v  # kCappedTasks, kCappedTicks: nothing beyond the 30-us cap
+        assert v[5] == 1, v  # kAbsorbedTasks: the chained task came late and absorbed it
+        assert abs(t[1] - t[0] - 1000e-6 * hz) <= 1, t  # it started at the first task's deadline
+        absorbed[idle] = v[4] / hz * 1e6  # kAbsorbedTicks, us
+    assert 0 < absorbed[0.0] < 25, absorbed
+    assert 7 <= absorbed[10.0] - absorbed[0.0] <= 20, absorbed
+
+
 def test_deadline_gate_waits_for_signal():
     """A gated task (deadline_sync.hpp) starts when its gate is raised on another stream (here after a
     4 ms idle wait there), not when its kernel launches, and a chained gated task whose gate opened after

@@ -90,6 +90,13 @@ def test_strategy_hip_graph_replay(strategy, model, params, data_dir):
     key = "runtime" if strategy == "fsdp" else "runtimes"
     assert len(r[key]) == 3
     assert r["prearm_go_timeouts"] == 0  # every armed replay was started by the host's go, none by the timeout
+    # lane graphs: one linear graph per stream, joined by device gates, every gate wait satisfied
+    lg = g["dlnb"]["lane_graphs"]
+    assert lg["enabled"] and lg["linear"], lg
+    assert len(lg["graphs"]) == len([x for x in lg["graphs"] if x["linear"]]) >= 2, lg
+    cc = g["dlnb"].get("chain_capped")
+    if cc:
+        assert cc["gate_wait_timeouts_max"] == 0 and cc["compute_gate_timeouts_max"] == 0, cc
 
 
 @pytest.mark.parametrize("prearm", ["1", "0"])
@@ -109,6 +116,9 @@ def test_graph_loop_prearm_and_clock_rate(prearm, data_dir):
     c = g["compute"]
     assert c["wallclock_hz_nominal"] == 1e8 and c["wallclock_hz"] != 1e8
     assert abs(c["wallclock_hz"] / c["wallclock_hz_nominal"] - 1) < 200e-6
+    # streamed readings fitted over thousands of host samples: well under a ppm (the launch-bracket
+    # readings of round 4 allowed +-20 ppm over the 500-ms window)
+    assert 0 <= c["wallclock_uncertainty_ppm"] < 1.0, c
 
 
 @pytest.mark.parametrize("zero", [1, 2])
@@ -241,6 +251,37 @@ def test_dp_backward_buckets_chain_deadline(root):
     assert 0 <= cc["tasks_per_iter_max"] <= 8 and 0 <= cc["ms_per_iter_max"] < 0.3, cc
     assert d["compute"]["chain_absorb_us"] == pytest.approx(30.0, abs=0.02)
     assert cc["gate_wait_timeouts_max"] == 0, cc
+
+
+@pytest.mark.parametrize("mode", ["lanes", "single", "eager"])
+def test_dp_exposed_comm_matches_the_step(mode, root):
+    """DP's barrier_time (the reference's exposed-communication timer, dp.cpp:102-104) is the
+    last all-reduce's end stamp on the comm stream minus the last backward's deadline (its own start stamp +
+    its duration) - stamps no graph executor can reorder - so on the comm-bound ViT-H step it accounts for
+    what the iteration takes over the compute floor, together with the capped lateness of tasks queued behind
+    a collective: within 0.03 ms replayed (lane graphs, the default, and a single graph), within the host's
+    enqueue / boundary overhead eager. The device span (forward start to last all-reduce end) minus the floor
+    is exactly barrier + capped lateness in every mode."""
+    env = {"DLNB_LANE_GRAPHS": "0"} if mode == "single" else {}
+    doc = engine.run_native("dp", "vit_h_32_float8", 8, base_path=root, warmup=5, runs=20, compute="gemm",
+                            backend="rccl", graph=mode != "eager", quiet=True, env=env)
+    d = doc["global"]["dlnb"]
+    it = d["iteration"]
+    r = doc["ranks"][0]
+    bt = r["barrier_time"]
+    assert len(bt) == 20
+    barrier = sum(bt) / len(bt) * 1e3
+    capped = d["chain_capped"]["ms_per_iter_max"]
+    step = it["median_ms"] - it["compute_floor_ms"]
+    span = sum(r["device_span_time"]) / len(r["device_span_time"]) * 1e3 - it["compute_floor_ms"]
+    assert barrier > 0.02, (barrier, step)  # the last bucket's 158 MB all-reduce copy is exposed
+    assert abs(span - (barrier + capped)) <= 0.01, (span, barrier, capped)
+    tol = 0.03 if mode != "eager" else 0.5
+    assert abs(barrier + capped - step) <= tol, (mode, barrier, capped, step)
+    if mode == "lanes":
+        assert d["lane_graphs"]["enabled"] and d["lane_graphs"]["linear"], d["lane_graphs"]
+        assert abs(barrier - step) <= 0.03, (barrier, step)
+    assert d["chain_capped"]["gate_wait_timeouts_max"] == 0
 
 
 @pytest.mark.parametrize("graph", [True, False])
