@@ -597,20 +597,21 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     std::vector<Stream*> ss = strat->streams();
     std::vector<Stream*> others(ss.begin() + 1, ss.end());
     std::string why;
-    bool lanes = false;
     if (env_int("DLNB_LANE_GRAPHS", 1) == 0) {
       why = "DLNB_LANE_GRAPHS=0";
     } else if (ss.size() < 2) {
       why = "one stream";
+    } else if (ctx.ranks_on_device > 1) {
+      // a task spinning on its gate holds its CUs, which another rank's
+      // compute on the same device - the one the collective waits for - needs
+      why = "ranks share the device";
     } else {
       std::string detail;
-      lanes = ctx.dev->queues_independent(ss, 0.05, &detail);
-      if (!lanes) why = "streams share a hardware queue (" + detail + ")";
-      // every rank takes the same decision (a gate-joined rank and an
-      // edge-joined one issue the same collectives, but keep the reports alike)
-      lanes = ctx.hg().allreduce_max(lanes ? 0.0 : 1.0) < 0.5;
-      if (!lanes && why.empty()) why = "another rank's streams share a hardware queue";
+      if (!ctx.dev->queues_independent(ss, 0.05, &detail)) why = "streams share a hardware queue (" + detail + ")";
     }
+    // every rank takes the same decision, and every rank takes part in it
+    bool lanes = ctx.hg().allreduce_max(why.empty() ? 0.0 : 1.0) < 0.5;
+    if (!lanes && why.empty()) why = "another rank cannot use lane graphs";
     TraceRange tr("dlnb:graph_capture");
     T.begin_capture();
     if (TL) TL->begin_capture();
@@ -619,11 +620,31 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       // each lane ends by clearing its own deadline slot for the next replay
       lane_graphs = ctx.dev->capture_lanes(
           ss, [&] { strat->enqueue_iteration(); }, [&](size_t i) { ctx.compute->reset_slot(*ss[i]); });
-      lanes_ss = ss;
-      // the first replay starts from cleared slots too
-      ctx.compute->reset_clocks(*ss[0]);
-      ss[0]->synchronize();
-    } else {
+      // A lane whose graph is not a chain (a library adding its own stream
+      // to the capture, e.g. a collective's side work joined back) would be
+      // spread over executor streams that may share the compute lane's
+      // hardware queue - where a gate wait could hold the node that raises
+      // its gate. Then the whole iteration is captured as one graph instead.
+      bool linear = true;
+      for (const auto& g : lane_graphs) linear = linear && g->linear();
+      linear = ctx.hg().allreduce_max(linear ? 0.0 : 1.0) < 0.5;
+      if (linear) {
+        lanes_ss = ss;
+        // the first replay starts from cleared slots too
+        ctx.compute->reset_clocks(*ss[0]);
+        ss[0]->synchronize();
+      } else {
+        lane_graphs.clear();
+        ctx.dev->set_gate_events(false);
+        lanes = false;
+        why = "a lane graph is not linear";
+        T.end_capture();
+        if (TL) TL->end_capture();
+        T.begin_capture();
+        if (TL) TL->begin_capture();
+      }
+    }
+    if (!lanes) {
       // the engine's slot reset heads the graph, before every stream's first node
       graph = ctx.dev->capture(
           *ss[0], others, [&] { strat->enqueue_iteration(); }, [&] { ctx.compute->reset_clocks(*ss[0]); });
