@@ -564,12 +564,15 @@ def _timeline_block(a: argparse.Namespace, world: int, rank: int, budget: "_Budg
     if t is None:
         return _skipped(budget)
     try:
-        _child_run(a, world, rank, ".tl", "fsdp", a.model, (a.units, world), t,
-                   backend=a.hybrid_backend, graph=a.graph and a.backend in ("auto", "rccl", "xgmi"),
-                   compute=a.compute, warmup=1, runs=2,
-                   schedule=a.schedule, wire_dtype="bf16", timeline=path, timeline_iters=2)
+        d = _child_run(a, world, rank, ".tl", "fsdp", a.model, (a.units, world), t,
+                       backend=a.hybrid_backend, graph=a.graph and a.backend in ("auto", "rccl", "xgmi"),
+                       compute=a.compute, warmup=1, runs=2,
+                       schedule=a.schedule, wire_dtype="bf16", timeline=path, timeline_iters=2)
         if rank != 0:
             return res
+        # launch hops / drains the chained compute tasks absorbed (not in the spans' idle time)
+        res["chain_absorbed_ms_per_iter"] = ((d["global"]["dlnb"].get("chain_capped") or {})
+                                             .get("absorbed_ms_per_iter_max"))
         ev = tlt.load(path)
         bad = tlt.check(ev)
         s = tlt.summarize(ev)

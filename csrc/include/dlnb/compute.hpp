@@ -72,9 +72,13 @@ class ComputeEngine {
   // of a stream on different hardware queues: ~10 us per hop, measured in
   // profiles/graph_queues_r2.md). The compute still lasts the table's total.
   // Other modes: run().
-  // start (optional): as run_stamped's.
-  virtual void run_chained(Stream& s, double us, double flops, uint64_t* start = nullptr) {
+  // start (optional): as run_stamped's. done (optional): an event recorded
+  // on s once the task is over (Stream::record semantics) - with gate events
+  // (lane graphs) a deadline task raises its gate from its own kernel, so no
+  // gate_signal kernel sits between two compute tasks.
+  virtual void run_chained(Stream& s, double us, double flops, uint64_t* start = nullptr, Event* done = nullptr) {
     run_stamped(s, us, flops, start);
+    if (done) s.record(*done);
   }
   virtual uint64_t task_ticks(double us) const { (void)us; return 0; }
   // Device-side dependency times (gemm mode; csrc/kernels/deadline_sync.hpp).
@@ -101,8 +105,8 @@ class ComputeEngine {
     DLNB_THROW("this compute mode has no device gates");
   }
   virtual void run_gated(Stream& s, double us, double flops, const std::vector<int>& gates, uint64_t* start,
-                         bool chain) {
-    (void)s; (void)us; (void)flops; (void)gates; (void)start; (void)chain;
+                         bool chain, Event* done = nullptr) {
+    (void)s; (void)us; (void)flops; (void)gates; (void)start; (void)chain; (void)done;
     DLNB_THROW("this compute mode has no device gates");
   }
   // A second host-mapped slot the next deadline task's kernel writes its

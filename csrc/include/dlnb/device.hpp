@@ -152,6 +152,13 @@ class Device {
   // profiles/absorb_r4.md). Waits are bounded (DLNB_GATE_TIMEOUT_S, 60) and
   // counted (gate_event_timeouts).
   virtual void set_gate_events(bool on) { DLNB_REQUIRE(!on, "gate events need a GPU device"); }
+  // With gate events on: record e on s as a gate a kernel the caller launches
+  // on s next raises itself (returns the gate and tag it must store; a
+  // deadline task's DlSync::done_gate). False (nothing recorded) otherwise.
+  virtual bool arm_gate_record(Event& e, Stream& s, uint64_t** gate, uint32_t* tag) {
+    (void)e; (void)s; (void)gate; (void)tag;
+    return false;
+  }
   virtual bool gate_events() const { return false; }
   virtual uint64_t gate_event_timeouts() { return 0; }
   // Whether each stream of `ss` runs while another of them is blocked: every

@@ -50,6 +50,12 @@ struct DlSync {
   uint64_t* counters = nullptr;      // DlCounter words (nullptr: none)
   const uint64_t* iter = nullptr;    // iteration word the gates' sequence numbers carry (nullptr: 0)
   uint64_t gate_timeout = 0;         // ticks a gate wait may last (0: 60 s)
+  // A gate the task raises itself when its compute is over (block 0 leaving
+  // the kernel, i.e. the deadline passed): the dependent collective's signal
+  // without a gate_signal kernel after the task (nullptr: none). Set on the
+  // task's last launch only.
+  uint64_t* done_gate = nullptr;
+  uint32_t done_tag = 0;
 };
 // Device gates: two words {seq, time} in device memory (16-byte aligned).
 // seq = iteration << 32 | tag, the iteration read from *iter (the device's

@@ -144,6 +144,16 @@ __device__ __forceinline__ uint64_t agree_t0(uint64_t* slot, uint32_t epoch, uin
   return t0;
 }
 
+// The task's own done gate (DlSync::done_gate): raised by thread 0 of block 0
+// as the kernel leaves (every block stops at the same deadline, so this is the
+// end of the task's compute, not of the last block's drain).
+__device__ __forceinline__ void task_done(const DlSync& s) {
+  if (!s.done_gate || blockIdx.x != 0 || threadIdx.x != 0) return;
+  const uint64_t seq = gate_seq(s.iter, s.done_tag);
+  __hip_atomic_store(s.done_gate + 1, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(s.done_gate, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace dl
 }  // namespace kernels
 }  // namespace dlnb

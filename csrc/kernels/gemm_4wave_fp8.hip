@@ -448,7 +448,10 @@ __global__ void __launch_bounds__(256, 1)
     if (tid == 0) d.t0 = dl::agree_t0(slot, epoch, ticks, sync);  // only thread 0 reads the clock
     for (int round = 0;; ++round) {
       tile_coords(xcd_remap((blockIdx.x + round * gridDim.x) % T, T), nt_m, nt_n, group, tm, tn);
-      if (!tile4<BF, true>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d)) return;
+      if (!tile4<BF, true>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d)) {
+        dl::task_done(sync);
+        return;
+      }
     }
   }
 }
@@ -544,6 +547,7 @@ __global__ void __launch_bounds__(256, 1)
     first = false;
   }
   wait_vm<0>();  // the clamped / next-tile staging still in flight
+  if constexpr (DL) dl::task_done(sync);
 }
 
 // ---------------------------------------------------------------------------

@@ -401,8 +401,11 @@ __global__ void __launch_bounds__(512, 1)
   } else {
     if (tid == 0) d.t0 = dl::agree_t0(slot, epoch, ticks, sync);  // only thread 0 reads the clock
     for (int round = 0;; ++round)
-      if (!tile<FP8, true, BAL, UNI>(c, A, B, C, M, N, K, ldc, xcd_remap((blockIdx.x + round * gridDim.x) % T, T), d))
+      if (!tile<FP8, true, BAL, UNI>(c, A, B, C, M, N, K, ldc, xcd_remap((blockIdx.x + round * gridDim.x) % T, T),
+                                     d)) {
+        dl::task_done(sync);
         return;
+      }
   }
 }
 
@@ -617,6 +620,7 @@ __global__ void __launch_bounds__(512, 1)
   // stopped (partial tile discarded): drain every staged half-tile, re-align the rows
   wait_vm<0>();
   if (c.wr == 0) raw_barrier();
+  dl::task_done(sync);
 }
 
 }  // namespace

@@ -463,7 +463,10 @@ __global__ void __launch_bounds__(128 * WN, WN == 4 ? 2 : 1)
       __syncthreads();
     }
   }
-  if (expired) return;  // partial tile: the stand-in result is not needed
+  if (expired) {  // partial tile: the stand-in result is not needed
+    if constexpr (DEADLINE) dl::task_done(sync);
+    return;
+  }
 
   store_tile<FN, WTN>(C, ldc, tm, tn, wm, wn, r16, h, acc);
   if constexpr (!DEADLINE) return;

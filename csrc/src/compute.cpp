@@ -178,17 +178,18 @@ class GpuCompute : public ComputeEngine {
   uint64_t task_ticks(double us) const override { return ticks(us * scale_); }
   void run(Stream& s, double us, double flops) override { run_stamped(s, us, flops, nullptr); }
 
-  void run_chained(Stream& s, double us, double flops, uint64_t* start) override {
+  void run_chained(Stream& s, double us, double flops, uint64_t* start, Event* done) override {
     if (mode_ == ComputeMode::Gemm && us * scale_ >= 20.0 && chain_live_[slot_for(s)]) {
       kernels::DlSync sync;
       sync.tstart[0] = start;
       sync.tstart[1] = extra_start_;
       extra_start_ = nullptr;
-      deadline_task(s, us * scale_, sync, true);
+      deadline_task(s, us * scale_, sync, true, done);
       ++chained_;
       return;
     }
     run_stamped(s, us, flops, start);
+    if (done) s.record(*done);
   }
 
   bool gates_task(double us) const override { return mode_ == ComputeMode::Gemm && us * scale_ >= 20.0; }
@@ -213,7 +214,7 @@ class GpuCompute : public ComputeEngine {
   }
 
   void run_gated(Stream& s, double us, double flops, const std::vector<int>& gates, uint64_t* start,
-                 bool chain) override {
+                 bool chain, Event* done) override {
     DLNB_REQUIRE(gates_task(us), "run_gated: the task cannot wait on gates (see gates_task)");
     DLNB_REQUIRE(gates.size() <= 2, "run_gated: at most 2 gates per task");
     (void)flops;
@@ -227,7 +228,7 @@ class GpuCompute : public ComputeEngine {
     sync.tstart[1] = extra_start_;
     extra_start_ = nullptr;
     const bool chained = chain && chain_live_[slot_for(s)];
-    deadline_task(s, us * scale_, sync, chained);
+    deadline_task(s, us * scale_, sync, chained, done);
     if (chained) ++chained_;
     ++gated_;
   }
@@ -347,7 +348,9 @@ class GpuCompute : public ComputeEngine {
   // epoch; the kernels agree its start through the stream's slot line,
   // csrc/kernels/deadline_sync.hpp). chain: start at the stream's previous
   // deadline (or the latest gate) instead of when the first block arrives.
-  void deadline_task(Stream& s, double d, kernels::DlSync sync, bool chain) {
+  // done (optional): recorded when the task is over - with gate events its
+  // gate is raised by the task's own kernel (DlSync::done_gate, last launch).
+  void deadline_task(Stream& s, double d, kernels::DlSync sync, bool chain, Event* done = nullptr) {
     uint64_t* slot = slot_for(s);
     uint32_t& ep = epoch_[slot];
     ep = ep % 65535 + 1;  // 1..65535, never 0 (a fresh slot reads as epoch 0)
@@ -355,13 +358,23 @@ class GpuCompute : public ComputeEngine {
     sync.counters = counters_.as<uint64_t>();
     sync.iter = dev_.iter_word();
     sync.gate_timeout = gate_timeout_ticks_;
+    uint64_t* dgate = nullptr;
+    uint32_t dtag = 0;
+    const bool folded = done && dev_.arm_gate_record(*done, s, &dgate, &dtag);
     const uint64_t total = ticks(d);
     const uint64_t slice = slice_us_ > 0 ? std::max<uint64_t>(ticks(slice_us_), 1) : total;
     for (uint64_t end = slice;; end += slice) {
+      kernels::DlSync ls = end == slice ? sync : kernels::DlSync();
+      if (end >= total && folded) {
+        ls.done_gate = dgate;
+        ls.done_tag = dtag;
+        ls.iter = sync.iter;
+      }
       kernels::gemm_tn_deadline(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, total, slot, ep, grid_,
-                                s.native(), std::min(end, total), end == slice ? sync : kernels::DlSync());
+                                s.native(), std::min(end, total), ls);
       if (end >= total) break;
     }
+    if (done && !folded) s.record(*done);
     chain_live_[slot] = true;
   }
 

@@ -114,6 +114,7 @@ class GpuDevice : public Device {
     arch_ = prop.gcnArchName;
     total_ = prop.totalGlobalMem;
     kernels::clock_cal_begin(idx_);  // the rate is taken at its first use (stamp_hz), after setup
+    ensure_pool();                   // gates / iteration word: never allocated while a stream captures
   }
   ~GpuDevice() override {
     if (pool_) (void)hipFree(pool_);
@@ -214,12 +215,23 @@ class GpuDevice : public Device {
     static const double s = static_cast<double>(env_int("DLNB_GATE_TIMEOUT_S", 60));
     return static_cast<uint64_t>(s * stamp_hz());
   }
-  void gate_record(GpuEvent& e, hipStream_t s) {
+  void gate_mark(GpuEvent& e, hipStream_t s) {
     if (!e.gate) e.gate = alloc_gate();
     e.tag = e.tag == 0xffffffffu ? 1u : e.tag + 1;
     e.on = s;
     e.gen = gen_;
+  }
+  void gate_record(GpuEvent& e, hipStream_t s) {
+    gate_mark(e, s);
     kernels::gate_signal(e.gate, iter_word(), e.tag, s);
+  }
+  bool arm_gate_record(Event& ev, Stream& s, uint64_t** gate, uint32_t* tag) override {
+    auto& e = static_cast<GpuEvent&>(ev);
+    if (!gate_events_ || !e.dev) return false;
+    gate_mark(e, static_cast<hipStream_t>(s.native()));
+    *gate = e.gate;
+    *tag = e.tag;
+    return true;
   }
   void gate_wait(GpuEvent& e, hipStream_t s) {
     if (e.tag == 0) return;  // never recorded: nothing to wait for (as a HIP event)

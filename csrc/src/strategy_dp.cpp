@@ -237,7 +237,9 @@ class DataParallel : public Strategy {
     for (int i = 0; i < nb_; ++i) {
       // only event records (or gate signals) on compute_ since the forward: one stretch of compute
       uint64_t* st = stamped && i == nb_ - 1 ? timers_->slot() : nullptr;
-      ce.run_chained(*compute_, bwd_us_[i], bwd_flops_[i], st);
+      // the bucket's gradients are ready when its backward is: ready_[i] is
+      // recorded by the task itself (lane graphs: raised from its own kernel)
+      ce.run_chained(*compute_, bwd_us_[i], bwd_flops_[i], st, comm_gates_ ? nullptr : ready_[i].get());
       if (st) last_start = st;
       if (comm_gates_) {
         ce.signal(*compute_, g_ready_[i]);
@@ -247,7 +249,6 @@ class DataParallel : public Strategy {
         for (int j = 0; j <= i; ++j) ahead += bwd_us_[j];
         ce.wait_gate(*comm_stream_, g_ready_[i], ahead * ctx.opt.time_scale * 4 + 1e6);
       } else {
-        compute_->record(*ready_[i]);
         comm_stream_->wait(*ready_[i]);
       }
       int t = timers_->begin(*comm_stream_);

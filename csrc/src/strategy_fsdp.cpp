@@ -183,10 +183,10 @@ class Fsdp : public Strategy {
   // The gated form (after the event waits on the gates' collectives): start
   // at max(previous task's deadline, the gates' times); the first task of
   // the iteration is not chained and has no timer.
-  void compute_gated(std::vector<int> gates, const char* timer, double us, double flops) {
+  void compute_gated(std::vector<int> gates, const char* timer, double us, double flops, Event* done) {
     ComputeEngine& ce = *ctx_->compute;
     uint64_t* st = timers_->slot();
-    ce.run_gated(*compute_, us, flops, gates, st, prev_start_ != nullptr);
+    ce.run_gated(*compute_, us, flops, gates, st, prev_start_ != nullptr, done);
     if (timer && prev_start_) timers_->gap(prev_start_, prev_ticks_, st, timer);
     prev_start_ = st;
     prev_ticks_ = ce.task_ticks(us);
@@ -223,11 +223,13 @@ class Fsdp : public Strategy {
       }
       if (gated_) {
         if (!lane) compute_->wait(*ag_f_[u]);
-        compute_gated({g_ag_f_[u]}, u == 0 ? nullptr : "allgather_wait_fwd", fwd_us_, fwd_flops_);
+        // fwd_done_[u] recorded by the task itself (lane graphs: raised from its kernel)
+        compute_gated({g_ag_f_[u]}, u == 0 ? nullptr : "allgather_wait_fwd", fwd_us_, fwd_flops_,
+                      fwd_done_[u].get());
       } else {
         compute_after(*ag_f_[u], u == 0 ? nullptr : "allgather_wait_fwd", fwd_us_, fwd_flops_);
+        compute_->record(*fwd_done_[u]);
       }
-      compute_->record(*fwd_done_[u]);
     }
 
     // ---- backward (unit U-1's parameters are still gathered)
@@ -248,15 +250,15 @@ class Fsdp : public Strategy {
           if (!lane) compute_->wait(*rs_done_[u + 2]);
           gates.push_back(g_rs_[u + 2]);
         }
-        compute_gated(gates, u < U_ - 1 ? "allgather_wait_bwd" : nullptr, bwd_us_, bwd_flops_);
+        compute_gated(gates, u < U_ - 1 ? "allgather_wait_bwd" : nullptr, bwd_us_, bwd_flops_, bwd_done_[u].get());
       } else {
         if (u + 2 <= U_ - 1) compute_->wait(*rs_done_[u + 2]);
         if (u < U_ - 1)
           compute_after(*ag_b_[u], "allgather_wait_bwd", bwd_us_, bwd_flops_);
         else
           compute_after(nullptr, nullptr, bwd_us_, bwd_flops_);
+        compute_->record(*bwd_done_[u]);
       }
-      compute_->record(*bwd_done_[u]);
 
       rs_stream_->wait(*bwd_done_[u]);
       int tk = timers_->begin(*rs_stream_);

@@ -393,8 +393,8 @@ class TracingCompute : public ComputeEngine {
     traced(s, "compute", us, [&] { in_->run_stamped(s, us, flops, start); });
   }
   bool stamps_task_start() const override { return in_->stamps_task_start(); }
-  void run_chained(Stream& s, double us, double flops, uint64_t* start) override {
-    traced(s, "compute (chained)", us, [&] { in_->run_chained(s, us, flops, start); });
+  void run_chained(Stream& s, double us, double flops, uint64_t* start, Event* done) override {
+    traced(s, "compute (chained)", us, [&] { in_->run_chained(s, us, flops, start, done); });
   }
   uint64_t task_ticks(double us) const override { return in_->task_ticks(us); }
   bool gates_task(double us) const override { return in_->gates_task(us); }
@@ -402,11 +402,11 @@ class TracingCompute : public ComputeEngine {
   void signal(Stream& s, int gate) override { in_->signal(s, gate); }
   void wait_gate(Stream& s, int gate, double timeout_us) override { in_->wait_gate(s, gate, timeout_us); }
   void run_gated(Stream& s, double us, double flops, const std::vector<int>& gates, uint64_t* start,
-                 bool chain) override {
+                 bool chain, Event* done) override {
     Json a = Json::object();
     a["gates"] = static_cast<int>(gates.size());
-    traced(s, chain ? "compute (chained)" : "compute", us, [&] { in_->run_gated(s, us, flops, gates, start, chain); },
-           a);
+    traced(s, chain ? "compute (chained)" : "compute", us,
+           [&] { in_->run_gated(s, us, flops, gates, start, chain, done); }, a);
   }
   void set_next_start_slot(uint64_t* slot) override { in_->set_next_start_slot(slot); }
   void reset_clocks(Stream& s) override { in_->reset_clocks(s); }
