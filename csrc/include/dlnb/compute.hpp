@@ -119,6 +119,20 @@ class ComputeEngine {
   // the lane's own tasks being done by then).
   virtual void reset_clocks(Stream& s) { (void)s; }
   virtual void reset_slot(Stream& s) { (void)s; }
+  // Compute programs (lane graphs): the deadline tasks enqueued on s between
+  // begin_program(s) and end_program(s) run as ONE persistent kernel
+  // (kernels::gemm_tn_deadline_program): each task starts, chains and gates
+  // exactly as a launch of its own, with no kernel boundary between two
+  // tasks. Nothing but compute tasks may be enqueued on s inside (the caller's
+  // compute lane carries only them: gate events folded into the tasks, stall
+  // timers from the tasks' own stamps); a task the program cannot take (an
+  // idle / spin task) is launched between two programs. begin_program
+  // returns false when the engine does not build programs (then tasks launch
+  // one by one). after_capture(): upload the task lists of programs built
+  // during a graph capture (device memory written outside the capture).
+  virtual bool begin_program(Stream& s) { (void)s; return false; }
+  virtual void end_program(Stream& s) { (void)s; }
+  virtual void after_capture() {}
   // Counters of the chained / gated deadline tasks (kernels::DlCounter):
   //   capped: tasks whose first block came later than the absorb cap after
   //     their chained start (a wait, not a launch hop: e.g. a replayed graph

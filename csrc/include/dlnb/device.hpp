@@ -160,6 +160,8 @@ class Device {
     return false;
   }
   virtual bool gate_events() const { return false; }
+  // Whether s is being captured into a graph (GPU; never on the CPU).
+  virtual bool capturing(Stream& s) { (void)s; return false; }
   virtual uint64_t gate_event_timeouts() { return 0; }
   // Whether each stream of `ss` runs while another of them is blocked: every
   // ordered pair is probed (a one-wave wait on one for a store enqueued later

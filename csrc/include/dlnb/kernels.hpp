@@ -57,6 +57,15 @@ struct DlSync {
   uint64_t* done_gate = nullptr;
   uint32_t done_tag = 0;
 };
+// One task of a deadline program (gemm_tn_deadline_program; device memory):
+// its duration, its epoch on the slot (1..65535, consecutive tasks differ)
+// and its start protocol (gates, chain, stamps, done gate).
+struct DlTask {
+  DlSync sync;
+  uint64_t ticks = 0;
+  uint32_t epoch = 0;
+  uint32_t pad = 0;
+};
 // Device gates: two words {seq, time} in device memory (16-byte aligned).
 // seq = iteration << 32 | tag, the iteration read from *iter (the device's
 // iteration word, Device::iter_word; nullptr = 0) when the kernel runs: a
@@ -181,6 +190,21 @@ void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N
 void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,
                       uint64_t* slot, uint32_t epoch, int grid, void* stream, uint64_t slice_end = 0,
                       const DlSync& sync = DlSync());
+
+// A deadline PROGRAM: the tasks of tasks[0..n) (device memory) back to back
+// in ONE persistent launch - each task agrees its start exactly like a
+// separate gemm_tn_deadline launch (deadline_sync.hpp: gates, chain to the
+// previous task's deadline, stamps), runs its tiles until its deadline and
+// raises its done gate, then the blocks go on to the next task without
+// leaving the kernel. A lane's compute is then one kernel per iteration: no
+// kernel boundary (drain, dispatch, fences: 15-30 us per task measured in
+// round 5) between two compute tasks, and nothing for a collective's
+// one-wave kernels to queue behind at a task boundary. Only where
+// deadline_program_ok() (the per-tile 8-phase and one-wave-per-SIMD
+// kernels; not the short-K streaming or single-K-tile fallbacks).
+bool deadline_program_ok(int M, int N, int K, DType in_t);
+void gemm_tn_deadline_program(const void* A, const void* B, void* C, int M, int N, int K, DType in_t,
+                              const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream);
 
 // Elementwise "optimizer" stand-in (SGD-momentum on bf16 shards, fp32 math):
 // p = p - lr * (m = beta*m + g). Used by the optional --optimizer step.

@@ -423,7 +423,8 @@ template <bool BF, bool DL>
 __global__ void __launch_bounds__(256, 1)
     gemm_4wave_fp8_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
                           int K, int lda, int ldb, int ldc, int group, uint64_t* __restrict__ slot, uint32_t epoch,
-                          uint64_t ticks, uint64_t slice_end, DlSync sync) {
+                          uint64_t ticks, uint64_t slice_end, DlSync sync, const DlTask* __restrict__ prog = nullptr,
+                          int ntasks = 0) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + 16];  // ONE array: staging + deadline flags
   const int tid = threadIdx.x;
   CtxF c;
@@ -445,10 +446,25 @@ __global__ void __launch_bounds__(256, 1)
     tile_coords(xcd_remap(blockIdx.x, T), nt_m, nt_n, group, tm, tn);
     tile4<BF, false>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d);
   } else {
-    if (tid == 0) d.t0 = dl::agree_t0(slot, epoch, ticks, sync);  // only thread 0 reads the clock
-    for (int round = 0;; ++round) {
-      tile_coords(xcd_remap((blockIdx.x + round * gridDim.x) % T, T), nt_m, nt_n, group, tm, tn);
-      if (!tile4<BF, true>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d)) {
+    // one task (prog == nullptr) or the tasks of a program, back to back
+    int round = 0;
+    for (int k = 0;; ++k) {
+      if (prog) d.ticks = d.slice_end = prog[k].ticks;  // a uniform (scalar) load: stays in SGPRs
+      if (tid == 0) {  // only thread 0 reads the clock and decides the stop
+        if (prog)
+          d.t0 = dl::agree_t0(slot, prog[k].epoch, d.ticks, prog[k].sync);
+        else
+          d.t0 = dl::agree_t0(slot, epoch, ticks, sync);
+      }
+      for (;; ++round) {
+        tile_coords(xcd_remap((blockIdx.x + round * gridDim.x) % T, T), nt_m, nt_n, group, tm, tn);
+        if (!tile4<BF, true>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d)) break;
+      }
+      ++round;  // the stopped tile's partial work is dropped; the next task starts on the next tile
+      if (prog) {
+        dl::task_done(prog[k].sync);
+        if (k + 1 >= ntasks) return;
+      } else {
         dl::task_done(sync);
         return;
       }
@@ -916,6 +932,27 @@ void gemm_tn_4wave_deadline(const void* A, const void* B, void* C, int M, int N,
                        epoch, ticks, slice_end, sync);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 4-wave deadline launch failed: " << hipGetErrorString(e));
+}
+
+void gemm_4wave_deadline_program(const void* A, const void* B, void* C, int M, int N, int K, DType in_t,
+                                 const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream) {
+  DLNB_REQUIRE(gemm_4wave_shape_ok(M, N, K, in_t) && in_t != DType::FP16,
+               "gemm 4-wave deadline program: unsupported shape");
+  DLNB_REQUIRE(tasks != nullptr && n > 0 && slot != nullptr && grid > 0, "gemm 4-wave deadline program: bad args");
+  const int esz = static_cast<int>(dtype_size(in_t));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  auto* a = static_cast<const char*>(A);
+  auto* b = static_cast<const char*>(B);
+  auto* c = static_cast<__bf16*>(C);
+  const DlSync none;
+  if (in_t == DType::BF16)
+    hipLaunchKernelGGL((gemm_4wave_fp8_kernel<true, true>), grid, 256, 0, st, a, b, c, M, N, K * esz, K * esz,
+                       K * esz, N, 8, slot, 1u, 0ull, 0ull, none, tasks, n);
+  else
+    hipLaunchKernelGGL((gemm_4wave_fp8_kernel<false, true>), grid, 256, 0, st, a, b, c, M, N, K, K, K, N, 8, slot, 1u,
+                       0ull, 0ull, none, tasks, n);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) DLNB_THROW("gemm 4-wave deadline program launch failed: " << hipGetErrorString(e));
 }
 
 void gemm_tn_4wave_fp8_deadline(const void* A, const void* B, void* C, int M, int N, int K, uint64_t ticks,

@@ -378,7 +378,8 @@ template <bool FP8, bool DL, bool BAL = false, bool UNI = false>
 __global__ void __launch_bounds__(512, 1)
     gemm_8phase_kernel(const char* __restrict__ A, const char* __restrict__ B, __bf16* __restrict__ C, int M, int N,
                        int K, int lda, int ldb, int ldc, uint64_t* __restrict__ slot, uint32_t epoch, uint64_t ticks,
-                       uint64_t slice_end, DlSync sync, int group = 8) {
+                       uint64_t slice_end, DlSync sync, int group = 8, const DlTask* __restrict__ prog = nullptr,
+                       int ntasks = 0) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + 16];  // ONE array: staging + deadline flags
   const int tid = threadIdx.x;
   Ctx c;
@@ -399,13 +400,28 @@ __global__ void __launch_bounds__(512, 1)
   if constexpr (!DL) {
     tile<FP8, false, BAL, UNI>(c, A, B, C, M, N, K, ldc, xcd_remap(blockIdx.x, T), d, group);
   } else {
-    if (tid == 0) d.t0 = dl::agree_t0(slot, epoch, ticks, sync);  // only thread 0 reads the clock
-    for (int round = 0;; ++round)
-      if (!tile<FP8, true, BAL, UNI>(c, A, B, C, M, N, K, ldc, xcd_remap((blockIdx.x + round * gridDim.x) % T, T),
-                                     d)) {
+    // one task (prog == nullptr) or the tasks of a program, back to back
+    int round = 0;
+    for (int k = 0;; ++k) {
+      if (prog) d.ticks = d.slice_end = prog[k].ticks;  // a uniform (scalar) load: stays in SGPRs
+      if (tid == 0) {  // only thread 0 reads the clock and decides the stop
+        if (prog)
+          d.t0 = dl::agree_t0(slot, prog[k].epoch, d.ticks, prog[k].sync);
+        else
+          d.t0 = dl::agree_t0(slot, epoch, ticks, sync);
+      }
+      while (tile<FP8, true, BAL, UNI>(c, A, B, C, M, N, K, ldc, xcd_remap((blockIdx.x + round * gridDim.x) % T, T),
+                                       d))
+        ++round;
+      ++round;  // the stopped tile's partial work is dropped; the next task starts on the next tile
+      if (prog) {
+        dl::task_done(prog[k].sync);
+        if (k + 1 >= ntasks) return;
+      } else {
         dl::task_done(sync);
         return;
       }
+    }
   }
 }
 
@@ -662,6 +678,37 @@ static int deadline_group() {
   const char* env = std::getenv("DLNB_DEADLINE_GROUP");
   const int g = env ? std::atoi(env) : 0;
   return g > 0 ? g : 8;
+}
+
+// The per-tile 8-phase deadline kernel in program mode (bf16 with more than
+// 16 K-tiles, or fp8 K-tiles the 4-wave kernel does not take).
+bool deadline_program_8phase_ok(int M, int N, int K, DType in_t) {
+  if (!gemm_8phase_shape_ok(M, N, K, in_t)) return false;
+  const int nk = static_cast<int>(static_cast<size_t>(K) * dtype_size(in_t) / kRB);
+  return !(in_t == DType::BF16 && nk <= 16);
+}
+
+void gemm_8phase_deadline_program(const void* A, const void* B, void* C, int M, int N, int K, DType in_t,
+                                  const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream) {
+  DLNB_REQUIRE(deadline_program_8phase_ok(M, N, K, in_t), "gemm 8-phase deadline program: unsupported shape");
+  DLNB_REQUIRE(tasks != nullptr && n > 0 && slot != nullptr && grid > 0, "gemm 8-phase deadline program: bad args");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  auto* a = static_cast<const char*>(A);
+  auto* b = static_cast<const char*>(B);
+  auto* cc = static_cast<__bf16*>(C);
+  const int nk = static_cast<int>(static_cast<size_t>(K) * dtype_size(in_t) / kRB);
+  const DlSync none;
+  if (in_t == DType::BF16 && nk % 2 == 0)
+    hipLaunchKernelGGL((gemm_8phase_kernel<false, true, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, 1u,
+                       0ull, 0ull, none, deadline_group(), tasks, n);
+  else if (in_t == DType::BF16)
+    hipLaunchKernelGGL((gemm_8phase_kernel<false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, 1u, 0ull,
+                       0ull, none, deadline_group(), tasks, n);
+  else
+    hipLaunchKernelGGL((gemm_8phase_kernel<true, true, false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N,
+                       slot, 1u, 0ull, 0ull, none, deadline_group(), tasks, n);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) DLNB_THROW("gemm 8-phase deadline program launch failed: " << hipGetErrorString(e));
 }
 
 void gemm_tn_8phase_deadline(const void* A, const void* B, void* C, int M, int N, int K, DType in_t, uint64_t ticks,

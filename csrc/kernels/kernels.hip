@@ -862,6 +862,37 @@ void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K
   dispatch_gemm<true>(in_t, grid, A, B, C, M, N, K, K, K, N, slot, epoch, ticks, slice_end, S(stream), sync);
 }
 
+// (gemm_8phase.hip, gemm_4wave_fp8.hip)
+bool deadline_program_8phase_ok(int M, int N, int K, DType in_t);
+void gemm_8phase_deadline_program(const void* A, const void* B, void* C, int M, int N, int K, DType in_t,
+                                  const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream);
+void gemm_4wave_deadline_program(const void* A, const void* B, void* C, int M, int N, int K, DType in_t,
+                                 const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream);
+
+// The same kernel choice as gemm_tn_deadline, for the kernels with a program mode.
+namespace {
+int program_kernel(int M, int N, int K, DType in_t) {
+  if (!gemm_shape_ok(M, N, K, in_t)) return 0;
+  if (gemm_4wave_fp8_shape_ok(M, N, K, in_t)) return 4;
+  if (in_t == DType::BF16 && env_or("DLNB_DEADLINE_BF16", "8phase") == "4wave" && gemm_4wave_shape_ok(M, N, K, in_t))
+    return 4;
+  if (gemm_8phase_shape_ok(M, N, K, in_t)) return deadline_program_8phase_ok(M, N, K, in_t) ? 8 : 0;
+  return 0;
+}
+}  // namespace
+
+bool deadline_program_ok(int M, int N, int K, DType in_t) { return program_kernel(M, N, K, in_t) != 0; }
+
+void gemm_tn_deadline_program(const void* A, const void* B, void* C, int M, int N, int K, DType in_t,
+                              const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream) {
+  const int k = program_kernel(M, N, K, in_t);
+  DLNB_REQUIRE(k != 0, "gemm_tn_deadline_program: no program-mode kernel for M=" << M << " N=" << N << " K=" << K);
+  if (k == 4)
+    gemm_4wave_deadline_program(A, B, C, M, N, K, in_t, tasks, n, slot, grid, stream);
+  else
+    gemm_8phase_deadline_program(A, B, C, M, N, K, in_t, tasks, n, slot, grid, stream);
+}
+
 void sgd_momentum_bf16(void* param, void* mom, const void* grad, size_t n, float lr, float beta, void* stream) {
   if (n == 0) return;
   int grid = grid_for((n + 7) / 8, 256);

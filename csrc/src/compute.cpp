@@ -157,6 +157,32 @@ class GpuCompute : public ComputeEngine {
     dev_.memset_async(c + kernels::kCappedTasks, 0, 2 * sizeof(uint64_t), s);
     dev_.memset_async(c + kernels::kAbsorbedTicks, 0, 2 * sizeof(uint64_t), s);
   }
+  bool begin_program(Stream& s) override {
+    if (mode_ != ComputeMode::Gemm || slice_us_ > 0 || env_int("DLNB_COMPUTE_PROGRAMS", 1) == 0 ||
+        !kernels::deadline_program_ok(kMmax, N_, K_, dtype_))
+      return false;
+    if (!prog_dev_.data()) prog_dev_ = dev_.alloc(kProgTasks * sizeof(kernels::DlTask));
+    Program& p = programs_[&s];
+    DLNB_REQUIRE(!p.open, "begin_program: a program is already open on this stream");
+    p.open = true;
+    p.tasks.clear();
+    return true;
+  }
+  void end_program(Stream& s) override {
+    auto it = programs_.find(&s);
+    if (it == programs_.end() || !it->second.open) return;
+    flush_program(s);
+    it->second.open = false;
+  }
+  void after_capture() override {
+    if (uploads_.empty()) return;
+    auto st = dev_.create_stream(false);
+    for (const auto& u : uploads_)
+      dev_.copy_async(u.dst, u.tasks.data(), u.tasks.size() * sizeof(kernels::DlTask), *st);
+    st->synchronize();
+    uploads_.clear();
+  }
+
   bool chain_counters(ChainCounters& out) override {
     if (!counters_.data()) return false;
     uint64_t v[kernels::kNumCounters] = {};
@@ -235,8 +261,34 @@ class GpuCompute : public ComputeEngine {
 
   void set_next_start_slot(uint64_t* slot) override { extra_start_ = slot; }
 
+  // Launch the open program's tasks so far (it stays open for the tasks after).
+  void flush_program(Stream& s) {
+    auto it = programs_.find(&s);
+    if (it == programs_.end() || it->second.tasks.empty()) return;
+    std::vector<kernels::DlTask>& ts = it->second.tasks;
+    const size_t n = ts.size();
+    DLNB_REQUIRE(n <= kProgTasks, "compute program of " << n << " tasks exceeds the ring (" << kProgTasks << ")");
+    if (prog_next_ + n > kProgTasks) prog_next_ = 0;  // (a program runs before the ring comes round again)
+    kernels::DlTask* dst = prog_dev_.as<kernels::DlTask>() + prog_next_;
+    prog_next_ += n;
+    if (dev_.capturing(s)) {
+      uploads_.push_back(Upload{dst, ts});  // written by after_capture(), before the first replay
+    } else {
+      // not captured: the list goes in with the launch (pageable source: the copy completes before it returns)
+      dev_.copy_async(dst, ts.data(), n * sizeof(kernels::DlTask), s);
+      s.synchronize();
+    }
+    kernels::gemm_tn_deadline_program(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, dst, static_cast<int>(n),
+                                      slot_for(s), grid_, s.native());
+    ++programs_launched_;
+    program_tasks_ += static_cast<long>(n);
+    ts.clear();
+  }
+
   void run_stamped(Stream& s, double us, double flops, uint64_t* start) override {
     double d = us * scale_;
+    // a task that is not a deadline kernel cannot join the open program
+    if (mode_ == ComputeMode::Gemm && d < 20.0) flush_program(s);
     if (mode_ == ComputeMode::Gemm) chain_live_[slot_for(s)] = false;  // a chain restarts at every unchained task
     if (mode_ == ComputeMode::Sleep || mode_ == ComputeMode::Spin) {
       // the kernel stamps its own start (stall timers: gap() from it)
@@ -316,6 +368,9 @@ class GpuCompute : public ComputeEngine {
       j["chained_tasks"] = chained_;  // enqueued so far (a captured graph counts its one iteration)
       j["chain_absorb_us"] = absorb_ticks_ / hz() * 1e6;  // most lateness a chained / gated task absorbs
       j["gated_tasks"] = gated_;      // tasks that waited on device gates instead of stream events
+      // compute programs enqueued so far (one persistent kernel each) and their tasks
+      j["programs"] = programs_launched_;
+      j["program_tasks"] = program_tasks_;
     }
     if (A_.data()) {
       j["gemm_dtype"] = dtype_name(dtype_);
@@ -362,6 +417,20 @@ class GpuCompute : public ComputeEngine {
     uint32_t dtag = 0;
     const bool folded = done && dev_.arm_gate_record(*done, s, &dgate, &dtag);
     const uint64_t total = ticks(d);
+    auto pit = programs_.find(&s);
+    if (pit != programs_.end() && pit->second.open) {
+      // a task of the open program: launched with it (end_program)
+      DLNB_REQUIRE(folded || !done, "a program task's done event needs gate events");
+      kernels::DlTask t;
+      t.sync = sync;
+      t.sync.done_gate = dgate;
+      t.sync.done_tag = dtag;
+      t.ticks = total;
+      t.epoch = ep;
+      pit->second.tasks.push_back(t);
+      chain_live_[slot] = true;
+      return;
+    }
     const uint64_t slice = slice_us_ > 0 ? std::max<uint64_t>(ticks(slice_us_), 1) : total;
     for (uint64_t end = slice;; end += slice) {
       kernels::DlSync ls = end == slice ? sync : kernels::DlSync();
@@ -469,6 +538,22 @@ class GpuCompute : public ComputeEngine {
   double scale_;
   Buffer slots_;
   Buffer counters_;  // kernels::DlCounter words (DlSync::counters)
+  // programs: the open task list per stream, the device ring their task lists
+  // live in, uploads deferred past a graph capture
+  struct Program {
+    bool open = false;
+    std::vector<kernels::DlTask> tasks;
+  };
+  std::map<Stream*, Program> programs_;
+  Buffer prog_dev_;
+  size_t prog_next_ = 0;
+  struct Upload {
+    kernels::DlTask* dst;
+    std::vector<kernels::DlTask> tasks;
+  };
+  std::vector<Upload> uploads_;
+  static constexpr size_t kProgTasks = 16384;
+  long programs_launched_ = 0, program_tasks_ = 0;
   std::vector<uint64_t*> gates_;          // device gates (Device::alloc_gate)
   std::map<Stream*, size_t> slot_of_;
   std::map<uint64_t*, uint32_t> epoch_;

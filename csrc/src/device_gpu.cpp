@@ -205,6 +205,11 @@ class GpuDevice : public Device {
     gate_events_ = on;
   }
   bool gate_events() const override { return gate_events_; }
+  bool capturing(Stream& s) override {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    DLNB_HIP_CHECK(hipStreamIsCapturing(static_cast<hipStream_t>(s.native()), &st));
+    return st != hipStreamCaptureStatusNone;
+  }
   uint64_t gate_event_timeouts() override {
     if (!pool_) return 0;
     uint64_t v = 0;

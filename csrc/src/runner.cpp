@@ -620,6 +620,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       // each lane ends by clearing its own deadline slot for the next replay
       lane_graphs = ctx.dev->capture_lanes(
           ss, [&] { strat->enqueue_iteration(); }, [&](size_t i) { ctx.compute->reset_slot(*ss[i]); });
+      ctx.compute->after_capture();  // the compute programs' task lists
       // A lane whose graph is not a chain (a library adding its own stream
       // to the capture, e.g. a collective's side work joined back) would be
       // spread over executor streams that may share the compute lane's

@@ -233,6 +233,10 @@ class DataParallel : public Strategy {
     const uint64_t* last_start = nullptr;
     const uint64_t* tail_end = nullptr;
     uint64_t* fwd_start = stamped ? timers_->slot() : nullptr;
+    // Lane graphs: the forward and the backward buckets are one compute
+    // program (one persistent kernel, ComputeEngine::begin_program); each
+    // bucket's done event is raised from inside it.
+    const bool prog = ctx.dev->gate_events() && !comm_gates_ && ce.begin_program(*compute_);
     ce.run_stamped(*compute_, fwd_us_, fwd_flops_, fwd_start);
     for (int i = 0; i < nb_; ++i) {
       // only event records (or gate signals) on compute_ since the forward: one stretch of compute
@@ -257,6 +261,7 @@ class DataParallel : public Strategy {
       const uint64_t* e = timers_->end(t, *comm_stream_, "allreduce_time");
       if (e) tail_end = e;
     }
+    if (prog) ce.end_program(*compute_);
     if (last_start && tail_end && !ctx.opt.optimizer) {
       // nothing follows on the compute stream: the iteration ends when both
       // streams have (graph join, lane done words, synchronize)

@@ -204,6 +204,9 @@ class Fsdp : public Strategy {
     // waits (and the records nobody else waits for) would add a gate kernel
     // each, on the compute or the comm lane.
     const bool lane = gated_ && ctx.dev->gate_events();
+    // ... and the iteration's 64 compute tasks are one compute program (one
+    // persistent kernel: no kernel boundary between two tasks)
+    const bool prog = lane && ce.begin_program(*compute_);
     auto gather = [&](int u, Event& done, bool first, int gate) {
       int tk = timers_->begin(*ag_stream_);
       ag_comm_->all_gather(params_[u].data(), gathered_[u & 1].data(), shard_[u], t, *ag_stream_);
@@ -277,6 +280,7 @@ class Fsdp : public Strategy {
         ar_stream_->record(*ar_done_[u]);
       }
     }
+    if (prog) ce.end_program(*compute_);
     // ---- tail: exposed reduce-scatter / replica all-reduce
     Event& tail = R_ > 1 ? *ar_done_[0] : *rs_done_[0];
     if (gated_ && !ctx.opt.optimizer && tail_end_ && prev_start_) {

@@ -411,6 +411,9 @@ class TracingCompute : public ComputeEngine {
   void set_next_start_slot(uint64_t* slot) override { in_->set_next_start_slot(slot); }
   void reset_clocks(Stream& s) override { in_->reset_clocks(s); }
   void reset_slot(Stream& s) override { in_->reset_slot(s); }
+  bool begin_program(Stream& s) override { return in_->begin_program(s); }
+  void end_program(Stream& s) override { in_->end_program(s); }
+  void after_capture() override { in_->after_capture(); }
   void reset_capped(Stream& s) override { in_->reset_capped(s); }
   bool chain_counters(ChainCounters& c) override { return in_->chain_counters(c); }
   void set_task_timers(TimerSet* t) override { in_->set_task_timers(t); }
