@@ -160,6 +160,10 @@ class Device {
     return false;
   }
   virtual bool gate_events() const { return false; }
+  // Enqueue on s a store of the iteration word into *host_word (alloc_stamps
+  // memory): the last node of a lane graph, so the host sees the lane done
+  // without waiting for the graph's own completion (GPU only).
+  virtual void lane_done(Stream& s, uint64_t* host_word) { (void)s; (void)host_word; DLNB_THROW("lane_done needs a GPU"); }
   // Whether s is being captured into a graph (GPU; never on the CPU).
   virtual bool capturing(Stream& s) { (void)s; return false; }
   virtual uint64_t gate_event_timeouts() { return 0; }

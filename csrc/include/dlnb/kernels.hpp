@@ -116,6 +116,9 @@ void stamp(uint64_t* slot, void* stream);
 // host_wait also stores iter_value into *iter_out (device memory; optional)
 // once released: the pre-armed loop's lane head sets the iteration word.
 void host_signal(uint64_t* word, uint64_t value, void* stream);
+// *word (host-coherent) = *iter (the device's iteration word) when the stream
+// gets here: a lane graph's last node (relaxed: no L2 write-back first).
+void lane_done(uint64_t* word, const uint64_t* iter, void* stream);
 void host_wait(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uint64_t* timeouts, void* stream,
                uint64_t* iter_out = nullptr, uint64_t iter_value = 0);
 int num_cus(int device);

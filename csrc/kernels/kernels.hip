@@ -161,6 +161,15 @@ __global__ void probe_wait_kernel(const uint64_t* word, uint64_t value, uint64_t
   }
 }
 
+// A lane's last node: the iteration number into the host's done word - a
+// relaxed system-scope store (a release would write the L2 back first: ~50 us
+// after a collective's copy, measured in round 5) inside the lane's graph.
+__global__ void lane_done_kernel(uint64_t* word, const uint64_t* iter) {
+  if (threadIdx.x == 0)
+    __hip_atomic_store(word, __hip_atomic_load(iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void host_signal_kernel(uint64_t* word, uint64_t value) {
   if (threadIdx.x == 0) __hip_atomic_store(word, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -567,6 +576,12 @@ bool queues_independent(void* a, void* b, uint64_t timeout_ticks) {
   DLNB_HIP_CHECK(ea);
   DLNB_HIP_CHECK(eb);
   return ok;
+}
+
+void lane_done(uint64_t* word, const uint64_t* iter, void* stream) {
+  DLNB_REQUIRE(word != nullptr && iter != nullptr, "lane_done: null word");
+  hipLaunchKernelGGL(lane_done_kernel, 1, 64, 0, S(stream), word, iter);
+  DLNB_HIP_CHECK(hipGetLastError());
 }
 
 void host_signal(uint64_t* word, uint64_t value, void* stream) {

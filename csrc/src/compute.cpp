@@ -117,6 +117,8 @@ class GpuCompute : public ComputeEngine {
       // one 64-byte line per compute stream; the counters (DlCounter)
       slots_ = dev_.alloc(kSlots * 64);
       counters_ = dev_.alloc(kernels::kNumCounters * sizeof(uint64_t));
+      // compute programs' task lists (never allocated while a stream captures)
+      prog_dev_ = dev_.alloc(kProgTasks * sizeof(kernels::DlTask));
       auto zs = dev_.create_stream(false);
       dev_.memset_async(slots_.data(), 0, kSlots * 64, *zs);
       dev_.memset_async(counters_.data(), 0, kernels::kNumCounters * sizeof(uint64_t), *zs);
@@ -161,7 +163,6 @@ class GpuCompute : public ComputeEngine {
     if (mode_ != ComputeMode::Gemm || slice_us_ > 0 || env_int("DLNB_COMPUTE_PROGRAMS", 1) == 0 ||
         !kernels::deadline_program_ok(kMmax, N_, K_, dtype_))
       return false;
-    if (!prog_dev_.data()) prog_dev_ = dev_.alloc(kProgTasks * sizeof(kernels::DlTask));
     Program& p = programs_[&s];
     DLNB_REQUIRE(!p.open, "begin_program: a program is already open on this stream");
     p.open = true;

@@ -200,6 +200,7 @@ class GpuDevice : public Device {
     return pool_;
   }
   void set_iteration(Stream& s, uint64_t it) override { kernels::set_word(iter_word(), it, s.native()); }
+  void lane_done(Stream& s, uint64_t* host_word) override { kernels::lane_done(host_word, iter_word(), s.native()); }
   void set_gate_events(bool on) override {
     if (on) ensure_pool();
     gate_events_ = on;

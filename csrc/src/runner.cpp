@@ -585,6 +585,18 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   // with event edges when they share one (lane_graphs.reason says why).
   std::unique_ptr<GraphExec> graph;
   std::vector<std::unique_ptr<GraphExec>> lane_graphs;
+  // lane graphs: each lane's last node stores the iteration number here (the
+  // host's completion words; Device::lane_done)
+  uint64_t* lane_done = nullptr;
+  size_t lane_done_n = 0;
+  struct LaneDone {
+    Device& d;
+    uint64_t*& p;
+    size_t& n;
+    ~LaneDone() {
+      if (p && std::uncaught_exceptions() == 0) d.free_stamps(p, n);
+    }
+  } lane_done_guard{*ctx.dev, lane_done, lane_done_n};
   Json lane_info = Json::object();
   std::vector<Stream*> lanes_ss;  // streams the replay is launched on (lane graphs: each; else the compute stream)
   if (opt.graph) {
@@ -618,8 +630,14 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     if (lanes) {
       ctx.dev->set_gate_events(true);
       // each lane ends by clearing its own deadline slot for the next replay
+      lane_done_n = ss.size();
+      lane_done = ctx.dev->alloc_stamps(lane_done_n);
       lane_graphs = ctx.dev->capture_lanes(
-          ss, [&] { strat->enqueue_iteration(); }, [&](size_t i) { ctx.compute->reset_slot(*ss[i]); });
+          ss, [&] { strat->enqueue_iteration(); },
+          [&](size_t i) {
+            ctx.compute->reset_slot(*ss[i]);
+            ctx.dev->lane_done(*ss[i], lane_done + i);
+          });
       ctx.compute->after_capture();  // the compute programs' task lists
       // A lane whose graph is not a chain (a library adding its own stream
       // to the capture, e.g. a collective's side work joined back) would be
@@ -703,6 +721,17 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       strat->enqueue_iteration();
     }
   };
+  // Host wait for the iteration just enqueued: lane graphs by their done words
+  // (the graphs' own completion comes later: each ends with a marker), else
+  // the streams.
+  auto wait_iteration = [&] {
+    if (lane_done) {
+      CompletionFlag cf(lane_done, lane_done_n, dev_iter);
+      strat->synchronize();
+    } else {
+      strat->synchronize();
+    }
+  };
   ctx.hg().barrier();
 
   // ---- warm-up
@@ -712,7 +741,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     TraceRange tr("dlnb:warmup_iteration");
     double t0 = now_s();
     enqueue();
-    strat->synchronize();
+    wait_iteration();
     warm.push_back(now_s() - t0);
     if (TL) TL->collect(-1);
   }
@@ -786,8 +815,10 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     }
   } handshake{*ctx.dev, hs, nhs};
   const double go_timeout_s = 30.0;
+  std::vector<uint64_t> armed_iter;  // device iteration number of each armed replay
   auto arm = [&](int r) {
     const uint64_t it = ++dev_iter;
+    armed_iter.push_back(it);
     for (size_t i = 0; i < nlanes; ++i) {
       Stream& l = *lanes_ss[i];
       ctx.dev->host_wait(l, hs, static_cast<uint64_t>(r) + 1, go_timeout_s, hs + 1, it);
@@ -797,7 +828,8 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       else
         lane_graphs[i]->launch(l);
       if (TL && tl_edges && i == 0) TL->edge(l, 1);
-      ctx.dev->host_signal(l, hs + 2 + i, static_cast<uint64_t>(r) + 1);
+      // (lane graphs signal from inside: their last node, lane_done)
+      if (!lane_done) ctx.dev->host_signal(l, hs + 2 + i, static_cast<uint64_t>(r) + 1);
     }
   };
   ctx.hg().barrier();
@@ -813,13 +845,18 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     if (hs) {
       __atomic_store_n(hs, static_cast<uint64_t>(r) + 1, __ATOMIC_RELEASE);  // go
       if (r + 1 < runs) arm(r + 1);
-      CompletionFlag cf(hs + 2, nlanes, static_cast<uint64_t>(r) + 1);
-      strat->synchronize();
+      if (lane_done) {
+        CompletionFlag cf(lane_done, lane_done_n, armed_iter.at(static_cast<size_t>(r)));
+        strat->synchronize();
+      } else {
+        CompletionFlag cf(hs + 2, nlanes, static_cast<uint64_t>(r) + 1);
+        strat->synchronize();
+      }
     } else {
       if (TL && replay && tl_edges) TL->edge(*origin, 0);
       enqueue();
       if (TL && replay && tl_edges) TL->edge(*origin, 1);
-      strat->synchronize();
+      wait_iteration();
     }
     const double t1 = now_s();
     T.add(rkey, t1 - t0);

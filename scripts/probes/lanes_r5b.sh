@@ -3,7 +3,7 @@
 # time-scaled headline, against lanes without programs and the single graph; a C5 kernel trace; the lane / timer /
 # deadline GPU tests.
 set -u
-O=gpurun_out/lanes_b
+O=${O:-gpurun_out/lanes_b}
 mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0 DLNB_NO_TORCH=1 DLNB_GATE_TIMEOUT_S=5
 step() { echo "$1 start $(date +%s)" >> $O/steps.log; }

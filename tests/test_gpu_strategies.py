@@ -90,10 +90,16 @@ def test_strategy_hip_graph_replay(strategy, model, params, data_dir):
     key = "runtime" if strategy == "fsdp" else "runtimes"
     assert len(r[key]) == 3
     assert r["prearm_go_timeouts"] == 0  # every armed replay was started by the host's go, none by the timeout
-    # lane graphs: one linear graph per stream, joined by device gates, every gate wait satisfied
+    # lane graphs: one linear graph per stream, joined by device gates, every gate wait satisfied; a strategy
+    # whose collectives add their own streams to a capture (RCCL's grouped all-to-all on the compute stream:
+    # hybrid_3d_moe) gets the single graph, with the reason reported
     lg = g["dlnb"]["lane_graphs"]
-    assert lg["enabled"] and lg["linear"], lg
-    assert len(lg["graphs"]) == len([x for x in lg["graphs"] if x["linear"]]) >= 2, lg
+    if strategy in ("dp", "fsdp"):
+        assert lg["enabled"] and lg["linear"], lg
+    if lg["enabled"]:
+        assert lg["linear"] and len(lg["graphs"]) >= 2 and all(x["linear"] for x in lg["graphs"]), lg
+    else:
+        assert lg["reason"], lg
     cc = g["dlnb"].get("chain_capped")
     if cc:
         assert cc["gate_wait_timeouts_max"] == 0 and cc["compute_gate_timeouts_max"] == 0, cc
