@@ -340,6 +340,7 @@ __device__ __forceinline__ void prologue(const CtxF& c, int wr, int wc, int offl
 // come first (tied to the last row, so no read is hoisted above them); the
 // lane's element offset is made opaque so the 64 store addresses are not
 // hoisted out of a tile loop (they would stay live across it and spill).
+template <bool NT = false>
 __device__ __forceinline__ void store_tile(f32x4 (&acc)[8][8], __bf16* __restrict__ C, int ldc, int tm, int tn, int wr,
                                            int wc, int r16, int h) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
@@ -353,7 +354,7 @@ __device__ __forceinline__ void store_tile(f32x4 (&acc)[8][8], __bf16* __restric
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; j += 2)
-      epi::store_pair(base + static_cast<size_t>(i * 16) * ldc + j * 16, acc[i][j], acc[i][j + 1], h, wide);
+      epi::store_pair<NT>(base + static_cast<size_t>(i * 16) * ldc + j * 16, acc[i][j], acc[i][j + 1], h, wide);
 }
 
 // One 256 x 256 tile of C. Returns false if the deadline stopped it (no
@@ -403,7 +404,7 @@ __device__ __forceinline__ bool tile4(CtxF& c, const char* __restrict__ A, const
   if constexpr (DL) {
     if (stop) return false;
   }
-  store_tile(acc, C, ldc, tm, tn, wr, wc, r16, h);
+  store_tile<DL>(acc, C, ldc, tm, tn, wr, wc, r16, h);
   return true;
 }
 
@@ -545,7 +546,7 @@ __global__ void __launch_bounds__(256, 1)
     stop = ktile<BF, 0, true, DL, true, -1>(c, 0, wr, wc, offl, offh, a, b, acc, scale, d, !first);
     stop = ktiles_rest<BF, DL>(c, nk, wr, wc, offl, offh, a, b, acc, scale, d, stop);
     if (DL && stop) break;  // partial tile: the stand-in result is not needed
-    store_tile(acc, C, ldc, tm, tn, wr, wc, r16, h);
+    store_tile<DL>(acc, C, ldc, tm, tn, wr, wc, r16, h);
     if (!c.has_next) break;
     // advance the stream: the next tile's K-tiles 0, 1 are staged, its K-tile-0
     // fragments (but a[7]) read

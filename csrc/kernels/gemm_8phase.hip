@@ -365,7 +365,7 @@ __device__ __forceinline__ bool tile(Ctx& c, const char* __restrict__ A, const c
       for (int i = 0; i < 4; ++i) {
         const int m = tm * kT + qm * 128 + c.wr * 64 + i * 16 + c.r16;
         const int n = tn * kT + qn * 128 + c.wc * 32;
-        epi::store_pair(C + static_cast<size_t>(m) * ldc + n, acc[qm][qn][i][0], acc[qm][qn][i][1], c.h, wide);
+        epi::store_pair<DL>(C + static_cast<size_t>(m) * ldc + n, acc[qm][qn][i][0], acc[qm][qn][i][1], c.h, wide);
       }
   return true;
 }
@@ -460,7 +460,7 @@ __device__ __forceinline__ void store_tile(const Ctx& c, __bf16* __restrict__ C,
     for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        epi::store_pair(base + static_cast<size_t>(qm * 128 + i * 16) * ldc + qn * 128, acc[qm][qn][i][0],
+        epi::store_pair<true>(base + static_cast<size_t>(qm * 128 + i * 16) * ldc + qn * 128, acc[qm][qn][i][0],
                         acc[qm][qn][i][1], c.h, wide);
         acc[qm][qn][i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
         acc[qm][qn][i][1] = f32x4{0.f, 0.f, 0.f, 0.f};

@@ -37,6 +37,12 @@ __device__ __forceinline__ bf16x4_t to_bf16(const f32x4_t& a) {
 }
 
 // row: C + (this lane's row) * ldc + (the pair's first column); h = lane / 16.
+// NT: non-temporal (streaming) stores - the deadline stand-in's output is
+// never read, and lines it leaves dirty in the XCDs' L2s have to be written
+// back at the kernel's end-of-kernel release: tens of us that every kernel
+// after it on any queue waits for (round 5: one-wave stamp / done kernels
+// took ~40 us right after a deadline GEMM ended).
+template <bool NT = false>
 __device__ __forceinline__ void store_pair(__bf16* row, const f32x4_t& f0, const f32x4_t& f1, int h, bool wide) {
   const bf16x4_t o0 = to_bf16(f0), o1 = to_bf16(f1);
   if (wide) {
@@ -44,10 +50,21 @@ __device__ __forceinline__ void store_pair(__bf16* row, const f32x4_t& f0, const
     const auto s0 = __builtin_amdgcn_permlane16_swap(u0[0], u1[0], false, false);
     const auto s1 = __builtin_amdgcn_permlane16_swap(u0[1], u1[1], false, false);
     const u32x4_t v = {s0[0], s1[0], s0[1], s1[1]};
-    *reinterpret_cast<u32x4_t*>(row + (h & 1) * 16 + (h >> 1) * 8) = v;
+    u32x4_t* p = reinterpret_cast<u32x4_t*>(row + (h & 1) * 16 + (h >> 1) * 8);
+    if constexpr (NT)
+      __builtin_nontemporal_store(v, p);
+    else
+      *p = v;
   } else {
-    *reinterpret_cast<bf16x4_t*>(row + 4 * h) = o0;
-    *reinterpret_cast<bf16x4_t*>(row + 16 + 4 * h) = o1;
+    bf16x4_t* p0 = reinterpret_cast<bf16x4_t*>(row + 4 * h);
+    bf16x4_t* p1 = reinterpret_cast<bf16x4_t*>(row + 16 + 4 * h);
+    if constexpr (NT) {
+      __builtin_nontemporal_store(o0, p0);
+      __builtin_nontemporal_store(o1, p1);
+    } else {
+      *p0 = o0;
+      *p1 = o1;
+    }
   }
 }
 
