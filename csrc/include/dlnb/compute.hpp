@@ -133,6 +133,19 @@ class ComputeEngine {
   virtual bool begin_program(Stream& s) { (void)s; return false; }
   virtual void end_program(Stream& s) { (void)s; }
   virtual void after_capture() {}
+  // Lane join (the runner, lane graphs): the next program ended on s finishes
+  // with a join task - thread 0 of block 0 waits for `gates` (the other
+  // lanes' end gates, raised with `tag`) and stores the iteration number into
+  // *host_done - so the iteration's completion is signalled from inside the
+  // still-running compute kernel (a kernel ending around the iteration's
+  // last collective costs the one-wave kernels near it ~40 us, round 5).
+  // program_joined(s): whether it happened (then the lanes need no done
+  // word of their own, nor a slot reset: program epochs follow the
+  // iteration word).
+  virtual void set_lane_join(Stream& s, const std::vector<uint64_t*>& gates, uint32_t tag, uint64_t* host_done) {
+    (void)s; (void)gates; (void)tag; (void)host_done;
+  }
+  virtual bool program_joined(Stream& s) { (void)s; return false; }
   // Counters of the chained / gated deadline tasks (kernels::DlCounter):
   //   capped: tasks whose first block came later than the absorb cap after
   //     their chained start (a wait, not a launch hop: e.g. a replayed graph

@@ -140,6 +140,11 @@ class Device {
   // next replay's waits. alloc_gate: a zeroed gate (freed with the device).
   virtual uint64_t* alloc_gate();
   virtual uint64_t* iter_word() { return nullptr; }
+  // Raise a gate from alloc_gate with `tag` when s gets here (GPU).
+  virtual void signal_gate(Stream& s, uint64_t* gate, uint32_t tag) {
+    (void)s; (void)gate; (void)tag;
+    DLNB_THROW("device gates need a GPU device");
+  }
   // Enqueue on s a store of `it` into the iteration word (a lane's head).
   virtual void set_iteration(Stream& s, uint64_t it);
   // Gate events: while on, recording a dependency-only event (create_event

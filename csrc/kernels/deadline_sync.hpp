@@ -154,6 +154,40 @@ __device__ __forceinline__ void task_done(const DlSync& s) {
   __hip_atomic_store(s.done_gate, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// A program's join task (DlTask with ticks == 0, the last of its program):
+// thread 0 of block 0 waits for its gates (the other lanes' end gates, as a
+// task's gates: bounded, counted) and then stores the iteration number into
+// the host's done word (sync.tstart[0]; relaxed, system scope) - the whole
+// iteration done, signalled while the kernel still runs.
+__device__ __forceinline__ void join(const DlSync& s) {
+  const uint64_t gate_timeout = s.gate_timeout ? s.gate_timeout : kGateTimeoutTicks;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    if (!s.gate[i]) continue;
+    const uint64_t want = gate_seq(s.iter, s.tag[i]);
+    const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(s.gate[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != want) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - w0 > gate_timeout) {
+        count(s.counters, kGateTimeouts, 1ull);
+        break;
+      }
+    }
+  }
+  if (s.tstart[0])
+    __hip_atomic_store(s.tstart[0], s.iter ? ld(s.iter) : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// A program task's epoch: from the iteration word and the task's index among
+// the stream's program tasks of the iteration (DlTask::epoch, < 4096), so
+// consecutive tasks - the last of one replay and the first of the next too -
+// always differ and no slot reset is needed between replays; 1..32767
+// (launches of their own take 32768..65534, ComputeEngine).
+__device__ __forceinline__ uint32_t program_epoch(const DlTask* prog, int k) {
+  const uint64_t it = prog[0].sync.iter ? ld(prog[0].sync.iter) : 0ull;
+  return static_cast<uint32_t>((it * 4096ull + prog[k].epoch) % 32767ull) + 1u;
+}
+
 }  // namespace dl
 }  // namespace kernels
 }  // namespace dlnb

@@ -403,10 +403,16 @@ __global__ void __launch_bounds__(512, 1)
     // one task (prog == nullptr) or the tasks of a program, back to back
     int round = 0;
     for (int k = 0;; ++k) {
-      if (prog) d.ticks = d.slice_end = prog[k].ticks;  // a uniform (scalar) load: stays in SGPRs
+      if (prog) {
+        d.ticks = d.slice_end = prog[k].ticks;  // a uniform (scalar) load: stays in SGPRs
+        if (d.ticks == 0) {                      // the join task (the program's last)
+          if (blockIdx.x == 0 && tid == 0) dl::join(prog[k].sync);
+          return;
+        }
+      }
       if (tid == 0) {  // only thread 0 reads the clock and decides the stop
         if (prog)
-          d.t0 = dl::agree_t0(slot, prog[k].epoch, d.ticks, prog[k].sync);
+          d.t0 = dl::agree_t0(slot, dl::program_epoch(prog, k), d.ticks, prog[k].sync);
         else
           d.t0 = dl::agree_t0(slot, epoch, ticks, sync);
       }

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cmath>
 #include <map>
+#include <set>
 
 #include "dlnb/kernels.hpp"
 
@@ -166,16 +167,46 @@ class GpuCompute : public ComputeEngine {
     Program& p = programs_[&s];
     DLNB_REQUIRE(!p.open, "begin_program: a program is already open on this stream");
     p.open = true;
+    p.index = 0;
     p.tasks.clear();
     return true;
   }
   void end_program(Stream& s) override {
     auto it = programs_.find(&s);
     if (it == programs_.end() || !it->second.open) return;
+    Program& p = it->second;
+    auto j = joins_.find(&s);
+    if (j != joins_.end() && !p.tasks.empty()) {
+      // the join task(s): up to two gates each, the last one stores the done word
+      const Join& jn = j->second;
+      size_t g = 0;
+      do {
+        kernels::DlTask t;
+        t.sync.iter = dev_.iter_word();
+        t.sync.counters = counters_.as<uint64_t>();
+        t.sync.gate_timeout = gate_timeout_ticks_;
+        for (int i = 0; i < 2 && g < jn.gates.size(); ++i, ++g) {
+          t.sync.gate[i] = jn.gates[g];
+          t.sync.tag[i] = jn.tag;
+        }
+        if (g >= jn.gates.size()) t.sync.tstart[0] = jn.host_done;
+        t.ticks = 0;
+        p.tasks.push_back(t);
+      } while (g < jn.gates.size());
+      joins_.erase(j);
+      joined_.insert(&s);
+    }
     flush_program(s);
-    it->second.open = false;
+    p.open = false;
   }
+  void set_lane_join(Stream& s, const std::vector<uint64_t*>& gates, uint32_t tag, uint64_t* host_done) override {
+    if (mode_ != ComputeMode::Gemm) return;
+    joins_[&s] = Join{gates, tag, host_done};
+    joined_.erase(&s);
+  }
+  bool program_joined(Stream& s) override { return joined_.count(&s) != 0; }
   void after_capture() override {
+    joins_.clear();  // a join no program took does not carry over
     if (uploads_.empty()) return;
     auto st = dev_.create_stream(false);
     for (const auto& u : uploads_)
@@ -408,8 +439,11 @@ class GpuCompute : public ComputeEngine {
   // gate is raised by the task's own kernel (DlSync::done_gate, last launch).
   void deadline_task(Stream& s, double d, kernels::DlSync sync, bool chain, Event* done = nullptr) {
     uint64_t* slot = slot_for(s);
-    uint32_t& ep = epoch_[slot];
-    ep = ep % 65535 + 1;  // 1..65535, never 0 (a fresh slot reads as epoch 0)
+    uint32_t& ep0 = epoch_[slot];
+    ep0 = ep0 % 32767 + 1;
+    // 32768..65534 (never 0: a fresh slot reads as epoch 0); program tasks
+    // take 1..32767 from the iteration word (deadline_sync.hpp program_epoch)
+    const uint32_t ep = 32767 + ep0;
     sync.chain = chain ? absorb_ticks_ : 0u;
     sync.counters = counters_.as<uint64_t>();
     sync.iter = dev_.iter_word();
@@ -427,7 +461,8 @@ class GpuCompute : public ComputeEngine {
       t.sync.done_gate = dgate;
       t.sync.done_tag = dtag;
       t.ticks = total;
-      t.epoch = ep;
+      DLNB_REQUIRE(pit->second.index < 4096, "more than 4096 program tasks per iteration on one stream");
+      t.epoch = pit->second.index++;  // the kernel derives the epoch from it and the iteration word
       pit->second.tasks.push_back(t);
       chain_live_[slot] = true;
       return;
@@ -543,9 +578,17 @@ class GpuCompute : public ComputeEngine {
   // live in, uploads deferred past a graph capture
   struct Program {
     bool open = false;
+    uint32_t index = 0;  // program tasks of the iteration so far (DlTask::epoch)
     std::vector<kernels::DlTask> tasks;
   };
   std::map<Stream*, Program> programs_;
+  struct Join {
+    std::vector<uint64_t*> gates;
+    uint32_t tag;
+    uint64_t* host_done;
+  };
+  std::map<Stream*, Join> joins_;  // set_lane_join, taken by the next end_program
+  std::set<Stream*> joined_;
   Buffer prog_dev_;
   size_t prog_next_ = 0;
   struct Upload {

@@ -201,6 +201,9 @@ class GpuDevice : public Device {
   }
   void set_iteration(Stream& s, uint64_t it) override { kernels::set_word(iter_word(), it, s.native()); }
   void lane_done(Stream& s, uint64_t* host_word) override { kernels::lane_done(host_word, iter_word(), s.native()); }
+  void signal_gate(Stream& s, uint64_t* gate, uint32_t tag) override {
+    kernels::gate_signal(gate, iter_word(), tag, s.native());
+  }
   void set_gate_events(bool on) override {
     if (on) ensure_pool();
     gate_events_ = on;

@@ -589,6 +589,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   // host's completion words; Device::lane_done)
   uint64_t* lane_done = nullptr;
   size_t lane_done_n = 0;
+  bool joined = false;  // the compute program's join signals the iteration (lane_done[0] alone)
   struct LaneDone {
     Device& d;
     uint64_t*& p;
@@ -632,13 +633,25 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       // each lane ends by clearing its own deadline slot for the next replay
       lane_done_n = ss.size();
       lane_done = ctx.dev->alloc_stamps(lane_done_n);
+      // A compute program on the compute lane ends with a join on the other
+      // lanes' end gates and signals the whole iteration from inside the
+      // kernel (ComputeEngine::set_lane_join); otherwise every lane ends with
+      // its own done word (and clears its deadline slot).
+      std::vector<uint64_t*> end_gates;
+      for (size_t i = 1; i < ss.size(); ++i) end_gates.push_back(ctx.dev->alloc_gate());
+      ctx.compute->set_lane_join(*ss[0], end_gates, 1u, lane_done);
       lane_graphs = ctx.dev->capture_lanes(
           ss, [&] { strat->enqueue_iteration(); },
           [&](size_t i) {
-            ctx.compute->reset_slot(*ss[i]);
-            ctx.dev->lane_done(*ss[i], lane_done + i);
+            if (ctx.compute->program_joined(*ss[0])) {
+              if (i > 0) ctx.dev->signal_gate(*ss[i], end_gates[i - 1], 1u);
+            } else {
+              ctx.compute->reset_slot(*ss[i]);
+              ctx.dev->lane_done(*ss[i], lane_done + i);
+            }
           });
       ctx.compute->after_capture();  // the compute programs' task lists
+      joined = ctx.compute->program_joined(*ss[0]);
       // A lane whose graph is not a chain (a library adding its own stream
       // to the capture, e.g. a collective's side work joined back) would be
       // spread over executor streams that may share the compute lane's
@@ -654,6 +667,10 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
         ss[0]->synchronize();
       } else {
         lane_graphs.clear();
+        ctx.dev->free_stamps(lane_done, lane_done_n);  // the single graph signals after its launch
+        lane_done = nullptr;
+        lane_done_n = 0;
+        joined = false;
         ctx.dev->set_gate_events(false);
         lanes = false;
         why = "a lane graph is not linear";
@@ -672,6 +689,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     T.end_capture();
     if (TL) TL->end_capture();
     lane_info["enabled"] = lanes;
+    if (lanes) lane_info["program_join"] = joined;
     if (!lanes) lane_info["reason"] = why;
     Json per = Json::array();
     size_t total = 0;
@@ -726,7 +744,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   // the streams.
   auto wait_iteration = [&] {
     if (lane_done) {
-      CompletionFlag cf(lane_done, lane_done_n, dev_iter);
+      CompletionFlag cf(lane_done, joined ? 1 : lane_done_n, dev_iter);
       strat->synchronize();
     } else {
       strat->synchronize();
@@ -846,7 +864,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       __atomic_store_n(hs, static_cast<uint64_t>(r) + 1, __ATOMIC_RELEASE);  // go
       if (r + 1 < runs) arm(r + 1);
       if (lane_done) {
-        CompletionFlag cf(lane_done, lane_done_n, armed_iter.at(static_cast<size_t>(r)));
+        CompletionFlag cf(lane_done, joined ? 1 : lane_done_n, armed_iter.at(static_cast<size_t>(r)));
         strat->synchronize();
       } else {
         CompletionFlag cf(hs + 2, nlanes, static_cast<uint64_t>(r) + 1);

@@ -414,6 +414,10 @@ class TracingCompute : public ComputeEngine {
   bool begin_program(Stream& s) override { return in_->begin_program(s); }
   void end_program(Stream& s) override { in_->end_program(s); }
   void after_capture() override { in_->after_capture(); }
+  void set_lane_join(Stream& s, const std::vector<uint64_t*>& gates, uint32_t tag, uint64_t* host_done) override {
+    in_->set_lane_join(s, gates, tag, host_done);
+  }
+  bool program_joined(Stream& s) override { return in_->program_joined(s); }
   void reset_capped(Stream& s) override { in_->reset_capped(s); }
   bool chain_counters(ChainCounters& c) override { return in_->chain_counters(c); }
   void set_task_timers(TimerSet* t) override { in_->set_task_timers(t); }
