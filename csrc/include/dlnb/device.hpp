@@ -140,6 +140,8 @@ class Device {
   // next replay's waits. alloc_gate: a zeroed gate (freed with the device).
   virtual uint64_t* alloc_gate();
   virtual uint64_t* iter_word() { return nullptr; }
+  // A no-op kernel on s (GPU): a graph's trailing node.
+  virtual void pad(Stream& s) { (void)s; }
   // Raise a gate from alloc_gate with `tag` when s gets here (GPU).
   virtual void signal_gate(Stream& s, uint64_t* gate, uint32_t tag) {
     (void)s; (void)gate; (void)tag;

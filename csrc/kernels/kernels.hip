@@ -8,6 +8,7 @@
 #include <mutex>
 #include <cmath>
 #include <vector>
+#include <algorithm>
 #include <chrono>
 
 #include "deadline_sync.hpp"
@@ -633,11 +634,11 @@ namespace {
 // once per process and device from two readings >= DLNB_CLOCK_CAL_MS (500)
 // apart. A reading (read_clock) streams the device clock into host memory for
 // 10 ms (clock_stream_kernel) while the host samples it with its own clock
-// around every load - thousands of (host, device) pairs - and fits the device
-// clock to the host clock over them: the fit's value at the samples' mean
-// host time is the reading, its standard error (the pairs' scatter / sqrt n,
-// tens of ns) the reading's uncertainty. The latency from a device store to
-// the host seeing it is the same at both readings and drops out of the rate.
+// around every load - thousands of (host, device) pairs; the reading is the
+// clocks' offset at a low percentile of the pairs' host-minus-device times
+// (how late the host saw a value has a floor, the same at both readings, so
+// it drops out of the rate) and its uncertainty the spread of the
+// percentiles next to it.
 // Round 4 paired one stamp with the tightest of 16 launch + synchronize
 // brackets (~5.5 us half-width): up to +-20 ppm over 500 ms, the
 // size of the headline deltas; this is ~0.1 ppm (wallclock_uncertainty_ppm).
@@ -696,31 +697,23 @@ bool read_clock(int device, double* host_us, uint64_t* tick, double* err_us) {
   DLNB_HIP_CHECK(hipSetDevice(prev));
   DLNB_HIP_CHECK(le);
   DLNB_HIP_CHECK(se);
-  if (hs.size() < 16) return false;
-  // least squares tick = a + b (h - hm), in ticks relative to the first
+  if (hs.size() < 64) return false;
+  // Every pair's host time minus its device time (nominal rate: 10 ms x 10 ppm
+  // is 0.1 us) is the clocks' offset plus how late the host saw the value
+  // (>= a floor: the store's and the load's latency, the same at both
+  // readings). The offset is read at a low percentile of that distribution -
+  // robust to a preempted sample, unlike a least-squares fit - and its
+  // uncertainty is the spread of the percentiles just above it.
+  const double b = wallclock_hz_nominal(device) * 1e-6;  // ticks per us
   const size_t n = hs.size();
-  double hm = 0, tm = 0;
-  for (size_t i = 0; i < n; ++i) {
-    hm += hs[i];
-    tm += static_cast<double>(ts[i] - ts[0]);
-  }
-  hm /= n;
-  tm /= n;
-  double sxx = 0, sxy = 0;
-  for (size_t i = 0; i < n; ++i) {
-    const double x = hs[i] - hm, y = static_cast<double>(ts[i] - ts[0]) - tm;
-    sxx += x * x;
-    sxy += x * y;
-  }
-  const double b = sxy / sxx;  // ticks per us
-  double ss = 0;
-  for (size_t i = 0; i < n; ++i) {
-    const double r = static_cast<double>(ts[i] - ts[0]) - tm - b * (hs[i] - hm);
-    ss += r * r;
-  }
-  *host_us = hm;
-  *tick = ts[0] + static_cast<uint64_t>(std::llround(tm));
-  *err_us = std::sqrt(ss / static_cast<double>(n - 2)) / b / std::sqrt(static_cast<double>(n));
+  const uint64_t tref = ts[n / 2];
+  std::vector<double> off(n);
+  for (size_t i = 0; i < n; ++i) off[i] = hs[i] - static_cast<double>(static_cast<int64_t>(ts[i] - tref)) / b;
+  std::sort(off.begin(), off.end());
+  const double p2 = off[n / 50], p5 = off[n / 20], p10 = off[n / 10];
+  *host_us = p5;  // the host time of device tick tref
+  *tick = tref;
+  *err_us = std::max(0.5 * (p10 - p2), 0.005);
   return true;
 }
 void clock_cal_begin_locked(int device, ClockCal& c) {

@@ -201,6 +201,7 @@ class GpuDevice : public Device {
   }
   void set_iteration(Stream& s, uint64_t it) override { kernels::set_word(iter_word(), it, s.native()); }
   void lane_done(Stream& s, uint64_t* host_word) override { kernels::lane_done(host_word, iter_word(), s.native()); }
+  void pad(Stream& s) override { kernels::set_word(pool_ + 2, 0, s.native()); }  // pool word 2: scratch
   void signal_gate(Stream& s, uint64_t* gate, uint32_t tag) override {
     kernels::gate_signal(gate, iter_word(), tag, s.native());
   }

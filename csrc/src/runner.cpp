@@ -649,6 +649,10 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
               ctx.compute->reset_slot(*ss[i]);
               ctx.dev->lane_done(*ss[i], lane_done + i);
             }
+            // The graph's last kernel carries its system-scope release (an L2
+            // write-back: ~50 us after a collective's copy, round 5 traces):
+            // a trailing no-op takes it, after the lane's signal is out.
+            if (env_int("DLNB_LANE_TAIL_PAD", 1) != 0) ctx.dev->pad(*ss[i]);
           });
       ctx.compute->after_capture();  // the compute programs' task lists
       joined = ctx.compute->program_joined(*ss[0]);

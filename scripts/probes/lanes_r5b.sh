@@ -35,6 +35,15 @@ timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o c5
   > $O/trace.log 2>&1 || { echo "trace rc=$?" >> $O/steps.log; exit 1; }
 ok trace
 unset DLNB_NO_TORCH DLNB_GATE_TIMEOUT_S
+if [ "${BENCH:-0}" = 1 ]; then
+  for m in lanes single; do
+    step bench_$m
+    if [ $m = single ]; then e="DLNB_LANE_GRAPHS=0"; else e=""; fi
+    env $e timeout -k 10 300 python bench.py --steps 5 --warmup 2 --c5-model none --stretch-steps 0 \
+      > $O/bench_$m.json 2> $O/bench_$m.err || { echo "bench_$m rc=$?" >> $O/steps.log; exit 1; }
+    ok bench_$m
+  done
+fi
 step tests
 timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_kernels.py \
   tests/test_gpu_strategies.py -m gpu -k "deadline or graph_replay or exposed or prearm or comm_gates or chain" \
