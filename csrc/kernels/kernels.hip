@@ -682,11 +682,12 @@ bool read_clock(int device, double* host_us, uint64_t* tick, double* err_us) {
   const double start = steady_us();
   uint64_t last = 0;
   while (__atomic_load_n(slot + 1, __ATOMIC_ACQUIRE) == 0 && steady_us() - start < 2e6) {
-    const double h0 = steady_us();
+    // the value was stored before this load returned, so before h1: h1 is
+    // late by the store's lag (and by any preemption), never early
     const uint64_t v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
     const double h1 = steady_us();
     if (v != last && v != 0 && hs.size() < (1u << 16)) {
-      hs.push_back(0.5 * (h0 + h1));
+      hs.push_back(h1);
       ts.push_back(v);
       last = v;
     }
@@ -710,10 +711,12 @@ bool read_clock(int device, double* host_us, uint64_t* tick, double* err_us) {
   std::vector<double> off(n);
   for (size_t i = 0; i < n; ++i) off[i] = hs[i] - static_cast<double>(static_cast<int64_t>(ts[i] - tref)) / b;
   std::sort(off.begin(), off.end());
-  const double p2 = off[n / 50], p5 = off[n / 20], p10 = off[n / 10];
-  *host_us = p5;  // the host time of device tick tref
+  // offsets are the true one plus a lag >= its floor: the lowest percent are
+  // the freshest observations
+  const double p1 = off[n / 100], p5 = off[n / 20];
+  *host_us = p1;  // the host time of device tick tref (+ the lag floor)
   *tick = tref;
-  *err_us = std::max(0.5 * (p10 - p2), 0.005);
+  *err_us = std::max(p5 - p1, 0.005);
   return true;
 }
 void clock_cal_begin_locked(int device, ClockCal& c) {

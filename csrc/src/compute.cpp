@@ -303,6 +303,15 @@ class GpuCompute : public ComputeEngine {
     if (prog_next_ + n > kProgTasks) prog_next_ = 0;  // (a program runs before the ring comes round again)
     kernels::DlTask* dst = prog_dev_.as<kernels::DlTask>() + prog_next_;
     prog_next_ += n;
+    // A program whose first task waits for gates (FSDP: the iteration's first
+    // all-gather) is launched only once they are up, behind one-wave gate
+    // waits: resident and waiting, its grid would hold the CUs that
+    // collective needs (round 5: the headline's first all-gather ran on the 32
+    // free CUs, 0.74 instead of 0.19 ms). Its first block then finds them up.
+    for (int i = 0; i < 2; ++i)
+      if (ts[0].sync.gate[i])
+        kernels::gate_wait(ts[0].sync.gate[i], dev_.iter_word(), ts[0].sync.tag[i], gate_timeout_ticks_,
+                           counters_.as<uint64_t>() + kernels::kWaitTimeouts, s.native());
     if (dev_.capturing(s)) {
       uploads_.push_back(Upload{dst, ts});  // written by after_capture(), before the first replay
     } else {

@@ -24,6 +24,8 @@ run head_single DLNB_LANE_GRAPHS=0 timeout -k 10 150 $H --json $O/head_single.js
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 run trace timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o c5 -- \
   build/bin/dp vit_h_32_float8 8 . --backend rccl --compute gemm --graph -w 2 -r 4 --quiet --silent
+run trace_single DLNB_LANE_GRAPHS=0 timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $O/trace_single -o c5 -- \
+  build/bin/dp vit_h_32_float8 8 . --backend rccl --compute gemm --graph -w 2 -r 4 --quiet --silent
 unset DLNB_NO_TORCH DLNB_GATE_TIMEOUT_S
 if [ "${BENCH:-0}" = 1 ]; then
   step bench_lanes
