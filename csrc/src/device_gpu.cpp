@@ -123,7 +123,9 @@ class GpuDevice : public Device {
   std::string name() const override { return name_ + " (" + arch_ + ")"; }
   int index() const override { return idx_; }
   std::unique_ptr<Stream> create_stream(bool high_priority) override {
-    return std::unique_ptr<Stream>(new GpuStream(idx_, high_priority));
+    // DLNB_HIGH_PRIORITY_STREAMS=0: comm lanes on normal-priority queues (A/B)
+    static const bool high_ok = env_int("DLNB_HIGH_PRIORITY_STREAMS", 1) != 0;
+    return std::unique_ptr<Stream>(new GpuStream(idx_, high_priority && high_ok));
   }
   std::unique_ptr<Event> create_event(bool timing) override {
     return std::unique_ptr<Event>(new GpuEvent(timing, this));

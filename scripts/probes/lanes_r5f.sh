@@ -5,6 +5,7 @@ set -u
 O=${O:-gpurun_out/lanes_f}
 mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0 DLNB_NO_TORCH=1 DLNB_GATE_TIMEOUT_S=5
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 step() { echo "$1 start $(date +%s)" >> $O/steps.log; }
 ok() { echo "$1 ok" >> $O/steps.log; }
 run() {  # name env... -- command
@@ -17,11 +18,14 @@ C5="build/bin/dp vit_h_32_float8 8 . --backend rccl --compute gemm -w 5 -r 30 --
 H="build/bin/fsdp llama3_8b_16_bfloat16 32 1 . --backend rccl --compute gemm --graph -w 2 -r 10 --time-scale 0.05 --quiet --silent"
 run c5_pad timeout -k 10 120 $C5 --json $O/c5_pad.json
 run c5_nopad DLNB_LANE_TAIL_PAD=0 timeout -k 10 120 $C5 --json $O/c5_nopad.json
+run c5_normprio DLNB_HIGH_PRIORITY_STREAMS=0 timeout -k 10 120 $C5 --json $O/c5_normprio.json
+run head_normprio DLNB_HIGH_PRIORITY_STREAMS=0 timeout -k 10 150 $H --json $O/head_normprio.json
+run trace_normprio DLNB_HIGH_PRIORITY_STREAMS=0 timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $O/trace_normprio -o c5 -- \
+  build/bin/dp vit_h_32_float8 8 . --backend rccl --compute gemm --graph -w 2 -r 4 --quiet --silent
 run c5_nojoin DLNB_COMPUTE_PROGRAMS=0 timeout -k 10 120 $C5 --json $O/c5_nojoin.json
 run c5_single DLNB_LANE_GRAPHS=0 timeout -k 10 120 $C5 --json $O/c5_single.json
 run head_pad timeout -k 10 150 $H --json $O/head_pad.json
 run head_single DLNB_LANE_GRAPHS=0 timeout -k 10 150 $H --json $O/head_single.json
-cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 run trace timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o c5 -- \
   build/bin/dp vit_h_32_float8 8 . --backend rccl --compute gemm --graph -w 2 -r 4 --quiet --silent
 run trace_single DLNB_LANE_GRAPHS=0 timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $O/trace_single -o c5 -- \
