@@ -600,6 +600,8 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   } lane_done_guard{*ctx.dev, lane_done, lane_done_n};
   Json lane_info = Json::object();
   std::vector<Stream*> lanes_ss;  // streams the replay is launched on (lane graphs: each; else the compute stream)
+  std::vector<std::unique_ptr<Stream>> alt_owned;
+  std::vector<Stream*> alt_ss;    // lane graphs: the second set, odd replays
   if (opt.graph) {
     DLNB_REQUIRE(ctx.dev->kind() == DeviceKind::GPU, "--graph needs a GPU");
     // xgmi kernels take their epochs from device-side counters, so a replayed
@@ -669,6 +671,27 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
         // the first replay starts from cleared slots too
         ctx.compute->reset_clocks(*ss[0]);
         ss[0]->synchronize();
+        // Every other replay goes to a second set of streams (same
+        // priorities: the compute lane normal, the comm lanes high): a
+        // launched graph's completion holds its queue for ~70-100 us after
+        // its last node (round 5 traces), and the pre-armed next replay would
+        // wait behind it. A graph runs on any stream; its nodes do not depend
+        // on the one it was captured on.
+        bool alt = env_int("DLNB_LANE_ALTERNATE", 1) != 0;
+        if (alt) {
+          std::vector<Stream*> all = ss;
+          for (size_t i = 0; i < ss.size(); ++i) {
+            alt_owned.push_back(ctx.dev->create_stream(i > 0));
+            all.push_back(alt_owned.back().get());
+          }
+          std::string detail;
+          alt = ctx.dev->queues_independent(all, 0.05, &detail);
+        }
+        alt = ctx.hg().allreduce_max(alt ? 0.0 : 1.0) < 0.5;
+        if (alt)
+          for (auto& a : alt_owned) alt_ss.push_back(a.get());
+        else
+          alt_owned.clear();
       } else {
         lane_graphs.clear();
         ctx.dev->free_stamps(lane_done, lane_done_n);  // the single graph signals after its launch
@@ -693,7 +716,10 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     T.end_capture();
     if (TL) TL->end_capture();
     lane_info["enabled"] = lanes;
-    if (lanes) lane_info["program_join"] = joined;
+    if (lanes) {
+      lane_info["program_join"] = joined;
+      lane_info["alternating_streams"] = !alt_ss.empty();
+    }
     if (!lanes) lane_info["reason"] = why;
     Json per = Json::array();
     size_t total = 0;
@@ -727,18 +753,23 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   // Device iteration word (gates' sequence numbers): one value per replay,
   // stored at the head of every lane before its graph runs.
   uint64_t dev_iter = 0;
-  auto launch_graphs = [&] {
+  // the streams replay `it` runs on (lane graphs alternate between two sets)
+  auto lanes_for = [&](uint64_t it) -> const std::vector<Stream*>& {
+    return !alt_ss.empty() && (it & 1) ? alt_ss : lanes_ss;
+  };
+  auto launch_graphs = [&](uint64_t it) {
     if (lane_graphs.empty()) {
       graph->launch(*origin);
       return;
     }
-    for (size_t i = 0; i < lane_graphs.size(); ++i) lane_graphs[i]->launch(*lanes_ss[i]);
+    const auto& L = lanes_for(it);
+    for (size_t i = 0; i < lane_graphs.size(); ++i) lane_graphs[i]->launch(*L[i]);
   };
   auto enqueue = [&] {
     if (replay) {
       const uint64_t it = ++dev_iter;
-      for (Stream* l : lanes_ss) ctx.dev->set_iteration(*l, it);
-      launch_graphs();
+      for (Stream* l : lanes_for(it)) ctx.dev->set_iteration(*l, it);
+      launch_graphs(it);
     } else {
       strat->enqueue_iteration();
     }
@@ -791,7 +822,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       fault.at_iteration(iter_no++, inject_task);
       TraceRange tr("dlnb:loop_iteration");
       enqueue();
-      strat->synchronize();
+      wait_iteration();
       if (TL) TL->collect(-1);
     }
     ctx.hg().barrier();
@@ -841,8 +872,9 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   auto arm = [&](int r) {
     const uint64_t it = ++dev_iter;
     armed_iter.push_back(it);
+    const auto& L = lanes_for(it);
     for (size_t i = 0; i < nlanes; ++i) {
-      Stream& l = *lanes_ss[i];
+      Stream& l = *L[i];
       ctx.dev->host_wait(l, hs, static_cast<uint64_t>(r) + 1, go_timeout_s, hs + 1, it);
       if (TL && tl_edges && i == 0) TL->edge(l, 0);
       if (lane_graphs.empty())
