@@ -677,21 +677,34 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
         // its last node (round 5 traces), and the pre-armed next replay would
         // wait behind it. A graph runs on any stream; its nodes do not depend
         // on the one it was captured on.
+        // Both sets are streams made here, after setup: replays on the
+        // strategy's own streams (made before the communicators) ran their
+        // collectives slower - every other iteration 0.13 ms (C5) / 0.3 ms
+        // (headline) longer in round 5's A/B - so by default (DLNB_LANE_FRESH)
+        // neither set is the capture's.
         bool alt = env_int("DLNB_LANE_ALTERNATE", 1) != 0;
+        const bool fresh = env_int("DLNB_LANE_FRESH", 1) != 0;
         if (alt) {
-          std::vector<Stream*> all = ss;
-          for (size_t i = 0; i < ss.size(); ++i) {
-            alt_owned.push_back(ctx.dev->create_stream(i > 0));
-            all.push_back(alt_owned.back().get());
-          }
+          std::vector<Stream*> all = fresh ? std::vector<Stream*>() : ss;
+          for (size_t k = 0; k < (fresh ? 2u : 1u); ++k)
+            for (size_t i = 0; i < ss.size(); ++i) {
+              alt_owned.push_back(ctx.dev->create_stream(i > 0));
+              all.push_back(alt_owned.back().get());
+            }
           std::string detail;
           alt = ctx.dev->queues_independent(all, 0.05, &detail);
         }
         alt = ctx.hg().allreduce_max(alt ? 0.0 : 1.0) < 0.5;
-        if (alt)
-          for (auto& a : alt_owned) alt_ss.push_back(a.get());
-        else
+        if (alt) {
+          const size_t n = ss.size();
+          if (fresh) {
+            lanes_ss.clear();
+            for (size_t i = 0; i < n; ++i) lanes_ss.push_back(alt_owned[i].get());
+          }
+          for (size_t i = 0; i < n; ++i) alt_ss.push_back(alt_owned[(fresh ? n : 0) + i].get());
+        } else {
           alt_owned.clear();
+        }
       } else {
         lane_graphs.clear();
         ctx.dev->free_stamps(lane_done, lane_done_n);  // the single graph signals after its launch
