@@ -711,12 +711,12 @@ bool read_clock(int device, double* host_us, uint64_t* tick, double* err_us) {
   std::vector<double> off(n);
   for (size_t i = 0; i < n; ++i) off[i] = hs[i] - static_cast<double>(static_cast<int64_t>(ts[i] - tref)) / b;
   std::sort(off.begin(), off.end());
-  // offsets are the true one plus a lag >= its floor: the lowest percent are
-  // the freshest observations
-  const double p1 = off[n / 100], p5 = off[n / 20];
-  *host_us = p1;  // the host time of device tick tref (+ the lag floor)
+  // offsets are the true one plus a lag >= its floor: the lowest half percent
+  // are the freshest observations (a preempted host thread only adds lag)
+  const double lo = off[n / 200], hi = off[n / 50];
+  *host_us = lo;  // the host time of device tick tref (+ the lag floor)
   *tick = tref;
-  *err_us = std::max(p5 - p1, 0.005);
+  *err_us = std::max(hi - lo, 0.005);
   return true;
 }
 void clock_cal_begin_locked(int device, ClockCal& c) {

@@ -34,6 +34,9 @@ def kind(name: str) -> str:
 
 def queues(path: str) -> None:
     rows = _rows(path)
+    # the iterations only: from the first compute kernel on (setup's fills and copies run on other queues)
+    first = min((int(r["Start_Timestamp"]) for r in rows if kind(r.get("Kernel_Name", "")) == "compute"), default=0)
+    rows = [r for r in rows if int(r["Start_Timestamp"]) >= first]
     by = defaultdict(Counter)
     names = defaultdict(Counter)
     for r in rows:

@@ -95,7 +95,10 @@ def test_strategy_hip_graph_replay(strategy, model, params, data_dir):
     # hybrid_3d_moe) gets the single graph, with the reason reported
     lg = g["dlnb"]["lane_graphs"]
     if strategy in ("dp", "fsdp"):
-        assert lg["enabled"] and lg["linear"], lg
+        # the compute lane is one persistent program whose join signals the iteration; replays alternate
+        # between two stream sets (docs/ARCHITECTURE.md "Lane graphs")
+        assert lg["enabled"] and lg["linear"] and lg["program_join"] and lg["alternating_streams"], lg
+        assert g["dlnb"]["compute"]["programs"] >= 1, g["dlnb"]["compute"]
     if lg["enabled"]:
         assert lg["linear"] and len(lg["graphs"]) >= 2 and all(x["linear"] for x in lg["graphs"]), lg
     else:
