@@ -110,7 +110,8 @@ __device__ __forceinline__ uint64_t agree_t0(uint64_t* slot, uint32_t epoch, uin
     uint64_t t;
     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-      if (__hip_atomic_load(s.gate[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == want) {
+      if (__hip_atomic_load(s.gate[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == want) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // once, not per poll
         t = ld(s.gate[i] + 1) & kMask48;
         break;
       }
@@ -177,13 +178,14 @@ __device__ __forceinline__ void join(const DlSync& s) {
     if (!s.gate[i]) continue;
     const uint64_t want = gate_seq(s.iter, s.tag[i]);
     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(s.gate[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != want) {
+    while (__hip_atomic_load(s.gate[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
       __builtin_amdgcn_s_sleep(2);
       if (__builtin_amdgcn_s_memrealtime() - w0 > gate_timeout) {
         count(s.counters, kGateTimeouts, 1ull);
         break;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   if (s.tstart[0])
     __hip_atomic_store(s.tstart[0], s.iter ? ld(s.iter) : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

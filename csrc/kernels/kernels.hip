@@ -134,13 +134,16 @@ __global__ void gate_wait_kernel(const uint64_t* gate, const uint64_t* iter, uin
   if (threadIdx.x == 0) {
     const uint64_t want = dl::gate_seq(iter, tag);
     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != want) {
+    // relaxed polls, one acquire at the end: an acquire load invalidates the
+    // cache on every poll (buffer_inv), under the compute running beside it
+    while (__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
       __builtin_amdgcn_s_sleep(2);
       if (__builtin_amdgcn_s_memrealtime() - w0 > timeout_ticks) {
         __hip_atomic_fetch_add(timeouts, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
 }
 
@@ -152,13 +155,14 @@ __global__ void set_word_kernel(uint64_t* word, uint64_t value) {
 __global__ void probe_wait_kernel(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uint64_t* timed_out) {
   if (threadIdx.x == 0) {
     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != value) {
+    while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != value) {
       __builtin_amdgcn_s_sleep(2);
       if (__builtin_amdgcn_s_memrealtime() - w0 > timeout_ticks) {
         __hip_atomic_store(timed_out, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
 }
 
@@ -179,13 +183,16 @@ __global__ void host_wait_kernel(const uint64_t* word, uint64_t value, uint64_t 
                                  uint64_t* iter_out, uint64_t iter_value) {
   if (threadIdx.x == 0) {
     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < value) {
+    // relaxed polls (an acquire load would invalidate the L2's system-scope
+    // lines on every poll, for the whole iteration an armed replay waits)
+    while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < value) {
       __builtin_amdgcn_s_sleep(2);
       if (__builtin_amdgcn_s_memrealtime() - w0 > timeout_ticks) {
         __hip_atomic_fetch_add(timeouts, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     if (iter_out) __hip_atomic_store(iter_out, iter_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -614,31 +621,44 @@ double wallclock_hz_nominal(int device) {
   return static_cast<double>(khz) * 1e3;
 }
 
-// One wave streams the device clock into host-coherent memory: slot[0] =
-// s_memrealtime, rewritten every few hundred ns for `ticks`, then slot[1] = 1.
-__global__ void clock_stream_kernel(uint64_t* slot, uint64_t ticks) {
+// One wave answers the host's clock requests (read_clock): for k = 1..n it
+// waits for the host's request word (slot[0]) to reach k, reads
+// s_memrealtime, and replies with the tick (slot[1]) and then k (slot[2]).
+// One request in flight at a time: a wave that streamed its clock into host
+// memory as fast as it could (round 5's first version) queued its stores up
+// to ~540 us behind (profiles/clock_r5.md). Every wait is bounded (1 s
+// without a request ends the kernel), so the grid drains if the host stops.
+__global__ void clock_pingpong_kernel(uint64_t* slot, int n, uint64_t idle_ticks) {
   if (threadIdx.x == 0) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    uint64_t t = t0;
-    while (t - t0 < ticks) {
-      __hip_atomic_store(slot, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __builtin_amdgcn_s_sleep(4);
-      t = __builtin_amdgcn_s_memrealtime();
+    for (int k = 1; k <= n; ++k) {
+      const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+      bool live = true;
+      while (__hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < static_cast<uint64_t>(k)) {
+        if (__builtin_amdgcn_s_memrealtime() - w0 > idle_ticks) {
+          live = false;
+          break;
+        }
+      }
+      if (!live) break;
+      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      __hip_atomic_store(slot + 1, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(slot + 2, static_cast<uint64_t>(k), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    __hip_atomic_store(slot + 1, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
 namespace {
 // The s_memrealtime clock's rate against the host's steady clock, measured
 // once per process and device from two readings >= DLNB_CLOCK_CAL_MS (500)
-// apart. A reading (read_clock) streams the device clock into host memory for
-// 10 ms (clock_stream_kernel) while the host samples it with its own clock
-// around every load - thousands of (host, device) pairs; the reading is the
-// clocks' offset at a low percentile of the pairs' host-minus-device times
-// (how late the host saw a value has a floor, the same at both readings, so
-// it drops out of the rate) and its uncertainty the spread of the
-// percentiles next to it.
+// apart. A reading (read_clock) is 2048 request / reply round trips with a
+// one-wave kernel (clock_pingpong_kernel, ~6 ms): the device's tick lies
+// between the host's clock before the request and after the reply, and the
+// offset is read at the midpoints of the tightest round trips (what the
+// midpoint misses by - unequal request and reply latencies - is the same at
+// both readings and drops out of the rate); its uncertainty is the spread of
+// those midpoints. (Round 5's first version streamed the clock into host
+// memory instead: the stores queued up to ~540 us behind, and the rate's
+// uncertainty came out at ~140 ppm - profiles/clock_r5.md.)
 // Round 4 paired one stamp with the tightest of 16 launch + synchronize
 // brackets (~5.5 us half-width): up to +-20 ppm over 500 ms, the
 // size of the headline deltas; this is ~0.1 ppm (wallclock_uncertainty_ppm).
@@ -660,7 +680,7 @@ ClockCal& clock_cal(int device) {
 double steady_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-// Returns false when the stream never showed up (then nothing is read).
+// Returns false when too few requests were answered (then nothing is read).
 bool read_clock(int device, double* host_us, uint64_t* tick, double* err_us) {
   int prev = 0;
   DLNB_HIP_CHECK(hipGetDevice(&prev));
@@ -670,53 +690,76 @@ bool read_clock(int device, double* host_us, uint64_t* tick, double* err_us) {
   void* p = nullptr;
   DLNB_HIP_CHECK(hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent));
   uint64_t* slot = static_cast<uint64_t*>(p);
-  slot[0] = 0;
-  slot[1] = 0;
+  slot[0] = slot[1] = slot[2] = 0;
   const double nominal = wallclock_hz_nominal(device);
-  hipLaunchKernelGGL(clock_stream_kernel, 1, 64, 0, s, slot, static_cast<uint64_t>(0.010 * nominal));
+  const int n = 2048;
+  hipLaunchKernelGGL(clock_pingpong_kernel, 1, 64, 0, s, slot, n, static_cast<uint64_t>(1.0 * nominal));
   const hipError_t le = hipGetLastError();
-  std::vector<double> hs;
-  std::vector<uint64_t> ts;
-  hs.reserve(1 << 16);
-  ts.reserve(1 << 16);
+  // (h0, h1, tick): the host's clock before its request and after the reply
+  struct Rt {
+    double h0, h1;
+    uint64_t t;
+  };
+  std::vector<Rt> rs;
+  rs.reserve(n);
   const double start = steady_us();
-  uint64_t last = 0;
-  while (__atomic_load_n(slot + 1, __ATOMIC_ACQUIRE) == 0 && steady_us() - start < 2e6) {
-    // the value was stored before this load returned, so before h1: h1 is
-    // late by the store's lag (and by any preemption), never early
-    const uint64_t v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
-    const double h1 = steady_us();
-    if (v != last && v != 0 && hs.size() < (1u << 16)) {
-      hs.push_back(h1);
-      ts.push_back(v);
-      last = v;
+  for (int k = 1; k <= n; ++k) {
+    const double h0 = steady_us();
+    __atomic_store_n(slot, static_cast<uint64_t>(k), __ATOMIC_RELEASE);
+    bool got = true;
+    while (__atomic_load_n(slot + 2, __ATOMIC_ACQUIRE) < static_cast<uint64_t>(k)) {
+      if (steady_us() - start > 2e6) {
+        got = false;
+        break;
+      }
     }
+    if (!got) break;
+    const double h1 = steady_us();
+    rs.push_back({h0, h1, __atomic_load_n(slot + 1, __ATOMIC_ACQUIRE)});
   }
+  __atomic_store_n(slot, static_cast<uint64_t>(n), __ATOMIC_RELEASE);  // ends the kernel's loop either way
   const hipError_t se = hipStreamSynchronize(s);
   (void)hipHostFree(p);
   (void)hipStreamDestroy(s);
   DLNB_HIP_CHECK(hipSetDevice(prev));
   DLNB_HIP_CHECK(le);
   DLNB_HIP_CHECK(se);
-  if (hs.size() < 64) return false;
-  // Every pair's host time minus its device time (nominal rate: 10 ms x 10 ppm
-  // is 0.1 us) is the clocks' offset plus how late the host saw the value
-  // (>= a floor: the store's and the load's latency, the same at both
-  // readings). The offset is read at a low percentile of that distribution -
-  // robust to a preempted sample, unlike a least-squares fit - and its
-  // uncertainty is the spread of the percentiles just above it.
-  const double b = wallclock_hz_nominal(device) * 1e-6;  // ticks per us
-  const size_t n = hs.size();
-  const uint64_t tref = ts[n / 2];
-  std::vector<double> off(n);
-  for (size_t i = 0; i < n; ++i) off[i] = hs[i] - static_cast<double>(static_cast<int64_t>(ts[i] - tref)) / b;
+  if (rs.size() < 64) return false;
+  // The device read its clock between h0 and h1: the pair's midpoint is the
+  // host time of tick t to within half its round trip, and the offset
+  // (midpoint minus the device time at the nominal rate: 10 ms x 10 ppm is
+  // 0.1 us) is read from the tightest round trips (a preempted host only
+  // widens one); its uncertainty is the spread of those offsets. What the
+  // midpoint misses by (the request's and the reply's unequal latencies) is
+  // the same at both readings and drops out of the rate.
+  const double b = nominal * 1e-6;  // ticks per us
+  const uint64_t tref = rs[rs.size() / 2].t;
+  std::vector<size_t> idx(rs.size());
+  for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+  std::sort(idx.begin(), idx.end(), [&](size_t x, size_t y) { return rs[x].h1 - rs[x].h0 < rs[y].h1 - rs[y].h0; });
+  const size_t m = std::max<size_t>(16, rs.size() / 20);
+  std::vector<double> off(m);
+  for (size_t j = 0; j < m; ++j) {
+    const Rt& r = rs[idx[j]];
+    off[j] = 0.5 * (r.h0 + r.h1) - static_cast<double>(static_cast<int64_t>(r.t - tref)) / b;
+  }
   std::sort(off.begin(), off.end());
-  // offsets are the true one plus a lag >= its floor: the lowest half percent
-  // are the freshest observations (a preempted host thread only adds lag)
-  const double lo = off[n / 200], hi = off[n / 50];
-  *host_us = lo;  // the host time of device tick tref (+ the lag floor)
+  const double med = off[m / 2];
+  // the offsets' spread over the tightest 5 %, as a standard error of their median
+  const double iqr = off[3 * m / 4] - off[m / 4];
+  *host_us = med;
   *tick = tref;
-  *err_us = std::max(hi - lo, 0.005);
+  *err_us = std::max(iqr / std::sqrt(static_cast<double>(m)), 0.002);
+  if (env_int("DLNB_CLOCK_DEBUG", 0) != 0) {
+    std::vector<double> rtt(rs.size());
+    for (size_t i = 0; i < rs.size(); ++i) rtt[i] = rs[i].h1 - rs[i].h0;
+    std::sort(rtt.begin(), rtt.end());
+    std::fprintf(stderr,
+                 "[dlnb] clock reading: %zu round trips over %.1f us, rtt (us) min %.3f p5 %.3f p50 %.3f max %.3f; "
+                 "best %zu offsets (us from median) min %.3f p25 %.3f p75 %.3f max %.3f; err %.4f us\n",
+                 rs.size(), rs.back().h1 - rs.front().h0, rtt[0], rtt[rtt.size() / 20], rtt[rtt.size() / 2],
+                 rtt.back(), m, off[0] - med, off[m / 4] - med, off[3 * m / 4] - med, off[m - 1] - med, *err_us);
+  }
   return true;
 }
 void clock_cal_begin_locked(int device, ClockCal& c) {

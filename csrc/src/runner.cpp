@@ -663,9 +663,16 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       // spread over executor streams that may share the compute lane's
       // hardware queue - where a gate wait could hold the node that raises
       // its gate. Then the whole iteration is captured as one graph instead.
+      // Lanes pay only when the compute lane is one compute program: a lane
+      // of one launch per task puts every kernel boundary (28-60 us: drain,
+      // dispatch) on one queue, which the single graph spreads over four
+      // (C5 7.40-7.65 ms against 7.27, gemm-work C5 14.5 ms against 7.8:
+      // profiles/lanes_r5.md). DLNB_LANE_GRAPHS=2 keeps such lanes anyway.
       bool linear = true;
       for (const auto& g : lane_graphs) linear = linear && g->linear();
-      linear = ctx.hg().allreduce_max(linear ? 0.0 : 1.0) < 0.5;
+      const bool program_ok = joined || env_int("DLNB_LANE_GRAPHS", 1) >= 2;
+      const double verdict = ctx.hg().allreduce_max(!linear ? 2.0 : (!program_ok ? 1.0 : 0.0));
+      linear = verdict < 0.5;
       if (linear) {
         lanes_ss = ss;
         // the first replay starts from cleared slots too
@@ -713,7 +720,8 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
         joined = false;
         ctx.dev->set_gate_events(false);
         lanes = false;
-        why = "a lane graph is not linear";
+        why = verdict > 1.5 ? "a lane graph is not linear"
+                            : "the compute lane is not one compute program (a launch per task)";
         T.end_capture();
         if (TL) TL->end_capture();
         T.begin_capture();
