@@ -910,6 +910,9 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   ctx.hg().barrier();
   ctx.compute->reset_capped(*strat->streams()[0]);  // count the timed iterations only
   ctx.dev->synchronize();
+  // host time of each arm() (the launches of the next replay): a launch that
+  // blocks on the runtime shows up here (profiles/stall_r5.md)
+  std::vector<double> arm_s;
   if (hs && runs > 0) arm(0);  // submitted, held until the first go
   const double T0 = now_s();
   for (int r = 0; r < runs; ++r) {
@@ -919,7 +922,11 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     double t0 = now_s();
     if (hs) {
       __atomic_store_n(hs, static_cast<uint64_t>(r) + 1, __ATOMIC_RELEASE);  // go
-      if (r + 1 < runs) arm(r + 1);
+      if (r + 1 < runs) {
+        const double a0 = now_s();
+        arm(r + 1);
+        arm_s.push_back(now_s() - a0);
+      }
       if (lane_done) {
         CompletionFlag cf(lane_done, joined ? 1 : lane_done_n, armed_iter.at(static_cast<size_t>(r)));
         strat->synchronize();
@@ -947,7 +954,12 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
 
   // ---- report
   Json rank = strat->rank_json();
-  if (hs) rank["prearm_go_timeouts"] = static_cast<double>(__atomic_load_n(hs + 1, __ATOMIC_ACQUIRE));
+  if (hs) {
+    rank["prearm_go_timeouts"] = static_cast<double>(__atomic_load_n(hs + 1, __ATOMIC_ACQUIRE));
+    Json a = Json::array();
+    for (double x : arm_s) a.push_back(x * 1e3);
+    rank["prearm_launch_ms"] = a;
+  }
   rank["energy_consumed"] = T.values_json("energy_consumed");
   {
     // chained deadline tasks: lateness absorbed (<= the cap each) and beyond
