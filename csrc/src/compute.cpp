@@ -2,10 +2,12 @@
 
 #include <algorithm>
 #include <cmath>
+#include <exception>
 #include <map>
 #include <set>
 
 #include "dlnb/kernels.hpp"
+#include "dlnb/timers.hpp"
 
 namespace dlnb {
 
@@ -238,6 +240,8 @@ class GpuCompute : public ComputeEngine {
 
   void run_chained(Stream& s, double us, double flops, uint64_t* start, Event* done) override {
     if (mode_ == ComputeMode::Gemm && us * scale_ >= 20.0 && chain_live_[slot_for(s)]) {
+      if (stall_timers_ && !start) start = stall_timers_->task_slot(s);
+      StartNote note{stall_timers_, s, start, ticks(us * scale_)};
       kernels::DlSync sync;
       sync.tstart[0] = start;
       sync.tstart[1] = extra_start_;
@@ -282,6 +286,8 @@ class GpuCompute : public ComputeEngine {
       sync.tag[i] = gate_tag_.at(gates[i]);
       DLNB_REQUIRE(sync.tag[i] != 0, "run_gated: gate " << gates[i] << " was never signalled");
     }
+    if (stall_timers_ && !start) start = stall_timers_->task_slot(s);
+    StartNote note{stall_timers_, s, start, ticks(us * scale_)};
     sync.tstart[0] = start;
     sync.tstart[1] = extra_start_;
     extra_start_ = nullptr;
@@ -327,6 +333,8 @@ class GpuCompute : public ComputeEngine {
   }
 
   void run_stamped(Stream& s, double us, double flops, uint64_t* start) override {
+    if (stall_timers_ && !start) start = stall_timers_->task_slot(s);
+    StartNote note{stall_timers_, s, start, ticks(std::max(0.0, us * scale_))};
     double d = us * scale_;
     // a task that is not a deadline kernel cannot join the open program
     if (mode_ == ComputeMode::Gemm && d < 20.0) flush_program(s);
@@ -391,7 +399,13 @@ class GpuCompute : public ComputeEngine {
   }
 
   void set_task_timers(TimerSet* t) override {
-    if (mode_ == ComputeMode::GemmWork || mode_ == ComputeMode::Flops) task_timers_ = t;
+    if (mode_ == ComputeMode::GemmWork || mode_ == ComputeMode::Flops) {
+      task_timers_ = t;
+    } else if (t && stamps_task_start() && env_int("DLNB_TASK_STAMP_TIMERS", 1) != 0) {
+      // every task's own start stamp feeds the stall timers (TimerSet::stall_before_task)
+      stall_timers_ = t;
+      t->set_task_stamps(true);
+    }
   }
 
   Json describe() const override {
@@ -613,6 +627,17 @@ class GpuCompute : public ComputeEngine {
   std::map<uint64_t*, bool> chain_live_;  // the stream's last task was a deadline task a chained one may continue
   std::vector<uint32_t> gate_tag_;        // last tag signalled per gate (never 0 once signalled)
   uint64_t* extra_start_ = nullptr;       // set_next_start_slot
+  TimerSet* stall_timers_ = nullptr;      // set_task_timers: task starts for the stall timers
+  // Reports a task's start slot and duration to the stall timers once it is enqueued.
+  struct StartNote {
+    TimerSet* t;
+    Stream& s;
+    const uint64_t* start;
+    uint64_t ticks;
+    ~StartNote() {
+      if (t && std::uncaught_exceptions() == 0) t->task_started(s, start, ticks);
+    }
+  };
   // Lateness a chained task absorbs (deadline_sync.hpp): the replayed graph's
   // queue hop (8-11 us) + the previous grid's drain (~13 us) measured in
   // round 3; anything later is a wait and stays in the iteration time.

@@ -643,7 +643,10 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       for (size_t i = 1; i < ss.size(); ++i) end_gates.push_back(ctx.dev->alloc_gate());
       ctx.compute->set_lane_join(*ss[0], end_gates, 1u, lane_done);
       lane_graphs = ctx.dev->capture_lanes(
-          ss, [&] { strat->enqueue_iteration(); },
+          ss, [&] {
+            strat->enqueue_iteration();
+            T.finish_stalls();
+          },
           [&](size_t i) {
             if (ctx.compute->program_joined(*ss[0])) {
               if (i > 0) ctx.dev->signal_gate(*ss[i], end_gates[i - 1], 1u);
@@ -731,7 +734,10 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     if (!lanes) {
       // the engine's slot reset heads the graph, before every stream's first node
       graph = ctx.dev->capture(
-          *ss[0], others, [&] { strat->enqueue_iteration(); }, [&] { ctx.compute->reset_clocks(*ss[0]); });
+          *ss[0], others, [&] {
+            strat->enqueue_iteration();
+            T.finish_stalls();
+          }, [&] { ctx.compute->reset_clocks(*ss[0]); });
       lanes_ss = {ss[0]};
     }
     T.end_capture();
@@ -793,6 +799,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       launch_graphs(it);
     } else {
       strat->enqueue_iteration();
+      T.finish_stalls();
     }
   };
   // Host wait for the iteration just enqueued: lane graphs by their done words

@@ -181,9 +181,9 @@ class ContextParallel : public Strategy {
           cp_comm_->group_end();
           timers_->end(t, *cp_stream_, tk);
           cp_stream_->record(*recvd_[j + 1]);
-          if (reference_) timers_->stall(*compute_, *recvd_[j + 1], "cp_exposed_time");  // no overlap
+          if (reference_) timers_->stall_before_task(*compute_, *recvd_[j + 1], "cp_exposed_time");  // no overlap
         }
-        if (j > 0 && !reference_) timers_->stall(*compute_, *recvd_[j], "cp_exposed_time");
+        if (j > 0 && !reference_) timers_->stall_before_task(*compute_, *recvd_[j], "cp_exposed_time");
         ce.run(*compute_, core_us / C_, core_flops / C_);
         compute_->record(*attn_done_[j]);
       }
@@ -203,7 +203,7 @@ class ContextParallel : public Strategy {
     cp_comm_->all_to_all(a2a_send_.data(), a2a_recv_.data(), per_peer, ctx_->wire, *cp_stream_);
     timers_->end(t, *cp_stream_, tk);
     cp_stream_->record(*a2a_done_);
-    timers_->stall(*compute_, *a2a_done_, "cp_exposed_time");
+    timers_->stall_before_task(*compute_, *a2a_done_, "cp_exposed_time");
   }
 
   void enqueue_iteration() override {
@@ -230,7 +230,7 @@ class ContextParallel : public Strategy {
       }
     }
     dp_stream_->record(*dp_done_);
-    timers_->stall(*compute_, *dp_done_, "dp_exposed_time");
+    timers_->stall_after_task(*compute_, *dp_done_, "dp_exposed_time");
     if (ctx.opt.optimizer) {
       size_t off = 0;
       for (int k = 0; k < nbk_; ++k) {

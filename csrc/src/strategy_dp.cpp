@@ -199,7 +199,7 @@ class DataParallel : public Strategy {
       }
     }
     comm_stream_->record(*done_);
-    timers_->stall(*compute_, *done_, "barrier_time");  // exposed gradient communication (as dp)
+    timers_->stall_after_task(*compute_, *done_, "barrier_time");  // exposed gradient communication (as dp)
     // Optimizer step on this rank's slice of each bucket, then that bucket's
     // parameter all-gather, which overlaps the next bucket's update.
     for (int i = 0; i < nb_; ++i) {
@@ -270,7 +270,7 @@ class DataParallel : public Strategy {
       timers_->gap(fwd_start, 0, tail_end, "device_span_time");
     } else {
       comm_stream_->record(*done_);
-      timers_->stall(*compute_, *done_, "barrier_time");
+      timers_->stall_after_task(*compute_, *done_, "barrier_time");
     }
     if (ctx.opt.optimizer) {
       // Optimizer over the full (replicated) gradient, bucket by bucket.

@@ -172,7 +172,7 @@ class Fsdp : public Strategy {
     }
     if (dep) {
       if (timer)
-        timers_->stall(*compute_, *dep, timer);
+        timers_->stall_before_task(*compute_, *dep, timer);
       else
         compute_->wait(*dep);
     }
@@ -291,7 +291,7 @@ class Fsdp : public Strategy {
       // every stream has (graph join / synchronize)
       timers_->gap(prev_start_, prev_ticks_, tail_end_, "barrier");
     } else {
-      timers_->stall(*compute_, tail, "barrier");
+      timers_->stall_after_task(*compute_, tail, "barrier");
     }
     if (ctx.opt.optimizer) {
       if (R_ > 1)

@@ -483,7 +483,7 @@ class Pipeline : public Strategy {
         prev_->recv(act_in_[b].data(), pipe_, t, prev_peer_, *prev_stream_);
         timers_->end(tk, *prev_stream_, "pp_recv_time");
         prev_stream_->record(*recv_f_[i]);
-        timers_->stall(*compute_, *recv_f_[i], "pp_comm_time");
+        timers_->stall_before_task(*compute_, *recv_f_[i], "pp_comm_time");
       } else {
         timers_->add("pp_comm_time", 0.0);
       }
@@ -508,7 +508,7 @@ class Pipeline : public Strategy {
         next_->recv(grad_in_[b].data(), pipe_, t, next_peer_, *next_stream_);
         timers_->end(tk, *next_stream_, "pp_recv_time");
         next_stream_->record(*recv_b_[i]);
-        timers_->stall(*compute_, *recv_b_[i], "pp_comm_time");
+        timers_->stall_before_task(*compute_, *recv_b_[i], "pp_comm_time");
       } else {
         timers_->add("pp_comm_time", 0.0);
       }
@@ -574,7 +574,7 @@ class Pipeline : public Strategy {
       }
     }
     dp_stream_->record(*dp_done_);
-    timers_->stall(*compute_, *dp_done_, "dp_exposed_time");
+    timers_->stall_after_task(*compute_, *dp_done_, "dp_exposed_time");
     if (ctx.opt.optimizer) {
       void* g = ctx.opt.in_place ? grad_.data() : sum_grad_.data();
       optimizer_step(ctx, *compute_, params_.data(), mom_.data(), g, dp_ar_);
@@ -622,7 +622,7 @@ class Pipeline : public Strategy {
 
   void fwd_step(int i) {
     if (prev_)
-      timers_->stall(*compute_, *recv_f_[i], "pp_comm_time");
+      timers_->stall_before_task(*compute_, *recv_f_[i], "pp_comm_time");
     else
       timers_->add("pp_comm_time", 0.0);
     if (next_ && i >= 2) compute_->wait(*send_f_[i - 2]);  // act_out[i & 1] sent
@@ -633,7 +633,7 @@ class Pipeline : public Strategy {
   void bwd_step(int j) {
     const int nbk = ctx_->opt.dp_buckets;
     if (next_)
-      timers_->stall(*compute_, *recv_b_[j], "pp_comm_time");
+      timers_->stall_before_task(*compute_, *recv_b_[j], "pp_comm_time");
     else
       timers_->add("pp_comm_time", 0.0);
     if (prev_ && j >= 2) compute_->wait(*send_b_[j - 2]);  // grad_out[j & 1] sent
@@ -694,7 +694,7 @@ class Pipeline : public Strategy {
 
   void fwd_chunk(int k) {
     if (S_ > 1 && in_f(k))
-      timers_->stall(*compute_, *recv_f_[k], "pp_comm_time");
+      timers_->stall_before_task(*compute_, *recv_f_[k], "pp_comm_time");
     else
       timers_->add("pp_comm_time", 0.0);
     if (S_ > 1 && k >= 2) compute_->wait(*send_f_[k - 2]);  // act_out[k & 1] sent (no-op if never recorded)
@@ -706,7 +706,7 @@ class Pipeline : public Strategy {
     const int nbk = ctx_->opt.dp_buckets;
     const int total = mb_ * V_;
     if (S_ > 1 && in_b(j))
-      timers_->stall(*compute_, *recv_b_[j], "pp_comm_time");
+      timers_->stall_before_task(*compute_, *recv_b_[j], "pp_comm_time");
     else
       timers_->add("pp_comm_time", 0.0);
     if (S_ > 1 && j >= 2) compute_->wait(*send_b_[j - 2]);  // grad_out[j & 1] sent
@@ -930,14 +930,14 @@ class Pipeline : public Strategy {
         const int slot = dp_slot(op.dir, op.mb);
         if (!op.bwd) {
           if (dp_pos(stage_, op.dir) > 0)
-            timers_->stall(*compute_, *recv_f_[slot], "pp_comm_time");
+            timers_->stall_before_task(*compute_, *recv_f_[slot], "pp_comm_time");
           else
             timers_->add("pp_comm_time", 0.0);
           micro_compute(fwd_mb_us_, fwd_mb_flops_);
           compute_->record(*fwd_done_[slot]);
         } else {
           if (dp_pos(stage_, op.dir) < S_ - 1)
-            timers_->stall(*compute_, *recv_b_[slot], "pp_comm_time");
+            timers_->stall_before_task(*compute_, *recv_b_[slot], "pp_comm_time");
           else
             timers_->add("pp_comm_time", 0.0);
           micro_compute(bwd_mb_us_, bwd_mb_flops_);

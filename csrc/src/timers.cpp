@@ -17,6 +17,10 @@ int TimerSet::begin(Stream& s) {
   DLNB_REQUIRE(next_ < cap_, "too many timer stamps in one iteration");
   int idx = static_cast<int>(next_++);
   dev_.stamp(s, stamps_ + idx);
+  if (task_stamps()) {
+    auto it = clocks_.find(&s);
+    if (it != clocks_.end() && !it->second.pending.empty()) close_pending(it->second, stamps_ + idx);
+  }
   return idx;
 }
 
@@ -26,6 +30,13 @@ const uint64_t* TimerSet::end(int token, Stream& s, const std::string& name) {
   int idx = static_cast<int>(next_++);
   dev_.stamp(s, stamps_ + idx);
   pending_.push_back(Pending{token, idx, name});
+  if (task_stamps()) {
+    auto it = clocks_.find(&s);
+    if (it != clocks_.end()) {  // the stream's next wait is timed from here
+      it->second.start = stamps_ + idx;
+      it->second.ticks = 0;
+    }
+  }
   return stamps_ + idx;
 }
 
@@ -38,6 +49,68 @@ void TimerSet::stall(Stream& s, Event& e, const std::string& name) {
   int t = begin(s);
   s.wait(e);
   end(t, s, name);
+}
+
+uint64_t* TimerSet::task_slot(Stream& s) {
+  (void)s;
+  if (!task_stamps()) return nullptr;
+  return slot();
+}
+
+void TimerSet::task_started(Stream& s, const uint64_t* start, uint64_t ticks) {
+  if (!task_stamps() || !owns(start)) return;
+  TaskClock& c = clocks_[&s];
+  close_pending(c, start);
+  c.start = start;
+  c.ticks = ticks;
+}
+
+void TimerSet::stall_before_task(Stream& s, Event& e, const std::string& name) {
+  auto it = clocks_.find(&s);
+  if (!task_stamps() || it == clocks_.end() || !it->second.start) {
+    stall(s, e, name);
+    return;
+  }
+  s.wait(e);
+  it->second.pending.push_back(name);
+}
+
+void TimerSet::stall_after_task(Stream& s, Event& e, const std::string& name) {
+  auto it = clocks_.find(&s);
+  if (!task_stamps() || it == clocks_.end() || !it->second.start || !it->second.pending.empty()) {
+    stall(s, e, name);
+    return;
+  }
+  s.wait(e);
+  DLNB_REQUIRE(next_ < cap_, "too many timer stamps in one iteration");
+  uint64_t* st = stamps_ + next_++;
+  dev_.stamp(s, st);
+  gap(it->second.start, it->second.ticks, st, name);
+  it->second.start = st;
+  it->second.ticks = 0;
+}
+
+// A stream's pending stall_before_task waits end where the stream reaches
+// `at` (a task's start or a timed operation's begin stamp).
+void TimerSet::close_pending(TaskClock& c, const uint64_t* at) {
+  for (size_t i = 0; i < c.pending.size(); ++i) {
+    if (i == 0)
+      gap(c.start, c.ticks, at, c.pending[i]);
+    else
+      gap(at, 0, at, c.pending[i]);  // one stream cannot tell consecutive waits apart: the first takes the gap
+  }
+  c.pending.clear();
+}
+
+void TimerSet::finish_stalls() {
+  for (auto& kv : clocks_) {
+    TaskClock& c = kv.second;
+    if (c.pending.empty() || !enabled_) continue;
+    uint64_t* st = slot();
+    dev_.stamp(*kv.first, st);
+    close_pending(c, st);
+  }
+  clocks_.clear();  // the next iteration's first wait has no task before it
 }
 
 uint64_t* TimerSet::slot() {
@@ -60,6 +133,7 @@ void TimerSet::add(const std::string& name, double seconds) {
 }
 
 void TimerSet::begin_capture() {
+  clocks_.clear();
   pending_.clear();
   gaps_.clear();
   next_ = 0;

@@ -317,6 +317,28 @@ def test_dp_exposed_comm_matches_the_step(mode, root):
     assert d["chain_capped"]["gate_wait_timeouts_max"] == 0
 
 
+def test_pipeline_stall_timers_from_task_stamps(data_dir):
+    """VERDICT r4 #1 for the pipeline: pp_comm_time / dp_exposed_time are timed from the compute tasks' own
+    start stamps (TimerSet::stall_before_task / stall_after_task: previous task's deadline to the next task's
+    start), not a stamp-wait-stamp pair a graph executor can reorder. Same entry counts as the stamp pairs
+    (DLNB_TASK_STAMP_TIMERS=0), no double counting (the waits on the compute stream add up to at most the
+    iteration over its floor), and the iteration is shorter without the two stamp kernels per wait."""
+    docs = {}
+    for stamps in ("1", "0"):
+        docs[stamps] = engine.run_native("hybrid_3d", "tiny_dense_8_bfloat16", 2, 8, 1, base_path=data_dir, warmup=2,
+                                         runs=5, compute="sleep", backend="loopback", ranks=2, quiet=True,
+                                         env={"DLNB_TASK_STAMP_TIMERS": stamps})
+    for stamps, doc in docs.items():
+        it = doc["global"]["dlnb"]["iteration"]
+        over = it["median_ms"] - it["compute_floor_ms"]
+        for r in doc["ranks"]:
+            assert len(r["pp_comm_time"]) == len(docs["0"]["ranks"][0]["pp_comm_time"]), r.keys()
+            assert all(v >= 0 for v in r["pp_comm_time"])
+            waits = sum(sum(r[k]) for k in ("pp_comm_time", "tp_comm_time", "dp_exposed_time")) / 5 * 1e3
+            assert waits <= over + 0.5, (stamps, waits, over)
+    assert docs["1"]["global"]["dlnb"]["iteration"]["median_ms"] < docs["0"]["global"]["dlnb"]["iteration"]["median_ms"]
+
+
 @pytest.mark.parametrize("graph", [True, False])
 def test_dp_comm_gates_exact_and_bounded(graph, data_dir):
     """DP with comm gates (each bucket's all-reduce waits on the device for its backward's gate), graph-replayed
