@@ -616,9 +616,11 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       why = "DLNB_LANE_GRAPHS=0";
     } else if (ss.size() < 2) {
       why = "one stream";
-    } else if (ctx.ranks_on_device > 1) {
+    } else if (ctx.ranks_on_device > 1 && env_int("DLNB_LANE_SHARED", 0) == 0) {
       // a task spinning on its gate holds its CUs, which another rank's
       // compute on the same device - the one the collective waits for - needs
+      // (DLNB_LANE_SHARED=1, with grids that fit side by side - --comm-cus -
+      // and no slicing: the multi-rank lane path rehearsed on one GPU)
       why = "ranks share the device";
     } else {
       std::string detail;
@@ -692,7 +694,10 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
         // collectives slower - every other iteration 0.13 ms (C5) / 0.3 ms
         // (headline) longer in round 5's A/B - so by default (DLNB_LANE_FRESH)
         // neither set is the capture's.
-        bool alt = env_int("DLNB_LANE_ALTERNATE", 1) != 0;
+        // (not with ranks sharing the device, DLNB_LANE_SHARED: two processes'
+        // extra stream sets oversubscribe the hardware queues - 2 ranks on one
+        // GPU ran 143.4 ms without and 149.5-164.7 with, profiles/lanes_n2_r5.md)
+        bool alt = env_int("DLNB_LANE_ALTERNATE", ctx.ranks_on_device > 1 ? 0 : 1) != 0;
         const bool fresh = env_int("DLNB_LANE_FRESH", 1) != 0;
         if (alt) {
           std::vector<Stream*> all = fresh ? std::vector<Stream*>() : ss;
