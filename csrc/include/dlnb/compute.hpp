@@ -146,6 +146,12 @@ class ComputeEngine {
     (void)s; (void)gates; (void)tag; (void)host_done;
   }
   virtual bool program_joined(Stream& s) { (void)s; return false; }
+  // Mean duration (us) of the compute tasks enqueued on s since set_lane_join
+  // (a lane capture), each one kernel (deadline / idle / spin); < 0 when any
+  // task took several launches (gemm-work, flops) or none ran. A lane of long
+  // single-kernel tasks pays its kernel boundaries on one queue at little
+  // cost (the runner keeps such lanes without a compute program).
+  virtual double lane_task_us(Stream& s) { (void)s; return -1.0; }
   // Counters of the chained / gated deadline tasks (kernels::DlCounter):
   //   capped: tasks whose first block came later than the absorb cap after
   //     their chained start (a wait, not a launch hop: e.g. a replayed graph

@@ -180,13 +180,18 @@ __global__ void host_signal_kernel(uint64_t* word, uint64_t value) {
 }
 
 __global__ void host_wait_kernel(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uint64_t* timeouts,
-                                 uint64_t* iter_out, uint64_t iter_value) {
+                                 uint64_t* iter_out, uint64_t iter_value, uint64_t tight_ticks) {
   if (threadIdx.x == 0) {
     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
     // relaxed polls (an acquire load would invalidate the L2's system-scope
-    // lines on every poll, for the whole iteration an armed replay waits)
+    // lines on every poll, for the whole iteration an armed replay waits);
+    // after tight_ticks (0: never) one poll every ~4 us
     while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < value) {
-      __builtin_amdgcn_s_sleep(2);
+      const uint64_t el = __builtin_amdgcn_s_memrealtime() - w0;
+      if (tight_ticks != 0 && el > tight_ticks)
+        __builtin_amdgcn_s_sleep(127);
+      else
+        __builtin_amdgcn_s_sleep(2);
       if (__builtin_amdgcn_s_memrealtime() - w0 > timeout_ticks) {
         __hip_atomic_fetch_add(timeouts, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
@@ -601,7 +606,15 @@ void host_signal(uint64_t* word, uint64_t value, void* stream) {
 void host_wait(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uint64_t* timeouts, void* stream,
                uint64_t* iter_out, uint64_t iter_value) {
   DLNB_REQUIRE(word != nullptr && timeouts != nullptr, "host_wait: null word");
-  hipLaunchKernelGGL(host_wait_kernel, 1, 64, 0, S(stream), word, value, timeout_ticks, timeouts, iter_out, iter_value);
+  // Tight polling for DLNB_HOST_WAIT_TIGHT_US (50), then one poll every ~4 us:
+  // an armed replay waits a whole iteration, and its wave's back-to-back
+  // host-memory reads slowed the iteration's HBM-bound copies (one-rank
+  // hybrid_3d: the 7-ms DP all-reduce copy 7.15-7.30 -> 6.89-6.93 ms, step
+  // -0.5 ms; headline 0.05x -0.025 ms; profiles/hostwait_r5.md). 0: tight.
+  static const long tight_us = env_int("DLNB_HOST_WAIT_TIGHT_US", 50);
+  const uint64_t tight = tight_us > 0 ? static_cast<uint64_t>(tight_us) * 100ull : 0ull;  // 100 MHz ticks
+  hipLaunchKernelGGL(host_wait_kernel, 1, 64, 0, S(stream), word, value, timeout_ticks, timeouts, iter_out, iter_value,
+                     tight);
   DLNB_HIP_CHECK(hipGetLastError());
 }
 

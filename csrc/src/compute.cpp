@@ -205,8 +205,14 @@ class GpuCompute : public ComputeEngine {
     if (mode_ != ComputeMode::Gemm) return;
     joins_[&s] = Join{gates, tag, host_done};
     joined_.erase(&s);
+    lane_stats_.clear();
   }
   bool program_joined(Stream& s) override { return joined_.count(&s) != 0; }
+  double lane_task_us(Stream& s) override {
+    auto it = lane_stats_.find(&s);
+    if (it == lane_stats_.end() || it->second.n == 0 || !it->second.single) return -1.0;
+    return it->second.us / static_cast<double>(it->second.n);
+  }
   void after_capture() override {
     joins_.clear();  // a join no program took does not carry over
     if (uploads_.empty()) return;
@@ -240,6 +246,7 @@ class GpuCompute : public ComputeEngine {
 
   void run_chained(Stream& s, double us, double flops, uint64_t* start, Event* done) override {
     if (mode_ == ComputeMode::Gemm && us * scale_ >= 20.0 && chain_live_[slot_for(s)]) {
+      note_task(s, us * scale_);
       if (stall_timers_ && !start) start = stall_timers_->task_slot(s);
       StartNote note{stall_timers_, s, start, ticks(us * scale_)};
       kernels::DlSync sync;
@@ -286,6 +293,7 @@ class GpuCompute : public ComputeEngine {
       sync.tag[i] = gate_tag_.at(gates[i]);
       DLNB_REQUIRE(sync.tag[i] != 0, "run_gated: gate " << gates[i] << " was never signalled");
     }
+    note_task(s, us * scale_);
     if (stall_timers_ && !start) start = stall_timers_->task_slot(s);
     StartNote note{stall_timers_, s, start, ticks(us * scale_)};
     sync.tstart[0] = start;
@@ -333,6 +341,7 @@ class GpuCompute : public ComputeEngine {
   }
 
   void run_stamped(Stream& s, double us, double flops, uint64_t* start) override {
+    note_task(s, us * scale_);
     if (stall_timers_ && !start) start = stall_timers_->task_slot(s);
     StartNote note{stall_timers_, s, start, ticks(std::max(0.0, us * scale_))};
     double d = us * scale_;
@@ -628,6 +637,19 @@ class GpuCompute : public ComputeEngine {
   std::vector<uint32_t> gate_tag_;        // last tag signalled per gate (never 0 once signalled)
   uint64_t* extra_start_ = nullptr;       // set_next_start_slot
   TimerSet* stall_timers_ = nullptr;      // set_task_timers: task starts for the stall timers
+  // lane_task_us: the tasks enqueued per stream since the last set_lane_join
+  struct LaneStats {
+    long n = 0;
+    double us = 0.0;
+    bool single = true;  // every task one kernel
+  };
+  std::map<Stream*, LaneStats> lane_stats_;
+  void note_task(Stream& s, double d) {
+    LaneStats& st = lane_stats_[&s];
+    ++st.n;
+    st.us += std::max(0.0, d);
+    if (mode_ == ComputeMode::GemmWork || mode_ == ComputeMode::Flops) st.single = false;
+  }
   // Reports a task's start slot and duration to the stall timers once it is enqueued.
   struct StartNote {
     TimerSet* t;
