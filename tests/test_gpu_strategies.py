@@ -319,13 +319,9 @@ def test_dp_exposed_comm_matches_the_step(mode, root):
     assert d["chain_capped"]["gate_wait_timeouts_max"] == 0
 
 
-def test_fsdp_lanes_two_ranks_one_gpu(root, tmp_path):
-    """The multi-rank lane-graph path on one GPU (profiles/lanes_n2_r5.md): 2 processes of the headline FSDP step
-    (U = 32, F = 2, 0.05x time) over the xgmi kernels, each rank's deadline grid on 96 CUs and the collectives
-    capped at 8 CTAs per lane so both ranks' grids and collectives fit side by side; lane graphs forced despite
-    the shared device (DLNB_LANE_SHARED=1). Both ranks replay linear lane graphs joined by the compute program,
-    every gate wait is satisfied, no task is late beyond the absorb cap, and the step is within 5 % of the
-    floor."""
+def _two_ranks_one_gpu(root, tmp_path, binary_name, params, extra_env=None, iters=8):
+    """Run one 2-rank job of a native binary with both ranks on GPU 0 (xgmi), every device wait bounded; returns
+    rank 0's report."""
     import json
     import os
     import socket
@@ -333,17 +329,18 @@ def test_fsdp_lanes_two_ranks_one_gpu(root, tmp_path):
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
-    binary = os.path.join(root, "build", "bin", "fsdp")
+    binary = os.path.join(root, "build", "bin", binary_name)
     procs = []
     for r in range(2):
         env = dict(os.environ, DLNB_NO_TORCH="1", DLNB_LANE_SHARED="1", DLNB_GEMM_SLICE_US="0", DLNB_GATE_TIMEOUT_S="5",
                    DLNB_XGMI_TIMEOUT_S="20", RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), LOCAL_WORLD_SIZE="2",
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **(extra_env or {}))
         out = str(tmp_path / f"r{r}.json")
         procs.append(subprocess.Popen(
-            [binary, "llama3_8b_16_bfloat16", "32", "2", root, "--backend", "xgmi", "--devices", "0,0", "--comm-cus",
-             "160", "--rccl-max-ctas", "8", "--compute", "gemm", "--graph", "-w", "3", "-r", "8", "--time-scale", "0.05",
-             "--quiet", "--silent", "--json", out], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+            [binary, "llama3_8b_16_bfloat16", *params, root, "--backend", "xgmi", "--devices", "0,0", "--comm-cus",
+             "160", "--rccl-max-ctas", "8", "--compute", "gemm", "--graph", "-w", "3", "-r", str(iters),
+             "--time-scale", "0.05", "--quiet", "--silent", "--json", out], env=env, stdout=subprocess.PIPE,
+            stderr=subprocess.PIPE, text=True))
     errs = []
     for p in procs:
         try:
@@ -353,7 +350,33 @@ def test_fsdp_lanes_two_ranks_one_gpu(root, tmp_path):
             _, err = p.communicate()
         errs.append((p.returncode, err[-1500:]))
     assert all(rc == 0 for rc, _ in errs), errs
-    doc = json.load(open(tmp_path / "r0.json"))
+    return json.load(open(tmp_path / "r0.json"))
+
+
+def test_pipeline_lanes_two_ranks_one_gpu(root, tmp_path):
+    """The pipeline hybrids keep lane graphs without a compute program (one long task per micro-batch,
+    DLNB_LANE_MIN_TASK_US): hybrid_3d S = 2, mb = 4 on 2 ranks sharing GPU 0 over xgmi - linear lane graphs on
+    both ranks, no gate timeout, and faster than the single graph (profiles/hostwait_r5.md: 100.3 vs 104.8 ms)."""
+    lanes = _two_ranks_one_gpu(root, tmp_path, "hybrid_3d", ["2", "4", "1"])
+    d = lanes["global"]["dlnb"]
+    lg = d["lane_graphs"]
+    assert lg["enabled"] and lg["linear"] and not lg["program_join"] and lg["compute_task_us"] >= 1000, lg
+    cc = d["chain_capped"]
+    assert cc["gate_wait_timeouts_max"] == 0 and cc["compute_gate_timeouts_max"] == 0, cc
+    single = _two_ranks_one_gpu(root, tmp_path, "hybrid_3d", ["2", "4", "1"], {"DLNB_LANE_GRAPHS": "0"})
+    assert not single["global"]["dlnb"]["lane_graphs"]["enabled"]
+    assert d["iteration"]["median_ms"] < single["global"]["dlnb"]["iteration"]["median_ms"], (d["iteration"],
+                                                                                              single["global"]["dlnb"]["iteration"])
+
+
+def test_fsdp_lanes_two_ranks_one_gpu(root, tmp_path):
+    """The multi-rank lane-graph path on one GPU (profiles/lanes_n2_r5.md): 2 processes of the headline FSDP step
+    (U = 32, F = 2, 0.05x time) over the xgmi kernels, each rank's deadline grid on 96 CUs and the collectives
+    capped at 8 CTAs per lane so both ranks' grids and collectives fit side by side; lane graphs forced despite
+    the shared device (DLNB_LANE_SHARED=1). Both ranks replay linear lane graphs joined by the compute program,
+    every gate wait is satisfied, no task is late beyond the absorb cap, and the step is within 5 % of the
+    floor."""
+    doc = _two_ranks_one_gpu(root, tmp_path, "fsdp", ["32", "2"])
     d = doc["global"]["dlnb"]
     lg = d["lane_graphs"]
     assert lg["enabled"] and lg["linear"] and lg["program_join"], lg
