@@ -319,7 +319,8 @@ def test_dp_exposed_comm_matches_the_step(mode, root):
     assert d["chain_capped"]["gate_wait_timeouts_max"] == 0
 
 
-def _two_ranks_one_gpu(root, tmp_path, binary_name, params, extra_env=None, iters=8):
+def _two_ranks_one_gpu(root, tmp_path, binary_name, params, extra_env=None, iters=8, model="llama3_8b_16_bfloat16",
+                       time_scale="0.05"):
     """Run one 2-rank job of a native binary with both ranks on GPU 0 (xgmi), every device wait bounded; returns
     rank 0's report."""
     import json
@@ -337,9 +338,9 @@ def _two_ranks_one_gpu(root, tmp_path, binary_name, params, extra_env=None, iter
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **(extra_env or {}))
         out = str(tmp_path / f"r{r}.json")
         procs.append(subprocess.Popen(
-            [binary, "llama3_8b_16_bfloat16", *params, root, "--backend", "xgmi", "--devices", "0,0", "--comm-cus",
+            [binary, model, *params, root, "--backend", "xgmi", "--devices", "0,0", "--comm-cus",
              "160", "--rccl-max-ctas", "8", "--compute", "gemm", "--graph", "-w", "3", "-r", str(iters),
-             "--time-scale", "0.05", "--quiet", "--silent", "--json", out], env=env, stdout=subprocess.PIPE,
+             "--time-scale", time_scale, "--quiet", "--silent", "--json", out], env=env, stdout=subprocess.PIPE,
             stderr=subprocess.PIPE, text=True))
     errs = []
     for p in procs:
@@ -367,6 +368,22 @@ def test_pipeline_lanes_two_ranks_one_gpu(root, tmp_path):
     assert not single["global"]["dlnb"]["lane_graphs"]["enabled"]
     assert d["iteration"]["median_ms"] < single["global"]["dlnb"]["iteration"]["median_ms"], (d["iteration"],
                                                                                               single["global"]["dlnb"]["iteration"])
+
+
+def test_dp_lanes_two_ranks_one_gpu(root, tmp_path):
+    """DP's compute program and all-reduce lane with two ranks on one GPU (the C5 ViT-H fp8 step, 8 buckets, over
+    xgmi, grids side by side): linear lane graphs joined by the program, no gate timeout, and the exposed
+    all-reduce timer (barrier_time, from the tasks' own stamps) inside the step's excess over its floor."""
+    doc = _two_ranks_one_gpu(root, tmp_path, "dp", ["8"], model="vit_h_32_float8", time_scale="1", iters=20)
+    d = doc["global"]["dlnb"]
+    lg = d["lane_graphs"]
+    assert lg["enabled"] and lg["linear"] and lg["program_join"], lg
+    cc = d["chain_capped"]
+    assert cc["gate_wait_timeouts_max"] == 0 and cc["compute_gate_timeouts_max"] == 0, cc
+    it = d["iteration"]
+    r = doc["ranks"][0]
+    barrier = sum(r["barrier_time"]) / len(r["barrier_time"]) * 1e3
+    assert 0 < barrier <= it["median_ms"] - it["compute_floor_ms"] + 0.05, (barrier, it)
 
 
 def test_fsdp_lanes_two_ranks_one_gpu(root, tmp_path):
