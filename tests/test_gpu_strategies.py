@@ -370,6 +370,21 @@ def test_pipeline_lanes_two_ranks_one_gpu(root, tmp_path):
                                                                                               single["global"]["dlnb"]["iteration"])
 
 
+def test_cp_stall_timers_two_ranks_one_gpu(root, tmp_path):
+    """Context parallelism's exposed-communication timers on a real 2-rank ring (two processes on GPU 0, xgmi, lane
+    graphs: 15-ms tasks at full time scale): cp_exposed_time / dp_exposed_time come from the tasks' own start
+    stamps (TimerSet::stall_before_task / stall_after_task), so per iteration they add up to at most the step's
+    excess over its compute floor."""
+    doc = _two_ranks_one_gpu(root, tmp_path, "hybrid_cp", ["2"], time_scale="0.2", iters=4)
+    d = doc["global"]["dlnb"]
+    it = d["iteration"]
+    for r in doc["ranks"]:
+        runs = len(r["runtimes"]) if "runtimes" in r else len(r["runtime"])
+        cp = sum(r["cp_exposed_time"]) / runs * 1e3
+        dp = sum(r.get("dp_exposed_time", [0.0])) / runs * 1e3
+        assert min(r["cp_exposed_time"]) >= 0 and cp + dp <= it["median_ms"] - it["compute_floor_ms"] + 0.5, (cp, dp, it)
+
+
 def test_dp_lanes_two_ranks_one_gpu(root, tmp_path):
     """DP's compute program and all-reduce lane with two ranks on one GPU (the C5 ViT-H fp8 step, 8 buckets, over
     xgmi, grids side by side): linear lane graphs joined by the program, no gate timeout, and the exposed
