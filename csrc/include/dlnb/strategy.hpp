@@ -83,6 +83,12 @@ class Strategy {
   // False when enqueue_iteration() blocks the host (--schedule reference),
   // which a graph capture cannot contain.
   virtual bool capturable() const = 0;
+  // Whether cross-rank collectives sit on the compute stream between compute
+  // tasks (pipeline TP / EP with more than one shard): lane graphs without a
+  // compute program then put each task-collective-task boundary on one queue
+  // (hybrid_3d T=2 on 2 ranks: 81.7 ms with lanes against 79.3 on the single
+  // graph, profiles/hostwait_r5.md), so the runner keeps the single graph.
+  virtual bool collectives_on_compute_stream() const { return false; }
   virtual std::string section_id() const = 0;
   virtual std::string section_title() const = 0;
   // Per-rank key of the host iteration times ("runtimes"; fsdp uses "runtime").

@@ -681,7 +681,8 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       // S=2 mb=4 on 2 ranks: 100.0 ms with lanes against 104.9-106.7,
       // profiles/lanes_n2_r5.md). DLNB_LANE_MIN_TASK_US (1000).
       const double task_us = ctx.compute->lane_task_us(*ss[0]);
-      const bool long_tasks = task_us >= static_cast<double>(env_int("DLNB_LANE_MIN_TASK_US", 1000));
+      const bool long_tasks = task_us >= static_cast<double>(env_int("DLNB_LANE_MIN_TASK_US", 1000)) &&
+                              !strat->collectives_on_compute_stream();
       const bool program_ok = joined || long_tasks || env_int("DLNB_LANE_GRAPHS", 1) >= 2;
       lane_info["compute_task_us"] = task_us;
       const double verdict = ctx.hg().allreduce_max(!linear ? 2.0 : (!program_ok ? 1.0 : 0.0));
@@ -737,7 +738,8 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
         ctx.dev->set_gate_events(false);
         lanes = false;
         why = verdict > 1.5 ? "a lane graph is not linear"
-                            : "the compute lane is neither one compute program nor long single-kernel tasks";
+                            : "the compute lane is neither one compute program nor long single-kernel tasks "
+                              "without collectives between them";
         T.end_capture();
         if (TL) TL->end_capture();
         T.begin_capture();

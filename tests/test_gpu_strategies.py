@@ -368,6 +368,10 @@ def test_pipeline_lanes_two_ranks_one_gpu(root, tmp_path):
     assert not single["global"]["dlnb"]["lane_graphs"]["enabled"]
     assert d["iteration"]["median_ms"] < single["global"]["dlnb"]["iteration"]["median_ms"], (d["iteration"],
                                                                                               single["global"]["dlnb"]["iteration"])
+    # TP collectives between the compute tasks (T = 2): the single graph, with the reason
+    tp = _two_ranks_one_gpu(root, tmp_path, "hybrid_3d", ["1", "4", "2"])
+    lg = tp["global"]["dlnb"]["lane_graphs"]
+    assert not lg["enabled"] and "collectives" in lg["reason"], lg
 
 
 def test_cp_stall_timers_two_ranks_one_gpu(root, tmp_path):
