@@ -51,6 +51,8 @@ class GraphExec {
   virtual void launch(Stream& s) = 0;
   virtual size_t nodes() const = 0;
   virtual size_t edges() const { return 0; }
+  // node count per node type ("kernel:12 memcpy:1 ..."), for the report
+  virtual std::string node_types() const { return ""; }
   // a chain: every node but the first depends on exactly the one before it,
   // so the executor runs the whole graph on the launch stream's queue
   bool linear() const { return nodes() == 0 || edges() + 1 == nodes(); }

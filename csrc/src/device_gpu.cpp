@@ -4,6 +4,9 @@
 
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <string>
+#include <vector>
 
 #include "dlnb/device.hpp"
 #include "dlnb/kernels.hpp"
@@ -75,27 +78,55 @@ class GpuStream : public Stream {
 
 class GpuGraphExec : public GraphExec {
  public:
-  GpuGraphExec(hipGraphExec_t e, size_t n, size_t edges) : exec_(e), n_(n), edges_(edges) {}
+  GpuGraphExec(hipGraphExec_t e, size_t n, size_t edges, std::string types)
+      : exec_(e), n_(n), edges_(edges), types_(std::move(types)) {}
   ~GpuGraphExec() override { (void)hipGraphExecDestroy(exec_); }
   void launch(Stream& s) override { DLNB_HIP_CHECK(hipGraphLaunch(exec_, static_cast<hipStream_t>(s.native()))); }
   size_t nodes() const override { return n_; }
   size_t edges() const override { return edges_; }
+  std::string node_types() const override { return types_; }
 
  private:
   hipGraphExec_t exec_;
   size_t n_, edges_;
+  std::string types_;
 };
+
+std::string graph_node_types(hipGraph_t g, size_t n) {
+  std::vector<hipGraphNode_t> nodes(n);
+  size_t got = n;
+  if (n == 0 || hipGraphGetNodes(g, nodes.data(), &got) != hipSuccess) return "";
+  std::map<std::string, int> count;
+  for (size_t i = 0; i < got; ++i) {
+    hipGraphNodeType t{};
+    if (hipGraphNodeGetType(nodes[i], &t) != hipSuccess) continue;
+    const char* name = t == hipGraphNodeTypeKernel ? "kernel"
+                       : t == hipGraphNodeTypeMemcpy ? "memcpy"
+                       : t == hipGraphNodeTypeMemset ? "memset"
+                       : t == hipGraphNodeTypeHost ? "host"
+                       : t == hipGraphNodeTypeGraph ? "child_graph"
+                       : t == hipGraphNodeTypeEmpty ? "empty"
+                       : t == hipGraphNodeTypeWaitEvent ? "wait_event"
+                       : t == hipGraphNodeTypeEventRecord ? "event_record"
+                                                            : "other";
+    ++count[name];
+  }
+  std::string out;
+  for (const auto& kv : count) out += (out.empty() ? "" : " ") + kv.first + ":" + std::to_string(kv.second);
+  return out;
+}
 
 // Instantiate a captured graph (destroying it); node and edge counts kept.
 std::unique_ptr<GraphExec> instantiate(hipGraph_t g) {
   size_t n = 0, ne = 0;
   (void)hipGraphGetNodes(g, nullptr, &n);
   (void)hipGraphGetEdges(g, nullptr, nullptr, &ne);
+  std::string types = graph_node_types(g, n);
   hipGraphExec_t e = nullptr;
   hipError_t err = hipGraphInstantiate(&e, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
   if (err != hipSuccess) DLNB_THROW("hipGraphInstantiate failed: " << hipGetErrorString(err));
-  return std::unique_ptr<GraphExec>(new GpuGraphExec(e, n, ne));
+  return std::unique_ptr<GraphExec>(new GpuGraphExec(e, n, ne, std::move(types)));
 }
 
 void host_trampoline(void* p) {

@@ -730,6 +730,16 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
           alt_owned.clear();
         }
       } else {
+        // the rejected lanes' shapes (which library added what to a capture)
+        Json rej = Json::array();
+        for (const auto& g : lane_graphs) {
+          Json e = Json::object();
+          e["nodes"] = static_cast<double>(g->nodes());
+          e["edges"] = static_cast<double>(g->edges());
+          e["node_types"] = g->node_types();
+          rej.push_back(e);
+        }
+        lane_info["rejected_lane_graphs"] = rej;
         lane_graphs.clear();
         ctx.dev->free_stamps(lane_done, lane_done_n);  // the single graph signals after its launch
         lane_done = nullptr;
@@ -771,6 +781,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       e["nodes"] = static_cast<double>(g.nodes());
       e["edges"] = static_cast<double>(g.edges());
       e["linear"] = g.linear();
+      e["node_types"] = g.node_types();
       total += g.nodes();
       all_linear = all_linear && g.linear();
       per.push_back(e);
