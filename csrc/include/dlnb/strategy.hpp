@@ -83,12 +83,15 @@ class Strategy {
   // False when enqueue_iteration() blocks the host (--schedule reference),
   // which a graph capture cannot contain.
   virtual bool capturable() const = 0;
-  // Whether cross-rank collectives sit on the compute stream between compute
-  // tasks (pipeline TP / EP with more than one shard): lane graphs without a
-  // compute program then put each task-collective-task boundary on one queue
-  // (hybrid_3d T=2 on 2 ranks: 81.7 ms with lanes against 79.3 on the single
-  // graph, profiles/hostwait_r5.md), so the runner keeps the single graph.
-  virtual bool collectives_on_compute_stream() const { return false; }
+  // Whether lane graphs pay for this strategy when its compute lane is not
+  // one compute program (each task a launch of its own, >= 1 ms on average):
+  // not when cross-rank collectives sit on the compute stream between the
+  // tasks (pipeline TP / EP with more than one shard: hybrid_3d T=2 on 2
+  // ranks ran 81.7 ms with lanes against 79.3 on the single graph), nor for
+  // CP's ~200 task boundaries per iteration (W=1: 4.16 ms over the floor
+  // against 1.3); the pipeline (2 ranks: 100.3 vs 104.8-106.4 ms) and ZeRO DP
+  // (21.7 vs 22.7 ms) do (profiles/hostwait_r5.md).
+  virtual bool lanes_without_program() const { return true; }
   virtual std::string section_id() const = 0;
   virtual std::string section_title() const = 0;
   // Per-rank key of the host iteration times ("runtimes"; fsdp uses "runtime").

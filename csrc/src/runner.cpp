@@ -682,7 +682,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       // profiles/lanes_n2_r5.md). DLNB_LANE_MIN_TASK_US (1000).
       const double task_us = ctx.compute->lane_task_us(*ss[0]);
       const bool long_tasks = task_us >= static_cast<double>(env_int("DLNB_LANE_MIN_TASK_US", 1000)) &&
-                              !strat->collectives_on_compute_stream();
+                              strat->lanes_without_program();
       const bool program_ok = joined || long_tasks || env_int("DLNB_LANE_GRAPHS", 1) >= 2;
       lane_info["compute_task_us"] = task_us;
       const double verdict = ctx.hg().allreduce_max(!linear ? 2.0 : (!program_ok ? 1.0 : 0.0));
@@ -748,8 +748,8 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
         ctx.dev->set_gate_events(false);
         lanes = false;
         why = verdict > 1.5 ? "a lane graph is not linear"
-                            : "the compute lane is neither one compute program nor long single-kernel tasks "
-                              "without collectives between them";
+                            : "the compute lane is not one compute program (and the strategy's launch-per-task "
+                              "lanes do not pay: Strategy::lanes_without_program)";
         T.end_capture();
         if (TL) TL->end_capture();
         T.begin_capture();

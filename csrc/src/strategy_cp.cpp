@@ -242,6 +242,7 @@ class ContextParallel : public Strategy {
 
   std::vector<Stream*> streams() override { return {compute_.get(), cp_stream_.get(), dp_stream_.get()}; }
   bool capturable() const override { return true; }
+  bool lanes_without_program() const override { return false; }  // strategy.hpp
 
   void synchronize() override {
     std::vector<Communicator*> cs = {dp_comm_.get()};

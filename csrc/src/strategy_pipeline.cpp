@@ -989,7 +989,7 @@ class Pipeline : public Strategy {
     return ss;
   }
   bool capturable() const override { return !reference_; }
-  bool collectives_on_compute_stream() const override { return (has_tp_ && T_ > 1) || (has_ep_ && E_ > 1); }
+  bool lanes_without_program() const override { return !((has_tp_ && T_ > 1) || (has_ep_ && E_ > 1)); }
 
   void synchronize() override {
     std::vector<Stream*> ss = {compute_.get(), dp_stream_.get()};

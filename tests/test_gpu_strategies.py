@@ -371,12 +371,12 @@ def test_pipeline_lanes_two_ranks_one_gpu(root, tmp_path):
     # TP collectives between the compute tasks (T = 2): the single graph, with the reason
     tp = _two_ranks_one_gpu(root, tmp_path, "hybrid_3d", ["1", "4", "2"])
     lg = tp["global"]["dlnb"]["lane_graphs"]
-    assert not lg["enabled"] and "collectives" in lg["reason"], lg
+    assert not lg["enabled"] and "program" in lg["reason"], lg
 
 
 def test_cp_stall_timers_two_ranks_one_gpu(root, tmp_path):
-    """Context parallelism's exposed-communication timers on a real 2-rank ring (two processes on GPU 0, xgmi, lane
-    graphs: 15-ms tasks at full time scale): cp_exposed_time / dp_exposed_time come from the tasks' own start
+    """Context parallelism's exposed-communication timers on a real 2-rank ring (two processes on GPU 0, xgmi, the
+    single graph - CP's ~200 task boundaries keep it off lanes): cp_exposed_time / dp_exposed_time come from the tasks' own start
     stamps (TimerSet::stall_before_task / stall_after_task), so per iteration they add up to at most the step's
     excess over its compute floor."""
     doc = _two_ranks_one_gpu(root, tmp_path, "hybrid_cp", ["2"], time_scale="0.2", iters=4)
