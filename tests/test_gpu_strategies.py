@@ -327,15 +327,19 @@ def _two_ranks_one_gpu(root, tmp_path, binary_name, params, extra_env=None, iter
     import os
     import socket
     import subprocess
-    with socket.socket() as so:
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
+    def free_port():
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            return so.getsockname()[1]
+    # the native store binds its own port (DLNB_STORE_PORT, else MASTER_PORT + 1, which may be taken): both free
+    port, store_port = free_port(), free_port()
     binary = os.path.join(root, "build", "bin", binary_name)
     procs = []
     for r in range(2):
         env = dict(os.environ, DLNB_NO_TORCH="1", DLNB_LANE_SHARED="1", DLNB_GEMM_SLICE_US="0", DLNB_GATE_TIMEOUT_S="5",
                    DLNB_XGMI_TIMEOUT_S="20", RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), LOCAL_WORLD_SIZE="2",
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **(extra_env or {}))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLNB_STORE_PORT=str(store_port),
+                   **(extra_env or {}))
         out = str(tmp_path / f"r{r}.json")
         procs.append(subprocess.Popen(
             [binary, model, *params, root, "--backend", "xgmi", "--devices", "0,0", "--comm-cus",
