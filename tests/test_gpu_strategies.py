@@ -379,18 +379,21 @@ def test_pipeline_lanes_two_ranks_one_gpu(root, tmp_path):
 
 
 def test_cp_stall_timers_two_ranks_one_gpu(root, tmp_path):
-    """Context parallelism's exposed-communication timers on a real 2-rank ring (two processes on GPU 0, xgmi, the
-    single graph - CP's ~200 task boundaries keep it off lanes): cp_exposed_time / dp_exposed_time come from the tasks' own start
-    stamps (TimerSet::stall_before_task / stall_after_task), so per iteration they add up to at most the step's
-    excess over its compute floor."""
-    doc = _two_ranks_one_gpu(root, tmp_path, "hybrid_cp", ["2"], time_scale="0.2", iters=4)
+    """Context parallelism's exposed-communication timers on a real 2-rank ring (two processes on GPU 0, xgmi):
+    cp_exposed_time / dp_exposed_time come from the tasks' own start stamps (TimerSet::stall_before_task /
+    stall_after_task), so per iteration they add up to at most the step's mean excess over its compute floor.
+    Lane graphs are forced (DLNB_LANE_GRAPHS=2; CP's default is the single graph): with two ranks' persistent
+    grids on one GPU the single graph's launches starve each other (iterations 0.6-1.6 s against a 0.28-s floor,
+    round 5), which is a property of the shared device, not of the timers."""
+    doc = _two_ranks_one_gpu(root, tmp_path, "hybrid_cp", ["2"], extra_env={"DLNB_LANE_GRAPHS": "2"},
+                             time_scale="0.2", iters=4)
     d = doc["global"]["dlnb"]
     it = d["iteration"]
     for r in doc["ranks"]:
         runs = len(r["runtimes"]) if "runtimes" in r else len(r["runtime"])
         cp = sum(r["cp_exposed_time"]) / runs * 1e3
         dp = sum(r.get("dp_exposed_time", [0.0])) / runs * 1e3
-        assert min(r["cp_exposed_time"]) >= 0 and cp + dp <= it["median_ms"] - it["compute_floor_ms"] + 0.5, (cp, dp, it)
+        assert min(r["cp_exposed_time"]) >= 0 and cp + dp <= it["mean_ms"] - it["compute_floor_ms"] + 0.5, (cp, dp, it)
 
 
 def test_dp_lanes_two_ranks_one_gpu(root, tmp_path):
