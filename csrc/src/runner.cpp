@@ -602,33 +602,11 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   std::vector<Stream*> lanes_ss;  // streams the replay is launched on (lane graphs: each; else the compute stream)
   std::vector<std::unique_ptr<Stream>> alt_owned;
   std::vector<Stream*> alt_ss;    // lane graphs: the second set, odd replays
-  if (opt.graph) {
-    DLNB_REQUIRE(ctx.dev->kind() == DeviceKind::GPU, "--graph needs a GPU");
-    // xgmi kernels take their epochs from device-side counters, so a replayed
-    // graph issues fresh ones; the loopback backends synchronise on the host.
-    DLNB_REQUIRE(backend == "rccl" || backend == "xgmi" || backend == "mixed",
-                 "--graph needs --backend rccl, xgmi or mixed");
-    DLNB_REQUIRE(strat->capturable(), "--graph cannot capture --schedule reference (it blocks the host)");
-    std::vector<Stream*> ss = strat->streams();
-    std::vector<Stream*> others(ss.begin() + 1, ss.end());
-    std::string why;
-    if (env_int("DLNB_LANE_GRAPHS", 1) == 0) {
-      why = "DLNB_LANE_GRAPHS=0";
-    } else if (ss.size() < 2) {
-      why = "one stream";
-    } else if (ctx.ranks_on_device > 1 && env_int("DLNB_LANE_SHARED", 0) == 0) {
-      // a task spinning on its gate holds its CUs, which another rank's
-      // compute on the same device - the one the collective waits for - needs
-      // (DLNB_LANE_SHARED=1, with grids that fit side by side - --comm-cus -
-      // and no slicing: the multi-rank lane path rehearsed on one GPU)
-      why = "ranks share the device";
-    } else {
-      std::string detail;
-      if (!ctx.dev->queues_independent(ss, 0.05, &detail)) why = "streams share a hardware queue (" + detail + ")";
-    }
-    // every rank takes the same decision, and every rank takes part in it
-    bool lanes = ctx.hg().allreduce_max(why.empty() ? 0.0 : 1.0) < 0.5;
-    if (!lanes && why.empty()) why = "another rank cannot use lane graphs";
+  std::vector<Stream*> ss, others;  // --graph: the strategy's streams (compute first)
+  // Capture one iteration: lane graphs when `lanes` (the capture may still
+  // fall back to the single graph: not linear, no program), else the single
+  // graph; `why` is the reason reported when there are no lanes.
+  std::function<void(bool, std::string)> build_graph = [&](bool lanes, std::string why) {
     TraceRange tr("dlnb:graph_capture");
     T.begin_capture();
     if (TL) TL->begin_capture();
@@ -800,6 +778,35 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
         std::cout << "[dlnb] captured one iteration into a HIP graph of " << total << " nodes"
                   << (why.empty() ? "" : " (no lane graphs: " + why + ")") << std::endl;
     }
+    };
+  if (opt.graph) {
+    DLNB_REQUIRE(ctx.dev->kind() == DeviceKind::GPU, "--graph needs a GPU");
+    // xgmi kernels take their epochs from device-side counters, so a replayed
+    // graph issues fresh ones; the loopback backends synchronise on the host.
+    DLNB_REQUIRE(backend == "rccl" || backend == "xgmi" || backend == "mixed",
+                 "--graph needs --backend rccl, xgmi or mixed");
+    DLNB_REQUIRE(strat->capturable(), "--graph cannot capture --schedule reference (it blocks the host)");
+    ss = strat->streams();
+    others.assign(ss.begin() + 1, ss.end());
+    std::string why;
+    if (env_int("DLNB_LANE_GRAPHS", 1) == 0) {
+      why = "DLNB_LANE_GRAPHS=0";
+    } else if (ss.size() < 2) {
+      why = "one stream";
+    } else if (ctx.ranks_on_device > 1 && env_int("DLNB_LANE_SHARED", 0) == 0) {
+      // a task spinning on its gate holds its CUs, which another rank's
+      // compute on the same device - the one the collective waits for - needs
+      // (DLNB_LANE_SHARED=1, with grids that fit side by side - --comm-cus -
+      // and no slicing: the multi-rank lane path rehearsed on one GPU)
+      why = "ranks share the device";
+    } else {
+      std::string detail;
+      if (!ctx.dev->queues_independent(ss, 0.05, &detail)) why = "streams share a hardware queue (" + detail + ")";
+    }
+    // every rank takes the same decision, and every rank takes part in it
+    bool lanes = ctx.hg().allreduce_max(why.empty() ? 0.0 : 1.0) < 0.5;
+    if (!lanes && why.empty()) why = "another rank cannot use lane graphs";
+    build_graph(lanes, why);
   }
   const bool replay = graph || !lane_graphs.empty();
   Stream* origin = replay ? strat->streams()[0] : nullptr;
@@ -851,6 +858,37 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     wait_iteration();
     warm.push_back(now_s() - t0);
     if (TL) TL->collect(-1);
+  }
+  // Lane replays that timed out a gate wait, or ran far longer than the
+  // compute floor, in the warm-up: re-capture the single graph and warm it
+  // once (every rank alike). A safety valve for a first run on hardware the
+  // lanes were not measured on (the 8-GPU node); `lane_graphs.fallback`.
+  if (!lane_graphs.empty() && !warm.empty()) {
+    ComputeEngine::ChainCounters cc;
+    double timeouts = static_cast<double>(ctx.dev->gate_event_timeouts());
+    if (ctx.compute->chain_counters(cc)) timeouts += cc.wait_timeouts + cc.gate_timeouts;
+    const double floor_s = strat->compute_floor_us(ctx) * 1e-6 * opt.time_scale;
+    const bool slow = warm.back() > 2.0 * floor_s + static_cast<double>(env_int("DLNB_LANE_WARM_SLACK_S", 5));
+    if (ctx.hg().allreduce_max((timeouts > 0 || slow) ? 1.0 : 0.0) > 0.5) {
+      const std::string what = timeouts > 0 ? "gate waits timed out in the warm-up"
+                                            : "a warm-up replay ran over twice the compute floor";
+      if (ri.rank == 0 && !opt.quiet) std::cerr << "[dlnb] lane graphs: " << what << "; the single graph instead\n";
+      ctx.dev->synchronize();
+      lane_graphs.clear();
+      if (lane_done) ctx.dev->free_stamps(lane_done, lane_done_n);
+      lane_done = nullptr;
+      lane_done_n = 0;
+      joined = false;
+      alt_ss.clear();
+      alt_owned.clear();
+      ctx.dev->set_gate_events(false);
+      lane_info = Json::object();
+      build_graph(false, "lanes fell back after the warm-up");
+      lane_info["fallback"] = what;
+      fault.at_iteration(iter_no++, inject_task);
+      enqueue();
+      wait_iteration();
+    }
   }
   T.clear();
 

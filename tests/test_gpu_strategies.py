@@ -85,6 +85,21 @@ def test_fsdp_program_lanes(root):
     assert not lg["enabled"] and "program" in lg["reason"], lg
 
 
+def test_lane_fallback_after_warmup(root):
+    """The post-warm-up safety valve: lane replays that time out a gate wait or run over twice the compute floor
+    (forced here with a negative slack) are replaced by the single graph, re-warmed once, and the run completes
+    at the same step time with the fallback reported."""
+    doc = engine.run_native("fsdp", "llama3_8b_16_bfloat16", 32, 1, base_path=root, warmup=2, runs=3,
+                            compute="gemm", backend="rccl", time_scale=0.05, graph=True, quiet=True,
+                            env={"DLNB_LANE_WARM_SLACK_S": "-100000"})
+    d = doc["global"]["dlnb"]
+    lg = d["lane_graphs"]
+    assert not lg["enabled"] and "warm-up" in lg["fallback"] and "fell back" in lg["reason"], lg
+    it = d["iteration"]
+    assert it["compute_floor_ms"] * 0.999 <= it["median_ms"] < it["compute_floor_ms"] * 1.02 + 1.0, it
+    assert doc["ranks"][0]["prearm_go_timeouts"] == 0
+
+
 def test_measured_stats_generator(tmp_path):
     """models.measure times a real block on the GPU and writes a parseable table."""
     from dlnetbench_amd.models import measure
