@@ -146,6 +146,8 @@ class ComputeEngine {
     (void)s; (void)gates; (void)tag; (void)host_done;
   }
   virtual bool program_joined(Stream& s) { (void)s; return false; }
+  // Bound (s) of the deadline tasks' gate waits enqueued from here on.
+  virtual void set_gate_timeout(double s) { (void)s; }
   // Mean duration (us) of the compute tasks enqueued on s since set_lane_join
   // (a lane capture), each one kernel (deadline / idle / spin); < 0 when any
   // task took several launches (gemm-work, flops) or none ran. A lane of long

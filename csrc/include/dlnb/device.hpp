@@ -161,6 +161,8 @@ class Device {
   // profiles/absorb_r4.md). Waits are bounded (DLNB_GATE_TIMEOUT_S, 60) and
   // counted (gate_event_timeouts).
   virtual void set_gate_events(bool on) { DLNB_REQUIRE(!on, "gate events need a GPU device"); }
+  // Bound (s) of the gate-event waits captured from here on (DLNB_GATE_TIMEOUT_S, 60, unless set).
+  virtual void set_gate_timeout(double s) { (void)s; }
   // With gate events on: record e on s as a gate a kernel the caller launches
   // on s next raises itself (returns the gate and tag it must store; a
   // deadline task's DlSync::done_gate). False (nothing recorded) otherwise.

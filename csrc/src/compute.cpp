@@ -208,6 +208,9 @@ class GpuCompute : public ComputeEngine {
     lane_stats_.clear();
   }
   bool program_joined(Stream& s) override { return joined_.count(&s) != 0; }
+  void set_gate_timeout(double s) override {
+    gate_timeout_ticks_ = static_cast<uint64_t>(s * kernels::wallclock_hz_nominal(dev_.index()));
+  }
   double lane_task_us(Stream& s) override {
     auto it = lane_stats_.find(&s);
     if (it == lane_stats_.end() || it->second.n == 0 || !it->second.single) return -1.0;

@@ -256,8 +256,10 @@ class GpuDevice : public Device {
   }
   uint64_t gate_timeout_ticks() {
     static const double s = static_cast<double>(env_int("DLNB_GATE_TIMEOUT_S", 60));
-    return static_cast<uint64_t>(s * stamp_hz());
+    return static_cast<uint64_t>((gate_timeout_s_ > 0 ? gate_timeout_s_ : s) * stamp_hz());
   }
+  void set_gate_timeout(double s) override { gate_timeout_s_ = s; }
+  double gate_timeout_s_ = 0.0;
   void gate_mark(GpuEvent& e, hipStream_t s) {
     if (!e.gate) e.gate = alloc_gate();
     e.tag = e.tag == 0xffffffffu ? 1u : e.tag + 1;

@@ -806,6 +806,15 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     // every rank takes the same decision, and every rank takes part in it
     bool lanes = ctx.hg().allreduce_max(why.empty() ? 0.0 : 1.0) < 0.5;
     if (!lanes && why.empty()) why = "another rank cannot use lane graphs";
+    // Gate waits bounded by 4x the compute floor (at least 15 s) unless
+    // DLNB_GATE_TIMEOUT_S is set: a gate that never comes costs the warm-up
+    // that much before the safety valve below, not 60 s per wait.
+    if (!std::getenv("DLNB_GATE_TIMEOUT_S")) {
+      const double t = std::max(15.0, 4.0 * strat->compute_floor_us(ctx) * 1e-6 * opt.time_scale);
+      ctx.dev->set_gate_timeout(t);
+      ctx.compute->set_gate_timeout(t);
+      lane_info["gate_timeout_s"] = t;
+    }
     build_graph(lanes, why);
   }
   const bool replay = graph || !lane_graphs.empty();

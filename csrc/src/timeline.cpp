@@ -418,6 +418,7 @@ class TracingCompute : public ComputeEngine {
     in_->set_lane_join(s, gates, tag, host_done);
   }
   bool program_joined(Stream& s) override { return in_->program_joined(s); }
+  void set_gate_timeout(double s) override { in_->set_gate_timeout(s); }
   double lane_task_us(Stream& s) override { return in_->lane_task_us(s); }
   void reset_capped(Stream& s) override { in_->reset_capped(s); }
   bool chain_counters(ChainCounters& c) override { return in_->chain_counters(c); }
