@@ -382,3 +382,23 @@ def test_slurm_environment_bootstrap(tmp_path, data_dir, root):
     assert d["global"]["world_size"] == 2 and sorted(r["rank"] for r in d["ranks"]) == [0, 1]
     assert [r["local_rank"] for r in sorted(d["ranks"], key=lambda r: r["rank"])] == [0, 1]
 
+
+
+def test_every_env_knob_is_documented(root):
+    """docs/KNOBS.md lists every DLNB_* variable the native runtime and the Python tools read."""
+    import re
+    pat = re.compile(r'(?:getenv|env_[a-z]+|environ\.get|environ\[)\(?\s*\{?"(DLNB_[A-Z0-9_]+)"')
+    used = set()
+    for top in ("csrc", "dlnetbench_amd"):
+        for d, _, files in os.walk(os.path.join(root, top)):
+            for f in files:
+                if f.endswith((".cpp", ".hpp", ".hip", ".py")):
+                    with open(os.path.join(d, f), errors="replace") as fh:
+                        used |= set(pat.findall(fh.read()))
+    with open(os.path.join(root, "bench.py")) as fh:
+        used |= set(pat.findall(fh.read()))
+    with open(os.path.join(root, "docs", "KNOBS.md")) as fh:
+        doc = fh.read()
+    assert len(used) > 30
+    missing = sorted(k for k in used if f"`{k}`" not in doc)
+    assert not missing, f"undocumented knobs: {missing}"
