@@ -845,19 +845,9 @@ def main() -> int:
     if xgmi_exact_ok and rel:
         os.environ["DLNB_XGMI_RELEASE"] = rel
 
-    from dlnetbench_amd import engine
     from dlnetbench_amd.utils.stats import load_stats
     st = load_stats(os.path.join(a.base_path, "model_stats", a.model + ".txt"))
     use_graph = a.graph and on_gpu and a.schedule == "overlap"
-
-    def run(phase: str, strategy: str, model: str, *params: int, graph: bool, **kw: Any) -> dict:
-        _store_env(world, rank, phase)
-        os.environ["DLNB_BLOCK"] = "headline"  # the in-process run's name for DLNB_INJECT_FAULT block=
-        try:
-            return engine.run(strategy, model, *params, base_path=a.base_path, backend=a.backend, silent=True,
-                              devices=a.devices, time_scale=a.time_scale, graph=graph or None, **kw)
-        finally:
-            os.environ.pop("DLNB_BLOCK", None)
 
     # The result line must be the only stdout line: route whatever the native
     # libraries print (e.g. RCCL's banner) to stderr while the benchmark runs.
@@ -867,40 +857,41 @@ def main() -> int:
     extra: Dict[str, Any] = {}
     doc: Optional[dict] = None
     headline_error: Optional[str] = None
-    # N > 1 with the RCCL half of the exactness pass not passed (wrong, or it
-    # never finished - a hung communicator setup would hang this process too):
-    # the headline runs as a bounded child of every rank, like every block after it.
-    head_child = (world > 1 and on_gpu and bool(exact) and a.backend == "auto"
-                  and (exact.get("exact") or {}).get("rccl") is not True)
+    headline_graph_error: Optional[str] = None
     try:
+        # The headline runs as a bounded child process of every rank (the
+        # native binary), like every block after it: a device
+        # failure ends that process - its queues, and any kernel still
+        # spinning on them, go with it - and never this one, which still
+        # prints the line.
         fsdp_kw = dict(schedule=a.schedule, wire_dtype="bf16")
         t0 = ph.now()
+        est0 = _Estimator(a, world, 20.0, 0, 3000.0)
+        nominal = est0.setup + (a.warmup + a.steps) * est0.iter_s("fsdp", a.model, (a.units, world))
+
+        def head(tag: str, graph: bool) -> dict:
+            # (the headline always runs: at least 60 s, more when the budget has it)
+            t = budget.plan(tag.lstrip("."), max(60.0, est0.want(nominal, 300)), 1.0) or 60.0
+            d = _child_run(a, world, rank, tag, "fsdp", a.model, (a.units, world), t, backend=a.backend,
+                           graph=graph, compute=a.compute, warmup=a.warmup, runs=a.steps, **fsdp_kw)
+            return d if rank == 0 else {}
+
         try:
-            if head_child:
-                est0 = _Estimator(a, world, 20.0, 0, 3000.0)
-                nominal = est0.setup + (a.warmup + a.steps) * est0.iter_s("fsdp", a.model, (a.units, world))
-                t = budget.plan("headline", est0.want(nominal, 300), nominal)
-                if t is None:
-                    raise RuntimeError(_skipped(budget)["skipped"])
-                d = _child_run(a, world, rank, ".head", "fsdp", a.model, (a.units, world), t, backend=a.backend,
-                               graph=use_graph, compute=a.compute, warmup=a.warmup, runs=a.steps, **fsdp_kw)
-                doc = d if rank == 0 else {}
-                if rank == 0 and a.json:
-                    with open(a.json, "w") as f:
-                        json.dump(d, f)
             try:
-                if not head_child:
-                    doc = run("", "fsdp", a.model, a.units, world, graph=use_graph, warmup=a.warmup, runs=a.steps,
-                              compute=a.compute, json=a.json, **fsdp_kw)
+                doc = head(".headline", use_graph)
             except RuntimeError as e:
-                if not use_graph or head_child:
+                if not use_graph:
                     raise
-                # Graph capture is symmetric across ranks, so every rank takes this
-                # path; the retry rendezvouses on a fresh store.
-                print(f"[bench] HIP graph run failed ({e}); retrying with per-iteration enqueue", file=sys.stderr)
+                # Graph capture is symmetric across ranks, so every rank takes
+                # this path; the retry is a fresh child on a fresh store.
+                headline_graph_error = str(e)[:300]
+                print(f"[bench] HIP graph run failed ({e}); retrying with per-iteration enqueue in a new process",
+                      file=sys.stderr)
                 use_graph = False
-                doc = run(".retry", "fsdp", a.model, a.units, world, graph=False, warmup=a.warmup, runs=a.steps,
-                          compute=a.compute, json=a.json, **fsdp_kw)
+                doc = head(".headline.retry", False)
+            if rank == 0 and a.json and doc:
+                with open(a.json, "w") as f:
+                    json.dump(doc, f)
         except Exception as e:  # noqa: BLE001
             # still print a line (value null, the error): the driver reads
             # what failed instead of nothing
@@ -1086,6 +1077,9 @@ def main() -> int:
             out["model_fit"] = fit
     if fallback is not None:
         out["headline_fallback"] = fallback
+    if headline_graph_error:
+        # the HIP-graph headline failed and the value (if any) is the per-iteration retry's
+        out["headline_graph_error"] = headline_graph_error
     out.update(exact)
     # Every timed number is qualified by the exactness verdict of its backend
     # (VERDICT r3 #4): "verified" per checked backend; a block timed on a

@@ -12,10 +12,13 @@
 //     energy counter with DLNB_ENERGY=amdsmi;
 //   * Tracer emits roctx ranges (libroctx64, dlopen'd) around iterations
 //     and phases when --trace is given, visible with rocprofv3 --marker-trace;
-//   * FaultInjector (DLNB_INJECT_FAULT="rank=R,iter=I,mode=exit|hang|throw[,block=TAG]";
+//   * FaultInjector (DLNB_INJECT_FAULT="rank=R,iter=I,mode=exit|hang|throw|task|gate[,gate=K][,block=TAG]";
 //     block: only in a run whose DLNB_BLOCK env is TAG)
 //     kills, hangs or fails one rank at one iteration to exercise the
-//     timeout / async-error detection and the launcher's teardown.
+//     timeout / async-error detection and the launcher's teardown; gate: a
+//     device-side hang - the K-th device gate signal of the run (0) is never
+//     raised, so the tasks and lanes waiting for it spin until the host's
+//     timeout aborts them (the failure containment of VERDICT r5 #2).
 #pragma once
 
 #include <functional>

@@ -19,9 +19,14 @@
 
 namespace dlnb {
 
+// The message of the last Error constructed on this thread (read by the
+// failure path of a GPU run while the exception is still unwinding, where
+// std::current_exception() has nothing yet).
+std::string& last_error_message();
+
 class Error : public std::runtime_error {
  public:
-  explicit Error(const std::string& what) : std::runtime_error(what) {}
+  explicit Error(const std::string& what) : std::runtime_error(what) { last_error_message() = what; }
 };
 
 #define DLNB_THROW(msg)                                                        \

@@ -14,12 +14,15 @@
 //           deadline: exactly the table's duration, with the matrix cores
 //           and HBM as busy as in training (the reference's usleep leaves
 //           the GPU idle, so its collectives never contend with compute).
-//   gemm-work - the same GEMM launched a fixed number of times, calibrated
-//           at start-up (after a DVFS settle) so the uncontended duration
-//           matches the table; contention / clock drops stretch it, like
-//           real training compute.
-//   flops - executes the table's FLOP count on the MI355X GEMM at whatever
-//           speed the hardware gives (MI355X-native compute time).
+//   gemm-work - the same GEMM as a fixed amount of work: full-K rounds of
+//           256 x 256 tiles over the same persistent grid plus a partial-K
+//           tail tile, calibrated at start-up (after a DVFS settle) so the
+//           uncontended duration matches the table; contention / clock drops
+//           stretch it, like real training compute. A task is a program task
+//           of the deadline kernels (one launch, or one task of the lane's
+//           compute program): it stamps its own start and end;
+//   flops - the same with the table's FLOP count as the work (MI355X-native
+//           compute time).
 #pragma once
 
 #include <memory>
@@ -81,6 +84,11 @@ class ComputeEngine {
     if (done) s.record(*done);
   }
   virtual uint64_t task_ticks(double us) const { (void)us; return 0; }
+  // Fixed-work compute (gemm-work, flops) has no deadline: its tasks stamp
+  // their end too, and this is the end slot of the last task enqueued on s
+  // (nullptr: the end is start + task_ticks(us)). A stall after a task is
+  // timed from there (task_mark()).
+  virtual const uint64_t* last_task_end(Stream& s) { (void)s; return nullptr; }
   // Device-side dependency times (gemm mode; csrc/kernels/deadline_sync.hpp).
   // A gate is a device word: signal(s, g) enqueues on s (a collective's
   // stream, after the collective, before the event the compute stream waits
@@ -130,9 +138,17 @@ class ComputeEngine {
   // returns false when the engine does not build programs (then tasks launch
   // one by one). after_capture(): upload the task lists of programs built
   // during a graph capture (device memory written outside the capture).
+  // end_program(s, join_ok): join_ok = nothing is enqueued on s after the
+  // program in this iteration, so a pending lane join (set_lane_join) may
+  // end it; otherwise the join is not taken and the lane ends with its own
+  // done word (work after the join - the optimizer, a stall stamp -
+  // would run outside the iteration the host times).
   virtual bool begin_program(Stream& s) { (void)s; return false; }
-  virtual void end_program(Stream& s) { (void)s; }
+  virtual void end_program(Stream& s, bool join_ok) { (void)s; (void)join_ok; }
   virtual void after_capture() {}
+  // Programs launched on s so far (a lane of one program per iteration pays
+  // no kernel boundaries between its tasks, joined or not).
+  virtual long programs_on(Stream& s) { (void)s; return 0; }
   // Lane join (the runner, lane graphs): the next program ended on s finishes
   // with a join task - thread 0 of block 0 waits for `gates` (the other
   // lanes' end gates, raised with `tag`) and stores the iteration number into
@@ -149,8 +165,8 @@ class ComputeEngine {
   // Bound (s) of the deadline tasks' gate waits enqueued from here on.
   virtual void set_gate_timeout(double s) { (void)s; }
   // Mean duration (us) of the compute tasks enqueued on s since set_lane_join
-  // (a lane capture), each one kernel (deadline / idle / spin); < 0 when any
-  // task took several launches (gemm-work, flops) or none ran. A lane of long
+  // (a lane capture), each one kernel (deadline / idle / spin / fixed work);
+  // < 0 when any task took several launches or none ran. A lane of long
   // single-kernel tasks pays its kernel boundaries on one queue at little
   // cost (the runner keeps such lanes without a compute program).
   virtual double lane_task_us(Stream& s) { (void)s; return -1.0; }
@@ -165,17 +181,22 @@ class ComputeEngine {
   //     tasks' gates; never expected, counted since the engine was made).
   // reset_capped zeroes the capped / absorbed counts (stream-ordered on s);
   // chain_counters reads them (host, after a sync).
+  //   aborted: waits that gave up on the host's abort word (Device::abort_word);
+  //   late_blocks: program blocks that reached a task after a later one was
+  //     claimed (dispatched late) and skipped it.
   struct ChainCounters {
     double capped_tasks = 0, capped_s = 0, absorbed_tasks = 0, absorbed_s = 0;
-    double wait_timeouts = 0, gate_timeouts = 0;
+    double wait_timeouts = 0, gate_timeouts = 0, aborted = 0, late_blocks = 0;
   };
   virtual void reset_capped(Stream& s) { (void)s; }
   virtual bool chain_counters(ChainCounters& c) { (void)c; return false; }
   // Fixed-work modes (gemm-work, flops): time every compute task on the
-  // device into t ("compute_task_time") next to its table duration
-  // ("compute_task_table"), so the runner can report how much collectives
-  // running beside the compute stretch it (compute_stretch). Deadline modes
-  // last exactly the table time by construction and record nothing.
+  // device into t ("compute_task_time", from the task's own start and end
+  // stamps) next to its table duration ("compute_task_table"), so the runner
+  // can report how much collectives running beside the compute stretch it
+  // (compute_stretch). Deadline modes last exactly the table time by
+  // construction and record nothing. Every GPU mode also feeds its tasks'
+  // start (and end) stamps to t's stall timers.
   virtual void set_task_timers(TimerSet* t) { (void)t; }
   virtual Json describe() const = 0;
   virtual ComputeMode mode() const = 0;
@@ -183,5 +204,16 @@ class ComputeEngine {
 
 std::unique_ptr<ComputeEngine> make_compute_engine(Device& dev, ComputeMode mode, const ComputeShape& shape,
                                                    double time_scale);
+
+// Where a compute task ends on the device clock, for a stall timer after it:
+// its end stamp (fixed work) or its start stamp + its deadline ticks.
+struct TaskMark {
+  const uint64_t* slot = nullptr;
+  uint64_t ticks = 0;
+};
+inline TaskMark task_mark(ComputeEngine& ce, Stream& s, const uint64_t* start, double us) {
+  if (const uint64_t* e = ce.last_task_end(s)) return {e, 0};
+  return {start, ce.task_ticks(us)};
+}
 
 }  // namespace dlnb

@@ -119,7 +119,25 @@ class Device {
   // the streams to go idle. CPU devices raise their abort switch (queued
   // tasks are skipped, event waits return) and drain; GPU devices: nothing
   // (the communicators were aborted, the runtime owns the queues).
-  virtual void abort_and_drain() {}
+  // GPU: raise the abort word (below), then wait - at most
+  // DLNB_ABORT_DRAIN_S (20) seconds - for every stream of the device to go
+  // idle; false when one did not (the caller must not free anything the
+  // device may still use: the process is then unusable for another run).
+  virtual bool abort_and_drain() { return true; }
+  // ---- failure containment: a host-mapped word every device-side wait polls
+  // next to what it waits for (the deadline tasks' gates and claims, the
+  // programs' joins, gate_wait and the pre-armed replays' go waits). Once
+  // raised (raise_abort, a host store: no queue needed) every such wait gives
+  // up, a deadline task that waited ends at once, and a pre-armed replay the
+  // abort releases runs through on a poisoned iteration word without
+  // computing or waiting (kernels::kPoisonIter). abort_word: the device-side
+  // pointer the kernels take (nullptr: none).
+  virtual const uint64_t* abort_word() { return nullptr; }
+  virtual void raise_abort() {}
+  virtual bool abort_raised() const { return false; }
+  // An idle wait of `us` on s (GPU: a one-wave s_memrealtime wait kernel;
+  // CPU: a sleeping task): the comm fault injector's delay.
+  virtual void idle(Stream& s, double us) = 0;
   // Timestamps taken when a stream reaches a point (device clock on GPU: a
   // one-wave kernel stores s_memrealtime into host-mapped memory; host clock
   // on CPU). Unlike timing events they are exact across cross-stream waits.

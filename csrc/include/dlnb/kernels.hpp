@@ -40,8 +40,15 @@ enum DlCounter : int {
   kGateTimeouts = 3,   // deadline tasks whose gate wait gave up (agree_t0)
   kAbsorbedTicks = 4,  // lateness chained tasks took out of their own compute (<= the cap each)
   kAbsorbedTasks = 5,  // chained tasks that absorbed any
+  kAborted = 6,        // waits (gates, claims, joins, go words) that left because the host raised the abort word
+  kLateBlocks = 7,     // program blocks that reached a task after a later task was claimed (skipped it)
   kNumCounters = 8
 };
+// The iteration word's value after an abort (host_wait stores it instead of
+// the iteration when the abort word is up): every deadline task that reads it
+// ends at once, every gate wait gives up - a pre-armed replay released by the
+// abort runs through without computing or waiting (deadline_sync.hpp).
+constexpr uint64_t kPoisonIter = ~0ull;
 struct DlSync {
   uint64_t* tstart[2] = {nullptr, nullptr};
   const uint64_t* gate[2] = {nullptr, nullptr};
@@ -56,15 +63,30 @@ struct DlSync {
   // task's last launch only.
   uint64_t* done_gate = nullptr;
   uint32_t done_tag = 0;
+  uint32_t pad = 0;
+  // Host-mapped abort word (Device::abort_word; nullptr: none): every wait of
+  // the task polls it next to what it waits for and gives up once it is
+  // non-zero (counted in kAborted); a task whose gate wait saw it ends at once.
+  const uint64_t* abort = nullptr;
 };
-// One task of a deadline program (gemm_tn_deadline_program; device memory):
-// its duration, its epoch on the slot (1..65535, consecutive tasks differ)
-// and its start protocol (gates, chain, stamps, done gate).
+// One task of a compute program (gemm_tn_deadline_program; device memory):
+// its start protocol (gates, chain, stamps, done gate) and either
+//   * a deadline task: `ticks` of the device clock after its agreed start, or
+//   * a fixed-work task (ticks == 0, work_rounds or tail_kt != 0): every block
+//     computes work_rounds full 256 x 256 tiles and then one tile of tail_kt
+//     K-tiles, however long that takes; it starts once the program's previous
+//     task is complete on every block (and its gates are up), the last block
+//     to finish stores the end time into *tend and raises the done gate, or
+//   * the join (ticks == 0, no work): the program's last task (dl::join).
+// epoch: the task's index among the stream's program tasks of the iteration.
 struct DlTask {
   DlSync sync;
   uint64_t ticks = 0;
   uint32_t epoch = 0;
+  uint32_t work_rounds = 0;
+  uint32_t tail_kt = 0;
   uint32_t pad = 0;
+  uint64_t* tend = nullptr;  // fixed-work: end stamp (host-mapped or device memory; nullptr: none)
 };
 // Device gates: two words {seq, time} in device memory (16-byte aligned).
 // seq = iteration << 32 | tag, the iteration read from *iter (the device's
@@ -75,13 +97,20 @@ struct DlTask {
 // gate_signal: one wave stores the time (s_memrealtime), then seq (release)
 // when the stream reaches this point. tag != 0.
 void gate_signal(uint64_t* gate, const uint64_t* iter, uint32_t tag, void* stream);
+// Fault injection (DLNB_INJECT_FAULT mode=gate): the index-th gate_signal of
+// this process (counted from now on, from 0) launches nothing, so whatever
+// waits for that gate waits until its timeout - or the host's abort.
+void fail_gate_signal(long index);
 // One wave waits until the gate carries this iteration's seq for tag (raised
 // by gate_signal on another stream), at most timeout ticks; a timeout adds 1
 // to *timeouts and lets the stream go on (a wait that can never be satisfied
 // - e.g. the raising kernel queued behind this one on the same hardware queue
 // - must not hang the GPU).
+// The wait gives up as soon as the host-mapped abort word (optional) is up.
+// A gate counts as raised once its sequence word is >= the one expected (the
+// words only grow within a run: a later replay's raise also satisfies it).
 void gate_wait(const uint64_t* gate, const uint64_t* iter, uint32_t tag, uint64_t timeout_ticks, uint64_t* timeouts,
-               void* stream);
+               void* stream, const uint64_t* abort = nullptr);
 // One wave stores value into *word (device memory, agent scope): the
 // iteration word at the head of a lane.
 void set_word(uint64_t* word, uint64_t value, void* stream);
@@ -115,12 +144,15 @@ void stamp(uint64_t* slot, void* stream);
 // one to *timeouts, so the stream always drains).
 // host_wait also stores iter_value into *iter_out (device memory; optional)
 // once released: the pre-armed loop's lane head sets the iteration word.
+// With the abort word (optional, host-mapped) up it stops waiting at once,
+// stores kPoisonIter into *iter_out and no timeout is counted: what it held
+// back runs through without computing or waiting (kernels read the poison).
 void host_signal(uint64_t* word, uint64_t value, void* stream);
 // *word (host-coherent) = *iter (the device's iteration word) when the stream
 // gets here: a lane graph's last node (relaxed: no L2 write-back first).
 void lane_done(uint64_t* word, const uint64_t* iter, void* stream);
 void host_wait(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uint64_t* timeouts, void* stream,
-               uint64_t* iter_out = nullptr, uint64_t iter_value = 0);
+               uint64_t* iter_out = nullptr, uint64_t iter_value = 0, const uint64_t* abort = nullptr);
 int num_cus(int device);
 
 // GEMM: requires M % 256 == 0, N % 256 == 0, K*elem_size % 128 == 0, leading
@@ -205,9 +237,21 @@ void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K
 // one-wave kernels to queue behind at a task boundary. Only where
 // deadline_program_ok() (the per-tile 8-phase and one-wave-per-SIMD
 // kernels; not the short-K streaming or single-K-tile fallbacks).
+// epoch: 0 = the tasks' claim sequence follows the device iteration word
+// (programs of a replayed lane graph: sequence = iteration * 4096 + task
+// index, monotonic, so a block that reaches a task after a later one was
+// claimed skips it - kLateBlocks); otherwise the one-launch epoch protocol of
+// gemm_tn_deadline (1..65535, different from the slot's previous task; n must
+// be 1): a fixed-work task launched on its own.
 bool deadline_program_ok(int M, int N, int K, DType in_t);
 void gemm_tn_deadline_program(const void* A, const void* B, void* C, int M, int N, int K, DType in_t,
-                              const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream);
+                              const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream,
+                              uint32_t epoch = 0);
+// K-tiles (128 bytes of K each) of one 256 x 256 tile of the program kernel
+// chosen for this shape, and the granularity of a fixed-work task's tail
+// (tail_kt must be a multiple of it, >= 2).
+int program_ktiles(int M, int N, int K, DType in_t);
+int program_tail_multiple(int M, int N, int K, DType in_t);
 
 // Elementwise "optimizer" stand-in (SGD-momentum on bf16 shards, fp32 math):
 // p = p - lr * (m = beta*m + g). Used by the optional --optimizer step.

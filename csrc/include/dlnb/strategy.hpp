@@ -40,6 +40,9 @@ struct Context {
   std::unique_ptr<Device> dev;
   std::unique_ptr<CommFactory> comms;
   std::vector<CommRecord> comm_log;
+  // every communicator the strategy created (outermost wrapper; owned by the
+  // strategy): the failure path aborts them all (device_failure)
+  std::vector<Communicator*> live_comms;
   std::unique_ptr<ComputeEngine> compute;
   ModelStats stats;
   bool have_arch = false;
@@ -144,8 +147,23 @@ Json run_benchmark(const Options& opt);
 int main_for(StrategyKind kind, int argc, char** argv);
 
 // Synchronise a set of streams with a deadline; polls communicator async
-// errors so a dead peer aborts the job instead of hanging it.
+// errors so a dead peer aborts the job instead of hanging it (the failure
+// goes through device_failure before the exception is thrown).
 void sync_streams(const std::vector<Stream*>& streams, const std::vector<Communicator*>& comms, Device& dev);
+
+// The failure path of a run on this thread, called where a
+// failure is detected (sync_streams' timeout / async error, an exception
+// leaving the timed loop, run_rank's catch) BEFORE anything is torn down:
+// raises the device's abort word - every device-side wait gives up, a
+// pre-armed replay runs through poisoned - and then, in a CLI process that
+// owns its ranks (no loopback hub), prints `why` and ends the process at once
+// (std::_Exit(3): the kernel driver reclaims the queues; no destructor waits
+// on device work that may never finish); otherwise (a library host) aborts
+// every communicator of the run. Once per run; a no-op outside one.
+void device_failure(const std::string& why);
+// Whether a failed run of this process left device work that did not drain
+// (Device::abort_and_drain): the process then refuses further runs.
+bool process_poisoned();
 
 // While alive on this thread: sync_streams() waits for flags[i] >= value for
 // every i < n (host-coherent words a kernel enqueued after each replayed

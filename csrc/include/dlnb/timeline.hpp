@@ -51,6 +51,11 @@ class Timeline {
   // after the deadline belongs to the next chained task, which starts at it).
   void end_after(int token, Stream& s, uint64_t dur_ticks, const char* cat, const std::string& name,
                  Json args = Json::object());
+  // End a span at a stamp the work writes itself into *end (host-mapped; a
+  // fixed-work task's own end stamp, ComputeEngine::last_task_end), read at
+  // collect() like the span's own slots.
+  void end_at(int token, Stream& s, const uint64_t* end, const char* cat, const std::string& name,
+              Json args = Json::object());
   // Track name of a stream (the first name given wins).
   void label(Stream& s, const std::string& name);
   // Graph mode: the spans enqueued between these are the captured
@@ -87,8 +92,9 @@ class Timeline {
   uint64_t* stamps_ = nullptr;
   size_t cap_ = 0, next_ = 0, max_events_ = 0;
   struct Span {
-    int a, b, lane;  // b < 0: the span lasts dur ticks from a
+    int a, b, lane;  // b < 0: the span lasts dur ticks from a (or ends at *end)
     uint64_t dur;
+    const uint64_t* end;
     const char* cat;
     std::string name;
     Json args;

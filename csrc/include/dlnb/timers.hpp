@@ -57,18 +57,31 @@ class TimerSet {
   // precedes the wait in the iteration; a stall_before_task that nothing
   // follows is closed by finish_stalls() (the runner, after each
   // enqueue_iteration) with a stamp on s.
+  // A task without a deadline (fixed work) reports its own end stamp too
+  // (task_started's `end`): the stream's next wait is timed from there.
+  // Without a task before it in the iteration, a wait is timed from a stamp
+  // right before it (mark: nothing waited for between the two).
   void set_task_stamps(bool on) { task_stamps_ = on; }
   bool task_stamps() const { return task_stamps_ && enabled_; }
   uint64_t* task_slot(Stream& s);
-  void task_started(Stream& s, const uint64_t* start, uint64_t ticks);
+  void task_started(Stream& s, const uint64_t* start, uint64_t ticks, const uint64_t* end = nullptr);
+  // A stamp kernel on s now (its slot; nullptr when disabled).
+  const uint64_t* mark(Stream& s);
+  // value = *b - *a for two stamp slots of this set (a task's own start and
+  // end: compute_task_time).
+  void pair(const uint64_t* a, const uint64_t* b, const std::string& name);
   void stall_before_task(Stream& s, Event& e, const std::string& name);
   void stall_after_task(Stream& s, Event& e, const std::string& name);
   void finish_stalls();
   void add(const std::string& name, double seconds);
   void ensure(const std::string& name);
-  // Call after the streams involved have been synchronised.
+  // Call after the streams involved have been synchronised. Intervals are
+  // causally ordered, so a negative one (mis-ordered stamps) is recorded as
+  // 0 and counted per timer (negatives_json: {name: {count, worst_ms}}).
   void resolve();
   void clear();
+  Json negatives_json() const;
+  bool has_negatives() const { return !negatives_.empty(); }
   // Graph mode: between begin_capture() and end_capture() host values are
   // recorded instead of applied; afterwards the stamp pairs and the recorded
   // host values are re-applied by every resolve() (one per graph replay).
@@ -106,6 +119,11 @@ class TimerSet {
   void close_pending(TaskClock& c, const uint64_t* at);
   bool task_stamps_ = false;
   std::map<std::string, std::vector<double>> vals_;
+  struct Negative {
+    long count = 0;
+    double worst_s = 0.0;
+  };
+  std::map<std::string, Negative> negatives_;
   std::vector<std::pair<std::string, double>> captured_adds_;
   bool capturing_ = false, frozen_ = false;
   bool enabled_ = true;

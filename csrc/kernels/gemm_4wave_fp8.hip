@@ -448,20 +448,44 @@ __global__ void __launch_bounds__(256, 1)
     tile4<BF, false>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d);
   } else {
     // one task (prog == nullptr) or the tasks of a program, back to back
+    // (epoch: the program's claim protocol, dl::program_seq)
     int round = 0;
     for (int k = 0;; ++k) {
+      bool fixed = false;
       if (prog) {
         d.ticks = d.slice_end = prog[k].ticks;  // a uniform (scalar) load: stays in SGPRs
-        if (d.ticks == 0) {                      // the join task (the program's last)
+        fixed = d.ticks == 0 && (prog[k].work_rounds | prog[k].tail_kt) != 0;
+        if (d.ticks == 0 && !fixed) {  // the join task (the program's last)
           if (blockIdx.x == 0 && tid == 0) dl::join(prog[k].sync);
           return;
         }
       }
       if (tid == 0) {  // only thread 0 reads the clock and decides the stop
-        if (prog)
-          d.t0 = dl::agree_t0(slot, dl::program_epoch(prog, k), d.ticks, prog[k].sync);
-        else
+        if (prog) {
+          const dl::ProgSeq ps = dl::program_seq(prog, k, epoch);
+          d.t0 = dl::start_task(slot, ps.seq, ps.ep16, ps.mono, d.ticks, prog[k].sync, ps.it, k > 0).t0;
+        } else {
           d.t0 = dl::agree_t0(slot, epoch, ticks, sync);
+        }
+      }
+      if (fixed) {
+        // fixed work: work_rounds full tiles, then one tile of tail_kt K-tiles
+        // (the deadline never passes: the stop checks compare 48-bit times)
+        d.ticks = d.slice_end = 1ull << 48;
+        // the task's fields are re-read per tile (scalar loads) rather than
+        // held across the tile body, which sits at the register limit
+        for (int r = 0; r < static_cast<int>(__builtin_nontemporal_load(&prog[k].work_rounds)); ++r, ++round) {
+          tile_coords(xcd_remap((blockIdx.x + round * gridDim.x) % T, T), nt_m, nt_n, group, tm, tn);
+          tile4<BF, true>(c, A, B, C, lda, ldb, ldc, K, tm, tn, lane, d);
+        }
+        if (__builtin_nontemporal_load(&prog[k].tail_kt) > 0) {
+          tile_coords(xcd_remap((blockIdx.x + round * gridDim.x) % T, T), nt_m, nt_n, group, tm, tn);
+          tile4<BF, true>(c, A, B, C, lda, ldb, ldc, static_cast<int>(prog[k].tail_kt) * kRB, tm, tn, lane, d);
+          ++round;
+        }
+        if (tid == 0) dl::fixed_done(slot, prog[k].sync, prog[k].tend);
+        if (k + 1 >= ntasks) return;
+        continue;
       }
       for (;; ++round) {
         tile_coords(xcd_remap((blockIdx.x + round * gridDim.x) % T, T), nt_m, nt_n, group, tm, tn);
@@ -942,7 +966,7 @@ void gemm_tn_4wave_deadline(const void* A, const void* B, void* C, int M, int N,
 }
 
 void gemm_4wave_deadline_program(const void* A, const void* B, void* C, int M, int N, int K, DType in_t,
-                                 const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream) {
+                                 const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream, uint32_t epoch) {
   DLNB_REQUIRE(gemm_4wave_shape_ok(M, N, K, in_t) && in_t != DType::FP16,
                "gemm 4-wave deadline program: unsupported shape");
   DLNB_REQUIRE(tasks != nullptr && n > 0 && slot != nullptr && grid > 0, "gemm 4-wave deadline program: bad args");
@@ -954,10 +978,10 @@ void gemm_4wave_deadline_program(const void* A, const void* B, void* C, int M, i
   const DlSync none;
   if (in_t == DType::BF16)
     hipLaunchKernelGGL((gemm_4wave_fp8_kernel<true, true>), grid, 256, 0, st, a, b, c, M, N, K * esz, K * esz,
-                       K * esz, N, 8, slot, 1u, 0ull, 0ull, none, tasks, n);
+                       K * esz, N, 8, slot, epoch, 0ull, 0ull, none, tasks, n);
   else
-    hipLaunchKernelGGL((gemm_4wave_fp8_kernel<false, true>), grid, 256, 0, st, a, b, c, M, N, K, K, K, N, 8, slot, 1u,
-                       0ull, 0ull, none, tasks, n);
+    hipLaunchKernelGGL((gemm_4wave_fp8_kernel<false, true>), grid, 256, 0, st, a, b, c, M, N, K, K, K, N, 8, slot,
+                       epoch, 0ull, 0ull, none, tasks, n);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 4-wave deadline program launch failed: " << hipGetErrorString(e));
 }

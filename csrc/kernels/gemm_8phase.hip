@@ -401,20 +401,42 @@ __global__ void __launch_bounds__(512, 1)
     tile<FP8, false, BAL, UNI>(c, A, B, C, M, N, K, ldc, xcd_remap(blockIdx.x, T), d, group);
   } else {
     // one task (prog == nullptr) or the tasks of a program, back to back
+    // (epoch: the program's claim protocol, dl::program_seq)
     int round = 0;
     for (int k = 0;; ++k) {
+      bool fixed = false;
       if (prog) {
         d.ticks = d.slice_end = prog[k].ticks;  // a uniform (scalar) load: stays in SGPRs
-        if (d.ticks == 0) {                      // the join task (the program's last)
+        fixed = d.ticks == 0 && (prog[k].work_rounds | prog[k].tail_kt) != 0;
+        if (d.ticks == 0 && !fixed) {  // the join task (the program's last)
           if (blockIdx.x == 0 && tid == 0) dl::join(prog[k].sync);
           return;
         }
       }
       if (tid == 0) {  // only thread 0 reads the clock and decides the stop
-        if (prog)
-          d.t0 = dl::agree_t0(slot, dl::program_epoch(prog, k), d.ticks, prog[k].sync);
-        else
+        if (prog) {
+          const dl::ProgSeq ps = dl::program_seq(prog, k, epoch);
+          d.t0 = dl::start_task(slot, ps.seq, ps.ep16, ps.mono, d.ticks, prog[k].sync, ps.it, k > 0).t0;
+        } else {
           d.t0 = dl::agree_t0(slot, epoch, ticks, sync);
+        }
+      }
+      if (fixed) {
+        // fixed work: work_rounds full tiles, then one tile of tail_kt K-tiles
+        // (the deadline never passes: the stop checks compare 48-bit times)
+        d.ticks = d.slice_end = 1ull << 48;
+        const int rounds = static_cast<int>(prog[k].work_rounds);
+        for (int r = 0; r < rounds; ++r, ++round)
+          tile<FP8, true, BAL, UNI>(c, A, B, C, M, N, K, ldc, xcd_remap((blockIdx.x + round * gridDim.x) % T, T), d);
+        const int tkt = static_cast<int>(prog[k].tail_kt);
+        if (tkt > 0) {
+          tile<FP8, true, BAL, UNI>(c, A, B, C, M, N, tkt * kRB / esz, ldc,
+                                    xcd_remap((blockIdx.x + round * gridDim.x) % T, T), d);
+          ++round;
+        }
+        if (tid == 0) dl::fixed_done(slot, prog[k].sync, prog[k].tend);
+        if (k + 1 >= ntasks) return;
+        continue;
       }
       while (tile<FP8, true, BAL, UNI>(c, A, B, C, M, N, K, ldc, xcd_remap((blockIdx.x + round * gridDim.x) % T, T),
                                        d))
@@ -686,16 +708,17 @@ static int deadline_group() {
   return g > 0 ? g : 8;
 }
 
-// The per-tile 8-phase deadline kernel in program mode (bf16 with more than
-// 16 K-tiles, or fp8 K-tiles the 4-wave kernel does not take).
+// The per-tile 8-phase deadline kernel in program mode (bf16, or fp8 K-tiles
+// the 4-wave kernel does not take).
 bool deadline_program_8phase_ok(int M, int N, int K, DType in_t) {
-  if (!gemm_8phase_shape_ok(M, N, K, in_t)) return false;
-  const int nk = static_cast<int>(static_cast<size_t>(K) * dtype_size(in_t) / kRB);
-  return !(in_t == DType::BF16 && nk <= 16);
+  // (short-K bf16 too: one launch of its own takes the streaming kernel
+  // there, a program the per-tile one - fixed work needs a program for every
+  // stand-in shape)
+  return gemm_8phase_shape_ok(M, N, K, in_t);
 }
 
 void gemm_8phase_deadline_program(const void* A, const void* B, void* C, int M, int N, int K, DType in_t,
-                                  const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream) {
+                                  const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream, uint32_t epoch) {
   DLNB_REQUIRE(deadline_program_8phase_ok(M, N, K, in_t), "gemm 8-phase deadline program: unsupported shape");
   DLNB_REQUIRE(tasks != nullptr && n > 0 && slot != nullptr && grid > 0, "gemm 8-phase deadline program: bad args");
   hipStream_t st = static_cast<hipStream_t>(stream);
@@ -705,14 +728,14 @@ void gemm_8phase_deadline_program(const void* A, const void* B, void* C, int M, 
   const int nk = static_cast<int>(static_cast<size_t>(K) * dtype_size(in_t) / kRB);
   const DlSync none;
   if (in_t == DType::BF16 && nk % 2 == 0)
-    hipLaunchKernelGGL((gemm_8phase_kernel<false, true, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, 1u,
-                       0ull, 0ull, none, deadline_group(), tasks, n);
+    hipLaunchKernelGGL((gemm_8phase_kernel<false, true, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot,
+                       epoch, 0ull, 0ull, none, deadline_group(), tasks, n);
   else if (in_t == DType::BF16)
-    hipLaunchKernelGGL((gemm_8phase_kernel<false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, 1u, 0ull,
-                       0ull, none, deadline_group(), tasks, n);
+    hipLaunchKernelGGL((gemm_8phase_kernel<false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N, slot, epoch,
+                       0ull, 0ull, none, deadline_group(), tasks, n);
   else
     hipLaunchKernelGGL((gemm_8phase_kernel<true, true, false, true>), grid, 512, 0, st, a, b, cc, M, N, K, K, K, N,
-                       slot, 1u, 0ull, 0ull, none, deadline_group(), tasks, n);
+                       slot, epoch, 0ull, 0ull, none, deadline_group(), tasks, n);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) DLNB_THROW("gemm 8-phase deadline program launch failed: " << hipGetErrorString(e));
 }

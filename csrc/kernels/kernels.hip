@@ -9,6 +9,7 @@
 #include <cmath>
 #include <vector>
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 
 #include "deadline_sync.hpp"
@@ -130,17 +131,23 @@ __global__ void gate_signal_kernel(uint64_t* gate, const uint64_t* iter, uint32_
 }
 
 __global__ void gate_wait_kernel(const uint64_t* gate, const uint64_t* iter, uint32_t tag, uint64_t timeout_ticks,
-                                 uint64_t* timeouts) {
+                                 uint64_t* timeouts, const uint64_t* abort) {
   if (threadIdx.x == 0) {
-    const uint64_t want = dl::gate_seq(iter, tag);
+    const uint64_t it = dl::iter_of(iter);
+    const uint64_t want = dl::gate_seq_of(it, tag);
     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
     // relaxed polls, one acquire at the end: an acquire load invalidates the
-    // cache on every poll (buffer_inv), under the compute running beside it
-    while (__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
-      __builtin_amdgcn_s_sleep(2);
-      if (__builtin_amdgcn_s_memrealtime() - w0 > timeout_ticks) {
-        __hip_atomic_fetch_add(timeouts, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
+    // cache on every poll (buffer_inv), under the compute running beside it.
+    // >=: the sequence words only grow (a later replay's raise satisfies it);
+    // a poisoned iteration (a replay the abort released) does not wait.
+    if (!(iter && it == kPoisonIter)) {
+      for (unsigned k = 1; __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want; ++k) {
+        __builtin_amdgcn_s_sleep(2);
+        if ((k & 63u) == 0 && dl::abort_up(abort)) break;
+        if (__builtin_amdgcn_s_memrealtime() - w0 > timeout_ticks) {
+          __hip_atomic_fetch_add(timeouts, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -180,25 +187,33 @@ __global__ void host_signal_kernel(uint64_t* word, uint64_t value) {
 }
 
 __global__ void host_wait_kernel(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uint64_t* timeouts,
-                                 uint64_t* iter_out, uint64_t iter_value, uint64_t tight_ticks) {
+                                 uint64_t* iter_out, uint64_t iter_value, uint64_t tight_ticks, const uint64_t* abort) {
   if (threadIdx.x == 0) {
     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+    bool aborted = false;
     // relaxed polls (an acquire load would invalidate the L2's system-scope
     // lines on every poll, for the whole iteration an armed replay waits);
-    // after tight_ticks (0: never) one poll every ~4 us
-    while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < value) {
+    // after tight_ticks (0: never) one poll every ~4 us. The host's abort
+    // word ends the wait too: what this held back then runs through on a
+    // poisoned iteration word (no compute, no waits: dl::start_task).
+    for (unsigned k = 1; __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < value; ++k) {
       const uint64_t el = __builtin_amdgcn_s_memrealtime() - w0;
       if (tight_ticks != 0 && el > tight_ticks)
         __builtin_amdgcn_s_sleep(127);
       else
         __builtin_amdgcn_s_sleep(2);
+      if (((k & 63u) == 0 || (tight_ticks != 0 && el > tight_ticks)) && dl::abort_up(abort)) {
+        aborted = true;
+        break;
+      }
       if (__builtin_amdgcn_s_memrealtime() - w0 > timeout_ticks) {
         __hip_atomic_fetch_add(timeouts, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    if (iter_out) __hip_atomic_store(iter_out, iter_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (iter_out)
+      __hip_atomic_store(iter_out, aborted ? kPoisonIter : iter_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -553,17 +568,31 @@ void idle_wait(uint64_t ticks, void* stream, uint64_t* start, uint64_t* start2) 
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
+namespace {
+std::atomic<long> g_gate_signals{0};
+std::atomic<long> g_gate_fault{-1};
+}  // namespace
+
+void fail_gate_signal(long index) { g_gate_fault.store(index); }
+
 void gate_signal(uint64_t* gate, const uint64_t* iter, uint32_t tag, void* stream) {
   DLNB_REQUIRE(gate != nullptr && tag > 0 && reinterpret_cast<uintptr_t>(gate) % 16 == 0, "gate_signal: bad gate/tag");
+  const long k = g_gate_signals.fetch_add(1);
+  const long f = g_gate_fault.load();
+  if (f >= 0 && k == f) {  // fault injection: this gate is never raised
+    std::fprintf(stderr, "[dlnb] fault injection: gate signal %ld of this process is not raised\n", k);
+    std::fflush(stderr);
+    return;
+  }
   hipLaunchKernelGGL(gate_signal_kernel, 1, 64, 0, S(stream), gate, iter, tag);
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
 void gate_wait(const uint64_t* gate, const uint64_t* iter, uint32_t tag, uint64_t timeout_ticks, uint64_t* timeouts,
-               void* stream) {
+               void* stream, const uint64_t* abort) {
   DLNB_REQUIRE(gate != nullptr && timeouts != nullptr && tag > 0 && reinterpret_cast<uintptr_t>(gate) % 16 == 0,
                "gate_wait: bad gate/tag");
-  hipLaunchKernelGGL(gate_wait_kernel, 1, 64, 0, S(stream), gate, iter, tag, timeout_ticks, timeouts);
+  hipLaunchKernelGGL(gate_wait_kernel, 1, 64, 0, S(stream), gate, iter, tag, timeout_ticks, timeouts, abort);
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
@@ -604,7 +633,7 @@ void host_signal(uint64_t* word, uint64_t value, void* stream) {
 }
 
 void host_wait(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uint64_t* timeouts, void* stream,
-               uint64_t* iter_out, uint64_t iter_value) {
+               uint64_t* iter_out, uint64_t iter_value, const uint64_t* abort) {
   DLNB_REQUIRE(word != nullptr && timeouts != nullptr, "host_wait: null word");
   // Tight polling for DLNB_HOST_WAIT_TIGHT_US (50), then one poll every ~4 us:
   // an armed replay waits a whole iteration, and its wave's back-to-back
@@ -614,7 +643,7 @@ void host_wait(const uint64_t* word, uint64_t value, uint64_t timeout_ticks, uin
   static const long tight_us = env_int("DLNB_HOST_WAIT_TIGHT_US", 50);
   const uint64_t tight = tight_us > 0 ? static_cast<uint64_t>(tight_us) * 100ull : 0ull;  // 100 MHz ticks
   hipLaunchKernelGGL(host_wait_kernel, 1, 64, 0, S(stream), word, value, timeout_ticks, timeouts, iter_out, iter_value,
-                     tight);
+                     tight, abort);
   DLNB_HIP_CHECK(hipGetLastError());
 }
 
@@ -932,9 +961,9 @@ void gemm_tn_deadline(const void* A, const void* B, void* C, int M, int N, int K
 // (gemm_8phase.hip, gemm_4wave_fp8.hip)
 bool deadline_program_8phase_ok(int M, int N, int K, DType in_t);
 void gemm_8phase_deadline_program(const void* A, const void* B, void* C, int M, int N, int K, DType in_t,
-                                  const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream);
+                                  const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream, uint32_t epoch);
 void gemm_4wave_deadline_program(const void* A, const void* B, void* C, int M, int N, int K, DType in_t,
-                                 const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream);
+                                 const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream, uint32_t epoch);
 
 // The same kernel choice as gemm_tn_deadline, for the kernels with a program mode.
 namespace {
@@ -950,14 +979,29 @@ int program_kernel(int M, int N, int K, DType in_t) {
 
 bool deadline_program_ok(int M, int N, int K, DType in_t) { return program_kernel(M, N, K, in_t) != 0; }
 
+int program_ktiles(int M, int N, int K, DType in_t) {
+  if (program_kernel(M, N, K, in_t) == 0) return 0;
+  return static_cast<int>(static_cast<size_t>(K) * dtype_size(in_t) / kRowBytes);
+}
+
+// The tail tile's K-tile count keeps the kernel's K-tile pairing: the 4-wave
+// and the balanced 8-phase bodies run K-tiles in pairs; 2 for all of them.
+int program_tail_multiple(int M, int N, int K, DType in_t) { return program_kernel(M, N, K, in_t) != 0 ? 2 : 0; }
+
 void gemm_tn_deadline_program(const void* A, const void* B, void* C, int M, int N, int K, DType in_t,
-                              const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream) {
+                              const DlTask* tasks, int n, uint64_t* slot, int grid, void* stream, uint32_t epoch) {
   const int k = program_kernel(M, N, K, in_t);
   DLNB_REQUIRE(k != 0, "gemm_tn_deadline_program: no program-mode kernel for M=" << M << " N=" << N << " K=" << K);
+  DLNB_REQUIRE(epoch == 0 || (n == 1 && epoch < 65536), "gemm_tn_deadline_program: a launch epoch needs one task");
+  // every block must be resident at once (one 128-KiB-LDS block per CU): a
+  // fixed-work task waits for all of them
+  int dev = 0;
+  DLNB_HIP_CHECK(hipGetDevice(&dev));
+  DLNB_REQUIRE(grid > 0 && grid <= num_cus(dev), "gemm_tn_deadline_program: grid " << grid << " exceeds the CUs");
   if (k == 4)
-    gemm_4wave_deadline_program(A, B, C, M, N, K, in_t, tasks, n, slot, grid, stream);
+    gemm_4wave_deadline_program(A, B, C, M, N, K, in_t, tasks, n, slot, grid, stream, epoch);
   else
-    gemm_8phase_deadline_program(A, B, C, M, N, K, in_t, tasks, n, slot, grid, stream);
+    gemm_8phase_deadline_program(A, B, C, M, N, K, in_t, tasks, n, slot, grid, stream, epoch);
 }
 
 void sgd_momentum_bf16(void* param, void* mom, const void* grad, size_t n, float lr, float beta, void* stream) {

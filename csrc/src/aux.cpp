@@ -1,4 +1,5 @@
 #include "dlnb/aux.hpp"
+#include "dlnb/kernels.hpp"
 
 #include <dirent.h>
 #include <dlfcn.h>
@@ -230,6 +231,7 @@ FaultInjector::FaultInjector(int rank) {
   if (spec.empty()) return;
   int r = -1;
   long long it = 0;
+  long gate = 0;
   std::string mode = "exit", block;
   for (auto& kv : split(spec, ',')) {
     auto p = split(kv, '=');
@@ -238,6 +240,7 @@ FaultInjector::FaultInjector(int rank) {
     if (p[0] == "iter") it = std::stoll(p[1]);
     if (p[0] == "mode") mode = p[1];
     if (p[0] == "block") block = p[1];
+    if (p[0] == "gate") gate = std::stol(p[1]);
   }
   // block=TAG: only in the run whose DLNB_BLOCK is TAG (bench.py names each
   // of its child runs, so one phase of the bench can be made to hang)
@@ -246,11 +249,18 @@ FaultInjector::FaultInjector(int rank) {
     armed_ = true;
     iter_ = it;
     mode_ = mode;
+    if (mode_ == "gate") {
+      // a device-side hang: the gate-th device gate signal of the run (from
+      // the strategy's setup on, so inside the captured graph) is never raised
+      std::fprintf(stderr, "[dlnb] DLNB_INJECT_FAULT: gate signal %ld will not be raised\n", gate);
+      std::fflush(stderr);
+      kernels::fail_gate_signal(gate);
+    }
   }
 }
 
 void FaultInjector::at_iteration(long long iter, const std::function<void()>& enqueue_failing_task) {
-  if (!armed_ || iter != iter_) return;
+  if (!armed_ || iter != iter_ || mode_ == "gate") return;
   std::fprintf(stderr, "[dlnb] DLNB_INJECT_FAULT: injecting '%s' at iteration %lld\n", mode_.c_str(), iter);
   std::fflush(stderr);
   if (mode_ == "task" && enqueue_failing_task) {

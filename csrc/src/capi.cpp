@@ -1,6 +1,8 @@
 // C ABI for the Python package (loaded with ctypes from
 // dlnetbench_amd/_lib/libdlnb.so). Every function returns 0 on success and a
 // non-zero code on failure; dlnb_last_error() describes the failure.
+#include <hip/hip_runtime.h>
+
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -122,6 +124,95 @@ int dlnb_gemm_deadline_ex(const void* A, const void* B, void* C, int M, int N, i
 int dlnb_gate_signal(void* gate, unsigned tag, void* stream) {
   return guard([&] { dlnb::kernels::gate_signal(static_cast<uint64_t*>(gate), nullptr, tag, stream); });
 }
+
+// The same with the sequence's iteration read from *iter (device word) when the kernel runs.
+int dlnb_gate_signal_iter(void* gate, const void* iter, unsigned tag, void* stream) {
+  return guard([&] {
+    dlnb::kernels::gate_signal(static_cast<uint64_t*>(gate), static_cast<const uint64_t*>(iter), tag, stream);
+  });
+}
+
+// One task of a compute program (kernels::DlTask) as the tests describe it:
+// ticks > 0 a deadline task; ticks == 0 with work a fixed-work task; neither
+// the join.
+struct dlnb_task_desc {
+  unsigned long long ticks;
+  unsigned long long chain_ticks;
+  void* gate0;
+  void* gate1;
+  unsigned tag0, tag1;
+  void* tstart0;
+  void* tstart1;
+  void* done_gate;
+  unsigned done_tag;
+  unsigned work_rounds;
+  unsigned tail_kt;
+  unsigned epoch;  // index among the program's tasks
+  void* tend;
+};
+
+int dlnb_task_size() { return static_cast<int>(sizeof(dlnb::kernels::DlTask)); }
+
+// A compute program (kernels::gemm_tn_deadline_program) of n described tasks:
+// the list is copied into task_buf (device memory, >= n * dlnb_task_size()
+// bytes) once the stream is idle, then the program is launched on the stream.
+// iter / counters / abort: the device iteration word, the DlCounter words,
+// the host-mapped abort word (each optional). epoch: 0 = program claims from
+// the iteration word; else a one-task launch epoch.
+int dlnb_gemm_program(const void* A, const void* B, void* C, int M, int N, int K, int dtype, const dlnb_task_desc* d,
+                      int n, const void* iter, void* counters, const void* abort, double gate_timeout_s, int device,
+                      void* slot, void* task_buf, int grid, void* stream, unsigned epoch) {
+  return guard([&] {
+    DLNB_REQUIRE(n > 0 && d && task_buf && slot, "dlnb_gemm_program: bad arguments");
+    if (grid <= 0) grid = dlnb::kernels::num_cus(device);
+    const double hz = dlnb::kernels::wallclock_hz_nominal(device);
+    std::vector<dlnb::kernels::DlTask> ts(static_cast<size_t>(n));
+    for (int i = 0; i < n; ++i) {
+      dlnb::kernels::DlTask& t = ts[static_cast<size_t>(i)];
+      t.ticks = d[i].ticks;
+      t.epoch = d[i].epoch;
+      t.work_rounds = d[i].work_rounds;
+      t.tail_kt = d[i].tail_kt;
+      t.tend = static_cast<uint64_t*>(d[i].tend);
+      t.sync.chain = static_cast<uint32_t>(d[i].chain_ticks);
+      t.sync.gate[0] = static_cast<const uint64_t*>(d[i].gate0);
+      t.sync.gate[1] = static_cast<const uint64_t*>(d[i].gate1);
+      t.sync.tag[0] = d[i].tag0;
+      t.sync.tag[1] = d[i].tag1;
+      t.sync.tstart[0] = static_cast<uint64_t*>(d[i].tstart0);
+      t.sync.tstart[1] = static_cast<uint64_t*>(d[i].tstart1);
+      t.sync.done_gate = static_cast<uint64_t*>(d[i].done_gate);
+      t.sync.done_tag = d[i].done_tag;
+      t.sync.iter = static_cast<const uint64_t*>(iter);
+      t.sync.counters = static_cast<uint64_t*>(counters);
+      t.sync.abort = static_cast<const uint64_t*>(abort);
+      t.sync.gate_timeout = static_cast<uint64_t>(gate_timeout_s * hz);
+    }
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (hipStreamSynchronize(st) != hipSuccess) DLNB_THROW("dlnb_gemm_program: stream synchronize failed");
+    if (hipMemcpy(task_buf, ts.data(), ts.size() * sizeof(dlnb::kernels::DlTask), hipMemcpyHostToDevice) != hipSuccess)
+      DLNB_THROW("dlnb_gemm_program: task list copy failed");
+    dlnb::kernels::gemm_tn_deadline_program(A, B, C, M, N, K, static_cast<dlnb::DType>(dtype),
+                                            static_cast<const dlnb::kernels::DlTask*>(task_buf), n,
+                                            static_cast<uint64_t*>(slot), grid, stream, epoch);
+  });
+}
+
+int dlnb_program_ktiles(int M, int N, int K, int dtype) {
+  return dlnb::kernels::program_ktiles(M, N, K, static_cast<dlnb::DType>(dtype));
+}
+
+// Host-mapped, device-visible words (an abort word for the tests): the host
+// pointer (the device pointer is returned in *dev).
+void* dlnb_host_words(int n, void** dev) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, static_cast<size_t>(n) * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+    return nullptr;
+  std::memset(p, 0, static_cast<size_t>(n) * 8);
+  if (dev && hipHostGetDevicePointer(dev, p, 0) != hipSuccess) *dev = p;
+  return p;
+}
+void dlnb_host_words_free(void* p) { (void)hipHostFree(p); }
 
 int dlnb_gemm_narrow_nf(int M, int N, int cus) { return dlnb::kernels::gemm_narrow_nf(M, N, cus); }
 

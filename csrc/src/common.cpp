@@ -41,6 +41,11 @@ DType parse_dtype(const std::string& s0) {
   DLNB_THROW("unknown dtype '" << s0 << "'");
 }
 
+std::string& last_error_message() {
+  thread_local std::string m;
+  return m;
+}
+
 std::string trim(const std::string& s) {
   size_t b = 0, e = s.size();
   while (b < e && std::isspace(static_cast<unsigned char>(s[b]))) ++b;

@@ -70,10 +70,18 @@ class CpuCompute : public ComputeEngine {
 
 // ------------------------------------------------------------------ GPU
 
-struct GemmLevel {
-  int M;
-  double us;     // measured duration of one launch (back-to-back)
-  double flops;  // 2*M*N*K
+// Fixed-work calibration of the program kernel: one full-K round (every block
+// of the grid one 256 x 256 tile) and one K-tile of the tail tile.
+struct FixedCal {
+  double round_us = 0.0;
+  double ktile_us = 0.0;
+};
+
+// The work of one fixed-work task: full-K rounds plus a tail tile of tail_kt
+// K-tiles per block, and its uncontended duration.
+struct FixedWork {
+  uint32_t rounds = 0, tail_kt = 0;
+  double us = 0.0;
 };
 
 class GpuCompute : public ComputeEngine {
@@ -88,6 +96,7 @@ class GpuCompute : public ComputeEngine {
     gate_timeout_ticks_ = static_cast<uint64_t>(static_cast<double>(env_int("DLNB_GATE_TIMEOUT_S", 60)) *
                                                 kernels::wallclock_hz_nominal(dev.index()));
     dtype_ = shape.dtype == DType::FP8_E4M3 ? DType::FP8_E4M3 : DType::BF16;
+    fixed_ = mode_ == ComputeMode::GemmWork || mode_ == ComputeMode::Flops;
     // The stand-in is the layer's FFN down projection, C[tokens, hidden] =
     // A[tokens, ffn] . W[hidden, ffn]^T: its long K (the FFN width) keeps
     // the per-tile pipeline fill / drain of the persistent kernel small. At
@@ -111,17 +120,17 @@ class GpuCompute : public ComputeEngine {
       };
       while (K_ > 512 && share > 0 && bytes(K_) > share) K_ = std::max(512, (K_ / 2 + kmul - 1) / kmul * kmul);
     }
-    // GEMM operands for every GEMM mode; the launch-time calibration only for
-    // the fixed-work modes (a deadline task lasts its table time whatever a
-    // launch costs, so the gemm mode skips the ~0.6 s of measuring).
+    // GEMM operands for every GEMM mode
     if (mode_ != ComputeMode::Sleep && mode_ != ComputeMode::Spin) alloc_operands();
-    if (mode_ == ComputeMode::GemmWork || mode_ == ComputeMode::Flops) calibrate();
-    if (mode_ == ComputeMode::Gemm) {
+    if (mode_ == ComputeMode::Gemm || fixed_) {
       // one 64-byte line per compute stream; the counters (DlCounter)
       slots_ = dev_.alloc(kSlots * 64);
       counters_ = dev_.alloc(kernels::kNumCounters * sizeof(uint64_t));
-      // compute programs' task lists (never allocated while a stream captures)
+      // compute programs' task lists: a device ring (lists captured into a
+      // graph, uploaded after the capture) and a host-mapped ring (lists
+      // launched at once: written by the host, read by the kernel, no copy)
       prog_dev_ = dev_.alloc(kProgTasks * sizeof(kernels::DlTask));
+      prog_host_ = reinterpret_cast<kernels::DlTask*>(dev_.alloc_stamps(kProgTasks * sizeof(kernels::DlTask) / 8));
       auto zs = dev_.create_stream(false);
       dev_.memset_async(slots_.data(), 0, kSlots * 64, *zs);
       dev_.memset_async(counters_.data(), 0, kernels::kNumCounters * sizeof(uint64_t), *zs);
@@ -132,6 +141,12 @@ class GpuCompute : public ComputeEngine {
       // room (with the whole chip taken, a comm kernel only starts at a
       // compute boundary, and overlap collapses).
       grid_ = std::max(1, cus_ - std::max(0, shape.comm_cus));
+      // Fixed work waits for every block of its grid between two tasks, so
+      // ranks sharing the device split the free CUs: all their grids must be
+      // resident at once.
+      if (fixed_) grid_ = std::max(1, grid_ / std::max(1, shape.ranks_on_device));
+    }
+    if (mode_ == ComputeMode::Gemm) {
       // One launch per task by default. Cutting a task into relaunched
       // slices (DLNB_GEMM_SLICE_US > 0) was meant to give collectives CUs at
       // slice boundaries, which the comm_cus reservation already does; at
@@ -144,14 +159,26 @@ class GpuCompute : public ComputeEngine {
       // for it) serialises behind it - 8 loopback ranks of the llama3_8b FSDP
       // config ran 459 vs 317 ms per iteration (profiles/loopback_w8_r3.md).
       slice_us_ = static_cast<double>(env_int("DLNB_GEMM_SLICE_US", shape.ranks_on_device > 1 ? 500 : 0));
+    } else {
+      slice_us_ = 0.0;
     }
+    if (fixed_) {
+      DLNB_REQUIRE(kernels::deadline_program_ok(kMmax, N_, K_, dtype_),
+                   "fixed-work compute: no program kernel for the stand-in shape " << kMmax << "x" << N_ << "x" << K_);
+      calibrate();
+    }
+  }
+  ~GpuCompute() override {
+    // (a task list a kernel may still read is never freed: the process is going away)
+    if (prog_host_ && !dev_.abort_raised())
+      dev_.free_stamps(reinterpret_cast<uint64_t*>(prog_host_), kProgTasks * sizeof(kernels::DlTask) / 8);
   }
 
   void reset_clocks(Stream& s) override {
-    if (mode_ == ComputeMode::Gemm) dev_.memset_async(slots_.data(), 0, kSlots * 64, s);
+    if (slots_.data()) dev_.memset_async(slots_.data(), 0, kSlots * 64, s);
   }
   void reset_slot(Stream& s) override {
-    if (mode_ != ComputeMode::Gemm) return;
+    if (!slots_.data()) return;
     auto it = slot_of_.find(&s);
     if (it != slot_of_.end()) dev_.memset_async(slots_.as<uint64_t>() + it->second * 8, 0, 64, s);
   }
@@ -163,7 +190,7 @@ class GpuCompute : public ComputeEngine {
     dev_.memset_async(c + kernels::kAbsorbedTicks, 0, 2 * sizeof(uint64_t), s);
   }
   bool begin_program(Stream& s) override {
-    if (mode_ != ComputeMode::Gemm || slice_us_ > 0 || env_int("DLNB_COMPUTE_PROGRAMS", 1) == 0 ||
+    if ((mode_ != ComputeMode::Gemm && !fixed_) || slice_us_ > 0 || env_int("DLNB_COMPUTE_PROGRAMS", 1) == 0 ||
         !kernels::deadline_program_ok(kMmax, N_, K_, dtype_))
       return false;
     Program& p = programs_[&s];
@@ -173,12 +200,12 @@ class GpuCompute : public ComputeEngine {
     p.tasks.clear();
     return true;
   }
-  void end_program(Stream& s) override {
+  void end_program(Stream& s, bool join_ok) override {
     auto it = programs_.find(&s);
     if (it == programs_.end() || !it->second.open) return;
     Program& p = it->second;
     auto j = joins_.find(&s);
-    if (j != joins_.end() && !p.tasks.empty()) {
+    if (j != joins_.end() && !p.tasks.empty() && join_ok) {
       // the join task(s): up to two gates each, the last one stores the done word
       const Join& jn = j->second;
       size_t g = 0;
@@ -187,6 +214,7 @@ class GpuCompute : public ComputeEngine {
         t.sync.iter = dev_.iter_word();
         t.sync.counters = counters_.as<uint64_t>();
         t.sync.gate_timeout = gate_timeout_ticks_;
+        t.sync.abort = dev_.abort_word();
         for (int i = 0; i < 2 && g < jn.gates.size(); ++i, ++g) {
           t.sync.gate[i] = jn.gates[g];
           t.sync.tag[i] = jn.tag;
@@ -202,12 +230,16 @@ class GpuCompute : public ComputeEngine {
     p.open = false;
   }
   void set_lane_join(Stream& s, const std::vector<uint64_t*>& gates, uint32_t tag, uint64_t* host_done) override {
-    if (mode_ != ComputeMode::Gemm) return;
+    if (mode_ != ComputeMode::Gemm && !fixed_) return;
     joins_[&s] = Join{gates, tag, host_done};
     joined_.erase(&s);
     lane_stats_.clear();
   }
   bool program_joined(Stream& s) override { return joined_.count(&s) != 0; }
+  long programs_on(Stream& s) override {
+    auto it = program_count_.find(&s);
+    return it == program_count_.end() ? 0 : it->second;
+  }
   void set_gate_timeout(double s) override {
     gate_timeout_ticks_ = static_cast<uint64_t>(s * kernels::wallclock_hz_nominal(dev_.index()));
   }
@@ -238,20 +270,30 @@ class GpuCompute : public ComputeEngine {
     out.absorbed_s = static_cast<double>(v[kernels::kAbsorbedTicks]) / hz();
     out.wait_timeouts = static_cast<double>(v[kernels::kWaitTimeouts]);
     out.gate_timeouts = static_cast<double>(v[kernels::kGateTimeouts]);
+    out.aborted = static_cast<double>(v[kernels::kAborted]);
+    out.late_blocks = static_cast<double>(v[kernels::kLateBlocks]);
     return true;
   }
 
-  bool stamps_task_start() const override {
-    return mode_ == ComputeMode::Gemm || mode_ == ComputeMode::Sleep || mode_ == ComputeMode::Spin;
+  // Every GPU mode's kernels stamp their own start (deadline / idle / spin:
+  // the kernel; fixed work: the program task, which also stamps its end).
+  bool stamps_task_start() const override { return true; }
+  uint64_t task_ticks(double us) const override { return fixed_ ? 0 : ticks(us * scale_); }
+  const uint64_t* last_task_end(Stream& s) override {
+    auto it = last_end_.find(&s);
+    return it == last_end_.end() ? nullptr : it->second;
   }
-  uint64_t task_ticks(double us) const override { return ticks(us * scale_); }
   void run(Stream& s, double us, double flops) override { run_stamped(s, us, flops, nullptr); }
 
   void run_chained(Stream& s, double us, double flops, uint64_t* start, Event* done) override {
+    if (fixed_) {
+      fixed_task(s, us, flops, start, {}, done);
+      return;
+    }
     if (mode_ == ComputeMode::Gemm && us * scale_ >= 20.0 && chain_live_[slot_for(s)]) {
       note_task(s, us * scale_);
       if (stall_timers_ && !start) start = stall_timers_->task_slot(s);
-      StartNote note{stall_timers_, s, start, ticks(us * scale_)};
+      StartNote note{stall_timers_, s, start, ticks(us * scale_), nullptr};
       kernels::DlSync sync;
       sync.tstart[0] = start;
       sync.tstart[1] = extra_start_;
@@ -264,10 +306,10 @@ class GpuCompute : public ComputeEngine {
     if (done) s.record(*done);
   }
 
-  bool gates_task(double us) const override { return mode_ == ComputeMode::Gemm && us * scale_ >= 20.0; }
+  bool gates_task(double us) const override { return fixed_ || (mode_ == ComputeMode::Gemm && us * scale_ >= 20.0); }
 
   int make_gate() override {
-    DLNB_REQUIRE(mode_ == ComputeMode::Gemm, "gates need the gemm (deadline) compute");
+    DLNB_REQUIRE(mode_ == ComputeMode::Gemm || fixed_, "gates need the gemm (deadline) or fixed-work GPU compute");
     gates_.push_back(dev_.alloc_gate());
     gate_tag_.push_back(0);
     return static_cast<int>(gates_.size()) - 1;
@@ -282,23 +324,27 @@ class GpuCompute : public ComputeEngine {
     const uint32_t tag = gate_tag_.at(gate);
     DLNB_REQUIRE(tag != 0, "wait_gate: gate " << gate << " was never signalled");
     kernels::gate_wait(gates_.at(gate), dev_.iter_word(), tag, ticks(timeout_us),
-                       counters_.as<uint64_t>() + kernels::kWaitTimeouts, s.native());
+                       counters_.as<uint64_t>() + kernels::kWaitTimeouts, s.native(), dev_.abort_word());
   }
 
   void run_gated(Stream& s, double us, double flops, const std::vector<int>& gates, uint64_t* start,
                  bool chain, Event* done) override {
     DLNB_REQUIRE(gates_task(us), "run_gated: the task cannot wait on gates (see gates_task)");
     DLNB_REQUIRE(gates.size() <= 2, "run_gated: at most 2 gates per task");
-    (void)flops;
     kernels::DlSync sync;
     for (size_t i = 0; i < gates.size(); ++i) {
       sync.gate[i] = gates_.at(gates[i]);
       sync.tag[i] = gate_tag_.at(gates[i]);
       DLNB_REQUIRE(sync.tag[i] != 0, "run_gated: gate " << gates[i] << " was never signalled");
     }
+    if (fixed_) {
+      fixed_task(s, us, flops, start, sync, done);
+      ++gated_;
+      return;
+    }
     note_task(s, us * scale_);
     if (stall_timers_ && !start) start = stall_timers_->task_slot(s);
-    StartNote note{stall_timers_, s, start, ticks(us * scale_)};
+    StartNote note{stall_timers_, s, start, ticks(us * scale_), nullptr};
     sync.tstart[0] = start;
     sync.tstart[1] = extra_start_;
     extra_start_ = nullptr;
@@ -315,11 +361,6 @@ class GpuCompute : public ComputeEngine {
     auto it = programs_.find(&s);
     if (it == programs_.end() || it->second.tasks.empty()) return;
     std::vector<kernels::DlTask>& ts = it->second.tasks;
-    const size_t n = ts.size();
-    DLNB_REQUIRE(n <= kProgTasks, "compute program of " << n << " tasks exceeds the ring (" << kProgTasks << ")");
-    if (prog_next_ + n > kProgTasks) prog_next_ = 0;  // (a program runs before the ring comes round again)
-    kernels::DlTask* dst = prog_dev_.as<kernels::DlTask>() + prog_next_;
-    prog_next_ += n;
     // A program whose first task waits for gates (FSDP: the iteration's first
     // all-gather) is launched only once they are up, behind one-wave gate
     // waits: resident and waiting, its grid would hold the CUs that
@@ -328,25 +369,24 @@ class GpuCompute : public ComputeEngine {
     for (int i = 0; i < 2; ++i)
       if (ts[0].sync.gate[i])
         kernels::gate_wait(ts[0].sync.gate[i], dev_.iter_word(), ts[0].sync.tag[i], gate_timeout_ticks_,
-                           counters_.as<uint64_t>() + kernels::kWaitTimeouts, s.native());
-    if (dev_.capturing(s)) {
-      uploads_.push_back(Upload{dst, ts});  // written by after_capture(), before the first replay
-    } else {
-      // not captured: the list goes in with the launch (pageable source: the copy completes before it returns)
-      dev_.copy_async(dst, ts.data(), n * sizeof(kernels::DlTask), s);
-      s.synchronize();
-    }
-    kernels::gemm_tn_deadline_program(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, dst, static_cast<int>(n),
-                                      slot_for(s), grid_, s.native());
+                           counters_.as<uint64_t>() + kernels::kWaitTimeouts, s.native(), dev_.abort_word());
+    const kernels::DlTask* dst = place_tasks(s, ts);
+    kernels::gemm_tn_deadline_program(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, dst,
+                                      static_cast<int>(ts.size()), slot_for(s), grid_, s.native(), 0u);
     ++programs_launched_;
-    program_tasks_ += static_cast<long>(n);
+    ++program_count_[&s];
+    program_tasks_ += static_cast<long>(ts.size());
     ts.clear();
   }
 
   void run_stamped(Stream& s, double us, double flops, uint64_t* start) override {
+    if (fixed_) {
+      fixed_task(s, us, flops, start, {}, nullptr);
+      return;
+    }
     note_task(s, us * scale_);
     if (stall_timers_ && !start) start = stall_timers_->task_slot(s);
-    StartNote note{stall_timers_, s, start, ticks(std::max(0.0, us * scale_))};
+    StartNote note{stall_timers_, s, start, ticks(std::max(0.0, us * scale_)), nullptr};
     double d = us * scale_;
     // a task that is not a deadline kernel cannot join the open program
     if (mode_ == ComputeMode::Gemm && d < 20.0) flush_program(s);
@@ -365,58 +405,37 @@ class GpuCompute : public ComputeEngine {
       }
       return;
     }
-    if (mode_ == ComputeMode::Gemm) {
-      // Fixed duration, real MFMA work: persistent deadline GEMM (the stand-in
-      // keeps the matrix cores and HBM busy for exactly the table's time, so
-      // DVFS or contention changes how much work is done, not how long).
-      if (d <= 0) {
-        if (start) dev_.stamp(s, start);
-        if (extra_start_) dev_.stamp(s, extra_start_);
-        extra_start_ = nullptr;
-        return;
-      }
-      if (d < 20.0) {
-        kernels::busy_spin(ticks(d), cus_, s.native(), start, extra_start_);
-        extra_start_ = nullptr;
-        return;
-      }
-      kernels::DlSync sync;
-      sync.tstart[0] = start;
-      sync.tstart[1] = extra_start_;
+    // Fixed duration, real MFMA work: persistent deadline GEMM (the stand-in
+    // keeps the matrix cores and HBM busy for exactly the table's time, so
+    // DVFS or contention changes how much work is done, not how long).
+    if (d <= 0) {
+      if (start) dev_.stamp(s, start);
+      if (extra_start_) dev_.stamp(s, extra_start_);
       extra_start_ = nullptr;
-      deadline_task(s, d, sync, false);
       return;
     }
-    // Fixed-work modes from here on: bracket the task with device stamps.
-    const int tok = task_timers_ && d > 0 ? task_timers_->begin(s) : -1;
-    if (mode_ == ComputeMode::Flops) {
-      double f = flops * scale_;
-      for (const auto& lv : levels_) {
-        long n = static_cast<long>(std::floor(f / lv.flops));
-        for (long i = 0; i < n; ++i) launch(lv.M, s);
-        f -= static_cast<double>(n) * lv.flops;
-      }
-      end_task(tok, s, flops * scale_ / levels_.front().flops * levels_.front().us);
+    if (d < 20.0) {
+      kernels::busy_spin(ticks(d), cus_, s.native(), start, extra_start_);
+      extra_start_ = nullptr;
       return;
     }
-    // gemm-work: greedy fill of the duration with calibrated launches, then spin.
-    double rem = d;
-    for (const auto& lv : levels_) {
-      long n = static_cast<long>(std::floor(rem / lv.us));
-      for (long i = 0; i < n; ++i) launch(lv.M, s);
-      rem -= static_cast<double>(n) * lv.us;
-    }
-    if (rem > 1.0) kernels::busy_spin(ticks(rem), cus_, s.native());
-    end_task(tok, s, d);
+    kernels::DlSync sync;
+    sync.tstart[0] = start;
+    sync.tstart[1] = extra_start_;
+    extra_start_ = nullptr;
+    deadline_task(s, d, sync, false);
   }
 
   void set_task_timers(TimerSet* t) override {
-    if (mode_ == ComputeMode::GemmWork || mode_ == ComputeMode::Flops) {
-      task_timers_ = t;
-    } else if (t && stamps_task_start() && env_int("DLNB_TASK_STAMP_TIMERS", 1) != 0) {
-      // every task's own start stamp feeds the stall timers (TimerSet::stall_before_task)
+    // every task's own start (and, fixed work, end) stamp feeds the stall
+    // timers (TimerSet::stall_before_task) and the fixed-work task times
+    // (compute_task_time / compute_task_table: compute_stretch)
+    task_timers_ = fixed_ ? t : nullptr;
+    if (t && env_int("DLNB_TASK_STAMP_TIMERS", 1) != 0) {
       stall_timers_ = t;
       t->set_task_stamps(true);
+    } else if (fixed_) {
+      stall_timers_ = t;  // fixed work needs its end slots even without the stall timers
     }
   }
 
@@ -428,7 +447,7 @@ class GpuCompute : public ComputeEngine {
     j["wallclock_hz_nominal"] = kernels::wallclock_hz_nominal(dev_.index());
     j["wallclock_uncertainty_ppm"] = kernels::wallclock_uncertainty_ppm(dev_.index());
     j["num_cus"] = cus_;
-    if (mode_ == ComputeMode::Gemm) {
+    if (mode_ == ComputeMode::Gemm || fixed_) {
       j["deadline_grid"] = grid_;
       j["comm_reserved_cus"] = cus_ - grid_;
       j["deadline_slice_us"] = slice_us_;
@@ -444,16 +463,18 @@ class GpuCompute : public ComputeEngine {
       j["gemm_N"] = N_;
       j["gemm_K"] = K_;
     }
-    if (!levels_.empty()) {
-      Json lv = Json::array();
-      for (const auto& l : levels_) {
-        Json e = Json::object();
-        e["M"] = l.M;
-        e["us_per_launch"] = l.us;
-        e["tflops"] = l.flops / (l.us * 1e-6) / 1e12;
-        lv.push_back(e);
-      }
-      j["gemm_levels"] = lv;
+    if (fixed_) {
+      // the fixed-work unit: one full-K round of 256 x 256 tiles over the grid
+      // and one K-tile of a tail tile, measured alone at start-up
+      Json f = Json::object();
+      f["round_us"] = cal_.round_us;
+      f["ktile_us"] = cal_.ktile_us;
+      f["grid"] = grid_;
+      f["ktiles_per_tile"] = nk_;
+      f["tflops"] = round_flops() / (cal_.round_us * 1e-6) / 1e12;
+      f["tasks"] = fixed_tasks_;
+      f["calibration"] = cal_given_ ? "DLNB_FIXED_WORK_CAL" : "measured";
+      j["fixed_work"] = f;
     }
     return j;
   }
@@ -466,6 +487,29 @@ class GpuCompute : public ComputeEngine {
     return hz_;
   }
 
+  // Where a task list goes: captured into a graph, the device ring (written
+  // by after_capture, before the first replay); launched at once, the
+  // host-mapped ring (the kernel reads it where the host wrote it).
+  const kernels::DlTask* place_tasks(Stream& s, const std::vector<kernels::DlTask>& ts) {
+    const size_t n = ts.size();
+    DLNB_REQUIRE(n <= kProgTasks, "compute program of " << n << " tasks exceeds the ring (" << kProgTasks << ")");
+    if (dev_.capturing(s)) {
+      if (prog_next_ + n > kProgTasks) prog_next_ = 0;  // (a program runs before the ring comes round again)
+      kernels::DlTask* dst = prog_dev_.as<kernels::DlTask>() + prog_next_;
+      prog_next_ += n;
+      uploads_.push_back(Upload{dst, ts});
+      return dst;
+    }
+    // (16384 entries: an iteration's launches - the host synchronises with
+    // every iteration - never come round to a list still being read)
+    if (host_next_ + n > kProgTasks) host_next_ = 0;
+    kernels::DlTask* dst = prog_host_ + host_next_;
+    host_next_ += n;
+    std::copy(ts.begin(), ts.end(), dst);
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    return dst;
+  }
+
   // One deadline task of d us on s (every slice launch carries the same
   // epoch; the kernels agree its start through the stream's slot line,
   // csrc/kernels/deadline_sync.hpp). chain: start at the stream's previous
@@ -474,15 +518,11 @@ class GpuCompute : public ComputeEngine {
   // gate is raised by the task's own kernel (DlSync::done_gate, last launch).
   void deadline_task(Stream& s, double d, kernels::DlSync sync, bool chain, Event* done = nullptr) {
     uint64_t* slot = slot_for(s);
-    uint32_t& ep0 = epoch_[slot];
-    ep0 = ep0 % 32767 + 1;
-    // 32768..65534 (never 0: a fresh slot reads as epoch 0); program tasks
-    // take 1..32767 from the iteration word (deadline_sync.hpp program_epoch)
-    const uint32_t ep = 32767 + ep0;
     sync.chain = chain ? absorb_ticks_ : 0u;
     sync.counters = counters_.as<uint64_t>();
     sync.iter = dev_.iter_word();
     sync.gate_timeout = gate_timeout_ticks_;
+    sync.abort = dev_.abort_word();
     uint64_t* dgate = nullptr;
     uint32_t dtag = 0;
     const bool folded = done && dev_.arm_gate_record(*done, s, &dgate, &dtag);
@@ -502,9 +542,11 @@ class GpuCompute : public ComputeEngine {
       chain_live_[slot] = true;
       return;
     }
+    const uint32_t ep = next_epoch(slot);
     const uint64_t slice = slice_us_ > 0 ? std::max<uint64_t>(ticks(slice_us_), 1) : total;
     for (uint64_t end = slice;; end += slice) {
       kernels::DlSync ls = end == slice ? sync : kernels::DlSync();
+      ls.abort = sync.abort;
       if (end >= total && folded) {
         ls.done_gate = dgate;
         ls.done_tag = dtag;
@@ -518,16 +560,87 @@ class GpuCompute : public ComputeEngine {
     chain_live_[slot] = true;
   }
 
-  // table_us: the task's uncontended duration (gemm-work: the table time;
-  // flops: the calibrated time of its FLOPs at the largest GEMM level).
-  void end_task(int tok, Stream& s, double table_us) {
-    if (tok < 0) return;
-    task_timers_->end(tok, s, "compute_task_time");
-    task_timers_->add("compute_task_table", table_us * 1e-6);
+  // A launch epoch of its own: 32768..65534 (never 0: a fresh slot reads as
+  // epoch 0); program tasks take 1..32767 from the iteration word.
+  uint32_t next_epoch(uint64_t* slot) {
+    uint32_t& ep0 = epoch_[slot];
+    ep0 = ep0 % 32767 + 1;
+    return 32767 + ep0;
   }
 
-  void launch(int M, Stream& s) {
-    kernels::gemm_tn(A_.data(), B_.data(), C_.data(), M, N_, K_, K_, K_, N_, dtype_, s.native());
+  // ---- fixed work (gemm-work, flops): program tasks of a given amount of
+  // MFMA work that stamp their own start and end (no stamp kernels).
+  double round_flops() const { return static_cast<double>(grid_) * 2.0 * kTile * kTile * K_; }
+  FixedWork size_work(double us, double flops) const {
+    FixedWork w;
+    double units;  // in full-K rounds
+    if (mode_ == ComputeMode::Flops)
+      units = std::max(0.0, flops * scale_) / round_flops();
+    else
+      units = std::max(0.0, us * scale_) / cal_.round_us;
+    w.rounds = static_cast<uint32_t>(std::floor(units));
+    // the rest as a tail tile of an even K-tile count (the kernels' pairing)
+    const double kt = (units - w.rounds) * nk_;
+    uint32_t tail = static_cast<uint32_t>(std::lround(kt / tail_mul_)) * tail_mul_;
+    if (tail >= static_cast<uint32_t>(nk_)) {
+      ++w.rounds;
+      tail = 0;
+    }
+    w.tail_kt = tail;
+    if (w.rounds == 0 && w.tail_kt == 0 && units > 0) w.tail_kt = tail_mul_;
+    w.us = w.rounds * cal_.round_us + w.tail_kt * cal_.ktile_us;
+    return w;
+  }
+
+  void fixed_task(Stream& s, double us, double flops, uint64_t* start, kernels::DlSync sync, Event* done) {
+    const FixedWork w = size_work(us, flops);
+    note_task(s, w.us);
+    if (stall_timers_ && !start) start = stall_timers_->slot();
+    uint64_t* end = stall_timers_ ? stall_timers_->slot() : nullptr;
+    sync.tstart[0] = start;
+    sync.tstart[1] = extra_start_;
+    extra_start_ = nullptr;
+    sync.counters = counters_.as<uint64_t>();
+    sync.iter = dev_.iter_word();
+    sync.gate_timeout = gate_timeout_ticks_;
+    sync.abort = dev_.abort_word();
+    uint64_t* dgate = nullptr;
+    uint32_t dtag = 0;
+    const bool folded = done && dev_.arm_gate_record(*done, s, &dgate, &dtag);
+    sync.done_gate = dgate;
+    sync.done_tag = dtag;
+    kernels::DlTask t;
+    t.sync = sync;
+    t.ticks = 0;
+    t.work_rounds = w.rounds;
+    t.tail_kt = w.tail_kt;
+    t.tend = end;
+    auto pit = programs_.find(&s);
+    if (pit != programs_.end() && pit->second.open) {
+      DLNB_REQUIRE(folded || !done, "a program task's done event needs gate events");
+      DLNB_REQUIRE(pit->second.index < 4096, "more than 4096 program tasks per iteration on one stream");
+      t.epoch = pit->second.index++;
+      pit->second.tasks.push_back(t);
+    } else {
+      // a launch of its own (a one-task program with an epoch of its own):
+      // the gates' one-wave waits first, as for a program's first task
+      for (int i = 0; i < 2; ++i)
+        if (t.sync.gate[i])
+          kernels::gate_wait(t.sync.gate[i], dev_.iter_word(), t.sync.tag[i], gate_timeout_ticks_,
+                             counters_.as<uint64_t>() + kernels::kWaitTimeouts, s.native(), dev_.abort_word());
+      uint64_t* slot = slot_for(s);
+      const kernels::DlTask* dst = place_tasks(s, {t});
+      kernels::gemm_tn_deadline_program(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, dst, 1, slot, grid_,
+                                        s.native(), next_epoch(slot));
+      if (done && !folded) s.record(*done);
+    }
+    ++fixed_tasks_;
+    if (end) last_end_[&s] = end;
+    if (stall_timers_) stall_timers_->task_started(s, start, 0, end);
+    if (task_timers_ && start && end) {
+      task_timers_->pair(start, end, "compute_task_time");
+      task_timers_->add("compute_task_table", (mode_ == ComputeMode::Flops ? w.us : us * scale_) * 1e-6);
+    }
   }
 
   uint64_t* slot_for(Stream& s) {
@@ -555,58 +668,74 @@ class GpuCompute : public ComputeEngine {
     s->synchronize();
   }
 
+  // Fixed work's unit costs with nothing else running: one-task programs of
+  // R full-K rounds (R = 20 and 60: the difference removes the launch and
+  // the first tile's ramp) and of a tail of nk / 2 K-tiles after one round.
   void calibrate() {
-    const int Mmax = kMmax;
-    auto s = dev_.create_stream(false);
-    // DLNB_GEMM_LEVELS="M:us,M:us,..." reuses an earlier calibration (the
-    // report's compute.gemm_levels) instead of measuring: a fixed-work run
+    nk_ = kernels::program_ktiles(kMmax, N_, K_, dtype_);
+    tail_mul_ = static_cast<uint32_t>(std::max(1, kernels::program_tail_multiple(kMmax, N_, K_, dtype_)));
+    // DLNB_FIXED_WORK_CAL="round_us:ktile_us" reuses an earlier calibration
+    // (the report's compute.fixed_work) instead of measuring: a fixed-work run
     // beside other jobs (tools/interference.py) must do the work it would do
     // alone, not what a contended calibration says fits the table time.
-    const std::string given = env_or("DLNB_GEMM_LEVELS", "");
+    const std::string given = env_or("DLNB_FIXED_WORK_CAL", "");
     if (!given.empty()) {
-      for (const auto& item : split(given, ',')) {
-        const auto kv = split(trim(item), ':');
-        DLNB_REQUIRE(kv.size() == 2, "DLNB_GEMM_LEVELS: expected M:us entries, got '" << item << "'");
-        const int M = std::stoi(kv[0]);
-        const double us = std::stod(kv[1]);
-        DLNB_REQUIRE(M > 0 && M <= Mmax && M % 256 == 0 && us > 0, "DLNB_GEMM_LEVELS: bad entry '" << item << "'");
-        levels_.push_back(GemmLevel{M, us, 2.0 * M * static_cast<double>(N_) * K_});
-      }
-      std::sort(levels_.begin(), levels_.end(), [](const GemmLevel& a, const GemmLevel& b) { return a.M > b.M; });
-      s->synchronize();
+      const auto kv = split(trim(given), ':');
+      DLNB_REQUIRE(kv.size() == 2, "DLNB_FIXED_WORK_CAL: expected round_us:ktile_us, got '" << given << "'");
+      cal_.round_us = std::stod(kv[0]);
+      cal_.ktile_us = std::stod(kv[1]);
+      DLNB_REQUIRE(cal_.round_us > 0 && cal_.ktile_us > 0, "DLNB_FIXED_WORK_CAL: bad values '" << given << "'");
+      cal_given_ = true;
       return;
     }
+    auto s = dev_.create_stream(false);
     auto e0 = dev_.create_event(true);
     auto e1 = dev_.create_event(true);
-    // Run ~0.3 s first so the measurement sees the sustained (DVFS-settled)
-    // clock rather than the cold-start boost.
-    for (int i = 0; i < 400; ++i) launch(Mmax, *s);
-    s->synchronize();
-    for (int M : {8192, 1024, 256}) {
-      // Size the batch to ~40 ms of work.
+    uint64_t* slot = slot_for(*s);
+    auto time_task = [&](uint32_t rounds, uint32_t tail) {
+      kernels::DlTask t;
+      t.sync.counters = counters_.as<uint64_t>();
+      t.sync.abort = dev_.abort_word();
+      t.work_rounds = rounds;
+      t.tail_kt = tail;
+      const kernels::DlTask* dst = place_tasks(*s, {t});
       s->record(*e0);
-      for (int i = 0; i < 3; ++i) launch(M, *s);
+      kernels::gemm_tn_deadline_program(A_.data(), B_.data(), C_.data(), kMmax, N_, K_, dtype_, dst, 1, slot, grid_,
+                                        s->native(), next_epoch(slot));
       s->record(*e1);
       s->synchronize();
-      double probe = dev_.elapsed_ms(*e0, *e1) / 3.0;
-      int reps = std::max(5, std::min(2000, static_cast<int>(40.0 / std::max(probe, 1e-3))));
-      double best = 1e30;
-      for (int trial = 0; trial < 2; ++trial) {
-        s->record(*e0);
-        for (int i = 0; i < reps; ++i) launch(M, *s);
-        s->record(*e1);
-        s->synchronize();
-        best = std::min(best, dev_.elapsed_ms(*e0, *e1) * 1e3 / reps);
-      }
-      levels_.push_back(GemmLevel{M, best, 2.0 * M * static_cast<double>(N_) * K_});
-    }
+      return dev_.elapsed_ms(*e0, *e1) * 1e3;
+    };
+    // ~0.3 s first so the measurement sees the sustained (DVFS-settled) clock
+    // rather than the cold-start boost
+    const double probe = std::max(1.0, time_task(8, 0) / 8.0);
+    const uint32_t warm = static_cast<uint32_t>(std::min(4000.0, std::max(20.0, 300000.0 / probe)));
+    (void)time_task(warm, 0);
+    auto best = [&](uint32_t r, uint32_t tail) {
+      double b = 1e30;
+      for (int i = 0; i < 3; ++i) b = std::min(b, time_task(r, tail));
+      return b;
+    };
+    const uint32_t r1 = 20, r2 = 60;
+    const double t1 = best(r1, 0), t2 = best(r2, 0);
+    cal_.round_us = std::max(1e-3, (t2 - t1) / (r2 - r1));
+    const uint32_t tail = std::max<uint32_t>(tail_mul_, static_cast<uint32_t>(nk_ / 2) / tail_mul_ * tail_mul_);
+    const double tt = best(r1, tail);
+    cal_.ktile_us = std::max(1e-4, (tt - t1) / tail);
+    // the slot's epoch / completion state is this stream's: the line is reset for the strategy's streams
+    dev_.memset_async(slot, 0, 64, *s);
+    s->synchronize();
+    slot_of_.clear();
+    epoch_.clear();
   }
 
   static constexpr int kMmax = 8192;
+  static constexpr int kTile = 256;
   static constexpr size_t kSlots = 64;
   Device& dev_;
   ComputeMode mode_;
   double scale_;
+  bool fixed_ = false;
   Buffer slots_;
   Buffer counters_;  // kernels::DlCounter words (DlSync::counters)
   // programs: the open task list per stream, the device ring their task lists
@@ -624,19 +753,23 @@ class GpuCompute : public ComputeEngine {
   };
   std::map<Stream*, Join> joins_;  // set_lane_join, taken by the next end_program
   std::set<Stream*> joined_;
+  std::map<Stream*, long> program_count_;  // programs launched per stream (programs_on)
   Buffer prog_dev_;
   size_t prog_next_ = 0;
+  kernels::DlTask* prog_host_ = nullptr;  // host-mapped ring (task lists launched at once)
+  size_t host_next_ = 0;
   struct Upload {
     kernels::DlTask* dst;
     std::vector<kernels::DlTask> tasks;
   };
   std::vector<Upload> uploads_;
   static constexpr size_t kProgTasks = 16384;
-  long programs_launched_ = 0, program_tasks_ = 0;
+  long programs_launched_ = 0, program_tasks_ = 0, fixed_tasks_ = 0;
   std::vector<uint64_t*> gates_;          // device gates (Device::alloc_gate)
   std::map<Stream*, size_t> slot_of_;
   std::map<uint64_t*, uint32_t> epoch_;
   std::map<uint64_t*, bool> chain_live_;  // the stream's last task was a deadline task a chained one may continue
+  std::map<Stream*, const uint64_t*> last_end_;  // fixed work: the end slot of the stream's last task
   std::vector<uint32_t> gate_tag_;        // last tag signalled per gate (never 0 once signalled)
   uint64_t* extra_start_ = nullptr;       // set_next_start_slot
   TimerSet* stall_timers_ = nullptr;      // set_task_timers: task starts for the stall timers
@@ -651,7 +784,6 @@ class GpuCompute : public ComputeEngine {
     LaneStats& st = lane_stats_[&s];
     ++st.n;
     st.us += std::max(0.0, d);
-    if (mode_ == ComputeMode::GemmWork || mode_ == ComputeMode::Flops) st.single = false;
   }
   // Reports a task's start slot and duration to the stall timers once it is enqueued.
   struct StartNote {
@@ -659,8 +791,9 @@ class GpuCompute : public ComputeEngine {
     Stream& s;
     const uint64_t* start;
     uint64_t ticks;
+    const uint64_t* end;
     ~StartNote() {
-      if (t && std::uncaught_exceptions() == 0) t->task_started(s, start, ticks);
+      if (t && std::uncaught_exceptions() == 0) t->task_started(s, start, ticks, end);
     }
   };
   // Lateness a chained task absorbs (deadline_sync.hpp): the replayed graph's
@@ -677,8 +810,11 @@ class GpuCompute : public ComputeEngine {
   int cus_ = 256;
   DType dtype_ = DType::BF16;
   int K_ = 4096, N_ = 16384;
+  int nk_ = 0;                 // K-tiles of a full tile (fixed work)
+  uint32_t tail_mul_ = 2;      // the tail's K-tile multiple
+  FixedCal cal_;
+  bool cal_given_ = false;
   Buffer A_, B_, C_;
-  std::vector<GemmLevel> levels_;
   TimerSet* task_timers_ = nullptr;
 };
 

@@ -297,10 +297,15 @@ class CpuDevice : public Device {
     std::lock_guard<std::mutex> g(reg_->mu);
     for (CpuStream* s : reg_->live) s->synchronize();
   }
-  void abort_and_drain() override {
+  bool abort_and_drain() override {
     abort_->store(true);
     std::lock_guard<std::mutex> g(reg_->mu);
     for (CpuStream* s : reg_->live) s->drain();
+    return true;
+  }
+  bool abort_raised() const override { return abort_->load(); }
+  void idle(Stream& s, double us) override {
+    dynamic_cast<CpuStream&>(s).enqueue([us] { precise_sleep_us(us); });
   }
   uint64_t* alloc_stamps(size_t n) override { return static_cast<uint64_t*>(std::calloc(n, sizeof(uint64_t))); }
   void free_stamps(uint64_t* p, size_t) override { std::free(p); }

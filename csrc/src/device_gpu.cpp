@@ -2,10 +2,14 @@
 #include <hip/hip_runtime.h>
 #include <hsa/hsa_ext_amd.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
+#include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "dlnb/device.hpp"
@@ -53,16 +57,30 @@ class GpuEvent : public Event {
   uint64_t gen = 0;          // the device's capture generation at that record
 };
 
+// The device's live streams (abort_and_drain polls them all).
+struct GpuStreamSet {
+  std::mutex mu;
+  std::set<hipStream_t> live;
+};
+
 class GpuStream : public Stream {
  public:
-  GpuStream(int device, bool high_priority) {
+  GpuStream(int device, bool high_priority, std::shared_ptr<GpuStreamSet> set) : set_(std::move(set)) {
     DLNB_HIP_CHECK(hipSetDevice(device));
     int lo = 0, hi = 0;
     DLNB_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     // hi is the numerically smallest (= greatest) priority.
     DLNB_HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high_priority ? hi : lo));
+    std::lock_guard<std::mutex> g(set_->mu);
+    set_->live.insert(s);
   }
-  ~GpuStream() override { (void)hipStreamDestroy(s); }
+  ~GpuStream() override {
+    {
+      std::lock_guard<std::mutex> g(set_->mu);
+      set_->live.erase(s);
+    }
+    (void)hipStreamDestroy(s);
+  }
   void record(Event& e) override;
   void wait(Event& e) override;
   void synchronize() override { DLNB_HIP_CHECK(hipStreamSynchronize(s)); }
@@ -74,6 +92,9 @@ class GpuStream : public Stream {
   }
   void* native() override { return s; }
   hipStream_t s{};
+
+ private:
+  std::shared_ptr<GpuStreamSet> set_;
 };
 
 class GpuGraphExec : public GraphExec {
@@ -146,9 +167,18 @@ class GpuDevice : public Device {
     total_ = prop.totalGlobalMem;
     kernels::clock_cal_begin(idx_);  // the rate is taken at its first use (stamp_hz), after setup
     ensure_pool();                   // gates / iteration word: never allocated while a stream captures
+    void* a = nullptr;
+    DLNB_HIP_CHECK(hipHostMalloc(&a, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    abort_host_ = static_cast<uint64_t*>(a);
+    std::memset(abort_host_, 0, 64);
+    void* ad = nullptr;
+    DLNB_HIP_CHECK(hipHostGetDevicePointer(&ad, a, 0));
+    abort_dev_ = static_cast<uint64_t*>(ad);
   }
   ~GpuDevice() override {
     if (pool_) (void)hipFree(pool_);
+    // (an abort word a kernel may still poll is never freed: the process is going away)
+    if (abort_host_ && !abort_raised()) (void)hipHostFree(abort_host_);
   }
   DeviceKind kind() const override { return DeviceKind::GPU; }
   std::string name() const override { return name_ + " (" + arch_ + ")"; }
@@ -156,7 +186,7 @@ class GpuDevice : public Device {
   std::unique_ptr<Stream> create_stream(bool high_priority) override {
     // DLNB_HIGH_PRIORITY_STREAMS=0: comm lanes on normal-priority queues (A/B)
     static const bool high_ok = env_int("DLNB_HIGH_PRIORITY_STREAMS", 1) != 0;
-    return std::unique_ptr<Stream>(new GpuStream(idx_, high_priority && high_ok));
+    return std::unique_ptr<Stream>(new GpuStream(idx_, high_priority && high_ok, streams_));
   }
   std::unique_ptr<Event> create_event(bool timing) override {
     return std::unique_ptr<Event>(new GpuEvent(timing, this));
@@ -205,6 +235,35 @@ class GpuDevice : public Device {
     DLNB_HIP_CHECK(hipLaunchHostFunc(static_cast<hipStream_t>(s.native()), host_trampoline, heap));
   }
   void synchronize() override { DLNB_HIP_CHECK(hipDeviceSynchronize()); }
+  const uint64_t* abort_word() override { return abort_dev_; }
+  void raise_abort() override { __atomic_store_n(abort_host_, 1ull, __ATOMIC_SEQ_CST); }
+  bool abort_raised() const override { return __atomic_load_n(abort_host_, __ATOMIC_ACQUIRE) != 0; }
+  bool abort_and_drain() override {
+    raise_abort();
+    // every device wait gives up on the abort word (and the communicators were
+    // aborted by the caller), so the queued work drains; bounded all the same
+    const double limit = static_cast<double>(env_int("DLNB_ABORT_DRAIN_S", 20));
+    const double t0 = now_s();
+    for (;;) {
+      bool idle = true;
+      {
+        std::lock_guard<std::mutex> g(streams_->mu);
+        for (hipStream_t s : streams_->live) {
+          const hipError_t e = hipStreamQuery(s);
+          if (e == hipErrorNotReady) {
+            idle = false;
+            break;
+          }
+        }
+      }
+      if (idle) return true;
+      if (now_s() - t0 > limit) return false;
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+  }
+  void idle(Stream& s, double us) override {
+    kernels::idle_wait(static_cast<uint64_t>(us * 1e-6 * stamp_hz() + 0.5), s.native());
+  }
   uint64_t* alloc_stamps(size_t n) override {
     void* p = nullptr;
     DLNB_HIP_CHECK(hipHostMalloc(&p, n * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent));
@@ -217,7 +276,7 @@ class GpuDevice : public Device {
   void host_wait(Stream& s, const uint64_t* word, uint64_t value, double timeout_s, uint64_t* timeouts,
                  uint64_t iter_value) override {
     kernels::host_wait(word, value, static_cast<uint64_t>(timeout_s * stamp_hz()), timeouts, s.native(),
-                       iter_value ? iter_word() : nullptr, iter_value);
+                       iter_value ? iter_word() : nullptr, iter_value, abort_dev_);
   }
 
   // ---- gates: one zeroed device block, carved without HIP calls (gates are
@@ -286,7 +345,7 @@ class GpuDevice : public Device {
     // would never match - as a HIP event outside the capture, nothing to wait
     // for inside the graph
     if (e.gen != gen_) return;
-    kernels::gate_wait(e.gate, iter_word(), e.tag, gate_timeout_ticks(), pool_ + 1, s);
+    kernels::gate_wait(e.gate, iter_word(), e.tag, gate_timeout_ticks(), pool_ + 1, s, abort_dev_);
   }
   bool queues_independent(const std::vector<Stream*>& ss, double timeout_s, std::string* detail) override {
     const uint64_t t = static_cast<uint64_t>(timeout_s * stamp_hz());
@@ -387,6 +446,9 @@ class GpuDevice : public Device {
     DLNB_HIP_CHECK(hipStreamSynchronize(nullptr));
   }
   uint64_t* pool_ = nullptr;
+  uint64_t* abort_host_ = nullptr;  // abort word: the host's pointer
+  uint64_t* abort_dev_ = nullptr;   // and the kernels'
+  std::shared_ptr<GpuStreamSet> streams_ = std::make_shared<GpuStreamSet>();
   size_t next_gate_ = 0;
   uint64_t gen_ = 0;  // capture generation (capture_lanes)
   bool gate_events_ = false;

@@ -38,7 +38,39 @@ namespace {
 thread_local const uint64_t* t_done_flag = nullptr;
 thread_local size_t t_done_n = 0;
 thread_local uint64_t t_done_value = 0;
+
+// The run on this thread, for device_failure (set by run_rank).
+struct FailGuard {
+  Device* dev = nullptr;
+  std::vector<Communicator*>* comms = nullptr;
+  bool cli_exit = false;  // CLI process owning its ranks: end the process at the first failure
+  int rank = 0;
+  bool fired = false;
+};
+thread_local FailGuard* t_fail = nullptr;
+std::atomic<bool> g_poisoned{false};
 }  // namespace
+
+void device_failure(const std::string& why) {
+  FailGuard* f = t_fail;
+  if (!f || f->fired) return;
+  f->fired = true;
+  if (f->dev) f->dev->raise_abort();
+  if (f->cli_exit && f->dev) {  // (GPU runs only: a CPU run's failure path is its own, unchanged)
+    std::fprintf(stderr,
+                 "[dlnb] rank %d error: %s\n[dlnb] rank %d: device waits aborted; exiting without teardown (the "
+                 "driver reclaims the GPU queues)\n",
+                 f->rank, why.c_str(), f->rank);
+    std::fflush(stdout);
+    std::fflush(stderr);
+    std::_Exit(3);
+  }
+  if (f->comms)
+    for (Communicator* c : *f->comms)
+      if (c) c->abort();
+}
+
+bool process_poisoned() { return g_poisoned.load(); }
 
 CompletionFlag::CompletionFlag(const uint64_t* flags, size_t n, uint64_t value)
     : prev_(t_done_flag), prev_n_(t_done_n), prev_value_(t_done_value) {
@@ -82,16 +114,19 @@ void sync_streams(const std::vector<Stream*>& streams, const std::vector<Communi
           if (!c) continue;
           std::string err = c->async_error();
           if (!err.empty()) {
+            device_failure("communication failure: " + err);
             for (Communicator* a : comms)
               if (a) a->abort();
             DLNB_THROW("communication failure: " << err);
           }
         }
         if (now_s() - t0 > timeout) {
+          std::ostringstream m;
+          m << "iteration did not complete within DLNB_TIMEOUT=" << timeout << " s (hung collective or dead peer)";
+          device_failure(m.str());
           for (Communicator* a : comms)
             if (a) a->abort();
-          DLNB_THROW("iteration did not complete within DLNB_TIMEOUT=" << timeout
-                                                                       << " s (hung collective or dead peer)");
+          DLNB_THROW(m.str());
         }
       }
       std::this_thread::sleep_for(std::chrono::microseconds(5));
@@ -226,8 +261,8 @@ namespace {
 // members, the library's own rank count) into ctx.comm_log for the report.
 class RecordingFactory : public CommFactory {
  public:
-  RecordingFactory(std::unique_ptr<CommFactory> inner, std::vector<CommRecord>* log)
-      : inner_(std::move(inner)), log_(log) {}
+  RecordingFactory(std::unique_ptr<CommFactory> inner, std::vector<CommRecord>* log, std::vector<Communicator*>* live)
+      : inner_(std::move(inner)), log_(log), live_(live) {}
   std::string backend_name() const override { return inner_->backend_name(); }
   std::unique_ptr<Communicator> create(const std::string& name, const std::vector<int>& members,
                                        size_t capacity_bytes, bool need_p2p, int max_ctas) override {
@@ -235,10 +270,31 @@ class RecordingFactory : public CommFactory {
     log_->push_back({name, c->backend_name(), c->size(), c->library_nranks()});
     return c;
   }
+  void add_live(Communicator* c) { live_->push_back(c); }
 
  private:
   std::unique_ptr<CommFactory> inner_;
   std::vector<CommRecord>* log_;
+  std::vector<Communicator*>* live_;
+};
+
+// The outermost communicator wrapper (tracing, when --timeline wraps the
+// factory afterwards) is what the strategy holds; it reports itself here.
+class LiveFactory : public CommFactory {
+ public:
+  LiveFactory(std::unique_ptr<CommFactory> inner, std::vector<Communicator*>* live)
+      : inner_(std::move(inner)), live_(live) {}
+  std::string backend_name() const override { return inner_->backend_name(); }
+  std::unique_ptr<Communicator> create(const std::string& name, const std::vector<int>& members,
+                                       size_t capacity_bytes, bool need_p2p, int max_ctas) override {
+    auto c = inner_->create(name, members, capacity_bytes, need_p2p, max_ctas);
+    live_->push_back(c.get());
+    return c;
+  }
+
+ private:
+  std::unique_ptr<CommFactory> inner_;
+  std::vector<Communicator*>* live_;
 };
 
 }  // namespace
@@ -322,7 +378,7 @@ std::string select_backend(Context& ctx, const std::string& requested, const std
     DLNB_THROW("unknown backend '" << backend << "' (auto, rccl, xgmi, mixed, cpu, loopback, loopback-cpu)");
   }
   ctx.comms = wrap_comm_faults(std::move(ctx.comms), *ctx.dev, ri.rank);
-  ctx.comms.reset(new RecordingFactory(std::move(ctx.comms), &ctx.comm_log));
+  ctx.comms.reset(new RecordingFactory(std::move(ctx.comms), &ctx.comm_log, &ctx.live_comms));
   return backend;
 }
 
@@ -429,6 +485,8 @@ Json run_loopback(const Options& opt) {
 bool cli_process() { return g_cli_process.load(); }
 
 Json run_benchmark(const Options& opt) {
+  DLNB_REQUIRE(!process_poisoned(),
+               "an earlier run of this process failed and left device work that did not drain: start a new process");
   if (opt.backend == "loopback" || opt.backend == "loopback-cpu") return run_loopback(opt);
   return run_rank(opt, bootstrap_from_env(opt.store_addr));
 }
@@ -445,14 +503,46 @@ Json run_rank(const Options& opt, std::unique_ptr<Bootstrap> boot) {
   ctx.opt = opt;
   ctx.boot = std::move(boot);
   std::unique_ptr<Strategy> strat;
+  FailGuard guard;
+  guard.comms = &ctx.live_comms;
+  guard.rank = ctx.boot->info.rank;
+  guard.cli_exit = g_cli_process.load() && !ctx.boot->hub && env_int("DLNB_FAIL_EXIT", 1) != 0;
+  struct GuardScope {
+    FailGuard* prev;
+    explicit GuardScope(FailGuard* g) : prev(t_fail) { t_fail = g; }
+    ~GuardScope() { t_fail = prev; }
+  } scope(&guard);
   try {
-    return run_rank_impl(opt, ctx, strat);
+    Json r = run_rank_impl(opt, ctx, strat);
+    t_fail = scope.prev;  // the run is over: strategy teardown is not a failure of it
+    return r;
   } catch (const std::exception& e) {
     // The strategy is destroyed before the device (ctx outlives strat): its
     // events, buffers and communicators must not go while a stream task still
     // uses them (a CPU stream waiting on a freed event never returned - seen
     // after a peer died mid-iteration, library host).
-    if (ctx.dev && !ctx.boot->hub) ctx.dev->abort_and_drain();
+    if (ctx.dev && ctx.dev->kind() == DeviceKind::GPU && !ctx.boot->hub) {
+      // GPU: abort the device waits (CLI: the process ends here), abort the
+      // communicators, then wait - bounded - for the device to drain; work
+      // that does not drain keeps everything it may use (nothing is freed) and
+      // this process runs nothing more.
+      guard.dev = ctx.dev.get();
+      device_failure(e.what());
+      if (!ctx.dev->abort_and_drain()) {
+        g_poisoned.store(true);
+        const std::string msg = std::string(e.what()) +
+                                " (device work did not drain within DLNB_ABORT_DRAIN_S after the abort: this process "
+                                "runs no further benchmark)";
+        (void)strat.release();
+        (void)ctx.timeline.release();
+        (void)ctx.compute.release();
+        (void)ctx.comms.release();
+        (void)ctx.dev.release();
+        throw Error(msg);
+      }
+    } else if (ctx.dev && !ctx.boot->hub) {
+      ctx.dev->abort_and_drain();
+    }
     if (ctx.boot->hub) {
       const std::string msg = "rank " + std::to_string(ctx.boot->info.rank) + ": " + e.what();
       loopback_abort(*ctx.boot->hub, msg);
@@ -475,6 +565,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
 
   // ---- backend / device (cpp/utils.hpp:62-117 set_local_device)
   const std::string backend = select_backend(ctx, opt.backend, opt.devices);
+  if (t_fail && ctx.dev->kind() == DeviceKind::GPU && !ctx.boot->hub) t_fail->dev = ctx.dev.get();
 
   // ---- workload
   std::string stats_path = opt.stats_file.empty() ? stats_path_for(opt.base_path, opt.model) : opt.stats_file;
@@ -509,6 +600,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     ctx.comms = make_tracing_factory(std::move(ctx.comms), ctx.timeline.get());
     ctx.compute = make_tracing_compute(std::move(ctx.compute), ctx.timeline.get());
   }
+  ctx.comms.reset(new LiveFactory(std::move(ctx.comms), &ctx.live_comms));
 
   if (opt.topology) print_topology(ctx);
 
@@ -661,7 +753,12 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       const double task_us = ctx.compute->lane_task_us(*ss[0]);
       const bool long_tasks = task_us >= static_cast<double>(env_int("DLNB_LANE_MIN_TASK_US", 1000)) &&
                               strat->lanes_without_program();
-      const bool program_ok = joined || long_tasks || env_int("DLNB_LANE_GRAPHS", 1) >= 2;
+      // a compute program per iteration qualifies joined or not (not joined:
+      // work follows it on the compute lane, which then ends with its own
+      // done word - ADVICE r5)
+      const bool program_ok = joined || ctx.compute->programs_on(*ss[0]) > 0 || long_tasks ||
+                              env_int("DLNB_LANE_GRAPHS", 1) >= 2;
+      lane_info["compute_programs"] = static_cast<double>(ctx.compute->programs_on(*ss[0]));
       lane_info["compute_task_us"] = task_us;
       const double verdict = ctx.hg().allreduce_max(!linear ? 2.0 : (!program_ok ? 1.0 : 0.0));
       linear = verdict < 0.5;
@@ -960,15 +1057,23 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     uint64_t*& p;
     size_t n;
     ~Handshake() {
-      if (!p) return;
-      if (std::uncaught_exceptions() == 0) {
-        d.free_stamps(p, n);
-      } else {  // release any armed graph (not freed: hipHostFree waits for the device, which may be hung)
-        __atomic_store_n(p, ~0ull, __ATOMIC_RELEASE);
+      if (std::uncaught_exceptions() != 0) {
+        // The run failed inside the timed loop: abort the device waits before
+        // anything is torn down - an armed replay is NOT released (its go
+        // wait sees the abort and lets it run through poisoned: no compute,
+        // no waits); a CLI process ends here (device_failure). The words are
+        // not freed (hipHostFree waits for the device, which may be hung).
+        device_failure("exception in the timed loop: " + last_error_message());
+        return;
       }
+      if (p) d.free_stamps(p, n);
     }
   } handshake{*ctx.dev, hs, nhs};
-  const double go_timeout_s = 30.0;
+  // An armed replay waits for its go through the whole iteration before it:
+  // its wait's bound (after which it runs anyway, counted in
+  // prearm_go_timeouts) is 4x the compute floor + 60 s.
+  const double go_timeout_s =
+      std::max(60.0, 4.0 * strat->compute_floor_us(ctx) * 1e-6 * opt.time_scale + 60.0);
   std::vector<uint64_t> armed_iter;  // device iteration number of each armed replay
   auto arm = [&](int r) {
     const uint64_t it = ++dev_iter;
@@ -1055,9 +1160,14 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       // lane's gate_wait, a deadline task's gate, a gate event's wait
       c["gate_wait_timeouts"] = cc.wait_timeouts + static_cast<double>(ctx.dev->gate_event_timeouts());
       c["compute_gate_timeouts"] = cc.gate_timeouts;
+      // waits that left on the host's abort word, program blocks that came late for a task
+      c["aborted_waits"] = cc.aborted;
+      c["late_blocks"] = cc.late_blocks;
       rank["chain_capped"] = c;
     }
   }
+  // intervals whose stamps came out of order (recorded as 0; never expected)
+  if (T.has_negatives()) rank["timer_negative_intervals"] = T.negatives_json();
   rank["hostname"] = ri.hostname;
   rank["rank"] = ri.rank;
   rank["local_rank"] = ri.local_rank;

@@ -202,6 +202,7 @@ class DataParallel : public Strategy {
     timers_->stall_after_task(*compute_, *done_, "barrier_time");  // exposed gradient communication (as dp)
     // Optimizer step on this rank's slice of each bucket, then that bucket's
     // parameter all-gather, which overlaps the next bucket's update.
+    const uint64_t* ag_end = nullptr;
     for (int i = 0; i < nb_; ++i) {
       const void* g = zero_ == 2 ? sums_[i].data()
                                  : (in_place_ ? grads_[i].at(me * shard_[i] * es_) : sums_[i].at(me * shard_[i] * es_));
@@ -210,10 +211,15 @@ class DataParallel : public Strategy {
       comm_stream_->wait(*opt_done_[i]);
       int t = timers_->begin(*comm_stream_);
       comm_->all_gather(pshard_[i].data(), pfull_[i].data(), shard_[i], ctx.wire, *comm_stream_);
-      timers_->end(t, *comm_stream_, "param_allgather_time");
+      ag_end = timers_->end(t, *comm_stream_, "param_allgather_time");
     }
+    // exposed parameter all-gather: from the optimizer's end on the compute
+    // stream (a stamp right behind its last kernel, no wait between) to the
+    // last all-gather's end stamp - a gap, never a stamp-wait-stamp pair
+    const uint64_t* opt_end = timers_->mark(*compute_);
     comm_stream_->record(*ag_done_);
-    timers_->stall(*compute_, *ag_done_, "param_allgather_exposed");
+    compute_->wait(*ag_done_);
+    if (opt_end && ag_end) timers_->gap(opt_end, 0, ag_end, "param_allgather_exposed");
   }
 
   void enqueue_iteration() override {
@@ -230,7 +236,7 @@ class DataParallel : public Strategy {
     // engine's kernels stamp their start (deadline / sleep / spin compute).
     // A stamp-wait-stamp on the compute stream (stall) otherwise.
     const bool stamped = ce.stamps_task_start();
-    const uint64_t* last_start = nullptr;
+    TaskMark last;
     const uint64_t* tail_end = nullptr;
     uint64_t* fwd_start = stamped ? timers_->slot() : nullptr;
     // Lane graphs: the forward and the backward buckets are one compute
@@ -244,7 +250,7 @@ class DataParallel : public Strategy {
       // the bucket's gradients are ready when its backward is: ready_[i] is
       // recorded by the task itself (lane graphs: raised from its own kernel)
       ce.run_chained(*compute_, bwd_us_[i], bwd_flops_[i], st, comm_gates_ ? nullptr : ready_[i].get());
-      if (st) last_start = st;
+      if (st) last = task_mark(ce, *compute_, st, bwd_us_[i]);
       if (comm_gates_) {
         ce.signal(*compute_, g_ready_[i]);
         // bounded by 4x the compute queued ahead of the signal (the forward and
@@ -261,11 +267,14 @@ class DataParallel : public Strategy {
       const uint64_t* e = timers_->end(t, *comm_stream_, "allreduce_time");
       if (e) tail_end = e;
     }
-    if (prog) ce.end_program(*compute_);
-    if (last_start && tail_end && !ctx.opt.optimizer) {
+    const bool tail_gap = last.slot && tail_end && !ctx.opt.optimizer;
+    // (the lane join ends the program only when nothing follows it on the
+    // compute stream: no stall stamp, no optimizer - ADVICE r5)
+    if (prog) ce.end_program(*compute_, tail_gap);
+    if (tail_gap) {
       // nothing follows on the compute stream: the iteration ends when both
       // streams have (graph join, lane done words, synchronize)
-      timers_->gap(last_start, ce.task_ticks(bwd_us_[nb_ - 1]), tail_end, "barrier_time");
+      timers_->gap(last.slot, last.ticks, tail_end, "barrier_time");
       // the iteration on the device clock: forward start to the last all-reduce's end
       timers_->gap(fwd_start, 0, tail_end, "device_span_time");
     } else {

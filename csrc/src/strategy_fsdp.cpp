@@ -165,9 +165,8 @@ class Fsdp : public Strategy {
       if (dep) compute_->wait(*dep);
       uint64_t* st = timers_->slot();
       ce.run_stamped(*compute_, us, flops, st);
-      if (timer && prev_start_) timers_->gap(prev_start_, prev_ticks_, st, timer);
-      prev_start_ = st;
-      prev_ticks_ = ce.task_ticks(us);
+      if (timer && prev_.slot) timers_->gap(prev_.slot, prev_.ticks, st, timer);
+      prev_ = task_mark(ce, *compute_, st, us);
       return;
     }
     if (dep) {
@@ -186,16 +185,15 @@ class Fsdp : public Strategy {
   void compute_gated(std::vector<int> gates, const char* timer, double us, double flops, Event* done) {
     ComputeEngine& ce = *ctx_->compute;
     uint64_t* st = timers_->slot();
-    ce.run_gated(*compute_, us, flops, gates, st, prev_start_ != nullptr, done);
-    if (timer && prev_start_) timers_->gap(prev_start_, prev_ticks_, st, timer);
-    prev_start_ = st;
-    prev_ticks_ = ce.task_ticks(us);
+    ce.run_gated(*compute_, us, flops, gates, st, prev_.slot != nullptr, done);
+    if (timer && prev_.slot) timers_->gap(prev_.slot, prev_.ticks, st, timer);
+    prev_ = task_mark(ce, *compute_, st, us);
   }
 
   void enqueue_iteration() override {
     Context& ctx = *ctx_;
     const DType t = ctx.wire;
-    prev_start_ = nullptr;
+    prev_ = TaskMark();
     tail_end_ = nullptr;
 
     ComputeEngine& ce = *ctx.compute;
@@ -280,16 +278,19 @@ class Fsdp : public Strategy {
         ar_stream_->record(*ar_done_[u]);
       }
     }
-    if (prog) ce.end_program(*compute_);
     // ---- tail: exposed reduce-scatter / replica all-reduce
+    const bool tail_gap = gated_ && !ctx.opt.optimizer && tail_end_ && prev_.slot;
+    // (the lane join ends the program only when nothing follows it on the
+    // compute stream: no stall stamp, no optimizer - ADVICE r5)
+    if (prog) ce.end_program(*compute_, tail_gap);
     Event& tail = R_ > 1 ? *ar_done_[0] : *rs_done_[0];
-    if (gated_ && !ctx.opt.optimizer && tail_end_ && prev_start_) {
+    if (tail_gap) {
       // nothing runs on the compute stream after the last backward: the
       // exposed tail is the last collective's end stamp minus the last
       // deadline, with no wait + stamp pair (a cross-queue hop and two
       // kernels) at the end of the iteration; the iteration still ends when
       // every stream has (graph join / synchronize)
-      timers_->gap(prev_start_, prev_ticks_, tail_end_, "barrier");
+      timers_->gap(prev_.slot, prev_.ticks, tail_end_, "barrier");
     } else {
       timers_->stall_after_task(*compute_, tail, "barrier");
     }
@@ -373,9 +374,8 @@ class Fsdp : public Strategy {
   Buffer gathered_[2], full_grad_[2];
   std::vector<std::unique_ptr<Event>> ag_f_, fwd_done_, ag_b_, bwd_done_, rs_done_, ar_done_;
   std::vector<CommStat> stats_;
-  const uint64_t* prev_start_ = nullptr;  // start stamp of the previous compute task
+  TaskMark prev_;                         // where the previous compute task ended (task_mark)
   const uint64_t* tail_end_ = nullptr;    // end stamp of the iteration's last collective
-  uint64_t prev_ticks_ = 0;
 };
 
 }  // namespace

@@ -58,14 +58,21 @@ void Timeline::end(int token, Stream& s, const char* cat, const std::string& nam
   if (token < 0) return;
   const int idx = static_cast<int>(next_++);  // begin() reserved room for it
   dev_.stamp(s, stamps_ + idx);
-  spans_.push_back(Span{token, idx, lane_of(s), 0, cat, name, std::move(args)});
+  spans_.push_back(Span{token, idx, lane_of(s), 0, nullptr, cat, name, std::move(args)});
 }
 
 void Timeline::end_after(int token, Stream& s, uint64_t dur_ticks, const char* cat, const std::string& name,
                          Json args) {
   if (token < 0) return;
   ++next_;  // keep begin()'s accounting (two slots per span)
-  spans_.push_back(Span{token, -1, lane_of(s), dur_ticks, cat, name, std::move(args)});
+  spans_.push_back(Span{token, -1, lane_of(s), dur_ticks, nullptr, cat, name, std::move(args)});
+}
+
+void Timeline::end_at(int token, Stream& s, const uint64_t* end, const char* cat, const std::string& name,
+                      Json args) {
+  if (token < 0) return;
+  ++next_;  // keep begin()'s accounting (two slots per span)
+  spans_.push_back(Span{token, -1, lane_of(s), 0, end, cat, name, std::move(args)});
 }
 
 void Timeline::begin_capture() {
@@ -84,7 +91,9 @@ void Timeline::collect(int iter) {
         break;
       }
       const uint64_t a = __atomic_load_n(stamps_ + sp.a, __ATOMIC_ACQUIRE);
-      const uint64_t b = sp.b < 0 ? a + sp.dur : __atomic_load_n(stamps_ + sp.b, __ATOMIC_ACQUIRE);
+      const uint64_t b = sp.end    ? __atomic_load_n(sp.end, __ATOMIC_ACQUIRE)
+                         : sp.b < 0 ? a + sp.dur
+                                    : __atomic_load_n(stamps_ + sp.b, __ATOMIC_ACQUIRE);
       events_.push_back(Event{iter, sp.lane, sp.cat, sp.name, sp.args, a, b >= a ? b : a});
     }
   }
@@ -412,7 +421,9 @@ class TracingCompute : public ComputeEngine {
   void reset_clocks(Stream& s) override { in_->reset_clocks(s); }
   void reset_slot(Stream& s) override { in_->reset_slot(s); }
   bool begin_program(Stream& s) override { return in_->begin_program(s); }
-  void end_program(Stream& s) override { in_->end_program(s); }
+  void end_program(Stream& s, bool join_ok) override { in_->end_program(s, join_ok); }
+  long programs_on(Stream& s) override { return in_->programs_on(s); }
+  const uint64_t* last_task_end(Stream& s) override { return in_->last_task_end(s); }
   void after_capture() override { in_->after_capture(); }
   void set_lane_join(Stream& s, const std::vector<uint64_t*>& gates, uint32_t tag, uint64_t* host_done) override {
     in_->set_lane_join(s, gates, tag, host_done);
@@ -444,10 +455,12 @@ class TracingCompute : public ComputeEngine {
     }
     fn();
     a["table_us"] = us;
-    if (in_->stamps_task_start())
-      tl_->end_after(tok, s, in_->task_ticks(us), "compute", name, a);
-    else
+    if (!in_->stamps_task_start())
       tl_->end(tok, s, "compute", name, a);
+    else if (const uint64_t* e = in_->last_task_end(s))
+      tl_->end_at(tok, s, e, "compute", name, a);  // fixed work: the task's own end stamp
+    else
+      tl_->end_after(tok, s, in_->task_ticks(us), "compute", name, a);
   }
   std::unique_ptr<ComputeEngine> in_;
   Timeline* tl_;

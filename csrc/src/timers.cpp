@@ -1,4 +1,6 @@
 #include "dlnb/timers.hpp"
+
+#include <algorithm>
 #include "dlnb/common.hpp"
 
 namespace dlnb {
@@ -46,6 +48,10 @@ void TimerSet::stall(Stream& s, Event& e, const std::string& name) {
     s.wait(e);
     return;
   }
+  // A stamp-wait-stamp pair read short under graph replay (round 4): inside a
+  // capture every stall is timed from task stamps (stall_before_task /
+  // stall_after_task) or as a gap between stamps nothing waits between.
+  DLNB_REQUIRE(!capturing_ || !task_stamps_, "TimerSet::stall(" << name << ") inside a graph capture");
   int t = begin(s);
   s.wait(e);
   end(t, s, name);
@@ -57,37 +63,65 @@ uint64_t* TimerSet::task_slot(Stream& s) {
   return slot();
 }
 
-void TimerSet::task_started(Stream& s, const uint64_t* start, uint64_t ticks) {
+void TimerSet::task_started(Stream& s, const uint64_t* start, uint64_t ticks, const uint64_t* end) {
   if (!task_stamps() || !owns(start)) return;
   TaskClock& c = clocks_[&s];
   close_pending(c, start);
-  c.start = start;
-  c.ticks = ticks;
+  if (end && owns(end)) {
+    c.start = end;  // fixed work: the task's own end stamp
+    c.ticks = 0;
+  } else {
+    c.start = start;
+    c.ticks = ticks;
+  }
+}
+
+const uint64_t* TimerSet::mark(Stream& s) {
+  if (!enabled_) return nullptr;
+  uint64_t* st = slot();
+  dev_.stamp(s, st);
+  return st;
+}
+
+void TimerSet::pair(const uint64_t* a, const uint64_t* b, const std::string& name) {
+  if (!enabled_ || !owns(a) || !owns(b)) return;
+  pending_.push_back(Pending{static_cast<int>(a - stamps_), static_cast<int>(b - stamps_), name});
 }
 
 void TimerSet::stall_before_task(Stream& s, Event& e, const std::string& name) {
-  auto it = clocks_.find(&s);
-  if (!task_stamps() || it == clocks_.end() || !it->second.start) {
+  if (!task_stamps()) {
     stall(s, e, name);
     return;
   }
+  TaskClock& c = clocks_[&s];
+  if (!c.start) {
+    // no task before the wait in this iteration: the reference is a stamp
+    // right before it (nothing is waited for between the two)
+    c.start = mark(s);
+    c.ticks = 0;
+  }
   s.wait(e);
-  it->second.pending.push_back(name);
+  c.pending.push_back(name);
 }
 
 void TimerSet::stall_after_task(Stream& s, Event& e, const std::string& name) {
-  auto it = clocks_.find(&s);
-  if (!task_stamps() || it == clocks_.end() || !it->second.start || !it->second.pending.empty()) {
+  if (!task_stamps()) {
     stall(s, e, name);
     return;
+  }
+  TaskClock& c = clocks_[&s];
+  if (!c.start) {
+    c.start = mark(s);
+    c.ticks = 0;
   }
   s.wait(e);
   DLNB_REQUIRE(next_ < cap_, "too many timer stamps in one iteration");
   uint64_t* st = stamps_ + next_++;
   dev_.stamp(s, st);
-  gap(it->second.start, it->second.ticks, st, name);
-  it->second.start = st;
-  it->second.ticks = 0;
+  c.pending.push_back(name);  // (after earlier waits with no task between: the first takes the gap)
+  close_pending(c, st);
+  c.start = st;
+  c.ticks = 0;
 }
 
 // A stream's pending stall_before_task waits end where the stream reaches
@@ -120,7 +154,7 @@ uint64_t* TimerSet::slot() {
 
 void TimerSet::gap(const uint64_t* prev_start, uint64_t prev_ticks, const uint64_t* next_start,
                    const std::string& name) {
-  if (!enabled_) return;
+  if (!enabled_ || !prev_start || !next_start) return;
   gaps_.push_back(Gap{static_cast<int>(prev_start - stamps_), static_cast<int>(next_start - stamps_), prev_ticks, name});
 }
 
@@ -153,16 +187,26 @@ void TimerSet::resolve() {
   const double hz = dev_.stamp_hz();
   if (frozen_ && enabled_)
     for (const auto& a : captured_adds_) vals_[a.first].push_back(a.second);
-  for (const auto& p : pending_) {
-    const uint64_t a = __atomic_load_n(stamps_ + p.a, __ATOMIC_ACQUIRE);
-    const uint64_t b = __atomic_load_n(stamps_ + p.b, __ATOMIC_ACQUIRE);
-    if (enabled_) vals_[p.name].push_back(b >= a ? static_cast<double>(b - a) / hz : 0.0);
-  }
-  for (const auto& g : gaps_) {
-    const uint64_t a = __atomic_load_n(stamps_ + g.prev, __ATOMIC_ACQUIRE) + g.prev_ticks;
-    const uint64_t b = __atomic_load_n(stamps_ + g.next, __ATOMIC_ACQUIRE);
-    if (enabled_) vals_[g.name].push_back(b >= a ? static_cast<double>(b - a) / hz : 0.0);
-  }
+  // Every interval here is causally ordered (a stall ends after the task or
+  // stamp it is timed from; a collective ends after it began): a negative one
+  // means mis-ordered stamps. It is recorded as 0 and counted
+  // (negatives_json()), never silently clamped.
+  auto put = [&](const std::string& name, uint64_t a, uint64_t b) {
+    if (!enabled_) return;
+    if (b >= a) {
+      vals_[name].push_back(static_cast<double>(b - a) / hz);
+      return;
+    }
+    vals_[name].push_back(0.0);
+    Negative& n = negatives_[name];
+    ++n.count;
+    n.worst_s = std::max(n.worst_s, static_cast<double>(a - b) / hz);
+  };
+  for (const auto& p : pending_)
+    put(p.name, __atomic_load_n(stamps_ + p.a, __ATOMIC_ACQUIRE), __atomic_load_n(stamps_ + p.b, __ATOMIC_ACQUIRE));
+  for (const auto& g : gaps_)
+    put(g.name, __atomic_load_n(stamps_ + g.prev, __ATOMIC_ACQUIRE) + g.prev_ticks,
+        __atomic_load_n(stamps_ + g.next, __ATOMIC_ACQUIRE));
   if (frozen_) return;  // the same stamps are rewritten by the next replay
   pending_.clear();
   gaps_.clear();
@@ -176,6 +220,18 @@ void TimerSet::clear() {
     next_ = 0;
   }
   for (auto& kv : vals_) kv.second.clear();
+  negatives_.clear();
+}
+
+Json TimerSet::negatives_json() const {
+  Json j = Json::object();
+  for (const auto& kv : negatives_) {
+    Json e = Json::object();
+    e["count"] = static_cast<double>(kv.second.count);
+    e["worst_ms"] = kv.second.worst_s * 1e3;
+    j[kv.first] = e;
+  }
+  return j;
 }
 
 const std::vector<double>& TimerSet::get(const std::string& name) const {

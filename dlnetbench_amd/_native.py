@@ -27,6 +27,19 @@ class NativeError(RuntimeError):
     pass
 
 
+class TaskDesc(ctypes.Structure):
+    """One task of a compute program (csrc/src/capi.cpp dlnb_task_desc ->
+    kernels::DlTask): ticks > 0 a deadline task, ticks == 0 with work_rounds /
+    tail_kt a fixed-work task, neither the join."""
+    _fields_ = [("ticks", ctypes.c_ulonglong), ("chain_ticks", ctypes.c_ulonglong),
+                ("gate0", ctypes.c_void_p), ("gate1", ctypes.c_void_p),
+                ("tag0", ctypes.c_uint), ("tag1", ctypes.c_uint),
+                ("tstart0", ctypes.c_void_p), ("tstart1", ctypes.c_void_p),
+                ("done_gate", ctypes.c_void_p), ("done_tag", ctypes.c_uint),
+                ("work_rounds", ctypes.c_uint), ("tail_kt", ctypes.c_uint), ("epoch", ctypes.c_uint),
+                ("tend", ctypes.c_void_p)]
+
+
 def lib() -> ctypes.CDLL:
     global _LIB
     if _LIB is not None:
@@ -59,6 +72,14 @@ def lib() -> ctypes.CDLL:
     L.dlnb_gemm_deadline_ex.argtypes = [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_dbl, c_int, c_vp, c_int, c_vp,
                                         ctypes.c_uint, c_dbl, c_vp, ctypes.c_uint, c_vp, ctypes.c_uint, c_vp, c_vp]
     L.dlnb_gate_signal.argtypes = [c_vp, ctypes.c_uint, c_vp]
+    L.dlnb_gate_signal_iter.argtypes = [c_vp, c_vp, ctypes.c_uint, c_vp]
+    L.dlnb_task_size.restype = c_int
+    L.dlnb_gemm_program.argtypes = [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, ctypes.POINTER(TaskDesc), c_int,
+                                    c_vp, c_vp, c_vp, c_dbl, c_int, c_vp, c_vp, c_int, c_vp, ctypes.c_uint]
+    L.dlnb_program_ktiles.argtypes = [c_int, c_int, c_int, c_int]
+    L.dlnb_host_words.argtypes = [c_int, ctypes.POINTER(c_vp)]
+    L.dlnb_host_words.restype = c_vp
+    L.dlnb_host_words_free.argtypes = [c_vp]
     L.dlnb_gemm_shape_ok.argtypes = [c_int, c_int, c_int, c_int]
     L.dlnb_gemm_narrow_nf.argtypes = [c_int, c_int, c_int]
     L.dlnb_idle_wait_us.argtypes = [c_dbl, c_int, c_vp]

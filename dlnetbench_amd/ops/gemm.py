@@ -145,3 +145,83 @@ def stamp_(slot, index: int = 0):
     when torch's current stream reaches this point."""
     _native.check(_native.lib().dlnb_stamp(slot.data_ptr() + 8 * index, _stream(slot)))
     return slot
+
+
+def gate_signal_iter_(gate, index: int, tag: int, iter_word):
+    """gate_signal_ with the sequence (iteration << 32 | tag) read from iter_word[0] (int64 CUDA
+    tensor) when the kernel runs."""
+    _native.check(_native.lib().dlnb_gate_signal_iter(gate.data_ptr() + 16 * index, iter_word.data_ptr(), tag,
+                                                      _stream(gate)))
+    return gate
+
+
+def task_size() -> int:
+    """Bytes of one kernels::DlTask (a program's task list entry)."""
+    return int(_native.lib().dlnb_task_size())
+
+
+def program_ktiles(M: int, N: int, K: int, dtype) -> int:
+    """K-tiles (128 bytes of K) of one tile of the program kernel for this shape (0: no program kernel)."""
+    import torch
+    dt = _native.DTYPES["bf16"] if dtype == torch.bfloat16 else _native.DTYPES["fp8_e4m3"]
+    return int(_native.lib().dlnb_program_ktiles(M, N, K, dt))
+
+
+def ptr(t, index: int = 0, words: int = 1) -> int:
+    """Device address of word `index` (of `words` 8-byte words) of an int64 tensor / HostWords."""
+    if isinstance(t, HostWords):
+        return t.dev + 8 * index
+    return t.data_ptr() + 8 * index
+
+
+class HostWords:
+    """n host-mapped, device-visible 64-bit words (hipHostMalloc mapped + coherent): `dev` is the
+    device address, indexing reads / writes them from the host (e.g. an abort word)."""
+
+    def __init__(self, n: int):
+        import ctypes
+        dev = ctypes.c_void_p()
+        self.host = _native.lib().dlnb_host_words(n, ctypes.byref(dev))
+        if not self.host:
+            raise _native.NativeError("hipHostMalloc failed")
+        self.dev = dev.value
+        self.n = n
+        self._arr = (ctypes.c_uint64 * n).from_address(self.host)
+
+    def __getitem__(self, i: int) -> int:
+        return int(self._arr[i])
+
+    def __setitem__(self, i: int, v: int) -> None:
+        self._arr[i] = v
+
+    def free(self) -> None:
+        if self.host:
+            _native.lib().dlnb_host_words_free(self.host)
+            self.host = None
+
+
+def gemm_program(a, b, c, tasks, slot, task_buf, iter_word=None, counters=None, abort=None,
+                 gate_timeout_s: float = 60.0, grid: int = 0, epoch: int = 0):
+    """A compute program (kernels::gemm_tn_deadline_program): `tasks` a list of _native.TaskDesc
+    (pointers as device addresses: see ptr()), `slot` an int64 CUDA tensor of 8 words (the stream's
+    slot line), `task_buf` a uint8 / int64 CUDA tensor of >= len(tasks) * task_size() bytes the list
+    is copied into (after torch's current stream is idle), `iter_word` an int64 CUDA tensor (the
+    iteration word the gates' sequences and program claims read), `counters` an int64 CUDA tensor of
+    >= 8 DlCounter words, `abort` a HostWords (word 0 the abort word). epoch 0: program claims from
+    the iteration word; else a one-task launch epoch (1..65535)."""
+    import torch
+    dt = _native.DTYPES["bf16"] if a.dtype == torch.bfloat16 else _native.DTYPES["fp8_e4m3"]
+    M, K = a.shape
+    N = b.shape[0]
+    if slot.numel() < 8 or slot.dtype != torch.int64:
+        raise ValueError("slot must be an int64 tensor of >= 8 elements")
+    if task_buf.numel() * task_buf.element_size() < len(tasks) * task_size():
+        raise ValueError("task_buf too small")
+    arr = (_native.TaskDesc * len(tasks))(*tasks)
+    _native.check(_native.lib().dlnb_gemm_program(
+        a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, dt, arr, len(tasks),
+        iter_word.data_ptr() if iter_word is not None else None,
+        counters.data_ptr() if counters is not None else None,
+        abort.dev if abort is not None else None, gate_timeout_s, a.device.index or 0, slot.data_ptr(),
+        task_buf.data_ptr(), grid, _stream(a), epoch))
+    return c

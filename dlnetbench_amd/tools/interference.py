@@ -101,10 +101,10 @@ def run(victim: str, victim_ranks: int, aggressor: str, aggressor_ranks: int, wa
     alone = [_summary(d) for d in docs]
     # Fixed-work compute (gemm-work / flops) keeps its alone calibration: a
     # calibration taken beside the aggressor would shrink the work to fit.
-    levels = docs[0]["global"]["dlnb"]["compute"].get("gemm_levels")
+    fw = docs[0]["global"]["dlnb"]["compute"].get("fixed_work")
     venv = dict(env)
-    if levels:
-        venv["DLNB_GEMM_LEVELS"] = ",".join(f"{int(lv['M'])}:{lv['us_per_launch']!r}" for lv in levels)
+    if fw:
+        venv["DLNB_FIXED_WORK_CAL"] = f"{fw['round_us']!r}:{fw['ktile_us']!r}"
     log = tempfile.TemporaryFile(mode="w+", prefix="dlnb_aggressor_")
 
     def log_tail() -> str:
@@ -137,7 +137,7 @@ def run(victim: str, victim_ranks: int, aggressor: str, aggressor_ranks: int, wa
             "aggressor_ranks": aggressor_ranks, "alone": a, "contended": c,
             "slowdown": round(c["median_ms"] / a["median_ms"], 4) if a["median_ms"] else None,
             "comm": comm, "repeats": repeats,
-            "fixed_work_levels": venv.get("DLNB_GEMM_LEVELS")}
+            "fixed_work_cal": venv.get("DLNB_FIXED_WORK_CAL")}
 
 
 def main(argv=None) -> int:

@@ -306,6 +306,30 @@ def test_bench_gpu_single_rank_secondaries(tmp_path):
 
 
 @pytest.mark.gpu
+def test_bench_gpu_headline_device_fault_still_prints_the_line(tmp_path):
+    """a device-side hang injected into the N = 1 headline (its first gate is never raised,
+    DLNB_INJECT_FAULT mode=gate, block=headline) costs only the headline's graph child: it exits at the host's
+    timeout, the per-iteration retry - a fresh child, where the fault is not armed - times the step, the line
+    carries the graph run's error, and the comm-bound block after it reports a normal value."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, DLNB_INJECT_FAULT="rank=0,iter=0,mode=gate,block=headline", DLNB_TIMEOUT="5")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--no-c5-ctas-ab", "--c5-bucket-ratio", "0", "--stretch-steps", "0"] + TINY,
+                       capture_output=True, text=True, timeout=300, cwd=str(tmp_path), env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1, p.stdout
+    o = lines[0]
+    assert "exit 3" in o["headline_graph_error"], o.get("headline_graph_error")
+    assert o["value"] > 0 and o["config"]["hip_graph"] is False, o
+    c5 = o["comm_bound"]
+    assert "error" not in c5 and c5["ms_per_step"] >= 0.9 * c5["floor_ms"], c5
+    assert c5["ms_per_step"] <= 1.5 * c5["floor_ms"] + 2.0, c5
+
+
+@pytest.mark.gpu
 def test_bench_torchrun_xgmi_two_ranks_one_gpu(tmp_path):
     """The driver's N > 1 launch on the GPU: torchrun, 2 ranks sharing GPU 0 over the xgmi kernels (RCCL
     refuses two ranks on one device), HIP graph, plus the comm_bound_xgmi child-process secondary."""

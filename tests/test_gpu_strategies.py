@@ -52,7 +52,7 @@ def test_strategy_runs_on_gpu(strategy, model, params, compute, data_dir):
         # (only the fixed-work modes measure one)
         c = g["dlnb"]["compute"]
         assert c["mode"] == "gemm" and c["deadline_grid"] == c["num_cus"] - 32 and c["gemm_K"] > 0
-        assert "gemm_levels" not in c
+        assert "fixed_work" not in c
 
 
 def test_fsdp_llama3_8b_single_gpu_iteration(root):

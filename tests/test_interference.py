@@ -52,5 +52,5 @@ def test_interference_same_gpu():
                          f"dp tiny_dense_8_bfloat16 4 {DATA} --backend rccl --compute gemm", 1, warm_s=2.0,
                          timeout=120)
     assert r["alone"]["backend"] == "RCCL" and r["slowdown"] > 0.95, r
-    assert r["fixed_work_levels"]  # the contended run reused the alone calibration (DLNB_GEMM_LEVELS)
+    assert r["fixed_work_cal"]  # the contended run reused the alone calibration (DLNB_FIXED_WORK_CAL)
     assert _no_leftover("dp")
