@@ -255,7 +255,11 @@ int program_tail_multiple(int M, int N, int K, DType in_t);
 
 // Elementwise "optimizer" stand-in (SGD-momentum on bf16 shards, fp32 math):
 // p = p - lr * (m = beta*m + g). Used by the optional --optimizer step.
-void sgd_momentum_bf16(void* param, void* mom, const void* grad, size_t n, float lr, float beta, void* stream);
+// end_stamp (optional, host-mapped): the kernel's end time (s_memrealtime),
+// stored by its last block; `done` is a zeroed device word it counts blocks
+// in (re-armed to 0 by that block).
+void sgd_momentum_bf16(void* param, void* mom, const void* grad, size_t n, float lr, float beta, void* stream,
+                       uint64_t* end_stamp = nullptr, uint32_t* done = nullptr);
 
 }  // namespace kernels
 }  // namespace dlnb

@@ -205,6 +205,9 @@ Json runtime_info();
 Json comm_log_json(const std::vector<CommRecord>& log);
 
 // Elementwise SGD-momentum over a bf16 shard (the optional --optimizer step).
-void optimizer_step(Context& ctx, Stream& s, void* param, void* mom, const void* grad, size_t n);
+// end_stamp (optional, a TimerSet slot): the step's end on the device clock,
+// stored by the kernel itself (GPU: `done` a zeroed device word; CPU: the task).
+void optimizer_step(Context& ctx, Stream& s, void* param, void* mom, const void* grad, size_t n,
+                    uint64_t* end_stamp = nullptr, uint32_t* done = nullptr);
 
 }  // namespace dlnb

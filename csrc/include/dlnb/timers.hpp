@@ -41,7 +41,11 @@ class TimerSet {
   // long the stream sat between the previous task's deadline and the next
   // task's first block (the dependency wait plus the launch).
   uint64_t* slot();
-  void gap(const uint64_t* prev_start, uint64_t prev_ticks, const uint64_t* next_start, const std::string& name);
+  // clamp: the two ends are not causally ordered (a collective that may
+  // finish before the compute it is compared with): a negative value is a
+  // real 0, not an error (negatives_json does not count it).
+  void gap(const uint64_t* prev_start, uint64_t prev_ticks, const uint64_t* next_start, const std::string& name,
+           bool clamp = false);
   // Stall timers from the compute tasks' own start stamps, for any strategy.
   // With set_task_stamps(true) (the engine's kernels stamp their start:
   // deadline / idle / spin compute), the engine takes a slot for every task
@@ -72,6 +76,22 @@ class TimerSet {
   void pair(const uint64_t* a, const uint64_t* b, const std::string& name);
   void stall_before_task(Stream& s, Event& e, const std::string& name);
   void stall_after_task(Stream& s, Event& e, const std::string& name);
+  // The waits pending on s (stall_before_task with no task after them yet)
+  // were for an operation on another stream that ended at op_end (its end
+  // stamp): they end there (clamped - the operation may have ended before s
+  // got to the wait), and s's next wait is timed from the later of its
+  // reference and op_end. E.g. the last all-to-all of a backward and the
+  // gradient all-reduce queued behind it on the same lane: the compute
+  // stream's wait for the all-reduce is not booked on the all-to-all.
+  void settle(Stream& s, const uint64_t* op_end);
+  // A stamp heading the iteration on s (the runner, before the strategy's
+  // enqueue; in a single graph the head node every stream's chain follows):
+  // s's first wait with no task before it is timed from there, not from a
+  // stamp queued right before the wait - in a single graph that one is a
+  // sibling of the other streams' first nodes and can run after them (a
+  // stage's wait for its first activation read ~0 instead of the forward of
+  // the stage before).
+  void iteration_start(Stream& s);
   void finish_stalls();
   void add(const std::string& name, double seconds);
   void ensure(const std::string& name);
@@ -107,16 +127,27 @@ class TimerSet {
     int prev, next;
     uint64_t prev_ticks;
     std::string name;
+    bool clamp;
+    int floor;  // >= 0: the interval starts no earlier than this slot
   };
   std::vector<Gap> gaps_;
   bool owns(const uint64_t* p) const { return p >= stamps_ && p < stamps_ + cap_; }
   struct TaskClock {
     const uint64_t* start = nullptr;  // the last task's start slot on the stream
     uint64_t ticks = 0;
+    const uint64_t* floor = nullptr;  // settle(): another stream's end stamp the next wait starts after
     std::vector<std::string> pending;  // stall_before_task names since it
   };
   std::map<Stream*, TaskClock> clocks_;
-  void close_pending(TaskClock& c, const uint64_t* at);
+  Stream* origin_ = nullptr;
+  const uint64_t* origin_start_ = nullptr;
+  void first_reference(Stream& s, TaskClock& c);
+  void close_pending(TaskClock& c, const uint64_t* at, bool clamp = false);
+  static void restart(TaskClock& c, const uint64_t* start, uint64_t ticks) {
+    c.start = start;
+    c.ticks = ticks;
+    c.floor = nullptr;
+  }
   bool task_stamps_ = false;
   std::map<std::string, std::vector<double>> vals_;
   struct Negative {

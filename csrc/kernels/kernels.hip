@@ -514,7 +514,7 @@ __global__ void __launch_bounds__(128 * WN, WN == 4 ? 2 : 1)
 // ------------------------------------------------------------- optimizer
 
 __global__ void sgd_momentum_kernel(__bf16* __restrict__ p, __bf16* __restrict__ m, const __bf16* __restrict__ g,
-                                    size_t n, float lr, float beta) {
+                                    size_t n, float lr, float beta, uint64_t* end_stamp, uint32_t* done) {
   size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x * 8;
   for (size_t i = (blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x) * 8; i < n; i += stride) {
     if (i + 8 <= n) {
@@ -534,6 +534,18 @@ __global__ void sgd_momentum_kernel(__bf16* __restrict__ p, __bf16* __restrict__
         float mm = beta * static_cast<float>(m[k]) + static_cast<float>(g[k]);
         m[k] = static_cast<__bf16>(mm);
         p[k] = static_cast<__bf16>(static_cast<float>(p[k]) - lr * mm);
+      }
+    }
+  }
+  if (end_stamp) {
+    // the kernel's end on the device clock: the last block to finish stores it
+    // (and re-arms the counter for the next launch)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      if (__hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+        __hip_atomic_store(end_stamp, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -1004,11 +1016,13 @@ void gemm_tn_deadline_program(const void* A, const void* B, void* C, int M, int 
     gemm_8phase_deadline_program(A, B, C, M, N, K, in_t, tasks, n, slot, grid, stream, epoch);
 }
 
-void sgd_momentum_bf16(void* param, void* mom, const void* grad, size_t n, float lr, float beta, void* stream) {
+void sgd_momentum_bf16(void* param, void* mom, const void* grad, size_t n, float lr, float beta, void* stream,
+                       uint64_t* end_stamp, uint32_t* done) {
   if (n == 0) return;
+  DLNB_REQUIRE(!end_stamp || done, "sgd_momentum_bf16: an end stamp needs its completion counter");
   int grid = grid_for((n + 7) / 8, 256);
   hipLaunchKernelGGL(sgd_momentum_kernel, grid, 256, 0, S(stream), static_cast<__bf16*>(param),
-                     static_cast<__bf16*>(mom), static_cast<const __bf16*>(grad), n, lr, beta);
+                     static_cast<__bf16*>(mom), static_cast<const __bf16*>(grad), n, lr, beta, end_stamp, done);
   DLNB_HIP_CHECK(hipGetLastError());
 }
 

@@ -159,9 +159,25 @@ Json comm_stats_json(const std::vector<CommStat>& stats, const TimerSet& t) {
   return out;
 }
 
-void optimizer_step(Context& ctx, Stream& s, void* param, void* mom, const void* grad, size_t n) {
+void optimizer_step(Context& ctx, Stream& s, void* param, void* mom, const void* grad, size_t n, uint64_t* end_stamp,
+                    uint32_t* done) {
   if (ctx.dev->kind() == DeviceKind::GPU) {
-    kernels::sgd_momentum_bf16(param, mom, grad, n, 1e-4f, 0.9f, s.native());
+    kernels::sgd_momentum_bf16(param, mom, grad, n, 1e-4f, 0.9f, s.native(), end_stamp, done);
+    return;
+  }
+  if (end_stamp) {
+    // (the CPU device's stamp: when the stream reaches it, i.e. after the task below)
+    ctx.dev->host_task(s, [param, mom, grad, n] {
+      auto* p = static_cast<uint16_t*>(param);
+      auto* m = static_cast<uint16_t*>(mom);
+      auto* g = static_cast<const uint16_t*>(grad);
+      for (size_t i = 0; i < n; ++i) {
+        float mv = 0.9f * bf16_to_float(m[i]) + bf16_to_float(g[i]);
+        m[i] = float_to_bf16(mv);
+        p[i] = float_to_bf16(bf16_to_float(p[i]) - 1e-4f * mv);
+      }
+    });
+    ctx.dev->stamp(s, end_stamp);
     return;
   }
   ctx.dev->host_task(s, [param, mom, grad, n] {
@@ -716,6 +732,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       ctx.compute->set_lane_join(*ss[0], end_gates, 1u, lane_done);
       lane_graphs = ctx.dev->capture_lanes(
           ss, [&] {
+            T.iteration_start(*ss[0]);
             strat->enqueue_iteration();
             T.finish_stalls();
           },
@@ -837,7 +854,11 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
           *ss[0], others, [&] {
             strat->enqueue_iteration();
             T.finish_stalls();
-          }, [&] { ctx.compute->reset_clocks(*ss[0]); });
+          }, [&] {
+            ctx.compute->reset_clocks(*ss[0]);
+            T.iteration_start(*ss[0]);
+          });
+      ctx.compute->after_capture();  // task lists of the launches captured (fixed-work tasks)
       lanes_ss = {ss[0]};
     }
     T.end_capture();
@@ -937,6 +958,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       for (Stream* l : lanes_for(it)) ctx.dev->set_iteration(*l, it);
       launch_graphs(it);
     } else {
+      T.iteration_start(*strat->streams()[0]);
       strat->enqueue_iteration();
       T.finish_stalls();
     }

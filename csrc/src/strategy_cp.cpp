@@ -324,6 +324,11 @@ class ContextParallel : public Strategy {
     r["cp_exposed_time"] = per_iter("cp_exposed_time", stall_per_iter);
     r["dp_comm_time"] = per_iter("dp_comm_time", static_cast<size_t>(nbk_));
     r["dp_exposed_time"] = timers_->values_json("dp_exposed_time");
+    // the same, one entry per wait / CP operation (in issue order)
+    r["cp_exposed_waits"] = timers_->values_json("cp_exposed_time");
+    for (const char* k : {"cp_fwd_time", "cp_bwd_time", "cp_qkv_time", "cp_out_time"})
+      if (!timers_->get(k).empty()) r[std::string(k) + "_ops"] = timers_->values_json(k);
+    r["dp_comm_ops"] = timers_->values_json("dp_comm_time");
     r["cp_id"] = cp_id_;
     r["dp_id"] = dp_id_;
     return r;

@@ -143,6 +143,7 @@ class DataParallel : public Strategy {
         opt_done_.push_back(dev.create_event());
       }
     }
+    if (zero_) opt_done_word_ = dev.alloc(64);  // the optimizer kernel's block counter (end stamp)
     done_ = dev.create_event();
     ag_done_ = dev.create_event();
     if (o.optimizer && !zero_) {
@@ -203,23 +204,34 @@ class DataParallel : public Strategy {
     // Optimizer step on this rank's slice of each bucket, then that bucket's
     // parameter all-gather, which overlaps the next bucket's update.
     const uint64_t* ag_end = nullptr;
+    uint64_t* opt_end = nullptr;
     for (int i = 0; i < nb_; ++i) {
       const void* g = zero_ == 2 ? sums_[i].data()
                                  : (in_place_ ? grads_[i].at(me * shard_[i] * es_) : sums_[i].at(me * shard_[i] * es_));
-      if (ctx.wire == DType::BF16) optimizer_step(ctx, *compute_, pshard_[i].data(), mshard_[i].data(), g, shard_[i]);
+      // the last step stamps its own end (its kernel's last block): the reference
+      // of the exposed parameter all-gather below
+      uint64_t* end = i == nb_ - 1 && timers_->enabled() ? timers_->slot() : nullptr;
+      if (ctx.wire == DType::BF16) {
+        optimizer_step(ctx, *compute_, pshard_[i].data(), mshard_[i].data(), g, shard_[i], end,
+                       end ? opt_done_word_.as<uint32_t>() : nullptr);
+        opt_end = end;
+      }
       compute_->record(*opt_done_[i]);
       comm_stream_->wait(*opt_done_[i]);
       int t = timers_->begin(*comm_stream_);
       comm_->all_gather(pshard_[i].data(), pfull_[i].data(), shard_[i], ctx.wire, *comm_stream_);
       ag_end = timers_->end(t, *comm_stream_, "param_allgather_time");
     }
-    // exposed parameter all-gather: from the optimizer's end on the compute
-    // stream (a stamp right behind its last kernel, no wait between) to the
-    // last all-gather's end stamp - a gap, never a stamp-wait-stamp pair
-    const uint64_t* opt_end = timers_->mark(*compute_);
+    // exposed parameter all-gather: from the optimizer's end (its last
+    // kernel's own stamp, or a stamp right behind it without the optimizer)
+    // to the last all-gather's end stamp - a gap, never a stamp-wait-stamp
+    // pair (a stamp kernel queued behind the all-gather read 0 in a single
+    // graph); the all-gather may end before the optimizer's last block (it is
+    // hidden then: 0)
+    const uint64_t* opt_mark = opt_end ? opt_end : timers_->mark(*compute_);
     comm_stream_->record(*ag_done_);
     compute_->wait(*ag_done_);
-    if (opt_end && ag_end) timers_->gap(opt_end, 0, ag_end, "param_allgather_exposed");
+    if (opt_mark && ag_end) timers_->gap(opt_mark, 0, ag_end, "param_allgather_exposed", true);
   }
 
   void enqueue_iteration() override {
@@ -376,6 +388,7 @@ class DataParallel : public Strategy {
   std::vector<uint64_t> shard_;        // per bucket: ceil(size / W)
   std::vector<Buffer> pshard_, mshard_, pfull_;  // ZeRO: parameter / momentum shards, gathered parameters
   std::vector<std::unique_ptr<Event>> opt_done_;
+  Buffer opt_done_word_;
   std::unique_ptr<Event> ag_done_;
   std::unique_ptr<Communicator> comm_;
   std::unique_ptr<Stream> compute_, comm_stream_;

@@ -34,10 +34,7 @@ const uint64_t* TimerSet::end(int token, Stream& s, const std::string& name) {
   pending_.push_back(Pending{token, idx, name});
   if (task_stamps()) {
     auto it = clocks_.find(&s);
-    if (it != clocks_.end()) {  // the stream's next wait is timed from here
-      it->second.start = stamps_ + idx;
-      it->second.ticks = 0;
-    }
+    if (it != clocks_.end()) restart(it->second, stamps_ + idx, 0);  // the stream's next wait is timed from here
   }
   return stamps_ + idx;
 }
@@ -67,13 +64,10 @@ void TimerSet::task_started(Stream& s, const uint64_t* start, uint64_t ticks, co
   if (!task_stamps() || !owns(start)) return;
   TaskClock& c = clocks_[&s];
   close_pending(c, start);
-  if (end && owns(end)) {
-    c.start = end;  // fixed work: the task's own end stamp
-    c.ticks = 0;
-  } else {
-    c.start = start;
-    c.ticks = ticks;
-  }
+  if (end && owns(end))
+    restart(c, end, 0);  // fixed work: the task's own end stamp
+  else
+    restart(c, start, ticks);
 }
 
 const uint64_t* TimerSet::mark(Stream& s) {
@@ -95,10 +89,9 @@ void TimerSet::stall_before_task(Stream& s, Event& e, const std::string& name) {
   }
   TaskClock& c = clocks_[&s];
   if (!c.start) {
-    // no task before the wait in this iteration: the reference is a stamp
-    // right before it (nothing is waited for between the two)
-    c.start = mark(s);
-    c.ticks = 0;
+    // no task before the wait in this iteration: the iteration's head stamp,
+    // or a stamp right before the wait (nothing is waited for between the two)
+    first_reference(s, c);
   }
   s.wait(e);
   c.pending.push_back(name);
@@ -110,27 +103,45 @@ void TimerSet::stall_after_task(Stream& s, Event& e, const std::string& name) {
     return;
   }
   TaskClock& c = clocks_[&s];
-  if (!c.start) {
-    c.start = mark(s);
-    c.ticks = 0;
-  }
+  if (!c.start) first_reference(s, c);
   s.wait(e);
   DLNB_REQUIRE(next_ < cap_, "too many timer stamps in one iteration");
   uint64_t* st = stamps_ + next_++;
   dev_.stamp(s, st);
   c.pending.push_back(name);  // (after earlier waits with no task between: the first takes the gap)
   close_pending(c, st);
-  c.start = st;
-  c.ticks = 0;
+  restart(c, st, 0);
+}
+
+void TimerSet::iteration_start(Stream& s) {
+  if (!task_stamps()) return;
+  origin_ = &s;
+  origin_start_ = mark(s);
+}
+
+void TimerSet::first_reference(Stream& s, TaskClock& c) {
+  if (&s == origin_ && origin_start_)
+    restart(c, origin_start_, 0);
+  else
+    restart(c, mark(s), 0);
+}
+
+void TimerSet::settle(Stream& s, const uint64_t* op_end) {
+  if (!task_stamps() || !owns(op_end)) return;
+  auto it = clocks_.find(&s);
+  if (it == clocks_.end() || !it->second.start || it->second.pending.empty()) return;
+  close_pending(it->second, op_end, true);
+  it->second.floor = op_end;
 }
 
 // A stream's pending stall_before_task waits end where the stream reaches
 // `at` (a task's start or a timed operation's begin stamp).
-void TimerSet::close_pending(TaskClock& c, const uint64_t* at) {
+void TimerSet::close_pending(TaskClock& c, const uint64_t* at, bool clamp) {
   for (size_t i = 0; i < c.pending.size(); ++i) {
-    if (i == 0)
-      gap(c.start, c.ticks, at, c.pending[i]);
-    else
+    if (i == 0) {
+      gap(c.start, c.ticks, at, c.pending[i], clamp);
+      if (c.floor && enabled_ && c.start && at) gaps_.back().floor = static_cast<int>(c.floor - stamps_);
+    } else
       gap(at, 0, at, c.pending[i]);  // one stream cannot tell consecutive waits apart: the first takes the gap
   }
   c.pending.clear();
@@ -145,6 +156,8 @@ void TimerSet::finish_stalls() {
     close_pending(c, st);
   }
   clocks_.clear();  // the next iteration's first wait has no task before it
+  origin_ = nullptr;
+  origin_start_ = nullptr;
 }
 
 uint64_t* TimerSet::slot() {
@@ -153,9 +166,10 @@ uint64_t* TimerSet::slot() {
 }
 
 void TimerSet::gap(const uint64_t* prev_start, uint64_t prev_ticks, const uint64_t* next_start,
-                   const std::string& name) {
+                   const std::string& name, bool clamp) {
   if (!enabled_ || !prev_start || !next_start) return;
-  gaps_.push_back(Gap{static_cast<int>(prev_start - stamps_), static_cast<int>(next_start - stamps_), prev_ticks, name});
+  gaps_.push_back(
+      Gap{static_cast<int>(prev_start - stamps_), static_cast<int>(next_start - stamps_), prev_ticks, name, clamp, -1});
 }
 
 void TimerSet::add(const std::string& name, double seconds) {
@@ -168,6 +182,8 @@ void TimerSet::add(const std::string& name, double seconds) {
 
 void TimerSet::begin_capture() {
   clocks_.clear();
+  origin_ = nullptr;
+  origin_start_ = nullptr;
   pending_.clear();
   gaps_.clear();
   next_ = 0;
@@ -191,10 +207,10 @@ void TimerSet::resolve() {
   // stamp it is timed from; a collective ends after it began): a negative one
   // means mis-ordered stamps. It is recorded as 0 and counted
   // (negatives_json()), never silently clamped.
-  auto put = [&](const std::string& name, uint64_t a, uint64_t b) {
+  auto put = [&](const std::string& name, uint64_t a, uint64_t b, bool clamp = false) {
     if (!enabled_) return;
-    if (b >= a) {
-      vals_[name].push_back(static_cast<double>(b - a) / hz);
+    if (b >= a || clamp) {  // (clamp: a gap whose ends are not ordered, TimerSet::gap)
+      vals_[name].push_back(b >= a ? static_cast<double>(b - a) / hz : 0.0);
       return;
     }
     vals_[name].push_back(0.0);
@@ -204,9 +220,11 @@ void TimerSet::resolve() {
   };
   for (const auto& p : pending_)
     put(p.name, __atomic_load_n(stamps_ + p.a, __ATOMIC_ACQUIRE), __atomic_load_n(stamps_ + p.b, __ATOMIC_ACQUIRE));
-  for (const auto& g : gaps_)
-    put(g.name, __atomic_load_n(stamps_ + g.prev, __ATOMIC_ACQUIRE) + g.prev_ticks,
-        __atomic_load_n(stamps_ + g.next, __ATOMIC_ACQUIRE));
+  for (const auto& g : gaps_) {
+    uint64_t a = __atomic_load_n(stamps_ + g.prev, __ATOMIC_ACQUIRE) + g.prev_ticks;
+    if (g.floor >= 0) a = std::max(a, __atomic_load_n(stamps_ + g.floor, __ATOMIC_ACQUIRE));
+    put(g.name, a, __atomic_load_n(stamps_ + g.next, __ATOMIC_ACQUIRE), g.clamp);
+  }
   if (frozen_) return;  // the same stamps are rewritten by the next replay
   pending_.clear();
   gaps_.clear();

@@ -67,8 +67,8 @@ def test_fsdp_llama3_8b_single_gpu_iteration(root):
 def test_fsdp_program_lanes(root):
     """Lane graphs on the headline's FSDP step (Llama-3 8B, 0.05x time): one linear graph per stream, the compute
     lane one persistent program whose join signals the iteration, replays alternating between two stream sets,
-    no gate timeout; fixed-work compute (a launch per task) takes the single graph instead, with the reason
-    (profiles/lanes_r5.md)."""
+    no gate timeout; fixed-work compute too (its tasks are program tasks of a fixed amount of
+    MFMA work), with its compute_stretch from the tasks' own start / end stamps."""
     doc = engine.run_native("fsdp", "llama3_8b_16_bfloat16", 32, 1, base_path=root, warmup=2, runs=3,
                             compute="gemm", backend="rccl", time_scale=0.05, graph=True, quiet=True)
     d = doc["global"]["dlnb"]
@@ -81,8 +81,14 @@ def test_fsdp_program_lanes(root):
     assert it["compute_floor_ms"] * 0.999 <= it["median_ms"] < it["compute_floor_ms"] * 1.02 + 1.0, it
     doc = engine.run_native("fsdp", "llama3_8b_16_bfloat16", 32, 1, base_path=root, warmup=1, runs=2,
                             compute="gemm-work", backend="rccl", time_scale=0.05, graph=True, quiet=True)
-    lg = doc["global"]["dlnb"]["lane_graphs"]
-    assert not lg["enabled"] and "program" in lg["reason"], lg
+    d = doc["global"]["dlnb"]
+    lg = d["lane_graphs"]
+    assert lg["enabled"] and lg["linear"] and lg["program_join"] and lg["compute_programs"] == 1, lg
+    c = d["compute"]
+    assert c["programs"] >= 1 and c["fixed_work"]["round_us"] > 0 and c["fixed_work"]["tasks"] >= 64, c
+    assert 0.9 < d["compute_stretch"] < 1.3, d["compute_stretch"]
+    assert d["chain_capped"]["gate_wait_timeouts_max"] == 0 and d["chain_capped"]["compute_gate_timeouts_max"] == 0
+    assert "timer_negative_intervals" not in doc["ranks"][0], doc["ranks"][0]
 
 
 def test_lane_fallback_after_warmup(root):
@@ -335,7 +341,7 @@ def test_dp_exposed_comm_matches_the_step(mode, root):
 
 
 def _two_ranks_one_gpu(root, tmp_path, binary_name, params, extra_env=None, iters=8, model="llama3_8b_16_bfloat16",
-                       time_scale="0.05"):
+                       time_scale="0.05", base=None):
     """Run one 2-rank job of a native binary with both ranks on GPU 0 (xgmi), every device wait bounded; returns
     rank 0's report."""
     import json
@@ -357,7 +363,7 @@ def _two_ranks_one_gpu(root, tmp_path, binary_name, params, extra_env=None, iter
                    **(extra_env or {}))
         out = str(tmp_path / f"r{r}.json")
         procs.append(subprocess.Popen(
-            [binary, model, *params, root, "--backend", "xgmi", "--devices", "0,0", "--comm-cus",
+            [binary, model, *params, base or root, "--backend", "xgmi", "--devices", "0,0", "--comm-cus",
              "160", "--rccl-max-ctas", "8", "--compute", "gemm", "--graph", "-w", "3", "-r", str(iters),
              "--time-scale", time_scale, "--quiet", "--silent", "--json", out], env=env, stdout=subprocess.PIPE,
             stderr=subprocess.PIPE, text=True))
@@ -387,10 +393,29 @@ def test_pipeline_lanes_two_ranks_one_gpu(root, tmp_path):
     assert not single["global"]["dlnb"]["lane_graphs"]["enabled"]
     assert d["iteration"]["median_ms"] < single["global"]["dlnb"]["iteration"]["median_ms"], (d["iteration"],
                                                                                               single["global"]["dlnb"]["iteration"])
-    # TP collectives between the compute tasks (T = 2): the single graph, with the reason
+    # TP collectives between the compute tasks (T = 2): on the inner lane, so lanes too
     tp = _two_ranks_one_gpu(root, tmp_path, "hybrid_3d", ["1", "4", "2"])
     lg = tp["global"]["dlnb"]["lane_graphs"]
-    assert not lg["enabled"] and "program" in lg["reason"], lg
+    assert lg["enabled"] and lg["linear"], lg
+
+
+@pytest.mark.parametrize("binary,model,params,scale", [("hybrid_3d", "llama3_8b_16_bfloat16", ["1", "4", "2"], "0.05"),
+                                                       ("hybrid_3d_moe", "slow_moe_8_bfloat16", ["1", "8", "2"], "1")])
+def test_tp_ep_lanes_two_ranks_one_gpu(binary, model, params, scale, root, data_dir, tmp_path):
+    """with the TP all-reduces / EP all-to-alls on the inner lane (the compute lane carries only
+    compute tasks and their waits), hybrid_3d 1 4 2 and hybrid_3d_moe 1 8 2 on 2 ranks sharing GPU 0 replay
+    linear lane graphs with no gate timeout, and no slower than the single graph."""
+    kw = dict(model=model, time_scale=scale, base=data_dir if model.startswith("slow") else root)
+    lanes = _two_ranks_one_gpu(root, tmp_path, binary, params, **kw)
+    d = lanes["global"]["dlnb"]
+    lg = d["lane_graphs"]
+    assert lg["enabled"] and lg["linear"], lg
+    cc = d["chain_capped"]
+    assert cc["gate_wait_timeouts_max"] == 0 and cc["compute_gate_timeouts_max"] == 0, cc
+    single = _two_ranks_one_gpu(root, tmp_path, binary, params, {"DLNB_LANE_GRAPHS": "0"}, **kw)
+    assert not single["global"]["dlnb"]["lane_graphs"]["enabled"]
+    m_l, m_s = d["iteration"]["median_ms"], single["global"]["dlnb"]["iteration"]["median_ms"]
+    assert m_l <= m_s * 1.005, (m_l, m_s)
 
 
 def test_cp_stall_timers_two_ranks_one_gpu(root, tmp_path):
