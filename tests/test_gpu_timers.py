@@ -23,6 +23,7 @@ from dlnetbench_amd import engine  # noqa: E402
 X_US = 500.0
 X_MS = X_US / 1e3
 TOL_MS = 0.03
+TOL_EAGER_MS = 0.06
 MODES = ["lanes", "single", "eager"]
 COMPUTE = ["gemm", "gemm-work"]
 
@@ -67,6 +68,12 @@ def _one_rank(strategy, model, params, mode, compute, fault, time_scale=None, ru
                              graph=mode != "eager", time_scale=time_scale, quiet=True, env=env, **kw)
 
 
+def _tol(doc):
+    """Eager mode puts the host's enqueue on the critical path: a task's launch can trail the end of the wait
+    before it by host jitter (tens of us, both runs), so the rise of a wait is checked to TOL_EAGER_MS there."""
+    return TOL_MS if doc["global"]["dlnb"].get("graph") else TOL_EAGER_MS
+
+
 def _check(base, slow, cases, dispatch_ms=0.25):
     """cases: (wait timer, its entry in the iteration, the delayed collective's duration timer, its entry,
     ranks). The wait entry rises by the duration entry's rise (+-TOL_MS); that rise is X plus at most the idle
@@ -81,7 +88,7 @@ def _check(base, slow, cases, dispatch_ms=0.25):
                 entry_mean(base, dur[0], di, dur[1] if dur[1] is not None else rank)
             w = entry_mean(slow, wait, wi, rank) - entry_mean(base, wait, wi, rank)
             assert X_MS - 0.05 <= d <= X_MS + dispatch_ms, (dur, rank, d)
-            assert abs(w - d) <= TOL_MS, (wait, rank, w, d, entries(base, wait, rank)[0][:8])
+            assert abs(w - d) <= _tol(slow), (wait, rank, w, d, entries(base, wait, rank)[0][:8])
 
 
 @pytest.mark.parametrize("compute", COMPUTE)
@@ -134,6 +141,7 @@ def test_fsdp_timers_rise_by_the_delay(mode, compute):
 
 
 HOPS_MS = 0.3
+HOPS_EAGER_MS = 0.5
 
 
 def _check_same_run(slow, cases, lower_ms=-TOL_MS):
@@ -145,15 +153,20 @@ def _check_same_run(slow, cases, lower_ms=-TOL_MS):
     after the handing task's end, the next task's start after the collective's end: HOPS_MS - 50-150 us each
     with two processes' kernels on one GPU), and never less (an under-read wait, as a stamp run after the
     collective, comes out below it). lower_ms: the first wait of an iteration in lane graphs is timed from the
-    compute lane's start, its receive from the receive lane's start; two lanes start up to ~0.1 ms apart."""
+    compute lane's start, its receive from the receive lane's start; two lanes start up to ~0.1 ms apart.
+    The first timed iteration is left out (its lanes start from the warmup's tail); eager, the hops are host
+    launches (HOPS_EAGER_MS). dur: one timer, or a tuple of timers whose entries add up (collectives queued
+    back to back on one lane)."""
+    hops = HOPS_MS if slow["global"]["dlnb"].get("graph") else HOPS_EAGER_MS
     for r in slow["ranks"]:
         assert "timer_negative_intervals" not in r, r["timer_negative_intervals"]
     for wait, wi, dur, di, ranks in cases:
         for rank in ranks:
-            w = [it[wi] for it in entries(slow, wait, rank)]
-            d = [it[di] for it in entries(slow, dur, rank)]
+            w = [it[wi] for it in entries(slow, wait, rank)][1:]
+            durs = dur if isinstance(dur, tuple) else (dur,)
+            d = [sum(v) for v in zip(*([it[di] for it in entries(slow, k, rank)][1:] for k in durs))]
             assert sum(d) / len(d) >= X_MS - 0.02, (dur, rank, d)
-            assert all(lower_ms <= a - b <= HOPS_MS for a, b in zip(w, d)), (wait, rank, w, d)
+            assert all(lower_ms <= a - b <= hops for a, b in zip(w, d)), (wait, rank, w, d)
 
 
 def _free_port():
@@ -235,7 +248,8 @@ def test_ep_timers_rise_by_the_delay(mode, compute):
     base = _one_rank("hybrid_3d_moe", "slow_moe_8_bfloat16", (1, 8, 1), mode, compute, None, **kw)
     slow = _one_rank("hybrid_3d_moe", "slow_moe_8_bfloat16", (1, 8, 1), mode, compute, fault, **kw)
     _check(base, slow, [("ep_comm_time", 0, ("ep_a2a_time", 0), 0, (0,))])
-    _check_same_run(slow, [("dp_exposed_time", 0, "dp_ep_comm_time", 0, (0,))])
+    # (the 1-rank DP all-reduce follows the EP all-reduce on the lane)
+    _check_same_run(slow, [("dp_exposed_time", 0, ("dp_ep_comm_time", "dp_comm_time"), 0, (0,))])
 
 
 # Pipeline and context parallelism need two ranks: both share GPU 0 (_check_same_run).
