@@ -473,6 +473,31 @@ def _per_run_ms(d: dict) -> list:
     return [round(x * 1e3, 3) for x in d["global"]["dlnb"]["iteration"].get("per_run_max_s", [])]
 
 
+def _slow_iterations(d: dict, margin_ms: float = 0.1) -> Optional[Dict[str, Any]]:
+    """Attribution of the iterations slower than median + margin: per timed iteration the
+    slowest rank's time, that rank's last collective's duration and its GPU's sclk (at the iteration's end,
+    and the lowest 5-ms sample inside it) and power at the end (hwmon)."""
+    per = _per_run_ms(d)
+    if not per:
+        return None
+    ranks = d.get("ranks") or []
+    slow_rank = (_rank_ms(d) or {}).get("slowest_rank", 0)
+    r = next((x for x in ranks if x.get("rank", 0) == slow_rank), ranks[0] if ranks else {})
+
+    def col(key, scale=1.0, nd=3):
+        v = r.get(key)
+        return [round(x * scale, nd) for x in v] if isinstance(v, list) and len(v) == len(per) else None
+
+    med = sorted(per)[len(per) // 2]
+    out = {"rank": slow_rank, "median_ms": med, "max_minus_median_ms": round(max(per) - med, 3),
+           "last_collective": r.get("iteration_last_collective"),
+           "last_collective_ms": col("iteration_last_collective_ms"),
+           "sclk_mhz": col("iteration_sclk_mhz", nd=0), "sclk_min_mhz": col("iteration_sclk_min_mhz", nd=0),
+           "power_w": col("iteration_power_w", nd=1)}
+    out["slow"] = [i for i, x in enumerate(per) if x > med + margin_ms]
+    return out
+
+
 def _hybrid_block(a: argparse.Namespace, world: int, rank: int, tag: str, strategy: str, model: str,
                   params: tuple, floor_note: str, budget: "_Budget", est: "_Estimator", runs: int,
                   ep_overlap: bool = False) -> Dict[str, Any]:
@@ -725,7 +750,12 @@ def _c5_blocks(a: argparse.Namespace, world: int, rank: int, budget: _Budget, es
                     v = {"bucket_ratio": a.c5_bucket_ratio, **v}
                 if key == "gemm_work":
                     v.pop("allreduce_busbw_GBps")
-                    v["compute_stretch"] = d["global"]["dlnb"].get("compute_stretch")
+                    v["compute_stretch"] = st = d["global"]["dlnb"].get("compute_stretch")
+                    it = d["global"]["dlnb"]["iteration"]
+                    if st:
+                        # the step's excess over the compute it actually ran (the floor stretched by the
+                        # collectives beside it): what exposed_comm_ms (the device-timed tail) must explain
+                        v["step_minus_stretched_floor_ms"] = round(it["median_ms"] - it["compute_floor_ms"] * st, 4)
                 c5[key] = v
         except _Skip:
             c5[key] = _skipped(budget)
@@ -1046,6 +1076,7 @@ def main() -> int:
             "prearm": g["dlnb"].get("prearm"),
             "median_ms": round(it["median_ms"], 3),
             "per_run_ms": _per_run_ms(doc),
+            "slow_iterations": _slow_iterations(doc),
             # every rank's mean iteration (ms): at N > 1 the straggler and the spread behind the max
             "rank_ms": _rank_ms(doc),
             "baseline_ms": BASELINE_MS,

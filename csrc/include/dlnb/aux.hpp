@@ -40,6 +40,17 @@ class EnergyMeter {
   virtual bool available() const { return false; }
   virtual double joules() { return 0.0; }  // monotonically increasing counter
   virtual std::string source() const { return "none"; }
+  // Clock / power sensors sampled with the energy (hwmon: every 5 ms by the
+  // sampler thread; nothing is read on the caller's thread). take() returns
+  // the latest readings and the lowest / highest sclk since the last take()
+  // (the iteration that just ended), false when there are none.
+  struct Sensors {
+    double sclk_mhz = 0, sclk_min_mhz = 0, sclk_max_mhz = 0, power_w = 0;
+  };
+  virtual bool take(Sensors& out) {
+    (void)out;
+    return false;
+  }
 };
 
 class Tracer {

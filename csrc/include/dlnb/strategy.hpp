@@ -108,6 +108,9 @@ class Strategy {
   virtual double compute_floor_us(const Context& ctx) const {
     return ctx.stats.avg_forward_time_us + ctx.stats.avg_backward_time_us;
   }
+  // The timer of the iteration's last collective (the runner reports its
+  // last entry per timed iteration: iteration_last_collective_ms).
+  virtual std::string tail_collective_timer() const { return ""; }
   TimerSet* timers() { return timers_.get(); }
 
  protected:

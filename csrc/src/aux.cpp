@@ -11,6 +11,9 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <algorithm>
 #include <thread>
 
 #include "dlnb/common.hpp"
@@ -109,25 +112,35 @@ class HwmonMeter : public EnergyMeter {
     }
     closedir(d);
     if (hw.empty()) return false;
-    for (const char* f : {"energy1_input"}) {
-      double v;
-      if (read_num(hw + "/" + f, v)) {
-        energy_path_ = hw + "/" + f;
-        src_ = "hwmon " + energy_path_;
-        return true;
-      }
+    double v;
+    if (read_num(hw + "/energy1_input", v)) {
+      energy_path_ = hw + "/energy1_input";
+      src_ = "hwmon " + energy_path_;
     }
     for (const char* f : {"power1_average", "power1_input"}) {
-      double v;
       if (read_num(hw + "/" + f, v)) {
         power_path_ = hw + "/" + f;
-        src_ = "hwmon " + power_path_ + " sampled every 5 ms";
-        stop_ = false;
-        th_ = std::thread([this] { sample(); });
-        return true;
+        if (energy_path_.empty()) src_ = "hwmon " + power_path_ + " sampled every 5 ms";
+        break;
       }
     }
-    return false;
+    // sclk: hwmon freq1_input (Hz), else the device's pp_dpm_sclk (the level
+    // marked '*', MHz)
+    if (read_num(hw + "/freq1_input", v))
+      sclk_path_ = hw + "/freq1_input";
+    else if (read_dpm(std::string("/sys/bus/pci/devices/") + b + "/pp_dpm_sclk", v))
+      dpm_path_ = std::string("/sys/bus/pci/devices/") + b + "/pp_dpm_sclk";
+    if (energy_path_.empty() && power_path_.empty()) return false;
+    stop_ = false;
+    th_ = std::thread([this] { sample(); });
+    return true;
+  }
+  bool take(Sensors& out) override {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!have_) return false;
+    out = cur_;
+    cur_.sclk_min_mhz = cur_.sclk_max_mhz = cur_.sclk_mhz;  // the next window starts at the latest reading
+    return true;
   }
   ~HwmonMeter() override {
     stop_ = true;
@@ -145,11 +158,35 @@ class HwmonMeter : public EnergyMeter {
 
  private:
   static bool read_num(const std::string& p, double& v) {
+    if (p.empty()) return false;
     FILE* f = std::fopen(p.c_str(), "r");
     if (!f) return false;
     bool ok = std::fscanf(f, "%lf", &v) == 1;
     std::fclose(f);
     return ok;
+  }
+  // "1: 2400Mhz *" -> 2400
+  static bool read_dpm(const std::string& p, double& mhz) {
+    FILE* f = std::fopen(p.c_str(), "r");
+    if (!f) return false;
+    char line[128];
+    bool ok = false;
+    while (std::fgets(line, sizeof(line), f)) {
+      if (!std::strchr(line, '*')) continue;
+      const char* c = std::strchr(line, ':');
+      ok = c && std::sscanf(c + 1, "%lf", &mhz) == 1;
+      break;
+    }
+    std::fclose(f);
+    return ok;
+  }
+  bool read_sclk(double& mhz) const {
+    double v;
+    if (read_num(sclk_path_, v)) {
+      mhz = v * 1e-6;
+      return true;
+    }
+    return !dpm_path_.empty() && read_dpm(dpm_path_, mhz);
   }
   void sample() {
     auto last = std::chrono::steady_clock::now();
@@ -162,12 +199,26 @@ class HwmonMeter : public EnergyMeter {
       double w = last_w;
       if (read_num(power_path_, v)) w = v * 1e-6;
       double dt = std::chrono::duration<double>(now - last).count();
-      acc_j_.store(acc_j_.load() + 0.5 * (w + last_w) * dt);
+      if (energy_path_.empty()) acc_j_.store(acc_j_.load() + 0.5 * (w + last_w) * dt);
       last = now;
       last_w = w;
+      double mhz = 0;
+      const bool clk = read_sclk(mhz);
+      std::lock_guard<std::mutex> g(mu_);
+      cur_.power_w = w;
+      if (clk) {
+        if (!have_) cur_.sclk_min_mhz = cur_.sclk_max_mhz = mhz;
+        cur_.sclk_mhz = mhz;
+        cur_.sclk_min_mhz = std::min(cur_.sclk_min_mhz, mhz);
+        cur_.sclk_max_mhz = std::max(cur_.sclk_max_mhz, mhz);
+      }
+      have_ = true;
     }
   }
-  std::string energy_path_, power_path_, src_;
+  std::string energy_path_, power_path_, sclk_path_, dpm_path_, src_;
+  std::mutex mu_;
+  Sensors cur_;
+  bool have_ = false;
   std::atomic<bool> stop_{true};
   std::atomic<double> acc_j_{0.0};
   std::thread th_;

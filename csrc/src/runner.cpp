@@ -1121,6 +1121,13 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
   // blocks on the runtime shows up here (profiles/stall_r5.md)
   std::vector<double> arm_s;
   if (hs && runs > 0) arm(0);  // submitted, held until the first go
+  // clock / power at each iteration's end (the sampler thread's latest
+  // readings, and sclk's range over the iteration: VERDICT r5 #7)
+  std::vector<EnergyMeter::Sensors> sensors;
+  {
+    EnergyMeter::Sensors s0;
+    meter->take(s0);  // the first window starts here
+  }
   const double T0 = now_s();
   for (int r = 0; r < runs; ++r) {
     fault.at_iteration(iter_no++, inject_task);
@@ -1154,6 +1161,8 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       TL->host_iteration(r, t0, t1);
     }
     if (meter->available()) T.add("energy_consumed", meter->joules() - j0);
+    EnergyMeter::Sensors sn;
+    if (meter->take(sn)) sensors.push_back(sn);
   }
   ctx.dev->synchronize();
   ctx.hg().barrier();
@@ -1168,6 +1177,31 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
     rank["prearm_launch_ms"] = a;
   }
   rank["energy_consumed"] = T.values_json("energy_consumed");
+  if (!sensors.empty()) {
+    Json c = Json::array(), lo = Json::array(), hi = Json::array(), w = Json::array();
+    for (const auto& x : sensors) {
+      c.push_back(x.sclk_mhz);
+      lo.push_back(x.sclk_min_mhz);
+      hi.push_back(x.sclk_max_mhz);
+      w.push_back(x.power_w);
+    }
+    rank["iteration_sclk_mhz"] = c;
+    rank["iteration_sclk_min_mhz"] = lo;
+    rank["iteration_sclk_max_mhz"] = hi;
+    rank["iteration_power_w"] = w;
+  }
+  {
+    // the duration of each timed iteration's last collective (ms)
+    const std::string tk = strat->tail_collective_timer();
+    const auto& v = tk.empty() ? std::vector<double>() : T.get(tk);
+    if (runs > 0 && !v.empty() && v.size() % static_cast<size_t>(runs) == 0) {
+      const size_t per = v.size() / static_cast<size_t>(runs);
+      Json a = Json::array();
+      for (int r = 0; r < runs; ++r) a.push_back(v[(static_cast<size_t>(r) + 1) * per - 1] * 1e3);
+      rank["iteration_last_collective_ms"] = a;
+      rank["iteration_last_collective"] = tk;
+    }
+  }
   {
     // chained deadline tasks: lateness absorbed (<= the cap each) and beyond
     // the cap (deadline_sync.hpp), gate waits that timed out

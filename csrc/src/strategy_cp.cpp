@@ -251,6 +251,7 @@ class ContextParallel : public Strategy {
     timers_->resolve();
   }
 
+  std::string tail_collective_timer() const override { return "dp_comm_time"; }
   std::string section_id() const override { return "dp_cp"; }
   std::string section_title() const override { return "Data + Context Parallelism"; }
 

@@ -312,6 +312,9 @@ class DataParallel : public Strategy {
     timers_->resolve();
   }
 
+  std::string tail_collective_timer() const override {
+    return zero_ ? "param_allgather_time" : "allreduce_time";
+  }
   std::string section_id() const override { return "dp"; }
   std::string section_title() const override { return "Data Parallelism"; }
 

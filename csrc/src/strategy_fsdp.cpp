@@ -318,6 +318,7 @@ class Fsdp : public Strategy {
     timers_->resolve();
   }
 
+  std::string tail_collective_timer() const override { return R_ > 1 ? "allreduce_time" : "reduce_scatter"; }
   std::string section_id() const override { return "fsdp"; }
   std::string section_title() const override { return "FSDP metrics"; }
   const char* runtime_key() const override { return "runtime"; }

@@ -1073,6 +1073,7 @@ class Pipeline : public Strategy {
     return (mb_ + static_cast<double>(S_ - 1) / V_) * (fwd_mb_us_ + bwd_mb_us_);
   }
 
+  std::string tail_collective_timer() const override { return "dp_comm_time"; }
   std::string section_id() const override {
     return kind_ == StrategyKind::Hybrid2D      ? "dp_pp"
            : kind_ == StrategyKind::Hybrid3D    ? "dp_pp_tp"
