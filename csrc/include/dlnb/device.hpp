@@ -189,6 +189,18 @@ class Device {
     return false;
   }
   virtual bool gate_events() const { return false; }
+  // Gate events folded into a consumer instead of gate kernels on s: while a
+  // fold is installed on s (a compute program open on it, ComputeEngine),
+  // s.wait(e) hands the gate and tag to wait for to fold_wait (nothing when
+  // there is nothing to wait for: e never recorded, recorded on s, or before
+  // this capture) and s.record(e) hands e to fold_record, which arms it
+  // (arm_gate_record) for a kernel it launches on s. nullptr removes it.
+  struct StreamFold {
+    virtual ~StreamFold() = default;
+    virtual void fold_wait(const uint64_t* gate, uint32_t tag) = 0;
+    virtual void fold_record(Event& e) = 0;
+  };
+  virtual void set_stream_fold(Stream& s, StreamFold* f) { (void)s; (void)f; }
   // Enqueue on s a store of the iteration word into *host_word (alloc_stamps
   // memory): the last node of a lane graph, so the host sees the lane done
   // without waiting for the graph's own completion (GPU only).

@@ -77,15 +77,21 @@ struct DlSync {
 //     K-tiles, however long that takes; it starts once the program's previous
 //     task is complete on every block (and its gates are up), the last block
 //     to finish stores the end time into *tend and raises the done gate, or
-//   * the join (ticks == 0, no work): the program's last task (dl::join).
+//   * a gate-only task (flags & kTaskGateOnly): the start protocol (its
+//     gates), no compute, then its done gate - a wait or an event record of
+//     the program's stream between two tasks (ComputeEngine folds them into
+//     the program: Device::StreamFold); ticks 1 in a deadline program (the
+//     stream's chain continues from when the gates opened), 0 in fixed work;
+//   * the join (ticks == 0, no work, no flag): the program's last task (dl::join).
 // epoch: the task's index among the stream's program tasks of the iteration.
+constexpr uint32_t kTaskGateOnly = 1;
 struct DlTask {
   DlSync sync;
   uint64_t ticks = 0;
   uint32_t epoch = 0;
   uint32_t work_rounds = 0;
   uint32_t tail_kt = 0;
-  uint32_t pad = 0;
+  uint32_t flags = 0;
   uint64_t* tend = nullptr;  // fixed-work: end stamp (host-mapped or device memory; nullptr: none)
 };
 // Device gates: two words {seq, time} in device memory (16-byte aligned).

@@ -84,6 +84,11 @@ class TimerSet {
   // gradient all-reduce queued behind it on the same lane: the compute
   // stream's wait for the all-reduce is not booked on the all-to-all.
   void settle(Stream& s, const uint64_t* op_end);
+  // s does not wait for the operation that ends at `end` (another stream's
+  // end stamp) - the iteration does (a lane join): `name` is the time from
+  // s's reference (its last task's end, or settle's floor) to `end`, clamped.
+  // Nothing is enqueued on s. Needs task stamps.
+  void stall_until(Stream& s, const uint64_t* end, const std::string& name);
   // A stamp heading the iteration on s (the runner, before the strategy's
   // enqueue; in a single graph the head node every stream's chain follows):
   // s's first wait with no task before it is timed from there, not from a

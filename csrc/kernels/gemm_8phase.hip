@@ -407,7 +407,7 @@ __global__ void __launch_bounds__(512, 1)
       bool fixed = false;
       if (prog) {
         d.ticks = d.slice_end = prog[k].ticks;  // a uniform (scalar) load: stays in SGPRs
-        fixed = d.ticks == 0 && (prog[k].work_rounds | prog[k].tail_kt) != 0;
+        fixed = d.ticks == 0 && (prog[k].work_rounds | prog[k].tail_kt | prog[k].flags) != 0;
         if (d.ticks == 0 && !fixed) {  // the join task (the program's last)
           if (blockIdx.x == 0 && tid == 0) dl::join(prog[k].sync);
           return;
@@ -435,6 +435,11 @@ __global__ void __launch_bounds__(512, 1)
           ++round;
         }
         if (tid == 0) dl::fixed_done(slot, prog[k].sync, prog[k].tend);
+        if (k + 1 >= ntasks) return;
+        continue;
+      }
+      if (prog && (prog[k].flags & kTaskGateOnly)) {  // its gates, then its done gate: no tiles
+        dl::task_done(prog[k].sync);
         if (k + 1 >= ntasks) return;
         continue;
       }

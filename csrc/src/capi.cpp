@@ -149,6 +149,7 @@ struct dlnb_task_desc {
   unsigned tail_kt;
   unsigned epoch;  // index among the program's tasks
   void* tend;
+  unsigned flags;  // kernels::kTaskGateOnly: a gate-only task
 };
 
 int dlnb_task_size() { return static_cast<int>(sizeof(dlnb::kernels::DlTask)); }
@@ -173,6 +174,7 @@ int dlnb_gemm_program(const void* A, const void* B, void* C, int M, int N, int K
       t.epoch = d[i].epoch;
       t.work_rounds = d[i].work_rounds;
       t.tail_kt = d[i].tail_kt;
+      t.flags = d[i].flags;
       t.tend = static_cast<uint64_t*>(d[i].tend);
       t.sync.chain = static_cast<uint32_t>(d[i].chain_ticks);
       t.sync.gate[0] = static_cast<const uint64_t*>(d[i].gate0);

@@ -198,12 +198,24 @@ class GpuCompute : public ComputeEngine {
     p.open = true;
     p.index = 0;
     p.tasks.clear();
+    p.pending.clear();
+    p.done_free = false;
+    if (dev_.gate_events()) {
+      // the stream's gate-event waits and records between the tasks become
+      // the tasks' gates and done gates (gate-only tasks where none fits):
+      // no gate kernel on the stream while its program is being built
+      p.fold.e = this;
+      p.fold.s = &s;
+      dev_.set_stream_fold(s, &p.fold);
+    }
     return true;
   }
   void end_program(Stream& s, bool join_ok) override {
     auto it = programs_.find(&s);
     if (it == programs_.end() || !it->second.open) return;
     Program& p = it->second;
+    dev_.set_stream_fold(s, nullptr);
+    emit_pending(s, p, nullptr, 0);  // waits after the last task: before the join
     auto j = joins_.find(&s);
     if (j != joins_.end() && !p.tasks.empty() && join_ok) {
       // the join task(s): up to two gates each, the last one stores the done word
@@ -359,7 +371,12 @@ class GpuCompute : public ComputeEngine {
   // Launch the open program's tasks so far (it stays open for the tasks after).
   void flush_program(Stream& s) {
     auto it = programs_.find(&s);
-    if (it == programs_.end() || it->second.tasks.empty()) return;
+    if (it == programs_.end()) return;
+    // folded waits not taken by a task yet: the launch ends with them (a
+    // kernel of its own follows it on the stream)
+    if (it->second.open) emit_pending(s, it->second, nullptr, 0);
+    if (it->second.tasks.empty()) return;
+    it->second.done_free = false;
     std::vector<kernels::DlTask>& ts = it->second.tasks;
     // A program whose first task waits for gates (FSDP: the iteration's first
     // all-gather) is launched only once they are up, behind one-wave gate
@@ -536,9 +553,11 @@ class GpuCompute : public ComputeEngine {
       t.sync.done_gate = dgate;
       t.sync.done_tag = dtag;
       t.ticks = total;
+      take_pending(s, pit->second, t.sync);
       DLNB_REQUIRE(pit->second.index < 4096, "more than 4096 program tasks per iteration on one stream");
       t.epoch = pit->second.index++;  // the kernel derives the epoch from it and the iteration word
       pit->second.tasks.push_back(t);
+      pit->second.done_free = t.sync.done_gate == nullptr;
       chain_live_[slot] = true;
       return;
     }
@@ -618,9 +637,11 @@ class GpuCompute : public ComputeEngine {
     auto pit = programs_.find(&s);
     if (pit != programs_.end() && pit->second.open) {
       DLNB_REQUIRE(folded || !done, "a program task's done event needs gate events");
+      take_pending(s, pit->second, t.sync);
       DLNB_REQUIRE(pit->second.index < 4096, "more than 4096 program tasks per iteration on one stream");
       t.epoch = pit->second.index++;
       pit->second.tasks.push_back(t);
+      pit->second.done_free = t.sync.done_gate == nullptr;
     } else {
       // a launch of its own (a one-task program with an epoch of its own):
       // the gates' one-wave waits first, as for a program's first task
@@ -740,11 +761,109 @@ class GpuCompute : public ComputeEngine {
   Buffer counters_;  // kernels::DlCounter words (DlSync::counters)
   // programs: the open task list per stream, the device ring their task lists
   // live in, uploads deferred past a graph capture
+  struct Fold : Device::StreamFold {
+    GpuCompute* e = nullptr;
+    Stream* s = nullptr;
+    void fold_wait(const uint64_t* gate, uint32_t tag) override { e->fold_wait(*s, gate, tag); }
+    void fold_record(Event& ev) override { e->fold_record(*s, ev); }
+  };
   struct Program {
     bool open = false;
     uint32_t index = 0;  // program tasks of the iteration so far (DlTask::epoch)
     std::vector<kernels::DlTask> tasks;
+    // folded gate-event waits (gate, tag) the next task takes as its gates
+    std::vector<std::pair<const uint64_t*, uint32_t>> pending;
+    bool done_free = false;  // tasks.back() has no done gate: a record right after it takes that one
+    Fold fold;
   };
+
+  // ---- gate events folded into the open program (Device::StreamFold)
+  void fold_wait(Stream& s, const uint64_t* gate, uint32_t tag) {
+    Program& p = programs_[&s];
+    for (auto& w : p.pending)
+      if (w.first == gate) {  // the same gate again: its latest record
+        w.second = tag;
+        return;
+      }
+    p.pending.emplace_back(gate, tag);
+  }
+  void fold_record(Stream& s, Event& ev) {
+    Program& p = programs_[&s];
+    uint64_t* g = nullptr;
+    uint32_t tag = 0;
+    DLNB_REQUIRE(dev_.arm_gate_record(ev, s, &g, &tag), "fold_record: not a gate event");
+    if (p.pending.empty() && p.done_free && !p.tasks.empty()) {
+      // recorded right after a task: that task's done gate
+      p.tasks.back().sync.done_gate = g;
+      p.tasks.back().sync.done_tag = tag;
+      p.done_free = false;
+      return;
+    }
+    emit_pending(s, p, g, tag);
+    if (p.tasks.empty() || p.tasks.back().sync.done_gate != g) {
+      // nothing pending and no task to carry it: a gate-only task raises it
+      kernels::DlTask t = gate_task();
+      t.sync.done_gate = g;
+      t.sync.done_tag = tag;
+      push_task(p, t);
+    }
+    p.done_free = false;
+  }
+  kernels::DlTask gate_task() const {
+    kernels::DlTask t;
+    t.sync.iter = dev_.iter_word();
+    t.sync.counters = counters_.as<uint64_t>();
+    t.sync.gate_timeout = gate_timeout_ticks_;
+    t.sync.abort = dev_.abort_word();
+    t.ticks = fixed_ ? 0 : 1;  // (deadline: the stream's chain goes on from when its gates opened)
+    t.flags = kernels::kTaskGateOnly;
+    return t;
+  }
+  void push_task(Program& p, const kernels::DlTask& t) {
+    DLNB_REQUIRE(p.index < 4096, "more than 4096 program tasks per iteration on one stream");
+    kernels::DlTask c = t;
+    c.epoch = p.index++;
+    p.tasks.push_back(c);
+  }
+  // The pending waits as gate-only tasks (two gates each); the last one
+  // raises done_gate when given.
+  void emit_pending(Stream& s, Program& p, uint64_t* done_gate, uint32_t done_tag) {
+    (void)s;
+    while (!p.pending.empty()) {
+      kernels::DlTask t = gate_task();
+      for (int i = 0; i < 2 && !p.pending.empty(); ++i) {
+        t.sync.gate[i] = p.pending.front().first;
+        t.sync.tag[i] = p.pending.front().second;
+        p.pending.erase(p.pending.begin());
+      }
+      if (p.pending.empty() && done_gate) {
+        t.sync.done_gate = done_gate;
+        t.sync.done_tag = done_tag;
+      }
+      push_task(p, t);
+      p.done_free = false;
+    }
+  }
+  // A task about to join the program takes the pending waits as its gates
+  // (those beyond its free gate slots go to gate-only tasks before it).
+  void take_pending(Stream& s, Program& p, kernels::DlSync& sync) {
+    if (p.pending.empty()) return;
+    const size_t free_slots = (sync.gate[0] ? 0u : 1u) + (sync.gate[1] ? 0u : 1u);
+    if (p.pending.size() > free_slots) {
+      // keep the last free_slots for the task, the rest before it
+      std::vector<std::pair<const uint64_t*, uint32_t>> keep(p.pending.end() - static_cast<long>(free_slots),
+                                                             p.pending.end());
+      p.pending.resize(p.pending.size() - free_slots);
+      emit_pending(s, p, nullptr, 0);
+      p.pending = keep;
+    }
+    for (int i = 0; i < 2 && !p.pending.empty(); ++i) {
+      if (sync.gate[i]) continue;
+      sync.gate[i] = p.pending.front().first;
+      sync.tag[i] = p.pending.front().second;
+      p.pending.erase(p.pending.begin());
+    }
+  }
   std::map<Stream*, Program> programs_;
   struct Join {
     std::vector<uint64_t*> gates;

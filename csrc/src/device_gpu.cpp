@@ -92,6 +92,7 @@ class GpuStream : public Stream {
   }
   void* native() override { return s; }
   hipStream_t s{};
+  Device::StreamFold* fold = nullptr;  // Device::set_stream_fold
 
  private:
   std::shared_ptr<GpuStreamSet> set_;
@@ -337,16 +338,25 @@ class GpuDevice : public Device {
     *tag = e.tag;
     return true;
   }
-  void gate_wait(GpuEvent& e, hipStream_t s) {
-    if (e.tag == 0) return;  // never recorded: nothing to wait for (as a HIP event)
-    if (e.on == s) return;   // recorded on this stream: already ordered
+  // Whether a wait on s for e's latest gate record must wait at all.
+  bool gate_needed(const GpuEvent& e, hipStream_t s) const {
+    if (e.tag == 0) return false;  // never recorded: nothing to wait for (as a HIP event)
+    if (e.on == s) return false;   // recorded on this stream: already ordered
     // recorded before this capture began (a previous iteration's record): in a
     // replay its gate carries the previous iteration's sequence number and
     // would never match - as a HIP event outside the capture, nothing to wait
     // for inside the graph
-    if (e.gen != gen_) return;
-    kernels::gate_wait(e.gate, iter_word(), e.tag, gate_timeout_ticks(), pool_ + 1, s, abort_dev_);
+    return e.gen == gen_;
   }
+  void gate_wait(GpuEvent& e, GpuStream& st) {
+    if (!gate_needed(e, st.s)) return;
+    if (st.fold) {
+      st.fold->fold_wait(e.gate, e.tag);
+      return;
+    }
+    kernels::gate_wait(e.gate, iter_word(), e.tag, gate_timeout_ticks(), pool_ + 1, st.s, abort_dev_);
+  }
+  void set_stream_fold(Stream& s, StreamFold* f) override { static_cast<GpuStream&>(s).fold = f; }
   bool queues_independent(const std::vector<Stream*>& ss, double timeout_s, std::string* detail) override {
     const uint64_t t = static_cast<uint64_t>(timeout_s * stamp_hz());
     bool ok = true;
@@ -462,7 +472,10 @@ class GpuDevice : public Device {
 void GpuStream::record(Event& e) {
   auto& g = static_cast<GpuEvent&>(e);
   if (g.dev && g.dev->gate_events()) {
-    g.dev->gate_record(g, s);
+    if (fold)
+      fold->fold_record(e);
+    else
+      g.dev->gate_record(g, s);
     return;
   }
   DLNB_HIP_CHECK(hipEventRecord(g.ev, s));
@@ -471,7 +484,7 @@ void GpuStream::record(Event& e) {
 void GpuStream::wait(Event& e) {
   auto& g = static_cast<GpuEvent&>(e);
   if (g.dev && g.dev->gate_events()) {
-    g.dev->gate_wait(g, s);
+    g.dev->gate_wait(g, *this);
     return;
   }
   DLNB_HIP_CHECK(hipStreamWaitEvent(s, g.ev, 0));

@@ -227,7 +227,11 @@ class Pipeline : public Strategy {
       if (has_tp_) {
         std::vector<int> m;
         for (int t = 0; t < T_; ++t) m.push_back(base + ep_id_ * T_ + t);
-        tp_comm_ = ctx.comms->create("tp/" + where + "/" + std::to_string(ep_id_), m, tp_shard_ * T_ * es_, false);
+        // T > 1: the compute waits for every TP all-reduce, so it gets the
+        // backend's own CTA count (no compute program holds the CUs meanwhile:
+        // program_ok()); a 1-rank group (a copy) stays in the lane budget
+        tp_comm_ = ctx.comms->create("tp/" + where + "/" + std::to_string(ep_id_), m, tp_shard_ * T_ * es_, false,
+                                     T_ > 1 ? 0 : ctx.lane_ctas);
       }
       if (has_ep_) {
         std::vector<int> m;
@@ -235,7 +239,7 @@ class Pipeline : public Strategy {
         const uint64_t cap = skew_counts_.empty() ? a2a_ * E_ : std::max<uint64_t>(a2a_ * E_, skew_counts_[0]);
         ep_comm_ = ctx.comms->create("ep/" + where + "/" + std::to_string(tp_id_), m,
                                      std::max<uint64_t>(cap, ne_) * es_, !skew_counts_.empty(),
-                                     o.ep_overlap ? ctx.lane_ctas : 0);  // --ep-overlap: on the DP lane
+                                     o.ep_overlap || E_ == 1 ? ctx.lane_ctas : 0);  // (as TP's)
       }
     }
     {
@@ -606,7 +610,8 @@ class Pipeline : public Strategy {
       int tk = timers_->begin(es);
       void* out = ctx.opt.in_place ? grad_.data() : sum_grad_.data();
       ep_comm_->all_reduce(grad_.data(), out, ne_, t, es);
-      timers_->end(tk, es, "dp_ep_comm_time");
+      const uint64_t* e = timers_->end(tk, es, "dp_ep_comm_time");
+      if (&es == dp_stream_.get()) dp_end_ = e;
     }
     if (nbk == 1 || reference_) {
       compute_->record(*bucket_ready_[0]);
@@ -615,7 +620,7 @@ class Pipeline : public Strategy {
         // MoE: the whole pair gradient after the EP all-reduce
         int tm = timers_->begin(*dp_stream_);
         mirror_comm_->all_reduce(grad_.data(), grad_.data(), dp_ar_, t, *dp_stream_);
-        timers_->end(tm, *dp_stream_, "pp_mirror_time");
+        dp_end_ = timers_->end(tm, *dp_stream_, "pp_mirror_time");
         dp_allreduce_bucket(0, 1);
       } else if (mirror_comm_) {
         // the half whose chunks finish last (model stage min(s, S-1-s)); the
@@ -630,8 +635,20 @@ class Pipeline : public Strategy {
         dp_allreduce_bucket(0, 1);
       }
     }
-    dp_stream_->record(*dp_done_);
-    timers_->stall_after_task(*compute_, *dp_done_, "dp_exposed_time");
+    // With a compute program and nothing after it on the compute stream (no
+    // optimizer), the program's join ends the iteration once the other lanes
+    // are done, and the DP tail exposed is the DP lane's last end stamp minus
+    // the compute's last task (a gap: no wait on the compute stream);
+    // otherwise the compute stream waits for the DP lane.
+    const bool join = prog_ && !ctx.opt.optimizer && dp_end_ && timers_->task_stamps();
+    if (prog_) ctx.compute->end_program(*compute_, join);
+    prog_ = false;
+    if (join) {
+      timers_->stall_until(*compute_, dp_end_, "dp_exposed_time");
+    } else {
+      dp_stream_->record(*dp_done_);
+      timers_->stall_after_task(*compute_, *dp_done_, "dp_exposed_time");
+    }
     if (ctx.opt.optimizer) {
       void* g = ctx.opt.in_place ? grad_.data() : sum_grad_.data();
       optimizer_step(ctx, *compute_, params_.data(), mom_.data(), g, dp_ar_);
@@ -1018,6 +1035,13 @@ class Pipeline : public Strategy {
   }
 
   void enqueue_iteration() override {
+    // Lane graphs: the compute stream's tasks of the iteration are one compute
+    // program (one persistent kernel); its event waits and records - the
+    // receives', the inner lane's, the sends' and the DP buckets' - fold into
+    // the tasks' gates (Device::StreamFold), so no other kernel sits between
+    // two tasks on the compute lane
+    dp_end_ = nullptr;
+    prog_ = ctx_->dev->gate_events() && !reference_ && program_ok() && ctx_->compute->begin_program(*compute_);
     if (dualpipe_)
       enqueue_dualpipe();
     else if (interleaved_)
@@ -1036,8 +1060,18 @@ class Pipeline : public Strategy {
     void* out = ctx_->opt.in_place ? in : sum_grad_.at(off * es_);
     int tk = timers_->begin(*dp_stream_);
     dp_comm_->all_reduce(in, out, n, ctx_->wire, *dp_stream_);
-    timers_->end(tk, *dp_stream_, "dp_comm_time");
+    dp_end_ = timers_->end(tk, *dp_stream_, "dp_comm_time");
   }
+
+  // Whether the compute lane may be one compute program: not with TP or EP
+  // groups of > 1 rank. Their collectives sit on the critical path between
+  // two compute tasks (the compute waits for each), and a program keeps its
+  // grid resident through those waits, leaving the collective only the CUs
+  // reserved for communication; with one launch per task the collective gets
+  // the CUs the finished task freed. hybrid_3d 1 4 2 on two ranks sharing GPU
+  // 0 (profiles/pipeline_program_r6.md): program 82.9 ms, one launch per task
+  // 80.6, single graph 80.3 at 32 CTAs per lane.
+  bool program_ok() const { return !(has_tp_ && T_ > 1) && !(has_ep_ && E_ > 1); }
 
   std::vector<Stream*> streams() override {
     std::vector<Stream*> ss = {compute_.get(), dp_stream_.get()};
@@ -1202,6 +1236,8 @@ class Pipeline : public Strategy {
   std::vector<std::unique_ptr<Event>> recv_f_, fwd_done_, send_f_, recv_b_, bwd_done_, send_b_, bucket_ready_;
   std::unique_ptr<Event> dp_done_;
   const uint64_t* inner_end_ = nullptr;
+  const uint64_t* dp_end_ = nullptr;  // the DP lane's last end stamp of the iteration
+  bool prog_ = false;                 // the iteration's compute tasks are one compute program
   std::vector<CommStat> stats_;
 };
 

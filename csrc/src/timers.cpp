@@ -113,6 +113,15 @@ void TimerSet::stall_after_task(Stream& s, Event& e, const std::string& name) {
   restart(c, st, 0);
 }
 
+void TimerSet::stall_until(Stream& s, const uint64_t* end, const std::string& name) {
+  if (!enabled_) return;
+  DLNB_REQUIRE(task_stamps() && owns(end), "TimerSet::stall_until(" << name << ") needs task stamps");
+  TaskClock& c = clocks_[&s];
+  DLNB_REQUIRE(c.start, "TimerSet::stall_until(" << name << "): no task before it on the stream");
+  c.pending.push_back(name);
+  close_pending(c, end, true);
+}
+
 void TimerSet::iteration_start(Stream& s) {
   if (!task_stamps()) return;
   origin_ = &s;

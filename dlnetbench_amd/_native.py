@@ -30,14 +30,15 @@ class NativeError(RuntimeError):
 class TaskDesc(ctypes.Structure):
     """One task of a compute program (csrc/src/capi.cpp dlnb_task_desc ->
     kernels::DlTask): ticks > 0 a deadline task, ticks == 0 with work_rounds /
-    tail_kt a fixed-work task, neither the join."""
+    tail_kt a fixed-work task, flags = 1 a gate-only task (its gates, then its
+    done gate), none of these the join."""
     _fields_ = [("ticks", ctypes.c_ulonglong), ("chain_ticks", ctypes.c_ulonglong),
                 ("gate0", ctypes.c_void_p), ("gate1", ctypes.c_void_p),
                 ("tag0", ctypes.c_uint), ("tag1", ctypes.c_uint),
                 ("tstart0", ctypes.c_void_p), ("tstart1", ctypes.c_void_p),
                 ("done_gate", ctypes.c_void_p), ("done_tag", ctypes.c_uint),
                 ("work_rounds", ctypes.c_uint), ("tail_kt", ctypes.c_uint), ("epoch", ctypes.c_uint),
-                ("tend", ctypes.c_void_p)]
+                ("tend", ctypes.c_void_p), ("flags", ctypes.c_uint)]
 
 
 def lib() -> ctypes.CDLL:

@@ -544,31 +544,26 @@ def test_stream_task_failure_raises_in_process_and_next_run_works(data_dir):
     assert time.time() - t0 < 20
 
 
-def _mean_ms(d, key, rank=0):
-    """The median entry (ms): one late stamp of a loaded host moves a mean by tens of ms."""
-    v = sorted(d["ranks"][rank][key])
-    return v[len(v) // 2] * 1e3
-
-
 def test_comm_delay_fault_raises_exposed_timers(data_dir, monkeypatch):
     """DLNB_COMM_FAULT mode=delay (an idle task of X after the operation on its stream): a delay on the
     operation an exposed-communication timer waits for raises that timer by X - here DP's last all-reduce of
     every iteration (barrier_time) and FSDP's last reduce-scatter (barrier) on 2 CPU ranks, X = 100 ms. Several
     specs (';') hit different ops; every=N picks the K-th op of every iteration. (CPU worker threads of 2
-    ranks x 3 streams on a shared host: the stall's own stamps can run late, so the plumbing is checked
-    loosely here; tests/test_gpu_timers.py checks the device timers to 0.03 ms.)"""
-    base = run(2, "dp", "tiny_dense_8_bfloat16", 5, data_dir, "-w", 1, "-r", 4)
+    ranks x 3 streams on a shared, possibly loaded host: only the lower bounds are load-proof - the delayed
+    operation lasts >= X and the wait for it >= X; tests/test_gpu_timers.py checks the device timers to
+    0.03 ms.)"""
+    X = 100.0
     monkeypatch.setenv("DLNB_COMM_FAULT", "mode=delay,us=100000,op=all_reduce,call=4,every=5")
     slow = run(2, "dp", "tiny_dense_8_bfloat16", 5, data_dir, "-w", 1, "-r", 4)
-    rise = _mean_ms(slow, "barrier_time") - _mean_ms(base, "barrier_time")
-    assert 60.0 <= rise <= 140.0, rise
-    monkeypatch.delenv("DLNB_COMM_FAULT")
-    base_f = run(2, "fsdp", "tiny_dense_8_bfloat16", 4, 2, data_dir, "-w", 1, "-r", 4)
+    for r in slow["ranks"]:
+        ar = [x * 1e3 for x in r["allreduce_time"]]
+        assert all(ar[k] >= X for k in range(4, len(ar), 5)), ar
+        assert min(r["barrier_time"]) * 1e3 >= 0.9 * X, r["barrier_time"]
     monkeypatch.setenv("DLNB_COMM_FAULT", "mode=delay,us=100000,op=reduce_scatter,call=3,every=4;"
                                           "mode=delay,us=1000,op=all_gather,call=99999")
     slow_f = run(2, "fsdp", "tiny_dense_8_bfloat16", 4, 2, data_dir, "-w", 1, "-r", 4)
-    rise = _mean_ms(slow_f, "barrier") - _mean_ms(base_f, "barrier")
-    assert 60.0 <= rise <= 140.0, rise
+    for r in slow_f["ranks"]:
+        assert min(r["barrier"]) * 1e3 >= 0.9 * X, r["barrier"]
 
 
 def test_comm_delay_fault_argument_checks(data_dir, monkeypatch):

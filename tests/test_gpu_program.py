@@ -156,6 +156,49 @@ def test_program_gated_task_starts_at_late_gate():
     assert abs(t[2] - t[1] - _ticks(1000.0)) <= 1, t
 
 
+@pytest.mark.parametrize("fixed", [False, True])
+def test_program_gate_only_task(fixed):
+    """A gate-only task (flags = 1: a stream's event wait and record folded into its compute program) between
+    two tasks, its gate raised on another stream 3 ms after the program began: no tiles, its done gate up
+    within 20 us of its gate, and the next task starts there - a chained deadline task continues from when
+    the gates opened, a fixed-work task once the gate-only task is complete on every block."""
+    a, b, c = _operands()
+    slot, it, ts, gates, done, te = Words(8), Words(1), Words(8), Words(4), Words(4), Words(8)
+    other = torch.cuda.Stream()
+    s = torch.cuda.current_stream()
+    for rep in range(2):
+        it.t.fill_(20 + rep)
+        tag = 9 + rep
+        e0 = torch.cuda.Event()
+        e0.record(s)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(other):
+            gemm.idle_wait_us(3000.0)
+            gemm.gate_signal_iter_(gates.t, 0, tag, it.t)
+        if fixed:
+            work = dict(ticks=0, work_rounds=1)
+            tasks = [_task(epoch=0, tstart0=ts.at(0), tend=te.at(0), **work),
+                     _task(ticks=0, flags=1, epoch=1, gate0=gates.at(0), tag0=tag, done_gate=done.at(0),
+                           done_tag=50, tstart0=ts.at(1)),
+                     _task(epoch=2, tstart0=ts.at(2), tend=te.at(2), **work)]
+        else:
+            tasks = [_task(ticks=_ticks(1000.0), epoch=0, tstart0=ts.at(0)),
+                     _task(ticks=1, flags=1, epoch=1, gate0=gates.at(0), tag0=tag, done_gate=done.at(0),
+                           done_tag=50, tstart0=ts.at(1)),
+                     _task(ticks=_ticks(500.0), chain_ticks=_ticks(30.0), epoch=2, tstart0=ts.at(2))]
+        gemm.gemm_program(a, b, c, tasks, slot.t, _buf(3), iter_word=it.t, grid=_grid())
+        torch.cuda.synchronize()
+    g, t, d = gates.list(), ts.list(), done.list()
+    assert d[0] == (21 << 32) | 50, d  # the gate-only task's done gate, this iteration's sequence
+    gate_t = g[1] & MASK48
+    us = lambda x: x / _hz() * 1e6  # noqa: E731
+    assert 0 <= us((t[1] & MASK48) - gate_t) <= 20.0, (t, g)  # it started when its gate opened
+    assert 0 <= us((d[1] & MASK48) - gate_t) <= 20.0, (d, g)
+    assert 0 <= us((t[2] & MASK48) - gate_t) <= 20.0, (t, g)  # the next task right behind it
+    if not fixed:
+        assert t[1] - t[0] >= _ticks(1000.0) + _ticks(500.0), t
+
+
 def test_program_done_gates_at_deadlines():
     """Each task's done gate is raised by block 0 as it leaves the task: within 20 us after the task's
     deadline (start + ticks), carrying the iteration's sequence."""
