@@ -553,3 +553,29 @@ def test_xgmi_kernel_occupancy_fits_the_cu_budget(root):
         blocks = bpc * max_ctas
         for name, b in occ.items():
             assert lanes * math.ceil(blocks / b) <= comm_cus, (name, lanes, b)
+
+
+@pytest.mark.parametrize("strategy,model,params", [("dp", "vit_h_32_float8", (8,)),
+                                                   ("fsdp", "llama3_8b_16_bfloat16", (32, 1)),
+                                                   ("hybrid_2d", "tiny_dense_8_bfloat16", (1, 4))])
+def test_graph_with_optimizer_is_not_joined(strategy, model, params, root, data_dir):
+    """with --optimizer the compute stream has work after the compute program (the optimizer
+    steps, the exposed-tail wait), so the program must not end the iteration with its join: lane graphs run
+    without program_join, the exposed tail is still timed (no negative interval), and the step is no slower
+    than the single graph's (+2 %) - the timed iteration includes the optimizer."""
+    base = data_dir if model.startswith("tiny") else root
+    kw = dict(base_path=base, warmup=2, runs=6, compute="gemm", backend="rccl", graph=True, quiet=True,
+              optimizer=True, time_scale=0.05 if model.startswith("llama") else None)
+    lanes = engine.run_native(strategy, model, *params, **kw)
+    single = engine.run_native(strategy, model, *params, env={"DLNB_LANE_GRAPHS": "0"}, **kw)
+    lg = lanes["global"]["dlnb"]["lane_graphs"]
+    assert not lg.get("program_join"), lg
+    for d in (lanes, single):
+        for r in d["ranks"]:
+            assert "timer_negative_intervals" not in r, r["timer_negative_intervals"]
+    tail = {"dp": "barrier_time", "fsdp": "barrier", "hybrid_2d": "dp_exposed_time"}[strategy]
+    assert len(lanes["ranks"][0][tail]) == 6
+    m_l = lanes["global"]["dlnb"]["iteration"]["median_ms"]
+    m_s = single["global"]["dlnb"]["iteration"]["median_ms"]
+    floor = lanes["global"]["dlnb"]["iteration"]["compute_floor_ms"]
+    assert floor <= m_l <= m_s * 1.02 + 0.05, (m_l, m_s, floor)
