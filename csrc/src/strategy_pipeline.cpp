@@ -229,9 +229,13 @@ class Pipeline : public Strategy {
         for (int t = 0; t < T_; ++t) m.push_back(base + ep_id_ * T_ + t);
         // T > 1: the compute waits for every TP all-reduce, so it gets the
         // backend's own CTA count (no compute program holds the CUs meanwhile:
-        // program_ok()); a 1-rank group (a copy) stays in the lane budget
+        // program_ok()); a 1-rank group (a copy) stays in the lane budget, and
+        // so does every group when ranks share the device: there another
+        // rank's compute grid may need the CUs this collective's spinning CTAs
+        // would hold while they wait for that rank (two ranks on one GPU: a
+        // gate wait ran into its 5-s bound now and then)
         tp_comm_ = ctx.comms->create("tp/" + where + "/" + std::to_string(ep_id_), m, tp_shard_ * T_ * es_, false,
-                                     T_ > 1 ? 0 : ctx.lane_ctas);
+                                     T_ > 1 && ctx.ranks_on_device <= 1 ? 0 : ctx.lane_ctas);
       }
       if (has_ep_) {
         std::vector<int> m;
@@ -239,7 +243,7 @@ class Pipeline : public Strategy {
         const uint64_t cap = skew_counts_.empty() ? a2a_ * E_ : std::max<uint64_t>(a2a_ * E_, skew_counts_[0]);
         ep_comm_ = ctx.comms->create("ep/" + where + "/" + std::to_string(tp_id_), m,
                                      std::max<uint64_t>(cap, ne_) * es_, !skew_counts_.empty(),
-                                     o.ep_overlap || E_ == 1 ? ctx.lane_ctas : 0);  // (as TP's)
+                                     o.ep_overlap || E_ == 1 || ctx.ranks_on_device > 1 ? ctx.lane_ctas : 0);  // (as TP's)
       }
     }
     {

@@ -322,7 +322,9 @@ def test_deadline_chain_continues_previous_deadline(dtype):
     assert (2000 + 300 - 30) * 1e-6 * hz - 1 <= t[1] - t[0] <= (2000 + 300 + 60) * 1e-6 * hz, t
     assert abs(t[2] - t[1] - 3000e-6 * hz) <= 1, t  # a launch hop only: absorbed exactly
     ms = e0.elapsed_time(e1)
-    assert 6.27 <= ms <= 6.3 * 1.01 + 0.08, ms  # 2 + 3 + 1 ms + the unabsorbed part of the wait
+    # 2 + 3 + 1 ms + the unabsorbed part of the wait; the events bracket four launches (on a busy box the
+    # first one's dispatch has added ~0.3 ms once in a full-suite run: the stamps above are the exact check)
+    assert 6.27 <= ms <= 6.3 * 1.01 + 0.35, ms
 
 
 def test_deadline_chain_counts_absorbed_lateness():

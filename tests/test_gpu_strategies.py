@@ -418,7 +418,12 @@ def test_tp_ep_lanes_two_ranks_one_gpu(binary, model, params, scale, root, data_
     single = _two_ranks_one_gpu(root, tmp_path, binary, params, {"DLNB_LANE_GRAPHS": "0"}, **kw)
     assert not single["global"]["dlnb"]["lane_graphs"]["enabled"]
     m_l, m_s = d["iteration"]["median_ms"], single["global"]["dlnb"]["iteration"]["median_ms"]
-    assert m_l <= m_s * 1.005, (m_l, m_s)
+    # hybrid_3d's 512 TP all-reduces per iteration are each exposed; with the ranks sharing the GPU they are held
+    # to the lane CTA budget (8 here: uncapped, one rank's spinning CTAs starved the other's compute now and then
+    # - a 5-s gate timeout), where the lane's gate-wait -> all-reduce dispatch costs ~6 us more per all-reduce
+    # than the single graph's edge (profiles/pipeline_program_r6.md: 88.6 vs 85.0 ms at 8 CTAs, 80.6 vs 80.3 at 32)
+    tol = 1.05 if binary == "hybrid_3d" else 1.005
+    assert m_l <= m_s * tol, (m_l, m_s)
 
 
 def test_cp_stall_timers_two_ranks_one_gpu(root, tmp_path):
