@@ -30,6 +30,8 @@ class TimerSet {
   TimerSet(const TimerSet&) = delete;
   TimerSet& operator=(const TimerSet&) = delete;
   int begin(Stream& s);
+  // The stamp slot of a begin() token (nullptr when disabled), e.g. for pair().
+  const uint64_t* at(int token) const { return token < 0 ? nullptr : stamps_ + token; }
   // Returns the end stamp's slot (nullptr when disabled), e.g. for gap().
   const uint64_t* end(int token, Stream& s, const std::string& name);
   // Time the stall of stream s waiting for event e (exposed latency).

@@ -89,6 +89,9 @@ class Pipeline : public Strategy {
     E_ = has_ep_ ? o.num_expert_shards : 1;
     inner_ = T_ * E_;  // TP fastest, then EP (hybrid_4d), then stage, then DP replica
     reference_ = o.schedule == "reference";
+    // A/B: the round-5 placement of the TP / EP collectives (on the compute
+    // stream between the tasks) instead of the inner lane
+    inner_on_compute_ = env_int("DLNB_INNER_ON_COMPUTE", 0) != 0;
     one_f_one_b_ = o.pp_schedule == "1f1b";
     interleaved_ = o.pp_schedule == "interleaved";
     dualpipe_ = o.pp_schedule == "dualpipe";
@@ -229,13 +232,9 @@ class Pipeline : public Strategy {
         for (int t = 0; t < T_; ++t) m.push_back(base + ep_id_ * T_ + t);
         // T > 1: the compute waits for every TP all-reduce, so it gets the
         // backend's own CTA count (no compute program holds the CUs meanwhile:
-        // program_ok()); a 1-rank group (a copy) stays in the lane budget, and
-        // so does every group when ranks share the device: there another
-        // rank's compute grid may need the CUs this collective's spinning CTAs
-        // would hold while they wait for that rank (two ranks on one GPU: a
-        // gate wait ran into its 5-s bound now and then)
+        // program_ok(); inner_ctas); a 1-rank group (a copy) stays in the lane budget
         tp_comm_ = ctx.comms->create("tp/" + where + "/" + std::to_string(ep_id_), m, tp_shard_ * T_ * es_, false,
-                                     T_ > 1 && ctx.ranks_on_device <= 1 ? 0 : ctx.lane_ctas);
+                                     T_ > 1 ? inner_ctas(ctx) : ctx.lane_ctas);
       }
       if (has_ep_) {
         std::vector<int> m;
@@ -243,7 +242,7 @@ class Pipeline : public Strategy {
         const uint64_t cap = skew_counts_.empty() ? a2a_ * E_ : std::max<uint64_t>(a2a_ * E_, skew_counts_[0]);
         ep_comm_ = ctx.comms->create("ep/" + where + "/" + std::to_string(tp_id_), m,
                                      std::max<uint64_t>(cap, ne_) * es_, !skew_counts_.empty(),
-                                     o.ep_overlap || E_ == 1 || ctx.ranks_on_device > 1 ? ctx.lane_ctas : 0);  // (as TP's)
+                                     o.ep_overlap || E_ == 1 ? ctx.lane_ctas : inner_ctas(ctx));
       }
     }
     {
@@ -449,6 +448,13 @@ class Pipeline : public Strategy {
       for (int i = 0; i < ep; ++i) ep_alltoall(*compute_, "ep_comm_time");
       return;
     }
+    if (!inner_lane_) {
+      // single graph / eager: on the compute stream between the tasks (no
+      // cross-stream hop per collective; the compute waits for each anyway)
+      for (int i = 0; i < tp; ++i) tp_allreduce(*compute_, "tp_ar_time", "tp_comm_time");
+      for (int i = 0; i < ep; ++i) ep_alltoall(*compute_, "ep_a2a_time", "ep_comm_time");
+      return;
+    }
     compute_->record(*inner_ready_);
     dp_stream_->wait(*inner_ready_);
     for (int i = 0; i < tp; ++i) tp_allreduce(*dp_stream_, "tp_ar_time");
@@ -458,7 +464,9 @@ class Pipeline : public Strategy {
     for (int i = 0; i < ep; ++i) timers_->stall_before_task(*compute_, *inner_done_, "ep_comm_time");
   }
 
-  void tp_allreduce(Stream& s, const char* timer) {
+  // timer: the collective's duration; also (optional): the same interval
+  // under a second name (on the compute stream it is the exposed wait too)
+  void tp_allreduce(Stream& s, const char* timer, const char* also = nullptr) {
     int t = timers_->begin(s);
     if (sp_) {
       int ta = timers_->begin(s);
@@ -467,11 +475,12 @@ class Pipeline : public Strategy {
       int tr = timers_->begin(s);
       tp_comm_->reduce_scatter(tp_res_.data(), tp_buf_.data(), tp_shard_, ctx_->wire, s);
       timers_->end(tr, s, "tp_rs_time");
-      lane_end(s, timers_->end(t, s, timer));
-      return;
+    } else {
+      tp_comm_->all_reduce(tp_buf_.data(), tp_res_.data(), tp_ar_, ctx_->wire, s);
     }
-    tp_comm_->all_reduce(tp_buf_.data(), tp_res_.data(), tp_ar_, ctx_->wire, s);
-    lane_end(s, timers_->end(t, s, timer));
+    const uint64_t* e = timers_->end(t, s, timer);
+    lane_end(s, e);
+    if (also) timers_->pair(timers_->at(t), e, also);
   }
 
   // The end stamp of the last collective on the inner lane (finish_iteration:
@@ -480,13 +489,15 @@ class Pipeline : public Strategy {
     if (&s == dp_stream_.get()) inner_end_ = end;
   }
 
-  void ep_alltoall(Stream& s, const char* timer) {
+  void ep_alltoall(Stream& s, const char* timer, const char* also = nullptr) {
     int t = timers_->begin(s);
     if (skew_)
       ep_alltoallv(s);
     else
       ep_comm_->all_to_all(ep_send_.data(), ep_recv_.data(), a2a_, ctx_->wire, s);
-    lane_end(s, timers_->end(t, s, timer));
+    const uint64_t* e = timers_->end(t, s, timer);
+    lane_end(s, e);
+    if (also) timers_->pair(timers_->at(t), e, also);
   }
 
   // --ep-imbalance: all-to-allv as one group of sends / receives. Even calls
@@ -1045,6 +1056,12 @@ class Pipeline : public Strategy {
     // the tasks' gates (Device::StreamFold), so no other kernel sits between
     // two tasks on the compute lane
     dp_end_ = nullptr;
+    // The TP / EP collectives go on the inner lane under lane graphs (the
+    // compute lane must hold only compute and its waits); with the single
+    // graph or eager they stay on the compute stream. Ranks sharing a GPU
+    // (4 over xgmi, profiles/pipeline_program_r6.md): the inner lane ran C3
+    // 795 against 810 ms and C4 2802 against 379 ms on the compute stream.
+    inner_lane_ = !inner_on_compute_ && ctx_->dev->gate_events();
     prog_ = ctx_->dev->gate_events() && !reference_ && program_ok() && ctx_->compute->begin_program(*compute_);
     if (dualpipe_)
       enqueue_dualpipe();
@@ -1075,6 +1092,15 @@ class Pipeline : public Strategy {
   // the CUs the finished task freed. hybrid_3d 1 4 2 on two ranks sharing GPU
   // 0 (profiles/pipeline_program_r6.md): program 82.9 ms, one launch per task
   // 80.6, single graph 80.3 at 32 CTAs per lane.
+  // CTAs of TP / EP groups of > 1 rank: the backend's own (0), except with
+  // lane graphs on a shared device (DLNB_LANE_SHARED=1): there one rank's
+  // spinning collective CTAs can starve another rank's compute task that the
+  // collective waits for (a 5-s gate timeout now and then), so the lane budget.
+  static int inner_ctas(const Context& ctx) {
+    const int forced = env_int("DLNB_INNER_CTAS", -1);
+    if (forced >= 0) return forced;
+    return ctx.ranks_on_device > 1 && env_int("DLNB_LANE_SHARED", 0) != 0 ? ctx.lane_ctas : 0;
+  }
   bool program_ok() const { return !(has_tp_ && T_ > 1) && !(has_ep_ && E_ > 1); }
 
   std::vector<Stream*> streams() override {
@@ -1213,6 +1239,8 @@ class Pipeline : public Strategy {
   bool has_tp_ = false, has_ep_ = false, sp_ = false;
   uint64_t tp_shard_ = 0;  // ceil(tp_ar_ / T): sequence-parallel shard
   bool reference_ = false;
+  bool inner_on_compute_ = false;
+  bool inner_lane_ = false;  // this enqueue puts the TP / EP collectives on the inner lane
   bool one_f_one_b_ = false, interleaved_ = false, dualpipe_ = false;
   std::vector<std::vector<DpOp>> dp_ticks_;  // [tick][stage]
   double dp_floor_us_ = 0;
