@@ -1101,7 +1101,13 @@ class Pipeline : public Strategy {
     if (forced >= 0) return forced;
     return ctx.ranks_on_device > 1 && env_int("DLNB_LANE_SHARED", 0) != 0 ? ctx.lane_ctas : 0;
   }
-  bool program_ok() const { return !(has_tp_ && T_ > 1) && !(has_ep_ && E_ > 1); }
+  // The interleaved schedule keeps one launch per task: as a program, two
+  // ranks on one GPU hung in its first lane replay (the gate waits did not
+  // time out: not a device gate; round 6, unresolved), while GPipe and 1F1B
+  // ran (tests/test_gpu_strategies.py). DualPipe takes the single graph (below).
+  bool program_ok() const {
+    return !(has_tp_ && T_ > 1) && !(has_ep_ && E_ > 1) && !interleaved_ && !dualpipe_;
+  }
 
   std::vector<Stream*> streams() override {
     std::vector<Stream*> ss = {compute_.get(), dp_stream_.get()};
@@ -1111,7 +1117,9 @@ class Pipeline : public Strategy {
   }
   bool capturable() const override { return !reference_; }
   // (TP / EP collectives are on the inner lane: the compute lane carries compute and waits only)
-  bool lanes_without_program() const override { return true; }
+  // DualPipe: its lanes (with or without a program) ran 166-167 ms against
+  // 152-162 ms on the single graph, two ranks on one GPU (round 6).
+  bool lanes_without_program() const override { return !dualpipe_; }
 
   void synchronize() override {
     std::vector<Stream*> ss = {compute_.get(), dp_stream_.get()};

@@ -341,7 +341,7 @@ def test_dp_exposed_comm_matches_the_step(mode, root):
 
 
 def _two_ranks_one_gpu(root, tmp_path, binary_name, params, extra_env=None, iters=8, model="llama3_8b_16_bfloat16",
-                       time_scale="0.05", base=None, ctas=8):
+                       time_scale="0.05", base=None, ctas=8, extra_args=()):
     """Run one 2-rank job of a native binary with both ranks on GPU 0 (xgmi), every device wait bounded; returns
     rank 0's report."""
     import json
@@ -359,18 +359,18 @@ def _two_ranks_one_gpu(root, tmp_path, binary_name, params, extra_env=None, iter
     for r in range(2):
         env = dict(os.environ, DLNB_NO_TORCH="1", DLNB_LANE_SHARED="1", DLNB_GEMM_SLICE_US="0", DLNB_GATE_TIMEOUT_S="5",
                    DLNB_XGMI_TIMEOUT_S="20", RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), LOCAL_WORLD_SIZE="2",
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLNB_STORE_PORT=str(store_port),
-                   **(extra_env or {}))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLNB_STORE_PORT=str(store_port))
+        env.update(extra_env or {})
         out = str(tmp_path / f"r{r}.json")
         procs.append(subprocess.Popen(
             [binary, model, *params, base or root, "--backend", "xgmi", "--devices", "0,0", "--comm-cus",
              "160", "--rccl-max-ctas", str(ctas), "--compute", "gemm", "--graph", "-w", "3", "-r", str(iters),
-             "--time-scale", time_scale, "--quiet", "--silent", "--json", out], env=env, stdout=subprocess.PIPE,
+             "--time-scale", time_scale, "--quiet", "--silent", "--json", out, *extra_args], env=env, stdout=subprocess.PIPE,
             stderr=subprocess.PIPE, text=True))
     errs = []
     for p in procs:
         try:
-            _, err = p.communicate(timeout=100)
+            _, err = p.communicate(timeout=int(os.environ.get("DLNB_TEST_JOB_TIMEOUT", "100")))
         except subprocess.TimeoutExpired:
             p.kill()
             _, err = p.communicate()
@@ -584,3 +584,29 @@ def test_graph_with_optimizer_is_not_joined(strategy, model, params, root, data_
     m_s = single["global"]["dlnb"]["iteration"]["median_ms"]
     floor = lanes["global"]["dlnb"]["iteration"]["compute_floor_ms"]
     assert floor <= m_l <= m_s * 1.02 + 0.05, (m_l, m_s, floor)
+
+
+@pytest.mark.parametrize("schedule", ["1f1b", "interleaved", "dualpipe"])
+def test_pipeline_schedules_program_two_ranks_one_gpu(schedule, root, tmp_path):
+    # (interleaved: lanes with one launch per task; DualPipe: the single graph - StrategyPipeline::program_ok,
+    # lanes_without_program)
+    """Every pipeline schedule's compute lane as one compute program (its receive / send / DP-bucket waits and
+    records folded into the tasks, gate-only tasks where needed) on 2 ranks sharing GPU 0: hybrid_2d S = 2,
+    mb = 4 replays linear lane graphs with program_join, no gate timeout, the step within 5 % of the single
+    graph's, and the exposed-wait timers without a negative interval."""
+    doc = _two_ranks_one_gpu(root, tmp_path, "hybrid_2d", ["2", "4"], None,
+                             extra_args=("--pp-schedule", schedule))
+    d = doc["global"]["dlnb"]
+    lg = d["lane_graphs"]
+    if schedule == "dualpipe":
+        assert not lg["enabled"], lg
+        return
+    assert lg["enabled"] and lg["linear"] and lg["program_join"] == (schedule != "interleaved"), lg
+    cc = d["chain_capped"]
+    assert cc["gate_wait_timeouts_max"] == 0 and cc["compute_gate_timeouts_max"] == 0, cc
+    for r in doc["ranks"]:
+        assert "timer_negative_intervals" not in r, r["timer_negative_intervals"]
+    single = _two_ranks_one_gpu(root, tmp_path, "hybrid_2d", ["2", "4"], {"DLNB_LANE_GRAPHS": "0"},
+                                extra_args=("--pp-schedule", schedule))
+    m_l, m_s = d["iteration"]["median_ms"], single["global"]["dlnb"]["iteration"]["median_ms"]
+    assert d["iteration"]["compute_floor_ms"] * 0.98 <= m_l <= m_s * 1.05, (m_l, m_s)
