@@ -383,7 +383,9 @@ def test_pipeline_lanes_two_ranks_one_gpu(root, tmp_path):
     """The pipeline hybrids' compute lane is one compute program (its receive / send / DP-bucket event waits
     and records folded into the tasks' gates, Device::StreamFold) ending in the lane join: hybrid_3d S = 2,
     mb = 4 on 2 ranks sharing GPU 0 over xgmi - linear lane graphs with program_join on both ranks, no gate
-    timeout, and faster than the single graph (profiles/hostwait_r5.md: 100.3 vs 104.8 ms)."""
+    timeout, and no slower than the single graph (+1 %: round 5 measured 100.3 vs 104.8 ms with one launch per
+    task, profiles/hostwait_r5.md; with the T = 1 copies back on the single graph's compute stream (round 6) the
+    two are within noise, 99.3 vs 99.0)."""
     lanes = _two_ranks_one_gpu(root, tmp_path, "hybrid_3d", ["2", "4", "1"])
     d = lanes["global"]["dlnb"]
     lg = d["lane_graphs"]
@@ -392,7 +394,7 @@ def test_pipeline_lanes_two_ranks_one_gpu(root, tmp_path):
     assert cc["gate_wait_timeouts_max"] == 0 and cc["compute_gate_timeouts_max"] == 0, cc
     single = _two_ranks_one_gpu(root, tmp_path, "hybrid_3d", ["2", "4", "1"], {"DLNB_LANE_GRAPHS": "0"})
     assert not single["global"]["dlnb"]["lane_graphs"]["enabled"]
-    assert d["iteration"]["median_ms"] < single["global"]["dlnb"]["iteration"]["median_ms"], (d["iteration"],
+    assert d["iteration"]["median_ms"] < 1.01 * single["global"]["dlnb"]["iteration"]["median_ms"], (d["iteration"],
                                                                                               single["global"]["dlnb"]["iteration"])
     # TP collectives between the compute tasks (T = 2): on the inner lane, so lanes too
     tp = _two_ranks_one_gpu(root, tmp_path, "hybrid_3d", ["1", "4", "2"])
@@ -474,8 +476,8 @@ def test_fsdp_lanes_two_ranks_one_gpu(root, tmp_path):
     assert not lg["alternating_streams"], lg  # one stream set when ranks share the device
     cc = d["chain_capped"]
     assert cc["gate_wait_timeouts_max"] == 0 and cc["compute_gate_timeouts_max"] == 0, cc
-    assert cc["tasks_per_iter_max"] == 0, cc
     it = d["iteration"]
+    assert cc["tasks_per_iter_max"] == 0, (cc["tasks_per_iter_max"], cc["ms_per_iter_max"], it["median_ms"])
     assert it["compute_floor_ms"] <= it["median_ms"] < 1.05 * it["compute_floor_ms"], it
 
 
@@ -485,11 +487,13 @@ def test_pipeline_stall_timers_from_task_stamps(data_dir):
     start), not a stamp-wait-stamp pair a graph executor can reorder. Same entry counts as the stamp pairs
     (DLNB_TASK_STAMP_TIMERS=0), no double counting (the waits on the compute stream add up to at most the
     iteration over its floor), and the iteration is shorter without the two stamp kernels per wait."""
-    docs = {}
-    for stamps in ("1", "0"):
+    docs, med = {}, {"1": [], "0": []}
+    # interleaved, twice each: the first run of a fresh process was ~2 ms slower whichever mode it ran
+    for stamps in ("1", "0", "1", "0"):
         docs[stamps] = engine.run_native("hybrid_3d", "tiny_dense_8_bfloat16", 2, 8, 1, base_path=data_dir, warmup=2,
                                          runs=5, compute="sleep", backend="loopback", ranks=2, quiet=True,
                                          env={"DLNB_TASK_STAMP_TIMERS": stamps})
+        med[stamps].append(docs[stamps]["global"]["dlnb"]["iteration"]["median_ms"])
     for stamps, doc in docs.items():
         it = doc["global"]["dlnb"]["iteration"]
         over = it["median_ms"] - it["compute_floor_ms"]
@@ -498,7 +502,7 @@ def test_pipeline_stall_timers_from_task_stamps(data_dir):
             assert all(v >= 0 for v in r["pp_comm_time"])
             waits = sum(sum(r[k]) for k in ("pp_comm_time", "tp_comm_time", "dp_exposed_time")) / 5 * 1e3
             assert waits <= over + 0.5, (stamps, waits, over)
-    assert docs["1"]["global"]["dlnb"]["iteration"]["median_ms"] < docs["0"]["global"]["dlnb"]["iteration"]["median_ms"]
+    assert min(med["1"]) < min(med["0"]), med
 
 
 @pytest.mark.parametrize("graph", [True, False])
