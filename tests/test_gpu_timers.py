@@ -23,7 +23,7 @@ from dlnetbench_amd import engine  # noqa: E402
 X_US = 500.0
 X_MS = X_US / 1e3
 TOL_MS = 0.03
-TOL_EAGER_MS = 0.06
+TOL_EAGER_MS = 0.12
 MODES = ["lanes", "single", "eager"]
 COMPUTE = ["gemm", "gemm-work"]
 
@@ -70,7 +70,9 @@ def _one_rank(strategy, model, params, mode, compute, fault, time_scale=None, ru
 
 def _tol(doc):
     """Eager mode puts the host's enqueue on the critical path: a task's launch can trail the end of the wait
-    before it by host jitter (tens of us, both runs), so the rise of a wait is checked to TOL_EAGER_MS there."""
+    before it by host jitter (tens of us, both runs; the worst seen over three full runs: 0.105 ms, ZeRO's
+    parameter all-gather behind eager optimizer launches), so the rise of a wait is checked to TOL_EAGER_MS
+    there."""
     return TOL_MS if doc["global"]["dlnb"].get("graph") else TOL_EAGER_MS
 
 
