@@ -1106,6 +1106,8 @@ class Pipeline : public Strategy {
   // time out: not a device gate; round 6, unresolved), while GPipe and 1F1B
   // ran (tests/test_gpu_strategies.py). DualPipe takes the single graph (below).
   bool program_ok() const {
+    const int forced = env_int("DLNB_PIPELINE_PROGRAM", -1);  // A/B: 0 never, 1 always (lane graphs)
+    if (forced >= 0) return forced != 0;
     return !(has_tp_ && T_ > 1) && !(has_ep_ && E_ > 1) && !interleaved_ && !dualpipe_;
   }
 
