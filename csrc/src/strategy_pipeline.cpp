@@ -655,7 +655,10 @@ class Pipeline : public Strategy {
     // are done, and the DP tail exposed is the DP lane's last end stamp minus
     // the compute's last task (a gap: no wait on the compute stream);
     // otherwise the compute stream waits for the DP lane.
-    const bool join = prog_ && !ctx.opt.optimizer && dp_end_ && timers_->task_stamps();
+    // (not for the interleaved schedule: with the join its lane replays hung on
+    // two ranks sharing a GPU - round 6, cause not found; as a program without
+    // the join, every lane ending with its own done word, it runs)
+    const bool join = prog_ && !ctx.opt.optimizer && dp_end_ && timers_->task_stamps() && !interleaved_;
     if (prog_) ctx.compute->end_program(*compute_, join);
     prog_ = false;
     if (join) {
@@ -1101,14 +1104,12 @@ class Pipeline : public Strategy {
     if (forced >= 0) return forced;
     return ctx.ranks_on_device > 1 && env_int("DLNB_LANE_SHARED", 0) != 0 ? ctx.lane_ctas : 0;
   }
-  // The interleaved schedule keeps one launch per task: as a program, two
-  // ranks on one GPU hung in its first lane replay (the gate waits did not
-  // time out: not a device gate; round 6, unresolved), while GPipe and 1F1B
-  // ran (tests/test_gpu_strategies.py). DualPipe takes the single graph (below).
+  // (The interleaved schedule's program ends without the lane join:
+  // finish_iteration.) DualPipe takes the single graph (below).
   bool program_ok() const {
     const int forced = env_int("DLNB_PIPELINE_PROGRAM", -1);  // A/B: 0 never, 1 always (lane graphs)
     if (forced >= 0) return forced != 0;
-    return !(has_tp_ && T_ > 1) && !(has_ep_ && E_ > 1) && !interleaved_ && !dualpipe_;
+    return !(has_tp_ && T_ > 1) && !(has_ep_ && E_ > 1) && !dualpipe_;
   }
 
   std::vector<Stream*> streams() override {

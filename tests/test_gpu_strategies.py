@@ -594,8 +594,8 @@ def test_graph_with_optimizer_is_not_joined(strategy, model, params, root, data_
 
 @pytest.mark.parametrize("schedule", ["1f1b", "interleaved", "dualpipe"])
 def test_pipeline_schedules_program_two_ranks_one_gpu(schedule, root, tmp_path):
-    # (interleaved: lanes with one launch per task; DualPipe: the single graph - StrategyPipeline::program_ok,
-    # lanes_without_program)
+    # (interleaved: a compute program without the lane join; DualPipe: the single graph -
+    # StrategyPipeline::program_ok, lanes_without_program)
     """Every pipeline schedule's compute lane as one compute program (its receive / send / DP-bucket waits and
     records folded into the tasks, gate-only tasks where needed) on 2 ranks sharing GPU 0: hybrid_2d S = 2,
     mb = 4 replays linear lane graphs with program_join, no gate timeout, the step within 5 % of the single
@@ -608,6 +608,7 @@ def test_pipeline_schedules_program_two_ranks_one_gpu(schedule, root, tmp_path):
         assert not lg["enabled"], lg
         return
     assert lg["enabled"] and lg["linear"] and lg["program_join"] == (schedule != "interleaved"), lg
+    assert lg["compute_programs"] >= 1, lg
     cc = d["chain_capped"]
     assert cc["gate_wait_timeouts_max"] == 0 and cc["compute_gate_timeouts_max"] == 0, cc
     for r in doc["ranks"]:
