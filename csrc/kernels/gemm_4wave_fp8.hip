@@ -455,8 +455,11 @@ __global__ void __launch_bounds__(256, 1)
       if (prog) {
         d.ticks = d.slice_end = prog[k].ticks;  // a uniform (scalar) load: stays in SGPRs
         fixed = d.ticks == 0 && (prog[k].work_rounds | prog[k].tail_kt | prog[k].flags) != 0;
-        if (d.ticks == 0 && !fixed) {  // the join task (the program's last)
-          if (blockIdx.x == 0 && tid == 0) dl::join(prog[k].sync);
+        if (d.ticks == 0 && !fixed) {  // the join task(s), the program's last
+          // (two end gates per join task: with more lanes the join is several
+          // tasks, the last of which stores the host's done word)
+          if (blockIdx.x == 0 && tid == 0)
+            for (int j = k; j < ntasks; ++j) dl::join(prog[j].sync);
           return;
         }
       }

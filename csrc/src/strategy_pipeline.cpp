@@ -655,10 +655,7 @@ class Pipeline : public Strategy {
     // are done, and the DP tail exposed is the DP lane's last end stamp minus
     // the compute's last task (a gap: no wait on the compute stream);
     // otherwise the compute stream waits for the DP lane.
-    // (not for the interleaved schedule: with the join its lane replays hung on
-    // two ranks sharing a GPU - round 6, cause not found; as a program without
-    // the join, every lane ending with its own done word, it runs)
-    const bool join = prog_ && !ctx.opt.optimizer && dp_end_ && timers_->task_stamps() && !interleaved_;
+    const bool join = prog_ && !ctx.opt.optimizer && dp_end_ && timers_->task_stamps();
     if (prog_) ctx.compute->end_program(*compute_, join);
     prog_ = false;
     if (join) {
@@ -1104,8 +1101,7 @@ class Pipeline : public Strategy {
     if (forced >= 0) return forced;
     return ctx.ranks_on_device > 1 && env_int("DLNB_LANE_SHARED", 0) != 0 ? ctx.lane_ctas : 0;
   }
-  // (The interleaved schedule's program ends without the lane join:
-  // finish_iteration.) DualPipe takes the single graph (below).
+  // DualPipe takes the single graph (below).
   bool program_ok() const {
     const int forced = env_int("DLNB_PIPELINE_PROGRAM", -1);  // A/B: 0 never, 1 always (lane graphs)
     if (forced >= 0) return forced != 0;

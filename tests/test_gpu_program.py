@@ -242,6 +242,33 @@ def test_program_join_after_end_gates():
     assert tj.list()[0] >= g[1], (tj.list(), g)
 
 
+def test_program_join_of_several_tasks():
+    """Three end gates (four lanes) make the join two tasks - two gates, then one gate and the host's done word:
+    every one of them runs (the kernel returned after the first before round 6, so the done word never came and
+    the host waited out its timeout), the done word only after the last gate (raised 3 ms late)."""
+    a, b, c = _operands()
+    slot, it, gates = Words(8), Words(1, 33), Words(8)
+    done, tj = Words(1, -1), Words(1)
+    other = torch.cuda.Stream()
+    s = torch.cuda.current_stream()
+    ev = torch.cuda.Event()
+    ev.record(s)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(other):
+        gemm.gate_signal_iter_(gates.t, 0, 1, it.t)  # (gate index i: 16 bytes each - Words.at(2 i))
+        gemm.gate_signal_iter_(gates.t, 1, 1, it.t)
+        gemm.idle_wait_us(3000.0)
+        gemm.gate_signal_iter_(gates.t, 2, 1, it.t)
+    tasks = [_task(ticks=_ticks(500.0), epoch=0),
+             _task(epoch=1, gate0=gates.at(0), tag0=1, gate1=gates.at(2), tag1=1),
+             _task(epoch=2, gate0=gates.at(4), tag0=1, tstart0=done.at(0), tstart1=tj.at(0))]
+    gemm.gemm_program(a, b, c, tasks, slot.t, _buf(3), iter_word=it.t, grid=_grid())
+    torch.cuda.synchronize()
+    assert done.list()[0] == 33, done.list()
+    g = gates.list()
+    assert tj.list()[0] >= g[5], (tj.list(), g)
+
+
 def test_program_gate_timeout_counted():
     """A gate never raised ends the wait at the gate timeout (2 ms here): the task runs, kGateTimeouts counts
     it, and the program finishes."""

@@ -594,8 +594,9 @@ def test_graph_with_optimizer_is_not_joined(strategy, model, params, root, data_
 
 @pytest.mark.parametrize("schedule", ["1f1b", "interleaved", "dualpipe"])
 def test_pipeline_schedules_program_two_ranks_one_gpu(schedule, root, tmp_path):
-    # (interleaved: a compute program without the lane join; DualPipe: the single graph -
-    # StrategyPipeline::program_ok, lanes_without_program)
+    # (DualPipe: the single graph - StrategyPipeline::program_ok, lanes_without_program; the interleaved
+    # schedule's 4 lanes need two join tasks - three end gates - which the kernel ran only the first of
+    # before round 6's fix: the host never saw the done word)
     """Every pipeline schedule's compute lane as one compute program (its receive / send / DP-bucket waits and
     records folded into the tasks, gate-only tasks where needed) on 2 ranks sharing GPU 0: hybrid_2d S = 2,
     mb = 4 replays linear lane graphs with program_join, no gate timeout, the step within 5 % of the single
@@ -607,7 +608,7 @@ def test_pipeline_schedules_program_two_ranks_one_gpu(schedule, root, tmp_path):
     if schedule == "dualpipe":
         assert not lg["enabled"], lg
         return
-    assert lg["enabled"] and lg["linear"] and lg["program_join"] == (schedule != "interleaved"), lg
+    assert lg["enabled"] and lg["linear"] and lg["program_join"], lg
     assert lg["compute_programs"] >= 1, lg
     cc = d["chain_capped"]
     assert cc["gate_wait_timeouts_max"] == 0 and cc["compute_gate_timeouts_max"] == 0, cc
