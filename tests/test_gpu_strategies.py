@@ -618,3 +618,21 @@ def test_pipeline_schedules_program_two_ranks_one_gpu(schedule, root, tmp_path):
                                 extra_args=("--pp-schedule", schedule))
     m_l, m_s = d["iteration"]["median_ms"], single["global"]["dlnb"]["iteration"]["median_ms"]
     assert d["iteration"]["compute_floor_ms"] * 0.98 <= m_l <= m_s * 1.05, (m_l, m_s)
+
+
+def test_hsdp_split_lanes_joined_two_ranks_one_gpu(root, tmp_path):
+    """HSDP (FSDP U = 32 with F = 1 on 2 ranks: two replicas, the replica all-reduce on a lane of its own with
+    --comm-lanes split): four lanes, so the compute program's join is two tasks (three end gates) - the case the
+    program kernels got wrong before round 6 (only the first join task ran; the iteration never ended). Lane
+    graphs with program_join, no gate timeout, the step no slower than the single graph's (+5 %; the replicas'
+    0.5-GB all-reduces share one GPU's 64 free CUs here, so neither is near the floor)."""
+    doc = _two_ranks_one_gpu(root, tmp_path, "fsdp", ["32", "1"], None, extra_args=("--comm-lanes", "split"))
+    single = _two_ranks_one_gpu(root, tmp_path, "fsdp", ["32", "1"], {"DLNB_LANE_GRAPHS": "0"},
+                                extra_args=("--comm-lanes", "split"))
+    d = doc["global"]["dlnb"]
+    lg = d["lane_graphs"]
+    assert lg["enabled"] and lg["linear"] and lg["program_join"] and len(lg["graphs"]) == 4, lg
+    cc = d["chain_capped"]
+    assert cc["gate_wait_timeouts_max"] == 0 and cc["compute_gate_timeouts_max"] == 0, cc
+    m_l, m_s = d["iteration"]["median_ms"], single["global"]["dlnb"]["iteration"]["median_ms"]
+    assert d["iteration"]["compute_floor_ms"] <= m_l <= 1.05 * m_s, (m_l, m_s)
