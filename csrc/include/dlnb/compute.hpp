@@ -149,6 +149,9 @@ class ComputeEngine {
   // Programs launched on s so far (a lane of one program per iteration pays
   // no kernel boundaries between its tasks, joined or not).
   virtual long programs_on(Stream& s) { (void)s; return 0; }
+  // Whether the last program opened on s was split by a task too short for a
+  // program (< 20 us: launched on its own between two launches of the program).
+  virtual bool program_split(Stream& s) { (void)s; return false; }
   // Lane join (the runner, lane graphs): the next program ended on s finishes
   // with a join task - thread 0 of block 0 waits for `gates` (the other
   // lanes' end gates, raised with `tag`) and stores the iteration number into

@@ -200,6 +200,7 @@ class GpuCompute : public ComputeEngine {
     p.tasks.clear();
     p.pending.clear();
     p.done_free = false;
+    p.split = false;
     if (dev_.gate_events()) {
       // the stream's gate-event waits and records between the tasks become
       // the tasks' gates and done gates (gate-only tasks where none fits):
@@ -248,6 +249,10 @@ class GpuCompute : public ComputeEngine {
     lane_stats_.clear();
   }
   bool program_joined(Stream& s) override { return joined_.count(&s) != 0; }
+  bool program_split(Stream& s) override {
+    auto it = programs_.find(&s);
+    return it != programs_.end() && it->second.split;
+  }
   long programs_on(Stream& s) override {
     auto it = program_count_.find(&s);
     return it == program_count_.end() ? 0 : it->second;
@@ -406,7 +411,11 @@ class GpuCompute : public ComputeEngine {
     StartNote note{stall_timers_, s, start, ticks(std::max(0.0, us * scale_)), nullptr};
     double d = us * scale_;
     // a task that is not a deadline kernel cannot join the open program
-    if (mode_ == ComputeMode::Gemm && d < 20.0) flush_program(s);
+    if (mode_ == ComputeMode::Gemm && d < 20.0) {
+      auto pit = programs_.find(&s);
+      if (pit != programs_.end() && pit->second.open) pit->second.split = true;
+      flush_program(s);
+    }
     if (mode_ == ComputeMode::Gemm) chain_live_[slot_for(s)] = false;  // a chain restarts at every unchained task
     if (mode_ == ComputeMode::Sleep || mode_ == ComputeMode::Spin) {
       // the kernel stamps its own start (stall timers: gap() from it)
@@ -774,6 +783,7 @@ class GpuCompute : public ComputeEngine {
     // folded gate-event waits (gate, tag) the next task takes as its gates
     std::vector<std::pair<const uint64_t*, uint32_t>> pending;
     bool done_free = false;  // tasks.back() has no done gate: a record right after it takes that one
+    bool split = false;      // a short task was launched on its own while the program was open
     Fold fold;
   };
 

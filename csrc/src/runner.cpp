@@ -730,6 +730,7 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       std::vector<uint64_t*> end_gates;
       for (size_t i = 1; i < ss.size(); ++i) end_gates.push_back(ctx.dev->alloc_gate());
       ctx.compute->set_lane_join(*ss[0], end_gates, 1u, lane_done);
+      const long progs0 = ctx.compute->programs_on(*ss[0]);
       lane_graphs = ctx.dev->capture_lanes(
           ss, [&] {
             T.iteration_start(*ss[0]);
@@ -773,9 +774,13 @@ Json run_rank_impl(const Options& opt, Context& ctx, std::unique_ptr<Strategy>& 
       // a compute program per iteration qualifies joined or not (not joined:
       // work follows it on the compute lane, which then ends with its own
       // done word - ADVICE r5)
-      const bool program_ok = joined || ctx.compute->programs_on(*ss[0]) > 0 || long_tasks ||
+      // - ONE program launch in the iteration: a task too short for a program
+      // (< 20 us) splits it into several launches with kernels between, whose
+      // boundaries all land on the compute lane's one queue
+      const long progs = ctx.compute->programs_on(*ss[0]) - progs0;
+      const bool program_ok = joined || (progs == 1 && !ctx.compute->program_split(*ss[0])) || long_tasks ||
                               env_int("DLNB_LANE_GRAPHS", 1) >= 2;
-      lane_info["compute_programs"] = static_cast<double>(ctx.compute->programs_on(*ss[0]));
+      lane_info["compute_programs"] = static_cast<double>(progs);
       lane_info["compute_task_us"] = task_us;
       const double verdict = ctx.hg().allreduce_max(!linear ? 2.0 : (!program_ok ? 1.0 : 0.0));
       linear = verdict < 0.5;

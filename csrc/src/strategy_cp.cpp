@@ -210,6 +210,12 @@ class ContextParallel : public Strategy {
     Context& ctx = *ctx_;
     ComputeEngine& ce = *ctx.compute;
     const double a = attn_frac_;
+    // Lane graphs: the iteration's compute tasks are one compute program, the
+    // CP and DP event waits / records folded into its tasks' gates
+    // (Device::StreamFold): the ~200 task boundaries per iteration that made
+    // CP's launch-per-task lanes lose to the single graph are gone.
+    const bool prog = ctx.dev->gate_events() && !reference_ && ce.begin_program(*compute_);
+    const uint64_t* dp_end = nullptr;
     for (int l = 0; l < L_; ++l) {
       ce.run(*compute_, fwd_layer_us_ * (1 - a) / 2, fwd_layer_flops_ * (1 - a) / 2);
       attention(true, fwd_layer_us_ * a, fwd_layer_flops_ * a);
@@ -225,12 +231,20 @@ class ContextParallel : public Strategy {
         dp_stream_->wait(*bucket_ready_[b]);
         int t = timers_->begin(*dp_stream_);
         dp_comm_->all_reduce(grads_[b].data(), grads_[b].data(), bucket_[b], ctx.wire, *dp_stream_);
-        timers_->end(t, *dp_stream_, "dp_comm_time");
+        dp_end = timers_->end(t, *dp_stream_, "dp_comm_time");
         ++b;
       }
     }
-    dp_stream_->record(*dp_done_);
-    timers_->stall_after_task(*compute_, *dp_done_, "dp_exposed_time");
+    // nothing after the program on the compute stream (no optimizer): it ends
+    // in the lane join and the DP tail is a gap (as the pipeline's)
+    const bool join = prog && !ctx.opt.optimizer && dp_end && timers_->task_stamps();
+    if (prog) ce.end_program(*compute_, join);
+    if (join) {
+      timers_->stall_until(*compute_, dp_end, "dp_exposed_time");
+    } else {
+      dp_stream_->record(*dp_done_);
+      timers_->stall_after_task(*compute_, *dp_done_, "dp_exposed_time");
+    }
     if (ctx.opt.optimizer) {
       size_t off = 0;
       for (int k = 0; k < nbk_; ++k) {
@@ -242,6 +256,8 @@ class ContextParallel : public Strategy {
 
   std::vector<Stream*> streams() override { return {compute_.get(), cp_stream_.get(), dp_stream_.get()}; }
   bool capturable() const override { return true; }
+  // (launch per task: ~200 task boundaries per iteration, slower than the
+  // single graph; a compute program - enqueue_iteration - takes lanes)
   bool lanes_without_program() const override { return false; }  // strategy.hpp
 
   void synchronize() override {

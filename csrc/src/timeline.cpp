@@ -423,6 +423,7 @@ class TracingCompute : public ComputeEngine {
   bool begin_program(Stream& s) override { return in_->begin_program(s); }
   void end_program(Stream& s, bool join_ok) override { in_->end_program(s, join_ok); }
   long programs_on(Stream& s) override { return in_->programs_on(s); }
+  bool program_split(Stream& s) override { return in_->program_split(s); }
   const uint64_t* last_task_end(Stream& s) override { return in_->last_task_end(s); }
   void after_capture() override { in_->after_capture(); }
   void set_lane_join(Stream& s, const std::vector<uint64_t*>& gates, uint32_t tag, uint64_t* host_done) override {

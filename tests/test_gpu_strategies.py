@@ -143,7 +143,9 @@ def test_strategy_hip_graph_replay(strategy, model, params, data_dir):
     if lg["enabled"]:
         assert lg["linear"] and len(lg["graphs"]) >= 2 and all(x["linear"] for x in lg["graphs"]), lg
         assert lg["program_join"] or lg["compute_task_us"] >= 1000, lg
-        assert lg["alternating_streams"], lg
+        # two stream sets need 2 x lanes independent hardware queues (GPU_MAX_HW_QUEUES = 4 here): CP's three
+        # lanes replay on one set
+        assert lg["alternating_streams"] or 2 * len(lg["graphs"]) > 4, lg
     else:
         assert lg["reason"], lg
     cc = g["dlnb"].get("chain_capped")
