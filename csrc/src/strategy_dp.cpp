@@ -181,6 +181,11 @@ class DataParallel : public Strategy {
     Context& ctx = *ctx_;
     ComputeEngine& ce = *ctx.compute;
     const int me = comm_->rank();
+    // Lane graphs: the forward and backward buckets are one compute program
+    // (their ready records folded into the tasks' done gates); it ends before
+    // the tail wait and the optimizer steps, which follow it on the compute
+    // lane (not joined: the lane ends with its own done word)
+    const bool prog = ctx.dev->gate_events() && ce.begin_program(*compute_);
     ce.run(*compute_, fwd_us_, fwd_flops_);
     for (int i = 0; i < nb_; ++i) {
       // only event records on compute_ since the forward: one stretch of compute
@@ -199,6 +204,7 @@ class DataParallel : public Strategy {
         timers_->end(t, *comm_stream_, "allreduce_time");
       }
     }
+    if (prog) ce.end_program(*compute_, false);
     comm_stream_->record(*done_);
     timers_->stall_after_task(*compute_, *done_, "barrier_time");  // exposed gradient communication (as dp)
     // Optimizer step on this rank's slice of each bucket, then that bucket's
