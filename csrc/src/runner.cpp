@@ -123,6 +123,11 @@ void sync_streams(const std::vector<Stream*>& streams, const std::vector<Communi
         if (now_s() - t0 > timeout) {
           std::ostringstream m;
           m << "iteration did not complete within DLNB_TIMEOUT=" << timeout << " s (hung collective or dead peer)";
+          if (flag) {
+            // lane graphs: which lanes' done words (host-mapped) are behind
+            m << "; lane done words (want " << want << "):";
+            for (size_t i = 0; i < nflags; ++i) m << " " << __atomic_load_n(flag + i, __ATOMIC_ACQUIRE);
+          }
           device_failure(m.str());
           for (Communicator* a : comms)
             if (a) a->abort();
