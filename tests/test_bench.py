@@ -47,6 +47,11 @@ def test_bench_torchrun_cpu(n, tmp_path):
     assert o["higher_is_better"] is False and o["scaling"] == "weak"
     assert o["ms_per_step"] == o["value"] > 0
     assert len(o["per_run_ms"]) == 2 and 0 < o["rank_ms"]["min"] <= o["rank_ms"]["max"] and o["rank_ms"]["slowest_rank"] in range(n)
+    # per-iteration attribution: the slowest rank's last collective per iteration (no hwmon
+    # sensors on the CPU backend)
+    si = o["slow_iterations"]
+    assert si["last_collective"] == "reduce_scatter" and len(si["last_collective_ms"]) == 2, si
+    assert all(x >= 0 for x in si["last_collective_ms"]) and si["sclk_mhz"] is None, si
     assert o["effective_busbw_GBps"]["allgather"] > 0 and o["effective_busbw_GBps"]["reduce_scatter"] > 0
     c5 = o["comm_bound"]
     assert "error" not in c5, c5
@@ -303,6 +308,12 @@ def test_bench_gpu_single_rank_secondaries(tmp_path):
     assert u["ms_per_step"] >= 0.9 * c5["floor_ms"] and u["allreduce_busbw_GBps"] is None
     # energy: the GPU's power sensor integrated over each step (hundreds of W x the step time)
     assert o["energy_J_per_step"] is None or o["energy_J_per_step"]["per_gpu"] > 0
+    # per-iteration attribution: last collective, and (hwmon) sclk within its window and power at the end
+    si = o["slow_iterations"]
+    assert len(si["last_collective_ms"]) == 2, si
+    if si["sclk_mhz"] is not None:
+        assert all(0 < lo <= x for lo, x in zip(si["sclk_min_mhz"], si["sclk_mhz"])), si
+        assert all(p > 0 for p in si["power_w"]), si
 
 
 @pytest.mark.gpu
