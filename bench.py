@@ -13,6 +13,10 @@ The headline is compute-bound by construction (2.8 s of compute against
 ~40 ms of all-link collectives at N = 8), so three secondary measurements
 ride along as extra keys of the same JSON line:
 
+* ``slow_iterations``: per timed iteration of the headline, the slowest
+  rank's last collective (its duration), its GPU's sclk at the iteration's
+  end and the lowest 5-ms sample inside it, and the power at the end (hwmon);
+  ``slow`` lists the iterations over median + 0.1 ms.
 * ``comm_bound``: the ViT-H/32 fp8 data-parallel proxy (BASELINE config 5,
   model_stats/vit_h_32_float8.txt: 7.13 ms of compute, a 1.26 GB bf16
   gradient all-reduce in 8 buckets) - the one baseline config where
