@@ -441,7 +441,8 @@ def _model_fit(a: argparse.Namespace, world: int, extra: Dict[str, Any]) -> Opti
             return None
         f = fit_link_model(lb[key], world)
         if not f.get("eta"):
-            return None
+            # (noisy link timings - a loaded host's CPU backend - can leave no positive fit)
+            return {"backend": key, "error": "no fit: the link timings gave eta " + str(f.get("eta"))}
         kw = {"eta": f["eta"], "alpha_us": f["alpha_us"]}
         pred: Dict[str, Any] = {"headline": _predicted_ms(a, world, "fsdp", a.model, (a.units, world), **kw)}
         if "comm_bound" in extra:
