@@ -198,8 +198,13 @@ class _Budget:
             dec = None
             while self._t() < deadline:
                 if os.path.exists(path):
-                    with open(path) as f:
-                        dec = json.load(f)["timeout"]
+                    try:
+                        with open(path) as f:
+                            dec = json.load(f)["timeout"]
+                    except FileNotFoundError:
+                        # rank 0 finished between the check and the read (its exit removes the plans):
+                        # nothing more runs with it - skip, as when the directory is already gone
+                        dec = None
                     break
                 if os.path.isdir(self.dir):
                     self.seen_dir = True
