@@ -499,11 +499,33 @@ def _slow_iterations(d: dict, margin_ms: float = 0.1) -> Optional[Dict[str, Any]
         return [round(x * scale, nd) for x in v] if isinstance(v, list) and len(v) == len(per) else None
 
     med = sorted(per)[len(per) // 2]
+
+    def per_iter_sum(keys):  # the timers' entries of each iteration, summed (ms)
+        tot = [0.0] * len(per)
+        found = False
+        for k in keys:
+            v = r.get(k)
+            if not isinstance(v, list) or not v or len(v) % len(per):
+                continue
+            n = len(v) // len(per)
+            found = True
+            for i in range(len(per)):
+                tot[i] += sum(v[i * n:(i + 1) * n]) * 1e3
+        return [round(x, 3) for x in tot] if found else None
+
     out = {"rank": slow_rank, "median_ms": med, "max_minus_median_ms": round(max(per) - med, 3),
            "last_collective": r.get("iteration_last_collective"),
            "last_collective_ms": col("iteration_last_collective_ms"),
+           # the exposed-communication waits of each iteration (device clock): a slow iteration whose waits did
+           # not grow lost its time elsewhere (launch, host)
+           "exposed_ms": per_iter_sum(("barrier_time", "allgather", "allgather_wait_fwd", "allgather_wait_bwd",
+                                       "barrier", "pp_comm_time", "tp_comm_time", "ep_comm_time",
+                                       "dp_exposed_time", "cp_exposed_time", "param_allgather_exposed")),
            "sclk_mhz": col("iteration_sclk_mhz", nd=0), "sclk_min_mhz": col("iteration_sclk_min_mhz", nd=0),
            "power_w": col("iteration_power_w", nd=1)}
+    pl = r.get("prearm_launch_ms")  # host time of each pre-armed launch (issued during the iteration before)
+    if isinstance(pl, list) and pl:
+        out["prearm_launch_ms"] = [round(x, 3) for x in pl]
     out["slow"] = [i for i, x in enumerate(per) if x > med + margin_ms]
     return out
 

@@ -51,6 +51,7 @@ def test_bench_torchrun_cpu(n, tmp_path):
     # sensors on the CPU backend)
     si = o["slow_iterations"]
     assert si["last_collective"] == "reduce_scatter" and len(si["last_collective_ms"]) == 2, si
+    assert len(si["exposed_ms"]) == 2 and all(x >= 0 for x in si["exposed_ms"]), si
     assert all(x >= 0 for x in si["last_collective_ms"]) and si["sclk_mhz"] is None, si
     assert o["effective_busbw_GBps"]["allgather"] > 0 and o["effective_busbw_GBps"]["reduce_scatter"] > 0
     c5 = o["comm_bound"]

@@ -330,7 +330,9 @@ def test_dp_exposed_comm_matches_the_step(mode, root):
     span = sum(r["device_span_time"]) / len(r["device_span_time"]) * 1e3 - it["compute_floor_ms"]
     assert barrier > 0.02, (barrier, step)  # the last bucket's 158 MB all-reduce copy is exposed
     assert abs(span - (barrier + capped)) <= 0.01, (span, barrier, capped)
-    tol = 0.03 if mode != "eager" else 0.5
+    # (single graph: 0.04 - its executor's queue hops moved the host-seen step by up to 0.033 ms against the
+    # device span in one of eight full-suite runs, round 6; lanes stay at 0.03)
+    tol = {"lanes": 0.03, "single": 0.04}.get(mode, 0.5)
     assert abs(barrier + capped - step) <= tol, (mode, barrier, capped, step)
     if mode == "lanes":
         # the compute lane is one persistent program whose join signals the iteration; replays alternate
